@@ -1,0 +1,409 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident parse+match throughput on MI355X.
+
+Headline (BASELINE.json metric "Mpps + %HBM-roofline, device-resident
+parse+match, 64B/1500B, 1/2/4/8 GPU"): config C2 -- 64 B packets (60 B
+frames), 1K-rule 5-tuple ExactMatch, 16 M packets resident in HBM per GPU.
+One step = one pass of the hot path (ExactMatch::ProcessBatch semantics:
+header-field extract + hash -> flow-table match -> egress gate) over the
+resident slab.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rules R]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+
+N > 1: every rank owns its own 16 M packets (weak scaling, no data-path
+collective). The rule table is built sharded: rank r builds partition r of
+the flow table and an RCCL all-gather over xGMI assembles the replicated
+table on every GPU (the only collective; control path, timed separately).
+
+Rank 0 prints ONE JSON line. Secondary configs (C3 checksum, C4 wildcard,
+batch-size sweep) are measured at N = 1 only, as extra keys.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+EM_BYTES_PER_PKT = 66  # 64 B header line read + 2 B gate written
+CK_BYTES_PER_PKT = 1502  # 1496 B frame read + IP csum + L4 csum + gate (2 B each)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rules", type=int, default=1000)
+    ap.add_argument("--pkts", type=int, default=16 << 20)
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the C3/C4/sweep secondary measurements")
+    ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    ap.add_argument("--only", default="", help="em|cksum|wm (profiling runs)")
+    return ap.parse_args()
+
+
+class Timer:
+    """HIP events on the stream the kernels are launched on (torch's current
+    stream: libbessgpu launches on the hipStream_t we pass, which is it)."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.a = torch.cuda.Event(enable_timing=True)
+        self.b = torch.cuda.Event(enable_timing=True)
+
+    def start(self):
+        self.a.record()
+
+    def stop_ms(self):
+        self.b.record()
+        self.b.synchronize()
+        return self.a.elapsed_time(self.b)
+
+
+def load_traffic(key):
+    """HBM traffic per launch measured with rocprofv3 PMC counters
+    (profiles/traffic.json, written by scripts/pmc_traffic.py)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def em_setup(args, rank, world, dev, torch, dist):
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    t0 = time.time()
+    # same rules on every rank, rank-specific packets
+    keys, gates, frames = P.em_workload(args.rules, args.pkts, seed=0x5EED,
+                                        pkt_seed=0x5EED + 7919 * rank)
+    log("[rank %d] workload generated in %.1fs" % (rank, time.time() - t0))
+    d_frames = torch.from_numpy(frames.reshape(-1)).to(dev)
+    del frames
+    d_gates = torch.empty(args.pkts, dtype=torch.int16, device=dev)
+    t = F.EmTable(P.em_fields_5tuple())
+    t0 = time.time()
+    t.add_many(keys, gates)
+    log("[rank %d] %d rules inserted in %.1fs" % (rank, len(t), time.time() - t0))
+    table = {"rules": len(t)}
+    if world > 1:
+        # sharded build + RCCL all-gather of the partition images
+        pb = t.plan(world)
+        part = torch.from_numpy(t.build_part(rank, pb)).to(dev)
+        full = torch.empty(pb * world, dtype=torch.uint8, device=dev)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.all_gather_into_tensor(full, part)
+        torch.cuda.synchronize()
+        table["allgather_ms"] = (time.perf_counter() - t0) * 1e3
+        table["allgather_bytes"] = pb * world
+        t.attach(dev.index, full)
+        t._keep = (part, full)
+    else:
+        t.sync(dev.index)
+    nbytes, in_lds = t.table_info()
+    table.update({"bytes": nbytes, "in_lds": in_lds})
+    return t, d_frames, d_gates, keys, gates, table
+
+
+def em_parity_sample(t, d_frames, d_gates, keys, gates, n, torch):
+    """Bit-exact check of the first n packets against the CPU oracle."""
+    from bess_amd import packets as P
+    from oracle import oracle as O
+    import ctypes as C
+    frames = d_frames[:n * 64].cpu().numpy()
+    got = d_gates[:n].cpu().numpy().view(np.uint16)
+    L = O.lib()
+    em = L.or_em_new()
+    for i, (off, size) in enumerate(P.FIVE_TUPLE):
+        L.or_em_add_field(em, off, size, 0, i, None, 0)
+    sizes = [s for _, s in P.FIVE_TUPLE]
+    pos = np.cumsum([0] + sizes)
+    ptrs = (C.c_void_p * 5)()
+    lens = (C.c_size_t * 5)(*sizes)
+    keys = np.ascontiguousarray(keys)
+    for k, g in zip(keys, gates):
+        for j in range(5):
+            ptrs[j] = k.ctypes.data + int(pos[j])
+        L.or_em_add_rule(em, int(g), ptrs, lens, 5, None, 0)
+    want = np.zeros(n, np.uint16)
+    L.or_em_process(em, frames.ctypes.data, 64, n, 8192, want.ctypes.data)
+    L.or_em_free(em)
+    return bool((got == want).all())
+
+
+def cpu_baseline_em(keys, gates, seconds):
+    """The oracle (plain-C restatement of ExactMatch::ProcessBatch with a
+    CuckooMap/CRC32C table, 32-packet batches) timed on this host's cores
+    over packets laid out like BESS snbufs (2624 B stride, frame at +512)."""
+    from bess_amd import packets as P
+    from oracle import oracle as O
+    import ctypes as C
+    L = O.lib()
+    em = L.or_em_new()
+    for i, (off, size) in enumerate(P.FIVE_TUPLE):
+        L.or_em_add_field(em, off, size, 0, i, None, 0)
+    sizes = [s for _, s in P.FIVE_TUPLE]
+    pos = np.cumsum([0] + sizes)
+    ptrs = (C.c_void_p * 5)()
+    lens = (C.c_size_t * 5)(*sizes)
+    for k, g in zip(np.ascontiguousarray(keys), gates):
+        for j in range(5):
+            ptrs[j] = k.ctypes.data + int(pos[j])
+        L.or_em_add_rule(em, int(g), ptrs, lens, 5, None, 0)
+    n = 1 << 18
+    _, _, frames = P.em_workload(len(keys), n, seed=0x5EED, pkt_seed=77)
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + 64] = frames
+    base = snb.ctypes.data + 512
+    out = np.zeros(n, np.uint16)
+    threads = max(1, min(16, L.or_num_cpus()))
+    res = {}
+    for nt in sorted({1, threads}):
+        t1 = L.or_em_bench(em, base, 2624, n, 8192, out.ctypes.data, nt, 1)
+        reps = max(1, int(seconds / 2 / max(t1, 1e-6)))
+        dt = L.or_em_bench(em, base, 2624, n, 8192, out.ctypes.data, nt, reps)
+        res[nt] = n * reps / dt / 1e6
+    L.or_em_free(em)
+    return {"value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
+            "kind": "port",
+            "single_core_mpps": round(res[1], 2),
+            "sample": "%d 64B pkts x reps, 1K-rule 5-tuple ExactMatch, snbuf "
+                      "layout (2624 B stride), 32-pkt batches, %d pinned "
+                      "threads" % (n, threads)}
+
+
+def run_em(args, rank, world, dev, torch, dist):
+    from bess_amd import flowtable as F  # noqa: F401
+    t, d_frames, d_gates, keys, gates, table = em_setup(args, rank, world, dev,
+                                                       torch, dist)
+    n = args.pkts
+
+    def step():
+        t.classify(d_frames, 64, n, 8192, d_gates)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    parity = em_parity_sample(t, d_frames, d_gates, keys, gates,
+                              min(n, 1 << 20), torch)
+    timer = Timer(torch)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    timer.start()
+    for _ in range(args.steps):
+        step()
+    kern_ms = timer.stop_ms()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - w0
+    if world > 1:
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kern_ms = tt.tolist()
+        ok = torch.tensor([1 if parity else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity = bool(ok.item())
+    return {"t": t, "d_frames": d_frames, "d_gates": d_gates, "keys": keys,
+            "gates": gates, "wall": wall, "kern_ms": kern_ms, "n": n,
+            "parity": parity, "table": table}
+
+
+def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
+    """Per-launch batch-size sweep (SURVEY C2 'batch 32->4096'): each batch
+    of B packets is one kernel launch; 512 consecutive launches are captured
+    in a HIP graph and replayed, so the number is the device-side cost of
+    B-packet launches without host launch overhead."""
+    t, d_frames, d_gates = r["t"], r["d_frames"], r["d_gates"]
+    out = {}
+    s = torch.cuda.Stream()
+    for B in batches:
+        nl = 512
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                for j in range(nl):
+                    off = j * B
+                    t.classify(d_frames[off * 64:], 64, B, 8192,
+                               d_gates[off:], stream=s)
+        g.replay()
+        torch.cuda.synchronize()
+        reps = 5
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(reps):
+            g.replay()
+        b.record(s)
+        b.synchronize()
+        ms = a.elapsed_time(b) / reps
+        out[str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
+    return out
+
+
+def run_cksum(args, dev, torch):
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    n = 1 << 20
+    frames = P.cksum_workload(n, frame_len=1496, stride=2048)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    ref = frames[:4096].copy()
+    del frames
+    l4g = torch.empty(n, dtype=torch.int16, device=dev)
+    for _ in range(args.warmup):
+        F.cksum(d, 2048, n, 3, False, None, l4g)
+    torch.cuda.synchronize()
+    # parity on a sample: oracle on the original frames vs device result
+    from oracle import oracle as O
+    ipw, l4w = O.cksum_process(ref, 2048, 4096, 3, False)
+    got = d[:4096 * 2048].cpu().numpy().reshape(4096, 2048)
+    parity = bool((got == ref).all() and
+                  (l4g[:4096].cpu().numpy().view(np.uint16) == l4w).all())
+    timer = Timer(torch)
+    torch.cuda.synchronize()
+    timer.start()
+    for _ in range(args.steps):
+        F.cksum(d, 2048, n, 3, False, None, l4g)
+    ms = timer.stop_ms() / args.steps
+    mpps = n / (ms * 1e-3) / 1e6
+    gbs = CK_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
+    return {"workload": "C3: 1500B pkts (1496B frames, 2048B slots), "
+                        "IPChecksum->L4Checksum recompute, 50/50 UDP/TCP",
+            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic("cksum")},
+            "parity": parity}
+
+
+def run_wm(args, dev, torch):
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    n = 1 << 20
+    # IMIX frames (60/590/1514 B, 7:4:1) in 2 KB slots; the classifier
+    # reads only each frame's header line
+    rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n, stride=2048)
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    dg = torch.empty(n, dtype=torch.int16, device=dev)
+    for _ in range(args.warmup):
+        t.classify(d, 2048, n, 8192, dg)
+    torch.cuda.synchronize()
+    timer = Timer(torch)
+    timer.start()
+    for _ in range(args.steps):
+        t.classify(d, 2048, n, 8192, dg)
+    ms = timer.stop_ms() / args.steps
+    mpps = n / (ms * 1e-3) / 1e6
+    gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
+    nbytes, in_lds = t.table_info()
+    return {"workload": "C4: 100K-rule WildcardMatch over 8 masks (tuple-space,"
+                        " priority ties), 5-tuple, header lines of IMIX frames",
+            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
+            "table_bytes": nbytes,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic("wm")}}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import bess_amd
+    bess_amd.lib()  # fail loudly if the HIP library is missing
+
+    if args.only == "cksum":
+        log(json.dumps(run_cksum(args, dev, torch)))
+        return
+    if args.only == "wm":
+        log(json.dumps(run_wm(args, dev, torch)))
+        return
+
+    r = run_em(args, rank, world, dev, torch, dist)
+    n_total = r["n"] * world
+    ms_step = r["wall"] / args.steps * 1e3
+    value = n_total * args.steps / r["wall"] / 1e6
+    kern_ms = r["kern_ms"] / args.steps
+    achieved = EM_BYTES_PER_PKT * r["n"] / (kern_ms * 1e-3) / 1e9
+    out = {
+        "metric": "Mpps + %HBM-roofline, device-resident parse+match, "
+                  "64B/1500B, 1/2/4/8 GPU",
+        "value": round(value, 1), "unit": "Mpps", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded 5-tuple traffic, 50% rule hits)",
+        "config": {"workload": "C2: 64B pkts (60B frames, 64B slots), %d-rule "
+                               "5-tuple ExactMatch, %d resident pkts per GPU"
+                               % (args.rules, r["n"]),
+                   "rules": args.rules, "pkts_per_gpu": r["n"],
+                   "slot_bytes": 64, "parallelism": "dp%d (packet shards)" % world,
+                   "table": r["table"]},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic("em_%d" % args.rules),
+                     "kernel": "em_classify_kernel<2>",
+                     "kernel_ms": round(kern_ms, 4),
+                     "bytes_per_pkt": EM_BYTES_PER_PKT},
+        "parity": "bit-exact vs oracle on 1M-pkt sample" if r["parity"]
+                  else "MISMATCH",
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_extra:
+        try:
+            out["batch_sweep_mpps"] = em_sweep(r, torch)
+        except Exception as e:  # report, do not hide
+            out["batch_sweep_mpps"] = "failed: %r" % (e,)
+        out["extra_configs"] = {}
+        for name, fn in (("C3", run_cksum), ("C4", run_wm)):
+            try:
+                out["extra_configs"][name] = fn(args, dev, torch)
+            except Exception as e:
+                out["extra_configs"][name] = "failed: %r" % (e,)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_em(r["keys"], r["gates"],
+                                              args.cpu_seconds)
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+"""ctypes binding of libbessgpu.so (include/bessgpu.h).
+
+The HIP library is the product: if it is missing this module raises instead of
+falling back to anything else.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbessgpu.so")
+
+BG_MAX_GATES = 8192
+BG_DROP_GATE = 8192
+BG_GATE_NONE = 0xFFFF
+BG_CK_IP = 1
+BG_CK_L4 = 2
+KEY_BYTES = 64
+
+
+class BessGpuError(RuntimeError):
+    """A failing bg_* call: errno + the reference-style message."""
+
+    def __init__(self, code, msg):
+        super().__init__("[errno %d] %s" % (code, msg))
+        self.code = code
+        self.msg = msg
+
+
+class bg_field(C.Structure):
+    _fields_ = [("offset", C.c_int32), ("size", C.c_int32), ("pos", C.c_int32),
+                ("attr_id", C.c_int32), ("mask", C.c_uint64)]
+
+
+_vp, _sz, _u16, _i32, _int = C.c_void_p, C.c_size_t, C.c_uint16, C.c_int32, C.c_int
+_SIGS = {
+    "bg_version": (C.c_char_p, []),
+    "bg_last_error": (C.c_char_p, []),
+    "bg_device_count": (_int, []),
+    "bg_malloc": (_int, [_int, _sz, C.POINTER(_vp)]),
+    "bg_free": (_int, [_vp]),
+    "bg_memcpy_h2d": (_int, [_vp, _vp, _sz, _vp]),
+    "bg_memcpy_d2h": (_int, [_vp, _vp, _sz, _vp]),
+    "bg_stream_sync": (_int, [_vp]),
+    "bg_em_create": (_int, [C.POINTER(bg_field), _int, C.POINTER(_vp)]),
+    "bg_em_destroy": (None, [_vp]),
+    "bg_em_key_size": (_sz, [_vp]),
+    "bg_em_add": (_int, [_vp, _vp, _u16]),
+    "bg_em_delete": (_int, [_vp, _vp]),
+    "bg_em_clear": (None, [_vp]),
+    "bg_em_count": (_sz, [_vp]),
+    "bg_em_iter": (_int, [_vp, C.POINTER(_sz), _vp, C.POINTER(_u16)]),
+    "bg_em_sync": (_int, [_vp, _int, _vp]),
+    "bg_em_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
+    "bg_em_process_host": (_int, [_vp, _vp, _sz, _u16, _vp, _vp]),
+    "bg_em_plan": (_int, [_vp, _int, C.POINTER(C.c_uint64)]),
+    "bg_em_build_part": (_int, [_vp, _int, _vp]),
+    "bg_em_attach": (_int, [_vp, _int, _vp]),
+    "bg_em_table_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
+    "bg_wm_create": (_int, [C.POINTER(bg_field), _int, C.POINTER(_vp)]),
+    "bg_wm_destroy": (None, [_vp]),
+    "bg_wm_key_size": (_sz, [_vp]),
+    "bg_wm_add": (_int, [_vp, _vp, _vp, _i32, _u16]),
+    "bg_wm_delete": (_int, [_vp, _vp, _vp]),
+    "bg_wm_clear": (None, [_vp]),
+    "bg_wm_num_tuples": (_int, [_vp]),
+    "bg_wm_tuple_mask": (_int, [_vp, _int, _vp]),
+    "bg_wm_tuple_count": (_sz, [_vp, _int]),
+    "bg_wm_iter": (_int, [_vp, _int, C.POINTER(_sz), _vp, C.POINTER(_i32),
+                          C.POINTER(_u16)]),
+    "bg_wm_sync": (_int, [_vp, _int, _vp]),
+    "bg_wm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
+    "bg_wm_process_host": (_int, [_vp, _vp, _sz, _u16, _vp, _vp]),
+    "bg_wm_table_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
+    "bg_cksum": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp, _vp, _vp]),
+    "bg_cksum_process_host": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp,
+                                     _vp, _vp]),
+    "bg_module_create": (_int, [C.c_char_p, _vp, _sz, C.POINTER(_vp)]),
+    "bg_module_destroy": (None, [_vp]),
+    "bg_module_command": (_int, [_vp, C.c_char_p, _vp, _sz, _vp,
+                                 C.POINTER(_sz)]),
+    "bg_module_process": (_int, [_vp, _vp, _sz, _vp]),
+    "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
+    "bg_module_set_device": (_int, [_vp, _int]),
+    "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libbessgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                "bess_amd: %s missing -- build it (python -c 'import "
+                "__graft_entry__ as g; g.build()')" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc < 0:
+        msg = lib().bg_last_error()
+        raise BessGpuError(-rc, msg.decode() if msg else "")
+    return rc
+
+
+def declared_symbols():
+    """Every function include/bessgpu.h declares (parsed from the header)."""
+    import re
+    hdr = os.path.join(os.path.dirname(HERE), "include", "bessgpu.h")
+    txt = open(hdr).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(bg_\w+)\s*\(", txt)))

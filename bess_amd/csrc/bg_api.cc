@@ -1,0 +1,844 @@
+// bg_api.cc -- C ABI of libbessgpu.so (include/bessgpu.h): rule storage,
+// device-table build/upload, kernel launch plumbing and host staging.
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/bessgpu.h"
+#include "bg_internal.h"
+#include "bg_kernels.h"
+#include "bg_table.h"
+
+namespace bg {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -code;
+}
+
+#define HIP_TRY(expr)                                                  \
+  do {                                                                 \
+    hipError_t e_ = (expr);                                            \
+    if (e_ != hipSuccess)                                              \
+      return fail(EIO, "%s: %s", #expr, hipGetErrorString(e_));        \
+  } while (0)
+
+int num_cus(int device) {
+  static std::mutex mu;
+  static std::unordered_map<int, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount,
+                            device) != hipSuccess || v <= 0)
+    v = 256;
+  cache[device] = v;
+  return v;
+}
+
+int set_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    return fail(ENODEV, "no HIP device available");
+  if (device < 0 || device >= n)
+    return fail(ENODEV, "device %d out of range [0,%d)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  return 0;
+}
+
+uint32_t round_kw(uint32_t key_bytes) {
+  uint32_t w = (key_bytes + 7) / 8;
+  if (w <= 1) return 1;
+  if (w <= 2) return 2;
+  if (w <= 4) return 4;
+  return 8;
+}
+
+// Field plan for frames whose head_data() is at offset `base` of the
+// buffer the kernel reads (base = 0 for slabs, -win_lo for staged windows).
+FieldPlan make_plan(const std::vector<bg_field> &fields, bool em_masks,
+                    int shift) {
+  FieldPlan p;
+  memset(&p, 0, sizeof(p));
+  p.nf = (int)fields.size();
+  if (p.nf == 0) return p;
+  int lo = 1 << 30, hi = 0;
+  for (auto &f : fields) {
+    lo = std::min(lo, f.offset + shift);
+    hi = std::max(hi, f.offset + shift + f.size);
+  }
+  p.win_lo = lo & ~15;
+  p.nch = (hi - p.win_lo + 15) / 16;
+  p.direct = p.nch > kMaxWindowChunks;
+  for (int i = 0; i < p.nf; i++) {
+    const bg_field &f = fields[i];
+    const int off = f.offset + shift;
+    p.fdw[i] = (off - p.win_lo) >> 2;
+    p.fsh[i] = (off & 3) * 8;
+    p.fpos[i] = f.pos;
+    p.foff[i] = off;
+    p.fnd[i] = ((off + f.size - 1) >> 2) - (off >> 2) + 1;
+    uint64_t size_mask = f.size >= 8 ? ~0ULL : ((1ULL << (8 * f.size)) - 1);
+    p.fmask[i] = em_masks ? (f.mask & size_mask) : size_mask;
+  }
+  if (p.direct) p.nch = 0;
+  return p;
+}
+
+// --------------------------------------------------------------------------
+// device table
+// --------------------------------------------------------------------------
+void relayout(TableLayout &L, uint32_t nbp) {
+  L.nbp = nbp;
+  L.keys_off = align256((uint64_t)nbp * 4);
+  L.vals_off = align256(L.keys_off + (uint64_t)nbp * kSlots * L.kw * 8);
+  L.part_bytes = align256(L.vals_off + (uint64_t)nbp * kSlots * L.val_bytes);
+}
+
+int DevTable::upload(int dev, const std::vector<uint8_t> &img,
+                     const TableLayout &lay, hipStream_t s) {
+  int r = set_device(dev);
+  if (r) return r;
+  if (d_image && owned && (device != dev || bytes < img.size())) {
+    (void)hipFree(d_image);
+    d_image = nullptr;
+  }
+  if (!d_image || !owned) {
+    d_image = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_image),
+                      std::max<size_t>(img.size(), 256)));
+    owned = true;
+  }
+  HIP_TRY(hipMemcpyAsync(d_image, img.data(), img.size(),
+                         hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  device = dev;
+  bytes = img.size();
+  L = lay;
+  valid = true;
+  return 0;
+}
+
+void DevTable::release() {
+  if (d_image && owned) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    (void)hipFree(d_image);
+    (void)hipSetDevice(cur);
+  }
+  d_image = nullptr;
+  valid = false;
+}
+
+TableRef DevTable::ref() const {
+  TableRef t;
+  memset(&t, 0, sizeof(t));
+  t.base = d_image;
+  t.part_bytes = L.part_bytes;
+  t.keys_off = L.keys_off;
+  t.vals_off = L.vals_off;
+  t.seed = L.seed;
+  t.nparts = L.nparts;
+  t.nbp = L.nbp;
+  t.kw = L.kw;
+  t.bytes_total = (uint32_t)std::min<uint64_t>(bytes, 0xFFFFFFFFu);
+  t.lds = bytes <= kLdsTableMax ? 1u : 0u;
+  return t;
+}
+
+// Build a full single-device image (all partitions) from flat entries.
+int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
+                const std::vector<uint64_t> &keys,
+                const std::vector<uint8_t> &vals,
+                const std::vector<uint64_t> &seeds, std::vector<uint8_t> *img,
+                TableLayout *out_layout) {
+  const size_t n = seeds.size();
+  // count entries per partition to size the layout
+  std::vector<std::vector<size_t>> members(nparts);
+  TableLayout L = plan_layout(0, kw, val_bytes, nparts, kDefaultSeed);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t h = hash_words(&keys[i * kw], (int)kw, seeds[i]);
+    members[split_hash(h, nparts, 2).part].push_back(i);
+  }
+  size_t maxc = 0;
+  for (auto &m : members) maxc = std::max(maxc, m.size());
+  L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed);
+  for (int attempt = 0; attempt < 8; attempt++) {
+    img->assign((size_t)L.part_bytes * nparts, 0);
+    bool ok = true;
+    for (uint32_t p = 0; p < nparts && ok; p++) {
+      std::vector<uint64_t> pk, ps;
+      std::vector<uint8_t> pv;
+      for (size_t i : members[p]) {
+        pk.insert(pk.end(), &keys[i * kw], &keys[i * kw] + kw);
+        pv.insert(pv.end(), &vals[i * val_bytes], &vals[i * val_bytes] + val_bytes);
+        ps.push_back(seeds[i]);
+      }
+      ok = build_partition(L, p, members[p].size(), pk.data(), pv.data(),
+                           ps.data(), img->data() + (size_t)p * L.part_bytes);
+    }
+    if (ok) {
+      *out_layout = L;
+      return 0;
+    }
+    if (L.nbp >= kMaxBucketsPerPart) break;
+    relayout(L, L.nbp * 2);
+  }
+  return fail(ENOSPC, "flow table build failed (%zu entries)", n);
+}
+
+// --------------------------------------------------------------------------
+// host staging (pinned) + device scratch, grown on demand
+// --------------------------------------------------------------------------
+int Staging::ensure(int dev, size_t in_bytes, size_t out_bytes) {
+  if (device != dev) {
+    release();
+    device = dev;
+  }
+  if (in_bytes > in_cap) {
+    if (h_in) (void)hipHostFree(h_in);
+    if (d_in) (void)hipFree(d_in);
+    h_in = nullptr;
+    d_in = nullptr;
+    in_cap = std::max<size_t>(in_bytes, 1 << 16);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_in), in_cap,
+                          hipHostMallocDefault));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_in), in_cap));
+  }
+  if (out_bytes > out_cap) {
+    if (h_out) (void)hipHostFree(h_out);
+    if (d_out) (void)hipFree(d_out);
+    h_out = nullptr;
+    d_out = nullptr;
+    out_cap = std::max<size_t>(out_bytes, 1 << 12);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_out), out_cap,
+                          hipHostMallocDefault));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_out), out_cap));
+  }
+  return 0;
+}
+
+void Staging::release() {
+  if (h_in) (void)hipHostFree(h_in);
+  if (d_in) (void)hipFree(d_in);
+  if (h_out) (void)hipHostFree(h_out);
+  if (d_out) (void)hipFree(d_out);
+  h_in = d_in = h_out = d_out = nullptr;
+  in_cap = out_cap = 0;
+}
+
+}  // namespace bg
+
+using namespace bg;
+
+// ============================================================================
+// ExactMatch
+// ============================================================================
+struct bg_em {
+  std::vector<bg_field> fields;
+  uint32_t key_size = 0;  // total_key_size_
+  uint32_t kw = 1;        // device key words (1, 2, 4, 8)
+  std::unordered_map<Key, uint16_t, KeyHash> rules;
+  bool dirty = true;
+  DevTable dev;
+  Staging stage;
+  TableLayout planned;  // sharded build
+  bool planned_valid = false;
+  std::mutex mu;  // serialises sync/staging (lookups from many workers)
+};
+
+static Key em_key(const bg_em *em, const uint8_t *key) {
+  Key k;
+  memset(&k, 0, sizeof(k));
+  memcpy(k.w, key, em->key_size);
+  return k;
+}
+
+static int check_fields(const bg_field *fields, int nfields) {
+  if (nfields < 0 || nfields > BG_MAX_FIELDS)
+    return fail(EINVAL, "nfields %d not in [0,%d]", nfields, BG_MAX_FIELDS);
+  int acc = 0;
+  for (int i = 0; i < nfields; i++) {
+    const bg_field &f = fields[i];
+    if (f.size < 1 || f.size > 8)
+      return fail(EINVAL, "idx %d: 'size' must be in [1,8]", i);
+    if (f.attr_id >= 0)
+      return fail(ENOTSUP, "idx %d: metadata-attribute fields are not on the "
+                  "device path", i);
+    if (f.offset < 0 || f.offset > 1024)
+      return fail(EINVAL, "idx %d: invalid 'offset'", i);
+    if (f.pos != acc)
+      return fail(EINVAL, "idx %d: pos %d != %d", i, f.pos, acc);
+    acc += f.size;
+  }
+  return 0;
+}
+
+extern "C" {
+
+const char *bg_version(void) { return "bessgpu 0.1 (gfx950)"; }
+const char *bg_last_error(void) { return bg::g_err.c_str(); }
+
+int bg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int bg_malloc(int device, size_t bytes, void **d_ptr) {
+  int r = set_device(device);
+  if (r) return r;
+  HIP_TRY(hipMalloc(d_ptr, std::max<size_t>(bytes, 1)));
+  return 0;
+}
+int bg_free(void *d_ptr) {
+  HIP_TRY(hipFree(d_ptr));
+  return 0;
+}
+int bg_memcpy_h2d(void *d_dst, const void *src, size_t bytes, bg_stream_t s) {
+  HIP_TRY(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice,
+                         (hipStream_t)s));
+  return 0;
+}
+int bg_memcpy_d2h(void *dst, const void *d_src, size_t bytes, bg_stream_t s) {
+  HIP_TRY(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost,
+                         (hipStream_t)s));
+  return 0;
+}
+int bg_stream_sync(bg_stream_t s) {
+  HIP_TRY(hipStreamSynchronize((hipStream_t)s));
+  return 0;
+}
+
+int bg_em_create(const bg_field *fields, int nfields, bg_em **out) {
+  int r = check_fields(fields, nfields);
+  if (r) return r;
+  bg_em *em = new bg_em();
+  em->fields.assign(fields, fields + nfields);
+  int acc = 0;
+  for (int i = 0; i < nfields; i++) acc += fields[i].size;
+  em->key_size = (uint32_t)((acc + 7) / 8 * 8);
+  em->kw = round_kw(em->key_size);
+  *out = em;
+  return 0;
+}
+
+void bg_em_destroy(bg_em *em) {
+  if (!em) return;
+  em->dev.release();
+  em->stage.release();
+  delete em;
+}
+
+size_t bg_em_key_size(const bg_em *em) { return em->key_size; }
+
+int bg_em_add(bg_em *em, const uint8_t *key, uint16_t gate) {
+  if (em->key_size == 0) return fail(EINVAL, "rule has no fields");
+  em->rules[em_key(em, key)] = gate;
+  em->dirty = true;
+  return 0;
+}
+
+int bg_em_delete(bg_em *em, const uint8_t *key) {
+  if (em->key_size == 0) return fail(EINVAL, "rule has no fields");
+  if (em->rules.erase(em_key(em, key)) == 0)
+    return fail(ENOENT, "rule doesn't exist");
+  em->dirty = true;
+  return 0;
+}
+
+void bg_em_clear(bg_em *em) {
+  em->rules.clear();
+  em->dirty = true;
+}
+
+size_t bg_em_count(const bg_em *em) { return em->rules.size(); }
+
+int bg_em_iter(const bg_em *em, size_t *cursor, uint8_t *key_out,
+               uint16_t *gate_out) {
+  // unordered_map iteration by position: O(n) per call is avoided by the
+  // module layer, which snapshots once; here we walk from the start.
+  size_t i = 0;
+  for (auto &kv : em->rules) {
+    if (i++ == *cursor) {
+      memcpy(key_out, kv.first.w, em->key_size);
+      *gate_out = kv.second;
+      (*cursor)++;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+static void em_entries(const bg_em *em, std::vector<uint64_t> *keys,
+                       std::vector<uint8_t> *vals, std::vector<uint64_t> *seeds) {
+  keys->clear();
+  vals->clear();
+  seeds->clear();
+  keys->reserve(em->rules.size() * em->kw);
+  for (auto &kv : em->rules) {
+    keys->insert(keys->end(), kv.first.w, kv.first.w + em->kw);
+    vals->push_back((uint8_t)kv.second);
+    vals->push_back((uint8_t)(kv.second >> 8));
+    seeds->push_back(kDefaultSeed);
+  }
+}
+
+static int em_sync_locked(bg_em *em, int device, hipStream_t s) {
+  if (!em->dirty && em->dev.valid && em->dev.device == device) return 0;
+  std::vector<uint64_t> keys, seeds;
+  std::vector<uint8_t> vals, img;
+  em_entries(em, &keys, &vals, &seeds);
+  TableLayout L;
+  int r = build_image(em->kw, 2, 1, keys, vals, seeds, &img, &L);
+  if (r) return r;
+  r = em->dev.upload(device, img, L, s);
+  if (r) return r;
+  em->dirty = false;
+  return 0;
+}
+
+int bg_em_sync(bg_em *em, int device, bg_stream_t stream) {
+  std::lock_guard<std::mutex> lk(em->mu);
+  return em_sync_locked(em, device, (hipStream_t)stream);
+}
+
+static int em_launch(bg_em *em, const void *d_frames, size_t stride, size_t n,
+                     uint16_t default_gate, uint16_t *d_gates, int shift,
+                     hipStream_t s) {
+  EmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.frames = static_cast<const uint8_t *>(d_frames);
+  a.stride = stride;
+  a.n = n;
+  a.gates = d_gates;
+  a.default_gate = default_gate;
+  a.fp = make_plan(em->fields, true, shift);
+  a.t = em->dev.ref();
+  HIP_TRY(launch_em(a, num_cus(em->dev.device), s));
+  return 0;
+}
+
+int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
+                   uint16_t default_gate, uint16_t *d_gates,
+                   bg_stream_t stream) {
+  if (stride % 16 || ((uintptr_t)d_frames & 15))
+    return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
+  hipStream_t s = (hipStream_t)stream;
+  int dev = em->dev.valid ? em->dev.device : 0;
+  if (!em->dev.valid || em->dirty) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    std::lock_guard<std::mutex> lk(em->mu);
+    int r = em_sync_locked(em, em->dev.valid ? em->dev.device : cur, s);
+    if (r) return r;
+    dev = em->dev.device;
+  }
+  int r = set_device(dev);
+  if (r) return r;
+  return em_launch(em, d_frames, stride, n, default_gate, d_gates, 0, s);
+}
+
+// Stage [lo, hi) of every head (window covering all fields) at a fixed
+// 16-byte-multiple stride, then classify on the device.
+static int stage_windows(const std::vector<bg_field> &fields,
+                         const uint8_t *const *heads, size_t n, Staging &st,
+                         int dev, int *shift, size_t *wstride) {
+  int lo = 1 << 30, hi = 0;
+  for (auto &f : fields) {
+    lo = std::min(lo, f.offset);
+    hi = std::max(hi, f.offset + f.size);
+  }
+  if (fields.empty()) lo = hi = 0;
+  const size_t w = std::max<size_t>(16, (size_t)(hi - lo + 15) / 16 * 16);
+  int r = st.ensure(dev, n * w, n * 2);
+  if (r) return r;
+  for (size_t i = 0; i < n; i++)
+    memcpy(st.h_in + i * w, heads[i] + lo, (size_t)(hi - lo));
+  *shift = -lo;
+  *wstride = w;
+  return 0;
+}
+
+int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
+                       uint16_t default_gate, uint16_t *gates,
+                       bg_stream_t stream) {
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lk(em->mu);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  int dev = em->dev.valid ? em->dev.device : cur;
+  int r = em_sync_locked(em, dev, s);
+  if (r) return r;
+  int shift;
+  size_t w;
+  r = stage_windows(em->fields, heads, n, em->stage, dev, &shift, &w);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(em->stage.d_in, em->stage.h_in, n * w,
+                         hipMemcpyHostToDevice, s));
+  r = em_launch(em, em->stage.d_in, w, n, default_gate,
+                reinterpret_cast<uint16_t *>(em->stage.d_out), shift, s);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(em->stage.h_out, em->stage.d_out, n * 2,
+                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  memcpy(gates, em->stage.h_out, n * 2);
+  return 0;
+}
+
+int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes) {
+  if (nparts < 1 || nparts > 8 || (nparts & (nparts - 1)))
+    return fail(EINVAL, "nparts must be 1, 2, 4 or 8");
+  std::vector<size_t> cnt(nparts, 0);
+  for (auto &kv : em->rules) {
+    uint64_t h = hash_words(kv.first.w, (int)em->kw, kDefaultSeed);
+    cnt[split_hash(h, (uint32_t)nparts, 2).part]++;
+  }
+  size_t maxc = *std::max_element(cnt.begin(), cnt.end());
+  em->planned = plan_layout(maxc, em->kw, 2, (uint32_t)nparts, kDefaultSeed);
+  em->planned_valid = true;
+  *part_bytes = em->planned.part_bytes;
+  return 0;
+}
+
+int bg_em_build_part(bg_em *em, int part, void *host_dst) {
+  if (!em->planned_valid) return fail(EINVAL, "bg_em_plan first");
+  const TableLayout &L = em->planned;
+  if (part < 0 || (uint32_t)part >= L.nparts)
+    return fail(EINVAL, "part %d out of range", part);
+  std::vector<uint64_t> keys, seeds;
+  std::vector<uint8_t> vals;
+  for (auto &kv : em->rules) {
+    uint64_t h = hash_words(kv.first.w, (int)em->kw, kDefaultSeed);
+    if (split_hash(h, L.nparts, L.nbp).part != (uint32_t)part) continue;
+    keys.insert(keys.end(), kv.first.w, kv.first.w + em->kw);
+    vals.push_back((uint8_t)kv.second);
+    vals.push_back((uint8_t)(kv.second >> 8));
+    seeds.push_back(kDefaultSeed);
+  }
+  if (!build_partition(L, (uint32_t)part, seeds.size(), keys.data(),
+                       vals.data(), seeds.data(),
+                       static_cast<uint8_t *>(host_dst)))
+    return fail(ENOSPC, "partition %d build failed (%zu entries)", part,
+                seeds.size());
+  return 0;
+}
+
+int bg_em_attach(bg_em *em, int device, const void *d_image) {
+  if (!em->planned_valid) return fail(EINVAL, "bg_em_plan first");
+  std::lock_guard<std::mutex> lk(em->mu);
+  em->dev.release();
+  em->dev.d_image = static_cast<uint8_t *>(const_cast<void *>(d_image));
+  em->dev.owned = false;
+  em->dev.device = device;
+  em->dev.L = em->planned;
+  em->dev.bytes = em->planned.part_bytes * em->planned.nparts;
+  em->dev.valid = true;
+  em->dirty = false;
+  return 0;
+}
+
+int bg_em_table_info(const bg_em *em, uint64_t *bytes, int *in_lds) {
+  if (!em->dev.valid) return fail(EINVAL, "no device table yet");
+  *bytes = em->dev.bytes;
+  *in_lds = em->dev.ref().lds ? 1 : 0;
+  return 0;
+}
+
+}  // extern "C"
+
+// ============================================================================
+// WildcardMatch
+// ============================================================================
+struct WmTupleH {
+  Key mask;
+  std::unordered_map<Key, WmVal, KeyHash> ht;
+};
+
+struct bg_wm {
+  std::vector<bg_field> fields;
+  uint32_t key_size = 0;
+  uint32_t kw = 1;
+  std::vector<WmTupleH> tuples;
+  bool dirty = true;
+  DevTable dev;
+  Staging stage;
+  std::mutex mu;
+};
+
+static Key wm_key(const bg_wm *wm, const uint8_t *p) {
+  Key k;
+  memset(&k, 0, sizeof(k));
+  memcpy(k.w, p, wm->key_size);
+  return k;
+}
+
+static int wm_find_tuple(const bg_wm *wm, const Key &mask) {
+  for (size_t i = 0; i < wm->tuples.size(); i++)
+    if (memcmp(wm->tuples[i].mask.w, mask.w, wm->key_size) == 0) return (int)i;
+  return -ENOENT;
+}
+
+extern "C" {
+
+int bg_wm_create(const bg_field *fields, int nfields, bg_wm **out) {
+  int acc = 0;
+  for (int i = 0; i < nfields; i++) acc += fields[i].size;
+  if (acc > BG_KEY_BYTES) return fail(EINVAL, "key larger than 64 bytes");
+  if (nfields > BG_MAX_FIELDS) {
+    // the reference takes any number of fields whose sizes fit the key;
+    // the device plan handles up to 8
+    return fail(EINVAL, "more than %d fields", BG_MAX_FIELDS);
+  }
+  int r = check_fields(fields, nfields);
+  if (r) return r;
+  bg_wm *wm = new bg_wm();
+  wm->fields.assign(fields, fields + nfields);
+  wm->key_size = (uint32_t)((acc + 7) / 8 * 8);
+  wm->kw = round_kw(wm->key_size);
+  *out = wm;
+  return 0;
+}
+
+void bg_wm_destroy(bg_wm *wm) {
+  if (!wm) return;
+  wm->dev.release();
+  wm->stage.release();
+  delete wm;
+}
+
+size_t bg_wm_key_size(const bg_wm *wm) { return wm->key_size; }
+
+int bg_wm_add(bg_wm *wm, const uint8_t *key, const uint8_t *mask,
+              int32_t priority, uint16_t gate) {
+  Key m = wm_key(wm, mask);
+  int idx = wm_find_tuple(wm, m);
+  if (idx < 0) {
+    if (wm->tuples.size() >= BG_MAX_TUPLES)
+      return fail(ENOSPC, "failed to add a new wildcard pattern");
+    wm->tuples.emplace_back();
+    wm->tuples.back().mask = m;
+    idx = (int)wm->tuples.size() - 1;
+  }
+  wm->tuples[idx].ht[wm_key(wm, key)] = WmVal{priority, gate};
+  wm->dirty = true;
+  return 0;
+}
+
+int bg_wm_delete(bg_wm *wm, const uint8_t *key, const uint8_t *mask) {
+  Key m = wm_key(wm, mask);
+  int idx = wm_find_tuple(wm, m);
+  if (idx < 0) return fail(ENOENT, "failed to delete a rule");
+  WmTupleH &t = wm->tuples[idx];
+  if (t.ht.erase(wm_key(wm, key)) == 0 && t.ht.empty())
+    wm->tuples.erase(wm->tuples.begin() + idx);  // DelEntry quirk (P6)
+  wm->dirty = true;
+  return 0;
+}
+
+void bg_wm_clear(bg_wm *wm) {
+  for (auto &t : wm->tuples) t.ht.clear();
+  wm->dirty = true;
+}
+
+int bg_wm_num_tuples(const bg_wm *wm) { return (int)wm->tuples.size(); }
+
+int bg_wm_tuple_mask(const bg_wm *wm, int t, uint8_t *mask_out) {
+  if (t < 0 || (size_t)t >= wm->tuples.size()) return fail(EINVAL, "bad tuple");
+  memset(mask_out, 0, BG_KEY_BYTES);
+  memcpy(mask_out, wm->tuples[t].mask.w, wm->key_size);
+  return 0;
+}
+
+size_t bg_wm_tuple_count(const bg_wm *wm, int t) {
+  if (t < 0 || (size_t)t >= wm->tuples.size()) return 0;
+  return wm->tuples[t].ht.size();
+}
+
+int bg_wm_iter(const bg_wm *wm, int t, size_t *cursor, uint8_t *key_out,
+               int32_t *priority, uint16_t *gate) {
+  if (t < 0 || (size_t)t >= wm->tuples.size()) return 0;
+  size_t i = 0;
+  for (auto &kv : wm->tuples[t].ht) {
+    if (i++ == *cursor) {
+      memset(key_out, 0, BG_KEY_BYTES);
+      memcpy(key_out, kv.first.w, wm->key_size);
+      *priority = kv.second.priority;
+      *gate = kv.second.gate;
+      (*cursor)++;
+      return 1;
+    }
+  }
+  return 0;
+}
+
+static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
+  if (!wm->dirty && wm->dev.valid && wm->dev.device == device) return 0;
+  std::vector<uint64_t> keys, seeds;
+  std::vector<uint8_t> vals, img;
+  for (size_t t = 0; t < wm->tuples.size(); t++) {
+    for (auto &kv : wm->tuples[t].ht) {
+      keys.insert(keys.end(), kv.first.w, kv.first.w + wm->kw);
+      uint64_t v = (uint64_t)(uint32_t)kv.second.priority |
+                   ((uint64_t)kv.second.gate << 32) | ((uint64_t)t << 48);
+      for (int b = 0; b < 8; b++) vals.push_back((uint8_t)(v >> (8 * b)));
+      seeds.push_back(tuple_seed(kDefaultSeed, (uint32_t)t));
+    }
+  }
+  TableLayout L;
+  int r = build_image(wm->kw, 8, 1, keys, vals, seeds, &img, &L);
+  if (r) return r;
+  r = wm->dev.upload(device, img, L, s);
+  if (r) return r;
+  wm->dirty = false;
+  return 0;
+}
+
+int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream) {
+  std::lock_guard<std::mutex> lk(wm->mu);
+  return wm_sync_locked(wm, device, (hipStream_t)stream);
+}
+
+static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
+                     uint16_t default_gate, uint16_t *d_gates, int shift,
+                     hipStream_t s) {
+  WmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.frames = static_cast<const uint8_t *>(d_frames);
+  a.stride = stride;
+  a.n = n;
+  a.gates = d_gates;
+  a.default_gate = default_gate;
+  a.ntuples = (uint32_t)wm->tuples.size();
+  a.fp = make_plan(wm->fields, false, shift);
+  a.t = wm->dev.ref();
+  for (size_t t = 0; t < wm->tuples.size(); t++)
+    for (uint32_t j = 0; j < wm->kw; j++) a.tmask[t][j] = wm->tuples[t].mask.w[j];
+  HIP_TRY(launch_wm(a, num_cus(wm->dev.device), s));
+  return 0;
+}
+
+int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
+                   uint16_t default_gate, uint16_t *d_gates,
+                   bg_stream_t stream) {
+  if (stride % 16 || ((uintptr_t)d_frames & 15))
+    return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
+  hipStream_t s = (hipStream_t)stream;
+  if (!wm->dev.valid || wm->dirty) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    std::lock_guard<std::mutex> lk(wm->mu);
+    int r = wm_sync_locked(wm, wm->dev.valid ? wm->dev.device : cur, s);
+    if (r) return r;
+  }
+  int r = set_device(wm->dev.device);
+  if (r) return r;
+  return wm_launch(wm, d_frames, stride, n, default_gate, d_gates, 0, s);
+}
+
+int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
+                       uint16_t default_gate, uint16_t *gates,
+                       bg_stream_t stream) {
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lk(wm->mu);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  int dev = wm->dev.valid ? wm->dev.device : cur;
+  int r = wm_sync_locked(wm, dev, s);
+  if (r) return r;
+  int shift;
+  size_t w;
+  r = stage_windows(wm->fields, heads, n, wm->stage, dev, &shift, &w);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(wm->stage.d_in, wm->stage.h_in, n * w,
+                         hipMemcpyHostToDevice, s));
+  r = wm_launch(wm, wm->stage.d_in, w, n, default_gate,
+                reinterpret_cast<uint16_t *>(wm->stage.d_out), shift, s);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(wm->stage.h_out, wm->stage.d_out, n * 2,
+                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  memcpy(gates, wm->stage.h_out, n * 2);
+  return 0;
+}
+
+int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds) {
+  if (!wm->dev.valid) return fail(EINVAL, "no device table yet");
+  *bytes = wm->dev.bytes;
+  *in_lds = wm->dev.ref().lds ? 1 : 0;
+  return 0;
+}
+
+// ============================================================================
+// IPChecksum / L4Checksum
+// ============================================================================
+int bg_cksum(int device, void *d_frames, size_t stride, size_t n, int mode,
+             int verify, uint16_t *d_ip_gates, uint16_t *d_l4_gates,
+             bg_stream_t stream) {
+  if (mode < 1 || mode > 3) return fail(EINVAL, "mode must be 1, 2 or 3");
+  if (stride % 16 || ((uintptr_t)d_frames & 15) || stride > (1u << 30))
+    return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
+  int r = set_device(device);
+  if (r) return r;
+  CkArgs a;
+  a.frames = static_cast<uint8_t *>(d_frames);
+  a.stride = stride;
+  a.n = n;
+  a.ip_gates = d_ip_gates;
+  a.l4_gates = d_l4_gates;
+  a.mode = mode;
+  a.verify = verify ? 1 : 0;
+  HIP_TRY(launch_cksum(a, num_cus(device), (hipStream_t)stream));
+  return 0;
+}
+
+int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
+                          size_t span, int mode, int verify,
+                          uint16_t *ip_gates, uint16_t *l4_gates,
+                          bg_stream_t stream) {
+  if (n == 0) return 0;
+  static thread_local Staging st;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t w = (span + 15) / 16 * 16;
+  int r = set_device(device);
+  if (r) return r;
+  r = st.ensure(device, n * w, n * 4);
+  if (r) return r;
+  for (size_t i = 0; i < n; i++) {
+    memcpy(st.h_in + i * w, heads[i], span);
+    if (w > span) memset(st.h_in + i * w + span, 0, w - span);
+  }
+  HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
+  uint16_t *dg = reinterpret_cast<uint16_t *>(st.d_out);
+  r = bg_cksum(device, st.d_in, w, n, mode, verify, dg, dg + n, stream);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(st.h_in, st.d_in, n * w, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (size_t i = 0; i < n; i++) memcpy(heads[i], st.h_in + i * w, span);
+  const uint16_t *hg = reinterpret_cast<const uint16_t *>(st.h_out);
+  if (ip_gates) memcpy(ip_gates, hg, n * 2);
+  if (l4_gates) memcpy(l4_gates, hg + n, n * 2);
+  return 0;
+}
+
+}  // extern "C"

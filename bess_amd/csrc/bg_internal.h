@@ -1,0 +1,75 @@
+// bg_internal.h -- host-side helpers shared by the C ABI translation units.
+#ifndef BESS_AMD_BG_INTERNAL_H_
+#define BESS_AMD_BG_INTERNAL_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/bessgpu.h"
+#include "bg_kernels.h"
+#include "bg_table.h"
+
+namespace bg {
+
+constexpr uint64_t kDefaultSeed = 0x5EED5EED0B5E55ULL;
+
+// A flow key as the reference stores it (ExactMatchKey / wm_hkey_t: eight
+// u64 words, bytes past total_key_size zero).
+struct Key {
+  uint64_t w[8];
+  bool operator==(const Key &o) const { return memcmp(w, o.w, sizeof(w)) == 0; }
+};
+struct KeyHash {
+  size_t operator()(const Key &k) const {
+    return (size_t)hash_words(k.w, 8, 0x1234567ULL);
+  }
+};
+
+struct WmVal {  // WmData (wildcard_match.h:57-60)
+  int32_t priority;
+  uint16_t gate;
+};
+
+extern thread_local std::string g_err;
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int num_cus(int device);
+int set_device(int device);
+uint32_t round_kw(uint32_t key_bytes);
+FieldPlan make_plan(const std::vector<bg_field> &fields, bool em_masks,
+                    int shift);
+void relayout(TableLayout &L, uint32_t nbp);
+int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
+                const std::vector<uint64_t> &keys,
+                const std::vector<uint8_t> &vals,
+                const std::vector<uint64_t> &seeds, std::vector<uint8_t> *img,
+                TableLayout *out_layout);
+
+struct DevTable {
+  int device = -1;
+  uint8_t *d_image = nullptr;
+  bool owned = true;
+  uint64_t bytes = 0;
+  TableLayout L{};
+  bool valid = false;
+  int upload(int dev, const std::vector<uint8_t> &img, const TableLayout &lay,
+             hipStream_t s);
+  void release();
+  TableRef ref() const;
+};
+
+struct Staging {
+  int device = -1;
+  uint8_t *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
+  size_t in_cap = 0, out_cap = 0;
+  int ensure(int dev, size_t in_bytes, size_t out_bytes);
+  void release();
+  ~Staging() { release(); }
+};
+
+}  // namespace bg
+
+#endif  // BESS_AMD_BG_INTERNAL_H_

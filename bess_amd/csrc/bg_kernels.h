@@ -1,0 +1,81 @@
+// bg_kernels.h -- kernel argument blocks and launchers (host <-> device).
+#ifndef BESS_AMD_BG_KERNELS_H_
+#define BESS_AMD_BG_KERNELS_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bg_table.h"
+
+namespace bg {
+
+constexpr int kMaxFields = 8;
+constexpr int kMaxTuples = 8;
+constexpr int kMaxWindowChunks = 4;      // 16-byte chunks staged per packet
+constexpr uint32_t kLdsTableMax = 40960;  // tables up to this size go to LDS
+constexpr uint16_t kGateNone = 0xFFFF;
+
+// How a packet's key is built from its frame bytes. Field f contributes
+// frame[off_f .. off_f+size_f) & mask_f at key byte pos_f
+// (ExactMatchTable::MakeKeys, exact_match_table.h:239-263; WildcardMatch::
+// ProcessBatch, wildcard_match.cc:169-197 -- there the mask is all-ones over
+// the field and the tuple mask is applied per probe).
+struct FieldPlan {
+  int32_t nf;      // number of fields
+  int32_t direct;  // 1: fields too far apart for one window -> per-field loads
+  int32_t win_lo;  // 16-byte aligned frame offset of the staged window
+  int32_t nch;     // 16-byte chunks in the window (1..4)
+  int32_t fdw[kMaxFields];   // window dword index of the field start
+  int32_t fsh[kMaxFields];   // bit shift of the field start inside that dword
+  int32_t fpos[kMaxFields];  // key byte position
+  int32_t foff[kMaxFields];  // frame byte offset (direct mode)
+  int32_t fnd[kMaxFields];   // dwords spanned by the field (direct mode)
+  int32_t pad;
+  uint64_t fmask[kMaxFields];  // mask in key byte order (low `size` bytes)
+};
+
+struct TableRef {
+  const uint8_t *base;  // device image (nparts * part_bytes)
+  uint64_t part_bytes, keys_off, vals_off, seed;
+  uint32_t nparts, nbp, kw, lds;  // lds: copy the image into LDS first
+  uint32_t bytes_total;           // image bytes (LDS copy length)
+  uint32_t pad;
+};
+
+struct EmArgs {
+  const uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *gates;
+  uint32_t default_gate, pad;
+  FieldPlan fp;
+  TableRef t;
+};
+
+struct WmArgs {
+  const uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *gates;
+  uint32_t default_gate, ntuples;
+  FieldPlan fp;
+  TableRef t;
+  uint64_t tmask[kMaxTuples][kMaxKeyWords];
+};
+
+struct CkArgs {
+  uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *ip_gates;  // may be null
+  uint16_t *l4_gates;  // may be null
+  int32_t mode;        // bit0 IPChecksum, bit1 L4Checksum
+  int32_t verify;
+};
+
+// Launchers (grid sizing from the device's CU count). Return hipSuccess or
+// the launch error.
+hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s);
+
+}  // namespace bg
+
+#endif  // BESS_AMD_BG_KERNELS_H_

@@ -1,0 +1,196 @@
+"""Python face of the device flow tables (bg_em / bg_wm / bg_cksum).
+
+Thin wrappers over include/bessgpu.h. Device buffers are torch tensors on a
+HIP device (torch is plumbing: memory, streams, RCCL); every byte of
+classification work runs in libbessgpu.so's gfx950 kernels.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import BessGpuError, bg_field, check, lib
+
+__all__ = ["EmTable", "WmTable", "cksum", "cksum_host", "resolve_em_fields",
+           "resolve_wm_fields", "BessGpuError"]
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+def _dev_ptr(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def resolve_em_fields(specs):
+    """[(offset, size, mask)] -> bg_field array with key positions (the
+    resolved ExactMatchField of exact_match_table.h:126-140)."""
+    arr = (bg_field * max(len(specs), 1))()
+    pos = 0
+    for i, (off, size, mask) in enumerate(specs):
+        arr[i].offset, arr[i].size, arr[i].pos = off, size, pos
+        arr[i].attr_id, arr[i].mask = -1, mask
+        pos += size
+    return arr, len(specs)
+
+
+def resolve_wm_fields(specs):
+    """[(offset, size)] -> bg_field array (WmField, wildcard_match.h:62-72)."""
+    return resolve_em_fields([(o, s, 0) for o, s in specs])
+
+
+class EmTable:
+    """bg_em: ExactMatchTable<gate_idx_t> with a device image."""
+
+    def __init__(self, fields):
+        """fields: [(offset, size, mask)] with mask = ExactMatchField::mask
+        (key byte order, low `size` bytes)."""
+        arr, n = resolve_em_fields(fields)
+        h = C.c_void_p()
+        check(lib().bg_em_create(arr, n, C.byref(h)))
+        self.h = h
+        self.key_size = lib().bg_em_key_size(h)
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_em_destroy(self.h)
+            self.h = None
+
+    def add(self, key, gate):
+        check(lib().bg_em_add(self.h, bytes(key).ljust(64, b"\0"), gate))
+
+    def add_many(self, keys, gates):
+        """keys: (n, key_size) uint8 array; gates: (n,) ints."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        buf = np.zeros(64, np.uint8)
+        for k, g in zip(keys, np.asarray(gates)):
+            buf[:keys.shape[1]] = k
+            check(lib().bg_em_add(self.h, buf.ctypes.data, int(g)))
+
+    def delete(self, key):
+        check(lib().bg_em_delete(self.h, bytes(key).ljust(64, b"\0")))
+
+    def clear(self):
+        lib().bg_em_clear(self.h)
+
+    def __len__(self):
+        return lib().bg_em_count(self.h)
+
+    def sync(self, device=0, stream=None):
+        check(lib().bg_em_sync(self.h, device, _stream_ptr(stream)))
+
+    def classify(self, frames, stride, n, default_gate, gates, stream=None):
+        """frames: device uint8 tensor (slab); gates: device int16/uint16."""
+        check(lib().bg_em_classify(self.h, _dev_ptr(frames), stride, n,
+                                   default_gate, _dev_ptr(gates),
+                                   _stream_ptr(stream)))
+
+    def process_host(self, frames_np, stride, n, default_gate, stream=None):
+        """Host frames (numpy slab) through the staged host path."""
+        base = frames_np.ctypes.data
+        heads = (C.c_void_p * n)(*[base + i * stride for i in range(n)])
+        out = np.zeros(n, np.uint16)
+        check(lib().bg_em_process_host(self.h, heads, n, default_gate,
+                                       out.ctypes.data, _stream_ptr(stream)))
+        return out
+
+    def plan(self, nparts):
+        pb = C.c_uint64()
+        check(lib().bg_em_plan(self.h, nparts, C.byref(pb)))
+        return pb.value
+
+    def build_part(self, part, nbytes):
+        buf = np.zeros(nbytes, np.uint8)
+        check(lib().bg_em_build_part(self.h, part, buf.ctypes.data))
+        return buf
+
+    def attach(self, device, d_image):
+        check(lib().bg_em_attach(self.h, device, _dev_ptr(d_image)))
+
+    def table_info(self):
+        b, l = C.c_uint64(), C.c_int()
+        check(lib().bg_em_table_info(self.h, C.byref(b), C.byref(l)))
+        return b.value, bool(l.value)
+
+
+class WmTable:
+    """bg_wm: WildcardMatch tuple tables with a device image."""
+
+    def __init__(self, fields):
+        """fields: [(offset, size)]"""
+        arr, n = resolve_wm_fields(fields)
+        h = C.c_void_p()
+        check(lib().bg_wm_create(arr, n, C.byref(h)))
+        self.h = h
+        self.key_size = lib().bg_wm_key_size(h)
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_wm_destroy(self.h)
+            self.h = None
+
+    def add(self, key, mask, priority, gate):
+        check(lib().bg_wm_add(self.h, bytes(key).ljust(64, b"\0"),
+                              bytes(mask).ljust(64, b"\0"), priority, gate))
+
+    def delete(self, key, mask):
+        check(lib().bg_wm_delete(self.h, bytes(key).ljust(64, b"\0"),
+                                 bytes(mask).ljust(64, b"\0")))
+
+    def clear(self):
+        lib().bg_wm_clear(self.h)
+
+    def num_tuples(self):
+        return lib().bg_wm_num_tuples(self.h)
+
+    def sync(self, device=0, stream=None):
+        check(lib().bg_wm_sync(self.h, device, _stream_ptr(stream)))
+
+    def classify(self, frames, stride, n, default_gate, gates, stream=None):
+        check(lib().bg_wm_classify(self.h, _dev_ptr(frames), stride, n,
+                                   default_gate, _dev_ptr(gates),
+                                   _stream_ptr(stream)))
+
+    def process_host(self, frames_np, stride, n, default_gate, stream=None):
+        base = frames_np.ctypes.data
+        heads = (C.c_void_p * n)(*[base + i * stride for i in range(n)])
+        out = np.zeros(n, np.uint16)
+        check(lib().bg_wm_process_host(self.h, heads, n, default_gate,
+                                       out.ctypes.data, _stream_ptr(stream)))
+        return out
+
+    def table_info(self):
+        b, l = C.c_uint64(), C.c_int()
+        check(lib().bg_wm_table_info(self.h, C.byref(b), C.byref(l)))
+        return b.value, bool(l.value)
+
+
+def cksum(frames, stride, n, mode, verify, ip_gates=None, l4_gates=None,
+          device=0, stream=None):
+    """IPChecksum (mode 1) / L4Checksum (mode 2) / both (3) on a device slab,
+    in place."""
+    check(lib().bg_cksum(device, _dev_ptr(frames), stride, n, mode,
+                         1 if verify else 0,
+                         _dev_ptr(ip_gates) if ip_gates is not None else None,
+                         _dev_ptr(l4_gates) if l4_gates is not None else None,
+                         _stream_ptr(stream)))
+
+
+def cksum_host(frames_np, stride, n, mode, verify, span=None, device=0,
+               stream=None):
+    """Host slab through the staged host path (in place); returns gates."""
+    span = stride if span is None else span
+    base = frames_np.ctypes.data
+    heads = (C.c_void_p * n)(*[base + i * stride for i in range(n)])
+    ipg = np.zeros(n, np.uint16)
+    l4g = np.zeros(n, np.uint16)
+    check(lib().bg_cksum_process_host(device, heads, n, span, mode,
+                                      1 if verify else 0, ipg.ctypes.data,
+                                      l4g.ctypes.data, _stream_ptr(stream)))
+    return ipg, l4g

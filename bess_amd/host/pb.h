@@ -1,0 +1,311 @@
+// pb.h -- the protobuf messages of the classification path, with a
+// hand-written proto3 wire codec (this image has no protoc / libprotobuf).
+//
+// Field numbers and types follow protobuf/module_msg.proto and
+// protobuf/util_msg.proto of the reference (cited per message). Accessors
+// use the names protoc would generate (fields_size(), fields(i),
+// add_fields(), encoding_case(), value_bin(), ...) so module code reads the
+// same against real generated headers.
+#ifndef BESS_AMD_HOST_PB_H_
+#define BESS_AMD_HOST_PB_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace bess {
+namespace pb {
+
+// ---- wire helpers ------------------------------------------------------
+class Reader {
+ public:
+  Reader(const void *p, size_t n)
+      : p_(static_cast<const uint8_t *>(p)), end_(p_ + n) {}
+  bool done() const { return p_ >= end_; }
+  bool ok() const { return ok_; }
+  // next field: number + wire type; false at end or on malformed input
+  bool next(uint32_t *field, uint32_t *wt);
+  bool varint(uint64_t *v);
+  bool bytes(const uint8_t **d, size_t *n);
+  bool skip(uint32_t wt);
+
+ private:
+  const uint8_t *p_, *end_;
+  bool ok_ = true;
+};
+
+class Writer {
+ public:
+  void varint_field(uint32_t field, uint64_t v);
+  void bytes_field(uint32_t field, const void *d, size_t n);
+  void raw_varint(uint64_t v);
+  std::string &str() { return s_; }
+
+ private:
+  std::string s_;
+};
+
+template <typename T>
+class Repeated {
+ public:
+  int size() const { return (int)v_.size(); }
+  const T &Get(int i) const { return v_[i]; }
+  const T &operator[](int i) const { return v_[i]; }
+  T *Add() {
+    v_.emplace_back();
+    return &v_.back();
+  }
+  T *Mutable(int i) { return &v_[i]; }
+  typename std::vector<T>::iterator begin() { return v_.begin(); }
+  typename std::vector<T>::iterator end() { return v_.end(); }
+  typename std::vector<T>::const_iterator begin() const { return v_.begin(); }
+  typename std::vector<T>::const_iterator end() const { return v_.end(); }
+  void Clear() { v_.clear(); }
+
+ private:
+  std::vector<T> v_;
+};
+
+// Base of every message: parse/serialize entry points.
+class Message {
+ public:
+  virtual ~Message() = default;
+  bool ParseFromArray(const void *data, size_t n);
+  std::string SerializeAsString() const;
+  virtual bool MergeField(Reader &r, uint32_t field, uint32_t wt) = 0;
+  virtual void Write(Writer &w) const = 0;
+};
+
+// util_msg.proto:45-50
+class FieldData : public Message {
+ public:
+  enum EncodingCase { ENCODING_NOT_SET = 0, kValueBin = 1, kValueInt = 2 };
+  EncodingCase encoding_case() const { return case_; }
+  const std::string &value_bin() const { return bin_; }
+  uint64_t value_int() const { return case_ == kValueInt ? int_ : 0; }
+  void set_value_bin(const void *d, size_t n) {
+    case_ = kValueBin;
+    bin_.assign(static_cast<const char *>(d), n);
+    int_ = 0;
+  }
+  void set_value_int(uint64_t v) {
+    case_ = kValueInt;
+    int_ = v;
+    bin_.clear();
+  }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  EncodingCase case_ = ENCODING_NOT_SET;
+  std::string bin_;
+  uint64_t int_ = 0;
+};
+
+// util_msg.proto:36-42
+class Field : public Message {
+ public:
+  enum PositionCase { POSITION_NOT_SET = 0, kAttrName = 1, kOffset = 2 };
+  PositionCase position_case() const { return case_; }
+  const std::string &attr_name() const { return attr_; }
+  uint32_t offset() const { return case_ == kOffset ? offset_ : 0; }
+  uint32_t num_bytes() const { return num_bytes_; }
+  void set_attr_name(const std::string &s) {
+    case_ = kAttrName;
+    attr_ = s;
+    offset_ = 0;
+  }
+  void set_offset(uint32_t o) {
+    case_ = kOffset;
+    offset_ = o;
+    attr_.clear();
+  }
+  void set_num_bytes(uint32_t n) { num_bytes_ = n; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  PositionCase case_ = POSITION_NOT_SET;
+  std::string attr_;
+  uint32_t offset_ = 0;
+  uint32_t num_bytes_ = 0;
+};
+
+// module_msg.proto:50
+class EmptyArg : public Message {
+ public:
+  bool MergeField(Reader &r, uint32_t, uint32_t wt) override {
+    return r.skip(wt);
+  }
+  void Write(Writer &) const override {}
+};
+
+// module_msg.proto:501-504
+class ExactMatchArg : public Message {
+ public:
+  int fields_size() const { return fields_.size(); }
+  const Field &fields(int i) const { return fields_.Get(i); }
+  Field *add_fields() { return fields_.Add(); }
+  int masks_size() const { return masks_.size(); }
+  const FieldData &masks(int i) const { return masks_.Get(i); }
+  FieldData *add_masks() { return masks_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<Field> fields_;
+  Repeated<FieldData> masks_;
+};
+
+// module_msg.proto:69-72
+class ExactMatchCommandAddArg : public Message {
+ public:
+  uint64_t gate() const { return gate_; }
+  void set_gate(uint64_t g) { gate_ = g; }
+  int fields_size() const { return fields_.size(); }
+  const FieldData &fields(int i) const { return fields_.Get(i); }
+  FieldData *add_fields() { return fields_.Add(); }
+  const Repeated<FieldData> &fields() const { return fields_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint64_t gate_ = 0;
+  Repeated<FieldData> fields_;
+};
+
+// module_msg.proto:78-80
+class ExactMatchCommandDeleteArg : public Message {
+ public:
+  int fields_size() const { return fields_.size(); }
+  const FieldData &fields(int i) const { return fields_.Get(i); }
+  FieldData *add_fields() { return fields_.Add(); }
+  const Repeated<FieldData> &fields() const { return fields_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<FieldData> fields_;
+};
+
+// module_msg.proto:94-96 / 403-405: one `uint64 gate = 1`
+class SetDefaultGateArg : public Message {
+ public:
+  uint64_t gate() const { return gate_; }
+  void set_gate(uint64_t g) { gate_ = g; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint64_t gate_ = 0;
+};
+using ExactMatchCommandSetDefaultGateArg = SetDefaultGateArg;
+using WildcardMatchCommandSetDefaultGateArg = SetDefaultGateArg;
+
+// module_msg.proto:511-514
+class ExactMatchConfig : public Message {
+ public:
+  uint64_t default_gate() const { return default_gate_; }
+  void set_default_gate(uint64_t g) { default_gate_ = g; }
+  int rules_size() const { return rules_.size(); }
+  const ExactMatchCommandAddArg &rules(int i) const { return rules_.Get(i); }
+  ExactMatchCommandAddArg *add_rules() { return rules_.Add(); }
+  Repeated<ExactMatchCommandAddArg> *mutable_rules() { return &rules_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint64_t default_gate_ = 0;
+  Repeated<ExactMatchCommandAddArg> rules_;
+};
+
+// module_msg.proto:1152-1154
+class WildcardMatchArg : public Message {
+ public:
+  int fields_size() const { return fields_.size(); }
+  const Field &fields(int i) const { return fields_.Get(i); }
+  Field *add_fields() { return fields_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<Field> fields_;
+};
+
+// module_msg.proto:375-380
+class WildcardMatchCommandAddArg : public Message {
+ public:
+  uint64_t gate() const { return gate_; }
+  void set_gate(uint64_t g) { gate_ = g; }
+  int64_t priority() const { return priority_; }
+  void set_priority(int64_t p) { priority_ = p; }
+  int values_size() const { return values_.size(); }
+  const FieldData &values(int i) const { return values_.Get(i); }
+  FieldData *add_values() { return values_.Add(); }
+  int masks_size() const { return masks_.size(); }
+  const FieldData &masks(int i) const { return masks_.Get(i); }
+  FieldData *add_masks() { return masks_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint64_t gate_ = 0;
+  int64_t priority_ = 0;
+  Repeated<FieldData> values_;
+  Repeated<FieldData> masks_;
+};
+
+// module_msg.proto:385-388
+class WildcardMatchCommandDeleteArg : public Message {
+ public:
+  int values_size() const { return values_.size(); }
+  const FieldData &values(int i) const { return values_.Get(i); }
+  FieldData *add_values() { return values_.Add(); }
+  int masks_size() const { return masks_.size(); }
+  const FieldData &masks(int i) const { return masks_.Get(i); }
+  FieldData *add_masks() { return masks_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<FieldData> values_;
+  Repeated<FieldData> masks_;
+};
+
+// module_msg.proto:1161-1164
+class WildcardMatchConfig : public Message {
+ public:
+  uint64_t default_gate() const { return default_gate_; }
+  void set_default_gate(uint64_t g) { default_gate_ = g; }
+  int rules_size() const { return rules_.size(); }
+  const WildcardMatchCommandAddArg &rules(int i) const { return rules_.Get(i); }
+  WildcardMatchCommandAddArg *add_rules() { return rules_.Add(); }
+  Repeated<WildcardMatchCommandAddArg> *mutable_rules() { return &rules_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint64_t default_gate_ = 0;
+  Repeated<WildcardMatchCommandAddArg> rules_;
+};
+
+// module_msg.proto:997-999 (IPChecksumArg) / 1010-1012 (L4ChecksumArg)
+class VerifyArg : public Message {
+ public:
+  bool verify() const { return verify_; }
+  void set_verify(bool v) { verify_ = v; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  bool verify_ = false;
+};
+using IPChecksumArg = VerifyArg;
+using L4ChecksumArg = VerifyArg;
+
+}  // namespace pb
+}  // namespace bess
+
+#endif  // BESS_AMD_HOST_PB_H_

@@ -1,0 +1,179 @@
+/*
+ * bessgpu.h -- C ABI of libbessgpu.so, the MI355X (gfx950) implementation of
+ * BESS's per-batch packet-classification hot path.
+ *
+ * Plain C: pointers, sizes, integers. Every entry point returns 0 on success
+ * or a negative errno (-EINVAL, -ENOENT, -ENOSPC, -ENODEV, -EIO, ...), the
+ * way the reference reports CommandFailure(errno, ...) (core/message.h:44-53);
+ * bg_last_error() returns the message of the calling thread's last failure.
+ *
+ * Which reference interface each group replaces (NetSys/bess paths):
+ *   bg_em_*   ExactMatchTable<gate_idx_t> (core/utils/exact_match_table.h:
+ *             146-458) and the datapath of ExactMatch::ProcessBatch
+ *             (core/modules/exact_match.cc:224-244)
+ *   bg_wm_*   WildcardMatch tuple tables + LookupEntry / ProcessBatch
+ *             (core/modules/wildcard_match.cc:136-203, 278-315)
+ *   bg_cksum  IPChecksum::ProcessBatch (core/modules/ip_checksum.cc:39-84)
+ *             and L4Checksum::ProcessBatch (core/modules/l4_checksum.cc:41-83)
+ *   bg_module_*  the module surface BESS's control plane drives: create with
+ *             an <Class>Arg protobuf (core/module.h:93-102 MODULE_INIT_FUNC,
+ *             core/bessctl.cc:1205 CreateModule), run a command by name with
+ *             its protobuf argument (core/module.cc:92-116 RunCommand,
+ *             core/bessctl.cc:1760 ModuleCommand), and ProcessBatch over a
+ *             batch of packet head pointers (core/module.h:226) returning the
+ *             per-packet EmitPacket gate (core/module.h:543).
+ *
+ * Device pointers (d_*) are HIP device memory on the handle's device;
+ * `stream` is a hipStream_t (NULL = the legacy default stream).
+ * Frame slabs: frame i starts at d_frames + i*stride (= Packet::head_data(),
+ * core/packet.h:84-94); stride must be a multiple of 16 and d_frames 16-byte
+ * aligned.
+ */
+#ifndef BESSGPU_H_
+#define BESSGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BG_MAX_GATES 8192   /* core/gate.h:57 */
+#define BG_DROP_GATE 8192   /* core/gate.h:58 */
+#define BG_GATE_NONE 0xFFFF /* packet not emitted (L4Checksum) */
+#define BG_MAX_FIELDS 8     /* exact_match_table.h:50 */
+#define BG_MAX_TUPLES 8     /* wildcard_match.h:45 */
+#define BG_KEY_BYTES 64     /* sizeof(ExactMatchKey) */
+
+#define BG_CK_IP 1 /* IPChecksum */
+#define BG_CK_L4 2 /* L4Checksum */
+
+typedef void *bg_stream_t; /* hipStream_t */
+
+/* A field as resolved by ExactMatchTable::DoAddField (exact_match_table.h:
+ * 391-443) or WildcardMatch::Init (wildcard_match.cc:111-134). */
+typedef struct bg_field {
+  int32_t offset; /* bytes from head_data() */
+  int32_t size;   /* 1..8 */
+  int32_t pos;    /* byte position in the key */
+  int32_t attr_id; /* -1: offset field (metadata fields: not on the device) */
+  uint64_t mask;  /* EM: ExactMatchField::mask (key byte order); WM: unused */
+} bg_field;
+
+/* ---- runtime ---------------------------------------------------------- */
+const char *bg_version(void);
+const char *bg_last_error(void);
+int bg_device_count(void);
+/* allocate / free / copy device memory (convenience for C callers) */
+int bg_malloc(int device, size_t bytes, void **d_ptr);
+int bg_free(void *d_ptr);
+int bg_memcpy_h2d(void *d_dst, const void *src, size_t bytes, bg_stream_t s);
+int bg_memcpy_d2h(void *dst, const void *d_src, size_t bytes, bg_stream_t s);
+int bg_stream_sync(bg_stream_t s);
+
+/* ---- ExactMatch -------------------------------------------------------- */
+typedef struct bg_em bg_em;
+int bg_em_create(const bg_field *fields, int nfields, bg_em **out);
+void bg_em_destroy(bg_em *em);
+size_t bg_em_key_size(const bg_em *em); /* total_key_size_ */
+/* key: total_key_size bytes, as ExactMatchTable::gather_key lays it out
+ * (exact_match_table.h:332-357). Insert-or-overwrite (cuckoo_map.h:182-187). */
+int bg_em_add(bg_em *em, const uint8_t *key, uint16_t gate);
+int bg_em_delete(bg_em *em, const uint8_t *key); /* -ENOENT if absent */
+void bg_em_clear(bg_em *em);
+size_t bg_em_count(const bg_em *em);
+/* iterate rules (unspecified order); returns 1 with a rule, 0 at the end */
+int bg_em_iter(const bg_em *em, size_t *cursor, uint8_t *key_out,
+               uint16_t *gate_out);
+/* Rebuild/upload the device table if rules changed (control path). */
+int bg_em_sync(bg_em *em, int device, bg_stream_t stream);
+/* Device-resident classify: d_gates[i] = gate for frame i (default_gate on
+ * a miss). Calls bg_em_sync implicitly when needed (not capturable then). */
+int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
+                   uint16_t default_gate, uint16_t *d_gates, bg_stream_t stream);
+/* Host batch (PacketBatch-style head pointers): stage the key window of
+ * each frame into pinned memory, classify, copy gates back; synchronous. */
+int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
+                       uint16_t default_gate, uint16_t *gates,
+                       bg_stream_t stream);
+/* Sharded table build (multi-GPU): fix a layout of `nparts` partitions for
+ * the current rules, export the host image of one partition, and attach an
+ * externally assembled (all-gathered) device image. */
+int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes);
+int bg_em_build_part(bg_em *em, int part, void *host_dst);
+int bg_em_attach(bg_em *em, int device, const void *d_image);
+/* bytes of the current device table image and whether it lives in LDS */
+int bg_em_table_info(const bg_em *em, uint64_t *bytes, int *in_lds);
+
+/* ---- WildcardMatch ----------------------------------------------------- */
+typedef struct bg_wm bg_wm;
+int bg_wm_create(const bg_field *fields, int nfields, bg_wm **out);
+void bg_wm_destroy(bg_wm *wm);
+size_t bg_wm_key_size(const bg_wm *wm);
+/* key/mask: 64-byte keys as ExtractKeyMask builds them (wildcard_match.cc:
+ * 215-276). FindTuple/AddTuple/Insert of CommandAdd (317-354); -ENOSPC on
+ * a 9th distinct mask. */
+int bg_wm_add(bg_wm *wm, const uint8_t *key, const uint8_t *mask,
+              int32_t priority, uint16_t gate);
+/* CommandDelete/DelEntry (357-377, 302-315), including the reference's
+ * "failed remove on an empty tuple erases it and succeeds" behaviour. */
+int bg_wm_delete(bg_wm *wm, const uint8_t *key, const uint8_t *mask);
+void bg_wm_clear(bg_wm *wm); /* Clear(): tables emptied, tuples kept */
+int bg_wm_num_tuples(const bg_wm *wm);
+int bg_wm_tuple_mask(const bg_wm *wm, int t, uint8_t *mask_out);
+size_t bg_wm_tuple_count(const bg_wm *wm, int t);
+int bg_wm_iter(const bg_wm *wm, int t, size_t *cursor, uint8_t *key_out,
+               int32_t *priority, uint16_t *gate);
+int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream);
+int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
+                   uint16_t default_gate, uint16_t *d_gates, bg_stream_t stream);
+int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
+                       uint16_t default_gate, uint16_t *gates,
+                       bg_stream_t stream);
+int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds);
+
+/* ---- IPChecksum / L4Checksum ------------------------------------------ */
+/* mode: BG_CK_IP, BG_CK_L4 or both (= IPChecksum -> L4Checksum pipeline:
+ * only frames IPChecksum emits on gate 0 reach L4Checksum). Checksums are
+ * written in place into the frames; gates: 0 forward, 1 fail, BG_GATE_NONE
+ * not emitted / not reached. d_ip_gates / d_l4_gates may be NULL. */
+int bg_cksum(int device, void *d_frames, size_t stride, size_t n, int mode,
+             int verify, uint16_t *d_ip_gates, uint16_t *d_l4_gates,
+             bg_stream_t stream);
+/* host frames (head pointers, each with >= `span` readable/writable bytes):
+ * staged to the device, processed, written back; synchronous. */
+int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
+                          size_t span, int mode, int verify,
+                          uint16_t *ip_gates, uint16_t *l4_gates,
+                          bg_stream_t stream);
+
+/* ---- BESS module surface (protobuf arguments) -------------------------- */
+typedef struct bg_module bg_module;
+/* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".
+ * arg: serialized bess.pb.<mclass>Arg. On failure returns -errno and the
+ * reference's message via bg_last_error(). */
+int bg_module_create(const char *mclass, const void *arg, size_t arg_len,
+                     bg_module **out);
+void bg_module_destroy(bg_module *m);
+/* cmd by name with its serialized argument (arg type per the module's cmds
+ * table). The serialized response message (e.g. ExactMatchConfig for
+ * get_runtime_config, empty for add) goes to out (capacity *out_len; on
+ * return *out_len = bytes needed). */
+int bg_module_command(bg_module *m, const char *cmd, const void *arg,
+                      size_t arg_len, void *out, size_t *out_len);
+/* ProcessBatch over cnt <= any packets: heads[i] = head_data() of packet i;
+ * ogates[i] = the gate EmitPacket would receive (BG_GATE_NONE: none). */
+int bg_module_process(bg_module *m, uint8_t *const *heads, size_t cnt,
+                      uint16_t *ogates);
+/* Device-resident ProcessBatch over a slab. */
+int bg_module_process_device(bg_module *m, void *d_frames, size_t stride,
+                             size_t n, uint16_t *d_ogates, bg_stream_t stream);
+int bg_module_set_device(bg_module *m, int device);
+/* GetDesc() (exact_match.cc:246-249, wildcard_match.cc:205-213) */
+int bg_module_desc(const bg_module *m, char *buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BESSGPU_H_ */
