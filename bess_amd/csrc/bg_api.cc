@@ -86,18 +86,16 @@ FieldPlan make_plan(const std::vector<bg_field> &fields, bool em_masks,
   p.win_lo = lo & ~15;
   p.nch = (hi - p.win_lo + 15) / 16;
   p.direct = p.nch > kMaxWindowChunks;
+  if (p.direct) p.nch = 0;
   for (int i = 0; i < p.nf; i++) {
     const bg_field &f = fields[i];
     const int off = f.offset + shift;
-    p.fdw[i] = (off - p.win_lo) >> 2;
-    p.fsh[i] = (off & 3) * 8;
-    p.fpos[i] = f.pos;
-    p.foff[i] = off;
-    p.fnd[i] = ((off + f.size - 1) >> 2) - (off >> 2) + 1;
+    const int nd = ((off + f.size - 1) >> 2) - (off >> 2) + 1;
+    const int d = p.direct ? (off >> 2) : ((off - p.win_lo) >> 2);
+    p.fspec[i] = pack_fspec(d, off & 3, f.pos, nd);
     uint64_t size_mask = f.size >= 8 ? ~0ULL : ((1ULL << (8 * f.size)) - 1);
     p.fmask[i] = em_masks ? (f.mask & size_mask) : size_mask;
   }
-  if (p.direct) p.nch = 0;
   return p;
 }
 

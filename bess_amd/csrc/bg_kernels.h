@@ -25,14 +25,21 @@ struct FieldPlan {
   int32_t direct;  // 1: fields too far apart for one window -> per-field loads
   int32_t win_lo;  // 16-byte aligned frame offset of the staged window
   int32_t nch;     // 16-byte chunks in the window (1..4)
-  int32_t fdw[kMaxFields];   // window dword index of the field start
-  int32_t fsh[kMaxFields];   // bit shift of the field start inside that dword
-  int32_t fpos[kMaxFields];  // key byte position
-  int32_t foff[kMaxFields];  // frame byte offset (direct mode)
-  int32_t fnd[kMaxFields];   // dwords spanned by the field (direct mode)
-  int32_t pad;
+  // per field, packed to keep the kernels' scalar registers low:
+  // bits 0-8 window dword index (direct: frame dword index), 9-10 byte shift
+  // inside that dword, 11-16 key byte position, 17-18 dwords spanned
+  uint32_t fspec[kMaxFields];
   uint64_t fmask[kMaxFields];  // mask in key byte order (low `size` bytes)
 };
+
+BG_HD uint32_t pack_fspec(int d, int byte_shift, int pos, int nd) {
+  return (uint32_t)(d & 0x1FF) | ((uint32_t)(byte_shift & 3) << 9) |
+         ((uint32_t)(pos & 0x3F) << 11) | ((uint32_t)(nd & 3) << 17);
+}
+BG_HD int fspec_d(uint32_t s) { return (int)(s & 0x1FF); }
+BG_HD int fspec_shift_bits(uint32_t s) { return (int)((s >> 9) & 3) * 8; }
+BG_HD int fspec_pos(uint32_t s) { return (int)((s >> 11) & 0x3F); }
+BG_HD int fspec_nd(uint32_t s) { return (int)((s >> 17) & 3); }
 
 struct TableRef {
   const uint8_t *base;  // device image (nparts * part_bytes)

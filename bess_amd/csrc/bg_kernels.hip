@@ -9,6 +9,9 @@
 // at frames + i*stride). No MFMA: there is no contraction on this path.
 #include <hip/hip_runtime.h>
 #include <limits.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "bg_kernels.h"
 
@@ -17,6 +20,7 @@ namespace {
 
 constexpr int kEmBlock = 512;  // 8 waves; LDS tables <= 40 KB -> 4 blocks/CU
 constexpr int kCkBlock = 256;
+constexpr int kDefaultPpl = 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -40,63 +44,112 @@ __device__ __forceinline__ uint32_t tag_match(uint32_t tags, uint32_t tag) {
   return compact_bytes((x - 0x01010101u) & ~x & 0x80808080u);
 }
 
-// Build the key of one frame. The window [win_lo, win_lo + 16*nch) is
-// staged in registers with 16-byte loads; each field is funnel-shifted out
-// of it with a wave-uniform dword index (s_set_gpr_idx, no scratch).
+// Key building (ExactMatchTable::MakeKeys exact_match_table.h:239-263 /
+// WildcardMatch::ProcessBatch wildcard_match.cc:169-197). The window
+// [win_lo, win_lo + 16*nch) of a frame is staged in registers with 16-byte
+// loads; each field is funnel-shifted out of it with a wave-uniform dword
+// index (s_set_gpr_idx, no scratch) and OR-ed into its key word(s).
+template <int NCH>
+__device__ __forceinline__ void load_window(const uint8_t *__restrict__ frame,
+                                            const FieldPlan &fp,
+                                            uint32_t (&w)[NCH * 4 + 2]) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(frame + fp.win_lo);
+#pragma unroll
+  for (int c = 0; c < NCH; c++) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (c < fp.nch) v = ld_stream(src + c);
+    w[4 * c + 0] = v.x;
+    w[4 * c + 1] = v.y;
+    w[4 * c + 2] = v.z;
+    w[4 * c + 3] = v.w;
+  }
+  w[NCH * 4] = 0;
+  w[NCH * 4 + 1] = 0;
+}
+
 template <int KW>
-__device__ __forceinline__ void build_key(const uint8_t *__restrict__ frame,
-                                          const FieldPlan &fp,
-                                          uint64_t (&k)[KW]) {
+__device__ __forceinline__ void place_field(uint64_t v, int p,
+                                            uint64_t (&k)[KW]) {
+  const int pw = p >> 3, pb = (p & 7) * 8;
+#pragma unroll
+  for (int j = 0; j < KW; j++) {
+    if (j == pw) k[j] |= v << pb;
+    if (pb && j == pw + 1) k[j] |= v >> (64 - pb);
+  }
+}
+
+template <int KW, int NCH>
+__device__ __forceinline__ void extract_key(const uint32_t (&w)[NCH * 4 + 2],
+                                            const FieldPlan &fp,
+                                            uint64_t (&k)[KW]) {
 #pragma unroll
   for (int j = 0; j < KW; j++) k[j] = 0;
-  if (!fp.direct) {
-    uint32_t w[kMaxWindowChunks * 4 + 2];
-    const uint4 *src = reinterpret_cast<const uint4 *>(frame + fp.win_lo);
 #pragma unroll
-    for (int c = 0; c < kMaxWindowChunks; c++) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (c < fp.nch) v = ld_stream(src + c);
-      w[4 * c + 0] = v.x;
-      w[4 * c + 1] = v.y;
-      w[4 * c + 2] = v.z;
-      w[4 * c + 3] = v.w;
+  for (int f = 0; f < kMaxFields; f++) {
+    if (f < fp.nf) {
+      const uint32_t spec = fp.fspec[f];
+      const int d = fspec_d(spec), sh = fspec_shift_bits(spec);
+      uint64_t lo = (uint64_t)w[d] | ((uint64_t)w[d + 1] << 32);
+      uint64_t v = sh ? ((lo >> sh) | ((uint64_t)w[d + 2] << (64 - sh))) : lo;
+      place_field<KW>(v & fp.fmask[f], fspec_pos(spec), k);
     }
-    w[kMaxWindowChunks * 4] = 0;
-    w[kMaxWindowChunks * 4 + 1] = 0;
+  }
+}
+
+// fields too far apart for one window: per-field aligned dword loads
+template <int KW>
+__device__ __forceinline__ void direct_key(const uint8_t *__restrict__ frame,
+                                           const FieldPlan &fp,
+                                           uint64_t (&k)[KW]) {
 #pragma unroll
-    for (int f = 0; f < kMaxFields; f++) {
-      if (f < fp.nf) {
-        const int d = fp.fdw[f], sh = fp.fsh[f];
-        uint64_t lo = (uint64_t)w[d] | ((uint64_t)w[d + 1] << 32);
-        uint64_t v = sh ? ((lo >> sh) | ((uint64_t)w[d + 2] << (64 - sh))) : lo;
-        v &= fp.fmask[f];
-        const int p = fp.fpos[f], pw = p >> 3, pb = (p & 7) * 8;
+  for (int j = 0; j < KW; j++) k[j] = 0;
 #pragma unroll
-        for (int j = 0; j < KW; j++) {
-          if (j == pw) k[j] |= v << pb;
-          if (pb && j == pw + 1) k[j] |= v >> (64 - pb);
-        }
+  for (int f = 0; f < kMaxFields; f++) {
+    if (f < fp.nf) {
+      const uint32_t spec = fp.fspec[f];
+      const uint32_t *q =
+          reinterpret_cast<const uint32_t *>(frame) + fspec_d(spec);
+      const int nd = fspec_nd(spec), sh = fspec_shift_bits(spec);
+      uint32_t d0 = q[0];
+      uint32_t d1 = nd > 1 ? q[1] : 0u;
+      uint32_t d2 = nd > 2 ? q[2] : 0u;
+      uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
+      uint64_t v = sh ? ((lo >> sh) | ((uint64_t)d2 << (64 - sh))) : lo;
+      place_field<KW>(v & fp.fmask[f], fspec_pos(spec), k);
+    }
+  }
+}
+
+// Keys of PPL packets handled by one lane (idx = base + j*blockDim.x): all
+// window loads are issued before any key is built (memory-level parallelism).
+template <int KW, int NCH, int PPL>
+__device__ __forceinline__ void build_keys(const uint8_t *__restrict__ frames,
+                                           uint64_t stride, uint64_t n,
+                                           uint64_t base, const FieldPlan &fp,
+                                           uint64_t (&k)[PPL][KW]) {
+  if constexpr (NCH > 0) {
+    uint32_t w[PPL][NCH * 4 + 2];
+#pragma unroll
+    for (int j = 0; j < PPL; j++) {
+      const uint64_t idx = base + (uint64_t)j * blockDim.x;
+      if (idx < n) {
+        load_window<NCH>(frames + idx * stride, fp, w[j]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < NCH * 4 + 2; q++) w[j][q] = 0;
       }
     }
+#pragma unroll
+    for (int j = 0; j < PPL; j++) extract_key<KW, NCH>(w[j], fp, k[j]);
   } else {
 #pragma unroll
-    for (int f = 0; f < kMaxFields; f++) {
-      if (f < fp.nf) {
-        const uint32_t *q =
-            reinterpret_cast<const uint32_t *>(frame + (fp.foff[f] & ~3));
-        const int nd = fp.fnd[f], sh = fp.fsh[f];
-        uint32_t d0 = q[0];
-        uint32_t d1 = nd > 1 ? q[1] : 0u;
-        uint32_t d2 = nd > 2 ? q[2] : 0u;
-        uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
-        uint64_t v = sh ? ((lo >> sh) | ((uint64_t)d2 << (64 - sh))) : lo;
-        v &= fp.fmask[f];
-        const int p = fp.fpos[f], pw = p >> 3, pb = (p & 7) * 8;
+    for (int j = 0; j < PPL; j++) {
+      const uint64_t idx = base + (uint64_t)j * blockDim.x;
+      if (idx < n) {
+        direct_key<KW>(frames + idx * stride, fp, k[j]);
+      } else {
 #pragma unroll
-        for (int j = 0; j < KW; j++) {
-          if (j == pw) k[j] |= v << pb;
-          if (pb && j == pw + 1) k[j] |= v >> (64 - pb);
-        }
+        for (int q = 0; q < KW; q++) k[j][q] = 0;
       }
     }
   }
@@ -168,24 +221,44 @@ __device__ __forceinline__ void copy_table_to_lds(uint8_t *lds,
 }
 
 // ---------------------------------------------------------------------------
-// ExactMatch: one lane per packet, grid-stride over the resident slab.
+// ExactMatch: one lane per packet (PPL packets per lane per iteration),
+// grid-stride over the resident slab with a residency-sized grid.
 // ---------------------------------------------------------------------------
-template <int KW>
-__global__ __launch_bounds__(kEmBlock) void em_classify_kernel(EmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+template <int KW, int NCH, int PPL>
+__device__ __forceinline__ void em_body(const EmArgs &a, uint8_t *lds) {
   if (a.t.lds) copy_table_to_lds(lds, a.t);
-  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
-       i += nthr) {
-    uint64_t k[KW];
-    build_key<KW>(a.frames + i * a.stride, a.fp, k);
-    uint32_t g;
-    if (a.t.lds)
-      g = em_lookup<KW>(lds, a.t, k, a.default_gate);
-    else
-      g = em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
-    a.gates[i] = (uint16_t)g;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x * PPL;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * PPL + threadIdx.x;
+       base < a.n; base += step) {
+    uint64_t k[PPL][KW];
+    build_keys<KW, NCH, PPL>(a.frames, a.stride, a.n, base, a.fp, k);
+#pragma unroll
+    for (int j = 0; j < PPL; j++) {
+      const uint64_t idx = base + (uint64_t)j * blockDim.x;
+      uint32_t g;
+      if (a.t.lds)
+        g = em_lookup<KW>(lds, a.t, k[j], a.default_gate);
+      else
+        g = em_lookup<KW>(a.t.base, a.t, k[j], a.default_gate);
+      if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    }
   }
+}
+
+// <= 80 SGPRs: the hardware then admits the occupancy the runtime reports
+// (MI355X_MICROARCH.md, residency), so a residency-sized grid has no tail.
+template <int KW, int NCH, int PPL>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
+void em_classify_kernel(EmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  em_body<KW, NCH, PPL>(a, lds);
+}
+
+// unconstrained SGPRs (A/B experiments only: BG_FAT=1)
+template <int KW, int NCH, int PPL>
+__global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  em_body<KW, NCH, PPL>(a, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -232,21 +305,25 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
   return gate;
 }
 
-template <int KW>
-__global__ __launch_bounds__(kEmBlock) void wm_classify_kernel(WmArgs a) {
+template <int KW, int NCH, int PPL>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80))) void wm_classify_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (a.t.lds) copy_table_to_lds(lds, a.t);
-  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
-       i += nthr) {
-    uint64_t k[KW];
-    build_key<KW>(a.frames + i * a.stride, a.fp, k);
-    uint32_t g;
-    if (a.t.lds)
-      g = wm_lookup<KW>(lds, a, k);
-    else
-      g = wm_lookup<KW>(a.t.base, a, k);
-    a.gates[i] = (uint16_t)g;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x * PPL;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * PPL + threadIdx.x;
+       base < a.n; base += step) {
+    uint64_t k[PPL][KW];
+    build_keys<KW, NCH, PPL>(a.frames, a.stride, a.n, base, a.fp, k);
+#pragma unroll
+    for (int j = 0; j < PPL; j++) {
+      const uint64_t idx = base + (uint64_t)j * blockDim.x;
+      uint32_t g;
+      if (a.t.lds)
+        g = wm_lookup<KW>(lds, a, k[j]);
+      else
+        g = wm_lookup<KW>(a.t.base, a, k[j]);
+      if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    }
   }
 }
 
@@ -259,11 +336,18 @@ __global__ __launch_bounds__(kEmBlock) void wm_classify_kernel(WmArgs a) {
 // end-around folded once. The folded value is independent of reduction order
 // and is 0 only for an all-zero input, exactly like CalculateSum's adc
 // chains (checksum.h:52-181) -- so the wave-tree reduction is bit-exact.
+//
+// Frames of <= 2 KiB are software-pipelined across a wave's packets: while
+// packet p is summed, packet p+1's tail and packet p+2's head are in flight.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   s = (s & 0xFFFFu) + (s >> 16);
   s = (s & 0xFFFFu) + (s >> 16);
   return s;
+}
+
+__device__ __forceinline__ uint32_t halves(uint32_t v) {
+  return (v & 0xFFFFu) + (v >> 16);
 }
 
 // u16-halves sum of the bytes of dword `dw` (frame offset o) inside [lo,hi)
@@ -275,8 +359,17 @@ __device__ __forceinline__ uint32_t range_sum(uint32_t dw, int o, int lo,
   const uint64_t one = 1;
   uint32_t m = e > s ? (uint32_t)(((one << (8 * e)) - 1) ^ ((one << (8 * s)) - 1))
                      : 0u;
-  const uint32_t v = dw & m;
-  return (v & 0xFFFFu) + (v >> 16);
+  return halves(dw & m);
+}
+
+// the 16-byte chunk at frame offset o restricted to [lo, hi)
+__device__ __forceinline__ uint32_t chunk_sum(const uint4 &c, int o, int lo,
+                                              int hi) {
+  if (o >= lo && o + 16 <= hi)
+    return halves(c.x) + halves(c.y) + halves(c.z) + halves(c.w);
+  if (o + 16 <= lo || o >= hi) return 0;
+  return range_sum(c.x, o, lo, hi) + range_sum(c.y, o + 4, lo, hi) +
+         range_sum(c.z, o + 8, lo, hi) + range_sum(c.w, o + 12, lo, hi);
 }
 
 __device__ __forceinline__ uint32_t sel4(const uint4 &c, int comp) {
@@ -296,228 +389,345 @@ __device__ __forceinline__ uint32_t hdr_le16(const uint4 &c0, int o) {
   return hdr_u8(c0, o) | (hdr_u8(c0, o + 1) << 8);
 }
 
+// Wave-wide sum, DPP row reductions (result valid in lane 63).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false);   // quad [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x4e, 0xf, 0xf, false);   // quad [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
 }
 
-__global__ __launch_bounds__(kCkBlock) void cksum_kernel(CkArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
-      ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  const int stride = (int)a.stride;
-  for (uint64_t pkt = wave0; pkt < a.n; pkt += nwaves) {
-    uint8_t *f = a.frames + pkt * a.stride;
-    const uint4 *f16 = reinterpret_cast<const uint4 *>(f);
-    uint4 c0 = make_uint4(0, 0, 0, 0);
-    if (lane * 16 < stride) c0 = ld_stream(f16 + lane);
+// Per-frame header walk (wave-uniform results).
+struct CkHdr {
+  int ip_state;  // 0 forward untouched, 1 IPv4 processed
+  int ip_off, ip_lo, ip_hi;
+  int l4_kind;   // 0 forward, 1 udp, 2 tcp, 3 not emitted
+  int l4_off, l4_len, l4_ck, l4_lo, l4_hi;
+  int l4_valid;
+  int end;       // bytes of the frame the sums need
+};
 
-    // ---- IPChecksum header walk (ip_checksum.cc:50-74)
-    int ip_lo = 0, ip_hi = 0;  // summed IPv4 header range
-    int ip_state = 0;          // 0 forward untouched, 1 process IPv4
-    int ip_off = 14;
-    if (a.mode & 1) {
-      uint32_t et = hdr_be16(c0, 12);
-      bool fwd = false;
-      if (et == 0x88a8) {
-        et = hdr_be16(c0, ip_off + 2);
-        ip_off += 4;
-        if (et != 0x8100) fwd = true;
-      }
-      if (!fwd && et == 0x8100) {
-        et = hdr_be16(c0, ip_off + 2);
-        ip_off += 4;
-      }
-      if (!fwd && et == 0x0800) {
-        ip_state = 1;
-        const int hl = (int)(hdr_u8(c0, ip_off) & 15) * 4;
-        if (hl >= 20) {
-          ip_lo = ip_off;
-          ip_hi = ip_off + hl;
-        }
+__device__ __forceinline__ CkHdr ck_parse(const uint4 &c0, int mode,
+                                          int stride) {
+  CkHdr h;
+  h.ip_state = 0;
+  h.ip_off = 14;
+  h.ip_lo = h.ip_hi = 0;
+  // IPChecksum::ProcessBatch ethertype walk (ip_checksum.cc:50-74)
+  if (mode & 1) {
+    uint32_t et = hdr_be16(c0, 12);
+    bool fwd = false;
+    if (et == 0x88a8) {  // kQinQ: must be followed by 802.1Q
+      et = hdr_be16(c0, h.ip_off + 2);
+      h.ip_off += 4;
+      if (et != 0x8100) fwd = true;
+    }
+    if (!fwd && et == 0x8100) {  // kVlan
+      et = hdr_be16(c0, h.ip_off + 2);
+      h.ip_off += 4;
+    }
+    if (!fwd && et == 0x0800) {
+      h.ip_state = 1;
+      const int hl = (int)(hdr_u8(c0, h.ip_off) & 15) * 4;
+      if (hl >= 20) {
+        h.ip_lo = h.ip_off;
+        h.ip_hi = h.ip_off + hl;
       }
     }
-    // ---- L4Checksum header walk (l4_checksum.cc:53-82): untagged only
-    int l4_lo = 0, l4_hi = 0, l4_kind = 0;  // 0 forward, 1 udp, 2 tcp, 3 none
-    int l4_off = 0, l4_len = 0, l4_ck = 0;
-    bool l4_valid = false;
-    if (a.mode & 2) {
-      if (hdr_be16(c0, 12) == 0x0800) {
-        const int hl = (int)(hdr_u8(c0, 14) & 15) * 4;
-        const uint32_t proto = hdr_u8(c0, 23);
-        l4_off = 14 + hl;
-        if (proto == 17) {
-          l4_kind = 1;
-          l4_len = (int)hdr_be16(c0, l4_off + 4);
-          l4_valid = l4_len >= 8;
-          l4_ck = l4_off + 6;
-        } else if (proto == 6) {
-          l4_kind = 2;
-          const int ip_len = (int)hdr_be16(c0, 16);
-          l4_valid = ip_len >= hl + 20;
-          l4_len = (ip_len - hl) & 0xFFFF;
-          l4_ck = l4_off + 16;
-        } else {
-          l4_kind = 3;
-        }
-        if (l4_valid) {
-          l4_lo = l4_off;
-          l4_hi = l4_off + l4_len;
-          if (l4_hi > stride) l4_hi = stride;  // reference reads past (UB)
-        }
-      }
+  }
+  // L4Checksum::ProcessBatch (l4_checksum.cc:53-82): untagged IPv4 only
+  h.l4_kind = 0;
+  h.l4_off = h.l4_len = h.l4_ck = h.l4_lo = h.l4_hi = 0;
+  h.l4_valid = 0;
+  if ((mode & 2) && hdr_be16(c0, 12) == 0x0800) {
+    const int hl = (int)(hdr_u8(c0, 14) & 15) * 4;
+    const uint32_t proto = hdr_u8(c0, 23);
+    h.l4_off = 14 + hl;
+    if (proto == 17) {
+      h.l4_kind = 1;
+      h.l4_len = (int)hdr_be16(c0, h.l4_off + 4);
+      h.l4_valid = h.l4_len >= 8;
+      h.l4_ck = h.l4_off + 6;
+    } else if (proto == 6) {
+      h.l4_kind = 2;
+      const int ip_len = (int)hdr_be16(c0, 16);
+      h.l4_valid = ip_len >= hl + 20;
+      h.l4_len = (ip_len - hl) & 0xFFFF;
+      h.l4_ck = h.l4_off + 16;
+    } else {
+      h.l4_kind = 3;
     }
-    if (ip_hi > stride) ip_hi = stride;
+    if (h.l4_valid) {
+      h.l4_lo = h.l4_off;
+      h.l4_hi = h.l4_off + h.l4_len;
+      if (h.l4_hi > stride) h.l4_hi = stride;  // the reference reads past (UB)
+    }
+  }
+  if (h.ip_hi > stride) h.ip_hi = stride;
+  h.end = h.ip_hi > h.l4_hi ? h.ip_hi : h.l4_hi;
+  return h;
+}
 
-    // ---- one pass over the frame: both range sums
-    const int end = ip_hi > l4_hi ? ip_hi : l4_hi;
-    uint32_t s_ip = 0, s_l4 = 0;
-    for (int base = 0; base < end; base += 1024) {
-      uint4 c;
-      const int o = base + lane * 16;
-      if (base == 0) {
-        c = c0;
-      } else {
-        c = make_uint4(0, 0, 0, 0);
-        if (o < end) c = ld_stream(f16 + (o >> 4));
-      }
-      s_ip += range_sum(c.x, o, ip_lo, ip_hi) + range_sum(c.y, o + 4, ip_lo, ip_hi) +
-              range_sum(c.z, o + 8, ip_lo, ip_hi) + range_sum(c.w, o + 12, ip_lo, ip_hi);
-      s_l4 += range_sum(c.x, o, l4_lo, l4_hi) + range_sum(c.y, o + 4, l4_lo, l4_hi) +
-              range_sum(c.z, o + 8, l4_lo, l4_hi) + range_sum(c.w, o + 12, l4_lo, l4_hi);
-    }
-    s_ip = wave_sum(s_ip);
-    s_l4 = wave_sum(s_l4);
-
-    // ---- IPChecksum result (checksum.h:254-318)
-    uint32_t ip_gate = 0;
-    bool ip_wrote = false;
-    uint32_t ip_new = 0;  // value written at ip_off+10 (LE u16)
-    if (ip_state == 1) {
-      if (ip_hi == 0) {  // IHL < 5
-        if (a.verify) {
-          ip_gate = 1;
-        } else {
-          ip_wrote = true;
-          ip_new = 0;
-        }
-      } else if (a.verify) {
-        ip_gate = fold16(s_ip) == 0xFFFFu ? 0u : 1u;
-      } else {
-        const uint32_t old = hdr_le16(c0, ip_off + 10);
-        ip_wrote = true;
-        ip_new = (~fold16(s_ip - old)) & 0xFFFFu;
-      }
-      if (ip_wrote && lane == 0) {
-        f[ip_off + 10] = (uint8_t)ip_new;
-        f[ip_off + 11] = (uint8_t)(ip_new >> 8);
-      }
-    }
-    // ---- L4Checksum result (checksum.h:324-504)
-    uint32_t l4_gate = kGateNone;
-    const bool l4_runs = (a.mode & 2) && (!(a.mode & 1) || ip_gate == 0);
-    if (l4_runs) {
-      if (l4_kind == 0) {
-        l4_gate = 0;
-      } else if (l4_kind == 3) {
-        l4_gate = kGateNone;
-      } else {
-        // pseudo header: src, dst (LE u16 words of the BE addresses),
-        // bswap16(length), and the protocol word 0x1100 / 0x0600
-        const uint32_t ps = hdr_le16(c0, 26) + hdr_le16(c0, 28) +
-                            hdr_le16(c0, 30) + hdr_le16(c0, 32) +
-                            (((uint32_t)l4_len >> 8) | (((uint32_t)l4_len & 0xFF) << 8)) +
-                            (l4_kind == 1 ? 0x1100u : 0x0600u);
-        uint32_t old = l4_valid ? hdr_le16(c0, l4_ck) : 0u;
-        // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
-        // the "L4 header" overlaps the IP checksum bytes 24..25.
-        if ((a.mode & 1) && ip_wrote && ip_off == 14) {
-          const uint32_t old_ip = hdr_le16(c0, 24);
+// Sums of one frame given its chunks (c[k] = bytes [1024k + 16 lane, +16)).
+// `l4_extra`: this lane's L4 partial sum of bytes beyond the NC chunks.
+template <int NC>
+__device__ __forceinline__ void ck_finish(uint8_t *f, uint64_t pkt,
+                                          const uint4 (&c)[NC], const CkHdr &h,
+                                          const CkArgs &a, int lane,
+                                          uint32_t l4_extra) {
+  const uint4 &c0 = c[0];
+  uint32_t s_ip = 0, s_l4 = l4_extra;
+  if (lane * 16 < h.ip_hi) s_ip = chunk_sum(c0, lane * 16, h.ip_lo, h.ip_hi);
 #pragma unroll
-          for (int b = 24; b < 26; b++) {
-            if (b >= l4_lo && b < l4_hi) {
-              const int sh = (b & 1) * 8;
-              s_l4 = s_l4 - (((old_ip >> sh) & 0xFFu) << sh) +
-                     (((ip_new >> sh) & 0xFFu) << sh);
-            }
+  for (int k = 0; k < NC; k++)
+    s_l4 += chunk_sum(c[k], k * 1024 + lane * 16, h.l4_lo, h.l4_hi);
+  // the IPv4 header lies in lanes 0..5 (offset <= 22 + 60)
+  uint32_t t_ip = 0;
+#pragma unroll
+  for (int l = 0; l < 6; l++) t_ip += __builtin_amdgcn_readlane(s_ip, l);
+  s_ip = t_ip;
+  s_l4 = wave_sum(s_l4);
+
+  // ---- IPChecksum result (checksum.h:254-318)
+  uint32_t ip_gate = 0;
+  bool ip_wrote = false;
+  uint32_t ip_new = 0;  // value written at ip_off+10 (LE u16)
+  if (h.ip_state == 1) {
+    if (h.ip_hi == 0) {  // IHL < 5: calc writes 0, verify fails
+      if (a.verify) {
+        ip_gate = 1;
+      } else {
+        ip_wrote = true;
+        ip_new = 0;
+      }
+    } else if (a.verify) {
+      ip_gate = fold16(s_ip) == 0xFFFFu ? 0u : 1u;
+    } else {
+      const uint32_t old = hdr_le16(c0, h.ip_off + 10);
+      ip_wrote = true;
+      ip_new = (~fold16(s_ip - old)) & 0xFFFFu;
+    }
+    if (ip_wrote && lane == 0)
+      *reinterpret_cast<uint16_t *>(f + h.ip_off + 10) = (uint16_t)ip_new;
+  }
+  // ---- L4Checksum result (checksum.h:324-504)
+  uint32_t l4_gate = kGateNone;
+  const bool l4_runs = (a.mode & 2) && (!(a.mode & 1) || ip_gate == 0);
+  if (l4_runs) {
+    if (h.l4_kind == 0) {
+      l4_gate = 0;
+    } else if (h.l4_kind == 3) {
+      l4_gate = kGateNone;
+    } else {
+      // pseudo header: src, dst (LE u16 words of the BE addresses),
+      // bswap16(length), protocol word 0x1100 (UDP) / 0x0600 (TCP)
+      const uint32_t len = (uint32_t)h.l4_len;
+      const uint32_t ps = hdr_le16(c0, 26) + hdr_le16(c0, 28) +
+                          hdr_le16(c0, 30) + hdr_le16(c0, 32) +
+                          ((len >> 8) | ((len & 0xFF) << 8)) +
+                          (h.l4_kind == 1 ? 0x1100u : 0x0600u);
+      uint32_t old = h.l4_valid ? hdr_le16(c0, h.l4_ck) : 0u;
+      // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
+      // the "L4 header" overlaps the IP checksum bytes 24..25.
+      if ((a.mode & 1) && ip_wrote && h.ip_off == 14) {
+        const uint32_t old_ip = hdr_le16(c0, 24);
+#pragma unroll
+        for (int b = 24; b < 26; b++) {
+          if (b >= h.l4_lo && b < h.l4_hi) {
+            const int sh = (b & 1) * 8;
+            s_l4 = s_l4 - (((old_ip >> sh) & 0xFFu) << sh) +
+                   (((ip_new >> sh) & 0xFFu) << sh);
           }
-          if (l4_valid && l4_ck == 24) old = ip_new;
         }
-        if (a.verify) {
-          if (!l4_valid) {
-            l4_gate = 1;
-          } else if (l4_kind == 1 && old == 0) {
-            l4_gate = 0;  // UDP checksum 0 = not computed (checksum.h:328-331)
-          } else {
-            l4_gate = fold16(s_l4 + ps) == 0xFFFFu ? 0u : 1u;
-          }
+        if (h.l4_valid && h.l4_ck == 24) old = ip_new;
+      }
+      if (a.verify) {
+        if (!h.l4_valid) {
+          l4_gate = 1;
+        } else if (h.l4_kind == 1 && old == 0) {
+          l4_gate = 0;  // UDP checksum 0 = not computed (checksum.h:328-331)
         } else {
-          uint32_t ck = 0;
-          if (l4_valid) {
-            ck = (~fold16(s_l4 - old + ps)) & 0xFFFFu;
-            if (l4_kind == 1 && ck == 0) ck = 0xFFFFu;  // RFC 768
-          }
-          // a UDP length < 8 / bad TCP length writes 0 at the field
-          const int at = l4_kind == 1 ? l4_off + 6 : l4_off + 16;
-          if (lane == 0 && at + 2 <= stride) {
-            f[at] = (uint8_t)ck;
-            f[at + 1] = (uint8_t)(ck >> 8);
-          }
-          l4_gate = l4_kind == 1 ? 0u : kGateNone;  // TCP: never emitted
+          l4_gate = fold16(s_l4 + ps) == 0xFFFFu ? 0u : 1u;
         }
+      } else {
+        uint32_t ck = 0;  // invalid UDP/TCP lengths write 0
+        if (h.l4_valid) {
+          ck = (~fold16(s_l4 - old + ps)) & 0xFFFFu;
+          if (h.l4_kind == 1 && ck == 0) ck = 0xFFFFu;  // RFC 768
+        }
+        const int at = h.l4_kind == 1 ? h.l4_off + 6 : h.l4_off + 16;
+        if (lane == 0 && at + 2 <= (int)a.stride)
+          *reinterpret_cast<uint16_t *>(f + at) = (uint16_t)ck;
+        l4_gate = h.l4_kind == 1 ? 0u : kGateNone;  // TCP: never emitted
       }
     }
-    if (lane == 0) {
-      if (a.ip_gates) a.ip_gates[pkt] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
-      if (a.l4_gates) a.l4_gates[pkt] = (uint16_t)l4_gate;
-    }
+  }
+  if (lane == 0) {
+    if (a.ip_gates) a.ip_gates[pkt] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
+    if (a.l4_gates) a.l4_gates[pkt] = (uint16_t)l4_gate;
   }
 }
 
+__device__ __forceinline__ uint4 ld_chunk(const uint8_t *f, int k, int lane,
+                                          int limit) {
+  const int o = k * 1024 + lane * 16;
+  if (o < limit) return ld_stream(reinterpret_cast<const uint4 *>(f + o));
+  return make_uint4(0, 0, 0, 0);
+}
+
+// stride <= 2048: two 1 KiB chunks per frame, pipelined over packets.
+__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80))) void cksum_kernel(CkArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
+      ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int stride = (int)a.stride;
+  if (wave0 >= a.n) return;
+  uint64_t p = wave0;
+  uint4 A[2], B0;
+  A[0] = ld_chunk(a.frames + p * a.stride, 0, lane, stride);
+  CkHdr hA = ck_parse(A[0], a.mode, stride);
+  A[1] = hA.end > 1024 ? ld_chunk(a.frames + p * a.stride, 1, lane, hA.end)
+                       : make_uint4(0, 0, 0, 0);
+  B0 = (p + nw < a.n) ? ld_chunk(a.frames + (p + nw) * a.stride, 0, lane, stride)
+                      : make_uint4(0, 0, 0, 0);
+  for (; p < a.n; p += nw) {
+    const uint64_t pn = p + nw, pnn = pn + nw;
+    CkHdr hB;
+    uint4 B1 = make_uint4(0, 0, 0, 0);
+    if (pn < a.n) {
+      hB = ck_parse(B0, a.mode, stride);
+      if (hB.end > 1024) B1 = ld_chunk(a.frames + pn * a.stride, 1, lane, hB.end);
+    }
+    uint4 C0 = make_uint4(0, 0, 0, 0);
+    if (pnn < a.n) C0 = ld_chunk(a.frames + pnn * a.stride, 0, lane, stride);
+    ck_finish<2>(a.frames + p * a.stride, p, A, hA, a, lane, 0u);
+    A[0] = B0;
+    A[1] = B1;
+    hA = hB;
+    B0 = C0;
+  }
+}
+
+// any stride: frame chunks loaded after the header walk, one frame at a time
+__global__ __launch_bounds__(kCkBlock) void cksum_kernel_generic(CkArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
+      ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const int stride = (int)a.stride;
+  for (uint64_t p = wave0; p < a.n; p += nw) {
+    uint8_t *f = a.frames + p * a.stride;
+    uint4 c[1];
+    c[0] = ld_chunk(f, 0, lane, stride);
+    const CkHdr h = ck_parse(c[0], a.mode, stride);
+    uint32_t extra = 0;  // L4 bytes beyond the first KiB
+    for (int k = 1; k * 1024 < h.end; k++)
+      extra += chunk_sum(ld_chunk(f, k, lane, h.end), k * 1024 + lane * 16,
+                         h.l4_lo, h.l4_hi);
+    ck_finish<1>(f, p, c, h, a, lane, extra);
+  }
+}
+
+// Launch-time knobs (defaults measured on MI355X; env overrides are for
+// A/B experiments in scripts/em_variants.py).
+int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
 template <typename Args, typename K>
-hipError_t launch_classify(K kernel, const Args &a, int num_cus,
-                           hipStream_t s) {
+hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
+                           int ppl) {
   if (a.n == 0) return hipSuccess;
-  uint64_t blocks = (a.n + kEmBlock - 1) / kEmBlock;
-  uint64_t cap = (uint64_t)num_cus * (a.t.lds ? 4 : 8);
-  if (blocks > cap) blocks = cap;
+  if (env_int("BG_NOLDS", 0)) a.t.lds = 0;
   const size_t lds = a.t.lds ? a.t.bytes_total : 0;
+  // Measured on MI355X (scripts/variants.py): with the table in LDS two
+  // 512-thread blocks per CU (16 waves) stream fastest -- fewer LDS table
+  // fills; with the table in L2/MALL, twice the resident grid.
+  int per_cu = env_int("BG_BLOCKS_PER_CU", 0);
+  if (per_cu <= 0) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, reinterpret_cast<const void *>(kernel), kEmBlock, lds) !=
+            hipSuccess ||
+        occ <= 0)
+      occ = 2;
+    per_cu = a.t.lds ? std::min(occ, 2) : occ * 2;
+    per_cu *= std::max(1, env_int("BG_GRID_MULT", 1));
+  }
+  uint64_t blocks = (a.n + (uint64_t)kEmBlock * ppl - 1) / ((uint64_t)kEmBlock * ppl);
+  const uint64_t cap = (uint64_t)num_cus * per_cu;
+  if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kEmBlock), lds, s, a);
   return hipGetLastError();
 }
 
+template <template <int, int, int> class Sel, typename Args>
+hipError_t dispatch(const Args &a, int num_cus, hipStream_t s) {
+  const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 ? 2 : 4);
+  const int ppl = env_int("BG_PPL", kDefaultPpl);
+#define BG_CASE(KW, NCH, PPL)                                                   \
+  if (a.t.kw == KW && nch == NCH && ppl == PPL)                                 \
+    return launch_classify(Sel<KW, NCH, PPL>::kernel(), a, num_cus, s, PPL);
+#define BG_PPLS(KW, NCH) BG_CASE(KW, NCH, 1) BG_CASE(KW, NCH, 2)
+#define BG_NCHS(KW) BG_PPLS(KW, 0) BG_PPLS(KW, 2) BG_PPLS(KW, 4)
+  BG_NCHS(1) BG_NCHS(2) BG_NCHS(4) BG_NCHS(8)
+#undef BG_NCHS
+#undef BG_PPLS
+#undef BG_CASE
+  return hipErrorInvalidValue;
+}
+
+template <int KW, int NCH, int PPL>
+struct EmSel {
+  static auto kernel() { return em_classify_kernel<KW, NCH, PPL>; }
+};
+template <int KW, int NCH, int PPL>
+struct WmSel {
+  static auto kernel() { return wm_classify_kernel<KW, NCH, PPL>; }
+};
+
 }  // namespace
 
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
-  switch (a.t.kw) {
-    case 1: return launch_classify(em_classify_kernel<1>, a, num_cus, s);
-    case 2: return launch_classify(em_classify_kernel<2>, a, num_cus, s);
-    case 4: return launch_classify(em_classify_kernel<4>, a, num_cus, s);
-    case 8: return launch_classify(em_classify_kernel<8>, a, num_cus, s);
-    default: return hipErrorInvalidValue;
+  if (env_int("BG_FAT", 0) && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2) {
+    if (env_int("BG_PPL", kDefaultPpl) == 2)
+      return launch_classify(em_classify_fat_kernel<2, 2, 2>, a, num_cus, s, 2);
+    return launch_classify(em_classify_fat_kernel<2, 2, 1>, a, num_cus, s, 1);
   }
+  return dispatch<EmSel>(a, num_cus, s);
 }
 
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
-  switch (a.t.kw) {
-    case 1: return launch_classify(wm_classify_kernel<1>, a, num_cus, s);
-    case 2: return launch_classify(wm_classify_kernel<2>, a, num_cus, s);
-    case 4: return launch_classify(wm_classify_kernel<4>, a, num_cus, s);
-    case 8: return launch_classify(wm_classify_kernel<8>, a, num_cus, s);
-    default: return hipErrorInvalidValue;
-  }
+  return dispatch<WmSel>(a, num_cus, s);
 }
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const uint64_t waves_per_block = kCkBlock / 64;
   uint64_t blocks = (a.n + waves_per_block - 1) / waves_per_block;
-  const uint64_t cap = (uint64_t)num_cus * 8;  // 32 waves/CU
+  int per_cu = env_int("BG_CK_BLOCKS_PER_CU", 0);
+  if (per_cu <= 0) {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, reinterpret_cast<const void *>(cksum_kernel), kCkBlock, 0) !=
+            hipSuccess ||
+        occ <= 0)
+      occ = 7;
+    per_cu = occ * std::max(1, env_int("BG_CK_GRID_MULT", 2));
+  }
+  const uint64_t cap = (uint64_t)num_cus * per_cu;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(cksum_kernel, dim3((unsigned)blocks), dim3(kCkBlock), 0, s,
-                     a);
+  if (a.stride <= 2048 && !env_int("BG_CK_GENERIC", 0))
+    hipLaunchKernelGGL(cksum_kernel, dim3((unsigned)blocks), dim3(kCkBlock), 0,
+                       s, a);
+  else
+    hipLaunchKernelGGL(cksum_kernel_generic, dim3((unsigned)blocks),
+                       dim3(kCkBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,191 @@
+// module.h -- the slice of BESS's module API that the classification
+// modules use, so they keep the reference's surface:
+//
+//   Module::ProcessBatch(Context *, bess::PacketBatch *)  core/module.h:226
+//   EmitPacket / DropPacket                               core/module.h:534-594
+//   CommandResponse, CommandSuccess / CommandFailure      core/message.h:44-53
+//   Commands {cmd, arg_type, func, THREAD_SAFE|UNSAFE}    core/commands.h:57-72
+//   ADD_MODULE registration (first registration wins)     core/module.h:719-733
+//   gate_idx_t / MAX_GATES / DROP_GATE                    core/gate.h:49-58
+//
+// In a bessd build the same module sources would include the real headers;
+// this file is the stand-alone host shell used here (no DPDK / protobuf /
+// gRPC in the image). Packets are plain head pointers into frame buffers.
+#ifndef BESS_AMD_HOST_MODULE_H_
+#define BESS_AMD_HOST_MODULE_H_
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdint.h>
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pb.h"
+
+typedef uint16_t gate_idx_t;
+#define MAX_GATES 8192
+#define DROP_GATE MAX_GATES
+#define INVALID_GATE UINT16_MAX
+
+namespace bess {
+
+// A packet as the classifiers see it: Packet::head_data() (core/packet.h:
+// 84-94) plus the bytes that may be read/written from there.
+class Packet {
+ public:
+  Packet() = default;
+  Packet(uint8_t *head, uint32_t span, uint32_t index)
+      : head_(head), span_(span), index_(index) {}
+  template <typename T = void *>
+  T head_data() const {
+    return reinterpret_cast<T>(head_);
+  }
+  uint32_t span() const { return span_; }
+  uint32_t index() const { return index_; }
+
+ private:
+  uint8_t *head_ = nullptr;
+  uint32_t span_ = 0;
+  uint32_t index_ = 0;
+};
+
+// core/pktbatch.h:40-75
+class PacketBatch {
+ public:
+  static const size_t kMaxBurst = 32;
+  int cnt() const { return cnt_; }
+  Packet *const *pkts() const { return pkts_; }
+  Packet **pkts() { return pkts_; }
+  void clear() { cnt_ = 0; }
+  void add(Packet *p) { pkts_[cnt_++] = p; }
+
+ private:
+  int cnt_ = 0;
+  Packet *pkts_[kMaxBurst];
+};
+
+}  // namespace bess
+
+// Per-call context (core/module.h:59-75): here it records where each packet
+// was emitted.
+struct Context {
+  uint16_t *ogates = nullptr;  // indexed by Packet::index()
+};
+
+class CommandResponse {
+ public:
+  int code() const { return code_; }
+  const std::string &errmsg() const { return msg_; }
+  const std::string &data() const { return data_; }
+  void set_error(int code, const std::string &msg) {
+    code_ = code;
+    msg_ = msg;
+  }
+  void set_data(const std::string &d) { data_ = d; }
+
+ private:
+  int code_ = 0;
+  std::string msg_;
+  std::string data_;  // serialized response message
+};
+
+CommandResponse CommandSuccess();
+CommandResponse CommandSuccess(const bess::pb::Message &m);
+CommandResponse CommandFailure(int code, const char *fmt = nullptr, ...)
+    __attribute__((format(printf, 2, 3)));
+
+class Module;
+
+struct Command {
+  enum ThreadSafety { THREAD_UNSAFE = 0, THREAD_SAFE = 1 };
+  std::string cmd;
+  std::string arg_type;
+  std::function<CommandResponse(Module *, const void *, size_t)> func;
+  ThreadSafety mt_safe;
+};
+using Commands = std::vector<Command>;
+
+// MODULE_CMD_FUNC: adapt `CommandResponse C::f(const Arg &)` to the
+// serialized-argument form the control plane delivers.
+template <typename C, typename Arg>
+std::function<CommandResponse(Module *, const void *, size_t)> ModuleCmdFunc(
+    CommandResponse (C::*f)(const Arg &)) {
+  return [f](Module *m, const void *arg, size_t len) {
+    Arg a;
+    if (!a.ParseFromArray(arg, len))
+      return CommandFailure(EINVAL, "failed to parse argument");
+    return (static_cast<C *>(m)->*f)(a);
+  };
+}
+#define MODULE_CMD_FUNC(f) ModuleCmdFunc(f)
+
+class Module {
+ public:
+  virtual ~Module() = default;
+  virtual void ProcessBatch(Context *ctx, bess::PacketBatch *batch) = 0;
+  virtual std::string GetDesc() const { return ""; }
+  virtual const Commands &cmds() const = 0;
+  // Device-resident datapath over a frame slab (libbessgpu.so).
+  virtual int ProcessDevice(void *d_frames, size_t stride, size_t n,
+                            uint16_t *d_ogates, void *stream) = 0;
+  void set_device(int d) { device_ = d; }
+  int device() const { return device_; }
+
+  // core/module.h:543-594: the chosen gate is recorded for the packet.
+  void EmitPacket(Context *ctx, bess::Packet *pkt, gate_idx_t ogate) {
+    ctx->ogates[pkt->index()] = ogate;
+  }
+  void DropPacket(Context *ctx, bess::Packet *pkt) {
+    ctx->ogates[pkt->index()] = DROP_GATE;
+  }
+
+ protected:
+  int device_ = 0;
+};
+
+// ModuleBuilder (core/module.h:108-172): class name -> factory taking the
+// serialized <Class>Arg and running Init.
+class ModuleBuilder {
+ public:
+  using Factory = std::function<CommandResponse(const void *, size_t,
+                                                std::unique_ptr<Module> *)>;
+  static bool RegisterModuleClass(const std::string &class_name,
+                                  const std::string &name_template,
+                                  const std::string &help, Factory f);
+  static const ModuleBuilder *Find(const std::string &class_name);
+  static std::vector<std::string> Classes();
+  const std::string &name_template() const { return name_template_; }
+  const std::string &help() const { return help_; }
+  CommandResponse Create(const void *arg, size_t len,
+                         std::unique_ptr<Module> *out) const {
+    return factory_(arg, len, out);
+  }
+
+ private:
+  std::string name_template_, help_;
+  Factory factory_;
+};
+
+template <typename C, typename Arg>
+ModuleBuilder::Factory MakeFactory() {
+  return [](const void *arg, size_t len, std::unique_ptr<Module> *out) {
+    Arg a;
+    if (!a.ParseFromArray(arg, len))
+      return CommandFailure(EINVAL, "failed to parse %s argument", "module");
+    std::unique_ptr<C> m(new C());
+    CommandResponse r = m->Init(a);
+    if (r.code() == 0) *out = std::move(m);
+    return r;
+  };
+}
+
+// ADD_MODULE(class, name_template, help) with the Init argument type.
+#define ADD_MODULE_ARG(_MOD, _ARG, _NAME_TEMPLATE, _HELP)                     \
+  static bool __module__##_MOD = ModuleBuilder::RegisterModuleClass(          \
+      #_MOD, _NAME_TEMPLATE, _HELP, MakeFactory<_MOD, _ARG>());
+
+#endif  // BESS_AMD_HOST_MODULE_H_

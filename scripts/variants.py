@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""A/B launch variants of the classify / checksum kernels in ONE process,
+interleaved over several rounds (cdna_hip_programming.md §5.4 rule 24).
+
+Variants are selected through the BG_* environment knobs read by the
+launchers in bess_amd/csrc/bg_kernels.hip. Prints one JSON line per kernel
+family with median / min milliseconds per launch for each variant.
+"""
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bess_amd import flowtable as F  # noqa: E402
+from bess_amd import packets as P  # noqa: E402
+
+KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
+         "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT"]
+
+
+def set_env(v):
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    for k, x in v.items():
+        os.environ[k] = str(x)
+
+
+def time_variants(fn, variants, rounds=5, reps=10):
+    res = {name: [] for name in variants}
+    for _ in range(rounds):
+        for name, env in variants.items():
+            set_env(env)
+            fn()  # warm (and re-select the variant)
+            torch.cuda.synchronize()
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(reps):
+                fn()
+            b.record()
+            b.synchronize()
+            res[name].append(a.elapsed_time(b) / reps)
+    set_env({})
+    return {k: {"median_ms": round(statistics.median(v), 4),
+                "min_ms": round(min(v), 4)} for k, v in res.items()}
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "em,ck,wm"
+    dev = torch.device("cuda:0")
+    out = {}
+    if "em" in which:
+        n = 16 << 20
+        keys, gates, frames = P.em_workload(1000, n)
+        d = torch.from_numpy(frames.reshape(-1)).to(dev)
+        del frames
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        t = F.EmTable(P.em_fields_5tuple())
+        t.add_many(keys, gates)
+        t.sync(0)
+        ref = None
+        variants = {
+            "slim_ppl1": {}, "slim_ppl2": {"BG_PPL": 2},
+            "slim_ppl1_x2": {"BG_GRID_MULT": 2},
+            "slim_ppl1_bpc2": {"BG_BLOCKS_PER_CU": 2},
+            "slim_ppl1_bpc8": {"BG_BLOCKS_PER_CU": 8},
+            "slim_ppl1_l2tab": {"BG_NOLDS": 1},
+            "slim_ppl1_l2tab_bpc16": {"BG_NOLDS": 1, "BG_BLOCKS_PER_CU": 16},
+            "fat_ppl1_bpc3": {"BG_FAT": 1, "BG_BLOCKS_PER_CU": 3},
+            "fat_ppl2_bpc3": {"BG_FAT": 1, "BG_PPL": 2, "BG_BLOCKS_PER_CU": 3},
+            "fat_ppl1_api": {"BG_FAT": 1},
+        }
+        # every variant must give identical gates
+        for name, env in variants.items():
+            set_env(env)
+            t.classify(d, 64, n, 8192, g)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = g.clone()
+            assert torch.equal(g, ref), name
+        r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants)
+        for k in r:
+            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+            r[k]["GBps_66B"] = round(66 * n / (r[k]["median_ms"] * 1e-3) / 1e9, 1)
+        out["em"] = r
+        del d, g
+    if "ck" in which:
+        n = 1 << 20
+        frames = P.cksum_workload(n, frame_len=1496)
+        d = torch.from_numpy(frames.reshape(-1)).to(dev)
+        l4 = torch.empty(n, dtype=torch.int16, device=dev)
+        variants = {"pipelined": {}, "generic": {"BG_CK_GENERIC": 1},
+                    "pipelined_x2": {"BG_CK_GRID_MULT": 2},
+                    "pipelined_bpc7": {"BG_CK_BLOCKS_PER_CU": 7},
+                    "pipelined_bpc4": {"BG_CK_BLOCKS_PER_CU": 4}}
+        # (idempotent after the first pass: recompute writes the same bytes)
+        r = time_variants(lambda: F.cksum(d, 2048, n, 3, False, None, l4),
+                          variants)
+        for k in r:
+            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+            r[k]["GBps_1502B"] = round(1502 * n / (r[k]["median_ms"] * 1e-3) / 1e9, 1)
+        out["ck"] = r
+        del d
+    if "wm" in which:
+        n = 1 << 22
+        rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n, stride=64,
+                                                      sizes=((60, 1),))
+        t = F.WmTable(P.FIVE_TUPLE)
+        for k, m, p, gg in zip(rk, rm, prio, gates):
+            t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
+        d = torch.from_numpy(frames.reshape(-1)).to(dev)
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        t.sync(0)
+        variants = {"ppl1": {}, "ppl2": {"BG_PPL": 2},
+                    "ppl1_bpc8": {"BG_BLOCKS_PER_CU": 8}}
+        r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants)
+        for k in r:
+            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+        out["wm"] = r
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
