@@ -251,6 +251,7 @@ using namespace bg;
 // ============================================================================
 struct bg_em {
   std::vector<bg_field> fields;
+  bool has_attr = false;  // metadata-attribute fields: control plane only
   uint32_t key_size = 0;  // total_key_size_
   uint32_t kw = 1;        // device key words (1, 2, 4, 8)
   std::unordered_map<Key, uint16_t, KeyHash> rules;
@@ -277,10 +278,7 @@ static int check_fields(const bg_field *fields, int nfields) {
     const bg_field &f = fields[i];
     if (f.size < 1 || f.size > 8)
       return fail(EINVAL, "idx %d: 'size' must be in [1,8]", i);
-    if (f.attr_id >= 0)
-      return fail(ENOTSUP, "idx %d: metadata-attribute fields are not on the "
-                  "device path", i);
-    if (f.offset < 0 || f.offset > 1024)
+    if (f.attr_id < 0 && (f.offset < 0 || f.offset > 1024))
       return fail(EINVAL, "idx %d: invalid 'offset'", i);
     if (f.pos != acc)
       return fail(EINVAL, "idx %d: pos %d != %d", i, f.pos, acc);
@@ -330,6 +328,7 @@ int bg_em_create(const bg_field *fields, int nfields, bg_em **out) {
   if (r) return r;
   bg_em *em = new bg_em();
   em->fields.assign(fields, fields + nfields);
+  for (int i = 0; i < nfields; i++) em->has_attr |= fields[i].attr_id >= 0;
   int acc = 0;
   for (int i = 0; i < nfields; i++) acc += fields[i].size;
   em->key_size = (uint32_t)((acc + 7) / 8 * 8);
@@ -434,9 +433,15 @@ static int em_launch(bg_em *em, const void *d_frames, size_t stride, size_t n,
   return 0;
 }
 
+static int no_attr_datapath() {
+  return fail(ENOTSUP, "metadata-attribute (attr_name) fields are not on the "
+              "device datapath");
+}
+
 int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
                    uint16_t default_gate, uint16_t *d_gates,
                    bg_stream_t stream) {
+  if (em->has_attr) return no_attr_datapath();
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   hipStream_t s = (hipStream_t)stream;
@@ -478,6 +483,7 @@ static int stage_windows(const std::vector<bg_field> &fields,
 int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
                        uint16_t default_gate, uint16_t *gates,
                        bg_stream_t stream) {
+  if (em->has_attr) return no_attr_datapath();
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> lk(em->mu);
@@ -573,6 +579,7 @@ struct WmTupleH {
 
 struct bg_wm {
   std::vector<bg_field> fields;
+  bool has_attr = false;
   uint32_t key_size = 0;
   uint32_t kw = 1;
   std::vector<WmTupleH> tuples;
@@ -610,6 +617,7 @@ int bg_wm_create(const bg_field *fields, int nfields, bg_wm **out) {
   if (r) return r;
   bg_wm *wm = new bg_wm();
   wm->fields.assign(fields, fields + nfields);
+  for (int i = 0; i < nfields; i++) wm->has_attr |= fields[i].attr_id >= 0;
   wm->key_size = (uint32_t)((acc + 7) / 8 * 8);
   wm->kw = round_kw(wm->key_size);
   *out = wm;
@@ -737,6 +745,7 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
 int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
                    uint16_t default_gate, uint16_t *d_gates,
                    bg_stream_t stream) {
+  if (wm->has_attr) return no_attr_datapath();
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   hipStream_t s = (hipStream_t)stream;
@@ -755,6 +764,7 @@ int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
 int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
                        uint16_t default_gate, uint16_t *gates,
                        bg_stream_t stream) {
+  if (wm->has_attr) return no_attr_datapath();
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> lk(wm->mu);

@@ -269,36 +269,51 @@ template <int KW>
 __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
                                               const WmArgs &a,
                                               const uint64_t (&k)[KW]) {
+  // Issue every tuple's two tag-word reads before resolving any of them:
+  // up to 16 independent table reads in flight per lane. (The WildcardMatch
+  // table has a single partition.)
+  uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples], w1[kMaxTuples],
+      w2[kMaxTuples];
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
+#pragma unroll
+  for (int tu = 0; tu < kMaxTuples; tu++) {
+    if (tu < (int)a.ntuples) {
+      uint64_t km[KW];
+#pragma unroll
+      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      const Probe p = split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)),
+                                 1, a.t.nbp);
+      b1[tu] = p.b1;
+      b2[tu] = p.b2;
+      tg[tu] = p.tag;
+      w1[tu] = tags[p.b1];
+      w2[tu] = tags[p.b2];
+    }
+  }
   int32_t best = INT_MIN;
   uint32_t gate = a.default_gate;
-  for (uint32_t tu = 0; tu < a.ntuples; tu++) {
-    uint64_t km[KW];
 #pragma unroll
-    for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
-    const uint8_t *pb;
-    const uint64_t seed = tuple_seed(a.t.seed, tu);
-    // the slot must also belong to this tuple: keys of different tuples
-    // share the table, tagged in the value word
-    const uint64_t h = hash_words(km, KW, seed);
-    const Probe p = split_hash(h, a.t.nparts, a.t.nbp);
-    pb = tab + (uint64_t)p.part * a.t.part_bytes;
-    const uint32_t *tags = reinterpret_cast<const uint32_t *>(pb);
-    uint32_t cand = tag_match(tags[p.b1], p.tag) |
-                    (tag_match(tags[p.b2], p.tag) << 4);
-    while (cand) {
-      const int s = __builtin_ctz(cand);
-      cand &= cand - 1;
-      const uint32_t slot = (s < 4 ? p.b1 : p.b2) * kSlots + (s & 3);
-      const uint64_t v =
-          reinterpret_cast<const uint64_t *>(pb + a.t.vals_off)[slot];
-      if ((uint32_t)(v >> 48) != tu) continue;
-      if (key_eq<KW>(pb + a.t.keys_off + (uint64_t)slot * KW * 8, km)) {
-        const int32_t prio = (int32_t)(uint32_t)v;
-        if (prio >= best) {
-          best = prio;
-          gate = (uint32_t)(v >> 32) & 0xFFFFu;
+  for (int tu = 0; tu < kMaxTuples; tu++) {
+    if (tu < (int)a.ntuples) {
+      uint32_t cand = tag_match(w1[tu], tg[tu]) | (tag_match(w2[tu], tg[tu]) << 4);
+      while (cand) {
+        const int sl = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const uint32_t slot = (sl < 4 ? b1[tu] : b2[tu]) * kSlots + (sl & 3);
+        const uint64_t v =
+            reinterpret_cast<const uint64_t *>(tab + a.t.vals_off)[slot];
+        if ((uint32_t)(v >> 48) != (uint32_t)tu) continue;
+        uint64_t km[KW];
+#pragma unroll
+        for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+        if (key_eq<KW>(tab + a.t.keys_off + (uint64_t)slot * KW * 8, km)) {
+          const int32_t prio = (int32_t)(uint32_t)v;
+          if (prio >= best) {  // '>=': the later tuple wins a tie (P5)
+            best = prio;
+            gate = (uint32_t)(v >> 32) & 0xFFFFu;
+          }
+          break;
         }
-        break;
       }
     }
   }
@@ -578,37 +593,258 @@ __device__ __forceinline__ uint4 ld_chunk(const uint8_t *f, int k, int lane,
   return make_uint4(0, 0, 0, 0);
 }
 
-// stride <= 2048: two 1 KiB chunks per frame, pipelined over packets.
-__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80))) void cksum_kernel(CkArgs a) {
+// ---------------------------------------------------------------------------
+// Tiled checksum kernel (stride <= 2048): a wave owns tiles of 64 frames.
+//   1. lane = frame: header walk of 64 frames at once (vector ALU, per-lane
+//      loads); results stay in VGPRs.
+//   2. frame by frame, all 64 lanes: coalesced 16 B/lane loads of the frame
+//      (next frame prefetched), masked range sums, DPP wave reductions; the
+//      two sums go back to the frame's lane (v_writelane).
+//   3. lane = frame: fold, write checksum words in place, write gates.
+// The scalar unit only handles the per-frame loop (no per-frame header walk),
+// which bounded the one-wave-per-frame form.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[12], int o) {
+  return (h[o >> 2] >> ((o & 3) * 8)) & 0xFFu;  // o compile-time constant
+}
+__device__ __forceinline__ uint32_t be16_of(const uint32_t (&h)[12], int o) {
+  return (byte_of(h, o) << 8) | byte_of(h, o + 1);
+}
+__device__ __forceinline__ uint32_t le16_of(const uint32_t (&h)[12], int o) {
+  return byte_of(h, o) | (byte_of(h, o + 1) << 8);
+}
+__device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) {
+  return *reinterpret_cast<const uint16_t *>(p);
+}
+
+struct CkLane {      // phase-1 results of this lane's frame
+  uint32_t ip_rng;   // ip_lo | ip_hi << 16 (0: no IPv4 header to sum)
+  uint32_t l4_rng;   // l4_lo | l4_hi << 16
+  uint32_t flags;    // bit0 ip_state, bit1 ihl<5, 2-3 l4_kind, 4 l4_valid
+  uint32_t ip_off;   // 14 / 18 / 22
+  uint32_t old_ip;   // IPv4 checksum field before the write
+  uint32_t l4_ck;    // frame offset of the L4 checksum word
+  uint32_t old_l4;
+  uint32_t ps;       // pseudo-header sum
+  uint32_t ip24;     // bytes 24..25 (pipeline overlap fix-up)
+};
+
+__device__ __forceinline__ CkLane ck_walk(const uint8_t *f, int mode,
+                                          int stride) {
+  CkLane r;
+  uint32_t h[12];
+  const uint4 *q = reinterpret_cast<const uint4 *>(f);
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const uint4 v = q[c];
+    h[4 * c] = v.x;
+    h[4 * c + 1] = v.y;
+    h[4 * c + 2] = v.z;
+    h[4 * c + 3] = v.w;
+  }
+  r.flags = 0;
+  r.ip_rng = 0;
+  r.l4_rng = 0;
+  r.ip_off = 14;
+  r.old_ip = 0;
+  r.l4_ck = 0;
+  r.old_l4 = 0;
+  r.ps = 0;
+  r.ip24 = le16_of(h, 24);
+  const uint32_t et12 = be16_of(h, 12);
+  // IPChecksum ethertype walk (ip_checksum.cc:50-74)
+  if (mode & 1) {
+    const uint32_t et16 = be16_of(h, 16), et20 = be16_of(h, 20);
+    bool fwd = false;
+    uint32_t et = et12, off = 14;
+    if (et == 0x88a8) {
+      et = et16;
+      off = 18;
+      if (et != 0x8100) fwd = true;
+    }
+    if (!fwd && et == 0x8100) {
+      et = off == 14 ? et16 : et20;
+      off += 4;
+    }
+    if (!fwd && et == 0x0800) {
+      r.flags |= 1;
+      r.ip_off = off;
+      const uint32_t vihl = off == 14 ? byte_of(h, 14)
+                           : off == 18 ? byte_of(h, 18) : byte_of(h, 22);
+      r.old_ip = off == 14 ? le16_of(h, 24)
+                 : off == 18 ? le16_of(h, 28) : le16_of(h, 32);
+      const uint32_t hl = (vihl & 15) * 4;
+      if (hl >= 20) {
+        uint32_t hi = off + hl;
+        if (hi > (uint32_t)stride) hi = stride;
+        r.ip_rng = off | (hi << 16);
+      } else {
+        r.flags |= 2;
+      }
+    }
+  }
+  // L4Checksum (l4_checksum.cc:53-82): untagged IPv4 only
+  if ((mode & 2) && et12 == 0x0800) {
+    const uint32_t hl = (byte_of(h, 14) & 15) * 4;
+    const uint32_t proto = byte_of(h, 23);
+    const uint32_t l4_off = 14 + hl;
+    uint32_t kind = 3, len = 0, valid = 0;
+    if (proto == 17) {
+      kind = 1;
+      const uint32_t v = ld_u16(f + l4_off + 4);
+      len = ((v & 0xFF) << 8) | (v >> 8);
+      valid = len >= 8;
+      r.l4_ck = l4_off + 6;
+    } else if (proto == 6) {
+      kind = 2;
+      const uint32_t ip_len = be16_of(h, 16);
+      valid = ip_len >= hl + 20;
+      len = (ip_len - hl) & 0xFFFF;
+      r.l4_ck = l4_off + 16;
+    }
+    r.flags |= kind << 2;
+    if (kind != 3) {
+      if (valid) {
+        r.flags |= 16;
+        uint32_t hi = l4_off + len;
+        if (hi > (uint32_t)stride) hi = stride;  // reference reads past (UB)
+        r.l4_rng = l4_off | (hi << 16);
+        r.old_l4 = ld_u16(f + r.l4_ck);
+      }
+      r.ps = le16_of(h, 26) + le16_of(h, 28) + le16_of(h, 30) + le16_of(h, 32) +
+             ((len >> 8) | ((len & 0xFF) << 8)) + (kind == 1 ? 0x1100u : 0x0600u);
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint32_t rng_lo(uint32_t r) { return r & 0xFFFFu; }
+__device__ __forceinline__ uint32_t rng_hi(uint32_t r) { return r >> 16; }
+
+__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
+void cksum_kernel(CkArgs a) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
       ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int stride = (int)a.stride;
-  if (wave0 >= a.n) return;
-  uint64_t p = wave0;
-  uint4 A[2], B0;
-  A[0] = ld_chunk(a.frames + p * a.stride, 0, lane, stride);
-  CkHdr hA = ck_parse(A[0], a.mode, stride);
-  A[1] = hA.end > 1024 ? ld_chunk(a.frames + p * a.stride, 1, lane, hA.end)
-                       : make_uint4(0, 0, 0, 0);
-  B0 = (p + nw < a.n) ? ld_chunk(a.frames + (p + nw) * a.stride, 0, lane, stride)
-                      : make_uint4(0, 0, 0, 0);
-  for (; p < a.n; p += nw) {
-    const uint64_t pn = p + nw, pnn = pn + nw;
-    CkHdr hB;
-    uint4 B1 = make_uint4(0, 0, 0, 0);
-    if (pn < a.n) {
-      hB = ck_parse(B0, a.mode, stride);
-      if (hB.end > 1024) B1 = ld_chunk(a.frames + pn * a.stride, 1, lane, hB.end);
+  const uint64_t ntiles = (a.n + 63) / 64;
+  for (uint64_t tile = wave0; tile < ntiles; tile += nw) {
+    const uint64_t p0 = tile * 64;
+    const int cnt = (int)((a.n - p0) < 64 ? (a.n - p0) : 64);
+    // ---- phase 1: lane = frame
+    CkLane L;
+    uint8_t *mine = a.frames + (p0 + lane) * a.stride;
+    if (lane < cnt) {
+      L = ck_walk(mine, a.mode, stride);
+    } else {
+      L.flags = L.ip_rng = L.l4_rng = 0;
+      L.ip_off = 14;
+      L.old_ip = L.l4_ck = L.old_l4 = L.ps = L.ip24 = 0;
     }
-    uint4 C0 = make_uint4(0, 0, 0, 0);
-    if (pnn < a.n) C0 = ld_chunk(a.frames + pnn * a.stride, 0, lane, stride);
-    ck_finish<2>(a.frames + p * a.stride, p, A, hA, a, lane, 0u);
-    A[0] = B0;
-    A[1] = B1;
-    hA = hB;
-    B0 = C0;
+    // ---- phase 2: frame by frame across the wave
+    uint32_t res_ip = 0, res_l4 = 0;
+    uint32_t ipr = __builtin_amdgcn_readlane(L.ip_rng, 0);
+    uint32_t l4r = __builtin_amdgcn_readlane(L.l4_rng, 0);
+    int end = (int)max(rng_hi(ipr), rng_hi(l4r));
+    const uint8_t *f = a.frames + p0 * a.stride;
+    uint4 c0 = ld_chunk(f, 0, lane, end), c1 = ld_chunk(f, 1, lane, end);
+    for (int j = 0; j < cnt; j++) {
+      // prefetch frame j+1
+      uint32_t ipr_n = 0, l4r_n = 0;
+      uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+      if (j + 1 < cnt) {
+        ipr_n = __builtin_amdgcn_readlane(L.ip_rng, j + 1);
+        l4r_n = __builtin_amdgcn_readlane(L.l4_rng, j + 1);
+        const int end_n = (int)max(rng_hi(ipr_n), rng_hi(l4r_n));
+        const uint8_t *fn = f + a.stride;
+        n0 = ld_chunk(fn, 0, lane, end_n);
+        n1 = ld_chunk(fn, 1, lane, end_n);
+      }
+      const int o = lane * 16;
+      uint32_t s_ip = 0;
+      if (o < (int)rng_hi(ipr))
+        s_ip = chunk_sum(c0, o, (int)rng_lo(ipr), (int)rng_hi(ipr));
+      const int l4lo = (int)rng_lo(l4r), l4hi = (int)rng_hi(l4r);
+      uint32_t s_l4 = chunk_sum(c0, o, l4lo, l4hi);
+      if (1024 + o < l4hi) s_l4 += chunk_sum(c1, 1024 + o, l4lo, l4hi);
+      s_ip = wave_sum(s_ip);
+      s_l4 = wave_sum(s_l4);
+      res_ip = lane == j ? s_ip : res_ip;
+      res_l4 = lane == j ? s_l4 : res_l4;
+      c0 = n0;
+      c1 = n1;
+      ipr = ipr_n;
+      l4r = l4r_n;
+      f += a.stride;
+    }
+    if (lane >= cnt) continue;
+    // ---- phase 3: lane = frame
+    uint32_t ip_gate = 0;
+    bool ip_wrote = false;
+    uint32_t ip_new = 0;
+    if (L.flags & 1) {
+      if (L.flags & 2) {  // IHL < 5: calc writes 0, verify fails
+        if (a.verify) {
+          ip_gate = 1;
+        } else {
+          ip_wrote = true;
+        }
+      } else if (a.verify) {
+        ip_gate = fold16(res_ip) == 0xFFFFu ? 0u : 1u;
+      } else {
+        ip_wrote = true;
+        ip_new = (~fold16(res_ip - L.old_ip)) & 0xFFFFu;
+      }
+      if (ip_wrote)
+        *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
+    }
+    uint32_t l4_gate = kGateNone;
+    const uint32_t kind = (L.flags >> 2) & 3;
+    const bool valid = L.flags & 16;
+    const bool l4_runs = (a.mode & 2) && (!(a.mode & 1) || ip_gate == 0);
+    if (l4_runs) {
+      if (kind == 0) {
+        l4_gate = 0;
+      } else if (kind == 3) {
+        l4_gate = kGateNone;
+      } else {
+        uint32_t s = res_l4, old = L.old_l4;
+        if ((a.mode & 1) && ip_wrote && L.ip_off == 14) {
+          // IHL < 5: the "L4 header" overlaps the IP checksum just written
+          const uint32_t lo = rng_lo(L.l4_rng), hi = rng_hi(L.l4_rng);
+#pragma unroll
+          for (uint32_t b = 24; b < 26; b++) {
+            if (valid && b >= lo && b < hi) {
+              const int sh = (b & 1) * 8;
+              s = s - (((L.ip24 >> sh) & 0xFFu) << sh) +
+                  (((ip_new >> sh) & 0xFFu) << sh);
+            }
+          }
+          if (valid && L.l4_ck == 24) old = ip_new;
+        }
+        if (a.verify) {
+          if (!valid)
+            l4_gate = 1;
+          else if (kind == 1 && old == 0)
+            l4_gate = 0;  // UDP checksum 0 = not computed
+          else
+            l4_gate = fold16(s + L.ps) == 0xFFFFu ? 0u : 1u;
+        } else {
+          uint32_t ck = 0;
+          if (valid) {
+            ck = (~fold16(s - old + L.ps)) & 0xFFFFu;
+            if (kind == 1 && ck == 0) ck = 0xFFFFu;  // RFC 768
+          }
+          const uint32_t at = L.l4_ck;
+          if (at + 2 <= (uint32_t)stride)
+            *reinterpret_cast<uint16_t *>(mine + at) = (uint16_t)ck;
+          l4_gate = kind == 1 ? 0u : kGateNone;  // TCP: never emitted
+        }
+      }
+    }
+    if (a.ip_gates) a.ip_gates[p0 + lane] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
+    if (a.l4_gates) a.l4_gates[p0 + lane] = (uint16_t)l4_gate;
   }
 }
 
@@ -708,21 +944,31 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const uint64_t waves_per_block = kCkBlock / 64;
-  uint64_t blocks = (a.n + waves_per_block - 1) / waves_per_block;
+  const bool tiled = a.stride <= 2048 && !env_int("BG_CK_GENERIC", 0);
+  const void *kern = tiled ? reinterpret_cast<const void *>(cksum_kernel)
+                           : reinterpret_cast<const void *>(cksum_kernel_generic);
   int per_cu = env_int("BG_CK_BLOCKS_PER_CU", 0);
   if (per_cu <= 0) {
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(cksum_kernel), kCkBlock, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kCkBlock, 0) !=
             hipSuccess ||
         occ <= 0)
       occ = 7;
     per_cu = occ * std::max(1, env_int("BG_CK_GRID_MULT", 2));
   }
-  const uint64_t cap = (uint64_t)num_cus * per_cu;
-  if (blocks > cap) blocks = cap;
-  if (a.stride <= 2048 && !env_int("BG_CK_GENERIC", 0))
+  const uint64_t waves_per_block = kCkBlock / 64;
+  const uint64_t max_waves = (uint64_t)num_cus * per_cu * waves_per_block;
+  uint64_t waves;
+  if (tiled) {
+    // equal tile counts per wave: no tail from a partial last round
+    const uint64_t ntiles = (a.n + 63) / 64;
+    const uint64_t rounds = (ntiles + max_waves - 1) / max_waves;
+    waves = (ntiles + rounds - 1) / rounds;
+  } else {
+    waves = std::min<uint64_t>(a.n, max_waves);
+  }
+  const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
+  if (tiled)
     hipLaunchKernelGGL(cksum_kernel, dim3((unsigned)blocks), dim3(kCkBlock), 0,
                        s, a);
   else

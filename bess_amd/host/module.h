@@ -127,6 +127,18 @@ class Module {
  public:
   virtual ~Module() = default;
   virtual void ProcessBatch(Context *ctx, bess::PacketBatch *batch) = 0;
+  // Any number of packets in one call (the GPU modules run them as one
+  // device batch; BESS hands ProcessBatch <= 32). Returns 0 or -errno.
+  virtual int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
+                             size_t cnt) {
+    for (size_t i = 0; i < cnt; i += bess::PacketBatch::kMaxBurst) {
+      bess::PacketBatch b;
+      for (size_t j = i; j < cnt && j < i + bess::PacketBatch::kMaxBurst; j++)
+        b.add(pkts[j]);
+      ProcessBatch(ctx, &b);
+    }
+    return 0;
+  }
   virtual std::string GetDesc() const { return ""; }
   virtual const Commands &cmds() const = 0;
   // Device-resident datapath over a frame slab (libbessgpu.so).
@@ -134,6 +146,23 @@ class Module {
                             uint16_t *d_ogates, void *stream) = 0;
   void set_device(int d) { device_ = d; }
   int device() const { return device_; }
+
+  // Module::AddMetadataAttr (core/module.cc:248-285): per-module metadata
+  // attributes; returns the attribute id or -errno.
+  struct Attribute {
+    std::string name;
+    size_t size;
+  };
+  int AddMetadataAttr(const std::string &name, size_t size) {
+    if (attrs_.size() >= 16) return -ENOSPC;         // kMaxAttrsPerModule
+    if (name.empty()) return -EINVAL;
+    if (size < 1 || size > 32) return -EINVAL;       // kMetadataAttrMaxSize
+    for (const auto &a : attrs_)
+      if (a.name == name) return -EEXIST;
+    attrs_.push_back(Attribute{name, size});
+    return (int)attrs_.size() - 1;
+  }
+  const std::vector<Attribute> &all_attrs() const { return attrs_; }
 
   // core/module.h:543-594: the chosen gate is recorded for the packet.
   void EmitPacket(Context *ctx, bess::Packet *pkt, gate_idx_t ogate) {
@@ -145,6 +174,7 @@ class Module {
 
  protected:
   int device_ = 0;
+  std::vector<Attribute> attrs_;
 };
 
 // ModuleBuilder (core/module.h:108-172): class name -> factory taking the

@@ -66,15 +66,11 @@ def main():
         t.sync(0)
         ref = None
         variants = {
-            "slim_ppl1": {}, "slim_ppl2": {"BG_PPL": 2},
-            "slim_ppl1_x2": {"BG_GRID_MULT": 2},
-            "slim_ppl1_bpc2": {"BG_BLOCKS_PER_CU": 2},
-            "slim_ppl1_bpc8": {"BG_BLOCKS_PER_CU": 8},
-            "slim_ppl1_l2tab": {"BG_NOLDS": 1},
-            "slim_ppl1_l2tab_bpc16": {"BG_NOLDS": 1, "BG_BLOCKS_PER_CU": 16},
-            "fat_ppl1_bpc3": {"BG_FAT": 1, "BG_BLOCKS_PER_CU": 3},
-            "fat_ppl2_bpc3": {"BG_FAT": 1, "BG_PPL": 2, "BG_BLOCKS_PER_CU": 3},
-            "fat_ppl1_api": {"BG_FAT": 1},
+            "default": {}, "ppl2": {"BG_PPL": 2},
+            "bpc1": {"BG_BLOCKS_PER_CU": 1}, "bpc3": {"BG_BLOCKS_PER_CU": 3},
+            "bpc4": {"BG_BLOCKS_PER_CU": 4},
+            "ppl2_bpc1": {"BG_PPL": 2, "BG_BLOCKS_PER_CU": 1},
+            "fat_ppl2_bpc2": {"BG_FAT": 1, "BG_PPL": 2, "BG_BLOCKS_PER_CU": 2},
         }
         # every variant must give identical gates
         for name, env in variants.items():
@@ -95,10 +91,21 @@ def main():
         frames = P.cksum_workload(n, frame_len=1496)
         d = torch.from_numpy(frames.reshape(-1)).to(dev)
         l4 = torch.empty(n, dtype=torch.int16, device=dev)
-        variants = {"pipelined": {}, "generic": {"BG_CK_GENERIC": 1},
-                    "pipelined_x2": {"BG_CK_GRID_MULT": 2},
-                    "pipelined_bpc7": {"BG_CK_BLOCKS_PER_CU": 7},
-                    "pipelined_bpc4": {"BG_CK_BLOCKS_PER_CU": 4}}
+        variants = {"tiled": {}, "generic": {"BG_CK_GENERIC": 1},
+                    "tiled_x2": {"BG_CK_GRID_MULT": 2},
+                    "tiled_bpc4": {"BG_CK_BLOCKS_PER_CU": 4},
+                    "tiled_bpc2": {"BG_CK_BLOCKS_PER_CU": 2}}
+        outs = {}
+        for name, env in variants.items():
+            dd = torch.from_numpy(frames.reshape(-1)).to(dev)
+            set_env(env)
+            F.cksum(dd, 2048, n, 3, False, None, l4)
+            torch.cuda.synchronize()
+            outs[name] = (dd.cpu(), l4.cpu())
+        base = next(iter(outs.values()))
+        for name, (x, y) in outs.items():
+            assert torch.equal(x, base[0]) and torch.equal(y, base[1]), name
+        del outs
         # (idempotent after the first pass: recompute writes the same bytes)
         r = time_variants(lambda: F.cksum(d, 2048, n, 3, False, None, l4),
                           variants)
@@ -118,7 +125,9 @@ def main():
         g = torch.empty(n, dtype=torch.int16, device=dev)
         t.sync(0)
         variants = {"ppl1": {}, "ppl2": {"BG_PPL": 2},
-                    "ppl1_bpc8": {"BG_BLOCKS_PER_CU": 8}}
+                    "ppl1_bpc4": {"BG_BLOCKS_PER_CU": 4},
+                    "ppl1_bpc2": {"BG_BLOCKS_PER_CU": 2},
+                    "ppl2_bpc4": {"BG_PPL": 2, "BG_BLOCKS_PER_CU": 4}}
         r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants)
         for k in r:
             r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
