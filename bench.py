@@ -101,18 +101,12 @@ def em_setup(args, rank, world, dev, torch, dist):
     table = {"rules": len(t)}
     if world > 1:
         # sharded build + RCCL all-gather of the partition images
-        pb = t.plan(world)
-        part = torch.from_numpy(t.build_part(rank, pb)).to(dev)
-        full = torch.empty(pb * world, dtype=torch.uint8, device=dev)
+        from bess_amd import dist as D
         dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        dist.all_gather_into_tensor(full, part)
-        torch.cuda.synchronize()
-        table["allgather_ms"] = (time.perf_counter() - t0) * 1e3
-        table["allgather_bytes"] = pb * world
-        t.attach(dev.index, full)
-        t._keep = (part, full)
+        _, st = D.sharded_em_table(t, rank, world, device=dev)
+        table["allgather_ms"] = round(st["allgather_ms"], 3)
+        table["allgather_bytes"] = st["bytes"]
+        table["part_build_ms"] = round(st["build_ms"], 2)
     else:
         t.sync(dev.index)
     nbytes, in_lds = t.table_info()

@@ -1,0 +1,161 @@
+"""pybess-style module handles over libbessgpu's module surface.
+
+    em = ExactMatch(fields=[{'offset': 26, 'num_bytes': 4}, ...])
+    em.add(fields=[{'value_bin': b'...'}, ...], gate=1)
+    em.set_default_gate(gate=3)
+    gates = em.process(frames, stride, n)
+
+Create and command calls carry serialized bess.pb messages through the
+bg_module_create / bg_module_command C ABI exactly as pybess carries them
+to bessd over gRPC (pybess/bess.py:458-500: `<mclass>Arg` for create, the
+command's argument type from the module's cmds table); failures raise
+ModuleError(errno, message) like pybess's BESS.Error.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib, pb
+from ._lib import BG_GATE_NONE, lib
+
+# command -> (argument message, response message or None); module cmds
+# tables: exact_match.cc:45-60, wildcard_match.cc:58-73
+_EM_CMDS = {
+    "get_initial_arg": ("EmptyArg", "ExactMatchArg"),
+    "get_runtime_config": ("EmptyArg", "ExactMatchConfig"),
+    "set_runtime_config": ("ExactMatchConfig", None),
+    "add": ("ExactMatchCommandAddArg", None),
+    "delete": ("ExactMatchCommandDeleteArg", None),
+    "clear": ("EmptyArg", None),
+    "set_default_gate": ("ExactMatchCommandSetDefaultGateArg", None),
+}
+_WM_CMDS = {
+    "get_initial_arg": ("EmptyArg", "WildcardMatchArg"),
+    "get_runtime_config": ("EmptyArg", "WildcardMatchConfig"),
+    "set_runtime_config": ("WildcardMatchConfig", None),
+    "add": ("WildcardMatchCommandAddArg", None),
+    "delete": ("WildcardMatchCommandDeleteArg", None),
+    "clear": ("EmptyArg", None),
+    "set_default_gate": ("WildcardMatchCommandSetDefaultGateArg", None),
+}
+
+
+class ModuleError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("[errno %d] %s" % (code, msg))
+        self.code = code
+        self.errmsg = msg
+
+
+def _check(rc):
+    if rc < 0:
+        m = lib().bg_last_error()
+        raise ModuleError(-rc, m.decode() if m else "")
+    return rc
+
+
+class Module:
+    mclass = None
+    cmds = {}
+
+    def __init__(self, **kwargs):
+        arg = pb.dict_to_protobuf(pb.message(self.mclass + "Arg"), kwargs)
+        buf = arg.SerializeToString()
+        h = C.c_void_p()
+        _check(lib().bg_module_create(self.mclass.encode(), buf, len(buf),
+                                      C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_module_destroy(self.h)
+            self.h = None
+
+    def command(self, cmd, arg_type=None, **kwargs):
+        """bg_module_command with a dict argument; returns the response
+        message (or None)."""
+        a_type, r_type = self.cmds.get(cmd, (arg_type or "EmptyArg", None))
+        arg = pb.dict_to_protobuf(pb.message(a_type), kwargs).SerializeToString()
+        cap = C.c_size_t(1 << 16)
+        out = C.create_string_buffer(cap.value)
+        rc = lib().bg_module_command(self.h, cmd.encode(), arg, len(arg), out,
+                                     C.byref(cap))
+        if rc < 0 and cap.value > len(out):
+            out = C.create_string_buffer(cap.value)
+            rc = lib().bg_module_command(self.h, cmd.encode(), arg, len(arg),
+                                         out, C.byref(cap))
+        _check(rc)
+        if r_type is None:
+            return None
+        return pb.message(r_type).FromString(out.raw[:cap.value])
+
+    def desc(self):
+        buf = C.create_string_buffer(256)
+        lib().bg_module_desc(self.h, buf, 256)
+        return buf.value.decode()
+
+    def set_device(self, device):
+        lib().bg_module_set_device(self.h, device)
+
+    def process(self, frames, stride, n):
+        """ProcessBatch over host frames (numpy uint8 slab, frame i at
+        i*stride, each with >= 2048 accessible bytes for the checksum
+        modules). Returns per-packet EmitPacket gates (BG_GATE_NONE: not
+        emitted). Checksum modules rewrite frames in place."""
+        base = frames.ctypes.data
+        heads = (C.c_void_p * n)(*[base + i * stride for i in range(n)])
+        og = np.full(n, BG_GATE_NONE, np.uint16)
+        _check(lib().bg_module_process(self.h, heads, n, og.ctypes.data))
+        return og
+
+    def process_device(self, d_frames, stride, n, d_ogates, stream=None):
+        """Device-resident ProcessBatch over a torch uint8 slab."""
+        from .flowtable import _stream_ptr
+        _check(lib().bg_module_process_device(
+            self.h, C.c_void_p(d_frames.data_ptr()), stride, n,
+            C.c_void_p(d_ogates.data_ptr()), _stream_ptr(stream)))
+
+
+class _RuleModule(Module):
+    def get_initial_arg(self):
+        return self.command("get_initial_arg")
+
+    def get_runtime_config(self):
+        return self.command("get_runtime_config")
+
+    def set_runtime_config(self, **kw):
+        return self.command("set_runtime_config", **kw)
+
+    def add(self, **kw):
+        return self.command("add", **kw)
+
+    def delete(self, **kw):
+        return self.command("delete", **kw)
+
+    def clear(self):
+        return self.command("clear")
+
+    def set_default_gate(self, **kw):
+        return self.command("set_default_gate", **kw)
+
+
+class ExactMatch(_RuleModule):
+    """core/modules/exact_match.cc on the GPU."""
+    mclass = "ExactMatch"
+    cmds = _EM_CMDS
+
+
+class WildcardMatch(_RuleModule):
+    """core/modules/wildcard_match.cc on the GPU."""
+    mclass = "WildcardMatch"
+    cmds = _WM_CMDS
+
+
+class IPChecksum(Module):
+    """core/modules/ip_checksum.cc on the GPU."""
+    mclass = "IPChecksum"
+
+
+class L4Checksum(Module):
+    """core/modules/l4_checksum.cc on the GPU."""
+    mclass = "L4Checksum"

@@ -1,0 +1,140 @@
+"""bess.pb messages of the classification path for Python callers.
+
+The reference generates these from protobuf/module_msg.proto and
+protobuf/util_msg.proto with protoc (absent here); the same messages --
+names, field numbers, types, oneofs -- are declared below as a
+FileDescriptorProto and materialised with the protobuf runtime, so bytes
+serialized here are wire-identical to what pybess sends to bessd
+(pybess/bess.py:458-500) and what libbessgpu's module layer parses.
+
+Also provides pybess's dict <-> message helpers
+(pybess/protobuf_to_dict.py semantics: dict_to_protobuf / protobuf_to_dict).
+"""
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+_F = descriptor_pb2.FieldDescriptorProto
+
+# (message, [(field, number, type, label, type_name or None, oneof or None)])
+_MESSAGES = [
+    ("EmptyArg", []),
+    # util_msg.proto:36-42
+    ("Field", [("attr_name", 1, _F.TYPE_STRING, 1, None, "position"),
+               ("offset", 2, _F.TYPE_UINT32, 1, None, "position"),
+               ("num_bytes", 3, _F.TYPE_UINT32, 1, None, None)]),
+    # util_msg.proto:45-50
+    ("FieldData", [("value_bin", 1, _F.TYPE_BYTES, 1, None, "encoding"),
+                   ("value_int", 2, _F.TYPE_UINT64, 1, None, "encoding")]),
+    # module_msg.proto:501-504
+    ("ExactMatchArg", [("fields", 1, _F.TYPE_MESSAGE, 3, ".bess.pb.Field", None),
+                       ("masks", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None)]),
+    # module_msg.proto:69-72
+    ("ExactMatchCommandAddArg", [
+        ("gate", 1, _F.TYPE_UINT64, 1, None, None),
+        ("fields", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None)]),
+    # module_msg.proto:78-80
+    ("ExactMatchCommandDeleteArg", [
+        ("fields", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None)]),
+    ("ExactMatchCommandClearArg", []),
+    # module_msg.proto:94-96
+    ("ExactMatchCommandSetDefaultGateArg", [("gate", 1, _F.TYPE_UINT64, 1, None, None)]),
+    # module_msg.proto:511-514
+    ("ExactMatchConfig", [
+        ("default_gate", 1, _F.TYPE_UINT64, 1, None, None),
+        ("rules", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.ExactMatchCommandAddArg", None)]),
+    # module_msg.proto:1152-1154
+    ("WildcardMatchArg", [("fields", 1, _F.TYPE_MESSAGE, 3, ".bess.pb.Field", None)]),
+    # module_msg.proto:375-380
+    ("WildcardMatchCommandAddArg", [
+        ("gate", 1, _F.TYPE_UINT64, 1, None, None),
+        ("priority", 2, _F.TYPE_INT64, 1, None, None),
+        ("values", 3, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None),
+        ("masks", 4, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None)]),
+    # module_msg.proto:385-388
+    ("WildcardMatchCommandDeleteArg", [
+        ("values", 1, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None),
+        ("masks", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.FieldData", None)]),
+    ("WildcardMatchCommandClearArg", []),
+    # module_msg.proto:403-405
+    ("WildcardMatchCommandSetDefaultGateArg", [("gate", 1, _F.TYPE_UINT64, 1, None, None)]),
+    # module_msg.proto:1161-1164
+    ("WildcardMatchConfig", [
+        ("default_gate", 1, _F.TYPE_UINT64, 1, None, None),
+        ("rules", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.WildcardMatchCommandAddArg", None)]),
+    # module_msg.proto:997-999 / 1010-1012
+    ("IPChecksumArg", [("verify", 1, _F.TYPE_BOOL, 1, None, None)]),
+    ("L4ChecksumArg", [("verify", 1, _F.TYPE_BOOL, 1, None, None)]),
+]
+
+
+def _build():
+    fdp = descriptor_pb2.FileDescriptorProto(
+        name="bess_amd/module_msg_subset.proto", package="bess.pb",
+        syntax="proto3")
+    for mname, fields in _MESSAGES:
+        m = fdp.message_type.add(name=mname)
+        oneofs = []
+        for fname, num, ftype, label, tname, oneof in fields:
+            f = m.field.add(name=fname, number=num, type=ftype, label=label)
+            if tname:
+                f.type_name = tname
+            if oneof:
+                if oneof not in oneofs:
+                    oneofs.append(oneof)
+                    m.oneof_decl.add(name=oneof)
+                f.oneof_index = oneofs.index(oneof)
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fdp)
+    out = {}
+    for mname, _ in _MESSAGES:
+        out[mname] = message_factory.GetMessageClass(
+            pool.FindMessageTypeByName("bess.pb." + mname))
+    return out
+
+
+_CLASSES = _build()
+globals().update(_CLASSES)
+
+
+def message(name):
+    return _CLASSES[name]
+
+
+def _repeated(fd):
+    r = getattr(fd, "is_repeated", None)
+    if r is not None:
+        return r
+    return fd.label == fd.LABEL_REPEATED
+
+
+def dict_to_protobuf(cls, d):
+    """pybess dict_to_protobuf: nested dicts / lists of dicts -> message."""
+    msg = cls() if isinstance(cls, type) else cls
+    for key, val in (d or {}).items():
+        fd = msg.DESCRIPTOR.fields_by_name[key]
+        if fd.type == fd.TYPE_MESSAGE:
+            if _repeated(fd):
+                for item in val:
+                    dict_to_protobuf(getattr(msg, key).add(), item)
+            else:
+                dict_to_protobuf(getattr(msg, key), val)
+        elif _repeated(fd):
+            getattr(msg, key).extend(val)
+        else:
+            setattr(msg, key, val)
+    return msg
+
+
+def protobuf_to_dict(msg):
+    """pybess protobuf_to_dict: only fields that are set (ListFields)."""
+    out = {}
+    for fd, val in msg.ListFields():
+        if fd.type == fd.TYPE_MESSAGE:
+            if _repeated(fd):
+                out[fd.name] = [protobuf_to_dict(v) for v in val]
+            else:
+                out[fd.name] = protobuf_to_dict(val)
+        elif _repeated(fd):
+            out[fd.name] = list(val)
+        else:
+            out[fd.name] = val
+    return out

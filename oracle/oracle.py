@@ -167,19 +167,23 @@ def _fd_kind(fd):
 
 
 class _MetadataRegistry:
-    """Module::AddMetadataAttr stand-in for the control plane: attribute ids
-    in order of first registration (core/metadata.cc); attr fields are only
-    carried through the configuration surface, not the datapath."""
+    """Module::AddMetadataAttr (core/module.cc:248-285) for the control
+    plane: per-module attribute list; attr fields are carried through the
+    configuration surface only (no datapath here)."""
 
     def __init__(self):
         self.names = []
         self.sizes = {}
 
     def add(self, name, size):
+        if len(self.names) >= 16:          # kMaxAttrsPerModule
+            return -errno.ENOSPC
+        if not name:
+            return -errno.EINVAL
+        if size < 1 or size > 32:          # kMetadataAttrMaxSize
+            return -errno.EINVAL
         if name in self.sizes:
-            if self.sizes[name] != size:
-                return -errno.EINVAL
-            return self.names.index(name)
+            return -errno.EEXIST
         self.names.append(name)
         self.sizes[name] = size
         return len(self.names) - 1
