@@ -594,99 +594,105 @@ __device__ __forceinline__ uint4 ld_chunk(const uint8_t *f, int k, int lane,
 }
 
 // ---------------------------------------------------------------------------
-// Tiled checksum kernel (stride <= 2048): a wave owns tiles of 64 frames.
-//   1. lane = frame: header walk of 64 frames at once (vector ALU, per-lane
-//      loads); results stay in VGPRs.
-//   2. frame by frame, all 64 lanes: coalesced 16 B/lane loads of the frame
-//      (next frame prefetched), masked range sums, DPP wave reductions; the
-//      two sums go back to the frame's lane (v_writelane).
-//   3. lane = frame: fold, write checksum words in place, write gates.
-// The scalar unit only handles the per-frame loop (no per-frame header walk),
-// which bounded the one-wave-per-frame form.
+// Tiled checksum kernel (128 <= stride <= 2048): a wave owns tiles of 64
+// frames.
+//   1. lane = frame: the first 128 bytes of the frame (one 128 B line) are
+//      loaded to registers; header walk, the IPv4 header sum and the L4 sum
+//      of bytes < 128 are computed there with static register indices.
+//   2. frame by frame, all 64 lanes: coalesced 16 B/lane loads of bytes
+//      [128, l4_end) (next frame prefetched), unmasked u16-halves sums with
+//      one tail mask, DPP wave reduction; the sum goes back to the frame's
+//      lane. Frames whose L4 range ends below 128 skip this phase.
+//   3. lane = frame: fold, patch the checksum words into the registers of
+//      the header line and store the whole 128 B line (no partial-line
+//      read-modify-write in HBM), write the gates.
+// The scalar unit only handles the per-frame loop.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t byte_of(const uint32_t (&h)[12], int o) {
-  return (h[o >> 2] >> ((o & 3) * 8)) & 0xFFu;  // o compile-time constant
-}
-__device__ __forceinline__ uint32_t be16_of(const uint32_t (&h)[12], int o) {
-  return (byte_of(h, o) << 8) | byte_of(h, o + 1);
-}
-__device__ __forceinline__ uint32_t le16_of(const uint32_t (&h)[12], int o) {
-  return byte_of(h, o) | (byte_of(h, o + 1) << 8);
-}
+constexpr int kHdrDw = 32;  // 128-byte header line
+
 __device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) {
   return *reinterpret_cast<const uint16_t *>(p);
 }
 
-struct CkLane {      // phase-1 results of this lane's frame
-  uint32_t ip_rng;   // ip_lo | ip_hi << 16 (0: no IPv4 header to sum)
-  uint32_t l4_rng;   // l4_lo | l4_hi << 16
-  uint32_t flags;    // bit0 ip_state, bit1 ihl<5, 2-3 l4_kind, 4 l4_valid
-  uint32_t ip_off;   // 14 / 18 / 22
-  uint32_t old_ip;   // IPv4 checksum field before the write
-  uint32_t l4_ck;    // frame offset of the L4 checksum word
-  uint32_t old_l4;
-  uint32_t ps;       // pseudo-header sum
-  uint32_t ip24;     // bytes 24..25 (pipeline overlap fix-up)
+// u16-halves sum of the bytes of h[d] (frame offset 4d) inside [lo, hi)
+__device__ __forceinline__ uint32_t dw_range_sum(uint32_t w, int o, int lo,
+                                                 int hi) {
+  int a = lo - o, b = hi - o;
+  a = a < 0 ? 0 : (a > 4 ? 4 : a);
+  b = b < 0 ? 0 : (b > 4 ? 4 : b);
+  const uint32_t m =
+      b > a ? ((0xFFFFFFFFu >> (32 - 8 * (b - a))) << (8 * a)) : 0u;
+  const uint32_t v = w & m;
+  return (v & 0xFFFFu) + (v >> 16);
+}
+
+__device__ __forceinline__ uint32_t hb(const uint32_t (&h)[kHdrDw], int o) {
+  return (h[o >> 2] >> ((o & 3) * 8)) & 0xFFu;  // o compile-time constant
+}
+__device__ __forceinline__ uint32_t hbe16(const uint32_t (&h)[kHdrDw], int o) {
+  return (hb(h, o) << 8) | hb(h, o + 1);
+}
+__device__ __forceinline__ uint32_t hle16(const uint32_t (&h)[kHdrDw], int o) {
+  return hb(h, o) | (hb(h, o + 1) << 8);
+}
+
+struct CkLane {       // phase-1 state of this lane's frame
+  uint32_t flags;     // bit0 ip_state, bit1 ihl<5, 2-3 l4_kind, 4 l4_valid
+  uint32_t ip_off;    // 14 / 18 / 22
+  uint32_t s_ip;      // IPv4 header sum (all header bytes)
+  uint32_t s_l4;      // L4 range sum over bytes < 128
+  uint32_t l4_lo, l4_hi;
+  uint32_t l4_ck;     // frame offset of the L4 checksum word
+  uint32_t ps;        // pseudo-header sum
 };
 
-__device__ __forceinline__ CkLane ck_walk(const uint8_t *f, int mode,
+// (Fields at per-lane offsets are read with per-lane 2-byte loads of the
+// frame -- L1 hits -- never by indexing the register array dynamically,
+// which would move it to scratch.)
+__device__ __forceinline__ CkLane ck_walk(const uint8_t *f,
+                                          const uint32_t (&h)[kHdrDw], int mode,
                                           int stride) {
   CkLane r;
-  uint32_t h[12];
-  const uint4 *q = reinterpret_cast<const uint4 *>(f);
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    const uint4 v = q[c];
-    h[4 * c] = v.x;
-    h[4 * c + 1] = v.y;
-    h[4 * c + 2] = v.z;
-    h[4 * c + 3] = v.w;
-  }
   r.flags = 0;
-  r.ip_rng = 0;
-  r.l4_rng = 0;
   r.ip_off = 14;
-  r.old_ip = 0;
+  r.s_ip = 0;
+  r.s_l4 = 0;
+  r.l4_lo = r.l4_hi = 0;
   r.l4_ck = 0;
-  r.old_l4 = 0;
   r.ps = 0;
-  r.ip24 = le16_of(h, 24);
-  const uint32_t et12 = be16_of(h, 12);
+  const uint32_t et12 = hbe16(h, 12);
   // IPChecksum ethertype walk (ip_checksum.cc:50-74)
   if (mode & 1) {
-    const uint32_t et16 = be16_of(h, 16), et20 = be16_of(h, 20);
-    bool fwd = false;
     uint32_t et = et12, off = 14;
-    if (et == 0x88a8) {
-      et = et16;
+    bool fwd = false;
+    if (et == 0x88a8) {  // kQinQ must carry an 802.1Q tag
+      et = hbe16(h, 16);
       off = 18;
       if (et != 0x8100) fwd = true;
     }
-    if (!fwd && et == 0x8100) {
-      et = off == 14 ? et16 : et20;
+    if (!fwd && et == 0x8100) {  // kVlan
+      et = off == 14 ? hbe16(h, 16) : hbe16(h, 20);
       off += 4;
     }
     if (!fwd && et == 0x0800) {
       r.flags |= 1;
       r.ip_off = off;
-      const uint32_t vihl = off == 14 ? byte_of(h, 14)
-                           : off == 18 ? byte_of(h, 18) : byte_of(h, 22);
-      r.old_ip = off == 14 ? le16_of(h, 24)
-                 : off == 18 ? le16_of(h, 28) : le16_of(h, 32);
+      const uint32_t vihl =
+          off == 14 ? hb(h, 14) : (off == 18 ? hb(h, 18) : hb(h, 22));
       const uint32_t hl = (vihl & 15) * 4;
-      if (hl >= 20) {
-        uint32_t hi = off + hl;
-        if (hi > (uint32_t)stride) hi = stride;
-        r.ip_rng = off | (hi << 16);
+      if (hl >= 20) {  // header <= 22 + 60 bytes: inside the 128 B line
+        const int lo = (int)off, hi = (int)(off + hl);
+#pragma unroll
+        for (int d = 3; d < 21; d++) r.s_ip += dw_range_sum(h[d], 4 * d, lo, hi);
       } else {
-        r.flags |= 2;
+        r.flags |= 2;  // IHL < 5: calc writes 0, verify fails
       }
     }
   }
   // L4Checksum (l4_checksum.cc:53-82): untagged IPv4 only
   if ((mode & 2) && et12 == 0x0800) {
-    const uint32_t hl = (byte_of(h, 14) & 15) * 4;
-    const uint32_t proto = byte_of(h, 23);
+    const uint32_t hl = (hb(h, 14) & 15) * 4;
+    const uint32_t proto = hb(h, 23);
     const uint32_t l4_off = 14 + hl;
     uint32_t kind = 3, len = 0, valid = 0;
     if (proto == 17) {
@@ -697,7 +703,7 @@ __device__ __forceinline__ CkLane ck_walk(const uint8_t *f, int mode,
       r.l4_ck = l4_off + 6;
     } else if (proto == 6) {
       kind = 2;
-      const uint32_t ip_len = be16_of(h, 16);
+      const uint32_t ip_len = hbe16(h, 16);
       valid = ip_len >= hl + 20;
       len = (ip_len - hl) & 0xFFFF;
       r.l4_ck = l4_off + 16;
@@ -708,21 +714,39 @@ __device__ __forceinline__ CkLane ck_walk(const uint8_t *f, int mode,
         r.flags |= 16;
         uint32_t hi = l4_off + len;
         if (hi > (uint32_t)stride) hi = stride;  // reference reads past (UB)
-        r.l4_rng = l4_off | (hi << 16);
-        r.old_l4 = ld_u16(f + r.l4_ck);
+        r.l4_lo = l4_off;
+        r.l4_hi = hi;
+#pragma unroll
+        for (int d = 3; d < kHdrDw; d++)
+          r.s_l4 += dw_range_sum(h[d], 4 * d, (int)l4_off, (int)hi);
       }
-      r.ps = le16_of(h, 26) + le16_of(h, 28) + le16_of(h, 30) + le16_of(h, 32) +
+      r.ps = hle16(h, 26) + hle16(h, 28) + hle16(h, 30) + hle16(h, 32) +
              ((len >> 8) | ((len & 0xFF) << 8)) + (kind == 1 ? 0x1100u : 0x0600u);
     }
   }
   return r;
 }
 
-__device__ __forceinline__ uint32_t rng_lo(uint32_t r) { return r & 0xFFFFu; }
-__device__ __forceinline__ uint32_t rng_hi(uint32_t r) { return r >> 16; }
+// 16 bytes at frame offset o >= 128 restricted to [., hi): whole dwords
+// before hi, a byte mask on the one that straddles it
+__device__ __forceinline__ uint32_t tail_sum(const uint4 &c, int o, int hi) {
+  uint32_t s = 0;
+  const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int b = hi - (o + 4 * k);
+    b = b < 0 ? 0 : (b > 4 ? 4 : b);
+    const uint32_t m = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    const uint32_t v = w[k] & m;
+    s += (v & 0xFFFFu) + (v >> 16);
+  }
+  return s;
+}
 
-__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
-void cksum_kernel(CkArgs a) {
+// RELOAD: phase 3 re-reads the header line (an L2 hit when it is still
+// resident) instead of holding it in 32 VGPRs through phase 2.
+template <bool RELOAD, int DEPTH>
+__device__ __forceinline__ void cksum_body(const CkArgs &a) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
       ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -733,53 +757,86 @@ void cksum_kernel(CkArgs a) {
     const uint64_t p0 = tile * 64;
     const int cnt = (int)((a.n - p0) < 64 ? (a.n - p0) : 64);
     // ---- phase 1: lane = frame
+    uint8_t *mine = a.frames + (p0 + (uint64_t)lane) * a.stride;
+    uint32_t h[kHdrDw];
     CkLane L;
-    uint8_t *mine = a.frames + (p0 + lane) * a.stride;
     if (lane < cnt) {
-      L = ck_walk(mine, a.mode, stride);
-    } else {
-      L.flags = L.ip_rng = L.l4_rng = 0;
-      L.ip_off = 14;
-      L.old_ip = L.l4_ck = L.old_l4 = L.ps = L.ip24 = 0;
-    }
-    // ---- phase 2: frame by frame across the wave
-    uint32_t res_ip = 0, res_l4 = 0;
-    uint32_t ipr = __builtin_amdgcn_readlane(L.ip_rng, 0);
-    uint32_t l4r = __builtin_amdgcn_readlane(L.l4_rng, 0);
-    int end = (int)max(rng_hi(ipr), rng_hi(l4r));
-    const uint8_t *f = a.frames + p0 * a.stride;
-    uint4 c0 = ld_chunk(f, 0, lane, end), c1 = ld_chunk(f, 1, lane, end);
-    for (int j = 0; j < cnt; j++) {
-      // prefetch frame j+1
-      uint32_t ipr_n = 0, l4r_n = 0;
-      uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
-      if (j + 1 < cnt) {
-        ipr_n = __builtin_amdgcn_readlane(L.ip_rng, j + 1);
-        l4r_n = __builtin_amdgcn_readlane(L.l4_rng, j + 1);
-        const int end_n = (int)max(rng_hi(ipr_n), rng_hi(l4r_n));
-        const uint8_t *fn = f + a.stride;
-        n0 = ld_chunk(fn, 0, lane, end_n);
-        n1 = ld_chunk(fn, 1, lane, end_n);
+      const uint4 *q = reinterpret_cast<const uint4 *>(mine);
+#pragma unroll
+      for (int c = 0; c < kHdrDw / 4; c++) {
+        const uint4 v = q[c];
+        h[4 * c] = v.x;
+        h[4 * c + 1] = v.y;
+        h[4 * c + 2] = v.z;
+        h[4 * c + 3] = v.w;
       }
-      const int o = lane * 16;
-      uint32_t s_ip = 0;
-      if (o < (int)rng_hi(ipr))
-        s_ip = chunk_sum(c0, o, (int)rng_lo(ipr), (int)rng_hi(ipr));
-      const int l4lo = (int)rng_lo(l4r), l4hi = (int)rng_hi(l4r);
-      uint32_t s_l4 = chunk_sum(c0, o, l4lo, l4hi);
-      if (1024 + o < l4hi) s_l4 += chunk_sum(c1, 1024 + o, l4lo, l4hi);
-      s_ip = wave_sum(s_ip);
-      s_l4 = wave_sum(s_l4);
-      res_ip = lane == j ? s_ip : res_ip;
-      res_l4 = lane == j ? s_l4 : res_l4;
-      c0 = n0;
-      c1 = n1;
-      ipr = ipr_n;
-      l4r = l4r_n;
+      L = ck_walk(mine, h, a.mode, stride);
+    } else {
+#pragma unroll
+      for (int d = 0; d < kHdrDw; d++) h[d] = 0;
+      L.flags = L.s_ip = L.s_l4 = L.l4_lo = L.l4_hi = L.l4_ck = L.ps = 0;
+      L.ip_off = 14;
+    }
+    // ---- phase 2: bytes [128, l4_hi) of each frame across the wave,
+    // DEPTH frames prefetched ahead
+    uint32_t tail = 0;
+    const uint8_t *f = a.frames + p0 * a.stride;
+    uint4 q0[DEPTH + 1], q1[DEPTH + 1];
+    int qh[DEPTH + 1];
+#pragma unroll
+    for (int d = 0; d <= DEPTH; d++) {
+      q0[d] = q1[d] = make_uint4(0, 0, 0, 0);
+      qh[d] = 0;
+      if (d < DEPTH && d < cnt) {
+        qh[d] = (int)__builtin_amdgcn_readlane(L.l4_hi, d);
+        if (qh[d] > 128) {
+          const uint8_t *fd = f + (size_t)d * a.stride + 128;
+          q0[d] = ld_chunk(fd, 0, lane, qh[d] - 128);
+          q1[d] = ld_chunk(fd, 1, lane, qh[d] - 128);
+        }
+      }
+    }
+    for (int j = 0; j < cnt; j++) {
+      if (j + DEPTH < cnt) {  // prefetch frame j+DEPTH
+        const int hn = (int)__builtin_amdgcn_readlane(L.l4_hi, j + DEPTH);
+        qh[DEPTH] = hn;
+        if (hn > 128) {
+          const uint8_t *fn = f + (size_t)DEPTH * a.stride + 128;
+          q0[DEPTH] = ld_chunk(fn, 0, lane, hn - 128);
+          q1[DEPTH] = ld_chunk(fn, 1, lane, hn - 128);
+        }
+      }
+      const int hi = qh[0];
+      if (hi > 128) {  // wave-uniform
+        const int o = 128 + lane * 16;
+        uint32_t s = tail_sum(q0[0], o, hi);
+        if (o + 1024 < hi) s += tail_sum(q1[0], o + 1024, hi);
+        s = wave_sum(s);
+        tail = lane == j ? s : tail;
+      }
+#pragma unroll
+      for (int d = 0; d < DEPTH; d++) {
+        q0[d] = q0[d + 1];
+        q1[d] = q1[d + 1];
+        qh[d] = qh[d + 1];
+      }
+      q0[DEPTH] = q1[DEPTH] = make_uint4(0, 0, 0, 0);
+      qh[DEPTH] = 0;
       f += a.stride;
     }
     if (lane >= cnt) continue;
     // ---- phase 3: lane = frame
+    if (RELOAD) {
+      const uint4 *q = reinterpret_cast<const uint4 *>(mine);
+#pragma unroll
+      for (int c = 0; c < kHdrDw / 4; c++) {
+        const uint4 v = q[c];
+        h[4 * c] = v.x;
+        h[4 * c + 1] = v.y;
+        h[4 * c + 2] = v.z;
+        h[4 * c + 3] = v.w;
+      }
+    }
     uint32_t ip_gate = 0;
     bool ip_wrote = false;
     uint32_t ip_new = 0;
@@ -791,15 +848,16 @@ void cksum_kernel(CkArgs a) {
           ip_wrote = true;
         }
       } else if (a.verify) {
-        ip_gate = fold16(res_ip) == 0xFFFFu ? 0u : 1u;
+        ip_gate = fold16(L.s_ip) == 0xFFFFu ? 0u : 1u;
       } else {
+        const uint32_t old = L.ip_off == 14 ? hle16(h, 24)
+                             : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
+        ip_new = (~fold16(L.s_ip - old)) & 0xFFFFu;
         ip_wrote = true;
-        ip_new = (~fold16(res_ip - L.old_ip)) & 0xFFFFu;
       }
-      if (ip_wrote)
-        *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
     }
-    uint32_t l4_gate = kGateNone;
+    uint32_t l4_gate = kGateNone, l4_new = 0;
+    bool l4_wrote = false;
     const uint32_t kind = (L.flags >> 2) & 3;
     const bool valid = L.flags & 16;
     const bool l4_runs = (a.mode & 2) && (!(a.mode & 1) || ip_gate == 0);
@@ -809,19 +867,16 @@ void cksum_kernel(CkArgs a) {
       } else if (kind == 3) {
         l4_gate = kGateNone;
       } else {
-        uint32_t s = res_l4, old = L.old_l4;
-        if ((a.mode & 1) && ip_wrote && L.ip_off == 14) {
-          // IHL < 5: the "L4 header" overlaps the IP checksum just written
-          const uint32_t lo = rng_lo(L.l4_rng), hi = rng_hi(L.l4_rng);
-#pragma unroll
-          for (uint32_t b = 24; b < 26; b++) {
-            if (valid && b >= lo && b < hi) {
-              const int sh = (b & 1) * 8;
-              s = s - (((L.ip24 >> sh) & 0xFFu) << sh) +
-                  (((ip_new >> sh) & 0xFFu) << sh);
-            }
-          }
-          if (valid && L.l4_ck == 24) old = ip_new;
+        uint32_t s = L.s_l4 + tail;
+        uint32_t old = valid ? ld_u16(mine + L.l4_ck) : 0u;
+        // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
+        // the "L4 header" overlaps the IP checksum bytes 24..25.
+        if (ip_wrote && L.ip_off == 14 && valid) {
+          const int lo2 = (int)L.l4_lo > 24 ? (int)L.l4_lo : 24;
+          const int hi2 = (int)L.l4_hi < 26 ? (int)L.l4_hi : 26;
+          s = s - dw_range_sum(hle16(h, 24), 24, lo2, hi2) +
+              dw_range_sum(ip_new, 24, lo2, hi2);
+          if (L.l4_ck == 24) old = ip_new;
         }
         if (a.verify) {
           if (!valid)
@@ -831,22 +886,41 @@ void cksum_kernel(CkArgs a) {
           else
             l4_gate = fold16(s + L.ps) == 0xFFFFu ? 0u : 1u;
         } else {
-          uint32_t ck = 0;
-          if (valid) {
-            ck = (~fold16(s - old + L.ps)) & 0xFFFFu;
-            if (kind == 1 && ck == 0) ck = 0xFFFFu;  // RFC 768
+          if (valid) {  // invalid UDP/TCP lengths write 0
+            l4_new = (~fold16(s - old + L.ps)) & 0xFFFFu;
+            if (kind == 1 && l4_new == 0) l4_new = 0xFFFFu;  // RFC 768
           }
-          const uint32_t at = L.l4_ck;
-          if (at + 2 <= (uint32_t)stride)
-            *reinterpret_cast<uint16_t *>(mine + at) = (uint16_t)ck;
+          l4_wrote = true;
           l4_gate = kind == 1 ? 0u : kGateNone;  // TCP: never emitted
         }
       }
+    }
+    if (ip_wrote || l4_wrote) {
+      // Store the whole 128 B header line first so the checksum words land
+      // in a fully written L2 line (no read-modify-write of a partial line
+      // in HBM), then the words themselves, in the reference's order.
+      uint4 *q = reinterpret_cast<uint4 *>(mine);
+#pragma unroll
+      for (int c = 0; c < kHdrDw / 4; c++)
+        q[c] = make_uint4(h[4 * c], h[4 * c + 1], h[4 * c + 2], h[4 * c + 3]);
+      if (ip_wrote)
+        *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
+      if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
+        *reinterpret_cast<uint16_t *>(mine + L.l4_ck) = (uint16_t)l4_new;
     }
     if (a.ip_gates) a.ip_gates[p0 + lane] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
     if (a.l4_gates) a.l4_gates[p0 + lane] = (uint16_t)l4_gate;
   }
 }
+
+template <bool RELOAD, int DEPTH>
+__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
+void cksum_kernel(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
+
+template <bool RELOAD, int DEPTH>
+__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
+__attribute__((amdgpu_waves_per_eu(5, 8)))
+void cksum_kernel_w5(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
 
 // any stride: frame chunks loaded after the header walk, one frame at a time
 __global__ __launch_bounds__(kCkBlock) void cksum_kernel_generic(CkArgs a) {
@@ -944,9 +1018,24 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const bool tiled = a.stride <= 2048 && !env_int("BG_CK_GENERIC", 0);
-  const void *kern = tiled ? reinterpret_cast<const void *>(cksum_kernel)
-                           : reinterpret_cast<const void *>(cksum_kernel_generic);
+  const bool tiled =
+      a.stride >= 128 && a.stride <= 2048 && !env_int("BG_CK_GENERIC", 0);
+  using CkKern = void (*)(CkArgs);
+  CkKern kfn = cksum_kernel_generic;
+  if (tiled) {
+    // measured on MI355X (scripts/variants.py): re-reading the header line
+    // in phase 3 beats holding it in registers; prefetch depth 2
+    switch (env_int("BG_CK_TILED", 0)) {
+      case 1: kfn = cksum_kernel<false, 1>; break;
+      case 2: kfn = cksum_kernel<true, 1>; break;
+      case 3: kfn = cksum_kernel<true, 3>; break;
+      case 4: kfn = cksum_kernel<false, 2>; break;
+      case 5: kfn = cksum_kernel_w5<true, 2>; break;
+      case 6: kfn = cksum_kernel_w5<true, 3>; break;
+      default: kfn = cksum_kernel<true, 2>; break;
+    }
+  }
+  const void *kern = reinterpret_cast<const void *>(kfn);
   int per_cu = env_int("BG_CK_BLOCKS_PER_CU", 0);
   if (per_cu <= 0) {
     int occ = 0;
@@ -954,7 +1043,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
             hipSuccess ||
         occ <= 0)
       occ = 7;
-    per_cu = occ * std::max(1, env_int("BG_CK_GRID_MULT", 2));
+    per_cu = occ * std::max(1, env_int("BG_CK_GRID_MULT", 4));
   }
   const uint64_t waves_per_block = kCkBlock / 64;
   const uint64_t max_waves = (uint64_t)num_cus * per_cu * waves_per_block;
@@ -968,12 +1057,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
     waves = std::min<uint64_t>(a.n, max_waves);
   }
   const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
-  if (tiled)
-    hipLaunchKernelGGL(cksum_kernel, dim3((unsigned)blocks), dim3(kCkBlock), 0,
-                       s, a);
-  else
-    hipLaunchKernelGGL(cksum_kernel_generic, dim3((unsigned)blocks),
-                       dim3(kCkBlock), 0, s, a);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kCkBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1,0 +1,41 @@
+#!/bin/bash
+# Full GPU session: tests, smoke, bench, rocprofv3 kernel stats + PMC passes.
+# Stops at the first step that ends in anything but success / test failure.
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >> "$OUT/steps.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "== $name rc=$rc" >> "$OUT/steps.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name rc=$rc" >> "$OUT/steps.log"; exit $rc; fi
+  return 0
+}
+MODE=${1:-all}
+if [[ "$MODE" == *tests* ]] || [ "$MODE" = all ]; then
+  step tests 900 python -m pytest tests -m gpu -q -rf --timeout 600
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ "$MODE" == *bench* ]] || [ "$MODE" = all ]; then
+  step bench 900 python bench.py
+fi
+if [[ "$MODE" == *prof* ]] || [ "$MODE" = all ]; then
+  step prof_em 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_em" -o em -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-extra --no-cpu --steps 20 --warmup 5
+  step prof_ck 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_ck" -o ck -- python3 "$GRAFT_REPO_ROOT/bench.py" --only cksum --steps 20 --warmup 3
+  step prof_wm 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_wm" -o wm -- python3 "$GRAFT_REPO_ROOT/bench.py" --only wm --steps 20 --warmup 3
+fi
+if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
+  rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+  i=0
+  for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_HIT_sum TCC_MISS_sum"; do
+    i=$((i+1))
+    for W in em cksum; do
+      if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only cksum --steps 3 --warmup 1"; fi
+      step pmc_${W}_$i 900 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
+    done
+  done
+fi
+echo done >> "$OUT/steps.log"

@@ -21,7 +21,8 @@ from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
-         "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT"]
+         "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
+         "BG_CK_TILED"]
 
 
 def set_env(v):
@@ -31,7 +32,7 @@ def set_env(v):
         os.environ[k] = str(x)
 
 
-def time_variants(fn, variants, rounds=5, reps=10):
+def time_variants(fn, variants, rounds=5, reps=40):
     res = {name: [] for name in variants}
     for _ in range(rounds):
         for name, env in variants.items():
@@ -67,10 +68,8 @@ def main():
         ref = None
         variants = {
             "default": {}, "ppl2": {"BG_PPL": 2},
-            "bpc1": {"BG_BLOCKS_PER_CU": 1}, "bpc3": {"BG_BLOCKS_PER_CU": 3},
-            "bpc4": {"BG_BLOCKS_PER_CU": 4},
-            "ppl2_bpc1": {"BG_PPL": 2, "BG_BLOCKS_PER_CU": 1},
-            "fat_ppl2_bpc2": {"BG_FAT": 1, "BG_PPL": 2, "BG_BLOCKS_PER_CU": 2},
+            "bpc3": {"BG_BLOCKS_PER_CU": 3}, "bpc4": {"BG_BLOCKS_PER_CU": 4},
+            "l2tab": {"BG_NOLDS": 1},
         }
         # every variant must give identical gates
         for name, env in variants.items():
@@ -91,10 +90,12 @@ def main():
         frames = P.cksum_workload(n, frame_len=1496)
         d = torch.from_numpy(frames.reshape(-1)).to(dev)
         l4 = torch.empty(n, dtype=torch.int16, device=dev)
-        variants = {"tiled": {}, "generic": {"BG_CK_GENERIC": 1},
-                    "tiled_x2": {"BG_CK_GRID_MULT": 2},
-                    "tiled_bpc4": {"BG_CK_BLOCKS_PER_CU": 4},
-                    "tiled_bpc2": {"BG_CK_BLOCKS_PER_CU": 2}}
+        variants = {"reload_d2": {}, "generic": {"BG_CK_GENERIC": 1},
+                    "regs_d1": {"BG_CK_TILED": 1}, "reload_d1": {"BG_CK_TILED": 2},
+                    "reload_d3": {"BG_CK_TILED": 3}, "regs_d2": {"BG_CK_TILED": 4},
+                    "w5_d2": {"BG_CK_TILED": 5}, "w5_d3": {"BG_CK_TILED": 6},
+                    "reload_d2_x8": {"BG_CK_GRID_MULT": 8},
+                    "reload_d2_x2": {"BG_CK_GRID_MULT": 2}}
         outs = {}
         for name, env in variants.items():
             dd = torch.from_numpy(frames.reshape(-1)).to(dev)

@@ -91,8 +91,9 @@ def test_em_module_random_traffic_vs_oracle():
         kb = k.tobytes()
         vals = [{"value_bin": kb[a:c]} for a, c in cut]
         # rule values: the masked bytes (value_bin = key-order bytes)
-        mk = [bytes([0xFF]), b"\x00\xff\xff\xff", b"\xff\xff\xff\xff",
-              b"\xff\xff", b"\xff\x0f"]
+        # offset-field value_int masks are taken big-endian (P1)
+        mk = [bytes([0xFF]), b"\xff\xff\xff\x00", b"\xff\xff\xff\xff",
+              b"\xff\xff", b"\x0f\xff"]
         vals = [{"value_bin": bytes(x & y for x, y in zip(v["value_bin"], mm))}
                 for v, mm in zip(vals, mk)]
         m.add(fields=vals, gate=int(g))
