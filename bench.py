@@ -73,14 +73,27 @@ class Timer:
 
 
 def load_traffic(key):
-    """HBM traffic per launch measured with rocprofv3 PMC counters
-    (profiles/traffic.json, written by scripts/pmc_traffic.py)."""
-    p = os.path.join(ROOT, "profiles", "traffic.json")
+    """HBM bytes per launch of the workload's kernel, measured with
+    rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE, gfx950-corrected) and
+    written by scripts/pmc_traffic.py to profiles/rNN_traffic.json; the
+    latest round's file is used."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None
     try:
-        with open(p) as f:
-            return json.load(f).get(key)
+        with open(files[-1]) as f:
+            e = json.load(f).get(key)
     except (OSError, ValueError):
         return None
+    return None if e is None else e.get("traffic_bytes")
+
+
+def traffic_gbs(key, kernel_ms):
+    """PMC bytes per launch / measured launch duration, in GB/s (same basis
+    as roofline.achieved); None until profiles/ holds a PMC measurement."""
+    b = load_traffic(key)
+    return None if b is None else round(b / (kernel_ms * 1e-3) / 1e9, 1)
 
 
 def em_setup(args, rank, world, dev, torch, dist):
@@ -192,6 +205,8 @@ def run_em(args, rank, world, dev, torch, dist):
 
     # parity first: the host-side check leaves the GPU idle for seconds,
     # so the warmup that follows brings the clocks back up before timing
+    step()
+    torch.cuda.synchronize()
     parity = em_parity_sample(t, d_frames, d_gates, keys, gates,
                               min(n, 1 << 20), torch)
     for _ in range(args.warmup):
@@ -224,34 +239,48 @@ def run_em(args, rank, world, dev, torch, dist):
 
 def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
     """Per-launch batch-size sweep (SURVEY C2 'batch 32->4096'): each batch
-    of B packets is one kernel launch; 512 consecutive launches are captured
-    in a HIP graph and replayed, so the number is the device-side cost of
-    B-packet launches without host launch overhead."""
+    of B packets is one kernel launch, 512 batches per measurement.
+      stream: back-to-back bg_em_classify calls on one stream (host launch
+              cost included: what one BESS worker issuing B-packet batches
+              sees);
+      graph:  the 512 launches captured in a HIP graph and replayed (no
+              host cost; the runtime may overlap independent launches)."""
     t, d_frames, d_gates = r["t"], r["d_frames"], r["d_gates"]
-    out = {}
+    out = {"stream": {}, "graph": {}}
     s = torch.cuda.Stream()
-    for B in batches:
-        nl = 512
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
-            torch.cuda.synchronize()
-            with torch.cuda.graph(g, stream=s):
-                for j in range(nl):
-                    off = j * B
-                    t.classify(d_frames[off * 64:], 64, B, 8192,
-                               d_gates[off:], stream=s)
-        g.replay()
-        torch.cuda.synchronize()
-        reps = 5
+    nl = 512
+
+    def launches(B):
+        for j in range(nl):
+            off = j * B
+            t.classify(d_frames[off * 64:], 64, B, 8192, d_gates[off:],
+                       stream=s)
+
+    def timed(fn, reps=5):
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(s)
         for _ in range(reps):
-            g.replay()
+            fn()
         b.record(s)
         b.synchronize()
-        ms = a.elapsed_time(b) / reps
-        out[str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
+        return a.elapsed_time(b) / reps
+
+    for B in batches:
+        with torch.cuda.stream(s):
+            launches(B)
+            torch.cuda.synchronize()
+            ms = timed(lambda: launches(B))
+        out["stream"][str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                launches(B)
+        g.replay()
+        torch.cuda.synchronize()
+        ms = timed(g.replay)
+        out["graph"][str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
     return out
 
 
@@ -289,7 +318,8 @@ def run_cksum(args, dev, torch):
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic("cksum")},
+                         "traffic": traffic_gbs("cksum", ms),
+                         "traffic_bytes_per_launch": load_traffic("cksum")},
             "parity": parity}
 
 
@@ -361,7 +391,8 @@ def run_wm(args, dev, torch):
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic("wm")}}
+                         "traffic": traffic_gbs("wm", ms),
+                         "traffic_bytes_per_launch": load_traffic("wm")}}
 
 
 def main():
@@ -411,8 +442,11 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic("em_%d" % args.rules),
-                     "kernel": "em_classify_kernel<2>",
+                     "traffic": traffic_gbs("em", kern_ms)
+                     if args.rules == 1000 and r["n"] == 16 << 20 else None,
+                     "traffic_bytes_per_launch": load_traffic("em")
+                     if args.rules == 1000 and r["n"] == 16 << 20 else None,
+                     "kernel": "em_classify_kernel",
                      "kernel_ms": round(kern_ms, 4),
                      "bytes_per_pkt": EM_BYTES_PER_PKT},
         "parity": "bit-exact vs oracle on 1M-pkt sample" if r["parity"]

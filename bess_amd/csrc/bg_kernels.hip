@@ -949,31 +949,44 @@ int env_int(const char *name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
+// Packets per workgroup below which staging the table into LDS costs more
+// than probing it in L2 (a 40 KB table fill vs. 64 B of header per packet).
+constexpr uint64_t kLdsMinPktsPerBlock = 4096;
+
 template <typename Args, typename K>
 hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
                            int ppl) {
   if (a.n == 0) return hipSuccess;
   if (env_int("BG_NOLDS", 0)) a.t.lds = 0;
-  const size_t lds = a.t.lds ? a.t.bytes_total : 0;
+  const uint64_t need = (a.n + (uint64_t)kEmBlock * ppl - 1) / ((uint64_t)kEmBlock * ppl);
   // Measured on MI355X (scripts/variants.py): with the table in LDS two
   // 512-thread blocks per CU (16 waves) stream fastest -- fewer LDS table
   // fills; with the table in L2/MALL, twice the resident grid.
   int per_cu = env_int("BG_BLOCKS_PER_CU", 0);
-  if (per_cu <= 0) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(kernel), kEmBlock, lds) !=
-            hipSuccess ||
-        occ <= 0)
-      occ = 2;
-    per_cu = a.t.lds ? std::min(occ, 2) : occ * 2;
-    per_cu *= std::max(1, env_int("BG_GRID_MULT", 1));
+  for (int pass = 0; pass < 2; pass++) {
+    const size_t lds = a.t.lds ? a.t.bytes_total : 0;
+    int pc = per_cu;
+    if (pc <= 0) {
+      int occ = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &occ, reinterpret_cast<const void *>(kernel), kEmBlock, lds) !=
+              hipSuccess ||
+          occ <= 0)
+        occ = 2;
+      pc = a.t.lds ? std::min(occ, 2) : occ * 2;
+      pc *= std::max(1, env_int("BG_GRID_MULT", 1));
+    }
+    const uint64_t cap = (uint64_t)num_cus * pc;
+    const uint64_t blocks = need > cap ? cap : need;
+    if (a.t.lds && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
+        !env_int("BG_FORCE_LDS", 0)) {
+      a.t.lds = 0;  // small launch: probe the table in L2 instead
+      continue;
+    }
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kEmBlock), lds, s, a);
+    return hipGetLastError();
   }
-  uint64_t blocks = (a.n + (uint64_t)kEmBlock * ppl - 1) / ((uint64_t)kEmBlock * ppl);
-  const uint64_t cap = (uint64_t)num_cus * per_cu;
-  if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kEmBlock), lds, s, a);
-  return hipGetLastError();
+  return hipErrorInvalidValue;
 }
 
 template <template <int, int, int> class Sel, typename Args>

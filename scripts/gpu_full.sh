@@ -23,19 +23,19 @@ if [[ "$MODE" == *bench* ]] || [ "$MODE" = all ]; then
   step bench 900 python bench.py
 fi
 if [[ "$MODE" == *prof* ]] || [ "$MODE" = all ]; then
-  step prof_em 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_em" -o em -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-extra --no-cpu --steps 20 --warmup 5
-  step prof_ck 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_ck" -o ck -- python3 "$GRAFT_REPO_ROOT/bench.py" --only cksum --steps 20 --warmup 3
-  step prof_wm 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_wm" -o wm -- python3 "$GRAFT_REPO_ROOT/bench.py" --only wm --steps 20 --warmup 3
+  # kernel trace of the default bench command (every kernel of the line)
+  step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py"
 fi
 if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
   rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
   i=0
-  for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_HIT_sum TCC_MISS_sum"; do
+  for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
     i=$((i+1))
-    for W in em cksum; do
-      if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only cksum --steps 3 --warmup 1"; fi
+    for W in em cksum wm; do
+      if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --steps 3 --warmup 1"; fi
       step pmc_${W}_$i 900 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
     done
   done
+  python3 scripts/pmc_traffic.py "$OUT" "$OUT/traffic.json" > "$OUT/pmc_traffic.out" 2>&1 || true
 fi
 echo done >> "$OUT/steps.log"

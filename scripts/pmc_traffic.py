@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from rocprofv3 --pmc passes (scripts/gpu_full.sh).
+
+    python scripts/pmc_traffic.py gpurun_out profiles/r01_traffic.json
+
+Reads every counter_collection.csv under gpurun_out/pmc_<workload>_<i>/,
+averages each counter over the dispatches of the workload's kernel and
+applies MI355X_MICROARCH.md's gfx950 corrections:
+  * FETCH_SIZE (KB) reports 1/2 of the bytes of wide streaming reads
+    (FETCH_SIZE = TCC_EA0_RDREQ x 64 B for 128 B requests) -> doubled;
+  * WRITE_SIZE (KB) is exact for 16 B/lane stores.
+traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 bytes per launch.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = {"em": "em_classify_kernel", "cksum": "cksum_kernel",
+           "wm": "wm_classify_kernel"}
+ALGO = {"em": 66 * (16 << 20), "cksum": 1502 * (1 << 20),
+        "wm": 66 * (1 << 20)}
+
+
+def collect(root, wl):
+    vals = defaultdict(list)
+    for p in glob.glob(os.path.join(root, "pmc_%s_*" % wl, "**", "*counter_collection.csv"),
+                       recursive=True):
+        per = defaultdict(float)  # (dispatch, counter) -> value
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                if KERNELS[wl] not in r["Kernel_Name"]:
+                    continue
+                per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (d, c), v in per.items():
+            vals[c].append(v)
+    return {c: sum(v) / len(v) for c, v in vals.items() if v}
+
+
+def main():
+    root, out = sys.argv[1], sys.argv[2]
+    res = {}
+    for wl in KERNELS:
+        c = collect(root, wl)
+        if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+            continue
+        fetch = 2 * c["FETCH_SIZE"] * 1024
+        write = c["WRITE_SIZE"] * 1024
+        e = {"traffic_bytes": round(fetch + write),
+             "fetch_bytes_corrected": round(fetch),
+             "write_bytes": round(write),
+             "algorithmic_bytes": ALGO[wl],
+             "traffic_over_algorithmic": round((fetch + write) / ALGO[wl], 4),
+             "raw": {k: round(v, 1) for k, v in c.items()}}
+        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+            e["l2_hit_rate"] = round(c["TCC_HIT_sum"] /
+                                     max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
+        res[wl] = e
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,34 @@ def to_dev(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).to(dev)
 
 
+# launcher choices of where the table is probed: its own (LDS for tables
+# <= 40 KB on launches with >= 4096 packets per workgroup, else L2), forced
+# LDS, forced L2 (BG_* knobs of bg_kernels.hip)
+TABLE_PATHS = ({}, {"BG_FORCE_LDS": "1"}, {"BG_NOLDS": "1"})
+
+
+def classify_all_paths(t, d_frames, stride, n, default_gate, dev):
+    """Gates from every table path; asserts they agree, returns them."""
+    outs = []
+    for env in TABLE_PATHS:
+        old = {k: os.environ.get(k) for k in ("BG_FORCE_LDS", "BG_NOLDS")}
+        os.environ.update(env)
+        try:
+            d_g = torch.zeros(n, dtype=torch.int16, device=dev)
+            t.classify(d_frames, stride, n, default_gate, d_g)
+            torch.cuda.synchronize()
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        outs.append(d_g.cpu().numpy().view(np.uint16))
+    for o, env in zip(outs[1:], TABLE_PATHS[1:]):
+        assert (o == outs[0]).all(), env
+    return outs[0]
+
+
 def oracle_em(fields, keys, gates):
     """fields: [(offset, size, mask)] resolved; keys: (n, key_size) u8."""
     L = O.lib()
@@ -54,11 +82,8 @@ def em_compare(fields, keys, gates, frames, stride, default_gate, dev):
     n = frames.shape[0]
     t = F.EmTable(fields)
     t.add_many(keys, gates)
-    d_frames = to_dev(frames, dev)
-    d_gates = torch.zeros(n, dtype=torch.int16, device=dev)
-    t.classify(d_frames, stride, n, default_gate, d_gates)
-    torch.cuda.synchronize()
-    got = d_gates.cpu().numpy().view(np.uint16)
+    got = classify_all_paths(t, to_dev(frames, dev), stride, n, default_gate,
+                             dev)
     em = oracle_em(fields, keys, gates)
     want = np.zeros(n, np.uint16)
     O.lib().or_em_process(em, frames.ctypes.data, stride, n, default_gate,
@@ -226,9 +251,7 @@ def test_wm_vs_oracle(n_rules, n_pkts, dev):
     for k, m, p, g in zip(rk, rm, prio, gates):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
     assert t.num_tuples() == 8
-    d_g = torch.zeros(n_pkts, dtype=torch.int16, device=dev)
-    t.classify(to_dev(frames, dev), 64, n_pkts, 77, d_g)
-    got = d_g.cpu().numpy().view(np.uint16)
+    got = classify_all_paths(t, to_dev(frames, dev), 64, n_pkts, 77, dev)
     wm = oracle_wm(P.FIVE_TUPLE, rk, rm, prio, gates)
     want = np.zeros(n_pkts, np.uint16)
     O.lib().or_wm_process(wm, frames.ctypes.data, 64, n_pkts, 77,
