@@ -250,11 +250,18 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
     s = torch.cuda.Stream()
     nl = 512
 
-    def launches(B):
+    import ctypes as C
+    from bess_amd import lib
+    classify = lib().bg_em_classify
+    fp, gp, sp = d_frames.data_ptr(), d_gates.data_ptr(), C.c_void_p(s.cuda_stream)
+
+    def launches(B):  # straight C-ABI calls: no per-launch tensor slicing
         for j in range(nl):
             off = j * B
-            t.classify(d_frames[off * 64:], 64, B, 8192, d_gates[off:],
-                       stream=s)
+            rc = classify(t.h, C.c_void_p(fp + off * 64), 64, B, 8192,
+                          C.c_void_p(gp + off * 2), sp)
+            if rc:
+                raise RuntimeError("bg_em_classify failed: %d" % rc)
 
     def timed(fn, reps=5):
         a = torch.cuda.Event(enable_timing=True)

@@ -53,11 +53,16 @@ int num_cus(int device) {
 }
 
 int set_device(int device) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
-    return fail(ENODEV, "no HIP device available");
+  // launch path: one cached count and a thread-local current-device check
+  static const int n = [] {
+    int c = 0;
+    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+  }();
+  if (n <= 0) return fail(ENODEV, "no HIP device available");
   if (device < 0 || device >= n)
     return fail(ENODEV, "device %d out of range [0,%d)", device, n);
+  int cur = -1;
+  if (hipGetDevice(&cur) == hipSuccess && cur == device) return 0;
   HIP_TRY(hipSetDevice(device));
   return 0;
 }
@@ -156,8 +161,11 @@ TableRef DevTable::ref() const {
   t.nparts = L.nparts;
   t.nbp = L.nbp;
   t.kw = L.kw;
-  t.bytes_total = (uint32_t)std::min<uint64_t>(bytes, 0xFFFFFFFFu);
-  t.lds = bytes <= kLdsTableMax ? 1u : 0u;
+  const uint64_t tb = filt_words ? filt_off : bytes;
+  t.bytes_total = (uint32_t)std::min<uint64_t>(tb, 0xFFFFFFFFu);
+  t.filt_words = filt_words;
+  t.filt_off = filt_off;
+  t.lds = tb <= kLdsTableMax ? kLdsTable : (filt_words ? kLdsFilter : kLdsNone);
   return t;
 }
 
@@ -712,8 +720,34 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   TableLayout L;
   int r = build_image(wm->kw, 8, 1, keys, vals, seeds, &img, &L);
   if (r) return r;
+  // Tables too big for LDS get a blocked Bloom filter (up to 16 bits per
+  // key, 64 KB by default so two workgroups fit a CU -- measured faster
+  // than 128 KB at one workgroup per CU) that the kernel stages in LDS.
+  uint32_t fw = 0;
+  const size_t nkeys = seeds.size();
+  const char *ekb = getenv("BG_WM_FILTER_KB");  // A/B knob (variants.py)
+  const int kb = (ekb && *ekb) ? atoi(ekb) : 64;
+  if (img.size() > kLdsTableMax && kb > 0 && nkeys > 0) {
+    const uint32_t cap = std::min<uint32_t>(kFilterMaxWords, (uint32_t)kb * 256);
+    fw = 1024;
+    while (fw < cap && (uint64_t)fw * 32 < (uint64_t)nkeys * 16) fw *= 2;
+    if ((uint64_t)fw * 32 < (uint64_t)nkeys * 4) fw = 0;  // < 4 bits/key
+  }
+  uint64_t foff = 0;
+  if (fw) {
+    foff = align256(img.size());
+    img.resize(foff + (uint64_t)fw * 4, 0);
+    uint32_t *f = reinterpret_cast<uint32_t *>(img.data() + foff);
+    for (size_t i = 0; i < nkeys; i++) {
+      const FilterProbe q =
+          filter_probe(hash_words(&keys[i * wm->kw], (int)wm->kw, seeds[i]), fw);
+      f[q.word] |= q.bits;
+    }
+  }
   r = wm->dev.upload(device, img, L, s);
   if (r) return r;
+  wm->dev.filt_off = foff;
+  wm->dev.filt_words = fw;
   wm->dirty = false;
   return 0;
 }
@@ -792,7 +826,7 @@ int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
 int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds) {
   if (!wm->dev.valid) return fail(EINVAL, "no device table yet");
   *bytes = wm->dev.bytes;
-  *in_lds = wm->dev.ref().lds ? 1 : 0;
+  *in_lds = (int)wm->dev.ref().lds;  // 2: key filter in LDS
   return 0;
 }
 

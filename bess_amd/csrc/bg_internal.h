@@ -55,6 +55,8 @@ struct DevTable {
   uint64_t bytes = 0;
   TableLayout L{};
   bool valid = false;
+  uint64_t filt_off = 0;    // key filter appended to the image (WM)
+  uint32_t filt_words = 0;
   int upload(int dev, const std::vector<uint8_t> &img, const TableLayout &lay,
              hipStream_t s);
   void release();

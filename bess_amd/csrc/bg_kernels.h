@@ -41,12 +41,19 @@ BG_HD int fspec_shift_bits(uint32_t s) { return (int)((s >> 9) & 3) * 8; }
 BG_HD int fspec_pos(uint32_t s) { return (int)((s >> 11) & 0x3F); }
 BG_HD int fspec_nd(uint32_t s) { return (int)((s >> 17) & 3); }
 
+// TableRef::lds values
+constexpr uint32_t kLdsNone = 0;    // table probed in L2 / MALL
+constexpr uint32_t kLdsTable = 1;   // whole image copied into LDS
+constexpr uint32_t kLdsFilter = 2;  // only the key filter copied into LDS
+constexpr uint32_t kFilterMaxWords = 32768;  // 128 KB of LDS
+
 struct TableRef {
-  const uint8_t *base;  // device image (nparts * part_bytes)
+  const uint8_t *base;  // device image (nparts * part_bytes [+ filter])
   uint64_t part_bytes, keys_off, vals_off, seed;
-  uint32_t nparts, nbp, kw, lds;  // lds: copy the image into LDS first
-  uint32_t bytes_total;           // image bytes (LDS copy length)
-  uint32_t pad;
+  uint32_t nparts, nbp, kw, lds;  // lds: kLds* above
+  uint32_t bytes_total;           // table bytes (LDS copy length)
+  uint32_t filt_words;            // 0: no filter
+  uint64_t filt_off;              // byte offset of the filter in the image
 };
 
 struct EmArgs {

@@ -8,6 +8,9 @@
 // All integer work; HBM-bound streaming over resident packet slabs (frame i
 // at frames + i*stride). No MFMA: there is no contraction on this path.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
 #include <limits.h>
 #include <stdlib.h>
 
@@ -177,47 +180,47 @@ __device__ __forceinline__ bool key_eq(const uint8_t *slot_key,
   }
 }
 
-// Probe one key. Returns the slot index (bucket*4+s) of the match inside
-// partition image `pb`, or -1. `tab` is either the global image or its LDS
+// Look one key up: the two tag words, then for each fingerprint match the
+// slot's key AND value, loaded together (one dependent round trip per
+// candidate instead of two). `tab` is either the global image or its LDS
 // copy; inlined separately for each so address spaces stay concrete.
-template <int KW>
-__device__ __forceinline__ int probe(const uint8_t *tab, const TableRef &t,
-                                     const uint64_t (&k)[KW], uint64_t seed,
-                                     const uint8_t **pb_out) {
-  const uint64_t h = hash_words(k, KW, seed);
-  const Probe p = split_hash(h, t.nparts, t.nbp);
-  const uint8_t *pb = tab + (uint64_t)p.part * t.part_bytes;
-  *pb_out = pb;
-  const uint32_t *tags = reinterpret_cast<const uint32_t *>(pb);
-  uint32_t cand = tag_match(tags[p.b1], p.tag) |
-                  (tag_match(tags[p.b2], p.tag) << 4);
-  while (cand) {
-    const int s = __builtin_ctz(cand);
-    cand &= cand - 1;
-    const uint32_t slot = (s < 4 ? p.b1 : p.b2) * kSlots + (s & 3);
-    if (key_eq<KW>(pb + t.keys_off + (uint64_t)slot * KW * 8, k)) return (int)slot;
-  }
-  return -1;
-}
-
 template <int KW>
 __device__ __forceinline__ uint32_t em_lookup(const uint8_t *tab,
                                               const TableRef &t,
                                               const uint64_t (&k)[KW],
                                               uint32_t dflt) {
-  const uint8_t *pb;
-  int slot = probe<KW>(tab, t, k, t.seed, &pb);
-  if (slot < 0) return dflt;
-  return reinterpret_cast<const uint16_t *>(pb + t.vals_off)[slot];
+  const uint64_t h = hash_words(k, KW, t.seed);
+  const Probe p = split_hash(h, t.nparts, t.nbp);
+  const uint8_t *pb = tab + (uint64_t)p.part * t.part_bytes;
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(pb);
+  uint32_t cand = tag_match(tags[p.b1], p.tag) |
+                  (tag_match(tags[p.b2], p.tag) << 4);
+  const uint16_t *vals = reinterpret_cast<const uint16_t *>(pb + t.vals_off);
+  while (cand) {
+    const int s = __builtin_ctz(cand);
+    cand &= cand - 1;
+    const uint32_t slot = (s < 4 ? p.b1 : p.b2) * kSlots + (s & 3);
+    const uint32_t v = vals[slot];
+    if (key_eq<KW>(pb + t.keys_off + (uint64_t)slot * KW * 8, k)) return v;
+  }
+  return dflt;
+}
+
+__device__ __forceinline__ void copy_to_lds(uint8_t *lds, const uint8_t *g,
+                                            uint32_t bytes) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(g);
+  uint4 *dst = reinterpret_cast<uint4 *>(lds);
+  for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x)
+    dst[i] = src[i];
+  __syncthreads();
 }
 
 __device__ __forceinline__ void copy_table_to_lds(uint8_t *lds,
                                                   const TableRef &t) {
-  const uint4 *src = reinterpret_cast<const uint4 *>(t.base);
-  uint4 *dst = reinterpret_cast<uint4 *>(lds);
-  for (uint32_t i = threadIdx.x; i < t.bytes_total / 16; i += blockDim.x)
-    dst[i] = src[i];
-  __syncthreads();
+  if (t.lds == kLdsTable)
+    copy_to_lds(lds, t.base, t.bytes_total);
+  else if (t.lds == kLdsFilter)
+    copy_to_lds(lds, t.base + t.filt_off, t.filt_words * 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -236,7 +239,7 @@ __device__ __forceinline__ void em_body(const EmArgs &a, uint8_t *lds) {
     for (int j = 0; j < PPL; j++) {
       const uint64_t idx = base + (uint64_t)j * blockDim.x;
       uint32_t g;
-      if (a.t.lds)
+      if (a.t.lds == kLdsTable)
         g = em_lookup<KW>(lds, a.t, k[j], a.default_gate);
       else
         g = em_lookup<KW>(a.t.base, a.t, k[j], a.default_gate);
@@ -266,28 +269,63 @@ __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
 // the best (priority, later-tuple-on-tie) entry wins (LookupEntry 136-157).
 // ---------------------------------------------------------------------------
 template <int KW>
-__device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
-                                              const WmArgs &a,
-                                              const uint64_t (&k)[KW]) {
-  // Issue every tuple's two tag-word reads before resolving any of them:
-  // up to 16 independent table reads in flight per lane. (The WildcardMatch
-  // table has a single partition.)
-  uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples], w1[kMaxTuples],
-      w2[kMaxTuples];
+__device__ __forceinline__ void load_key(const uint8_t *p, uint64_t (&o)[KW]) {
+  if constexpr (KW % 2 == 0) {
+    const uint4 *s = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+    for (int j = 0; j < KW / 2; j++) {
+      const uint4 v = s[j];
+      o[2 * j] = (uint64_t)v.y << 32 | v.x;
+      o[2 * j + 1] = (uint64_t)v.w << 32 | v.z;
+    }
+  } else {
+    const uint64_t *s = reinterpret_cast<const uint64_t *>(p);
+#pragma unroll
+    for (int j = 0; j < KW; j++) o[j] = s[j];
+  }
+}
+
+// WildcardMatch entry value: priority | gate << 32 | tuple << 48. A slot
+// matches tuple `tu` when its tuple field is tu and its key is k & mask.
+template <int KW>
+__device__ __forceinline__ bool wm_slot_hit(uint64_t v, const uint64_t (&sk)[KW],
+                                            const uint64_t (&km)[KW], int tu) {
+  bool eq = (uint32_t)(v >> 48) == (uint32_t)tu;
+#pragma unroll
+  for (int j = 0; j < KW; j++) eq &= sk[j] == km[j];
+  return eq;
+}
+
+// Round-1 lookup (A/B baseline, BG_WM_V=1): tag reads batched over all
+// tuples, then each tuple's candidates probed in turn (value, then key).
+template <int KW, bool FILT>
+__device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
+                                                  const WmArgs &a,
+                                                  const uint64_t (&k)[KW],
+                                                  const uint32_t *filt) {
+  uint64_t hs[kMaxTuples];
+  uint32_t w1[kMaxTuples], w2[kMaxTuples];
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
+    hs[tu] = 0;
+    w1[tu] = w2[tu] = 0;
     if (tu < (int)a.ntuples) {
       uint64_t km[KW];
 #pragma unroll
       for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
-      const Probe p = split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)),
-                                 1, a.t.nbp);
-      b1[tu] = p.b1;
-      b2[tu] = p.b2;
-      tg[tu] = p.tag;
-      w1[tu] = tags[p.b1];
-      w2[tu] = tags[p.b2];
+      const uint64_t h = hash_words(km, KW, tuple_seed(a.t.seed, tu));
+      hs[tu] = h;
+      bool pass = true;
+      if (FILT) {
+        const FilterProbe q = filter_probe(h, a.t.filt_words);
+        pass = (filt[q.word] & q.bits) == q.bits;
+      }
+      if (pass) {
+        const Probe p = split_hash(h, 1, a.t.nbp);
+        w1[tu] = tags[p.b1];
+        w2[tu] = tags[p.b2];
+      }
     }
   }
   int32_t best = INT_MIN;
@@ -295,11 +333,12 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
     if (tu < (int)a.ntuples) {
-      uint32_t cand = tag_match(w1[tu], tg[tu]) | (tag_match(w2[tu], tg[tu]) << 4);
+      const Probe p = split_hash(hs[tu], 1, a.t.nbp);
+      uint32_t cand = tag_match(w1[tu], p.tag) | (tag_match(w2[tu], p.tag) << 4);
       while (cand) {
         const int sl = __builtin_ctz(cand);
         cand &= cand - 1;
-        const uint32_t slot = (sl < 4 ? b1[tu] : b2[tu]) * kSlots + (sl & 3);
+        const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
         const uint64_t v =
             reinterpret_cast<const uint64_t *>(tab + a.t.vals_off)[slot];
         if ((uint32_t)(v >> 48) != (uint32_t)tu) continue;
@@ -308,7 +347,7 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
         for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
         if (key_eq<KW>(tab + a.t.keys_off + (uint64_t)slot * KW * 8, km)) {
           const int32_t prio = (int32_t)(uint32_t)v;
-          if (prio >= best) {  // '>=': the later tuple wins a tie (P5)
+          if (prio >= best) {
             best = prio;
             gate = (uint32_t)(v >> 32) & 0xFFFFu;
           }
@@ -320,10 +359,124 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
   return gate;
 }
 
-template <int KW, int NCH, int PPL>
-__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80))) void wm_classify_kernel(WmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  if (a.t.lds) copy_table_to_lds(lds, a.t);
+template <int KW, bool FILT, int G>
+__device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
+                                              const WmArgs &a,
+                                              const uint64_t (&k)[KW],
+                                              const uint32_t *filt) {
+  // Three batched rounds, each issuing every tuple's reads before any is
+  // consumed (the WildcardMatch table has a single partition):
+  //   A. hash per tuple, LDS key filter, both tag words (<= 16 loads);
+  //   B. for each tuple's first fingerprint match, its key and value;
+  //   C. resolve in tuple order (LookupEntry order, '>=' tie-break);
+  //      further fingerprint matches of a tuple (rare) are probed there.
+  uint32_t w1[kMaxTuples], w2[kMaxTuples];
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
+  const uint8_t *keys = tab + a.t.keys_off;
+#pragma unroll
+  for (int tu = 0; tu < kMaxTuples; tu++) {
+    w1[tu] = w2[tu] = 0;  // 0: four empty slots
+    if (tu < (int)a.ntuples) {
+      uint64_t km[KW];
+#pragma unroll
+      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      const uint64_t h = hash_words(km, KW, tuple_seed(a.t.seed, tu));
+      bool pass = true;
+      if (FILT) {  // key filter in LDS: skip tuples that cannot match
+        const FilterProbe q = filter_probe(h, a.t.filt_words);
+        pass = (filt[q.word] & q.bits) == q.bits;
+      }
+      if (pass) {
+        const Probe p = split_hash(h, 1, a.t.nbp);
+        w1[tu] = tags[p.b1];
+        w2[tu] = tags[p.b2];
+      }
+    }
+  }
+  int32_t best = INT_MIN;
+  uint32_t gate = a.default_gate;
+  // rounds B and C run over groups of G tuples (register budget)
+#pragma unroll
+  for (int g0 = 0; g0 < kMaxTuples; g0 += G) {
+  // cand: bit 8 = the tuple had a fingerprint match, bits 0-7 = the
+  // matches not yet probed (bits 0-3 bucket b1's slots, 4-7 bucket b2's)
+  uint32_t cand[G];
+  uint64_t v1[G], sk1[G][KW];
+#pragma unroll
+  for (int gi = 0; gi < G; gi++) {
+    const int tu = g0 + gi;
+    cand[gi] = 0;
+    v1[gi] = 0;
+#pragma unroll
+    for (int j = 0; j < KW; j++) sk1[gi][j] = 0;
+    if (tu < (int)a.ntuples && (w1[tu] | w2[tu])) {
+      uint64_t km[KW];
+#pragma unroll
+      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      const Probe p =
+          split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)), 1, a.t.nbp);
+      uint32_t c = tag_match(w1[tu], p.tag) | (tag_match(w2[tu], p.tag) << 4);
+      if (c) {
+        const int sl = __builtin_ctz(c);
+        const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
+        v1[gi] = vals[slot];
+        load_key<KW>(keys + (uint64_t)slot * KW * 8, sk1[gi]);
+        cand[gi] = 0x100u | (c & (c - 1));
+      }
+    }
+  }
+#pragma unroll
+  for (int gi = 0; gi < G; gi++) {
+    const int tu = g0 + gi;
+    if (tu < (int)a.ntuples && (cand[gi] & 0x100u)) {
+      uint64_t km[KW];
+#pragma unroll
+      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      bool hit = wm_slot_hit<KW>(v1[gi], sk1[gi], km, tu);
+      uint64_t v = v1[gi];
+      uint32_t c = cand[gi] & 0xFFu;
+      if (!hit && c) {  // another fingerprint match in this tuple (rare)
+        const Probe p = split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)),
+                                   1, a.t.nbp);
+        while (c && !hit) {
+          const int sl = __builtin_ctz(c);
+          c &= c - 1;
+          const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
+          uint64_t sk[KW];
+          v = vals[slot];
+          load_key<KW>(keys + (uint64_t)slot * KW * 8, sk);
+          hit = wm_slot_hit<KW>(v, sk, km, tu);
+        }
+      }
+      if (hit) {
+        const int32_t prio = (int32_t)(uint32_t)v;
+        if (prio >= best) {  // '>=': the later tuple wins a tie (P5)
+          best = prio;
+          gate = (uint32_t)(v >> 32) & 0xFFFFu;
+        }
+      }
+    }
+  }
+  }
+  return gate;
+}
+
+// lookup variant: V 1 = wm_lookup_seq, 2 = batched rounds over groups of G
+template <int KW, bool FILT, int V, int G>
+__device__ __forceinline__ uint32_t wm_lookup_v(const uint8_t *tab,
+                                                const WmArgs &a,
+                                                const uint64_t (&k)[KW],
+                                                const uint32_t *filt) {
+  if constexpr (V == 1)
+    return wm_lookup_seq<KW, FILT>(tab, a, k, filt);
+  else
+    return wm_lookup<KW, FILT, G>(tab, a, k, filt);
+}
+
+template <int KW, int NCH, int PPL, int V, int G>
+__device__ __forceinline__ void wm_body(const WmArgs &a, uint8_t *lds) {
+  copy_table_to_lds(lds, a.t);
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x * PPL;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * PPL + threadIdx.x;
        base < a.n; base += step) {
@@ -333,13 +486,31 @@ __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80))) void
     for (int j = 0; j < PPL; j++) {
       const uint64_t idx = base + (uint64_t)j * blockDim.x;
       uint32_t g;
-      if (a.t.lds)
-        g = wm_lookup<KW>(lds, a, k[j]);
+      if (a.t.lds == kLdsTable)
+        g = wm_lookup_v<KW, false, V, G>(lds, a, k[j], nullptr);
+      else if (a.t.lds == kLdsFilter)
+        g = wm_lookup_v<KW, true, V, G>(a.t.base, a, k[j],
+                                        reinterpret_cast<const uint32_t *>(lds));
       else
-        g = wm_lookup<KW>(a.t.base, a, k[j]);
+        g = wm_lookup_v<KW, false, V, G>(a.t.base, a, k[j], nullptr);
       if (idx < a.n) a.gates[idx] = (uint16_t)g;
     }
   }
+}
+
+template <int KW, int NCH, int PPL>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
+void wm_classify_kernel(WmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  wm_body<KW, NCH, PPL, 2, 4>(a, lds);
+}
+
+// A/B variants for the 5-tuple shape (BG_WM_V / BG_WM_G)
+template <int PPL, int V, int G>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
+void wm_classify_exp_kernel(WmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  wm_body<2, 2, PPL, V, G>(a, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -953,6 +1124,28 @@ int env_int(const char *name, int dflt) {
 // than probing it in L2 (a 40 KB table fill vs. 64 B of header per packet).
 constexpr uint64_t kLdsMinPktsPerBlock = 4096;
 
+// hipOccupancyMaxActiveBlocksPerMultiprocessor, memoised per (kernel, LDS
+// bytes, block) -- it is not free and the answer never changes
+int occupancy(const void *kernel, int block, size_t lds, int dflt) {
+  struct Ent {
+    const void *k;
+    size_t lds;
+    int block, occ;
+  };
+  static std::mutex mu;
+  static std::vector<Ent> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Ent &e : cache)
+    if (e.k == kernel && e.lds == lds && e.block == block) return e.occ;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, lds) !=
+          hipSuccess ||
+      occ <= 0)
+    occ = dflt;
+  cache.push_back({kernel, lds, block, occ});
+  return occ;
+}
+
 template <typename Args, typename K>
 hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
                            int ppl) {
@@ -964,15 +1157,13 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
   // fills; with the table in L2/MALL, twice the resident grid.
   int per_cu = env_int("BG_BLOCKS_PER_CU", 0);
   for (int pass = 0; pass < 2; pass++) {
-    const size_t lds = a.t.lds ? a.t.bytes_total : 0;
+    const size_t lds = a.t.lds == kLdsTable    ? a.t.bytes_total
+                       : a.t.lds == kLdsFilter ? (size_t)a.t.filt_words * 4
+                                               : 0;
     int pc = per_cu;
     if (pc <= 0) {
-      int occ = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &occ, reinterpret_cast<const void *>(kernel), kEmBlock, lds) !=
-              hipSuccess ||
-          occ <= 0)
-        occ = 2;
+      const int occ =
+          occupancy(reinterpret_cast<const void *>(kernel), kEmBlock, lds, 2);
       pc = a.t.lds ? std::min(occ, 2) : occ * 2;
       pc *= std::max(1, env_int("BG_GRID_MULT", 1));
     }
@@ -990,9 +1181,9 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
 }
 
 template <template <int, int, int> class Sel, typename Args>
-hipError_t dispatch(const Args &a, int num_cus, hipStream_t s) {
+hipError_t dispatch(const Args &a, int num_cus, hipStream_t s, int dflt_ppl) {
   const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 ? 2 : 4);
-  const int ppl = env_int("BG_PPL", kDefaultPpl);
+  const int ppl = env_int("BG_PPL", dflt_ppl);
 #define BG_CASE(KW, NCH, PPL)                                                   \
   if (a.t.kw == KW && nch == NCH && ppl == PPL)                                 \
     return launch_classify(Sel<KW, NCH, PPL>::kernel(), a, num_cus, s, PPL);
@@ -1022,11 +1213,24 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
       return launch_classify(em_classify_fat_kernel<2, 2, 2>, a, num_cus, s, 2);
     return launch_classify(em_classify_fat_kernel<2, 2, 1>, a, num_cus, s, 1);
   }
-  return dispatch<EmSel>(a, num_cus, s);
+  return dispatch<EmSel>(a, num_cus, s, kDefaultPpl);
 }
 
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
-  return dispatch<WmSel>(a, num_cus, s);
+  const int v = env_int("BG_WM_V", 0), g = env_int("BG_WM_G", 4);
+  if (v && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2) {
+    const int ppl = env_int("BG_PPL", 2);
+#define BG_WMX(P, V, G)                                                    \
+  if (ppl == P && v == V && (V == 1 || g == G))                            \
+    return launch_classify(wm_classify_exp_kernel<P, V, G>, a, num_cus, s, P);
+    BG_WMX(1, 1, 8) BG_WMX(2, 1, 8) BG_WMX(1, 2, 8) BG_WMX(2, 2, 8)
+    BG_WMX(1, 2, 4) BG_WMX(2, 2, 4) BG_WMX(1, 2, 2) BG_WMX(2, 2, 2)
+#undef BG_WMX
+    return hipErrorInvalidValue;
+  }
+  // two packets per lane: the PPL=1 instantiation holds ~150 VGPRs
+  // (occupancy 3), PPL=2 ~65 (occupancy 7)
+  return dispatch<WmSel>(a, num_cus, s, 2);
 }
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
@@ -1051,11 +1255,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   const void *kern = reinterpret_cast<const void *>(kfn);
   int per_cu = env_int("BG_CK_BLOCKS_PER_CU", 0);
   if (per_cu <= 0) {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kCkBlock, 0) !=
-            hipSuccess ||
-        occ <= 0)
-      occ = 7;
+    const int occ = occupancy(kern, kCkBlock, 0, 7);
     per_cu = occ * std::max(1, env_int("BG_CK_GRID_MULT", 4));
   }
   const uint64_t waves_per_block = kCkBlock / 64;

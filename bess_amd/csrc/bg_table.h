@@ -89,6 +89,21 @@ BG_HD Probe split_hash(uint64_t h, uint32_t nparts, uint32_t nbp) {
   return p;
 }
 
+// Blocked Bloom filter over a table's keys (one 32-bit word per probe, two
+// bits set in it). Kept in LDS in front of an L2-resident WildcardMatch
+// table so that most (packet, tuple) pairs that cannot match skip both
+// scattered tag reads. `nwords` is a power of two <= 2^16.
+struct FilterProbe {
+  uint32_t word, bits;
+};
+
+BG_HD FilterProbe filter_probe(uint64_t h, uint32_t nwords) {
+  FilterProbe f;
+  f.word = (uint32_t)(h >> 40) & (nwords - 1);
+  f.bits = (1u << ((uint32_t)(h >> 8) & 31)) | (1u << ((uint32_t)(h >> 14) & 31));
+  return f;
+}
+
 TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
                         uint32_t val_bytes, uint32_t nparts, uint64_t seed,
                         double max_load = 0.75);

@@ -22,7 +22,7 @@ from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
-         "BG_CK_TILED"]
+         "BG_CK_TILED", "BG_WM_V", "BG_WM_G"]
 
 
 def set_env(v):
@@ -119,19 +119,56 @@ def main():
         n = 1 << 22
         rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n, stride=64,
                                                       sizes=((60, 1),))
-        t = F.WmTable(P.FIVE_TUPLE)
-        for k, m, p, gg in zip(rk, rm, prio, gates):
-            t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
         d = torch.from_numpy(frames.reshape(-1)).to(dev)
         g = torch.empty(n, dtype=torch.int16, device=dev)
-        t.sync(0)
-        variants = {"ppl1": {}, "ppl2": {"BG_PPL": 2},
-                    "ppl1_bpc4": {"BG_BLOCKS_PER_CU": 4},
-                    "ppl1_bpc2": {"BG_BLOCKS_PER_CU": 2},
-                    "ppl2_bpc4": {"BG_PPL": 2, "BG_BLOCKS_PER_CU": 4}}
-        r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants)
-        for k in r:
-            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+        tables = {}
+        for kb in (0, 32, 64, 128):  # key filter size is fixed at sync time
+            os.environ["BG_WM_FILTER_KB"] = str(kb)
+            t = F.WmTable(P.FIVE_TUPLE)
+            for k, m, p, gg in zip(rk, rm, prio, gates):
+                t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
+            t.sync(0)
+            tables[kb] = t
+        os.environ.pop("BG_WM_FILTER_KB", None)
+        variants = {"default": (64, {}),
+                    "seq_p2": (64, {"BG_WM_V": 1, "BG_PPL": 2}),
+                    "seq_p1": (64, {"BG_WM_V": 1, "BG_PPL": 1}),
+                    "g8_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 8, "BG_PPL": 1}),
+                    "g8_p2": (64, {"BG_WM_V": 2, "BG_WM_G": 8, "BG_PPL": 2}),
+                    "g4_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 4, "BG_PPL": 1}),
+                    "g2_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 2, "BG_PPL": 1}),
+                    "g2_p2": (64, {"BG_WM_V": 2, "BG_WM_G": 2, "BG_PPL": 2}),
+                    "f32_default": (32, {}), "f128_default": (128, {}),
+                    "nofilter_default": (0, {})}
+        ref = None
+        for name, (kb, env) in variants.items():
+            set_env(env)
+            tables[kb].classify(d, 64, n, 8192, g)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = g.clone()
+            assert torch.equal(g, ref), name
+        res = {k: [] for k in variants}
+        for _ in range(5):
+            for name, (kb, env) in variants.items():
+                set_env(env)
+                tables[kb].classify(d, 64, n, 8192, g)
+                torch.cuda.synchronize()
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(20):
+                    tables[kb].classify(d, 64, n, 8192, g)
+                b.record()
+                b.synchronize()
+                res[name].append(a.elapsed_time(b) / 20)
+        set_env({})
+        r = {}
+        for k, v in res.items():
+            med = statistics.median(v)
+            r[k] = {"median_ms": round(med, 4), "min_ms": round(min(v), 4),
+                    "Mpps": round(n / (med * 1e-3) / 1e6, 1),
+                    "table": tables[variants[k][0]].table_info()}
         out["wm"] = r
     print(json.dumps(out))
 
