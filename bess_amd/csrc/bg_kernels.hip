@@ -502,7 +502,9 @@ template <int KW, int NCH, int PPL>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void wm_classify_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wm_body<KW, NCH, PPL, 2, 4>(a, lds);
+  // measured on MI355X (scripts/variants.py, C4): the sequential resolve
+  // beats the batched-rounds lookup, which hashes every tuple twice
+  wm_body<KW, NCH, PPL, 1, 8>(a, lds);
 }
 
 // A/B variants for the 5-tuple shape (BG_WM_V / BG_WM_G)
@@ -1228,9 +1230,7 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
 #undef BG_WMX
     return hipErrorInvalidValue;
   }
-  // two packets per lane: the PPL=1 instantiation holds ~150 VGPRs
-  // (occupancy 3), PPL=2 ~65 (occupancy 7)
-  return dispatch<WmSel>(a, num_cus, s, 2);
+  return dispatch<WmSel>(a, num_cus, s, 1);
 }
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {

@@ -29,7 +29,7 @@ fi
 if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
   rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
   i=0
-  for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     for W in em cksum wm; do
       if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --steps 3 --warmup 1"; fi
