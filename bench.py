@@ -50,7 +50,7 @@ def parse():
                     help="skip the C3/C4/sweep secondary measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
-    ap.add_argument("--only", default="", help="em|cksum|wm (profiling runs)")
+    ap.add_argument("--only", default="", help="cksum|wm|c5 (profiling runs)")
     return ap.parse_args()
 
 
@@ -151,6 +151,20 @@ def em_parity_sample(t, d_frames, d_gates, keys, gates, n, torch):
     L.or_em_process(em, frames.ctypes.data, 64, n, 8192, want.ctypes.data)
     L.or_em_free(em)
     return bool((got == want).all())
+
+
+def cpu_rate(bench, n, seconds):
+    """Time the oracle's pthread bench driver `bench(nthreads, reps)` (returns
+    seconds) at 1 thread and at T = min(16, usable cores) threads; about
+    `seconds` of CPU work in total. Returns (T, {threads: Mpps})."""
+    from oracle import oracle as O
+    threads = max(1, min(16, O.lib().or_num_cpus()))
+    res = {}
+    for nt in sorted({1, threads}):
+        t1 = bench(nt, 1)
+        reps = max(1, int(seconds / 2 / max(t1, 1e-6)))
+        res[nt] = n * reps / bench(nt, reps) / 1e6
+    return threads, res
 
 
 def cpu_baseline_em(keys, gates, seconds):
@@ -298,6 +312,7 @@ def run_cksum(args, dev, torch):
     frames = P.cksum_workload(n, frame_len=1496, stride=2048)
     d = torch.from_numpy(frames.reshape(-1)).to(dev)
     ref = frames[:4096].copy()
+    cpu_frames = frames[:1 << 16].copy()
     del frames
     l4g = torch.empty(n, dtype=torch.int16, device=dev)
     F.cksum(d, 2048, n, 3, False, None, l4g)
@@ -319,67 +334,69 @@ def run_cksum(args, dev, torch):
     ms = timer.stop_ms() / args.steps
     mpps = n / (ms * 1e-3) / 1e6
     gbs = CK_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
-    return {"workload": "C3: 1500B pkts (1496B frames, 2048B slots), "
-                        "IPChecksum->L4Checksum recompute, 50/50 UDP/TCP",
-            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
-            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": traffic_gbs("cksum", ms),
-                         "traffic_bytes_per_launch": load_traffic("cksum")},
-            "parity": parity}
-
-
-def run_e2e_host(r, args, torch):
-    """End-to-end rate from host memory (the reference's path starts and
-    ends in mbufs): frames in snbuf-like host buffers (2624 B stride, frame
-    at +512), key windows gathered into pinned memory, H2D, em_classify,
-    D2H of the gates, per batch of B packets (bg_em_process_host)."""
-    import ctypes as C
-    from bess_amd import packets as P
-    t = r["t"]
-    n = 1 << 20
-    _, _, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=99)
-    snb = np.zeros((n, 2624), np.uint8)
-    snb[:, 512:512 + 64] = frames
-    base = snb.ctypes.data + 512
-    heads = (C.c_void_p * n)(*range(base, base + n * 2624, 2624))
-    out = np.zeros(n, np.uint16)
-    from bess_amd._lib import lib
-    res = {}
-    for B in (32, 1024, 65536, n):
-        lib().bg_em_process_host(t.h, heads, B, 8192, out.ctypes.data, None)
-        reps = max(1, min(200, (1 << 22) // B))
-        t0 = time.perf_counter()
-        done = 0
-        for i in range(reps):
-            off = (i * B) % n
-            if off + B > n:
-                off = 0
-            lib().bg_em_process_host(
-                t.h, C.cast(C.byref(heads, off * C.sizeof(C.c_void_p)),
-                            C.POINTER(C.c_void_p)),
-                B, 8192, out[off:].ctypes.data, None)
-            done += B
-        dt = time.perf_counter() - t0
-        res[str(B)] = round(done / dt / 1e6, 1)
-    return {"what": "ExactMatch from host snbufs: gather windows -> pinned "
-                    "-> H2D -> kernel -> D2H, synchronous per batch",
-            "Mpps_by_batch": res}
+    out = {"workload": "C3: 1500B pkts (1496B frames, 2048B slots), "
+                       "IPChecksum->L4Checksum recompute, 50/50 UDP/TCP",
+           "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "traffic": traffic_gbs("cksum", ms),
+                        "traffic_bytes_per_launch": load_traffic("cksum")},
+           "parity": parity}
+    if not args.no_cpu:
+        L = O.lib()
+        cn = cpu_frames.shape[0]
+        g = np.zeros(cn, np.uint16)
+        threads, res = cpu_rate(
+            lambda nt, reps: L.or_cksum_bench(cpu_frames.ctypes.data, 2048, cn,
+                                              3, 0, g.ctypes.data, nt, reps),
+            cn, args.cpu_seconds / 2)
+        out["cpu_baseline"] = {
+            "value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
+            "kind": "port", "single_core_mpps": round(res[1], 2),
+            "sample": "%d 1496B frames x reps in 2048B slots, IPChecksum->"
+                      "L4Checksum (AVX2/adc CalculateSum restated)" % cn}
+    return out
 
 
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
-    n = 1 << 20
+    from oracle import oracle as O
+    n0, rep = 1 << 20, 8
+    n = n0 * rep
     # IMIX frames (60/590/1514 B, 7:4:1) in 2 KB slots; the classifier
-    # reads only each frame's header line
-    rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n, stride=2048)
+    # reads only each frame's header line. 1M distinct frames generated on
+    # the host, the 16 GB device slab holds them 8 times over.
+    rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n0, stride=2048)
     t = F.WmTable(P.FIVE_TUPLE)
     for k, m, p, g in zip(rk, rm, prio, gates):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
-    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
+    d = d0.repeat(rep)
+    del d0
     dg = torch.empty(n, dtype=torch.int16, device=dev)
+    t.classify(d, 2048, n, 8192, dg)
+    torch.cuda.synchronize()
+    # parity: oracle WildcardMatch on the first 64K frames
+    L = O.lib()
+    ow = L.or_wm_new()
+    for off, size in P.FIVE_TUPLE:
+        L.or_wm_add_field(ow, off, size, None, 0)
+    L.or_wm_init_done(ow)
+    kb = np.zeros(64, np.uint8)
+    mb = np.zeros(64, np.uint8)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        kb[:16] = k
+        mb[:16] = m
+        L.or_wm_add(ow, kb.ctypes.data, mb.ctypes.data, int(p), int(g))
+    ns = 1 << 16
+    sample = np.ascontiguousarray(frames[:ns])
+    want = np.zeros(ns, np.uint16)
+    L.or_wm_process(ow, sample.ctypes.data, 2048, ns, 8192, want.ctypes.data)
+    got = dg.cpu().numpy().view(np.uint16)
+    parity = bool((got[:ns] == want).all() and
+                  (got.reshape(rep, n0) == got[:n0]).all())
     for _ in range(args.warmup):
         t.classify(d, 2048, n, 8192, dg)
     torch.cuda.synchronize()
@@ -391,15 +408,107 @@ def run_wm(args, dev, torch):
     mpps = n / (ms * 1e-3) / 1e6
     gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
     nbytes, in_lds = t.table_info()
-    return {"workload": "C4: 100K-rule WildcardMatch over 8 masks (tuple-space,"
-                        " priority ties), 5-tuple, header lines of IMIX frames",
-            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
-            "table_bytes": nbytes,
+    out = {"workload": "C4: 100K-rule WildcardMatch over 8 masks (tuple-space,"
+                       " priority ties), 5-tuple, header lines of IMIX frames "
+                       "in 2KB slots",
+           "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
+           "table_bytes": nbytes,
+           "table_in_lds": {0: "no (L2/MALL)", 1: "whole table",
+                            2: "key filter (table in L2/MALL)"}[in_lds],
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "traffic": traffic_gbs("wm", ms),
+                        "traffic_bytes_per_launch": load_traffic("wm")},
+           "parity": "bit-exact vs oracle on 64K-pkt sample" if parity
+                     else "MISMATCH"}
+    if not args.no_cpu:
+        cn = 1 << 16
+        g = np.zeros(cn, np.uint16)
+        threads, res = cpu_rate(
+            lambda nt, reps: L.or_wm_bench(ow, sample.ctypes.data, 2048, cn,
+                                           8192, g.ctypes.data, nt, reps),
+            cn, args.cpu_seconds / 2)
+        out["cpu_baseline"] = {
+            "value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
+            "kind": "port", "single_core_mpps": round(res[1], 2),
+            "sample": "%d IMIX frames x reps in 2048B slots, 100K-rule "
+                      "WildcardMatch (8 CuckooMap tuples, CRC32C)" % cn}
+    L.or_wm_free(ow)
+    return out
+
+
+def run_c5(args, dev, torch):
+    """C5 on one GPU: 1M-rule 5-tuple ExactMatch (table in HBM / MALL, not
+    LDS), 16M resident 64 B packets. The multi-GPU form builds the table
+    sharded and all-gathers it (dist.sharded_em_table); here the 8-way
+    partition build is timed on the host as it would run per rank."""
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    n, nr = 16 << 20, 1 << 20
+    keys, gates, frames = P.em_workload(nr, n, seed=0xC5, pkt_seed=0xC55)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    sample = np.ascontiguousarray(frames[:1 << 18])
+    del frames
+    dg = torch.empty(n, dtype=torch.int16, device=dev)
+    t = F.EmTable(P.em_fields_5tuple())
+    t0 = time.perf_counter()
+    t.add_many(keys, gates)
+    t.sync(dev.index)
+    build_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    pb = t.plan(8)
+    part = t.build_part(0, pb)
+    part_s = time.perf_counter() - t0
+    del part
+    t.sync(dev.index)  # back to the single-device image
+    t.classify(d, 64, n, 8192, dg)
+    torch.cuda.synchronize()
+    # parity on the first 256K packets
+    from oracle import oracle as O
+    import ctypes as C
+    L = O.lib()
+    em = L.or_em_new()
+    for i, (off, size) in enumerate(P.FIVE_TUPLE):
+        L.or_em_add_field(em, off, size, 0, i, None, 0)
+    sizes = [s for _, s in P.FIVE_TUPLE]
+    pos = np.cumsum([0] + sizes)
+    ptrs = (C.c_void_p * 5)()
+    lens = (C.c_size_t * 5)(*sizes)
+    for k, g in zip(np.ascontiguousarray(keys), gates):
+        for j in range(5):
+            ptrs[j] = k.ctypes.data + int(pos[j])
+        L.or_em_add_rule(em, int(g), ptrs, lens, 5, None, 0)
+    ns = sample.shape[0]
+    want = np.zeros(ns, np.uint16)
+    L.or_em_process(em, sample.ctypes.data, 64, ns, 8192, want.ctypes.data)
+    L.or_em_free(em)
+    parity = bool((dg[:ns].cpu().numpy().view(np.uint16) == want).all())
+    for _ in range(args.warmup):
+        t.classify(d, 64, n, 8192, dg)
+    torch.cuda.synchronize()
+    timer = Timer(torch)
+    timer.start()
+    for _ in range(args.steps):
+        t.classify(d, 64, n, 8192, dg)
+    ms = timer.stop_ms() / args.steps
+    mpps = n / (ms * 1e-3) / 1e6
+    gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
+    nbytes, in_lds = t.table_info()
+    return {"workload": "C5 (1 GPU): 64B pkts, 1M-rule 5-tuple ExactMatch, "
+                        "16M resident pkts, table in HBM/MALL",
+            "pkts": n, "rules": nr, "ms_per_step": round(ms, 4),
+            "Mpps": round(mpps, 1), "table_bytes": nbytes,
+            "host_table_build_s": round(build_s, 2),
+            "host_partition_build_s_per_rank_of_8": round(part_s, 3),
+            "partition_bytes": pb,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": traffic_gbs("wm", ms),
-                         "traffic_bytes_per_launch": load_traffic("wm")}}
+                         "traffic": traffic_gbs("c5", ms),
+                         "traffic_bytes_per_launch": load_traffic("c5")},
+            "parity": "bit-exact vs oracle on 256K-pkt sample" if parity
+                      else "MISMATCH"}
 
 
 def main():
@@ -424,6 +533,9 @@ def main():
         return
     if args.only == "wm":
         log(json.dumps(run_wm(args, dev, torch)))
+        return
+    if args.only == "c5":
+        log(json.dumps(run_c5(args, dev, torch)))
         return
 
     r = run_em(args, rank, world, dev, torch, dist)
@@ -470,7 +582,7 @@ def main():
             out["e2e_host"] = run_e2e_host(r, args, torch)
         except Exception as e:
             out["e2e_host"] = "failed: %r" % (e,)
-        for name, fn in (("C3", run_cksum), ("C4", run_wm)):
+        for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

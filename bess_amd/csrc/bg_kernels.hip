@@ -257,6 +257,31 @@ void em_classify_kernel(EmArgs a) {
   em_body<KW, NCH, PPL>(a, lds);
 }
 
+// next grid-stride packet's window prefetched (A/B experiments: BG_EM_PF=1)
+template <int KW, int NCH>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
+void em_classify_pf_kernel(EmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  copy_table_to_lds(lds, a.t);
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t wn[NCH * 4 + 2];
+  if (idx < a.n) load_window<NCH>(a.frames + idx * a.stride, a.fp, wn);
+  for (; idx < a.n; idx += step) {
+    uint32_t w[NCH * 4 + 2];
+#pragma unroll
+    for (int q = 0; q < NCH * 4 + 2; q++) w[q] = wn[q];
+    if (idx + step < a.n)
+      load_window<NCH>(a.frames + (idx + step) * a.stride, a.fp, wn);
+    uint64_t k[KW];
+    extract_key<KW, NCH>(w, a.fp, k);
+    const uint32_t g = a.t.lds == kLdsTable
+                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
+                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
+    a.gates[idx] = (uint16_t)g;
+  }
+}
+
 // unconstrained SGPRs (A/B experiments only: BG_FAT=1)
 template <int KW, int NCH, int PPL>
 __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
@@ -296,8 +321,9 @@ __device__ __forceinline__ bool wm_slot_hit(uint64_t v, const uint64_t (&sk)[KW]
   return eq;
 }
 
-// Round-1 lookup (A/B baseline, BG_WM_V=1): tag reads batched over all
-// tuples, then each tuple's candidates probed in turn (value, then key).
+// Sequential-resolve lookup (default): tag reads batched over all tuples,
+// then each tuple's fingerprint matches probed in turn, the slot's key and
+// value loaded together.
 template <int KW, bool FILT>
 __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
                                                   const WmArgs &a,
@@ -330,28 +356,32 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
   }
   int32_t best = INT_MIN;
   uint32_t gate = a.default_gate;
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
     if (tu < (int)a.ntuples) {
       const Probe p = split_hash(hs[tu], 1, a.t.nbp);
       uint32_t cand = tag_match(w1[tu], p.tag) | (tag_match(w2[tu], p.tag) << 4);
-      while (cand) {
-        const int sl = __builtin_ctz(cand);
-        cand &= cand - 1;
-        const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
-        const uint64_t v =
-            reinterpret_cast<const uint64_t *>(tab + a.t.vals_off)[slot];
-        if ((uint32_t)(v >> 48) != (uint32_t)tu) continue;
+      if (cand) {
         uint64_t km[KW];
 #pragma unroll
         for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
-        if (key_eq<KW>(tab + a.t.keys_off + (uint64_t)slot * KW * 8, km)) {
-          const int32_t prio = (int32_t)(uint32_t)v;
-          if (prio >= best) {
-            best = prio;
-            gate = (uint32_t)(v >> 32) & 0xFFFFu;
+        while (cand) {
+          const int sl = __builtin_ctz(cand);
+          cand &= cand - 1;
+          const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
+          // value and key of the slot in one round trip
+          const uint64_t v = vals[slot];
+          uint64_t sk[KW];
+          load_key<KW>(tab + a.t.keys_off + (uint64_t)slot * KW * 8, sk);
+          if (wm_slot_hit<KW>(v, sk, km, tu)) {
+            const int32_t prio = (int32_t)(uint32_t)v;
+            if (prio >= best) {  // '>=': the later tuple wins a tie (P5)
+              best = prio;
+              gate = (uint32_t)(v >> 32) & 0xFFFFu;
+            }
+            break;
           }
-          break;
         }
       }
     }
@@ -474,9 +504,40 @@ __device__ __forceinline__ uint32_t wm_lookup_v(const uint8_t *tab,
     return wm_lookup<KW, FILT, G>(tab, a, k, filt);
 }
 
-template <int KW, int NCH, int PPL, int V, int G>
+template <int KW, bool FILT, int V, int G>
+__device__ __forceinline__ uint32_t wm_lookup_any(const WmArgs &a,
+                                                  const uint64_t (&k)[KW],
+                                                  const uint8_t *lds) {
+  if (a.t.lds == kLdsTable)
+    return wm_lookup_v<KW, false, V, G>(lds, a, k, nullptr);
+  if (a.t.lds == kLdsFilter)
+    return wm_lookup_v<KW, true, V, G>(a.t.base, a, k,
+                                       reinterpret_cast<const uint32_t *>(lds));
+  return wm_lookup_v<KW, false, V, G>(a.t.base, a, k, nullptr);
+}
+
+template <int KW, int NCH, int PPL, int V, int G, bool PF>
 __device__ __forceinline__ void wm_body(const WmArgs &a, uint8_t *lds) {
   copy_table_to_lds(lds, a.t);
+  if constexpr (PF && NCH > 0 && PPL == 1) {
+    // one packet per lane, the next grid-stride packet's header window
+    // loaded while this one is looked up
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t wn[NCH * 4 + 2];
+    if (idx < a.n) load_window<NCH>(a.frames + idx * a.stride, a.fp, wn);
+    for (; idx < a.n; idx += step) {
+      uint32_t w[NCH * 4 + 2];
+#pragma unroll
+      for (int q = 0; q < NCH * 4 + 2; q++) w[q] = wn[q];
+      if (idx + step < a.n)
+        load_window<NCH>(a.frames + (idx + step) * a.stride, a.fp, wn);
+      uint64_t k[KW];
+      extract_key<KW, NCH>(w, a.fp, k);
+      a.gates[idx] = (uint16_t)wm_lookup_any<KW, true, V, G>(a, k, lds);
+    }
+    return;
+  }
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x * PPL;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * PPL + threadIdx.x;
        base < a.n; base += step) {
@@ -485,14 +546,7 @@ __device__ __forceinline__ void wm_body(const WmArgs &a, uint8_t *lds) {
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
       const uint64_t idx = base + (uint64_t)j * blockDim.x;
-      uint32_t g;
-      if (a.t.lds == kLdsTable)
-        g = wm_lookup_v<KW, false, V, G>(lds, a, k[j], nullptr);
-      else if (a.t.lds == kLdsFilter)
-        g = wm_lookup_v<KW, true, V, G>(a.t.base, a, k[j],
-                                        reinterpret_cast<const uint32_t *>(lds));
-      else
-        g = wm_lookup_v<KW, false, V, G>(a.t.base, a, k[j], nullptr);
+      const uint32_t g = wm_lookup_any<KW, true, V, G>(a, k[j], lds);
       if (idx < a.n) a.gates[idx] = (uint16_t)g;
     }
   }
@@ -504,15 +558,15 @@ void wm_classify_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // measured on MI355X (scripts/variants.py, C4): the sequential resolve
   // beats the batched-rounds lookup, which hashes every tuple twice
-  wm_body<KW, NCH, PPL, 1, 8>(a, lds);
+  wm_body<KW, NCH, PPL, 1, 8, false>(a, lds);
 }
 
 // A/B variants for the 5-tuple shape (BG_WM_V / BG_WM_G)
-template <int PPL, int V, int G>
+template <int PPL, int V, int G, bool PF>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void wm_classify_exp_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wm_body<2, 2, PPL, V, G>(a, lds);
+  wm_body<2, 2, PPL, V, G, PF>(a, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1210,6 +1264,8 @@ struct WmSel {
 }  // namespace
 
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
+  if (env_int("BG_EM_PF", 0) && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2)
+    return launch_classify(em_classify_pf_kernel<2, 2>, a, num_cus, s, 1);
   if (env_int("BG_FAT", 0) && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2) {
     if (env_int("BG_PPL", kDefaultPpl) == 2)
       return launch_classify(em_classify_fat_kernel<2, 2, 2>, a, num_cus, s, 2);
@@ -1222,11 +1278,13 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
   const int v = env_int("BG_WM_V", 0), g = env_int("BG_WM_G", 4);
   if (v && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2) {
     const int ppl = env_int("BG_PPL", 2);
-#define BG_WMX(P, V, G)                                                    \
-  if (ppl == P && v == V && (V == 1 || g == G))                            \
-    return launch_classify(wm_classify_exp_kernel<P, V, G>, a, num_cus, s, P);
-    BG_WMX(1, 1, 8) BG_WMX(2, 1, 8) BG_WMX(1, 2, 8) BG_WMX(2, 2, 8)
-    BG_WMX(1, 2, 4) BG_WMX(2, 2, 4) BG_WMX(1, 2, 2) BG_WMX(2, 2, 2)
+    const bool pf = env_int("BG_WM_PF", 0) != 0;
+#define BG_WMX(P, V, G, PF)                                                \
+  if (ppl == P && v == V && (V == 1 || g == G) && pf == PF)                \
+    return launch_classify(wm_classify_exp_kernel<P, V, G, PF>, a, num_cus, s, P);
+    BG_WMX(1, 1, 8, false) BG_WMX(2, 1, 8, false) BG_WMX(1, 2, 8, false)
+    BG_WMX(1, 2, 4, false) BG_WMX(2, 2, 4, false) BG_WMX(1, 1, 8, true)
+    BG_WMX(1, 2, 4, true) BG_WMX(1, 2, 8, true)
 #undef BG_WMX
     return hipErrorInvalidValue;
   }

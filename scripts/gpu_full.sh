@@ -31,8 +31,8 @@ if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
   i=0
   for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
     i=$((i+1))
-    for W in em cksum wm; do
-      if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --steps 3 --warmup 1"; fi
+    for W in em cksum wm c5; do
+      if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --no-cpu --steps 3 --warmup 1"; fi
       step pmc_${W}_$i 900 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
     done
   done

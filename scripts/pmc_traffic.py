@@ -19,9 +19,10 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"em": "em_classify_kernel", "cksum": "cksum_kernel",
-           "wm": "wm_classify_kernel"}
+           "wm": "wm_classify_kernel", "c5": "em_classify_kernel"}
+# algorithmic bytes per launch of each bench workload
 ALGO = {"em": 66 * (16 << 20), "cksum": 1502 * (1 << 20),
-        "wm": 66 * (1 << 20)}
+        "wm": 66 * (8 << 20), "c5": 66 * (16 << 20)}
 
 
 def collect(root, wl):

@@ -22,7 +22,7 @@ from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
-         "BG_CK_TILED", "BG_WM_V", "BG_WM_G"]
+         "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF"]
 
 
 def set_env(v):
@@ -67,9 +67,9 @@ def main():
         t.sync(0)
         ref = None
         variants = {
-            "default": {}, "ppl2": {"BG_PPL": 2},
-            "bpc3": {"BG_BLOCKS_PER_CU": 3}, "bpc4": {"BG_BLOCKS_PER_CU": 4},
-            "l2tab": {"BG_NOLDS": 1},
+            "default": {}, "ppl2": {"BG_PPL": 2}, "pf": {"BG_EM_PF": 1},
+            "pf_bpc3": {"BG_EM_PF": 1, "BG_BLOCKS_PER_CU": 3},
+            "bpc3": {"BG_BLOCKS_PER_CU": 3}, "l2tab": {"BG_NOLDS": 1},
         }
         # every variant must give identical gates
         for name, env in variants.items():
@@ -131,14 +131,13 @@ def main():
             tables[kb] = t
         os.environ.pop("BG_WM_FILTER_KB", None)
         variants = {"default": (64, {}),
+                    "seq_pf": (64, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "seq_p2": (64, {"BG_WM_V": 1, "BG_PPL": 2}),
-                    "seq_p1": (64, {"BG_WM_V": 1, "BG_PPL": 1}),
-                    "g8_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 8, "BG_PPL": 1}),
-                    "g8_p2": (64, {"BG_WM_V": 2, "BG_WM_G": 8, "BG_PPL": 2}),
+                    "g4_pf": (64, {"BG_WM_V": 2, "BG_WM_G": 4, "BG_WM_PF": 1, "BG_PPL": 1}),
+                    "g8_pf": (64, {"BG_WM_V": 2, "BG_WM_G": 8, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "g4_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 4, "BG_PPL": 1}),
-                    "g2_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 2, "BG_PPL": 1}),
-                    "g2_p2": (64, {"BG_WM_V": 2, "BG_WM_G": 2, "BG_PPL": 2}),
-                    "f32_default": (32, {}), "f128_default": (128, {}),
+                    "seq_pf_f128": (128, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
+                    "nofilter_seq_pf": (0, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "nofilter_default": (0, {})}
         ref = None
         for name, (kb, env) in variants.items():
