@@ -82,6 +82,7 @@ _SIGS = {
     "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
     "bg_module_set_device": (_int, [_vp, _int]),
     "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
+    "bg_debug_key": (_int, [C.POINTER(bg_field), _int, _int, _vp, _vp]),
 }
 
 _lib = None

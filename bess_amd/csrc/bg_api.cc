@@ -77,6 +77,86 @@ uint32_t round_kw(uint32_t key_bytes) {
 
 // Field plan for frames whose head_data() is at offset `base` of the
 // buffer the kernel reads (base = 0 for slabs, -win_lo for staged windows).
+// Byte-permute plan (FieldPlan::kd_*): for every key byte, the window byte
+// it comes from and its mask byte; each key dword's sources are covered by
+// dword pairs {w[d+1]:w[d]} of the window, one v_perm_b32 per pair (at most
+// four: one per byte).
+static void plan_perm(const std::vector<bg_field> &fields, int shift,
+                      FieldPlan *p) {
+  constexpr int kKeyBytes = 8 * kMaxKeyWords;
+  int src[kKeyBytes];
+  uint8_t mbyte[kKeyBytes] = {0};
+  for (int b = 0; b < kKeyBytes; b++) src[b] = -1;
+  for (int i = 0; i < p->nf; i++) {
+    const bg_field &f = fields[i];
+    for (int j = 0; j < f.size; j++) {
+      const int kb = f.pos + j;
+      if (kb < 0 || kb >= kKeyBytes) continue;
+      src[kb] = f.offset + shift - p->win_lo + j;
+      mbyte[kb] = (uint8_t)(p->fmask[i] >> (8 * j));
+    }
+  }
+  int nkd = 0;
+  for (int q = 0; q < 2 * kMaxKeyWords; q++) {
+    uint32_t dw[4] = {0, 0, 0, 0}, mask = 0;
+    uint32_t sel[4] = {kPermZero, kPermZero, kPermZero, kPermZero};
+    int nops = 0;
+    for (int b = 0; b < 4; b++) {
+      const int s = src[4 * q + b];
+      mask |= (uint32_t)mbyte[4 * q + b] << (8 * b);
+      if (s < 0) continue;
+      int op = -1;
+      for (int o = 0; o < nops; o++)
+        if (s >= (int)dw[o] * 4 && s < (int)dw[o] * 4 + 8) op = o;
+      if (op < 0) {
+        op = nops++;
+        dw[op] = (uint32_t)(s / 4);
+      }
+      sel[op] = (sel[op] & ~(0xFFu << (8 * b))) |
+                ((uint32_t)(s - 4 * (int)dw[op]) << (8 * b));
+    }
+    if (nops) nkd = q + 1;
+    p->kd_nops[q >> 2] |= (uint32_t)nops << (8 * (q & 3));
+    p->kd_dw[q] = dw[0] | (dw[1] << 8) | (dw[2] << 16) | (dw[3] << 24);
+    for (int o = 0; o < 4; o++) p->kd_sel[o][q] = sel[o];
+    p->kd_mask[q] = mask;
+  }
+  p->nkd = nkd;
+}
+
+// The device key of one frame, built on the host exactly as the kernels
+// build it (window or direct mode) -- bg_debug_key.
+static void host_key(const FieldPlan &p, const uint8_t *frame, int kw,
+                     uint64_t *k) {
+  for (int j = 0; j < kw; j++) k[j] = 0;
+  if (!p.direct) {
+    uint32_t w[kMaxWindowChunks * 4 + 2] = {0};
+    memcpy(w, frame + p.win_lo, (size_t)p.nch * 16);
+    for (int q = 0; q < 2 * kw && q < p.nkd; q++) {
+      uint32_t x = 0;
+      for (int o = 0; o < kd_nops_of(p, q); o++) {
+        const uint32_t d = (p.kd_dw[q] >> (8 * o)) & 0xFF;
+        x |= perm_host(w[d + 1], w[d], p.kd_sel[o][q]);
+      }
+      x &= p.kd_mask[q];
+      k[q >> 1] |= (uint64_t)x << (32 * (q & 1));
+    }
+    return;
+  }
+  for (int f = 0; f < p.nf; f++) {
+    const uint32_t spec = p.fspec[f];
+    uint32_t d[3] = {0, 0, 0};
+    memcpy(d, frame + 4 * fspec_d(spec), 4 * (size_t)fspec_nd(spec));
+    const uint64_t lo = (uint64_t)d[0] | ((uint64_t)d[1] << 32);
+    const int sh = fspec_shift_bits(spec);
+    const uint64_t v =
+        (sh ? ((lo >> sh) | ((uint64_t)d[2] << (64 - sh))) : lo) & p.fmask[f];
+    const int pos = fspec_pos(spec), pw = pos >> 3, pb = (pos & 7) * 8;
+    if (pw < kw) k[pw] |= v << pb;
+    if (pb && pw + 1 < kw) k[pw + 1] |= v >> (64 - pb);
+  }
+}
+
 FieldPlan make_plan(const std::vector<bg_field> &fields, bool em_masks,
                     int shift) {
   FieldPlan p;
@@ -101,6 +181,7 @@ FieldPlan make_plan(const std::vector<bg_field> &fields, bool em_masks,
     uint64_t size_mask = f.size >= 8 ? ~0ULL : ((1ULL << (8 * f.size)) - 1);
     p.fmask[i] = em_masks ? (f.mask & size_mask) : size_mask;
   }
+  if (!p.direct) plan_perm(fields, shift, &p);  // window mode
   return p;
 }
 
@@ -884,3 +965,17 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 }
 
 }  // extern "C"
+
+extern "C" int bg_debug_key(const bg_field *fields, int nfields,
+                            int em_masks, const uint8_t *frame,
+                            uint8_t *key_out) {
+  if (nfields < 0 || nfields > kMaxFields || (nfields && !fields) || !frame ||
+      !key_out)
+    return fail(EINVAL, "bad arguments");
+  std::vector<bg_field> f(fields, fields + nfields);
+  const FieldPlan p = make_plan(f, em_masks != 0, 0);
+  uint64_t k[kMaxKeyWords];
+  host_key(p, frame, kMaxKeyWords, k);
+  memcpy(key_out, k, sizeof(k));
+  return 0;
+}

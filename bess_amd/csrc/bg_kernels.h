@@ -30,7 +30,37 @@ struct FieldPlan {
   // inside that dword, 11-16 key byte position, 17-18 dwords spanned
   uint32_t fspec[kMaxFields];
   uint64_t fmask[kMaxFields];  // mask in key byte order (low `size` bytes)
+  // Byte-permute form of the key build, used by every window-mode kernel:
+  //   key dword q = (OR over o < nops(q) of perm(w[d+1], w[d], kd_sel[o][q]),
+  //                  d = byte o of kd_dw[q]) & kd_mask[q]
+  // nops(q) = byte q of kd_nops (0..4). v_perm_b32 selectors pick byte 0..7
+  // of {w[d+1]:w[d]}; 0x0C gives a zero byte.
+  int32_t nkd;  // key dwords that carry bytes
+  uint32_t kd_nops[2 * kMaxKeyWords / 4];
+  uint32_t kd_dw[2 * kMaxKeyWords];
+  uint32_t kd_sel[4][2 * kMaxKeyWords];
+  uint32_t kd_mask[2 * kMaxKeyWords];
 };
+
+BG_HD int kd_nops_of(const FieldPlan &p, int q) {
+  return (int)((p.kd_nops[q >> 2] >> (8 * (q & 3))) & 0xFF);
+}
+
+constexpr uint32_t kPermZero = 0x0C0C0C0Cu;  // v_perm_b32: four zero bytes
+
+// v_perm_b32 semantics on the host (plan checks, bg_debug_key)
+inline uint32_t perm_host(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t d = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) {
+    const uint32_t b = (sel >> (8 * i)) & 0xFF;
+    uint32_t v = 0;
+    if (b < 8) v = (uint32_t)(d >> (8 * b)) & 0xFF;
+    else if (b >= 0x0D) v = 0xFF;
+    r |= v << (8 * i);
+  }
+  return r;
+}
 
 BG_HD uint32_t pack_fspec(int d, int byte_shift, int pos, int nd) {
   return (uint32_t)(d & 0x1FF) | ((uint32_t)(byte_shift & 3) << 9) |

@@ -12,6 +12,7 @@
 #include <mutex>
 #include <vector>
 #include <limits.h>
+#include <stddef.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -81,22 +82,31 @@ __device__ __forceinline__ void place_field(uint64_t v, int p,
   }
 }
 
+// Key from the byte-permute plan (FieldPlan::kd_*): per key dword one
+// v_perm_b32 per source dword pair (wave-uniform window index: s_set_gpr_idx,
+// no scratch) and one AND. ExactMatchTable::MakeKeys semantics (mask per
+// field, bytes past the key zero) are folded into selectors and masks.
 template <int KW, int NCH>
 __device__ __forceinline__ void extract_key(const uint32_t (&w)[NCH * 4 + 2],
                                             const FieldPlan &fp,
                                             uint64_t (&k)[KW]) {
+  // NCH == 2 kernels are only dispatched for plans with <= 2 permutes per
+  // key dword. Branch-free: unused permutes have all-zero selectors.
+  constexpr int kMaxOps = NCH == 2 ? 2 : 4;
+  uint32_t kd[2 * KW];
 #pragma unroll
-  for (int j = 0; j < KW; j++) k[j] = 0;
+  for (int q = 0; q < 2 * KW; q++) {
+    const uint32_t dws = fp.kd_dw[q];
+    uint32_t x = 0;
 #pragma unroll
-  for (int f = 0; f < kMaxFields; f++) {
-    if (f < fp.nf) {
-      const uint32_t spec = fp.fspec[f];
-      const int d = fspec_d(spec), sh = fspec_shift_bits(spec);
-      uint64_t lo = (uint64_t)w[d] | ((uint64_t)w[d + 1] << 32);
-      uint64_t v = sh ? ((lo >> sh) | ((uint64_t)w[d + 2] << (64 - sh))) : lo;
-      place_field<KW>(v & fp.fmask[f], fspec_pos(spec), k);
+    for (int o = 0; o < kMaxOps; o++) {
+      const uint32_t d = (dws >> (8 * o)) & 0xFF;
+      x |= __builtin_amdgcn_perm(w[d + 1], w[d], fp.kd_sel[o][q]);
     }
+    kd[q] = x & fp.kd_mask[q];
   }
+#pragma unroll
+  for (int j = 0; j < KW; j++) k[j] = (uint64_t)kd[2 * j + 1] << 32 | kd[2 * j];
 }
 
 // fields too far apart for one window: per-field aligned dword loads
@@ -206,12 +216,24 @@ __device__ __forceinline__ uint32_t em_lookup(const uint8_t *tab,
   return dflt;
 }
 
+// Table / filter fill: four 16-byte loads in flight per thread before
+// their LDS writes (a 40 KB table is ~5 loads per thread of a 512-thread
+// block; one round trip instead of five).
 __device__ __forceinline__ void copy_to_lds(uint8_t *lds, const uint8_t *g,
                                             uint32_t bytes) {
   const uint4 *src = reinterpret_cast<const uint4 *>(g);
   uint4 *dst = reinterpret_cast<uint4 *>(lds);
-  for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x)
-    dst[i] = src[i];
+  const uint32_t n = bytes / 16, step = blockDim.x;
+  uint32_t i = threadIdx.x;
+  for (; i + 3 * step < n; i += 4 * step) {
+    const uint4 a = src[i], b = src[i + step], c = src[i + 2 * step],
+                d = src[i + 3 * step];
+    dst[i] = a;
+    dst[i + step] = b;
+    dst[i + 2 * step] = c;
+    dst[i + 3 * step] = d;
+  }
+  for (; i < n; i += step) dst[i] = src[i];
   __syncthreads();
 }
 
@@ -293,6 +315,22 @@ __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
 // WildcardMatch: tuple-space search over <= 8 masks in one combined table;
 // the best (priority, later-tuple-on-tie) entry wins (LookupEntry 136-157).
 // ---------------------------------------------------------------------------
+// The WildcardMatch tuple masks (up to 64 words) would otherwise be hoisted
+// into scalar registers for the whole kernel and spilled; laundering the
+// kernarg pointer per packet makes them cheap scalar-cache loads instead.
+// (The WmArgs block is the kernel's only argument, so it starts at the
+// kernarg segment; taking the parameter's address instead would copy the
+// whole block to scratch.)
+typedef const uint64_t __attribute__((address_space(4))) *kconst_u64;
+__device__ __forceinline__ kconst_u64 tuple_masks(const WmArgs &) {
+  const __attribute__((address_space(4))) uint8_t *ka =
+      (const __attribute__((address_space(4))) uint8_t *)
+          __builtin_amdgcn_kernarg_segment_ptr();
+  kconst_u64 p = (kconst_u64)(ka + offsetof(WmArgs, tmask));
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <int KW>
 __device__ __forceinline__ void load_key(const uint8_t *p, uint64_t (&o)[KW]) {
   if constexpr (KW % 2 == 0) {
@@ -329,6 +367,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
                                                   const WmArgs &a,
                                                   const uint64_t (&k)[KW],
                                                   const uint32_t *filt) {
+  const kconst_u64 tm = tuple_masks(a);
   uint64_t hs[kMaxTuples];
   uint32_t w1[kMaxTuples], w2[kMaxTuples];
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
@@ -339,7 +378,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
     if (tu < (int)a.ntuples) {
       uint64_t km[KW];
 #pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
       const uint64_t h = hash_words(km, KW, tuple_seed(a.t.seed, tu));
       hs[tu] = h;
       bool pass = true;
@@ -365,7 +404,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
       if (cand) {
         uint64_t km[KW];
 #pragma unroll
-        for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+        for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
         while (cand) {
           const int sl = __builtin_ctz(cand);
           cand &= cand - 1;
@@ -394,6 +433,7 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
                                               const WmArgs &a,
                                               const uint64_t (&k)[KW],
                                               const uint32_t *filt) {
+  const kconst_u64 tm = tuple_masks(a);
   // Three batched rounds, each issuing every tuple's reads before any is
   // consumed (the WildcardMatch table has a single partition):
   //   A. hash per tuple, LDS key filter, both tag words (<= 16 loads);
@@ -410,7 +450,7 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
     if (tu < (int)a.ntuples) {
       uint64_t km[KW];
 #pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
       const uint64_t h = hash_words(km, KW, tuple_seed(a.t.seed, tu));
       bool pass = true;
       if (FILT) {  // key filter in LDS: skip tuples that cannot match
@@ -443,7 +483,7 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
     if (tu < (int)a.ntuples && (w1[tu] | w2[tu])) {
       uint64_t km[KW];
 #pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
       const Probe p =
           split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)), 1, a.t.nbp);
       uint32_t c = tag_match(w1[tu], p.tag) | (tag_match(w2[tu], p.tag) << 4);
@@ -462,7 +502,7 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
     if (tu < (int)a.ntuples && (cand[gi] & 0x100u)) {
       uint64_t km[KW];
 #pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & a.tmask[tu][j];
+      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
       bool hit = wm_slot_hit<KW>(v1[gi], sk1[gi], km, tu);
       uint64_t v = v1[gi];
       uint32_t c = cand[gi] & 0xFFu;
@@ -1238,7 +1278,9 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
 
 template <template <int, int, int> class Sel, typename Args>
 hipError_t dispatch(const Args &a, int num_cus, hipStream_t s, int dflt_ppl) {
-  const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 ? 2 : 4);
+  int maxops = 0;
+  for (int q = 0; q < a.fp.nkd; q++) maxops = std::max(maxops, kd_nops_of(a.fp, q));
+  const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 && maxops <= 2 ? 2 : 4);
   const int ppl = env_int("BG_PPL", dflt_ppl);
 #define BG_CASE(KW, NCH, PPL)                                                   \
   if (a.t.kw == KW && nch == NCH && ppl == PPL)                                 \
@@ -1263,10 +1305,17 @@ struct WmSel {
 
 }  // namespace
 
+bool fits_nch2(const FieldPlan &fp) {
+  if (fp.direct || fp.nch > 2) return false;
+  for (int q = 0; q < fp.nkd; q++)
+    if (kd_nops_of(fp, q) > 2) return false;
+  return true;
+}
+
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
-  if (env_int("BG_EM_PF", 0) && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2)
+  if (env_int("BG_EM_PF", 0) && a.t.kw == 2 && fits_nch2(a.fp))
     return launch_classify(em_classify_pf_kernel<2, 2>, a, num_cus, s, 1);
-  if (env_int("BG_FAT", 0) && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2) {
+  if (env_int("BG_FAT", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {
     if (env_int("BG_PPL", kDefaultPpl) == 2)
       return launch_classify(em_classify_fat_kernel<2, 2, 2>, a, num_cus, s, 2);
     return launch_classify(em_classify_fat_kernel<2, 2, 1>, a, num_cus, s, 1);
@@ -1276,7 +1325,7 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
 
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
   const int v = env_int("BG_WM_V", 0), g = env_int("BG_WM_G", 4);
-  if (v && a.t.kw == 2 && !a.fp.direct && a.fp.nch <= 2) {
+  if (v && a.t.kw == 2 && fits_nch2(a.fp)) {
     const int ppl = env_int("BG_PPL", 2);
     const bool pf = env_int("BG_WM_PF", 0) != 0;
 #define BG_WMX(P, V, G, PF)                                                \

@@ -148,6 +148,14 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
                           uint16_t *ip_gates, uint16_t *l4_gates,
                           bg_stream_t stream);
 
+/* ---- diagnostics ------------------------------------------------------- */
+/* The key the classify kernels build for `frame` from `fields` (em_masks 1:
+ * ExactMatch field masks applied; 0: WildcardMatch raw field bytes), run on
+ * the host with the kernels' own field plan (byte-permute or direct form).
+ * key_out: 64 bytes. No device needed. */
+int bg_debug_key(const bg_field *fields, int nfields, int em_masks,
+                 const uint8_t *frame, uint8_t *key_out);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".
