@@ -359,6 +359,44 @@ def run_cksum(args, dev, torch):
     return out
 
 
+def run_e2e_host(r, args, torch):
+    """End-to-end rate from host memory (the reference's path starts and
+    ends in mbufs): frames in snbuf-like host buffers (2624 B stride, frame
+    at +512), key windows gathered into pinned memory, H2D, em_classify,
+    D2H of the gates, per batch of B packets (bg_em_process_host)."""
+    import ctypes as C
+    from bess_amd import packets as P
+    t = r["t"]
+    n = 1 << 20
+    _, _, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=99)
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + 64] = frames
+    base = snb.ctypes.data + 512
+    heads = (C.c_void_p * n)(*range(base, base + n * 2624, 2624))
+    out = np.zeros(n, np.uint16)
+    from bess_amd._lib import lib
+    res = {}
+    for B in (32, 1024, 65536, n):
+        lib().bg_em_process_host(t.h, heads, B, 8192, out.ctypes.data, None)
+        reps = max(1, min(200, (1 << 22) // B))
+        t0 = time.perf_counter()
+        done = 0
+        for i in range(reps):
+            off = (i * B) % n
+            if off + B > n:
+                off = 0
+            lib().bg_em_process_host(
+                t.h, C.cast(C.byref(heads, off * C.sizeof(C.c_void_p)),
+                            C.POINTER(C.c_void_p)),
+                B, 8192, out[off:].ctypes.data, None)
+            done += B
+        dt = time.perf_counter() - t0
+        res[str(B)] = round(done / dt / 1e6, 1)
+    return {"what": "ExactMatch from host snbufs: gather windows -> pinned "
+                    "-> H2D -> kernel -> D2H, synchronous per batch",
+            "Mpps_by_batch": res}
+
+
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
@@ -414,7 +452,7 @@ def run_wm(args, dev, torch):
            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
            "table_bytes": nbytes,
            "table_in_lds": {0: "no (L2/MALL)", 1: "whole table",
-                            2: "key filter (table in L2/MALL)"}[in_lds],
+                            2: "key filter (table in L2/MALL)"}[int(in_lds)],
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),

@@ -304,6 +304,92 @@ void em_classify_pf_kernel(EmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// ExactMatch over a dense 64-byte-slot slab (stride 64, key window inside
+// the slot): the slab is read with fully coalesced 16 B/lane loads -- a
+// wave's 64 slots are 4 KB contiguous, 4 loads per lane -- and transposed
+// through a per-wave 4 KB LDS stage so that each lane then reads its own
+// slot's window. Measured (scripts/hbm_probe.hip): lane-contiguous loads
+// stream the slab at ~7.1 TB/s where one-slot-per-lane 16 B loads at a
+// 64 B stride reach ~5.0 TB/s. The stage is swizzled (slot s keeps chunk q
+// at unit 4s + ((q + s/4) & 3)) so both the writes and the per-slot reads
+// of 16 lanes hit 16 distinct 16-byte bank groups.
+// PF: the next tile's four loads are issued before this tile is looked up.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
+  return slot * 4 + ((q + (slot >> 2)) & 3);
+}
+
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int KW, int NCH, int PF>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
+void em_slab_kernel(EmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  copy_table_to_lds(lds, a.t);
+  const uint32_t stage_off =
+      a.t.lds == kLdsTable ? ((a.t.bytes_total + 15) & ~15u) : 0u;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_off) + wid * 256;
+  constexpr int kWaves = kEmBlock / 64;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
+  const uint32_t q0 = (uint32_t)a.fp.win_lo >> 4;
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  uint4 v[4], v2[4];
+  auto load_tile = [&](uint64_t tile, uint4 (&o)[4]) {
+    const uint64_t p0 = tile * 64;
+    const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
+    const uint4 *g = src + p0 * 4;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      o[c] = u < units ? ld_stream(g + u) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (t < ntiles) load_tile(t, v);
+  if (PF == 2 && t + nwaves < ntiles) load_tile(t + nwaves, v2);
+  for (; t < ntiles; t += nwaves) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      stage[stage_unit(u >> 2, u & 3)] = v[c];
+    }
+    lds_fence();
+    if (PF == 1 && t + nwaves < ntiles) load_tile(t + nwaves, v);
+    if (PF == 2) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) v[c] = v2[c];
+      if (t + 2 * nwaves < ntiles) load_tile(t + 2 * nwaves, v2);
+    }
+    uint32_t w[NCH * 4 + 2];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (c < a.fp.nch) x = stage[stage_unit(lane, q0 + c)];
+      w[4 * c] = x.x;
+      w[4 * c + 1] = x.y;
+      w[4 * c + 2] = x.z;
+      w[4 * c + 3] = x.w;
+    }
+    w[NCH * 4] = 0;
+    w[NCH * 4 + 1] = 0;
+    uint64_t k[KW];
+    extract_key<KW, NCH>(w, a.fp, k);
+    const uint32_t g = a.t.lds == kLdsTable
+                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
+                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
+    const uint64_t idx = t * 64 + lane;
+    if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    lds_fence();  // this tile's stage reads retire before the next writes
+    if (PF == 0 && t + nwaves < ntiles) load_tile(t + nwaves, v);
+  }
+}
+
 // unconstrained SGPRs (A/B experiments only: BG_FAT=1)
 template <int KW, int NCH, int PPL>
 __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
@@ -597,8 +683,9 @@ __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void wm_classify_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // measured on MI355X (scripts/variants.py, C4): the sequential resolve
-  // beats the batched-rounds lookup, which hashes every tuple twice
-  wm_body<KW, NCH, PPL, 1, 8, false>(a, lds);
+  // beats the batched-rounds lookup, which hashes every tuple twice; the
+  // next packet's header is prefetched (PPL = 1)
+  wm_body<KW, NCH, PPL, 1, 8, true>(a, lds);
 }
 
 // A/B variants for the 5-tuple shape (BG_WM_V / BG_WM_G)
@@ -1312,7 +1399,53 @@ bool fits_nch2(const FieldPlan &fp) {
   return true;
 }
 
+// Dense 64 B slots with the key window inside the slot: the coalesced
+// slab kernel (em_slab_kernel). LDS = table (if staged) + 4 KB per wave.
+template <int KW, int NCH>
+hipError_t launch_em_slab(EmArgs a, int num_cus, hipStream_t s) {
+  if (env_int("BG_NOLDS", 0)) a.t.lds = kLdsNone;
+  // prefetch depth (tiles ahead), measured on MI355X: scripts/variants.py
+  const int pf = std::min(2, std::max(0, env_int("BG_SLAB_PF", 1)));
+  using K = void (*)(EmArgs);
+  const K kern = pf == 2   ? em_slab_kernel<KW, NCH, 2>
+                 : pf == 1 ? em_slab_kernel<KW, NCH, 1>
+                           : em_slab_kernel<KW, NCH, 0>;
+  const uint64_t need = (a.n + kEmBlock - 1) / kEmBlock;
+  constexpr size_t kStage = (size_t)(kEmBlock / 64) * 4096;
+  for (int pass = 0; pass < 2; pass++) {
+    const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
+    const size_t lds = tab + kStage;
+    int pc = env_int("BG_BLOCKS_PER_CU", 0);
+    if (pc <= 0) pc = occupancy(reinterpret_cast<const void *>(kern), kEmBlock, lds, 1);
+    const uint64_t cap = (uint64_t)num_cus * pc;
+    const uint64_t blocks = need > cap ? cap : need;
+    if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
+        !env_int("BG_FORCE_LDS", 0)) {
+      a.t.lds = kLdsNone;  // small launch: probe the table in L2 instead
+      continue;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kEmBlock), lds, s, a);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+bool slab_ok(const EmArgs &a) {
+  return a.stride == 64 && !a.fp.direct && a.fp.win_lo >= 0 &&
+         a.fp.win_lo + 16 * a.fp.nch <= 64 && ((uintptr_t)a.frames & 15) == 0 &&
+         !env_int("BG_NO_SLAB", 0);
+}
+
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
+  if (slab_ok(a)) {
+    const bool two = fits_nch2(a.fp);
+#define BG_SLAB(KW)                                                        \
+  if (a.t.kw == KW)                                                        \
+    return two ? launch_em_slab<KW, 2>(a, num_cus, s)                      \
+               : launch_em_slab<KW, 4>(a, num_cus, s);
+    BG_SLAB(1) BG_SLAB(2) BG_SLAB(4) BG_SLAB(8)
+#undef BG_SLAB
+  }
   if (env_int("BG_EM_PF", 0) && a.t.kw == 2 && fits_nch2(a.fp))
     return launch_classify(em_classify_pf_kernel<2, 2>, a, num_cus, s, 1);
   if (env_int("BG_FAT", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {

@@ -168,7 +168,7 @@ class WmTable:
     def table_info(self):
         b, l = C.c_uint64(), C.c_int()
         check(lib().bg_wm_table_info(self.h, C.byref(b), C.byref(l)))
-        return b.value, bool(l.value)
+        return b.value, l.value  # 0 L2/MALL, 1 table in LDS, 2 key filter in LDS
 
 
 def cksum(frames, stride, n, mode, verify, ip_gates=None, l4_gates=None,

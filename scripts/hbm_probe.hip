@@ -1,0 +1,122 @@
+// hbm_probe.hip -- calibration of the HBM read roofline on the box, for the
+// access shapes the classify kernels use (not part of libbessgpu).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o hbm_probe scripts/hbm_probe.hip
+//   ./hbm_probe [GiB]
+//
+// Shapes over one resident slab of 64-byte packet slots:
+//   full16  : every byte, 16 B per lane per load, lanes contiguous
+//   em32    : bytes 16..47 of every 64 B slot (two 16 B loads per lane, lane
+//             = slot) + one 2-byte store per slot -- the C2 ExactMatch shape
+//   slot64  : all 64 B of every slot (four 16 B loads per lane, lane = slot)
+// Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
+// bytes read (median of 5 rounds of 20 back-to-back launches).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 ldnt(const u32x4 *p) {
+  return __builtin_nontemporal_load(p);
+}
+
+__global__ __launch_bounds__(512) void full16(const u32x4 *src, size_t n16,
+                                              uint32_t *sink) {
+  uint32_t acc = 0;
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+       i += step) {
+    u32x4 v = ldnt(src + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) sink[threadIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(512) void em32(const u32x4 *src, size_t nslots,
+                                            uint16_t *gates) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
+       i += step) {
+    u32x4 a = ldnt(src + 4 * i + 1), b = ldnt(src + 4 * i + 2);
+    gates[i] = (uint16_t)(a.x ^ a.w ^ b.y ^ b.z);
+  }
+}
+
+__global__ __launch_bounds__(512) void slot64(const u32x4 *src, size_t nslots,
+                                              uint16_t *gates) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
+       i += step) {
+    u32x4 a = ldnt(src + 4 * i), b = ldnt(src + 4 * i + 1),
+          c = ldnt(src + 4 * i + 2), d = ldnt(src + 4 * i + 3);
+    gates[i] = (uint16_t)(a.x ^ b.w ^ c.y ^ d.z);
+  }
+}
+
+#define CK(x)                                                            \
+  do {                                                                   \
+    hipError_t e = (x);                                                  \
+    if (e != hipSuccess) {                                               \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));             \
+      exit(1);                                                           \
+    }                                                                    \
+  } while (0)
+
+int main(int argc, char **argv) {
+  const double gib = argc > 1 ? atof(argv[1]) : 1.0;
+  const size_t bytes = (size_t)(gib * (1 << 30)) & ~(size_t)63;
+  const size_t nslots = bytes / 64;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  u32x4 *src;
+  uint16_t *gates;
+  uint32_t *sink;
+  CK(hipMalloc(&src, bytes));
+  CK(hipMalloc(&gates, nslots * 2));
+  CK(hipMalloc(&sink, 4096));
+  CK(hipMemset(src, 0x5a, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const char *names[3] = {"full16", "em32", "slot64"};
+  for (int shape = 0; shape < 3; shape++) {
+    for (int bpc : {1, 2, 4, 8}) {
+      const int blocks = cus * bpc;
+      auto launch = [&]() {
+        if (shape == 0)
+          hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
+                             bytes / 16, sink);
+        else if (shape == 1)
+          hipLaunchKernelGGL(em32, dim3(blocks), dim3(512), 0, 0, src, nslots,
+                             gates);
+        else
+          hipLaunchKernelGGL(slot64, dim3(blocks), dim3(512), 0, 0, src,
+                             nslots, gates);
+      };
+      for (int w = 0; w < 20; w++) launch();
+      CK(hipDeviceSynchronize());
+      std::vector<float> ms;
+      for (int r = 0; r < 5; r++) {
+        CK(hipEventRecord(e0, 0));
+        for (int k = 0; k < 20; k++) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t / 20);
+      }
+      std::sort(ms.begin(), ms.end());
+      const double t = ms[2] * 1e-3;
+      printf("{\"shape\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, "
+             "\"slab_TBps\": %.3f}\n",
+             names[shape], bpc, ms[2], bytes / t / 1e12);
+      fflush(stdout);
+    }
+  }
+  return 0;
+}

@@ -22,7 +22,8 @@ from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
-         "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF"]
+         "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF",
+         "BG_NO_SLAB", "BG_SLAB_PF"]
 
 
 def set_env(v):
@@ -67,9 +68,11 @@ def main():
         t.sync(0)
         ref = None
         variants = {
-            "default": {}, "ppl2": {"BG_PPL": 2}, "pf": {"BG_EM_PF": 1},
-            "pf_bpc3": {"BG_EM_PF": 1, "BG_BLOCKS_PER_CU": 3},
-            "bpc3": {"BG_BLOCKS_PER_CU": 3}, "l2tab": {"BG_NOLDS": 1},
+            "default": {}, "slab_pf2": {"BG_SLAB_PF": 2},
+            "slab_pf1_bpc1": {"BG_SLAB_PF": 1, "BG_BLOCKS_PER_CU": 1},
+            "slab_pf2_bpc1": {"BG_SLAB_PF": 2, "BG_BLOCKS_PER_CU": 1},
+            "slab_l2tab_pf2": {"BG_NOLDS": 1, "BG_SLAB_PF": 2},
+            "lane": {"BG_NO_SLAB": 1},
         }
         # every variant must give identical gates
         for name, env in variants.items():

@@ -28,17 +28,20 @@ def to_dev(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).to(dev)
 
 
-# launcher choices of where the table is probed: its own (LDS for tables
-# <= 40 KB on launches with >= 4096 packets per workgroup, else L2), forced
-# LDS, forced L2 (BG_* knobs of bg_kernels.hip)
-TABLE_PATHS = ({}, {"BG_FORCE_LDS": "1"}, {"BG_NOLDS": "1"})
+# launcher choices (BG_* knobs of bg_kernels.hip): where the table is probed
+# -- its own choice (LDS for tables <= 40 KB on launches with >= 4096 packets
+# per workgroup, else L2), forced LDS, forced L2 -- and, for dense 64 B
+# slots, the coalesced slab kernel (default) or the one-slot-per-lane one
+TABLE_PATHS = ({}, {"BG_FORCE_LDS": "1"}, {"BG_NOLDS": "1"},
+               {"BG_NO_SLAB": "1"}, {"BG_NO_SLAB": "1", "BG_FORCE_LDS": "1"})
 
 
 def classify_all_paths(t, d_frames, stride, n, default_gate, dev):
     """Gates from every table path; asserts they agree, returns them."""
     outs = []
     for env in TABLE_PATHS:
-        old = {k: os.environ.get(k) for k in ("BG_FORCE_LDS", "BG_NOLDS")}
+        old = {k: os.environ.get(k)
+               for k in ("BG_FORCE_LDS", "BG_NOLDS", "BG_NO_SLAB")}
         os.environ.update(env)
         try:
             d_g = torch.zeros(n, dtype=torch.int16, device=dev)
