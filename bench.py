@@ -376,7 +376,7 @@ def run_e2e_host(r, args, torch):
     out = np.zeros(n, np.uint16)
     from bess_amd._lib import lib
     res = {}
-    for B in (32, 1024, 65536, n):
+    for B in (32, 65536, n):
         lib().bg_em_process_host(t.h, heads, B, 8192, out.ctypes.data, None)
         reps = max(1, min(200, (1 << 22) // B))
         t0 = time.perf_counter()
@@ -395,6 +395,108 @@ def run_e2e_host(r, args, torch):
     return {"what": "ExactMatch from host snbufs: gather windows -> pinned "
                     "-> H2D -> kernel -> D2H, synchronous per batch",
             "Mpps_by_batch": res}
+
+
+def _pipe_rate(make_pipe, heads, lens, threads, reps, burst=32):
+    """aggregate Mpps of `threads` BESS-style workers, each with its own
+    bg_pipe over the shared packet pool (its own rotation of it), each
+    running the native worker loop (bg_pipe_run) `reps` times"""
+    import threading
+    n = len(heads)
+    pipes = [make_pipe() for _ in range(threads)]
+    rots = [np.roll(heads, -(i * n) // threads) for i in range(threads)]
+    lrots = [None if lens is None else np.roll(lens, -(i * n) // threads)
+             for i in range(threads)]
+    for p, h, ln in zip(pipes, rots, lrots):  # warm: staging, tables, caches
+        p.run(h[:65536], None if ln is None else ln[:65536])
+    errs = []
+
+    def work(p, h, ln):
+        try:
+            for _ in range(reps):
+                p.run(h, ln, burst=burst)
+        except Exception as e:  # reported below
+            errs.append(e)
+    ths = [threading.Thread(target=work, args=a) for a in zip(pipes, rots, lrots)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    for p in pipes:
+        p.close()
+    if errs:
+        raise errs[0]
+    return round(threads * reps * n / dt / 1e6, 1)
+
+
+def run_e2e_pipe(args, torch):
+    """End-to-end from host memory through the aggregation queue (bg_pipe):
+    packets in snbuf-like host buffers (2624 B objects, frame at +512) are
+    submitted 32 per ProcessBatch call by native worker loops; each worker's
+    pipe gathers the bytes the device reads into pinned slots of `batch`
+    packets and runs H2D -> kernel -> D2H on 4 streams; gates come back in
+    submission order. Parity: the gates of one pass vs the oracle."""
+    from bess_amd import packets as P
+    from bess_amd.modules import ExactMatch, L4Checksum, Pipe
+    from oracle import oracle as O
+    out = {"burst": 32, "depth": 4,
+           "host_cpus_used": "1 worker thread per pipe"}
+    # ExactMatch, C2 rules, 64 B packets
+    n = 1 << 20
+    keys, gates, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=77)
+    fields = [{"offset": o, "num_bytes": s} for o, s in P.FIVE_TUPLE]
+    m = ExactMatch(fields=fields)
+    om = O.OracleExactMatch(fields=fields)
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    for k, g in zip(keys, gates):
+        kb = k.tobytes()
+        v = [{"value_bin": kb[a:c]} for a, c in cut]
+        m.add(fields=v, gate=int(g))
+        om.add(fields=v, gate=int(g))
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + 64] = frames
+    heads = snb.ctypes.data + 512 + 2624 * np.arange(n, dtype=np.uintp)
+    want = om.process(frames, 64, n)
+    del frames
+    em = {}
+    for batch in (4096, 65536):
+        p = Pipe(m, batch=batch, depth=4)
+        em["parity_batch%d" % batch] = bool((p.run(heads) == want).all())
+        p.close()
+        rates = {}
+        for th in (1, 4, 16):
+            rates[str(th)] = _pipe_rate(
+                lambda: Pipe(m, batch=batch, depth=4), heads, None, th,
+                reps=2 if th == 1 else 4)
+        em["Mpps_by_threads_batch%d" % batch] = rates
+    out["ExactMatch_64B"] = em
+    del snb
+    # L4Checksum (recompute), 1500 B packets: frames H2D, header lines back
+    n = 1 << 17
+    cf = P.cksum_workload(n, frame_len=1496)
+    ref = cf.copy()
+    _, l4w = O.cksum_process(ref, 2048, n, 2, False)
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + 2048] = cf
+    heads = snb.ctypes.data + 512 + 2624 * np.arange(n, dtype=np.uintp)
+    lens = np.full(n, 1496, np.uint16)
+    mk = L4Checksum(verify=False)
+    p = Pipe(mk, batch=8192, depth=4, span=1504)
+    g = p.run(heads, lens)
+    p.close()
+    ck = {"parity": bool((g == l4w).all() and
+                         (snb[:, 512:512 + 1496] == ref[:, :1496]).all())}
+    rates = {}
+    for th in (1, 4, 16):
+        rates[str(th)] = _pipe_rate(
+            lambda: Pipe(mk, batch=8192, depth=4, span=1504), heads, lens, th,
+            reps=4)
+    ck["Mpps_by_threads_batch8192"] = rates
+    ck["bytes_per_pkt_pcie"] = {"h2d": 1504, "d2h": 130}
+    out["L4Checksum_1500B"] = ck
+    return out
 
 
 def run_wm(args, dev, torch):
@@ -575,6 +677,9 @@ def main():
     if args.only == "c5":
         log(json.dumps(run_c5(args, dev, torch)))
         return
+    if args.only == "pipe":
+        log(json.dumps(run_e2e_pipe(args, torch)))
+        return
 
     r = run_em(args, rank, world, dev, torch, dist)
     n_total = r["n"] * world
@@ -620,6 +725,10 @@ def main():
             out["e2e_host"] = run_e2e_host(r, args, torch)
         except Exception as e:
             out["e2e_host"] = "failed: %r" % (e,)
+        try:
+            out["e2e_pipe"] = run_e2e_pipe(args, torch)
+        except Exception as e:
+            out["e2e_pipe"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)

@@ -83,6 +83,19 @@ _SIGS = {
     "bg_module_set_device": (_int, [_vp, _int]),
     "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
     "bg_debug_key": (_int, [C.POINTER(bg_field), _int, _int, _vp, _vp]),
+    "bg_em_classify_window": (_int, [_vp, _vp, _sz, _sz, _int, _u16, _vp, _vp]),
+    "bg_em_window": (None, [_vp, C.POINTER(_int), C.POINTER(_int)]),
+    "bg_wm_classify_window": (_int, [_vp, _vp, _sz, _sz, _int, _u16, _vp, _vp]),
+    "bg_wm_window": (None, [_vp, C.POINTER(_int), C.POINTER(_int)]),
+    "bg_pipe_create": (_int, [_vp, _int, _sz, _int, _sz, C.POINTER(_vp)]),
+    "bg_pipe_destroy": (None, [_vp]),
+    "bg_pipe_window": (_int, [_vp, C.POINTER(_int), C.POINTER(_int),
+                              C.POINTER(_sz)]),
+    "bg_pipe_submit": (_int, [_vp, _vp, _vp, _vp, _sz]),
+    "bg_pipe_flush": (_int, [_vp]),
+    "bg_pipe_poll": (C.c_long, [_vp, _int, _vp, _vp, _sz]),
+    "bg_pipe_pending": (_sz, [_vp]),
+    "bg_pipe_run": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
 }
 
 _lib = None

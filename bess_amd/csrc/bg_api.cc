@@ -31,13 +31,6 @@ int fail(int code, const char *fmt, ...) {
   return -code;
 }
 
-#define HIP_TRY(expr)                                                  \
-  do {                                                                 \
-    hipError_t e_ = (expr);                                            \
-    if (e_ != hipSuccess)                                              \
-      return fail(EIO, "%s: %s", #expr, hipGetErrorString(e_));        \
-  } while (0)
-
 int num_cus(int device) {
   static std::mutex mu;
   static std::unordered_map<int, int> cache;
@@ -530,7 +523,15 @@ static int no_attr_datapath() {
 int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
                    uint16_t default_gate, uint16_t *d_gates,
                    bg_stream_t stream) {
+  return bg_em_classify_window(em, d_frames, stride, n, 0, default_gate,
+                               d_gates, stream);
+}
+
+int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
+                          size_t n, int win_off, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream) {
   if (em->has_attr) return no_attr_datapath();
+  if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   hipStream_t s = (hipStream_t)stream;
@@ -545,7 +546,7 @@ int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
   }
   int r = set_device(dev);
   if (r) return r;
-  return em_launch(em, d_frames, stride, n, default_gate, d_gates, 0, s);
+  return em_launch(em, d_frames, stride, n, default_gate, d_gates, -win_off, s);
 }
 
 // Stage [lo, hi) of every head (window covering all fields) at a fixed
@@ -595,6 +596,22 @@ int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
   HIP_TRY(hipStreamSynchronize(s));
   memcpy(gates, em->stage.h_out, n * 2);
   return 0;
+}
+
+static void fields_window(const std::vector<bg_field> &fields, int *lo,
+                          int *hi) {
+  int l = 1 << 30, h = 0;
+  for (auto &f : fields) {
+    l = std::min(l, f.offset);
+    h = std::max(h, f.offset + f.size);
+  }
+  if (fields.empty()) l = h = 0;
+  *lo = l;
+  *hi = h;
+}
+
+void bg_em_window(const bg_em *em, int *lo, int *hi) {
+  fields_window(em->fields, lo, hi);
 }
 
 int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes) {
@@ -860,7 +877,15 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
 int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
                    uint16_t default_gate, uint16_t *d_gates,
                    bg_stream_t stream) {
+  return bg_wm_classify_window(wm, d_frames, stride, n, 0, default_gate,
+                               d_gates, stream);
+}
+
+int bg_wm_classify_window(bg_wm *wm, const void *d_frames, size_t stride,
+                          size_t n, int win_off, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream) {
   if (wm->has_attr) return no_attr_datapath();
+  if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   hipStream_t s = (hipStream_t)stream;
@@ -873,7 +898,7 @@ int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
   }
   int r = set_device(wm->dev.device);
   if (r) return r;
-  return wm_launch(wm, d_frames, stride, n, default_gate, d_gates, 0, s);
+  return wm_launch(wm, d_frames, stride, n, default_gate, d_gates, -win_off, s);
 }
 
 int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
@@ -902,6 +927,10 @@ int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
   HIP_TRY(hipStreamSynchronize(s));
   memcpy(gates, wm->stage.h_out, n * 2);
   return 0;
+}
+
+void bg_wm_window(const bg_wm *wm, int *lo, int *hi) {
+  fields_window(wm->fields, lo, hi);
 }
 
 int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds) {

@@ -36,6 +36,13 @@ struct WmVal {  // WmData (wildcard_match.h:57-60)
 
 extern thread_local std::string g_err;
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#define HIP_TRY(expr)                                                  \
+  do {                                                                 \
+    hipError_t e_ = (expr);                                            \
+    if (e_ != hipSuccess)                                              \
+      return ::bg::fail(EIO, "%s: %s", #expr, hipGetErrorString(e_));  \
+  } while (0)
 int num_cus(int device);
 int set_device(int device);
 uint32_t round_kw(uint32_t key_bytes);

@@ -688,6 +688,15 @@ void wm_classify_kernel(WmArgs a) {
   wm_body<KW, NCH, PPL, 1, 8, true>(a, lds);
 }
 
+// 1024-thread workgroups: one LDS key-filter copy serves 16 waves
+// (A/B: BG_WM_BLOCK=1024)
+template <int PPL>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_sgpr(80)))
+void wm_classify_k1024_kernel(WmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  wm_body<2, 2, PPL, 1, 8, PPL == 1>(a, lds);
+}
+
 // A/B variants for the 5-tuple shape (BG_WM_V / BG_WM_G)
 template <int PPL, int V, int G, bool PF>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
@@ -1331,10 +1340,10 @@ int occupancy(const void *kernel, int block, size_t lds, int dflt) {
 
 template <typename Args, typename K>
 hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
-                           int ppl) {
+                           int ppl, int block = kEmBlock) {
   if (a.n == 0) return hipSuccess;
   if (env_int("BG_NOLDS", 0)) a.t.lds = 0;
-  const uint64_t need = (a.n + (uint64_t)kEmBlock * ppl - 1) / ((uint64_t)kEmBlock * ppl);
+  const uint64_t need = (a.n + (uint64_t)block * ppl - 1) / ((uint64_t)block * ppl);
   // Measured on MI355X (scripts/variants.py): with the table in LDS two
   // 512-thread blocks per CU (16 waves) stream fastest -- fewer LDS table
   // fills; with the table in L2/MALL, twice the resident grid.
@@ -1346,7 +1355,7 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
     int pc = per_cu;
     if (pc <= 0) {
       const int occ =
-          occupancy(reinterpret_cast<const void *>(kernel), kEmBlock, lds, 2);
+          occupancy(reinterpret_cast<const void *>(kernel), block, lds, 2);
       pc = a.t.lds ? std::min(occ, 2) : occ * 2;
       pc *= std::max(1, env_int("BG_GRID_MULT", 1));
     }
@@ -1357,7 +1366,7 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
       a.t.lds = 0;  // small launch: probe the table in L2 instead
       continue;
     }
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kEmBlock), lds, s, a);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(block), lds, s, a);
     return hipGetLastError();
   }
   return hipErrorInvalidValue;
@@ -1457,6 +1466,11 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
 }
 
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
+  if (env_int("BG_WM_BLOCK", 512) == 1024 && a.t.kw == 2 && fits_nch2(a.fp)) {
+    if (env_int("BG_PPL", 1) == 2)
+      return launch_classify(wm_classify_k1024_kernel<2>, a, num_cus, s, 2, 1024);
+    return launch_classify(wm_classify_k1024_kernel<1>, a, num_cus, s, 1, 1024);
+  }
   const int v = env_int("BG_WM_V", 0), g = env_int("BG_WM_G", 4);
   if (v && a.t.kw == 2 && fits_nch2(a.fp)) {
     const int ppl = env_int("BG_PPL", 2);

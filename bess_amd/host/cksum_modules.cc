@@ -53,6 +53,14 @@ class ChecksumModule : public Module {
     return 0;
   }
 
+  // the whole frame goes to the device; the recomputed checksum words come
+  // back (bg_pipe writes the header line back into the packet buffer)
+  void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
+    *lo = 0;
+    *hi = 2048;
+    *writeback = true;
+  }
+
   int ProcessDevice(void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_cksum(device_, d_frames, stride, n, kMode, verify_ ? 1 : 0,

@@ -124,6 +124,19 @@ class ExactMatch final : public Module {
                           stream);
   }
 
+  void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
+    bg_em_window(table_, lo, hi);
+    *writeback = false;
+  }
+
+  int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n, int win_off,
+                          uint16_t *d_ogates, void *stream) override {
+    int rc = bg_em_sync(table_, device_, stream);
+    if (rc < 0) return rc;
+    return bg_em_classify_window(table_, d_win, wstride, n, win_off,
+                                 default_gate_, d_ogates, stream);
+  }
+
   // exact_match.cc:122-147
   CommandResponse GetInitialArg(const EmptyArg &) {
     ExactMatchArg r;

@@ -64,12 +64,6 @@ std::vector<std::string> ModuleBuilder::Classes() {
   return v;
 }
 
-struct bg_module {
-  std::unique_ptr<Module> m;
-  std::string mclass;
-  std::mutex mu;  // commands vs. process (THREAD_UNSAFE commands)
-};
-
 using bg::fail;
 
 static int respond(const CommandResponse &r) {

@@ -21,6 +21,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -144,6 +145,22 @@ class Module {
   // Device-resident datapath over a frame slab (libbessgpu.so).
   virtual int ProcessDevice(void *d_frames, size_t stride, size_t n,
                             uint16_t *d_ogates, void *stream) = 0;
+  // Host ingress/egress staging (bg_pipe, bess_amd/host/pipe.cc): the frame
+  // bytes [*lo, *hi) the device datapath reads, and whether it writes frame
+  // bytes that must go back into the packet buffers.
+  virtual void DeviceWindow(int *lo, int *hi, bool *writeback) const {
+    *lo = 0;
+    *hi = 2048;  // SNBUF_DATA (core/snbuf_layout.h:34-68)
+    *writeback = false;
+  }
+  // ProcessDevice over staged windows: byte 0 of window i is frame offset
+  // `win_off` of packet i.
+  virtual int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n,
+                                  int win_off, uint16_t *d_ogates,
+                                  void *stream) {
+    if (win_off != 0) return -EINVAL;
+    return ProcessDevice(d_win, wstride, n, d_ogates, stream);
+  }
   void set_device(int d) { device_ = d; }
   int device() const { return device_; }
 
@@ -217,5 +234,12 @@ ModuleBuilder::Factory MakeFactory() {
 #define ADD_MODULE_ARG(_MOD, _ARG, _NAME_TEMPLATE, _HELP)                     \
   static bool __module__##_MOD = ModuleBuilder::RegisterModuleClass(          \
       #_MOD, _NAME_TEMPLATE, _HELP, MakeFactory<_MOD, _ARG>());
+
+// The C ABI's module handle (include/bessgpu.h bg_module_*).
+struct bg_module {
+  std::unique_ptr<Module> m;
+  std::string mclass;
+  std::mutex mu;  // commands vs. process (THREAD_UNSAFE commands)
+};
 
 #endif  // BESS_AMD_HOST_MODULE_H_

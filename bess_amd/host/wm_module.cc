@@ -112,6 +112,19 @@ class WildcardMatch final : public Module {
                           stream);
   }
 
+  void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
+    bg_wm_window(table_, lo, hi);
+    *writeback = false;
+  }
+
+  int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n, int win_off,
+                          uint16_t *d_ogates, void *stream) override {
+    int rc = bg_wm_sync(table_, device_, stream);
+    if (rc < 0) return rc;
+    return bg_wm_classify_window(table_, d_win, wstride, n, win_off,
+                                 default_gate_, d_ogates, stream);
+  }
+
   // wildcard_match.cc:317-354
   CommandResponse CommandAdd(const WildcardMatchCommandAddArg &arg) {
     const gate_idx_t gate = (gate_idx_t)arg.gate();

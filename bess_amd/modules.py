@@ -159,3 +159,83 @@ class IPChecksum(Module):
 class L4Checksum(Module):
     """core/modules/l4_checksum.cc on the GPU."""
     mclass = "L4Checksum"
+
+
+class Pipe:
+    """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
+    are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered
+    into pinned slots of `batch` packets, launched H2D -> device -> D2H on
+    `depth` streams, and returned by poll() in submission order with their
+    EmitPacket gate (core/modules/queue.cc:173/190 split)."""
+
+    def __init__(self, module, device=0, batch=4096, depth=4, span=0):
+        h = C.c_void_p()
+        _check(lib().bg_pipe_create(module.h, device, batch, depth, span,
+                                    C.byref(h)))
+        self.h = h
+        self.module = module  # keep the module alive while the pipe is
+
+    def close(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_pipe_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def window(self):
+        lo, hi, st = C.c_int(), C.c_int(), C.c_size_t()
+        lib().bg_pipe_window(self.h, C.byref(lo), C.byref(hi), C.byref(st))
+        return lo.value, hi.value, st.value
+
+    def submit(self, heads, lens=None, cookies=None):
+        """heads: numpy uintp array of head_data() addresses."""
+        heads = np.ascontiguousarray(heads, dtype=np.uintp)
+        n = len(heads)
+        lp = None
+        if lens is not None:
+            lens = np.ascontiguousarray(lens, dtype=np.uint16)
+            lp = lens.ctypes.data
+        cp = None
+        if cookies is not None:
+            cookies = np.ascontiguousarray(cookies, dtype=np.uintp)
+            cp = cookies.ctypes.data
+        _check(lib().bg_pipe_submit(self.h, heads.ctypes.data, lp, cp, n))
+
+    def flush(self):
+        _check(lib().bg_pipe_flush(self.h))
+
+    def poll(self, wait=False, cap=1 << 16):
+        """-> (cookies uintp array, gates uint16 array)"""
+        ck = np.empty(cap, np.uintp)
+        g = np.empty(cap, np.uint16)
+        k = _check(lib().bg_pipe_poll(self.h, 1 if wait else 0, ck.ctypes.data,
+                                      g.ctypes.data, cap))
+        return ck[:k], g[:k]
+
+    def pending(self):
+        return lib().bg_pipe_pending(self.h)
+
+    def run(self, heads, lens=None, burst=32):
+        """native worker loop over all packets (bg_pipe_run); -> gates"""
+        heads = np.ascontiguousarray(heads, dtype=np.uintp)
+        n = len(heads)
+        og = np.full(n, BG_GATE_NONE, np.uint16)
+        lp = None
+        if lens is not None:
+            lens = np.ascontiguousarray(lens, dtype=np.uint16)
+            lp = lens.ctypes.data
+        _check(lib().bg_pipe_run(self.h, heads.ctypes.data, lp, n, burst,
+                                 og.ctypes.data))
+        return og
+
+    def drain(self):
+        """flush and wait for everything submitted"""
+        self.flush()
+        cs, gs = [], []
+        while self.pending():
+            c, g = self.poll(wait=True)
+            cs.append(c)
+            gs.append(g)
+        if not cs:
+            return np.empty(0, np.uintp), np.empty(0, np.uint16)
+        return np.concatenate(cs), np.concatenate(gs)

@@ -105,6 +105,13 @@ int bg_em_build_part(bg_em *em, int part, void *host_dst);
 int bg_em_attach(bg_em *em, int device, const void *d_image);
 /* bytes of the current device table image and whether it lives in LDS */
 int bg_em_table_info(const bg_em *em, uint64_t *bytes, int *in_lds);
+/* Classify staged windows: byte 0 of window i (at d_win + i*stride) is frame
+ * offset win_off of packet i (the host path stages only the field window). */
+int bg_em_classify_window(bg_em *em, const void *d_win, size_t stride,
+                          size_t n, int win_off, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream);
+/* [lo, hi): the frame bytes the fields cover (MakeKeys reads) */
+void bg_em_window(const bg_em *em, int *lo, int *hi);
 
 /* ---- WildcardMatch ----------------------------------------------------- */
 typedef struct bg_wm bg_wm;
@@ -133,6 +140,10 @@ int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
                        bg_stream_t stream);
 /* in_lds: 0 table probed in L2/MALL, 1 table in LDS, 2 key filter in LDS */
 int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds);
+int bg_wm_classify_window(bg_wm *wm, const void *d_win, size_t stride,
+                          size_t n, int win_off, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream);
+void bg_wm_window(const bg_wm *wm, int *lo, int *hi);
 
 /* ---- IPChecksum / L4Checksum ------------------------------------------ */
 /* mode: BG_CK_IP, BG_CK_L4 or both (= IPChecksum -> L4Checksum pipeline:
@@ -181,6 +192,42 @@ int bg_module_process_device(bg_module *m, void *d_frames, size_t stride,
 int bg_module_set_device(bg_module *m, int device);
 /* GetDesc() (exact_match.cc:246-249, wildcard_match.cc:205-213) */
 int bg_module_desc(const bg_module *m, char *buf, size_t len);
+
+/* ---- Asynchronous host ingress/egress: the aggregation queue ------------
+ * Replaces the per-call synchronous host path for BESS pipelines, where a
+ * module receives <= 32 packets per ProcessBatch (core/pktbatch.h:70). Like
+ * the Queue module (core/modules/queue.cc:173 enqueue in ProcessBatch, 190
+ * emit from RunTask), submit() enqueues and poll() returns finished packets:
+ *   submit: gathers each packet's device bytes (the field window for
+ *           ExactMatch/WildcardMatch; the frame for IP/L4Checksum, span
+ *           bytes at most, data_len when lens != NULL) into a pinned slot;
+ *           a full slot (batch packets) is launched on its own HIP stream:
+ *           H2D -> device ProcessBatch -> D2H (gates [+ header lines]).
+ *           Blocks only when all `depth` slots are in flight.
+ *   flush:  launches the partially filled slot (a RunTask deadline).
+ *   poll:   completed packets in submission order: cookie (default: the
+ *           head pointer) and the gate EmitPacket would get (BG_GATE_NONE:
+ *           not emitted); checksum modules' recomputed header lines are
+ *           written back into the packet buffers first. wait != 0 blocks
+ *           until a launched slot completes (returns 0 if none in flight).
+ * Packets stay owned by the caller until poll returns them. One pipe per
+ * worker thread; pipes may share a module. */
+typedef struct bg_pipe bg_pipe;
+int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
+                   size_t span, bg_pipe **out);
+void bg_pipe_destroy(bg_pipe *p); /* waits for in-flight slots */
+int bg_pipe_window(const bg_pipe *p, int *lo, int *hi, size_t *stride);
+int bg_pipe_submit(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
+                   void *const *cookies, size_t cnt);
+int bg_pipe_flush(bg_pipe *p);
+long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
+                  size_t cap);
+size_t bg_pipe_pending(const bg_pipe *p);
+/* A worker loop (Source -> module -> Sink): n packets submitted in bursts of
+ * `burst`, completions polled after each submit; ogates[i] = packet i's
+ * gate. Returns when all n are back. */
+int bg_pipe_run(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
+                size_t n, size_t burst, uint16_t *ogates);
 
 #ifdef __cplusplus
 }

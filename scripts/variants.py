@@ -23,7 +23,7 @@ from bess_amd import packets as P  # noqa: E402
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF",
-         "BG_NO_SLAB", "BG_SLAB_PF"]
+         "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK"]
 
 
 def set_env(v):
@@ -88,6 +88,39 @@ def main():
             r[k]["GBps_66B"] = round(66 * n / (r[k]["median_ms"] * 1e-3) / 1e9, 1)
         out["em"] = r
         del d, g
+    if "c5" in which:
+        n = 16 << 20
+        keys, gates, frames = P.em_workload(1 << 20, n)
+        d = torch.from_numpy(frames.reshape(-1)).to(dev)
+        del frames
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        t = F.EmTable(P.em_fields_5tuple())
+        t.add_many(keys, gates)
+        t.sync(0)
+        variants = {
+            "default": {}, "slab_pf2": {"BG_SLAB_PF": 2},
+            "slab_pf0": {"BG_SLAB_PF": 0},
+            "slab_bpc2": {"BG_BLOCKS_PER_CU": 2},
+            "slab_bpc4": {"BG_BLOCKS_PER_CU": 4},
+            "lane_p1": {"BG_NO_SLAB": 1, "BG_PPL": 1},
+            "lane_p2": {"BG_NO_SLAB": 1, "BG_PPL": 2},
+            "lane_p2_x2": {"BG_NO_SLAB": 1, "BG_PPL": 2, "BG_GRID_MULT": 2},
+            "lane_pf": {"BG_NO_SLAB": 1, "BG_EM_PF": 1},
+        }
+        ref = None
+        for name, env in variants.items():
+            set_env(env)
+            t.classify(d, 64, n, 8192, g)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = g.clone()
+            assert torch.equal(g, ref), name
+        r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants,
+                          reps=10)
+        for k in r:
+            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+        out["c5"] = r
+        del d, g
     if "ck" in which:
         n = 1 << 20
         frames = P.cksum_workload(n, frame_len=1496)
@@ -141,6 +174,10 @@ def main():
                     "g4_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 4, "BG_PPL": 1}),
                     "seq_pf_f128": (128, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "nofilter_seq_pf": (0, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
+                    "k1024": (64, {"BG_WM_BLOCK": 1024}),
+                    "k1024_p2": (64, {"BG_WM_BLOCK": 1024, "BG_PPL": 2}),
+                    "k1024_f128": (128, {"BG_WM_BLOCK": 1024}),
+                    "k1024_f32": (32, {"BG_WM_BLOCK": 1024}),
                     "nofilter_default": (0, {})}
         ref = None
         for name, (kb, env) in variants.items():
