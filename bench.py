@@ -499,6 +499,86 @@ def run_e2e_pipe(args, torch):
     return out
 
 
+def _time_steps(step, args, torch):
+    """warmup, then ms per launch over args.steps launches (HIP events on
+    the launching stream)"""
+    for _ in range(max(3, args.warmup // 4)):
+        step()
+    torch.cuda.synchronize()
+    timer = Timer(torch)
+    reps = max(10, args.steps // 4)
+    timer.start()
+    for _ in range(reps):
+        step()
+    return timer.stop_ms() / reps
+
+
+def _roof(bytes_per_pkt, n, ms, key=None):
+    gbs = bytes_per_pkt * n / (ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+         "bytes_per_pkt": bytes_per_pkt}
+    if key:
+        r["traffic"] = traffic_gbs(key, ms)
+        r["traffic_bytes_per_launch"] = load_traffic(key)
+    return r
+
+
+def _snbuf_sample(frames, n):
+    """the first n frames copied into snbuf-like objects (2624 B, +512):
+    the CPU reference's memory layout"""
+    w = min(frames.shape[1], 2048)
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + w] = frames[:n, :w]
+    return snb
+
+
+def run_hashlb(args, dev, torch):
+    """HashLB (core/modules/hash_lb.cc) on the C2 slab: 16M 64 B packets,
+    8 gates; l4 mode (the default) and a 5-tuple fields mode"""
+    from bess_amd import packets as P
+    from bess_amd.modules import HashLB
+    from oracle import oracle_more as OM
+    n = args.pkts
+    _, _, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=5)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    g = torch.empty(n, dtype=torch.int16, device=dev)
+    out = {"workload": "HashLB: 64B pkts (64B slots), 8 gates, %d resident "
+                       "pkts" % n, "pkts": n}
+    five = [{"offset": o, "num_bytes": s} for o, s in P.FIVE_TUPLE]
+    for name, kw in (("l4", dict(mode="l4")), ("fields_5tuple", dict(fields=five))):
+        m = HashLB(gates=list(range(8)), **kw)
+        o = OM.OracleHashLB(gates=list(range(8)), **kw)
+        m.process_device(d, 64, n, g)
+        torch.cuda.synchronize()
+        k = min(n, 1 << 20)
+        parity = bool((g[:k].cpu().numpy().view(np.uint16) ==
+                       o.process(frames, 64, k)).all())
+        ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+        out[name] = {"ms_per_step": round(ms, 4),
+                     "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+                     "roofline": _roof(EM_BYTES_PER_PKT, n, ms),
+                     "parity": "bit-exact vs oracle on %d pkts" % k
+                               if parity else "MISMATCH"}
+        if name == "l4" and not args.no_cpu:
+            cn = 1 << 18
+            snb = _snbuf_sample(frames, cn)
+            og = np.zeros(cn, np.uint16)
+            gt = np.array(o.gates_, np.uint16)
+            L = OM.mlib()
+            threads, res = cpu_rate(
+                lambda nt, reps: L.or_hashlb_bench(
+                    o.mode, None, 0, gt.ctypes.data, 8, snb.ctypes.data + 512,
+                    2624, cn, og.ctypes.data, nt, reps), cn, args.cpu_seconds / 3)
+            out[name]["cpu_baseline"] = {
+                "value": round(res[threads], 2), "unit": "Mpps",
+                "cores": threads, "kind": "port",
+                "single_core_mpps": round(res[1], 2),
+                "sample": "%d 64B pkts x reps in snbuf layout, HashLB l4 "
+                          "(SSE4.2 CRC32C)" % cn}
+    return out
+
+
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
@@ -677,6 +757,9 @@ def main():
     if args.only == "c5":
         log(json.dumps(run_c5(args, dev, torch)))
         return
+    if args.only == "hashlb":
+        log(json.dumps(run_hashlb(args, dev, torch)))
+        return
     if args.only == "pipe":
         log(json.dumps(run_e2e_pipe(args, torch)))
         return
@@ -729,7 +812,8 @@ def main():
             out["e2e_pipe"] = run_e2e_pipe(args, torch)
         except Exception as e:
             out["e2e_pipe"] = "failed: %r" % (e,)
-        for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5)):
+        for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
+                         ("HashLB", run_hashlb)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

@@ -96,6 +96,12 @@ _SIGS = {
     "bg_pipe_poll": (C.c_long, [_vp, _int, _vp, _vp, _sz]),
     "bg_pipe_pending": (_sz, [_vp]),
     "bg_pipe_run": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "bg_hlb_create": (_int, [_int, C.POINTER(bg_field), _int, C.POINTER(_vp)]),
+    "bg_hlb_destroy": (None, [_vp]),
+    "bg_hlb_set_mode": (_int, [_vp, _int, C.POINTER(bg_field), _int, _int]),
+    "bg_hlb_set_gates": (_int, [_vp, _vp, _sz, _sz]),
+    "bg_hlb_window": (None, [_vp, C.POINTER(_int), C.POINTER(_int)]),
+    "bg_hlb_classify": (_int, [_vp, _vp, _sz, _sz, _int, _vp, _vp]),
 }
 
 _lib = None

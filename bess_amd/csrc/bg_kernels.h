@@ -114,11 +114,27 @@ struct CkArgs {
   int32_t verify;
 };
 
+// HashLB (core/modules/hash_lb.cc): CRC32C of the mode's hash input, then
+// gates[(crc * num_gates) >> 32]. The CRC of an L-byte input with init 0 is
+// linear in the input bytes, so it is the XOR of one table entry per byte
+// position: crc = XOR_i crc_tab[i*256 + byte_i] (tables built on the host).
+constexpr int kHlbL2 = 0, kHlbL3 = 1, kHlbL4 = 2, kHlbFields = 3;
+struct HlbArgs {
+  const uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *out;
+  const uint32_t *crc_tab;  // L x 256
+  const uint16_t *gtab;     // max(num_gates, 1) entries
+  uint32_t mode, L, num_gates, ngtab;
+  FieldPlan fp;             // kHlbFields
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s);
 
 }  // namespace bg
 

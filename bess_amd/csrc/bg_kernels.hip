@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "bg_kernels.h"
+#include "bg_keys_dev.h"
 
 namespace bg {
 namespace {
@@ -25,15 +26,6 @@ namespace {
 constexpr int kEmBlock = 512;  // 8 waves; LDS tables <= 40 KB -> 4 blocks/CU
 constexpr int kCkBlock = 256;
 constexpr int kDefaultPpl = 1;
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// streaming (read-once) 16-byte load: nontemporal so packet bytes do not
-// evict the flow table from L2
-__device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
-  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
 
 __device__ __forceinline__ uint32_t compact_bytes(uint32_t m) {
   // bits 7, 15, 23, 31 -> bits 0..3
@@ -46,126 +38,6 @@ __device__ __forceinline__ uint32_t compact_bytes(uint32_t m) {
 __device__ __forceinline__ uint32_t tag_match(uint32_t tags, uint32_t tag) {
   uint32_t x = tags ^ (tag * 0x01010101u);
   return compact_bytes((x - 0x01010101u) & ~x & 0x80808080u);
-}
-
-// Key building (ExactMatchTable::MakeKeys exact_match_table.h:239-263 /
-// WildcardMatch::ProcessBatch wildcard_match.cc:169-197). The window
-// [win_lo, win_lo + 16*nch) of a frame is staged in registers with 16-byte
-// loads; each field is funnel-shifted out of it with a wave-uniform dword
-// index (s_set_gpr_idx, no scratch) and OR-ed into its key word(s).
-template <int NCH>
-__device__ __forceinline__ void load_window(const uint8_t *__restrict__ frame,
-                                            const FieldPlan &fp,
-                                            uint32_t (&w)[NCH * 4 + 2]) {
-  const uint4 *src = reinterpret_cast<const uint4 *>(frame + fp.win_lo);
-#pragma unroll
-  for (int c = 0; c < NCH; c++) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (c < fp.nch) v = ld_stream(src + c);
-    w[4 * c + 0] = v.x;
-    w[4 * c + 1] = v.y;
-    w[4 * c + 2] = v.z;
-    w[4 * c + 3] = v.w;
-  }
-  w[NCH * 4] = 0;
-  w[NCH * 4 + 1] = 0;
-}
-
-template <int KW>
-__device__ __forceinline__ void place_field(uint64_t v, int p,
-                                            uint64_t (&k)[KW]) {
-  const int pw = p >> 3, pb = (p & 7) * 8;
-#pragma unroll
-  for (int j = 0; j < KW; j++) {
-    if (j == pw) k[j] |= v << pb;
-    if (pb && j == pw + 1) k[j] |= v >> (64 - pb);
-  }
-}
-
-// Key from the byte-permute plan (FieldPlan::kd_*): per key dword one
-// v_perm_b32 per source dword pair (wave-uniform window index: s_set_gpr_idx,
-// no scratch) and one AND. ExactMatchTable::MakeKeys semantics (mask per
-// field, bytes past the key zero) are folded into selectors and masks.
-template <int KW, int NCH>
-__device__ __forceinline__ void extract_key(const uint32_t (&w)[NCH * 4 + 2],
-                                            const FieldPlan &fp,
-                                            uint64_t (&k)[KW]) {
-  // NCH == 2 kernels are only dispatched for plans with <= 2 permutes per
-  // key dword. Branch-free: unused permutes have all-zero selectors.
-  constexpr int kMaxOps = NCH == 2 ? 2 : 4;
-  uint32_t kd[2 * KW];
-#pragma unroll
-  for (int q = 0; q < 2 * KW; q++) {
-    const uint32_t dws = fp.kd_dw[q];
-    uint32_t x = 0;
-#pragma unroll
-    for (int o = 0; o < kMaxOps; o++) {
-      const uint32_t d = (dws >> (8 * o)) & 0xFF;
-      x |= __builtin_amdgcn_perm(w[d + 1], w[d], fp.kd_sel[o][q]);
-    }
-    kd[q] = x & fp.kd_mask[q];
-  }
-#pragma unroll
-  for (int j = 0; j < KW; j++) k[j] = (uint64_t)kd[2 * j + 1] << 32 | kd[2 * j];
-}
-
-// fields too far apart for one window: per-field aligned dword loads
-template <int KW>
-__device__ __forceinline__ void direct_key(const uint8_t *__restrict__ frame,
-                                           const FieldPlan &fp,
-                                           uint64_t (&k)[KW]) {
-#pragma unroll
-  for (int j = 0; j < KW; j++) k[j] = 0;
-#pragma unroll
-  for (int f = 0; f < kMaxFields; f++) {
-    if (f < fp.nf) {
-      const uint32_t spec = fp.fspec[f];
-      const uint32_t *q =
-          reinterpret_cast<const uint32_t *>(frame) + fspec_d(spec);
-      const int nd = fspec_nd(spec), sh = fspec_shift_bits(spec);
-      uint32_t d0 = q[0];
-      uint32_t d1 = nd > 1 ? q[1] : 0u;
-      uint32_t d2 = nd > 2 ? q[2] : 0u;
-      uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
-      uint64_t v = sh ? ((lo >> sh) | ((uint64_t)d2 << (64 - sh))) : lo;
-      place_field<KW>(v & fp.fmask[f], fspec_pos(spec), k);
-    }
-  }
-}
-
-// Keys of PPL packets handled by one lane (idx = base + j*blockDim.x): all
-// window loads are issued before any key is built (memory-level parallelism).
-template <int KW, int NCH, int PPL>
-__device__ __forceinline__ void build_keys(const uint8_t *__restrict__ frames,
-                                           uint64_t stride, uint64_t n,
-                                           uint64_t base, const FieldPlan &fp,
-                                           uint64_t (&k)[PPL][KW]) {
-  if constexpr (NCH > 0) {
-    uint32_t w[PPL][NCH * 4 + 2];
-#pragma unroll
-    for (int j = 0; j < PPL; j++) {
-      const uint64_t idx = base + (uint64_t)j * blockDim.x;
-      if (idx < n) {
-        load_window<NCH>(frames + idx * stride, fp, w[j]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < NCH * 4 + 2; q++) w[j][q] = 0;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < PPL; j++) extract_key<KW, NCH>(w[j], fp, k[j]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < PPL; j++) {
-      const uint64_t idx = base + (uint64_t)j * blockDim.x;
-      if (idx < n) {
-        direct_key<KW>(frames + idx * stride, fp, k[j]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < KW; q++) k[j][q] = 0;
-      }
-    }
-  }
 }
 
 template <int KW>

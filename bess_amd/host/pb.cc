@@ -281,5 +281,138 @@ void VerifyArg::Write(Writer &w) const {
   if (verify_) w.varint_field(1, 1);
 }
 
+// ---- HashLB / ACL / IPLookup -------------------------------------------
+namespace {
+bool read_str(Reader &r, uint32_t wt, std::string *s) {
+  if (wt != kLen) return r.skip(wt);
+  const uint8_t *d;
+  size_t n;
+  if (!r.bytes(&d, &n)) return false;
+  s->assign(reinterpret_cast<const char *>(d), n);
+  return true;
+}
+bool read_bool(Reader &r, uint32_t wt, bool *b) {
+  uint64_t v;
+  if (wt != kVarint) return r.skip(wt);
+  if (!r.varint(&v)) return false;
+  *b = v != 0;
+  return true;
+}
+bool read_u32(Reader &r, uint32_t wt, uint32_t *x) {
+  uint64_t v;
+  if (wt != kVarint) return r.skip(wt);
+  if (!r.varint(&v)) return false;
+  *x = (uint32_t)v;
+  return true;
+}
+void write_str(Writer &w, uint32_t field, const std::string &s) {
+  if (!s.empty()) w.bytes_field(field, s.data(), s.size());
+}
+}  // namespace
+
+bool Int64List::Merge(Reader &r, uint32_t wt) {
+  uint64_t v;
+  if (wt == kVarint) {
+    if (!r.varint(&v)) return false;
+    v_.push_back((int64_t)v);
+    return true;
+  }
+  if (wt != kLen) return r.skip(wt);
+  const uint8_t *d;
+  size_t n;
+  if (!r.bytes(&d, &n)) return false;
+  Reader sub(d, n);
+  while (!sub.done()) {
+    if (!sub.varint(&v)) return false;
+    v_.push_back((int64_t)v);
+  }
+  return true;
+}
+
+void Int64List::Write(Writer &w, uint32_t field) const {
+  if (v_.empty()) return;
+  Writer packed;
+  for (int64_t x : v_) packed.raw_varint((uint64_t)x);
+  w.bytes_field(field, packed.str().data(), packed.str().size());
+}
+
+bool HashLBArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return gates_.Merge(r, wt);
+  if (field == 2) return read_str(r, wt, &mode_);
+  if (field == 3) return read_msg(r, wt, fields_.Add());
+  return r.skip(wt);
+}
+void HashLBArg::Write(Writer &w) const {
+  gates_.Write(w, 1);
+  write_str(w, 2, mode_);
+  for (auto &f : fields_) write_msg(w, 3, f);
+}
+
+bool HashLBCommandSetModeArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_str(r, wt, &mode_);
+  if (field == 2) return read_msg(r, wt, fields_.Add());
+  return r.skip(wt);
+}
+void HashLBCommandSetModeArg::Write(Writer &w) const {
+  write_str(w, 1, mode_);
+  for (auto &f : fields_) write_msg(w, 2, f);
+}
+
+bool HashLBCommandSetGatesArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return gates_.Merge(r, wt);
+  return r.skip(wt);
+}
+void HashLBCommandSetGatesArg::Write(Writer &w) const { gates_.Write(w, 1); }
+
+bool ACLArg_Rule::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  switch (field) {
+    case 1: return read_str(r, wt, &src_ip_);
+    case 2: return read_str(r, wt, &dst_ip_);
+    case 3: return read_u32(r, wt, &src_port_);
+    case 4: return read_u32(r, wt, &dst_port_);
+    case 5: return read_bool(r, wt, &established_);
+    case 6: return read_bool(r, wt, &drop_);
+    default: return r.skip(wt);
+  }
+}
+void ACLArg_Rule::Write(Writer &w) const {
+  write_str(w, 1, src_ip_);
+  write_str(w, 2, dst_ip_);
+  if (src_port_) w.varint_field(3, src_port_);
+  if (dst_port_) w.varint_field(4, dst_port_);
+  if (established_) w.varint_field(5, 1);
+  if (drop_) w.varint_field(6, 1);
+}
+
+bool ACLArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_msg(r, wt, rules_.Add());
+  return r.skip(wt);
+}
+void ACLArg::Write(Writer &w) const {
+  for (auto &x : rules_) write_msg(w, 1, x);
+}
+
+bool IPLookupArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_u32(r, wt, &max_rules_);
+  if (field == 2) return read_u32(r, wt, &max_tbl8s_);
+  return r.skip(wt);
+}
+void IPLookupArg::Write(Writer &w) const {
+  if (max_rules_) w.varint_field(1, max_rules_);
+  if (max_tbl8s_) w.varint_field(2, max_tbl8s_);
+}
+
+bool IPLookupCommandAddArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_str(r, wt, &prefix_);
+  if (field == 2) return read_u64(r, wt, &prefix_len_);
+  if (field == 3) return read_u64(r, wt, &gate_);
+  return r.skip(wt);
+}
+void IPLookupCommandAddArg::Write(Writer &w) const {
+  write_str(w, 1, prefix_);
+  if (prefix_len_) w.varint_field(2, prefix_len_);
+  if (gate_) w.varint_field(3, gate_);
+}
+
 }  // namespace pb
 }  // namespace bess

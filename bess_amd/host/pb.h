@@ -305,6 +305,144 @@ class VerifyArg : public Message {
 using IPChecksumArg = VerifyArg;
 using L4ChecksumArg = VerifyArg;
 
+// ---- HashLB / ACL / IPLookup --------------------------------
+// repeated int64 (proto3: packed on the wire; unpacked accepted too)
+class Int64List {
+ public:
+  int size() const { return (int)v_.size(); }
+  int64_t Get(int i) const { return v_[i]; }
+  int64_t operator[](int i) const { return v_[i]; }
+  void Add(int64_t x) { v_.push_back(x); }
+  bool Merge(Reader &r, uint32_t wt);
+  void Write(Writer &w, uint32_t field) const;
+  typename std::vector<int64_t>::const_iterator begin() const { return v_.begin(); }
+  typename std::vector<int64_t>::const_iterator end() const { return v_.end(); }
+
+ private:
+  std::vector<int64_t> v_;
+};
+
+// module_msg.proto:589-593
+class HashLBArg : public Message {
+ public:
+  const Int64List &gates() const { return gates_; }
+  Int64List *mutable_gates() { return &gates_; }
+  const std::string &mode() const { return mode_; }
+  void set_mode(const std::string &m) { mode_ = m; }
+  int fields_size() const { return fields_.size(); }
+  const Field &fields(int i) const { return fields_.Get(i); }
+  Field *add_fields() { return fields_.Add(); }
+  const Repeated<Field> &fields() const { return fields_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Int64List gates_;
+  std::string mode_;
+  Repeated<Field> fields_;
+};
+
+// module_msg.proto:116-119
+class HashLBCommandSetModeArg : public Message {
+ public:
+  const std::string &mode() const { return mode_; }
+  void set_mode(const std::string &m) { mode_ = m; }
+  int fields_size() const { return fields_.size(); }
+  const Field &fields(int i) const { return fields_.Get(i); }
+  Field *add_fields() { return fields_.Add(); }
+  Repeated<Field> *mutable_fields() { return &fields_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  std::string mode_;
+  Repeated<Field> fields_;
+};
+
+// module_msg.proto:126-128
+class HashLBCommandSetGatesArg : public Message {
+ public:
+  const Int64List &gates() const { return gates_; }
+  Int64List *mutable_gates() { return &gates_; }
+  int gates_size() const { return gates_.size(); }
+  int64_t gates(int i) const { return gates_.Get(i); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Int64List gates_;
+};
+
+// module_msg.proto:412-425
+class ACLArg_Rule : public Message {
+ public:
+  const std::string &src_ip() const { return src_ip_; }
+  const std::string &dst_ip() const { return dst_ip_; }
+  uint32_t src_port() const { return src_port_; }
+  uint32_t dst_port() const { return dst_port_; }
+  bool established() const { return established_; }
+  bool drop() const { return drop_; }
+  void set_src_ip(const std::string &v) { src_ip_ = v; }
+  void set_dst_ip(const std::string &v) { dst_ip_ = v; }
+  void set_src_port(uint32_t v) { src_port_ = v; }
+  void set_dst_port(uint32_t v) { dst_port_ = v; }
+  void set_drop(bool v) { drop_ = v; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  std::string src_ip_, dst_ip_;
+  uint32_t src_port_ = 0, dst_port_ = 0;
+  bool established_ = false, drop_ = false;
+};
+
+class ACLArg : public Message {
+ public:
+  int rules_size() const { return rules_.size(); }
+  const ACLArg_Rule &rules(int i) const { return rules_.Get(i); }
+  const Repeated<ACLArg_Rule> &rules() const { return rules_; }
+  ACLArg_Rule *add_rules() { return rules_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<ACLArg_Rule> rules_;
+};
+
+// module_msg.proto:614-617
+class IPLookupArg : public Message {
+ public:
+  uint32_t max_rules() const { return max_rules_; }
+  uint32_t max_tbl8s() const { return max_tbl8s_; }
+  void set_max_rules(uint32_t v) { max_rules_ = v; }
+  void set_max_tbl8s(uint32_t v) { max_tbl8s_ = v; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint32_t max_rules_ = 0, max_tbl8s_ = 0;
+};
+
+// module_msg.proto:136-140 (gate unused by delete, 147-150)
+class IPLookupCommandAddArg : public Message {
+ public:
+  const std::string &prefix() const { return prefix_; }
+  uint64_t prefix_len() const { return prefix_len_; }
+  uint64_t gate() const { return gate_; }
+  void set_prefix(const std::string &v) { prefix_ = v; }
+  void set_prefix_len(uint64_t v) { prefix_len_ = v; }
+  void set_gate(uint64_t v) { gate_ = v; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  std::string prefix_;
+  uint64_t prefix_len_ = 0, gate_ = 0;
+};
+using IPLookupCommandDeleteArg = IPLookupCommandAddArg;
+
+using UpdateTTLArg = EmptyArg;
+
 }  // namespace pb
 }  // namespace bess
 

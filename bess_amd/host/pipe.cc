@@ -288,6 +288,10 @@ int bg_pipe_run(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
   for (size_t i = 0; i < n; i += burst) {
     const size_t c = std::min(burst, n - i);
     for (size_t j = 0; j < c; j++) ck[j] = reinterpret_cast<void *>(i + j);
+    // the next ProcessBatch's packets: their header lines are in flight
+    // while this batch is gathered
+    for (size_t j = i + c; j < std::min(n, i + c + burst); j++)
+      __builtin_prefetch(heads[j] + p->lo);
     int r = bg_pipe_submit(p, heads + i, lens ? lens + i : nullptr, ck.data(), c);
     if (r < 0) return r;
     if (p->inflight && (r = emit(0)) < 0) return r;

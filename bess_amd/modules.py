@@ -161,6 +161,19 @@ class L4Checksum(Module):
     mclass = "L4Checksum"
 
 
+class HashLB(Module):
+    """core/modules/hash_lb.cc on the GPU."""
+    mclass = "HashLB"
+    cmds = {"set_mode": ("HashLBCommandSetModeArg", None),
+            "set_gates": ("HashLBCommandSetGatesArg", None)}
+
+    def set_mode(self, **kw):
+        return self.command("set_mode", **kw)
+
+    def set_gates(self, **kw):
+        return self.command("set_gates", **kw)
+
+
 class Pipe:
     """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
     are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered

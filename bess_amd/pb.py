@@ -63,6 +63,33 @@ _MESSAGES = [
     # module_msg.proto:997-999 / 1010-1012
     ("IPChecksumArg", [("verify", 1, _F.TYPE_BOOL, 1, None, None)]),
     ("L4ChecksumArg", [("verify", 1, _F.TYPE_BOOL, 1, None, None)]),
+    # module_msg.proto:589-593 / 116-119 / 126-128
+    ("HashLBArg", [("gates", 1, _F.TYPE_INT64, 3, None, None),
+                   ("mode", 2, _F.TYPE_STRING, 1, None, None),
+                   ("fields", 3, _F.TYPE_MESSAGE, 3, ".bess.pb.Field", None)]),
+    ("HashLBCommandSetModeArg", [
+        ("mode", 1, _F.TYPE_STRING, 1, None, None),
+        ("fields", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.Field", None)]),
+    ("HashLBCommandSetGatesArg", [("gates", 1, _F.TYPE_INT64, 3, None, None)]),
+    # module_msg.proto:412-425 (ACLArg.Rule as a top-level message; the
+    # wire bytes are the same)
+    ("ACLArg_Rule", [("src_ip", 1, _F.TYPE_STRING, 1, None, None),
+                     ("dst_ip", 2, _F.TYPE_STRING, 1, None, None),
+                     ("src_port", 3, _F.TYPE_UINT32, 1, None, None),
+                     ("dst_port", 4, _F.TYPE_UINT32, 1, None, None),
+                     ("established", 5, _F.TYPE_BOOL, 1, None, None),
+                     ("drop", 6, _F.TYPE_BOOL, 1, None, None)]),
+    ("ACLArg", [("rules", 1, _F.TYPE_MESSAGE, 3, ".bess.pb.ACLArg_Rule", None)]),
+    # module_msg.proto:614-617 / 136-140 / 147-150
+    ("IPLookupArg", [("max_rules", 1, _F.TYPE_UINT32, 1, None, None),
+                     ("max_tbl8s", 2, _F.TYPE_UINT32, 1, None, None)]),
+    ("IPLookupCommandAddArg", [("prefix", 1, _F.TYPE_STRING, 1, None, None),
+                               ("prefix_len", 2, _F.TYPE_UINT64, 1, None, None),
+                               ("gate", 3, _F.TYPE_UINT64, 1, None, None)]),
+    ("IPLookupCommandDeleteArg", [
+        ("prefix", 1, _F.TYPE_STRING, 1, None, None),
+        ("prefix_len", 2, _F.TYPE_UINT64, 1, None, None)]),
+    ("UpdateTTLArg", []),
 ]
 
 

@@ -168,6 +168,30 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 int bg_debug_key(const bg_field *fields, int nfields, int em_masks,
                  const uint8_t *frame, uint8_t *key_out);
 
+/* ---- HashLB (core/modules/hash_lb.cc) --------------------------------- */
+/* ProcessBatch 155-236: CRC32C of the mode's hash input (l2: MAC words,
+ * l3: IPs, l4: IPs + ports + proto, fields: MakeKeys key over
+ * total_key_size), gate = gates[(crc * num_gates) >> 32] (hash_range 53-68).
+ * l2/l3/l4 read the frame from offset 0 (slots of >= 16/64 bytes). */
+#define BG_HLB_L2 0
+#define BG_HLB_L3 1
+#define BG_HLB_L4 2
+#define BG_HLB_FIELDS 3
+#define BG_HLB_MAX_GATES 16384 /* hash_lb.h kMaxGates */
+typedef struct bg_hlb bg_hlb;
+int bg_hlb_create(int mode, const bg_field *fields, int nfields, bg_hlb **out);
+void bg_hlb_destroy(bg_hlb *h);
+/* hash_len: bytes hashed (fields mode); -1 = total_key_size of the fields */
+int bg_hlb_set_mode(bg_hlb *h, int mode, const bg_field *fields, int nfields,
+                    int hash_len);
+/* gate table gates[0..n) (n >= 1: the reference's gates_ prefix) and
+ * num_gates <= n. num_gates == 0: every packet takes gates[0]. */
+int bg_hlb_set_gates(bg_hlb *h, const uint16_t *gates, size_t n,
+                     size_t num_gates);
+void bg_hlb_window(const bg_hlb *h, int *lo, int *hi);
+int bg_hlb_classify(bg_hlb *h, const void *d_frames, size_t stride, size_t n,
+                    int win_off, uint16_t *d_gates, bg_stream_t stream);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".

@@ -519,6 +519,20 @@ int or_em_iter(const or_em *em, size_t *cursor, uint8_t key_out[OR_KEY_BYTES],
   return 1;
 }
 
+/* ExactMatchTable::MakeKeys (exact_match_table.h:239-263) for one packet;
+ * the key is zeroed first (the reference zeroes only the last key word;
+ * words past total_key_size are never read by its callers). */
+void or_em_make_key(const or_em *em, const uint8_t *head, uint64_t key[8]) {
+  memset(key, 0, 64);
+  for (size_t f = 0; f < em->num_fields; f++) {
+    uint64_t v = ld64(head + em->fields[f].offset) & em->fields[f].mask;
+    uint8_t tmp[16];
+    memcpy(tmp, &v, 8);
+    int pos = em->fields[f].pos;
+    memcpy((uint8_t *)key + pos, tmp, (size_t)(pos + 8 <= 64 ? 8 : 64 - pos));
+  }
+}
+
 /* MakeKeys 239-263 + ExactMatch::ProcessBatch 224-244 + Find 273-278 */
 void or_em_process_batch(const or_em *em, const uint8_t *const *heads, int cnt,
                          uint16_t default_gate, uint16_t *gates) {

@@ -64,6 +64,8 @@ int or_em_iter(const or_em *em, size_t *cursor, uint8_t key_out[OR_KEY_BYTES],
  * packets given their head_data() pointers. gates[i] = EmitPacket gate. */
 void or_em_process_batch(const or_em *em, const uint8_t *const *heads, int cnt,
                          uint16_t default_gate, uint16_t *gates);
+/* MakeKeys for one packet (key zero-filled past the fields) */
+void or_em_make_key(const or_em *em, const uint8_t *head, uint64_t key[8]);
 /* the same over n packets at base + i*stride, in kMaxBurst batches */
 void or_em_process(const or_em *em, const uint8_t *base, size_t stride,
                    size_t n, uint16_t default_gate, uint16_t *gates);
@@ -126,6 +128,25 @@ void or_l4_checksum_batch(uint8_t *const *heads, int cnt, int verify,
  * L4Checksum). ip_gates / l4_gates may be NULL. */
 void or_cksum_process(uint8_t *base, size_t stride, size_t n, int mode,
                       int verify, uint16_t *ip_gates, uint16_t *l4_gates);
+
+/* ---- HashLB (core/modules/hash_lb.cc) -- oracle_more.c ----------------- */
+#define OR_HLB_L2 0
+#define OR_HLB_L3 1
+#define OR_HLB_L4 2
+#define OR_HLB_FIELDS 3
+/* hash_range 53-68 */
+uint16_t or_hash_range(uint32_t hashval, uint16_t range);
+/* HashLB::DoProcessBatch<mode> 140-236: out[i] = gates[hash_range(hash,
+ * num_gates)]; fields mode: MakeKeys of `fields` (an or_em whose fields were
+ * added with mask 0) hashed over hash_len bytes (ExactMatchKeyHash). */
+void or_hashlb_process(int mode, const or_em *fields, size_t hash_len,
+                       const uint16_t *gates, size_t num_gates,
+                       const uint8_t *base, size_t stride, size_t n,
+                       uint16_t *out);
+double or_hashlb_bench(int mode, const or_em *fields, size_t hash_len,
+                       const uint16_t *gates, size_t num_gates,
+                       const uint8_t *base, size_t stride, size_t n,
+                       uint16_t *out, int nthreads, int reps);
 
 /* ---- multi-threaded CPU baseline drivers ------------------------------ */
 /* Each thread owns a contiguous slice of the n packets (pointer batches of

@@ -1,0 +1,186 @@
+/*
+ * oracle_more.c -- TEST INFRASTRUCTURE ONLY (see oracle.h): CPU
+ * restatements of the SURVEY §8f modules that sit beside the
+ * classification path -- HashLB, ACL, IPLookup, UpdateTTL. Only tests/,
+ * smoke() and bench.py's cpu_baseline leg load it.
+ *
+ * Each function cites the reference file:line it follows. CRC32C is computed
+ * with the same SSE4.2 instructions the reference's DPDK helpers compile to
+ * (rte_hash_crc.h crc32c_sse42_u16/u32/u64 = _mm_crc32_u16/u32/u64).
+ */
+#define _GNU_SOURCE
+#include <nmmintrin.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "oracle.h"
+
+static inline uint16_t ld16(const uint8_t *p) {
+  uint16_t v;
+  memcpy(&v, p, 2);
+  return v;
+}
+static inline uint32_t ld32(const uint8_t *p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+
+/* ====================================================================== */
+/* HashLB (core/modules/hash_lb.cc)                                        */
+/* ====================================================================== */
+
+/* hash_range 53-68: 1.(b0)..(b31) as a double, minus 1, times range */
+uint16_t or_hash_range(uint32_t hashval, uint16_t range) {
+  union {
+    uint64_t i;
+    double d;
+  } tmp;
+  tmp.i = 0x3ff0000000000000ull | ((uint64_t)hashval << 20);
+  return (uint16_t)((tmp.d - 1.0) * range);
+}
+
+static uint32_t hlb_hash(int mode, const or_em *fields, size_t hash_len,
+                         const uint8_t *head) {
+  switch (mode) {
+    case OR_HLB_L2: { /* 152-170 */
+      uint16_t sum = 0;
+      for (int j = 0; j < 6; j++) sum ^= ld16(head + 2 * j);
+      return _mm_crc32_u16(0, sum); /* hash_16(sum, 0) */
+    }
+    case OR_HLB_L3: { /* 174-190 */
+      const int ip = 14;
+      uint32_t v0 = ld32(head + ip + 12) ^ ld32(head + ip + 16);
+      return _mm_crc32_u32(0, v0);
+    }
+    case OR_HLB_L4: { /* 194-219 */
+      const int ip = 14;
+      uint32_t l4 = ip + ((head[ip] & 0x0F) << 2);
+      uint32_t v0 = ld32(head + ip + 12);
+      v0 ^= ld32(head + ip + 16);
+      v0 ^= ld16(head + l4);
+      v0 ^= ld16(head + l4 + 2);
+      v0 ^= head[ip + 9];
+      return _mm_crc32_u32(0, v0);
+    }
+    default: { /* 140-150: MakeKeys + ExactMatchKeyHash (exact_match_table.h:101-119) */
+      uint64_t key[8];
+      or_em_make_key(fields, head, key);
+      uint64_t h = 0;
+      for (size_t i = 0; i < hash_len / 8; i++) h = _mm_crc32_u64(h, key[i]);
+      return (uint32_t)h;
+    }
+  }
+}
+
+void or_hashlb_process(int mode, const or_em *fields, size_t hash_len,
+                       const uint16_t *gates, size_t num_gates,
+                       const uint8_t *base, size_t stride, size_t n,
+                       uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    uint32_t h = hlb_hash(mode, fields, hash_len, base + i * stride);
+    out[i] = gates[or_hash_range(h, (uint16_t)num_gates)];
+  }
+}
+
+/* ====================================================================== */
+/* threaded CPU-baseline driver                                            */
+/* ====================================================================== */
+
+typedef void (*slice_fn)(void *ctx, size_t begin, size_t end);
+
+typedef struct {
+  slice_fn fn;
+  void *ctx;
+  size_t begin, end;
+  int reps, cpu;
+  pthread_barrier_t *bar;
+} slice_arg;
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void *slice_thread(void *p) {
+  slice_arg *a = (slice_arg *)p;
+  if (a->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(a->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  }
+  pthread_barrier_wait(a->bar);
+  for (int r = 0; r < a->reps; r++) a->fn(a->ctx, a->begin, a->end);
+  pthread_barrier_wait(a->bar);
+  return NULL;
+}
+
+/* each thread (pinned to the next CPU of the affinity mask) owns a
+ * contiguous, 32-packet aligned slice; returns the wall seconds */
+static double run_slices(slice_fn fn, void *ctx, size_t n, int nthreads,
+                         int reps) {
+  if (nthreads < 1) nthreads = 1;
+  cpu_set_t set;
+  int cpus[1024], ncpu = 0;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0)
+    for (int c = 0; c < CPU_SETSIZE && ncpu < 1024; c++)
+      if (CPU_ISSET(c, &set)) cpus[ncpu++] = c;
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)nthreads + 1);
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  slice_arg *args = (slice_arg *)calloc((size_t)nthreads, sizeof(slice_arg));
+  size_t nb = (n + OR_MAX_BURST - 1) / OR_MAX_BURST;
+  for (int t = 0; t < nthreads; t++) {
+    slice_arg *a = &args[t];
+    size_t b0 = nb * (size_t)t / (size_t)nthreads,
+           b1 = nb * (size_t)(t + 1) / (size_t)nthreads;
+    a->fn = fn;
+    a->ctx = ctx;
+    a->begin = b0 * OR_MAX_BURST;
+    a->end = b1 * OR_MAX_BURST < n ? b1 * OR_MAX_BURST : n;
+    if (a->begin > a->end) a->begin = a->end;
+    a->reps = reps;
+    a->cpu = ncpu ? cpus[t % ncpu] : -1;
+    a->bar = &bar;
+    pthread_create(&th[t], NULL, slice_thread, a);
+  }
+  pthread_barrier_wait(&bar);
+  double t0 = now_s();
+  pthread_barrier_wait(&bar);
+  double t1 = now_s();
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  pthread_barrier_destroy(&bar);
+  free(th);
+  free(args);
+  return t1 - t0;
+}
+
+typedef struct {
+  int mode;
+  const or_em *fields;
+  size_t hash_len;
+  const uint16_t *gates;
+  size_t num_gates;
+  const uint8_t *base;
+  size_t stride;
+  uint16_t *out;
+} hlb_ctx;
+
+static void hlb_slice(void *p, size_t b, size_t e) {
+  hlb_ctx *c = (hlb_ctx *)p;
+  or_hashlb_process(c->mode, c->fields, c->hash_len, c->gates, c->num_gates,
+                    c->base + b * c->stride, c->stride, e - b, c->out + b);
+}
+
+double or_hashlb_bench(int mode, const or_em *fields, size_t hash_len,
+                       const uint16_t *gates, size_t num_gates,
+                       const uint8_t *base, size_t stride, size_t n,
+                       uint16_t *out, int nthreads, int reps) {
+  hlb_ctx c = {mode, fields, hash_len, gates, num_gates, base, stride, out};
+  return run_slices(hlb_slice, &c, n, nthreads, reps);
+}

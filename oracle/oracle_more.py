@@ -1,0 +1,131 @@
+"""TEST INFRASTRUCTURE ONLY: control-plane restatements of the SURVEY §8f
+modules (HashLB, ACL, IPLookup, UpdateTTL) around oracle_more.c. Only
+tests/, smoke() and bench.py's cpu_baseline leg import this. Each method
+cites the reference file:line it follows; errors raise OracleError(errno,
+message) with the reference's text."""
+import ctypes as C
+import errno as E
+
+import numpy as np
+
+from .oracle import OracleError, lib, _ptr
+
+_sz, _vp = C.c_size_t, C.c_void_p
+_SIGS = {
+    "or_em_make_key": (None, [_vp, _vp, _vp]),
+    "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
+    "or_hashlb_process": (None, [C.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _sz,
+                                 _vp]),
+    "or_hashlb_bench": (C.c_double, [C.c_int, _vp, _sz, _vp, _sz, _vp, _sz,
+                                     _sz, _vp, C.c_int, C.c_int]),
+}
+_done = False
+
+
+def mlib():
+    global _done
+    L = lib()
+    if not _done:
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _done = True
+    return L
+
+
+MAX_GATES = 8192
+DROP_GATE = 8192
+
+
+def _valid_gate(g):
+    return g < MAX_GATES or g == DROP_GATE
+
+
+class OracleHashLB:
+    """core/modules/hash_lb.{h,cc}"""
+    L2, L3, L4, FIELDS = 0, 1, 2, 3
+    K_MAX_GATES = 16384  # hash_lb.h kMaxGates
+
+    def __init__(self, gates=(), mode="", fields=()):
+        # 115-134
+        self.gates_ = [0] * self.K_MAX_GATES
+        self.num_gates = 0
+        self.mode = self.L4
+        self.fields = []          # fields_table_ fields (offset, size)
+        self.hash_len = 0         # hasher_(0)
+        self._em = None
+        self.set_gates(gates=gates)
+        if not mode and not fields:
+            self.mode = self.L4  # kDefaultMode
+            return
+        self.set_mode(mode=mode, fields=fields)
+
+    def set_mode(self, mode="", fields=()):
+        # 76-98
+        if fields:
+            self.mode = self.FIELDS
+            L = mlib()
+            if self._em:
+                L.or_em_free(self._em)
+            self._em = L.or_em_new()
+            self.fields = []
+            for i, f in enumerate(fields):
+                off = int(f.get("offset", 0)) & 0xFFFFFFFF
+                if off >= 1 << 31:
+                    off -= 1 << 32  # uint32 -> int
+                msg = C.create_string_buffer(256)
+                rc = L.or_em_add_field(self._em, off, int(f.get("num_bytes", 0)),
+                                       0, i, msg, 256)
+                if rc:
+                    raise OracleError(rc, "Error adding field %d: %s"
+                                      % (i, msg.value.decode()))
+                self.fields.append((off, int(f.get("num_bytes", 0))))
+            self.hash_len = L.or_em_total_key_size(self._em)
+        elif mode == "l2":
+            self.mode = self.L2
+        elif mode == "l3":
+            self.mode = self.L3
+        elif mode == "l4":
+            self.mode = self.L4
+        else:
+            raise OracleError(E.EINVAL, "available LB modes: l2, l3, l4")
+
+    def set_gates(self, gates=()):
+        # 100-113
+        if len(gates) > self.K_MAX_GATES:
+            raise OracleError(E.EINVAL, "HashLB can have at most %d ogates"
+                              % self.K_MAX_GATES)
+        for i, g in enumerate(gates):
+            self.gates_[i] = int(g) & 0xFFFF  # gate_idx_t
+            if not _valid_gate(self.gates_[i]):
+                raise OracleError(E.EINVAL, "Invalid ogate %d" % self.gates_[i])
+        self.num_gates = len(gates)
+
+    def get_desc(self):
+        # 136-138
+        return "%d fields" % len(self.fields)
+
+    def process(self, frames, stride, n):
+        out = np.empty(n, np.uint16)
+        g = np.array(self.gates_, np.uint16)
+        mlib().or_hashlb_process(self.mode, self._em, self.hash_len,
+                                 g.ctypes.data, self.num_gates, _ptr(frames),
+                                 stride, n, out.ctypes.data)
+        return out
+
+    def bench(self, frames, stride, n, threads, reps):
+        out = np.empty(n, np.uint16)
+        g = np.array(self.gates_, np.uint16)
+        return mlib().or_hashlb_bench(self.mode, self._em, self.hash_len,
+                                      g.ctypes.data, self.num_gates,
+                                      _ptr(frames), stride, n, out.ctypes.data,
+                                      threads, reps)
+
+    def __del__(self):
+        if getattr(self, "_em", None):
+            try:
+                lib().or_em_free(self._em)
+            except Exception:
+                pass
+            self._em = None
