@@ -579,6 +579,48 @@ def run_hashlb(args, dev, torch):
     return out
 
 
+def run_acl(args, dev, torch):
+    """ACL (core/modules/acl.cc) on the C2 slab: 16M 64 B packets, random
+    ordered rule lists (prefixes /0../32, port wildcards, 30 % drop rules),
+    70 % of packets derived from some rule's tuple"""
+    import sys as _s
+    _s.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_acl import workload
+    from bess_amd.modules import ACL
+    from oracle import oracle_more as OM
+    n = args.pkts
+    out = {"workload": "ACL: 64B pkts (64B slots), %d resident pkts, first-"
+                       "match over an ordered rule list" % n, "pkts": n}
+    g = torch.empty(n, dtype=torch.int16, device=dev)
+    for nr in (100, 1000):
+        rules, frames = workload(nr, n, seed=nr)
+        d = torch.from_numpy(frames.reshape(-1)).to(dev)
+        m = ACL(rules=rules)
+        o = OM.OracleACL(rules=rules)
+        m.process_device(d, 64, n, g)
+        torch.cuda.synchronize()
+        k = min(n, 1 << 18)
+        parity = bool((g[:k].cpu().numpy().view(np.uint16) ==
+                       o.process(frames, 64, k)).all())
+        ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+        e = {"ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+             "roofline": _roof(EM_BYTES_PER_PKT, n, ms),
+             "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}
+        if not args.no_cpu:
+            cn = 1 << 16
+            snb = _snbuf_sample(frames, cn)
+            threads, res = cpu_rate(
+                lambda nt, reps: o.bench(snb.ctypes.data + 512, 2624, cn, nt, reps),
+                cn, args.cpu_seconds / 4)
+            e["cpu_baseline"] = {
+                "value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
+                "kind": "port", "single_core_mpps": round(res[1], 2),
+                "sample": "%d 64B pkts x reps in snbuf layout, %d-rule ACL" % (cn, nr)}
+        out["rules_%d" % nr] = e
+        del d
+    return out
+
+
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
@@ -757,6 +799,9 @@ def main():
     if args.only == "c5":
         log(json.dumps(run_c5(args, dev, torch)))
         return
+    if args.only == "acl":
+        log(json.dumps(run_acl(args, dev, torch)))
+        return
     if args.only == "hashlb":
         log(json.dumps(run_hashlb(args, dev, torch)))
         return
@@ -813,7 +858,7 @@ def main():
         except Exception as e:
             out["e2e_pipe"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
-                         ("HashLB", run_hashlb)):
+                         ("HashLB", run_hashlb), ("ACL", run_acl)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

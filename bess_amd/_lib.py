@@ -102,6 +102,12 @@ _SIGS = {
     "bg_hlb_set_gates": (_int, [_vp, _vp, _sz, _sz]),
     "bg_hlb_window": (None, [_vp, C.POINTER(_int), C.POINTER(_int)]),
     "bg_hlb_classify": (_int, [_vp, _vp, _sz, _sz, _int, _vp, _vp]),
+    "bg_acl_create": (_int, [C.POINTER(_vp)]),
+    "bg_acl_destroy": (None, [_vp]),
+    "bg_acl_add": (_int, [_vp, _vp, _sz]),
+    "bg_acl_clear": (None, [_vp]),
+    "bg_acl_count": (_sz, [_vp]),
+    "bg_acl_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
 }
 
 _lib = None

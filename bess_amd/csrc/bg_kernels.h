@@ -129,12 +129,25 @@ struct HlbArgs {
   FieldPlan fp;             // kHlbFields
 };
 
+// ACL (core/modules/acl.cc): first matching rule in order; rule r is 8
+// dwords {src addr, src mask, dst addr, dst mask, ports, port mask, drop,
+// valid} in the packet's LE byte order (addresses / ports as loaded from the
+// frame); nrules is padded to a multiple of 4 with valid = 0 rules.
+struct AclArgs {
+  const uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *out;
+  const uint32_t *rules;
+  uint32_t nrules, igate;
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s);
 
 }  // namespace bg
 

@@ -1,0 +1,189 @@
+// bg_line_dev.h -- generic "header-line" packet kernels: one decision per
+// packet from the frame's first 64 bytes (HashLB l2/l3/l4, ACL, IPLookup,
+// UpdateTTL). Included only from .hip translation units.
+//
+// An Op provides
+//   using Args = ...;   // with frames, stride, n, out (uint16_t per packet)
+//   static constexpr int c0, c1;   // 16-byte chunks [c0, c1) of the line used
+//   static size_t lds_bytes(const Args &);            (host) tables in LDS
+//   __device__ static void stage(uint32_t *lds, const Args &);   fill them
+//   __device__ static uint32_t decide(const Args &, const uint32_t *lds,
+//                                     const uint32_t (&d)[16], uint8_t *f);
+// d[] holds the line's dwords (only chunks [c0, c1) valid); f is the frame
+// (for rare reads past the line, or in-place writes).
+//
+// Two launch shapes:
+//   line_kernel      one packet per lane, its chunks loaded directly (any
+//                    16-byte-multiple stride >= 64);
+//   line_slab_kernel dense 64-byte slots (stride 64): a wave reads 64 slots
+//                    = 4 KB with lane-contiguous 16-byte loads into a
+//                    swizzled per-wave LDS stage (slot s keeps chunk q at
+//                    unit 4s + ((q + s/4) & 3): conflict-free writes and
+//                    per-slot reads), each lane then takes its own slot from
+//                    LDS; the next tile's loads are in flight meanwhile.
+//                    Lane-contiguous loads stream the slab at ~7.1 TB/s where
+//                    slot-per-lane 16-byte loads reach ~5 TB/s
+//                    (scripts/hbm_probe.hip).
+#ifndef BESS_AMD_BG_LINE_DEV_H_
+#define BESS_AMD_BG_LINE_DEV_H_
+
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "bg_kernels.h"
+#include "bg_keys_dev.h"
+
+namespace bg {
+namespace {
+
+constexpr int kLineBlock = 512;
+
+__device__ __forceinline__ uint32_t line_stage_unit(uint32_t slot, uint32_t q) {
+  return slot * 4 + ((q + (slot >> 2)) & 3);
+}
+
+template <class Op>
+__global__ __launch_bounds__(kLineBlock) void line_kernel(typename Op::Args a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  Op::stage(lds, a);
+  __syncthreads();
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < a.n;
+       idx += step) {
+    uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * a.stride;
+    const uint4 *p = reinterpret_cast<const uint4 *>(f);
+    uint32_t d[16];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c >= Op::c0 && c < Op::c1) v = ld_stream(p + c);
+      d[4 * c] = v.x;
+      d[4 * c + 1] = v.y;
+      d[4 * c + 2] = v.z;
+      d[4 * c + 3] = v.w;
+    }
+    a.out[idx] = (uint16_t)Op::decide(a, lds, d, f);
+  }
+}
+
+template <class Op>
+__global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args a,
+                                                              uint32_t stage_words) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  Op::stage(lds, a);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kWaves = kLineBlock / 64;
+  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_words) + wid * 256;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  uint4 v[4];
+  auto load_tile = [&](uint64_t tile) {
+    const uint64_t p0 = tile * 64;
+    const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      const uint32_t q = u & 3;  // chunk of the slot this unit holds
+      v[c] = (u < units && q >= (uint32_t)Op::c0 && q < (uint32_t)Op::c1)
+                 ? ld_stream(src + p0 * 4 + u)
+                 : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (t < ntiles) load_tile(t);
+  for (; t < ntiles; t += nwaves) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      stage[line_stage_unit(u >> 2, u & 3)] = v[c];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + nwaves < ntiles) load_tile(t + nwaves);
+    uint32_t d[16];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (c >= Op::c0 && c < Op::c1) x = stage[line_stage_unit(lane, c)];
+      d[4 * c] = x.x;
+      d[4 * c + 1] = x.y;
+      d[4 * c + 2] = x.z;
+      d[4 * c + 3] = x.w;
+    }
+    const uint64_t idx = t * 64 + lane;
+    if (idx < a.n) {
+      uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * 64;
+      a.out[idx] = (uint16_t)Op::decide(a, lds, d, f);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// The 4 bytes at l4 = 14 + 4*IHL (untagged IPv4: src port, dst port) as a
+// LE dword, from the line d[] (IHL = low nibble of byte 14). l4 = 4*(3+IHL)
+// + 2, so they are the high half of dword 3+IHL and the low half of dword
+// 4+IHL; IHL 12..15 reach past the line and are read from the frame, only
+// inside its slot (bytes past `stride` read as zero).
+__device__ __forceinline__ uint32_t l4_ports(const uint32_t (&d)[16],
+                                             const uint8_t *f, uint64_t stride) {
+  const uint32_t ihl = (d[3] >> 16) & 0x0F;
+  uint32_t p = 0;
+#pragma unroll
+  for (int j = 0; j < 12; j++)
+    if (ihl == (uint32_t)j) p = (d[3 + j] >> 16) | (d[4 + j] << 16);
+  if (ihl >= 12) {
+    const uint32_t l4 = 14 + 4 * ihl;
+    const uint16_t *q = reinterpret_cast<const uint16_t *>(f + l4);
+    const uint32_t sp = l4 + 2 <= stride ? q[0] : 0u;
+    const uint32_t dp = l4 + 4 <= stride ? q[1] : 0u;
+    p = sp | (dp << 16);
+  }
+  return p;
+}
+
+// IPv4 src / dst address (bytes 26..29 / 30..33) as LE dwords
+__device__ __forceinline__ uint32_t ip_src_le(const uint32_t (&d)[16]) {
+  return __builtin_amdgcn_alignbyte(d[7], d[6], 2);
+}
+__device__ __forceinline__ uint32_t ip_dst_le(const uint32_t (&d)[16]) {
+  return __builtin_amdgcn_alignbyte(d[8], d[7], 2);
+}
+
+inline int line_occupancy(const void *kern, size_t lds) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kLineBlock, lds) !=
+          hipSuccess ||
+      occ <= 0)
+    occ = 1;
+  return occ;
+}
+
+// Residency-sized grid; the slab shape for dense 64-byte slots.
+template <class Op>
+hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  const size_t tab = (Op::lds_bytes(a) + 15) & ~(size_t)15;
+  const uint64_t need = (a.n + kLineBlock - 1) / kLineBlock;
+  if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 && !getenv("BG_NO_SLAB")) {
+    auto kern = line_slab_kernel<Op>;
+    const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
+    const int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);
+    const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLineBlock), lds, s, a,
+                       (uint32_t)(tab / 4));
+    return hipGetLastError();
+  }
+  auto kern = line_kernel<Op>;
+  const int occ = line_occupancy(reinterpret_cast<const void *>(kern), tab);
+  const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLineBlock), tab, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+}  // namespace bg
+
+#endif  // BESS_AMD_BG_LINE_DEV_H_

@@ -174,6 +174,18 @@ class HashLB(Module):
         return self.command("set_gates", **kw)
 
 
+class ACL(Module):
+    """core/modules/acl.cc on the GPU."""
+    mclass = "ACL"
+    cmds = {"add": ("ACLArg", None), "clear": ("EmptyArg", None)}
+
+    def add(self, **kw):
+        return self.command("add", **kw)
+
+    def clear(self):
+        return self.command("clear")
+
+
 class Pipe:
     """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
     are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered

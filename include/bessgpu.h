@@ -192,6 +192,26 @@ void bg_hlb_window(const bg_hlb *h, int *lo, int *hi);
 int bg_hlb_classify(bg_hlb *h, const void *d_frames, size_t stride, size_t n,
                     int win_off, uint16_t *d_gates, bg_stream_t stream);
 
+/* ---- ACL (core/modules/acl.cc) ----------------------------------------- */
+/* ACL::ACLRule (acl.h:43-57) in host byte order: Ipv4Prefix addr / mask
+ * values, be16_t port values (0 = wildcard). */
+typedef struct bg_acl_rule {
+  uint32_t src_addr, src_mask, dst_addr, dst_mask;
+  uint16_t src_port, dst_port;
+  uint8_t drop, pad[3];
+} bg_acl_rule;
+typedef struct bg_acl bg_acl;
+int bg_acl_create(bg_acl **out);
+void bg_acl_destroy(bg_acl *h);
+/* append rules in order (ACL::CommandAdd -> Init, acl.cc:42-58) */
+int bg_acl_add(bg_acl *h, const bg_acl_rule *rules, size_t n);
+void bg_acl_clear(bg_acl *h);
+size_t bg_acl_count(const bg_acl *h);
+/* ProcessBatch 63-95: out[i] = igate (first matching rule forwards) or
+ * BG_DROP_GATE (it drops, or no rule matches). Stride >= 64. */
+int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
+                    uint16_t igate, uint16_t *d_out, bg_stream_t stream);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".

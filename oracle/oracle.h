@@ -148,6 +148,21 @@ double or_hashlb_bench(int mode, const or_em *fields, size_t hash_len,
                        const uint8_t *base, size_t stride, size_t n,
                        uint16_t *out, int nthreads, int reps);
 
+/* ---- ACL (core/modules/acl.cc) -- oracle_more.c ------------------------- */
+#define OR_DROP_GATE 8192
+typedef struct or_acl_rule { /* ACLRule, host byte order */
+  uint32_t src_addr, src_mask, dst_addr, dst_mask;
+  uint16_t src_port, dst_port;
+  uint8_t drop, pad[3];
+} or_acl_rule;
+/* Ipv4Prefix(string) (ip.cc:63-79); -1 where std::stoi would throw */
+int or_ipv4_prefix(const char *prefix, uint32_t *addr, uint32_t *mask);
+void or_acl_process(const or_acl_rule *rules, size_t nrules, const uint8_t *base,
+                    size_t stride, size_t n, uint16_t igate, uint16_t *out);
+double or_acl_bench(const or_acl_rule *rules, size_t nrules, const uint8_t *base,
+                    size_t stride, size_t n, uint16_t igate, uint16_t *out,
+                    int nthreads, int reps);
+
 /* ---- multi-threaded CPU baseline drivers ------------------------------ */
 /* Each thread owns a contiguous slice of the n packets (pointer batches of
  * 32 over base + i*stride) and sweeps it `reps` times; threads are pinned to

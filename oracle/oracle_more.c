@@ -184,3 +184,90 @@ double or_hashlb_bench(int mode, const or_em *fields, size_t hash_len,
   hlb_ctx c = {mode, fields, hash_len, gates, num_gates, base, stride, out};
   return run_slices(hlb_slice, &c, n, nthreads, reps);
 }
+
+/* ====================================================================== */
+/* ACL (core/modules/acl.{h,cc})                                           */
+/* ====================================================================== */
+
+#include <errno.h>
+#include <limits.h>
+#include <stdio.h>
+
+static uint32_t be32(const uint8_t *p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) |
+         p[3];
+}
+static uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+/* Ipv4Prefix::Ipv4Prefix (core/utils/ip.cc:63-79) + ParseIpv4Address
+ * (40-51) + SetBitsLow (bits.h:193-198). Returns 0, or -1 where std::stoi
+ * would throw (no digits / out of int range). */
+int or_ipv4_prefix(const char *prefix, uint32_t *addr, uint32_t *mask) {
+  *addr = 0;
+  *mask = 0;
+  const char *slash = strchr(prefix, '/');
+  if (!*prefix || !slash) return 0;
+  char ip[256];
+  size_t il = (size_t)(slash - prefix);
+  if (il >= sizeof(ip)) il = sizeof(ip) - 1;
+  memcpy(ip, prefix, il);
+  ip[il] = 0;
+  unsigned a, b, c, d;
+  if (sscanf(ip, "%u.%u.%u.%u", &a, &b, &c, &d) == 4 && a < 256 && b < 256 &&
+      c < 256 && d < 256)
+    *addr = (a << 24) | (b << 16) | (c << 8) | d;
+  char *end;
+  errno = 0;
+  long v = strtol(slash + 1, &end, 10);
+  if (end == slash + 1 || errno == ERANGE || v > INT_MAX || v < INT_MIN) return -1;
+  size_t n = (size_t)(long)(int)v;
+  *mask = n == 0 ? 0u : n >= 32 ? 0xFFFFFFFFu : ~((1u << (32 - n)) - 1u);
+  return 0;
+}
+
+/* ACL::ProcessBatch (acl.cc:63-95) with ACLRule::Match (acl.h:45-50) */
+void or_acl_process(const or_acl_rule *rules, size_t nrules, const uint8_t *base,
+                    size_t stride, size_t n, uint16_t igate, uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *eth = base + i * stride;
+    const uint8_t *ip = eth + 14;
+    size_t ip_bytes = (size_t)(ip[0] & 0x0F) << 2; /* header_length << 2 */
+    const uint8_t *udp = ip + ip_bytes;
+    uint32_t src = be32(ip + 12), dst = be32(ip + 16);
+    uint16_t sp = be16(udp), dp = be16(udp + 2);
+    uint16_t g = OR_DROP_GATE;
+    for (size_t r = 0; r < nrules; r++) {
+      const or_acl_rule *R = &rules[r];
+      if ((R->src_addr & R->src_mask) == (src & R->src_mask) &&
+          (R->dst_addr & R->dst_mask) == (dst & R->dst_mask) &&
+          (R->src_port == 0 || R->src_port == sp) &&
+          (R->dst_port == 0 || R->dst_port == dp)) {
+        if (!R->drop) g = igate;
+        break; /* stop matching other rules */
+      }
+    }
+    out[i] = g;
+  }
+}
+
+typedef struct {
+  const or_acl_rule *rules;
+  size_t nrules;
+  const uint8_t *base;
+  size_t stride;
+  uint16_t igate;
+  uint16_t *out;
+} acl_ctx;
+
+static void acl_slice(void *p, size_t b, size_t e) {
+  acl_ctx *c = (acl_ctx *)p;
+  or_acl_process(c->rules, c->nrules, c->base + b * c->stride, c->stride, e - b,
+                 c->igate, c->out + b);
+}
+
+double or_acl_bench(const or_acl_rule *rules, size_t nrules, const uint8_t *base,
+                    size_t stride, size_t n, uint16_t igate, uint16_t *out,
+                    int nthreads, int reps) {
+  acl_ctx c = {rules, nrules, base, stride, igate, out};
+  return run_slices(acl_slice, &c, n, nthreads, reps);
+}

@@ -11,7 +11,19 @@ import numpy as np
 from .oracle import OracleError, lib, _ptr
 
 _sz, _vp = C.c_size_t, C.c_void_p
+class or_acl_rule(C.Structure):
+    _fields_ = [("src_addr", C.c_uint32), ("src_mask", C.c_uint32),
+                ("dst_addr", C.c_uint32), ("dst_mask", C.c_uint32),
+                ("src_port", C.c_uint16), ("dst_port", C.c_uint16),
+                ("drop", C.c_uint8), ("pad", C.c_uint8 * 3)]
+
+
 _SIGS = {
+    "or_ipv4_prefix": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_uint32)]),
+    "or_acl_process": (None, [_vp, _sz, _vp, _sz, _sz, C.c_uint16, _vp]),
+    "or_acl_bench": (C.c_double, [_vp, _sz, _vp, _sz, _sz, C.c_uint16, _vp,
+                                  C.c_int, C.c_int]),
     "or_em_make_key": (None, [_vp, _vp, _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
     "or_hashlb_process": (None, [C.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _sz,
@@ -129,3 +141,54 @@ class OracleHashLB:
             except Exception:
                 pass
             self._em = None
+
+
+def ipv4_prefix(prefix):
+    """Ipv4Prefix(string) (core/utils/ip.cc:63-79) -> (addr, mask) host
+    order; OracleError(EINVAL) where the reference's std::stoi throws"""
+    a, m = C.c_uint32(), C.c_uint32()
+    if mlib().or_ipv4_prefix(prefix.encode(), C.byref(a), C.byref(m)) < 0:
+        raise OracleError(E.EINVAL, "invalid prefix length")
+    return a.value, m.value
+
+
+class OracleACL:
+    """core/modules/acl.{h,cc}"""
+
+    def __init__(self, rules=()):
+        self.rules = []
+        self.add(rules=rules)
+
+    def add(self, rules=()):
+        # Init 42-53 (CommandAdd 55-58 calls Init)
+        new = []
+        for r in rules:
+            sa, sm = ipv4_prefix(r.get("src_ip", ""))
+            da, dm = ipv4_prefix(r.get("dst_ip", ""))
+            new.append((sa, sm, da, dm, int(r.get("src_port", 0)) & 0xFFFF,
+                        int(r.get("dst_port", 0)) & 0xFFFF,
+                        1 if r.get("drop", False) else 0))
+        self.rules.extend(new)
+
+    def clear(self):
+        self.rules = []
+
+    def _arr(self):
+        arr = (or_acl_rule * max(1, len(self.rules)))()
+        for i, r in enumerate(self.rules):
+            (arr[i].src_addr, arr[i].src_mask, arr[i].dst_addr, arr[i].dst_mask,
+             arr[i].src_port, arr[i].dst_port, arr[i].drop) = r
+        return arr
+
+    def process(self, frames, stride, n, igate=0):
+        out = np.empty(n, np.uint16)
+        arr = self._arr()
+        mlib().or_acl_process(arr, len(self.rules), _ptr(frames), stride, n,
+                              igate, out.ctypes.data)
+        return out
+
+    def bench(self, base, stride, n, threads, reps, igate=0):
+        out = np.empty(n, np.uint16)
+        arr = self._arr()
+        return mlib().or_acl_bench(arr, len(self.rules), base, stride, n, igate,
+                                   out.ctypes.data, threads, reps)

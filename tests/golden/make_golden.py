@@ -476,6 +476,73 @@ def uint64_to_bin_cases():
     return cases
 
 
+# --------------------------------------------------------------------------
+# SURVEY §8f modules: bessctl/module_tests/{acl,iplookup,update_ttl}.py.
+# Gates: the output gate a packet left on; 8192 (DROP_GATE) = dropped.
+# --------------------------------------------------------------------------
+DROP = 8192
+
+
+def acl_module_kat():
+    p22 = tcp_packet("22.22.22.22", "22.22.22.22")
+    p96 = tcp_packet("96.22.22.22", "22.22.22.22")
+    udp_a = udp_frame(bytes.fromhex("06163e1b7232021e679f4dae0800"),
+                      "172.12.0.3", "127.12.0.4", 1234, 5678, b"\x00" * 18)
+    tcp_b = tcp_packet("192.168.32.4", "1.2.3.4")
+    rules3 = [{"src_ip": "172.12.0.0/16", "drop": False},
+              {"dst_ip": "192.168.32.4/32", "dst_port": 4455,
+               "src_ip": "134.54.33.2/32", "drop": False},
+              {"src_ip": "133.133.133.0/24", "src_port": 43,
+               "dst_ip": "96.96.96.155/32", "dst_port": 9, "drop": False}]
+    return [
+        {"name": "test_acl_simple", "cite": "acl.py:57-66",
+         "arg": {"rules": [{"src_ip": "0.0.0.0/0", "drop": False}]},
+         "packets": [hx(p22)], "expect": [0]},
+        {"name": "tests_acl_back2back", "cite": "acl.py:68-80",
+         "arg": {"rules": [{"src_ip": "96.0.0.0/8", "drop": False}]},
+         "packets": [hx(p22), hx(p96)], "expect": [DROP, 0]},
+        {"name": "test_run_acl_custom", "cite": "acl.py:82-106: its rules "
+         "and Rewrite templates; the test asserts only liveness, the "
+         "expectation follows ACLRule::Match (acl.h:45-50)",
+         "arg": {"rules": rules3},
+         "packets": [hx(udp_a), hx(tcp_b)], "expect": [0, DROP]},
+    ]
+
+
+def iplookup_module_kat():
+    pkts = [tcp_packet("12.22.22.22", d) for d in
+            ("22.22.22.22", "32.22.22.22", "42.22.22.22")]
+    return [
+        {"name": "test_iplookup", "cite": "iplookup.py:37-56",
+         "arg": {},
+         "cmds": [["add", {"prefix": "22.22.22.0", "prefix_len": 24, "gate": 0}],
+                  ["add", {"prefix": "32.22.22.0", "prefix_len": 24, "gate": 1}],
+                  ["add", {"prefix": "42.22.22.0", "prefix_len": 24, "gate": 1}],
+                  ["delete", {"prefix": "42.22.22.0", "prefix_len": 24}],
+                  ["delete", {"prefix": "52.22.22.0", "prefix_len": 24},
+                   "error"]],
+         "packets": [hx(p) for p in pkts], "expect": [0, 1, DROP]},
+        {"name": "test_prefix", "cite": "iplookup.py:58-61",
+         "arg": {},
+         "cmds": [["add", {"prefix": "22.22.22.0", "prefix_len": 16, "gate": 0},
+                   "error"]],
+         "packets": [hx(pkts[0])], "expect": [DROP]},
+    ]
+
+
+def update_ttl_module_kat():
+    def with_ttl(t):
+        return tcp_packet("1.2.3.4", "5.6.7.8", ttl=t)
+    return [
+        {"name": "test_decrement", "cite": "update_ttl.py:40-51",
+         "in": hx(with_ttl(2)), "out": hx(with_ttl(1)), "gate": 0},
+        {"name": "test_drop ttl 0", "cite": "update_ttl.py:53-75",
+         "in": hx(with_ttl(0)), "out": hx(with_ttl(0)), "gate": DROP},
+        {"name": "test_drop ttl 1", "cite": "update_ttl.py:53-75",
+         "in": hx(with_ttl(1)), "out": hx(with_ttl(1)), "gate": DROP},
+    ]
+
+
 def main():
     fixtures = {
         "em_table_kat.json": em_table_kat(),
@@ -486,6 +553,9 @@ def main():
         "ip_checksum_module_kat.json": ip_checksum_module_kat(),
         "checksum_kat.json": checksum_kat(),
         "uint64_to_bin.json": uint64_to_bin_cases(),
+        "acl_module_kat.json": acl_module_kat(),
+        "iplookup_module_kat.json": iplookup_module_kat(),
+        "update_ttl_module_kat.json": update_ttl_module_kat(),
     }
     for name, obj in fixtures.items():
         with open(os.path.join(HERE, name), "w") as f:
