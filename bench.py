@@ -621,6 +621,38 @@ def run_acl(args, dev, torch):
     return out
 
 
+def run_iplookup(args, dev, torch):
+    """IPLookup (core/modules/ip_lookup.cc) on the C2 slab: 16M 64 B packets,
+    10K routes (/8../24, 5 % /25../32, nested), half the destinations inside
+    a route; DIR-24-8 tables (32 MB tbl24) in HBM/MALL"""
+    import sys as _s
+    _s.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_iplookup import build, dsts_inside, frames_to, routes
+    from oracle import oracle as O
+    n = args.pkts
+    rng = np.random.default_rng(0x5EED)
+    rt = routes(10000, rng, 0.05)
+    m, o = build(rt, max_rules=20000, max_tbl8s=4096)
+    dst = np.concatenate([dsts_inside(rt, n // 2, rng),
+                          rng.integers(0, 1 << 32, n - n // 2, dtype=np.uint64)])
+    rng.shuffle(dst)
+    frames = frames_to(dst)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    g = torch.empty(n, dtype=torch.int16, device=dev)
+    m.process_device(d, 64, n, g)
+    torch.cuda.synchronize()
+    k = min(n, 1 << 20)
+    parity = bool((g[:k].cpu().numpy().view(np.uint16) ==
+                   o.process(frames, 64, k)).all())
+    ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+    out = {"workload": "IPLookup: 64B pkts (64B slots), %d resident pkts, 10K "
+                       "routes, DIR-24-8" % n, "pkts": n, "routes": len(o.rules),
+           "ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+           "roofline": _roof(EM_BYTES_PER_PKT, n, ms),
+           "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}
+    return out
+
+
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
@@ -799,6 +831,9 @@ def main():
     if args.only == "c5":
         log(json.dumps(run_c5(args, dev, torch)))
         return
+    if args.only == "iplookup":
+        log(json.dumps(run_iplookup(args, dev, torch)))
+        return
     if args.only == "acl":
         log(json.dumps(run_acl(args, dev, torch)))
         return
@@ -858,7 +893,8 @@ def main():
         except Exception as e:
             out["e2e_pipe"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
-                         ("HashLB", run_hashlb), ("ACL", run_acl)):
+                         ("HashLB", run_hashlb), ("ACL", run_acl),
+                         ("IPLookup", run_iplookup)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

@@ -108,6 +108,13 @@ _SIGS = {
     "bg_acl_clear": (None, [_vp]),
     "bg_acl_count": (_sz, [_vp]),
     "bg_acl_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
+    "bg_lpm_create": (_int, [C.c_uint32, C.c_uint32, C.POINTER(_vp)]),
+    "bg_lpm_destroy": (None, [_vp]),
+    "bg_lpm_add": (_int, [_vp, C.c_uint32, _int, C.c_uint32]),
+    "bg_lpm_delete": (_int, [_vp, C.c_uint32, _int]),
+    "bg_lpm_clear": (None, [_vp]),
+    "bg_lpm_count": (_sz, [_vp]),
+    "bg_lpm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
 }
 
 _lib = None

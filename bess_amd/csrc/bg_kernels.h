@@ -141,6 +141,18 @@ struct AclArgs {
   uint32_t nrules, igate;
 };
 
+// IPLookup (core/modules/ip_lookup.cc): DIR-24-8 longest-prefix match on
+// the destination address. Entries (u16): 0 = no route, 0x8000 | g = the
+// /24 is extended into tbl8 group g, else next hop + 1.
+struct LpmArgs {
+  const uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *out;
+  const uint16_t *tbl24;  // 2^24 entries
+  const uint16_t *tbl8;   // groups x 256 entries
+  uint32_t default_gate, pad;
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -148,6 +160,7 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 
 }  // namespace bg
 

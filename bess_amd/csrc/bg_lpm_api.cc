@@ -1,0 +1,193 @@
+// bg_lpm_api.cc -- C ABI of the IPLookup datapath (include/bessgpu.h
+// bg_lpm_*): the route table with rte_lpm's add / delete / capacity
+// semantics (DPDK 19.11 rte_lpm.c, as IPLookup uses it), laid out as
+// DIR-24-8 and uploaded to the device when it changes (bg_lpm.hip).
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "bg_internal.h"
+
+using namespace bg;
+
+namespace {
+constexpr uint32_t kTbl24 = 1u << 24;
+constexpr uint32_t kMaxGroups = 0x7FFF;  // u16 entries: 15-bit group index
+constexpr uint32_t kMaxNextHop = 0x7FFE;  // u16 entries: next hop + 1
+
+uint32_t depth_mask(int depth) {
+  return depth == 0 ? 0u : depth >= 32 ? 0xFFFFFFFFu : ~((1u << (32 - depth)) - 1u);
+}
+}  // namespace
+
+struct bg_lpm {
+  uint32_t max_rules = 1024, max_tbl8s = 128;
+  // (depth, masked ip) -> next hop: map order = ascending depth, the order
+  // DIR-24-8 is filled in (longer prefixes overwrite shorter ones)
+  std::map<std::pair<int, uint32_t>, uint32_t> rules;
+  std::map<uint32_t, int> ext;  // /24 block -> rules deeper than /24 in it
+  bool dirty = true;
+  int device = -1;
+  uint16_t *d_tbl24 = nullptr, *d_tbl8 = nullptr;
+  size_t d_cap8 = 0;  // groups
+  std::mutex mu;
+  ~bg_lpm() {
+    if (d_tbl24) (void)hipFree(d_tbl24);
+    if (d_tbl8) (void)hipFree(d_tbl8);
+  }
+};
+
+static int lpm_sync_locked(bg_lpm *h, int dev, hipStream_t s) {
+  if (!h->dirty && h->device == dev && h->d_tbl24) return 0;
+  int r = set_device(dev);
+  if (r) return r;
+  std::vector<uint16_t> t24(kTbl24, 0);
+  std::vector<uint16_t> t8;
+  std::map<uint32_t, std::vector<std::pair<int, uint32_t>>> deep;  // block -> rules
+  for (const auto &kv : h->rules) {
+    const int depth = kv.first.first;
+    const uint32_t ip = kv.first.second, nh = kv.second;
+    if (depth <= 24) {
+      const uint32_t start = ip >> 8, cnt = 1u << (24 - depth);
+      std::fill(t24.begin() + start, t24.begin() + start + cnt, (uint16_t)(nh + 1));
+    } else {
+      deep[ip >> 8].push_back(kv.first);
+    }
+  }
+  uint32_t g = 0;
+  for (const auto &b : deep) {
+    t8.resize((size_t)(g + 1) * 256, t24[b.first]);  // the covering <= /24 route
+    uint16_t *grp = t8.data() + (size_t)g * 256;
+    for (const auto &k : b.second) {  // ascending depth (map order)
+      const uint32_t start = k.second & 0xFF, cnt = 1u << (32 - k.first);
+      std::fill(grp + start, grp + start + cnt, (uint16_t)(h->rules[k] + 1));
+    }
+    t24[b.first] = (uint16_t)(0x8000u | g);
+    g++;
+  }
+  if (!h->d_tbl24 || h->device != dev) {
+    if (h->d_tbl24) (void)hipFree(h->d_tbl24);
+    h->d_tbl24 = nullptr;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl24), (size_t)kTbl24 * 2));
+  }
+  const size_t ng = std::max<size_t>(g, 1);
+  if (!h->d_tbl8 || h->d_cap8 < ng || h->device != dev) {
+    if (h->d_tbl8) (void)hipFree(h->d_tbl8);
+    h->d_tbl8 = nullptr;
+    h->d_cap8 = std::max<size_t>(ng, 64);
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl8), h->d_cap8 * 512));
+  }
+  HIP_TRY(hipMemcpyAsync(h->d_tbl24, t24.data(), (size_t)kTbl24 * 2,
+                         hipMemcpyHostToDevice, s));
+  if (g)
+    HIP_TRY(hipMemcpyAsync(h->d_tbl8, t8.data(), t8.size() * 2,
+                           hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  h->device = dev;
+  h->dirty = false;
+  return 0;
+}
+
+extern "C" {
+
+int bg_lpm_create(uint32_t max_rules, uint32_t max_tbl8s, bg_lpm **out) {
+  if (!out) return fail(EINVAL, "bad arguments");
+  bg_lpm *h = new bg_lpm();
+  h->max_rules = max_rules ? max_rules : 1024;
+  h->max_tbl8s = max_tbl8s ? max_tbl8s : 128;
+  *out = h;
+  return 0;
+}
+
+void bg_lpm_destroy(bg_lpm *h) { delete h; }
+
+// rte_lpm_add: an existing (prefix, depth) gets the new next hop; a new rule
+// needs room in the rule table (max_rules) and, deeper than /24 in a /24
+// block that has no such rule yet, a free tbl8 group (max_tbl8s).
+int bg_lpm_add(bg_lpm *h, uint32_t ip, int depth, uint32_t next_hop) {
+  if (depth < 1 || depth > 32) return fail(EINVAL, "depth %d", depth);
+  if (next_hop > kMaxNextHop) return fail(EINVAL, "next hop %u", next_hop);
+  std::lock_guard<std::mutex> lk(h->mu);
+  const uint32_t ipm = ip & depth_mask(depth);
+  auto key = std::make_pair(depth, ipm);
+  auto it = h->rules.find(key);
+  if (it != h->rules.end()) {
+    it->second = next_hop;
+    h->dirty = true;
+    return 0;
+  }
+  if (h->rules.size() >= h->max_rules) return fail(ENOSPC, "rule table full");
+  if (depth > 24) {
+    auto e = h->ext.find(ipm >> 8);
+    if (e == h->ext.end()) {
+      if (h->ext.size() >= std::min(h->max_tbl8s, kMaxGroups))
+        return fail(ENOSPC, "no free tbl8 group");
+      h->ext[ipm >> 8] = 1;
+    } else {
+      e->second++;
+    }
+  }
+  h->rules[key] = next_hop;
+  h->dirty = true;
+  return 0;
+}
+
+int bg_lpm_delete(bg_lpm *h, uint32_t ip, int depth) {
+  if (depth < 1 || depth > 32) return fail(EINVAL, "depth %d", depth);
+  std::lock_guard<std::mutex> lk(h->mu);
+  const uint32_t ipm = ip & depth_mask(depth);
+  auto it = h->rules.find(std::make_pair(depth, ipm));
+  if (it == h->rules.end()) return fail(EINVAL, "no such rule");
+  h->rules.erase(it);
+  if (depth > 24) {
+    auto e = h->ext.find(ipm >> 8);
+    if (--e->second == 0) h->ext.erase(e);  // tbl8 group recycled
+  }
+  h->dirty = true;
+  return 0;
+}
+
+void bg_lpm_clear(bg_lpm *h) {
+  std::lock_guard<std::mutex> lk(h->mu);
+  h->rules.clear();
+  h->ext.clear();
+  h->dirty = true;
+}
+
+size_t bg_lpm_count(const bg_lpm *h) { return h->rules.size(); }
+
+int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
+                    uint16_t default_gate, uint16_t *d_out, bg_stream_t stream) {
+  if (stride % 16 || stride < 64 || ((uintptr_t)d_frames & 15))
+    return fail(EINVAL, "frame slab must be 16-byte aligned, stride a 16-byte "
+                "multiple >= 64");
+  hipStream_t s = (hipStream_t)stream;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  LpmArgs a;
+  memset(&a, 0, sizeof(a));
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->device >= 0) dev = h->device;
+    int r = lpm_sync_locked(h, dev, s);
+    if (r) return r;
+    a.tbl24 = h->d_tbl24;
+    a.tbl8 = h->d_tbl8;
+  }
+  int r = set_device(dev);
+  if (r) return r;
+  a.frames = static_cast<const uint8_t *>(d_frames);
+  a.stride = stride;
+  a.n = n;
+  a.out = d_out;
+  a.default_gate = default_gate;
+  HIP_TRY(launch_lpm(a, num_cus(dev), s));
+  return 0;
+}
+
+}  // extern "C"

@@ -186,6 +186,23 @@ class ACL(Module):
         return self.command("clear")
 
 
+class IPLookup(Module):
+    """core/modules/ip_lookup.cc on the GPU."""
+    mclass = "IPLookup"
+    cmds = {"add": ("IPLookupCommandAddArg", None),
+            "delete": ("IPLookupCommandDeleteArg", None),
+            "clear": ("EmptyArg", None)}
+
+    def add(self, **kw):
+        return self.command("add", **kw)
+
+    def delete(self, **kw):
+        return self.command("delete", **kw)
+
+    def clear(self):
+        return self.command("clear")
+
+
 class Pipe:
     """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
     are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered

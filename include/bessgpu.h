@@ -212,6 +212,25 @@ size_t bg_acl_count(const bg_acl *h);
 int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
                     uint16_t igate, uint16_t *d_out, bg_stream_t stream);
 
+/* ---- IPLookup (core/modules/ip_lookup.cc) ----------------------------- */
+/* Longest-prefix match on the IPv4 destination with rte_lpm's table
+ * semantics (DPDK 19.11, as ip_lookup.cc:54-241 uses it): add replaces the
+ * next hop of an existing (prefix, depth); a new rule fails with -ENOSPC
+ * when max_rules rules exist or, deeper than /24, when its /24 block needs a
+ * tbl8 group and max_tbl8s are in use; delete of an absent rule -EINVAL.
+ * Addresses in host byte order; depth 1..32; next hop <= 0x7FFE. */
+typedef struct bg_lpm bg_lpm;
+int bg_lpm_create(uint32_t max_rules, uint32_t max_tbl8s, bg_lpm **out);
+void bg_lpm_destroy(bg_lpm *h);
+int bg_lpm_add(bg_lpm *h, uint32_t ip, int depth, uint32_t next_hop);
+int bg_lpm_delete(bg_lpm *h, uint32_t ip, int depth);
+void bg_lpm_clear(bg_lpm *h); /* rte_lpm_delete_all */
+size_t bg_lpm_count(const bg_lpm *h);
+/* ProcessBatch 76-150: out[i] = next hop of the longest matching prefix of
+ * packet i's destination (bytes 30..33), else default_gate. Stride >= 64. */
+int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
+                    uint16_t default_gate, uint16_t *d_out, bg_stream_t stream);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".

@@ -155,6 +155,8 @@ typedef struct or_acl_rule { /* ACLRule, host byte order */
   uint16_t src_port, dst_port;
   uint8_t drop, pad[3];
 } or_acl_rule;
+/* ParseIpv4Address (ip.cc:40-51): 1 on success */
+int or_ipv4_address(const char *str, uint32_t *addr);
 /* Ipv4Prefix(string) (ip.cc:63-79); -1 where std::stoi would throw */
 int or_ipv4_prefix(const char *prefix, uint32_t *addr, uint32_t *mask);
 void or_acl_process(const or_acl_rule *rules, size_t nrules, const uint8_t *base,
@@ -162,6 +164,14 @@ void or_acl_process(const or_acl_rule *rules, size_t nrules, const uint8_t *base
 double or_acl_bench(const or_acl_rule *rules, size_t nrules, const uint8_t *base,
                     size_t stride, size_t n, uint16_t igate, uint16_t *out,
                     int nthreads, int reps);
+
+/* ---- IPLookup (core/modules/ip_lookup.cc) -- oracle_more.c ------------ */
+/* longest-prefix match of each packet's IPv4 dst over (ip, depth, next hop)
+ * rules; default_gate when none matches */
+void or_lpm_process(const uint32_t *ips, const uint8_t *depths,
+                    const uint32_t *nhs, size_t nrules, const uint8_t *base,
+                    size_t stride, size_t n, uint16_t default_gate,
+                    uint16_t *out);
 
 /* ---- multi-threaded CPU baseline drivers ------------------------------ */
 /* Each thread owns a contiguous slice of the n packets (pointer batches of

@@ -199,6 +199,16 @@ static uint32_t be32(const uint8_t *p) {
 }
 static uint16_t be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
 
+/* ParseIpv4Address (core/utils/ip.cc:40-51): 1 on success */
+int or_ipv4_address(const char *str, uint32_t *addr) {
+  unsigned a, b, c, d;
+  if (sscanf(str, "%u.%u.%u.%u", &a, &b, &c, &d) != 4 || a >= 256 || b >= 256 ||
+      c >= 256 || d >= 256)
+    return 0;
+  *addr = (a << 24) | (b << 16) | (c << 8) | d;
+  return 1;
+}
+
 /* Ipv4Prefix::Ipv4Prefix (core/utils/ip.cc:63-79) + ParseIpv4Address
  * (40-51) + SetBitsLow (bits.h:193-198). Returns 0, or -1 where std::stoi
  * would throw (no digits / out of int range). */
@@ -270,4 +280,60 @@ double or_acl_bench(const or_acl_rule *rules, size_t nrules, const uint8_t *base
                     int nthreads, int reps) {
   acl_ctx c = {rules, nrules, base, stride, igate, out};
   return run_slices(acl_slice, &c, n, nthreads, reps);
+}
+
+/* ====================================================================== */
+/* IPLookup (core/modules/ip_lookup.cc) -- longest-prefix match            */
+/* ====================================================================== */
+/* The reference delegates to DPDK 19.11 rte_lpm (DIR-24-8); its lookup
+ * result is the next hop of the longest rule (ip & mask(depth) == rule ip)
+ * or the module's default gate (ip_lookup.cc:76-150). Restated here as a
+ * search over per-depth sorted rule arrays, longest depth first -- an
+ * independent formulation of the same function (no DIR-24-8). */
+
+typedef struct {
+  uint32_t ip, nh;
+} lpm_ent;
+
+static int lpm_cmp(const void *a, const void *b) {
+  uint32_t x = ((const lpm_ent *)a)->ip, y = ((const lpm_ent *)b)->ip;
+  return x < y ? -1 : x > y;
+}
+
+static uint32_t lpm_mask(int d) {
+  return d == 0 ? 0u : d >= 32 ? 0xFFFFFFFFu : ~((1u << (32 - d)) - 1u);
+}
+
+void or_lpm_process(const uint32_t *ips, const uint8_t *depths,
+                    const uint32_t *nhs, size_t nrules, const uint8_t *base,
+                    size_t stride, size_t n, uint16_t default_gate,
+                    uint16_t *out) {
+  lpm_ent *by[33];
+  size_t cnt[33] = {0};
+  for (size_t r = 0; r < nrules; r++) cnt[depths[r]]++;
+  for (int d = 0; d <= 32; d++) by[d] = (lpm_ent *)malloc((cnt[d] + 1) * sizeof(lpm_ent));
+  size_t fill[33] = {0};
+  for (size_t r = 0; r < nrules; r++) {
+    int d = depths[r];
+    by[d][fill[d]].ip = ips[r] & lpm_mask(d);
+    by[d][fill[d]].nh = nhs[r];
+    fill[d]++;
+  }
+  for (int d = 0; d <= 32; d++) qsort(by[d], cnt[d], sizeof(lpm_ent), lpm_cmp);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *ip = base + i * stride + 14;
+    uint32_t dst = be32(ip + 16); /* ip->dst.value() */
+    uint16_t g = default_gate;
+    for (int d = 32; d >= 1; d--) {
+      if (!cnt[d]) continue;
+      lpm_ent key = {dst & lpm_mask(d), 0};
+      lpm_ent *e = (lpm_ent *)bsearch(&key, by[d], cnt[d], sizeof(lpm_ent), lpm_cmp);
+      if (e) {
+        g = (uint16_t)e->nh;
+        break;
+      }
+    }
+    out[i] = g;
+  }
+  for (int d = 0; d <= 32; d++) free(by[d]);
 }

@@ -19,12 +19,15 @@ class or_acl_rule(C.Structure):
 
 
 _SIGS = {
+    "or_ipv4_address": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32)]),
     "or_ipv4_prefix": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint32),
                                  C.POINTER(C.c_uint32)]),
     "or_acl_process": (None, [_vp, _sz, _vp, _sz, _sz, C.c_uint16, _vp]),
     "or_acl_bench": (C.c_double, [_vp, _sz, _vp, _sz, _sz, C.c_uint16, _vp,
                                   C.c_int, C.c_int]),
     "or_em_make_key": (None, [_vp, _vp, _vp]),
+    "or_lpm_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_uint16,
+                              _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
     "or_hashlb_process": (None, [C.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _sz,
                                  _vp]),
@@ -192,3 +195,82 @@ class OracleACL:
         arr = self._arr()
         return mlib().or_acl_bench(arr, len(self.rules), base, stride, n, igate,
                                    out.ctypes.data, threads, reps)
+
+
+class OracleIPLookup:
+    """core/modules/ip_lookup.{h,cc} with the rte_lpm (DPDK 19.11) table
+    semantics it relies on: an existing (prefix, depth) is updated in place;
+    a new rule needs room for max_rules rules, and -- deeper than /24 -- a
+    tbl8 group for its /24 block unless one is in use (one group per /24
+    block holding deeper rules, recycled when the last one goes)."""
+
+    def __init__(self, max_rules=0, max_tbl8s=0):
+        # 54-69
+        self.max_rules = max_rules or 1024
+        self.max_tbl8s = max_tbl8s or 128
+        self.default_gate = DROP_GATE
+        self.rules = {}  # (masked ip, depth) -> next hop
+
+    @staticmethod
+    def _parse(prefix, prefix_len):
+        # 153-184 ParseIpv4Prefix
+        if not prefix:
+            raise OracleError(E.EINVAL, "prefix' is missing")
+        addr = C.c_uint32()
+        if not mlib().or_ipv4_address(prefix.encode(), C.byref(addr)):
+            raise OracleError(E.EINVAL, "Invalid IP prefix: %s" % prefix)
+        a = addr.value
+        if prefix_len > 32:
+            raise OracleError(E.EINVAL, "Invalid prefix length: %d" % prefix_len)
+        mask = 0 if prefix_len == 0 else (0xFFFFFFFF << (32 - prefix_len)) & 0xFFFFFFFF
+        if a & ~mask & 0xFFFFFFFF:
+            raise OracleError(E.EINVAL, "Invalid IP prefix %s/%d %x %x"
+                              % (prefix, prefix_len, a, mask))
+        return a
+
+    def _tbl8s_in_use(self):
+        return len({ip >> 8 for (ip, d) in self.rules if d > 24})
+
+    def add(self, prefix="", prefix_len=0, gate=0):
+        # 186-211
+        gate = int(gate) & 0xFFFF
+        a = self._parse(prefix, prefix_len)
+        if not _valid_gate(gate):
+            raise OracleError(E.EINVAL, "Invalid gate: %d" % gate)
+        if prefix_len == 0:
+            self.default_gate = gate
+            return
+        key = (a, prefix_len)
+        if key not in self.rules:
+            if len(self.rules) >= self.max_rules:
+                raise OracleError(E.ENOSPC, "rpm_lpm_add() failed")
+            if prefix_len > 24 and not any(d > 24 and ip >> 8 == a >> 8
+                                           for (ip, d) in self.rules):
+                if self._tbl8s_in_use() >= min(self.max_tbl8s, 0x7FFF):
+                    raise OracleError(E.ENOSPC, "rpm_lpm_add() failed")
+        self.rules[key] = gate
+
+    def delete(self, prefix="", prefix_len=0):
+        # 213-233
+        a = self._parse(prefix, prefix_len)
+        if prefix_len == 0:
+            self.default_gate = DROP_GATE
+            return
+        if (a, prefix_len) not in self.rules:
+            raise OracleError(E.EINVAL, "rpm_lpm_delete() failed")
+        del self.rules[(a, prefix_len)]
+
+    def clear(self):
+        self.rules = {}
+
+    def process(self, frames, stride, n):
+        out = np.empty(n, np.uint16)
+        k = list(self.rules.items())
+        ips = np.array([x[0][0] for x in k] or [0], np.uint32)
+        ds = np.array([x[0][1] for x in k] or [0], np.uint8)
+        nh = np.array([x[1] for x in k] or [0], np.uint32)
+        mlib().or_lpm_process(ips.ctypes.data, ds.ctypes.data, nh.ctypes.data,
+                              len(k), _ptr(frames), stride, n, self.default_gate,
+                              out.ctypes.data)
+        return out
+
