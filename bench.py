@@ -653,6 +653,40 @@ def run_iplookup(args, dev, torch):
     return out
 
 
+def run_update_ttl(args, dev, torch):
+    """UpdateTTL (core/modules/update_ttl.cc) in place on the C2 slab: 16M
+    64 B packets, TTL 200 (every timed launch decrements and rewrites: the
+    launches stay below 200). Bytes/pkt: 64 B header line read + the same
+    line written back whole (a partial-line write costs HBM a read-modify-
+    write, measured slower) + 2 B gate = 130."""
+    from bess_amd import packets as P
+    from bess_amd.modules import UpdateTTL
+    from oracle import oracle_more as OM
+    n = args.pkts
+    _, _, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=11)
+    frames[:, 22] = 200
+    k = min(n, 1 << 20)
+    ref = frames[:k].copy()
+    want = OM.update_ttl_process(ref, 64, k)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    g = torch.empty(n, dtype=torch.int16, device=dev)
+    m = UpdateTTL()
+    m.process_device(d, 64, n, g)
+    torch.cuda.synchronize()
+    parity = bool((g[:k].cpu().numpy().view(np.uint16) == want).all() and
+                  (d[:k * 64].cpu().numpy().reshape(k, 64) == ref).all())
+    reps = max(10, args.steps // 4)
+    warm = max(3, args.warmup // 4)
+    assert reps + warm + 1 < 199
+    ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+    return {"workload": "UpdateTTL: 64B pkts (64B slots), %d resident pkts, in "
+                        "place" % n, "pkts": n, "ms_per_step": round(ms, 4),
+            "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+            "roofline": _roof(130, n, ms),
+            "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
+                      if parity else "MISMATCH"}
+
+
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
@@ -831,6 +865,9 @@ def main():
     if args.only == "c5":
         log(json.dumps(run_c5(args, dev, torch)))
         return
+    if args.only == "ttl":
+        log(json.dumps(run_update_ttl(args, dev, torch)))
+        return
     if args.only == "iplookup":
         log(json.dumps(run_iplookup(args, dev, torch)))
         return
@@ -894,7 +931,8 @@ def main():
             out["e2e_pipe"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
                          ("HashLB", run_hashlb), ("ACL", run_acl),
-                         ("IPLookup", run_iplookup)):
+                         ("IPLookup", run_iplookup),
+                         ("UpdateTTL", run_update_ttl)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

@@ -115,6 +115,7 @@ _SIGS = {
     "bg_lpm_clear": (None, [_vp]),
     "bg_lpm_count": (_sz, [_vp]),
     "bg_lpm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
+    "bg_update_ttl": (_int, [_int, _vp, _sz, _sz, _vp, _vp]),
 }
 
 _lib = None

@@ -19,11 +19,12 @@ namespace {
 
 struct AclOp {
   using Args = AclArgs;
+  static constexpr bool kWrites = false;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const AclArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const AclArgs &) {}
   __device__ static uint32_t decide(const AclArgs &x, const uint32_t *,
-                                    const uint32_t (&d)[16], uint8_t *f) {
+                                    uint32_t (&d)[16], uint8_t *f) {
     const uint32_t sip = ip_src_le(d), dip = ip_dst_le(d);
     const uint32_t ports = l4_ports(d, f, x.stride);
     // the rule list through the constant address space: wave-uniform

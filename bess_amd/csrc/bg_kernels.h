@@ -153,6 +153,13 @@ struct LpmArgs {
   uint32_t default_gate, pad;
 };
 
+// UpdateTTL (core/modules/update_ttl.cc): in place on the frames.
+struct TtlArgs {
+  uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *out;  // 0 (emitted) or DROP_GATE
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -161,6 +168,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 
 }  // namespace bg
 

@@ -50,6 +50,7 @@ __device__ __forceinline__ uint32_t crc4(const uint32_t *T, uint32_t x) {
 template <int MODE>
 struct HlbOp {
   using Args = HlbArgs;
+  static constexpr bool kWrites = false;
   // 16-byte chunks of the first 64 bytes each mode reads
   static constexpr int c0 = MODE == kHlbL3 ? 1 : 0;
   static constexpr int c1 = MODE == kHlbL2 ? 1 : MODE == kHlbL3 ? 3 : 4;
@@ -60,7 +61,7 @@ struct HlbOp {
     hlb_stage_lds(lds, x);
   }
   __device__ static uint32_t decide(const HlbArgs &x, const uint32_t *T,
-                                    const uint32_t (&d)[16], uint8_t *f) {
+                                    uint32_t (&d)[16], uint8_t *f) {
     uint32_t crc;
     if constexpr (MODE == kHlbL2) {
       const uint32_t v = d[0] ^ d[1] ^ d[2];  // bytes [0, 12): both MACs

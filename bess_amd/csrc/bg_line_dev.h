@@ -5,12 +5,15 @@
 // An Op provides
 //   using Args = ...;   // with frames, stride, n, out (uint16_t per packet)
 //   static constexpr int c0, c1;   // 16-byte chunks [c0, c1) of the line used
+//   static constexpr bool kWrites;  // d[] chunks [c0, c1) are written back
 //   static size_t lds_bytes(const Args &);            (host) tables in LDS
 //   __device__ static void stage(uint32_t *lds, const Args &);   fill them
 //   __device__ static uint32_t decide(const Args &, const uint32_t *lds,
-//                                     const uint32_t (&d)[16], uint8_t *f);
-// d[] holds the line's dwords (only chunks [c0, c1) valid); f is the frame
-// (for rare reads past the line, or in-place writes).
+//                                     uint32_t (&d)[16], uint8_t *f);
+// d[] holds the line's dwords (only chunks [c0, c1) valid; a writing op
+// updates them in place); f is the frame (for rare reads past the line).
+// Writing ops store the chunks back whole -- through the LDS stage as
+// lane-contiguous 16-byte stores in the slab kernel -- never partial dwords.
 //
 // Two launch shapes:
 //   line_kernel      one packet per lane, its chunks loaded directly (any
@@ -65,6 +68,12 @@ __global__ __launch_bounds__(kLineBlock) void line_kernel(typename Op::Args a) {
       d[4 * c + 3] = v.w;
     }
     a.out[idx] = (uint16_t)Op::decide(a, lds, d, f);
+    if constexpr (Op::kWrites) {
+      uint4 *q = reinterpret_cast<uint4 *>(f);
+#pragma unroll
+      for (int c = Op::c0; c < Op::c1; c++)
+        q[c] = make_uint4(d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]);
+    }
   }
 }
 
@@ -118,6 +127,25 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
       uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * 64;
       a.out[idx] = (uint16_t)Op::decide(a, lds, d, f);
     }
+    if constexpr (Op::kWrites) {
+      // updated chunks back into this lane's slot of the stage, then the
+      // tile leaves with lane-contiguous 16-byte stores (whole chunks)
+#pragma unroll
+      for (int c = Op::c0; c < Op::c1; c++)
+        stage[line_stage_unit(lane, c)] =
+            make_uint4(d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const uint64_t p0 = t * 64;
+      const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
+      uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(a.frames));
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t u = c * 64 + lane;
+        const uint32_t q = u & 3;
+        if (u < units && q >= (uint32_t)Op::c0 && q < (uint32_t)Op::c1)
+          dst[p0 * 4 + u] = stage[line_stage_unit(u >> 2, q)];
+      }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
@@ -127,7 +155,7 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
 // + 2, so they are the high half of dword 3+IHL and the low half of dword
 // 4+IHL; IHL 12..15 reach past the line and are read from the frame, only
 // inside its slot (bytes past `stride` read as zero).
-__device__ __forceinline__ uint32_t l4_ports(const uint32_t (&d)[16],
+__device__ __forceinline__ uint32_t l4_ports(uint32_t (&d)[16],
                                              const uint8_t *f, uint64_t stride) {
   const uint32_t ihl = (d[3] >> 16) & 0x0F;
   uint32_t p = 0;
@@ -145,10 +173,10 @@ __device__ __forceinline__ uint32_t l4_ports(const uint32_t (&d)[16],
 }
 
 // IPv4 src / dst address (bytes 26..29 / 30..33) as LE dwords
-__device__ __forceinline__ uint32_t ip_src_le(const uint32_t (&d)[16]) {
+__device__ __forceinline__ uint32_t ip_src_le(uint32_t (&d)[16]) {
   return __builtin_amdgcn_alignbyte(d[7], d[6], 2);
 }
-__device__ __forceinline__ uint32_t ip_dst_le(const uint32_t (&d)[16]) {
+__device__ __forceinline__ uint32_t ip_dst_le(uint32_t (&d)[16]) {
   return __builtin_amdgcn_alignbyte(d[8], d[7], 2);
 }
 

@@ -19,11 +19,12 @@ namespace {
 
 struct LpmOp {
   using Args = LpmArgs;
+  static constexpr bool kWrites = false;
   static constexpr int c0 = 1, c1 = 3;  // bytes [16, 48): dst IP at 30..33
   static size_t lds_bytes(const LpmArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const LpmArgs &) {}
   __device__ static uint32_t decide(const LpmArgs &x, const uint32_t *,
-                                    const uint32_t (&d)[16], uint8_t *) {
+                                    uint32_t (&d)[16], uint8_t *) {
     const uint32_t ip = __builtin_bswap32(ip_dst_le(d));  // host order
     uint32_t e = x.tbl24[ip >> 8];
     if (e & 0x8000u) e = x.tbl8[(e & 0x7FFFu) * 256u + (ip & 0xFFu)];

@@ -203,6 +203,11 @@ class IPLookup(Module):
         return self.command("clear")
 
 
+class UpdateTTL(Module):
+    """core/modules/update_ttl.cc on the GPU."""
+    mclass = "UpdateTTL"
+
+
 class Pipe:
     """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
     are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered

@@ -231,6 +231,13 @@ size_t bg_lpm_count(const bg_lpm *h);
 int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
                     uint16_t default_gate, uint16_t *d_out, bg_stream_t stream);
 
+/* ---- UpdateTTL (core/modules/update_ttl.cc) --------------------------- */
+/* ProcessBatch 39-58 in place on a device slab: ttl > 1 -> ttl - 1 and the
+ * IPv4 checksum updated incrementally (UpdateChecksum16(csum, 2, 1)), out[i]
+ * = 0; ttl <= 1 -> out[i] = BG_DROP_GATE, frame untouched. Stride >= 32. */
+int bg_update_ttl(int device, void *d_frames, size_t stride, size_t n,
+                  uint16_t *d_out, bg_stream_t stream);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".

@@ -173,6 +173,10 @@ void or_lpm_process(const uint32_t *ips, const uint8_t *depths,
                     size_t stride, size_t n, uint16_t default_gate,
                     uint16_t *out);
 
+/* ---- UpdateTTL (core/modules/update_ttl.cc) -- oracle_more.c ---------- */
+/* in place; out[i] = 0 (emitted) or OR_DROP_GATE */
+void or_update_ttl_process(uint8_t *base, size_t stride, size_t n, uint16_t *out);
+
 /* ---- multi-threaded CPU baseline drivers ------------------------------ */
 /* Each thread owns a contiguous slice of the n packets (pointer batches of
  * 32 over base + i*stride) and sweeps it `reps` times; threads are pinned to

@@ -337,3 +337,22 @@ void or_lpm_process(const uint32_t *ips, const uint8_t *depths,
   }
   for (int d = 0; d <= 32; d++) free(by[d]);
 }
+
+/* ====================================================================== */
+/* UpdateTTL (core/modules/update_ttl.cc:39-58)                            */
+/* ====================================================================== */
+void or_update_ttl_process(uint8_t *base, size_t stride, size_t n, uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    uint8_t *ip = base + i * stride + 14;
+    if (ip[8] > 1) { /* ip->ttl */
+      uint16_t ck;
+      memcpy(&ck, ip + 10, 2);
+      ck = or_update_checksum16(ck, 2, 1);
+      memcpy(ip + 10, &ck, 2);
+      ip[8] -= 1;
+      out[i] = 0;
+    } else {
+      out[i] = OR_DROP_GATE;
+    }
+  }
+}

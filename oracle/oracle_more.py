@@ -26,6 +26,7 @@ _SIGS = {
     "or_acl_bench": (C.c_double, [_vp, _sz, _vp, _sz, _sz, C.c_uint16, _vp,
                                   C.c_int, C.c_int]),
     "or_em_make_key": (None, [_vp, _vp, _vp]),
+    "or_update_ttl_process": (None, [_vp, _sz, _sz, _vp]),
     "or_lpm_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_uint16,
                               _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
@@ -274,3 +275,10 @@ class OracleIPLookup:
                               out.ctypes.data)
         return out
 
+
+
+def update_ttl_process(frames, stride, n):
+    """UpdateTTL::ProcessBatch (update_ttl.cc:39-58), in place -> gates"""
+    out = np.empty(n, np.uint16)
+    mlib().or_update_ttl_process(_ptr(frames), stride, n, out.ctypes.data)
+    return out
