@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the C3/C4/sweep secondary measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host end-to-end legs (16 launching threads "
+                         "crash rocprofv3's kernel tracer)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
     ap.add_argument("--only", default="", help="cksum|wm|c5 (profiling runs)")
     return ap.parse_args()
@@ -557,7 +560,8 @@ def run_hashlb(args, dev, torch):
         ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
         out[name] = {"ms_per_step": round(ms, 4),
                      "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-                     "roofline": _roof(EM_BYTES_PER_PKT, n, ms),
+                     "roofline": _roof(EM_BYTES_PER_PKT, n, ms,
+                                       "hashlb" if name == "l4" else None),
                      "parity": "bit-exact vs oracle on %d pkts" % k
                                if parity else "MISMATCH"}
         if name == "l4" and not args.no_cpu:
@@ -604,7 +608,7 @@ def run_acl(args, dev, torch):
                        o.process(frames, 64, k)).all())
         ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
         e = {"ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-             "roofline": _roof(EM_BYTES_PER_PKT, n, ms),
+             "roofline": _roof(EM_BYTES_PER_PKT, n, ms, "acl"),
              "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}
         if not args.no_cpu:
             cn = 1 << 16
@@ -648,7 +652,7 @@ def run_iplookup(args, dev, torch):
     out = {"workload": "IPLookup: 64B pkts (64B slots), %d resident pkts, 10K "
                        "routes, DIR-24-8" % n, "pkts": n, "routes": len(o.rules),
            "ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-           "roofline": _roof(EM_BYTES_PER_PKT, n, ms),
+           "roofline": _roof(EM_BYTES_PER_PKT, n, ms, "iplookup"),
            "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}
     return out
 
@@ -682,7 +686,7 @@ def run_update_ttl(args, dev, torch):
     return {"workload": "UpdateTTL: 64B pkts (64B slots), %d resident pkts, in "
                         "place" % n, "pkts": n, "ms_per_step": round(ms, 4),
             "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-            "roofline": _roof(130, n, ms),
+            "roofline": _roof(130, n, ms, "ttl"),
             "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
                       if parity else "MISMATCH"}
 
@@ -908,7 +912,7 @@ def main():
                      if args.rules == 1000 and r["n"] == 16 << 20 else None,
                      "traffic_bytes_per_launch": load_traffic("em")
                      if args.rules == 1000 and r["n"] == 16 << 20 else None,
-                     "kernel": "em_classify_kernel",
+                     "kernel": "em_slab_kernel",
                      "kernel_ms": round(kern_ms, 4),
                      "bytes_per_pkt": EM_BYTES_PER_PKT},
         "parity": "bit-exact vs oracle on 1M-pkt sample" if r["parity"]
@@ -921,14 +925,15 @@ def main():
         except Exception as e:  # report, do not hide
             out["batch_sweep_mpps"] = "failed: %r" % (e,)
         out["extra_configs"] = {}
-        try:
-            out["e2e_host"] = run_e2e_host(r, args, torch)
-        except Exception as e:
-            out["e2e_host"] = "failed: %r" % (e,)
-        try:
-            out["e2e_pipe"] = run_e2e_pipe(args, torch)
-        except Exception as e:
-            out["e2e_pipe"] = "failed: %r" % (e,)
+        if not args.no_e2e:
+            try:
+                out["e2e_host"] = run_e2e_host(r, args, torch)
+            except Exception as e:
+                out["e2e_host"] = "failed: %r" % (e,)
+            try:
+                out["e2e_pipe"] = run_e2e_pipe(args, torch)
+            except Exception as e:
+                out["e2e_pipe"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
                          ("HashLB", run_hashlb), ("ACL", run_acl),
                          ("IPLookup", run_iplookup),

@@ -24,16 +24,18 @@ if [[ "$MODE" == *bench* ]] || [ "$MODE" = all ]; then
 fi
 if [[ "$MODE" == *prof* ]] || [ "$MODE" = all ]; then
   # kernel trace of the default bench command (every kernel of the line)
-  step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py"
+  # (the host end-to-end legs launch from 16 threads, which crashes the
+  # tracer; every device-resident kernel of the line is traced)
+  step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-e2e
 fi
 if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
   rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
   i=0
-  for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+  for C in ${PMC_SETS:-"FETCH_SIZE" "WRITE_SIZE"}; do
     i=$((i+1))
-    for W in em cksum wm c5; do
+    for W in ${PMC_WL:-em cksum wm c5 hashlb acl iplookup ttl}; do
       if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --no-cpu --steps 3 --warmup 1"; fi
-      step pmc_${W}_$i 900 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
+      step pmc_${W}_$i 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
     done
   done
   python3 scripts/pmc_traffic.py "$OUT" "$OUT/traffic.json" > "$OUT/pmc_traffic.out" 2>&1 || true

@@ -50,11 +50,13 @@ def routes(n, rng, deep_frac=0.1):
 
 
 def dsts_inside(rt, n, rng):
+    """n destinations, each inside a uniformly picked route"""
     import ipaddress
+    base = np.array([int(ipaddress.IPv4Address(p)) for p, _, _ in rt], np.uint64)
+    plen = np.array([pl for _, pl, _ in rt], np.int64)
     pick = rng.integers(0, len(rt), n)
-    base = np.array([int(ipaddress.IPv4Address(rt[i][0])) for i in pick], np.uint64)
-    host = np.array([rng.integers(0, 1 << (32 - rt[i][1])) for i in pick], np.uint64)
-    return base | host
+    host = rng.integers(0, np.left_shift(1, 32 - plen[pick]), dtype=np.int64)
+    return base[pick] | host.astype(np.uint64)
 
 
 def frames_to(dsts, stride=64):
