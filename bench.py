@@ -53,7 +53,7 @@ def parse():
                     help="skip the host end-to-end legs (16 launching threads "
                          "crash rocprofv3's kernel tracer)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
-    ap.add_argument("--only", default="", help="cksum|wm|c5 (profiling runs)")
+    ap.add_argument("--only", default="", help="cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|pipe (profiling runs)")
     return ap.parse_args()
 
 
@@ -691,6 +691,55 @@ def run_update_ttl(args, dev, torch):
                       if parity else "MISMATCH"}
 
 
+def nat_pairs():
+    """16 pairs: 8 /16s 10.i.0.0 -> 100.i.0.0 then their images mapped
+    back, so every launch translates the same packets again (steady state)"""
+    pairs = []
+    for back in (0, 1):
+        for i in range(8):
+            a, b = "10.%d" % i, "100.%d" % i
+            if back:
+                a, b = b, a
+            pairs.append({"int_range": {"start": a + ".0.0", "end": a + ".255.255"},
+                          "ext_range": {"start": b + ".0.0", "end": b + ".255.255"}})
+    return pairs
+
+
+def run_static_nat(args, dev, torch):
+    """StaticNAT (core/modules/static_nat.cc) forward direction in place on
+    the C2 slab: 16M 64 B packets, 16 address pairs, half the sources inside
+    a pair (translated, IP + L4 checksums updated), half outside (all 16
+    pairs scanned). Bytes/pkt: 64 B line read + 64 B written back + 2 B
+    gate = 130."""
+    from bess_amd import packets as P
+    from bess_amd.modules import StaticNAT
+    from oracle import oracle_more as OM
+    n = args.pkts
+    _, _, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=13)
+    rng = np.random.default_rng(13)
+    hit = rng.random(n) < 0.5
+    frames[hit, 26] = 10
+    frames[hit, 27] = rng.integers(0, 8, int(hit.sum()), dtype=np.uint8)
+    k = min(n, 1 << 20)
+    ref = frames[:k].copy()
+    want = OM.OracleStaticNAT(pairs=nat_pairs()).process(ref, 64, k)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    g = torch.empty(n, dtype=torch.int16, device=dev)
+    m = StaticNAT(pairs=nat_pairs())
+    m.process_device(d, 64, n, g)
+    torch.cuda.synchronize()
+    parity = bool((g[:k].cpu().numpy().view(np.uint16) == want).all() and
+                  (d[:k * 64].cpu().numpy().reshape(k, 64) == ref).all())
+    ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+    return {"workload": "StaticNAT forward: 64B pkts (64B slots), %d resident "
+                        "pkts, 16 pairs, 50%% translated, in place" % n,
+            "pkts": n, "ms_per_step": round(ms, 4),
+            "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+            "roofline": _roof(130, n, ms, "nat"),
+            "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
+                      if parity else "MISMATCH"}
+
+
 def run_wm(args, dev, torch):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
@@ -872,6 +921,9 @@ def main():
     if args.only == "ttl":
         log(json.dumps(run_update_ttl(args, dev, torch)))
         return
+    if args.only == "nat":
+        log(json.dumps(run_static_nat(args, dev, torch)))
+        return
     if args.only == "iplookup":
         log(json.dumps(run_iplookup(args, dev, torch)))
         return
@@ -937,7 +989,8 @@ def main():
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
                          ("HashLB", run_hashlb), ("ACL", run_acl),
                          ("IPLookup", run_iplookup),
-                         ("UpdateTTL", run_update_ttl)):
+                         ("UpdateTTL", run_update_ttl),
+                         ("StaticNAT", run_static_nat)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

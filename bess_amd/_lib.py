@@ -81,6 +81,7 @@ _SIGS = {
     "bg_module_process": (_int, [_vp, _vp, _sz, _vp]),
     "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
     "bg_module_set_device": (_int, [_vp, _int]),
+    "bg_module_set_igate": (_int, [_vp, _u16]),
     "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
     "bg_debug_key": (_int, [C.POINTER(bg_field), _int, _int, _vp, _vp]),
     "bg_em_classify_window": (_int, [_vp, _vp, _sz, _sz, _int, _u16, _vp, _vp]),
@@ -116,6 +117,11 @@ _SIGS = {
     "bg_lpm_count": (_sz, [_vp]),
     "bg_lpm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
     "bg_update_ttl": (_int, [_int, _vp, _sz, _sz, _vp, _vp]),
+    "bg_snat_create": (_int, [C.POINTER(_vp)]),
+    "bg_snat_destroy": (None, [_vp]),
+    "bg_snat_add": (_int, [_vp, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "bg_snat_count": (_sz, [_vp]),
+    "bg_snat_classify": (_int, [_vp, _vp, _sz, _sz, _int, _vp, _vp]),
 }
 
 _lib = None

@@ -160,6 +160,18 @@ struct TtlArgs {
   uint16_t *out;  // 0 (emitted) or DROP_GATE
 };
 
+// StaticNAT (core/modules/static_nat.cc): pairs of 4 dwords {start in
+// the matched direction, start on the other side, size, 0} (host order),
+// padded to a multiple of 4 with size-0 pairs; dir 0 rewrites the source
+// (input gate 0 -> output gate 1), dir 1 the destination (1 -> 0).
+struct NatArgs {
+  uint8_t *frames;
+  uint64_t stride, n;
+  uint16_t *out;
+  const uint32_t *pairs;
+  uint32_t npairs, dir;
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -169,6 +181,7 @@ hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
 
 }  // namespace bg
 

@@ -262,6 +262,74 @@ void em_slab_kernel(EmArgs a) {
   }
 }
 
+// Compact-stage slab kernel: only the NCH chunks of each slot's key window
+// are loaded and staged (64 x NCH x 16 B per wave instead of 4 KB), so a
+// workgroup of BLOCK threads fits beside the LDS table at twice the
+// occupancy. Lane l of load c takes unit u = 64c + l of the tile: slot
+// u / NCH, window chunk u % NCH -- pieces of 16 * NCH contiguous bytes per
+// slot. Stage unit of (slot s, chunk j): s*NCH + ((j + s/8) % NCH), which
+// keeps the per-slot reads of 16 lanes on distinct bank groups.
+template <int KW, int NCH, int BLOCK>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80)))
+void em_slab2_kernel(EmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  copy_table_to_lds(lds, a.t);
+  const uint32_t stage_off =
+      a.t.lds == kLdsTable ? ((a.t.bytes_total + 15) & ~15u) : 0u;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  constexpr int kWaves = BLOCK / 64;
+  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_off) + wid * (64 * NCH);
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
+  const uint32_t q0 = (uint32_t)a.fp.win_lo >> 4;
+  const uint32_t nch = (uint32_t)a.fp.nch;
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  uint4 v[NCH];
+  auto load_tile = [&](uint64_t tile) {
+    const uint64_t p0 = tile * 64;
+    const uint32_t nslots = (uint32_t)(a.n - p0 < 64 ? a.n - p0 : 64);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const uint32_t u = c * 64 + lane;
+      const uint32_t sl = u / NCH, j = u % NCH;
+      v[c] = (sl < nslots && j < nch) ? ld_stream(src + (p0 + sl) * 4 + q0 + j)
+                                      : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (t < ntiles) load_tile(t);
+  for (; t < ntiles; t += nwaves) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const uint32_t u = c * 64 + lane;
+      const uint32_t sl = u / NCH, j = u % NCH;
+      stage[sl * NCH + ((j + (sl >> 3)) % NCH)] = v[c];
+    }
+    lds_fence();
+    if (t + nwaves < ntiles) load_tile(t + nwaves);
+    uint32_t w[NCH * 4 + 2];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const uint4 x = stage[lane * NCH + ((c + (lane >> 3)) % NCH)];
+      w[4 * c] = x.x;
+      w[4 * c + 1] = x.y;
+      w[4 * c + 2] = x.z;
+      w[4 * c + 3] = x.w;
+    }
+    w[NCH * 4] = 0;
+    w[NCH * 4 + 1] = 0;
+    uint64_t k[KW];
+    extract_key<KW, NCH>(w, a.fp, k);
+    const uint32_t g = a.t.lds == kLdsTable
+                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
+                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
+    const uint64_t idx = t * 64 + lane;
+    if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    lds_fence();  // this tile's stage reads retire before the next writes
+  }
+}
+
 // unconstrained SGPRs (A/B experiments only: BG_FAT=1)
 template <int KW, int NCH, int PPL>
 __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
@@ -1282,9 +1350,35 @@ bool fits_nch2(const FieldPlan &fp) {
 
 // Dense 64 B slots with the key window inside the slot: the coalesced
 // slab kernel (em_slab_kernel). LDS = table (if staged) + 4 KB per wave.
+template <int KW, int NCH, int BLOCK>
+hipError_t launch_em_slab2(EmArgs a, int num_cus, hipStream_t s) {
+  auto kern = em_slab2_kernel<KW, NCH, BLOCK>;
+  const uint64_t need = (a.n + BLOCK - 1) / BLOCK;
+  constexpr size_t kStage = (size_t)(BLOCK / 64) * 64 * NCH * 16;
+  for (int pass = 0; pass < 2; pass++) {
+    const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
+    const size_t lds = tab + kStage;
+    int pc = env_int("BG_BLOCKS_PER_CU", 0);
+    if (pc <= 0) pc = occupancy(reinterpret_cast<const void *>(kern), BLOCK, lds, 1);
+    const uint64_t cap = (uint64_t)num_cus * pc;
+    const uint64_t blocks = need > cap ? cap : need;
+    if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
+        !env_int("BG_FORCE_LDS", 0)) {
+      a.t.lds = kLdsNone;  // small launch: probe the table in L2 instead
+      continue;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), lds, s, a);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int KW, int NCH>
 hipError_t launch_em_slab(EmArgs a, int num_cus, hipStream_t s) {
   if (env_int("BG_NOLDS", 0)) a.t.lds = kLdsNone;
+  const int v2 = env_int("BG_SLAB2", 0);
+  if (v2 == 512) return launch_em_slab2<KW, NCH, 512>(a, num_cus, s);
+  if (v2 == 1024) return launch_em_slab2<KW, NCH, 1024>(a, num_cus, s);
   // prefetch depth (tiles ahead), measured on MI355X: scripts/variants.py
   const int pf = std::min(2, std::max(0, env_int("BG_SLAB_PF", 1)));
   using K = void (*)(EmArgs);

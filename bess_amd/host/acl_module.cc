@@ -141,7 +141,6 @@ class ACL final : public Module {
 
  private:
   bg_acl *h_ = nullptr;
-  gate_idx_t igate_ = 0;  // ctx->current_igate: the module's single input
 };
 
 const Commands ACL::kCmds = {

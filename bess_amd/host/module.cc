@@ -141,6 +141,11 @@ int bg_module_set_device(bg_module *h, int device) {
   return 0;
 }
 
+int bg_module_set_igate(bg_module *h, uint16_t igate) {
+  h->m->set_igate(igate);
+  return 0;
+}
+
 int bg_module_desc(const bg_module *h, char *buf, size_t len) {
   std::string d = h->m->GetDesc();
   if (buf && len) {

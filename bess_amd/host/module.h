@@ -163,6 +163,9 @@ class Module {
   }
   void set_device(int d) { device_ = d; }
   int device() const { return device_; }
+  // ctx->current_igate of the calls that follow (core/module.h:59-75)
+  void set_igate(gate_idx_t g) { igate_ = g; }
+  gate_idx_t igate() const { return igate_; }
 
   // Module::AddMetadataAttr (core/module.cc:248-285): per-module metadata
   // attributes; returns the attribute id or -errno.
@@ -191,6 +194,7 @@ class Module {
 
  protected:
   int device_ = 0;
+  gate_idx_t igate_ = 0;
   std::vector<Attribute> attrs_;
 };
 

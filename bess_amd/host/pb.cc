@@ -414,5 +414,35 @@ void IPLookupCommandAddArg::Write(Writer &w) const {
   if (gate_) w.varint_field(3, gate_);
 }
 
+bool StaticNATArg_AddressRange::MergeField(Reader &r, uint32_t field,
+                                           uint32_t wt) {
+  if (field == 1) return read_str(r, wt, &start_);
+  if (field == 2) return read_str(r, wt, &end_);
+  return r.skip(wt);
+}
+void StaticNATArg_AddressRange::Write(Writer &w) const {
+  write_str(w, 1, start_);
+  write_str(w, 2, end_);
+}
+
+bool StaticNATArg_AddressRangePair::MergeField(Reader &r, uint32_t field,
+                                               uint32_t wt) {
+  if (field == 1) return read_msg(r, wt, &int_range_);
+  if (field == 2) return read_msg(r, wt, &ext_range_);
+  return r.skip(wt);
+}
+void StaticNATArg_AddressRangePair::Write(Writer &w) const {
+  write_msg(w, 1, int_range_);
+  write_msg(w, 2, ext_range_);
+}
+
+bool StaticNATArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_msg(r, wt, pairs_.Add());
+  return r.skip(wt);
+}
+void StaticNATArg::Write(Writer &w) const {
+  for (auto &x : pairs_) write_msg(w, 1, x);
+}
+
 }  // namespace pb
 }  // namespace bess

@@ -443,6 +443,46 @@ using IPLookupCommandDeleteArg = IPLookupCommandAddArg;
 
 using UpdateTTLArg = EmptyArg;
 
+// module_msg.proto:729-741
+class StaticNATArg_AddressRange : public Message {
+ public:
+  const std::string &start() const { return start_; }
+  const std::string &end() const { return end_; }
+  void set_start(const std::string &v) { start_ = v; }
+  void set_end(const std::string &v) { end_ = v; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  std::string start_, end_;
+};
+
+class StaticNATArg_AddressRangePair : public Message {
+ public:
+  const StaticNATArg_AddressRange &int_range() const { return int_range_; }
+  const StaticNATArg_AddressRange &ext_range() const { return ext_range_; }
+  StaticNATArg_AddressRange *mutable_int_range() { return &int_range_; }
+  StaticNATArg_AddressRange *mutable_ext_range() { return &ext_range_; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  StaticNATArg_AddressRange int_range_, ext_range_;
+};
+
+class StaticNATArg : public Message {
+ public:
+  int pairs_size() const { return pairs_.size(); }
+  const StaticNATArg_AddressRangePair &pairs(int i) const { return pairs_.Get(i); }
+  const Repeated<StaticNATArg_AddressRangePair> &pairs() const { return pairs_; }
+  StaticNATArg_AddressRangePair *add_pairs() { return pairs_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<StaticNATArg_AddressRangePair> pairs_;
+};
+
 }  // namespace pb
 }  // namespace bess
 

@@ -97,6 +97,11 @@ class Module:
     def set_device(self, device):
         lib().bg_module_set_device(self.h, device)
 
+    def set_igate(self, igate):
+        """the input gate the following process calls arrive on
+        (ctx->current_igate, core/module.h:59-75)"""
+        lib().bg_module_set_igate(self.h, igate)
+
     def process(self, frames, stride, n):
         """ProcessBatch over host frames (numpy uint8 slab, frame i at
         i*stride, each with >= 2048 accessible bytes for the checksum
@@ -206,6 +211,18 @@ class IPLookup(Module):
 class UpdateTTL(Module):
     """core/modules/update_ttl.cc on the GPU."""
     mclass = "UpdateTTL"
+
+
+class StaticNAT(Module):
+    """core/modules/static_nat.cc on the GPU: input gate 0 translates the
+    source (emits on 1), input gate 1 the destination (emits on 0)."""
+    mclass = "StaticNAT"
+    cmds = {"get_initial_arg": ("EmptyArg", "StaticNATArg"),
+            "get_runtime_config": ("EmptyArg", None),
+            "set_runtime_config": ("EmptyArg", None)}
+
+    def get_initial_arg(self):
+        return self.command("get_initial_arg")
 
 
 class Pipe:

@@ -90,6 +90,15 @@ _MESSAGES = [
         ("prefix", 1, _F.TYPE_STRING, 1, None, None),
         ("prefix_len", 2, _F.TYPE_UINT64, 1, None, None)]),
     ("UpdateTTLArg", []),
+    # module_msg.proto:729-741 (nested messages as top-level ones; the wire
+    # bytes are the same)
+    ("StaticNATArg_AddressRange", [("start", 1, _F.TYPE_STRING, 1, None, None),
+                                   ("end", 2, _F.TYPE_STRING, 1, None, None)]),
+    ("StaticNATArg_AddressRangePair", [
+        ("int_range", 1, _F.TYPE_MESSAGE, 1, ".bess.pb.StaticNATArg_AddressRange", None),
+        ("ext_range", 2, _F.TYPE_MESSAGE, 1, ".bess.pb.StaticNATArg_AddressRange", None)]),
+    ("StaticNATArg", [("pairs", 1, _F.TYPE_MESSAGE, 3,
+                       ".bess.pb.StaticNATArg_AddressRangePair", None)]),
 ]
 
 

@@ -238,6 +238,20 @@ int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
 int bg_update_ttl(int device, void *d_frames, size_t stride, size_t n,
                   uint16_t *d_out, bg_stream_t stream);
 
+/* ---- StaticNAT (core/modules/static_nat.cc) --------------------------- */
+/* Address pairs [int_addr, +size) <-> [ext_addr, +size), host byte order,
+ * in order. ProcessBatch 146-181 in place: dir 0 (input gate 0) maps the
+ * source of the first pair whose internal range holds it and emits on gate
+ * 1; dir 1 maps the destination from the external range and emits on gate
+ * 0; IPv4 and TCP/UDP checksums updated incrementally (RFC 1624). */
+typedef struct bg_snat bg_snat;
+int bg_snat_create(bg_snat **out);
+void bg_snat_destroy(bg_snat *h);
+int bg_snat_add(bg_snat *h, uint32_t int_addr, uint32_t ext_addr, uint32_t size);
+size_t bg_snat_count(const bg_snat *h);
+int bg_snat_classify(bg_snat *h, void *d_frames, size_t stride, size_t n,
+                     int dir, uint16_t *d_out, bg_stream_t stream);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".
@@ -260,6 +274,9 @@ int bg_module_process(bg_module *m, uint8_t *const *heads, size_t cnt,
 int bg_module_process_device(bg_module *m, void *d_frames, size_t stride,
                              size_t n, uint16_t *d_ogates, bg_stream_t stream);
 int bg_module_set_device(bg_module *m, int device);
+/* the input gate the next process calls arrive on (ctx->current_igate:
+ * ACL emits on it, StaticNAT picks its direction by it); default 0 */
+int bg_module_set_igate(bg_module *m, uint16_t igate);
 /* GetDesc() (exact_match.cc:246-249, wildcard_match.cc:205-213) */
 int bg_module_desc(const bg_module *m, char *buf, size_t len);
 

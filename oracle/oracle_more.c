@@ -356,3 +356,65 @@ void or_update_ttl_process(uint8_t *base, size_t stride, size_t n, uint16_t *out
     }
   }
 }
+
+/* ====================================================================== */
+/* StaticNAT (core/modules/static_nat.cc)                                  */
+/* ====================================================================== */
+/* UpdateChecksumWithIncrement (checksum.h:535-538) */
+static uint16_t upd_ck(uint16_t ck, uint32_t incr) {
+  return or_fold_checksum((uint32_t)(~ck & 0xFFFF) + incr);
+}
+
+/* UpdateChecksum 118-144 */
+static void snat_update_checksum(uint8_t *ip, uint32_t incr) {
+  size_t ip_bytes = (size_t)(ip[0] & 0x0F) << 2;
+  uint8_t *l4 = ip + ip_bytes;
+  uint8_t proto = ip[9];
+  uint16_t ck;
+  memcpy(&ck, ip + 10, 2);
+  ck = upd_ck(ck, incr);
+  memcpy(ip + 10, &ck, 2);
+  if (proto == 6) {
+    memcpy(&ck, l4 + 16, 2);
+    ck = upd_ck(ck, incr);
+    memcpy(l4 + 16, &ck, 2);
+  } else if (proto == 17) {
+    memcpy(&ck, l4 + 6, 2);
+    if (ck != 0) {
+      ck = upd_ck(ck, incr);
+      if (ck == 0) ck = 0xFFFF;
+      memcpy(l4 + 6, &ck, 2);
+    }
+  }
+}
+
+/* DoProcessBatch<dir> 146-181: dir 0 forward (src, emit on 1), 1 reverse */
+void or_static_nat_process(const uint32_t *int_addr, const uint32_t *ext_addr,
+                           const uint32_t *size, size_t npairs, uint8_t *base,
+                           size_t stride, size_t n, int dir, uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    uint8_t *ip = base + i * stride + 14;
+    uint8_t *a = dir == 0 ? ip + 12 : ip + 16;
+    uint32_t raw;
+    memcpy(&raw, a, 4);
+    uint32_t addr = be32(a);
+    for (size_t p = 0; p < npairs; p++) {
+      uint32_t start = dir == 0 ? int_addr[p] : ext_addr[p];
+      if (start <= addr && addr < start + size[p]) {
+        uint32_t diff = dir == 0 ? ext_addr[p] - int_addr[p] : int_addr[p] - ext_addr[p];
+        uint32_t na = addr + diff;
+        uint8_t nb[4] = {(uint8_t)(na >> 24), (uint8_t)(na >> 16), (uint8_t)(na >> 8),
+                         (uint8_t)na};
+        uint32_t nraw;
+        memcpy(&nraw, nb, 4);
+        /* ChecksumIncrement32(old raw, new raw) 520-525 */
+        uint32_t incr = (~raw >> 16) + (~raw & 0xFFFF);
+        incr += (nraw >> 16) + (nraw & 0xFFFF);
+        snat_update_checksum(ip, incr);
+        memcpy(a, nb, 4);
+        break;
+      }
+    }
+    out[i] = dir == 0 ? 1 : 0;
+  }
+}

@@ -1,5 +1,5 @@
 """TEST INFRASTRUCTURE ONLY: control-plane restatements of the SURVEY §8f
-modules (HashLB, ACL, IPLookup, UpdateTTL) around oracle_more.c. Only
+modules (HashLB, ACL, IPLookup, UpdateTTL, StaticNAT) around oracle_more.c. Only
 tests/, smoke() and bench.py's cpu_baseline leg import this. Each method
 cites the reference file:line it follows; errors raise OracleError(errno,
 message) with the reference's text."""
@@ -27,6 +27,8 @@ _SIGS = {
                                   C.c_int, C.c_int]),
     "or_em_make_key": (None, [_vp, _vp, _vp]),
     "or_update_ttl_process": (None, [_vp, _sz, _sz, _vp]),
+    "or_static_nat_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_int,
+                                     _vp]),
     "or_lpm_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_uint16,
                               _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
@@ -282,3 +284,60 @@ def update_ttl_process(frames, stride, n):
     out = np.empty(n, np.uint16)
     mlib().or_update_ttl_process(_ptr(frames), stride, n, out.ctypes.data)
     return out
+
+
+def _ipv4(s):
+    """ParseIpv4Address (core/utils/ip.cc:40-51) -> host-order int or None"""
+    a = C.c_uint32()
+    return a.value if mlib().or_ipv4_address(s.encode(), C.byref(a)) else None
+
+
+class OracleStaticNAT:
+    """core/modules/static_nat.{h,cc}"""
+
+    def __init__(self, pairs=()):
+        # Init 46-90
+        self.pairs_ = []
+        for p in pairs:
+            ir, er = p.get("int_range", {}), p.get("ext_range", {})
+            vals = []
+            for rng, what in ((ir, "internal"), (er, "external")):
+                st, en = rng.get("start", ""), rng.get("end", "")
+                a = _ipv4(st)
+                if a is None:
+                    raise OracleError(E.EINVAL, "invalid IP address %s" % st)
+                b = _ipv4(en)
+                if b is None:
+                    raise OracleError(E.EINVAL, "invalid IP address %s" % en)
+                if a > b:
+                    raise OracleError(E.EINVAL,
+                                      "invalid %s IP address range" % what)
+                vals += [a, b]
+            is_, ie, es, ee = vals
+            if ie == 0xFFFFFFFF or ee == 0xFFFFFFFF:
+                raise OracleError(E.EINVAL, "cannot map broadcast address")
+            if ie - is_ != ee - es:
+                raise OracleError(E.EINVAL,
+                                  "internal/external address ranges differ")
+            self.pairs_.append((is_, es, ie - is_ + 1))
+
+    def get_initial_arg(self):
+        # 92-109: the end reported is start + size (one past the range)
+        f = lambda a: "%d.%d.%d.%d" % (a >> 24, (a >> 16) & 255, (a >> 8) & 255,
+                                       a & 255)
+        return {"pairs": [{"int_range": {"start": f(i), "end": f(i + z)},
+                           "ext_range": {"start": f(e), "end": f(e + z)}}
+                          for i, e, z in self.pairs_]}
+
+    def process(self, frames, stride, n, igate=0):
+        """ProcessBatch 179-187 (igate 0 forward, else reverse), in place"""
+        k = self.pairs_ or [(0, 0, 0)]
+        ia = np.array([x[0] for x in k], np.uint32)
+        ea = np.array([x[1] for x in k], np.uint32)
+        sz = np.array([x[2] for x in k], np.uint32)
+        out = np.empty(n, np.uint16)
+        mlib().or_static_nat_process(ia.ctypes.data, ea.ctypes.data,
+                                     sz.ctypes.data, len(self.pairs_),
+                                     _ptr(frames), stride, n,
+                                     0 if igate == 0 else 1, out.ctypes.data)
+        return out

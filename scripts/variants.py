@@ -23,7 +23,7 @@ from bess_amd import packets as P  # noqa: E402
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF",
-         "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK"]
+         "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2"]
 
 
 def set_env(v):
@@ -73,6 +73,9 @@ def main():
             "slab_pf2_bpc1": {"BG_SLAB_PF": 2, "BG_BLOCKS_PER_CU": 1},
             "slab_l2tab_pf2": {"BG_NOLDS": 1, "BG_SLAB_PF": 2},
             "lane": {"BG_NO_SLAB": 1},
+            "slab2_512": {"BG_SLAB2": 512},
+            "slab2_1024": {"BG_SLAB2": 1024},
+            "slab2_1024_l2tab": {"BG_SLAB2": 1024, "BG_NOLDS": 1},
         }
         # every variant must give identical gates
         for name, env in variants.items():
