@@ -795,7 +795,8 @@ def run_wm(args, dev, torch):
            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
            "table_bytes": nbytes,
            "table_in_lds": {0: "no (L2/MALL)", 1: "whole table",
-                            2: "key filter (table in L2/MALL)"}[int(in_lds)],
+                            2: "key filter (table in L2/MALL)",
+                            3: "tag words (keys/values in L2/MALL)"}[int(in_lds)],
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),

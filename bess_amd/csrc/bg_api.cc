@@ -239,7 +239,10 @@ TableRef DevTable::ref() const {
   t.bytes_total = (uint32_t)std::min<uint64_t>(tb, 0xFFFFFFFFu);
   t.filt_words = filt_words;
   t.filt_off = filt_off;
-  t.lds = tb <= kLdsTableMax ? kLdsTable : (filt_words ? kLdsFilter : kLdsNone);
+  t.lds = tb <= kLdsTableMax ? kLdsTable
+          : tags_lds       ? kLdsTags
+          : filt_words     ? kLdsFilter
+                           : kLdsNone;
   return t;
 }
 
@@ -247,19 +250,17 @@ TableRef DevTable::ref() const {
 int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
                 const std::vector<uint64_t> &keys,
                 const std::vector<uint8_t> &vals,
-                const std::vector<uint64_t> &seeds, std::vector<uint8_t> *img,
-                TableLayout *out_layout) {
-  const size_t n = seeds.size();
+                const std::vector<uint64_t> &hashes, std::vector<uint8_t> *img,
+                TableLayout *out_layout, double max_load) {
+  const size_t n = hashes.size();
   // count entries per partition to size the layout
   std::vector<std::vector<size_t>> members(nparts);
   TableLayout L = plan_layout(0, kw, val_bytes, nparts, kDefaultSeed);
-  for (size_t i = 0; i < n; i++) {
-    uint64_t h = hash_words(&keys[i * kw], (int)kw, seeds[i]);
-    members[split_hash(h, nparts, 2).part].push_back(i);
-  }
+  for (size_t i = 0; i < n; i++)
+    members[split_hash(hashes[i], nparts, 2).part].push_back(i);
   size_t maxc = 0;
   for (auto &m : members) maxc = std::max(maxc, m.size());
-  L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed);
+  L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load);
   for (int attempt = 0; attempt < 8; attempt++) {
     img->assign((size_t)L.part_bytes * nparts, 0);
     bool ok = true;
@@ -269,7 +270,7 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
       for (size_t i : members[p]) {
         pk.insert(pk.end(), &keys[i * kw], &keys[i * kw] + kw);
         pv.insert(pv.end(), &vals[i * val_bytes], &vals[i * val_bytes] + val_bytes);
-        ps.push_back(seeds[i]);
+        ps.push_back(hashes[i]);
       }
       ok = build_partition(L, p, members[p].size(), pk.data(), pv.data(),
                            ps.data(), img->data() + (size_t)p * L.part_bytes);
@@ -476,7 +477,7 @@ static void em_entries(const bg_em *em, std::vector<uint64_t> *keys,
     keys->insert(keys->end(), kv.first.w, kv.first.w + em->kw);
     vals->push_back((uint8_t)kv.second);
     vals->push_back((uint8_t)(kv.second >> 8));
-    seeds->push_back(kDefaultSeed);
+    seeds->push_back(hash_words(kv.first.w, (int)em->kw, kDefaultSeed));
   }
 }
 
@@ -642,7 +643,7 @@ int bg_em_build_part(bg_em *em, int part, void *host_dst) {
     keys.insert(keys.end(), kv.first.w, kv.first.w + em->kw);
     vals.push_back((uint8_t)kv.second);
     vals.push_back((uint8_t)(kv.second >> 8));
-    seeds.push_back(kDefaultSeed);
+    seeds.push_back(h);
   }
   if (!build_partition(L, (uint32_t)part, seeds.size(), keys.data(),
                        vals.data(), seeds.data(),
@@ -815,17 +816,38 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
       seeds.push_back(tuple_seed(kDefaultSeed, (uint32_t)t));
     }
   }
+  const size_t nkeys = seeds.size();
+  std::vector<uint64_t> hashes(nkeys);
+  for (size_t i = 0; i < nkeys; i++)
+    hashes[i] = hash_words(&keys[i * wm->kw], (int)wm->kw, seeds[i]);
   TableLayout L;
-  int r = build_image(wm->kw, 8, 1, keys, vals, seeds, &img, &L);
+  int r = build_image(wm->kw, 8, 1, keys, vals, hashes, &img, &L);
   if (r) return r;
+  // Past the whole-table LDS size, a table whose tag words fit LDS (at a
+  // higher load factor if need be: the bucketized 2x4 cuckoo table inserts
+  // well past 0.9) keeps them there (bg_wm.hip) and needs no key filter.
+  bool tags_lds = false;
+  const char *etg = getenv("BG_WM_TAGS");  // A/B knob (variants.py)
+  if (img.size() > kLdsTableMax && !(etg && *etg && atoi(etg) == 0)) {
+    for (double load : {0.75, 0.93}) {
+      std::vector<uint8_t> img2;
+      TableLayout L2;
+      if (build_image(wm->kw, 8, 1, keys, vals, hashes, &img2, &L2, load) == 0 &&
+          (uint64_t)L2.nbp * 4 <= kTagsLdsMax) {
+        img.swap(img2);
+        L = L2;
+        tags_lds = true;
+        break;
+      }
+    }
+  }
   // Tables too big for LDS get a blocked Bloom filter (up to 16 bits per
   // key, 64 KB by default so two workgroups fit a CU -- measured faster
   // than 128 KB at one workgroup per CU) that the kernel stages in LDS.
   uint32_t fw = 0;
-  const size_t nkeys = seeds.size();
   const char *ekb = getenv("BG_WM_FILTER_KB");  // A/B knob (variants.py)
   const int kb = (ekb && *ekb) ? atoi(ekb) : 64;
-  if (img.size() > kLdsTableMax && kb > 0 && nkeys > 0) {
+  if (img.size() > kLdsTableMax && !tags_lds && kb > 0 && nkeys > 0) {
     const uint32_t cap = std::min<uint32_t>(kFilterMaxWords, (uint32_t)kb * 256);
     fw = 1024;
     while (fw < cap && (uint64_t)fw * 32 < (uint64_t)nkeys * 16) fw *= 2;
@@ -846,6 +868,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   if (r) return r;
   wm->dev.filt_off = foff;
   wm->dev.filt_words = fw;
+  wm->dev.tags_lds = tags_lds;
   wm->dirty = false;
   return 0;
 }

@@ -52,8 +52,8 @@ void relayout(TableLayout &L, uint32_t nbp);
 int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
                 const std::vector<uint64_t> &keys,
                 const std::vector<uint8_t> &vals,
-                const std::vector<uint64_t> &seeds, std::vector<uint8_t> *img,
-                TableLayout *out_layout);
+                const std::vector<uint64_t> &hashes, std::vector<uint8_t> *img,
+                TableLayout *out_layout, double max_load = 0.75);
 
 struct DevTable {
   int device = -1;
@@ -64,6 +64,7 @@ struct DevTable {
   bool valid = false;
   uint64_t filt_off = 0;    // key filter appended to the image (WM)
   uint32_t filt_words = 0;
+  bool tags_lds = false;    // tag words staged in LDS (WM, bg_wm.hip)
   int upload(int dev, const std::vector<uint8_t> &img, const TableLayout &lay,
              hipStream_t s);
   void release();

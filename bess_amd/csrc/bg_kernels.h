@@ -76,6 +76,8 @@ constexpr uint32_t kLdsNone = 0;    // table probed in L2 / MALL
 constexpr uint32_t kLdsTable = 1;   // whole image copied into LDS
 constexpr uint32_t kLdsFilter = 2;  // only the key filter copied into LDS
 constexpr uint32_t kFilterMaxWords = 32768;  // 128 KB of LDS
+constexpr uint32_t kLdsTags = 3;    // only the tag words in LDS (bg_wm.hip)
+constexpr uint64_t kTagsLdsMax = 131072;  // tag bytes staged by bg_wm.hip
 
 struct TableRef {
   const uint8_t *base;  // device image (nparts * part_bytes [+ filter])
@@ -182,6 +184,10 @@ hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
+// WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
+hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
+// all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword
+bool fits_nch2(const FieldPlan &fp);
 
 }  // namespace bg
 

@@ -27,19 +27,6 @@ constexpr int kEmBlock = 512;  // 8 waves; LDS tables <= 40 KB -> 4 blocks/CU
 constexpr int kCkBlock = 256;
 constexpr int kDefaultPpl = 1;
 
-__device__ __forceinline__ uint32_t compact_bytes(uint32_t m) {
-  // bits 7, 15, 23, 31 -> bits 0..3
-  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) |
-         ((m >> 28) & 8u);
-}
-
-// SWAR "which tag bytes equal `tag`": no false negatives; rare false
-// positives only cost an extra key compare.
-__device__ __forceinline__ uint32_t tag_match(uint32_t tags, uint32_t tag) {
-  uint32_t x = tags ^ (tag * 0x01010101u);
-  return compact_bytes((x - 0x01010101u) & ~x & 0x80808080u);
-}
-
 template <int KW>
 __device__ __forceinline__ bool key_eq(const uint8_t *slot_key,
                                        const uint64_t (&k)[KW]) {
@@ -192,9 +179,6 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
   return slot * 4 + ((q + (slot >> 2)) & 3);
 }
 
-__device__ __forceinline__ void lds_fence() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
 
 template <int KW, int NCH, int PF>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
@@ -341,22 +325,6 @@ __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
 // WildcardMatch: tuple-space search over <= 8 masks in one combined table;
 // the best (priority, later-tuple-on-tie) entry wins (LookupEntry 136-157).
 // ---------------------------------------------------------------------------
-// The WildcardMatch tuple masks (up to 64 words) would otherwise be hoisted
-// into scalar registers for the whole kernel and spilled; laundering the
-// kernarg pointer per packet makes them cheap scalar-cache loads instead.
-// (The WmArgs block is the kernel's only argument, so it starts at the
-// kernarg segment; taking the parameter's address instead would copy the
-// whole block to scratch.)
-typedef const uint64_t __attribute__((address_space(4))) *kconst_u64;
-__device__ __forceinline__ kconst_u64 tuple_masks(const WmArgs &) {
-  const __attribute__((address_space(4))) uint8_t *ka =
-      (const __attribute__((address_space(4))) uint8_t *)
-          __builtin_amdgcn_kernarg_segment_ptr();
-  kconst_u64 p = (kconst_u64)(ka + offsetof(WmArgs, tmask));
-  asm volatile("" : "+s"(p));
-  return p;
-}
-
 template <int KW>
 __device__ __forceinline__ void load_key(const uint8_t *p, uint64_t (&o)[KW]) {
   if constexpr (KW % 2 == 0) {
@@ -394,26 +362,29 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
                                                   const uint64_t (&k)[KW],
                                                   const uint32_t *filt) {
   const kconst_u64 tm = tuple_masks(a);
-  uint64_t hs[kMaxTuples];
+  uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples];
   uint32_t w1[kMaxTuples], w2[kMaxTuples];
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
-    hs[tu] = 0;
+    b1[tu] = b2[tu] = 0;
+    tg[tu] = 1;  // fingerprints are never 0, so empty (0) tag words never match
     w1[tu] = w2[tu] = 0;
     if (tu < (int)a.ntuples) {
       uint64_t km[KW];
 #pragma unroll
       for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
-      const uint64_t h = hash_words(km, KW, tuple_seed(a.t.seed, tu));
-      hs[tu] = h;
+      const uint32_t h1 = hash_words_h1(km, KW, tuple_seed(a.t.seed, tu));
       bool pass = true;
       if (FILT) {
-        const FilterProbe q = filter_probe(h, a.t.filt_words);
+        const FilterProbe q = filter_probe(h1, a.t.filt_words);
         pass = (filt[q.word] & q.bits) == q.bits;
       }
-      if (pass) {
-        const Probe p = split_hash(h, 1, a.t.nbp);
+      if (pass) {  // the second hash only for tuples the filter lets through
+        const Probe p = split_hash(hash_join(h1), 1, a.t.nbp);
+        b1[tu] = p.b1;
+        b2[tu] = p.b2;
+        tg[tu] = p.tag;
         w1[tu] = tags[p.b1];
         w2[tu] = tags[p.b2];
       }
@@ -425,8 +396,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
     if (tu < (int)a.ntuples) {
-      const Probe p = split_hash(hs[tu], 1, a.t.nbp);
-      uint32_t cand = tag_match(w1[tu], p.tag) | (tag_match(w2[tu], p.tag) << 4);
+      uint32_t cand = tag_match(w1[tu], tg[tu]) | (tag_match(w2[tu], tg[tu]) << 4);
       if (cand) {
         uint64_t km[KW];
 #pragma unroll
@@ -434,7 +404,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
         while (cand) {
           const int sl = __builtin_ctz(cand);
           cand &= cand - 1;
-          const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
+          const uint32_t slot = (sl < 4 ? b1[tu] : b2[tu]) * kSlots + (sl & 3);
           // value and key of the slot in one round trip
           const uint64_t v = vals[slot];
           uint64_t sk[KW];
@@ -1432,6 +1402,12 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
 }
 
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
+  if (a.t.lds == kLdsTags) {
+    if (!a.fp.direct && a.fp.nch <= 4) return launch_wm_tags(a, num_cus, s);
+    WmArgs b = a;  // fields too far apart for a window: probe in L2
+    b.t.lds = kLdsNone;
+    return dispatch<WmSel>(b, num_cus, s, 1);
+  }
   if (env_int("BG_WM_BLOCK", 512) == 1024 && a.t.kw == 2 && fits_nch2(a.fp)) {
     if (env_int("BG_PPL", 1) == 2)
       return launch_classify(wm_classify_k1024_kernel<2>, a, num_cus, s, 2, 1024);

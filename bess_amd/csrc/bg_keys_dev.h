@@ -14,6 +14,46 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ uint32_t compact_bytes(uint32_t m) {
+  // bits 7, 15, 23, 31 -> bits 0..3
+  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) |
+         ((m >> 28) & 8u);
+}
+
+// bit 7 of every byte of x that is zero -- exact (the carry-free form: no
+// borrow crosses a byte), so an empty slot (fingerprint 0) never matches a
+// fingerprint, which is never 0
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+  const uint32_t y = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(y | x | 0x7F7F7F7Fu);
+}
+
+// SWAR "which tag bytes equal `tag`" -> bits 0..3
+__device__ __forceinline__ uint32_t tag_match(uint32_t tags, uint32_t tag) {
+  return compact_bytes(zero_bytes(tags ^ (tag * 0x01010101u)));
+}
+
+// The WildcardMatch tuple masks (up to 64 words) would otherwise be hoisted
+// into scalar registers for the whole kernel and spilled; laundering the
+// kernarg pointer per packet makes them cheap scalar-cache loads instead.
+// (The WmArgs block is the kernel's only argument, so it starts at the
+// kernarg segment; taking the parameter's address instead would copy the
+// whole block to scratch.)
+typedef const uint64_t __attribute__((address_space(4))) *kconst_u64;
+__device__ __forceinline__ kconst_u64 tuple_masks(const WmArgs &) {
+  const __attribute__((address_space(4))) uint8_t *ka =
+      (const __attribute__((address_space(4))) uint8_t *)
+          __builtin_amdgcn_kernarg_segment_ptr();
+  kconst_u64 p = (kconst_u64)(ka + offsetof(WmArgs, tmask));
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+__device__ __forceinline__ void lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+
 // streaming (read-once) 16-byte load: nontemporal so packet bytes do not
 // evict the flow table from L2
 __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {

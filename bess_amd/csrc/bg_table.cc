@@ -43,14 +43,13 @@ struct Xorshift {
 
 bool build_partition(const TableLayout &L, uint32_t part, size_t n,
                      const uint64_t *keys, const uint8_t *vals,
-                     const uint64_t *seeds, uint8_t *dst) {
+                     const uint64_t *hashes, uint8_t *dst) {
   const uint32_t nslots = L.nbp * kSlots;
   if (n > nslots) return false;
   std::vector<int32_t> occ(nslots, -1);
   std::vector<Probe> pr(n);
   for (size_t i = 0; i < n; i++) {
-    uint64_t h = hash_words(keys + i * L.kw, (int)L.kw, seeds[i]);
-    pr[i] = split_hash(h, L.nparts, L.nbp);
+    pr[i] = split_hash(hashes[i], L.nparts, L.nbp);
     if (pr[i].part != part) return false;  // caller filtered wrongly
   }
   Xorshift rng{(L.seed ^ (0x9E3779B97F4A7C15ULL * (part + 1))) | 1};

@@ -48,24 +48,42 @@ struct TableLayout {
 
 BG_HD uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
-// Full 64-bit hash of a key: one multiply-xorshift round per word plus a
-// splitmix64 finalizer (cheap on gfx950: 32-bit MULs, no CRC instruction).
-BG_HD uint64_t mix64(uint64_t x) {
-  x ^= x >> 30;
-  x *= 0xbf58476d1ce4e5b9ULL;
-  x ^= x >> 27;
-  x *= 0x94d049bb133111ebULL;
-  x ^= x >> 31;
-  return x;
+// Key hash, all 32-bit arithmetic (gfx950 has no 64-bit multiply: a
+// 64 x 64 product is four 32-bit multiplies plus adds, and a multiply is a
+// quarter-rate VALU op). h1 walks the key's u32 halves with one
+// multiply-xorshift step each -- a bijection of the state for a fixed
+// input word and of the input word for a fixed state, so two keys collide
+// only by a 2^-32 chance -- then the murmur3 finalizer. h1 alone gives the
+// first bucket, the fingerprint and the WildcardMatch filter probe; h2
+// (second bucket, partition) is one more finalizer over h1, so a lookup
+// that the filter rejects never computes it.
+BG_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
-BG_HD uint64_t hash_words(const uint64_t *k, int n, uint64_t seed) {
-  uint64_t h = seed ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(n + 1));
+BG_HD uint32_t hash_words_h1(const uint64_t *k, int n, uint64_t seed) {
+  uint32_t h = (uint32_t)seed ^ (uint32_t)(seed >> 32) ^ ((uint32_t)n * 0x9E3779B9u);
   for (int i = 0; i < n; i++) {
-    h = (h ^ k[i]) * 0x9E3779B97F4A7C15ULL;
-    h ^= h >> 29;
+    h = (h ^ (uint32_t)k[i]) * 0x9E3779B1u;
+    h ^= h >> 15;
+    h = (h ^ (uint32_t)(k[i] >> 32)) * 0x85EBCA77u;
+    h ^= h >> 13;
   }
-  return mix64(h);
+  return fmix32(h);
+}
+
+BG_HD uint32_t hash_h2(uint32_t h1) { return fmix32(h1 ^ 0x5BD1E995u); }
+
+// the full hash: h2 << 32 | h1
+BG_HD uint64_t hash_join(uint32_t h1) { return (uint64_t)hash_h2(h1) << 32 | h1; }
+
+BG_HD uint64_t hash_words(const uint64_t *k, int n, uint64_t seed) {
+  return hash_join(hash_words_h1(k, n, seed));
 }
 
 // per-tuple seed for the combined WildcardMatch table
@@ -77,14 +95,17 @@ struct Probe {
   uint32_t part, b1, b2, tag;
 };
 
+// h1: first bucket (low bits) and fingerprint (top byte); h2: second
+// bucket (low bits) and partition (top 3 bits). Buckets per partition are
+// <= 2^24, so no two fields share a bit.
 BG_HD Probe split_hash(uint64_t h, uint32_t nparts, uint32_t nbp) {
   Probe p;
-  uint32_t m = nbp - 1;
-  p.part = (uint32_t)(h >> 48) & (nparts - 1);
-  p.b1 = (uint32_t)h & m;
-  p.b2 = (uint32_t)(h >> 24) & m;
+  const uint32_t m = nbp - 1, h1 = (uint32_t)h, h2 = (uint32_t)(h >> 32);
+  p.part = (h2 >> 29) & (nparts - 1);
+  p.b1 = h1 & m;
+  p.b2 = h2 & m;
   if (p.b2 == p.b1) p.b2 = (p.b1 ^ 1u) & m;
-  uint32_t t = (uint32_t)(h >> 56);
+  const uint32_t t = h1 >> 24;
   p.tag = t ? t : 1u;
   return p;
 }
@@ -97,10 +118,12 @@ struct FilterProbe {
   uint32_t word, bits;
 };
 
+// from h1 only (the low 32 bits of the hash)
 BG_HD FilterProbe filter_probe(uint64_t h, uint32_t nwords) {
   FilterProbe f;
-  f.word = (uint32_t)(h >> 40) & (nwords - 1);
-  f.bits = (1u << ((uint32_t)(h >> 8) & 31)) | (1u << ((uint32_t)(h >> 14) & 31));
+  const uint32_t h1 = (uint32_t)h;
+  f.word = (h1 >> 4) & (nwords - 1);
+  f.bits = (1u << ((h1 >> 20) & 31)) | (1u << ((h1 >> 25) & 31));
   return f;
 }
 
@@ -110,12 +133,13 @@ TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
 
 // Lay out the partition image of `part` at `dst` (layout.part_bytes bytes)
 // from the given entries (keys[i*kw .. ], vals[i*val_bytes ..]) that hash
-// into this partition (callers filter). `seeds[i]` is the hash seed of entry
-// i (tuple seeds for WildcardMatch). Returns false if cuckoo insertion failed
-// (caller retries with a bigger nbp).
+// into this partition (callers filter). `hashes[i]` is entry i's full hash
+// (hash_words with its seed -- tuple seeds for WildcardMatch). Returns
+// false if cuckoo
+// insertion failed (caller retries with a bigger nbp).
 bool build_partition(const TableLayout &L, uint32_t part, size_t n,
                      const uint64_t *keys, const uint8_t *vals,
-                     const uint64_t *seeds, uint8_t *dst);
+                     const uint64_t *hashes, uint8_t *dst);
 
 }  // namespace bg
 

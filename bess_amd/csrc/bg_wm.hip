@@ -1,0 +1,215 @@
+// bg_wm.hip -- WildcardMatch::ProcessBatch (core/modules/wildcard_match.cc:
+// 159-203, LookupEntry 136-157) for tables whose tag words fit in LDS.
+//
+// The combined tuple table (bg_table.h: one table, a seed per tuple) keeps
+// its tag words -- one u32 of four 8-bit fingerprints per bucket, <= 128 KB
+// -- in LDS, so the per-(packet, tuple) probe of both candidate buckets is
+// two LDS reads and a SWAR compare; nothing leaves the CU unless a
+// fingerprint matches. Lane = packet, 64 packets per wave tile:
+//
+//   1. header window -> raw key (WildcardMatch's unmasked 8-byte loads,
+//      P4), the next tile's window in flight;
+//   2. per tuple (wave-uniform): key & mask, hash, both tag words from
+//      LDS (all tuples' reads issued before any is used); every
+//      fingerprint match is appended to a per-wave LDS queue as
+//      (slot, lane, tuple) with a ballot + mbcnt prefix, so the key checks
+//      run on dense lanes instead of on whichever lanes happen to match;
+//   3. each full 64-entry batch of the queue (and the remainder at the end
+//      of the tile) is checked in one round trip: a lane loads the slot's
+//      key and value from L2, compares it with its packet's masked key
+//      (fetched from the owning lane with ds_bpermute) and folds a hit into
+//      the packet's best with a 64-bit LDS atomic max over
+//      (priority, tuple, gate) -- the highest priority wins and an equal
+//      priority goes to the later tuple, LookupEntry's '>=' (P5);
+//   4. gate = the best's gate, or the default gate when nothing matched.
+//
+// One 1024-thread workgroup per CU (tags <= 128 KB + 1 KB per wave).
+#include <hip/hip_runtime.h>
+#include <limits.h>
+
+#include "bg_kernels.h"
+#include "bg_keys_dev.h"
+
+namespace bg {
+namespace {
+
+constexpr int kWmBlock = 1024;
+constexpr int kWaves = kWmBlock / 64;
+constexpr uint32_t kQueue = 128;        // entries per wave (ring)
+constexpr uint32_t kWaveLds = 64 * 8 + kQueue * 4;  // best[64] + queue
+
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
+// Check queue entries [head, head + m), one per lane: slot | lane << 20 |
+// tuple << 26.
+template <int KW>
+__device__ __forceinline__ void wm_check(const WmArgs &a, const uint64_t *mlds,
+                                         uint64_t *best, const uint32_t *q,
+                                         uint32_t head, uint32_t m, int lane,
+                                         const uint64_t (&k)[KW]) {
+  const uint32_t e = q[(head + lane) & (kQueue - 1)];
+  const uint32_t slot = e & 0xFFFFFu, pl = (e >> 20) & 63u, tu = e >> 26;
+  // the owning lane's key (every lane takes part in the permutes)
+  uint64_t kk[KW];
+#pragma unroll
+  for (int j = 0; j < KW; j++) {
+    const uint32_t lo = shfl32((uint32_t)k[j], (int)pl);
+    const uint32_t hi = shfl32((uint32_t)(k[j] >> 32), (int)pl);
+    kk[j] = (uint64_t)hi << 32 | lo;
+  }
+  if ((uint32_t)lane < m) {
+    const uint8_t *tab = a.t.base;
+    const uint64_t v = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off)[slot];
+    const uint64_t *sk =
+        reinterpret_cast<const uint64_t *>(tab + a.t.keys_off) + (uint64_t)slot * KW;
+    bool hit = (uint32_t)(v >> 48) == tu;
+#pragma unroll
+    for (int j = 0; j < KW; j++) hit &= sk[j] == (kk[j] & mlds[tu * KW + j]);
+    if (hit) {
+      // (priority as unsigned order, valid bit, tuple, gate)
+      const uint64_t comb = ((uint64_t)((uint32_t)v ^ 0x80000000u) << 32) |
+                            (1u << 19) | (tu << 16) | ((uint32_t)(v >> 32) & 0xFFFFu);
+      atomicMax(reinterpret_cast<unsigned long long *>(best + pl),
+                (unsigned long long)comb);
+    }
+  }
+}
+
+template <int KW, int NCH>
+__global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
+  {  // stage the tag words
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.t.base);
+    uint4 *dst = reinterpret_cast<uint4 *>(lds);
+    for (uint32_t i = threadIdx.x; i < tag_bytes / 16; i += kWmBlock) dst[i] = src[i];
+  }
+  uint64_t *mlds = reinterpret_cast<uint64_t *>(lds + tag_bytes);
+  {
+    const kconst_u64 tm = tuple_masks(a);
+    if (threadIdx.x < kMaxTuples * KW)
+      mlds[threadIdx.x] = tm[(threadIdx.x / KW) * kMaxKeyWords + threadIdx.x % KW];
+  }
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + wid * kWaveLds;
+  uint64_t *best = reinterpret_cast<uint64_t *>(wl);
+  uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
+  best[lane] = 0;
+  __syncthreads();
+
+  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  uint32_t wn[NCH * 4 + 2];
+  if (t < ntiles && t * 64 + lane < a.n)
+    load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
+  for (; t < ntiles; t += nw) {
+    const uint64_t idx = t * 64 + lane;
+    const bool live = idx < a.n;
+    uint32_t w[NCH * 4 + 2];
+#pragma unroll
+    for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
+    const uint64_t nidx = (t + nw) * 64 + lane;
+    if (t + nw < ntiles && nidx < a.n)
+      load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
+    uint64_t k[KW];
+    extract_key<KW, NCH>(w, a.fp, k);
+    const kconst_u64 tm = tuple_masks(a);  // laundered per tile: no hoisting
+
+    // A. every tuple's hash and both tag words (16 LDS reads in flight)
+    uint32_t b1[kMaxTuples], b2[kMaxTuples], tw1[kMaxTuples], tw2[kMaxTuples],
+        tb[kMaxTuples];
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      b1[tu] = b2[tu] = tw1[tu] = tw2[tu] = tb[tu] = 0;
+      if (tu < (int)a.ntuples) {
+        uint64_t km[KW];
+#pragma unroll
+        for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
+        const Probe p = split_hash(
+            hash_join(hash_words_h1(km, KW, tuple_seed(a.t.seed, tu))), 1, a.t.nbp);
+        b1[tu] = p.b1;
+        b2[tu] = p.b2;
+        tb[tu] = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
+        tw1[tu] = tags[p.b1];
+        tw2[tu] = tags[p.b2];
+      }
+    }
+    // B. fingerprint matches -> queue; full batches checked on the way
+    uint32_t head = 0, qlen = 0;  // wave-uniform
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      if (tu < (int)a.ntuples) {
+        // bytes of the tag words equal to the fingerprint: bit 7 of each
+        uint32_t c1 = zero_bytes(tw1[tu] ^ tb[tu]);
+        uint32_t c2 = zero_bytes(tw2[tu] ^ tb[tu]);
+        if (!live) c1 = c2 = 0;
+        for (;;) {
+          const bool has = (c1 | c2) != 0;
+          const uint64_t bal = __ballot(has);
+          if (!bal) break;
+          if (has) {
+            uint32_t slot;
+            if (c1) {
+              slot = b1[tu] * kSlots + (__builtin_ctz(c1) >> 3);
+              c1 &= c1 - 1;
+            } else {
+              slot = b2[tu] * kSlots + (__builtin_ctz(c2) >> 3);
+              c2 &= c2 - 1;
+            }
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+            q[(head + qlen + rank) & (kQueue - 1)] =
+                slot | ((uint32_t)lane << 20) | ((uint32_t)tu << 26);
+          }
+          qlen += (uint32_t)__popcll(bal);
+          if (qlen >= 64) {
+            lds_fence();
+            wm_check<KW>(a, mlds, best, q, head, 64, lane, k);
+            head += 64;
+            qlen -= 64;
+          }
+        }
+      }
+    }
+    if (qlen) {
+      lds_fence();
+      wm_check<KW>(a, mlds, best, q, head, qlen, lane, k);
+    }
+    lds_fence();
+    const uint64_t b = best[lane];
+    best[lane] = 0;
+    if (live) a.gates[idx] = b ? (uint16_t)b : (uint16_t)a.default_gate;
+  }
+}
+
+template <int KW, int NCH>
+hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
+  const size_t lds = ((a.t.nbp * 4 + 15) & ~(size_t)15) + kMaxTuples * KW * 8 +
+                     (size_t)kWaves * kWaveLds;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
+  if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((wm_tags_kernel<KW, NCH>), dim3((unsigned)blocks),
+                     dim3(kWmBlock), lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
+  const bool n2 = fits_nch2(a.fp);
+  if (a.fp.direct || a.fp.nch > 4) return hipErrorInvalidValue;
+#define BG_WT(KW)                                                          \
+  if (a.t.kw == KW)                                                        \
+    return n2 ? launch_tags<KW, 2>(a, num_cus, s) : launch_tags<KW, 4>(a, num_cus, s);
+  BG_WT(1) BG_WT(2) BG_WT(4) BG_WT(8)
+#undef BG_WT
+  return hipErrorInvalidValue;
+}
+
+}  // namespace bg

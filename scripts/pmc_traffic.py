@@ -20,7 +20,7 @@ from collections import defaultdict
 
 # bench workload -> substring of its timed kernel's name
 KERNELS = {"em": "em_slab_kernel", "cksum": "cksum_kernel",
-           "wm": "wm_classify_kernel", "c5": "em_slab_kernel",
+           "wm": "wm_tags_kernel", "c5": "em_slab_kernel",
            "hashlb": "HlbOp<2>", "acl": "AclOp", "iplookup": "LpmOp",
            "ttl": "TtlOp<4>", "nat": "NatOp"}
 # algorithmic bytes per launch of each bench workload

@@ -244,9 +244,14 @@ def test_wm_module_kat(golden, dev):
         assert list(d_g.cpu().numpy().view(np.uint16)) == case["expect"]
 
 
-@pytest.mark.parametrize("n_rules,n_pkts", [(64, 4096), (5000, 65536),
-                                            (100000, 131072)])
-def test_wm_vs_oracle(n_rules, n_pkts, dev):
+@pytest.mark.parametrize("n_rules,n_pkts,tags", [
+    (64, 4096, 1), (5000, 65536, 1), (5000, 65536, 0), (100000, 131072, 1),
+    (100000, 131072, 0), (300000, 65536, 1)])
+def test_wm_vs_oracle(n_rules, n_pkts, tags, dev, monkeypatch):
+    """tags 1: tables past the whole-table LDS size keep their tag words in
+    LDS (bg_wm.hip) when they fit; 0 (BG_WM_TAGS=0): the key-filter path;
+    300 K rules: tags too big for LDS, the key-filter path either way"""
+    monkeypatch.setenv("BG_WM_TAGS", str(tags))
     rk, rm, prio, gates, frames, _ = P.wm_workload(n_rules, n_pkts,
                                                   seed=n_rules, stride=64,
                                                   sizes=((60, 1),))
@@ -264,12 +269,18 @@ def test_wm_vs_oracle(n_rules, n_pkts, dev):
     assert (want != 77).mean() > 0.3
 
 
-def test_wm_priority_ties(dev):
+@pytest.mark.parametrize("filler", [0, 5000])
+def test_wm_priority_ties(dev, filler):
+    """filler: extra rules in the third tuple make the table too big for
+    LDS, so the tag-words-in-LDS kernel (bg_wm.hip) resolves the ties"""
     f = [(0, 1), (1, 1)]
     t = F.WmTable(f)
     t.add(b"\x01\x00", b"\xff\x00", 5, 1)
     t.add(b"\x00\x02", b"\x00\xff", 5, 2)   # later tuple, same prio: wins
     t.add(b"\x01\x02", b"\xff\xff", 4, 3)   # lower prio: loses
+    rng = np.random.default_rng(7)
+    for v in rng.choice(np.arange(0x2000, 0xFF00), filler, replace=False):
+        t.add(int(v).to_bytes(2, "little"), b"\xff\xff", 9, 4)
     frames = np.zeros((4, 64), np.uint8)
     frames[0, :2] = [1, 2]
     frames[1, :2] = [1, 9]
