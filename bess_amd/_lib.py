@@ -82,6 +82,9 @@ _SIGS = {
     "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
     "bg_module_set_device": (_int, [_vp, _int]),
     "bg_module_set_igate": (_int, [_vp, _u16]),
+    "bg_module_bind_meta": (_int, [_vp, _int, _vp, _vp, _int]),
+    "bg_em_bind_meta": (_int, [_vp, _int, _vp, _int]),
+    "bg_wm_bind_meta": (_int, [_vp, _int, _vp, _int]),
     "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
     "bg_debug_key": (_int, [C.POINTER(bg_field), _int, _int, _vp, _vp]),
     "bg_em_classify_window": (_int, [_vp, _vp, _sz, _sz, _int, _u16, _vp, _vp]),

@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -46,12 +47,18 @@ int num_cus(int device) {
 }
 
 int set_device(int device) {
-  // launch path: one cached count and a thread-local current-device check
-  static const int n = [] {
+  // launch path: one cached count (once positive) and a current-device check
+  static std::atomic<int> cached{0};
+  int n = cached.load(std::memory_order_relaxed);
+  if (n <= 0) {
     int c = 0;
-    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
-  }();
-  if (n <= 0) return fail(ENODEV, "no HIP device available");
+    const hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess || c <= 0)
+      return fail(ENODEV, "no HIP device available (hipGetDeviceCount: %s, %d)",
+                  hipGetErrorString(e), c);
+    cached.store(c, std::memory_order_relaxed);
+    n = c;
+  }
   if (device < 0 || device >= n)
     return fail(ENODEV, "device %d out of range [0,%d)", device, n);
   int cur = -1;
@@ -334,7 +341,11 @@ using namespace bg;
 // ============================================================================
 struct bg_em {
   std::vector<bg_field> fields;
-  bool has_attr = false;  // metadata-attribute fields: control plane only
+  bool has_attr = false;  // metadata-attribute fields (P15)
+  // fields as the device reads them: attr fields resolved to slot offsets
+  // by bg_em_bind_meta (meta_bound), otherwise = fields
+  std::vector<bg_field> dfields;
+  bool meta_bound = false;
   uint32_t key_size = 0;  // total_key_size_
   uint32_t kw = 1;        // device key words (1, 2, 4, 8)
   std::unordered_map<Key, uint16_t, KeyHash> rules;
@@ -411,6 +422,7 @@ int bg_em_create(const bg_field *fields, int nfields, bg_em **out) {
   if (r) return r;
   bg_em *em = new bg_em();
   em->fields.assign(fields, fields + nfields);
+  em->dfields = em->fields;
   for (int i = 0; i < nfields; i++) em->has_attr |= fields[i].attr_id >= 0;
   int acc = 0;
   for (int i = 0; i < nfields; i++) acc += fields[i].size;
@@ -510,15 +522,50 @@ static int em_launch(bg_em *em, const void *d_frames, size_t stride, size_t n,
   a.n = n;
   a.gates = d_gates;
   a.default_gate = default_gate;
-  a.fp = make_plan(em->fields, true, shift);
+  a.fp = make_plan(em->dfields, true, shift);
   a.t = em->dev.ref();
   HIP_TRY(launch_em(a, num_cus(em->dev.device), s));
   return 0;
 }
 
 static int no_attr_datapath() {
-  return fail(ENOTSUP, "metadata-attribute (attr_name) fields are not on the "
-              "device datapath");
+  return fail(ENOTSUP, "metadata-attribute (attr_name) fields need the "
+              "packets' metadata in the slot: bind its layout first "
+              "(bg_em_bind_meta / bg_wm_bind_meta); host staging does not "
+              "carry metadata");
+}
+
+// P15: attr fields read the packet's metadata area at the attribute's
+// metadata offset (exact_match.cc:230-236 ptr_attr; wildcard_match.cc:
+// 177-195 mt_offset_to_databuf_offset). The device slot carries the
+// metadata area at meta_off, so an attr field becomes an offset field at
+// meta_off + attr_offsets[attr_id].
+static int bind_meta(const std::vector<bg_field> &fields, int meta_off,
+                     const int32_t *attr_offsets, int nattrs,
+                     std::vector<bg_field> *out) {
+  if (meta_off < 0 || meta_off > 2048)
+    return fail(EINVAL, "meta_off %d not in [0,2048]", meta_off);
+  std::vector<bg_field> d = fields;
+  for (auto &f : d) {
+    if (f.attr_id < 0) continue;
+    if (f.attr_id >= nattrs || !attr_offsets || attr_offsets[f.attr_id] < 0)
+      return fail(EINVAL, "attribute %d has no metadata offset", f.attr_id);
+    f.offset = meta_off + attr_offsets[f.attr_id];
+    f.attr_id = -1;
+    if (f.offset + 8 > 2048)  // raw 8-byte loads stay inside 2 KB
+      return fail(EINVAL, "metadata field at slot offset %d: past 2040", f.offset);
+  }
+  out->swap(d);
+  return 0;
+}
+
+int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
+                    int nattrs) {
+  std::lock_guard<std::mutex> lk(em->mu);
+  int r = bind_meta(em->fields, meta_off, attr_offsets, nattrs, &em->dfields);
+  if (r) return r;
+  em->meta_bound = true;
+  return 0;
 }
 
 int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
@@ -531,7 +578,7 @@ int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
 int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,
                           uint16_t *d_gates, bg_stream_t stream) {
-  if (em->has_attr) return no_attr_datapath();
+  if (em->has_attr && !em->meta_bound) return no_attr_datapath();
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
@@ -687,6 +734,8 @@ struct WmTupleH {
 struct bg_wm {
   std::vector<bg_field> fields;
   bool has_attr = false;
+  std::vector<bg_field> dfields;  // as in bg_em
+  bool meta_bound = false;
   uint32_t key_size = 0;
   uint32_t kw = 1;
   std::vector<WmTupleH> tuples;
@@ -724,6 +773,7 @@ int bg_wm_create(const bg_field *fields, int nfields, bg_wm **out) {
   if (r) return r;
   bg_wm *wm = new bg_wm();
   wm->fields.assign(fields, fields + nfields);
+  wm->dfields = wm->fields;
   for (int i = 0; i < nfields; i++) wm->has_attr |= fields[i].attr_id >= 0;
   wm->key_size = (uint32_t)((acc + 7) / 8 * 8);
   wm->kw = round_kw(wm->key_size);
@@ -889,11 +939,20 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
   a.gates = d_gates;
   a.default_gate = default_gate;
   a.ntuples = (uint32_t)wm->tuples.size();
-  a.fp = make_plan(wm->fields, false, shift);
+  a.fp = make_plan(wm->dfields, false, shift);
   a.t = wm->dev.ref();
   for (size_t t = 0; t < wm->tuples.size(); t++)
     for (uint32_t j = 0; j < wm->kw; j++) a.tmask[t][j] = wm->tuples[t].mask.w[j];
   HIP_TRY(launch_wm(a, num_cus(wm->dev.device), s));
+  return 0;
+}
+
+int bg_wm_bind_meta(bg_wm *wm, int meta_off, const int32_t *attr_offsets,
+                    int nattrs) {
+  std::lock_guard<std::mutex> lk(wm->mu);
+  int r = bind_meta(wm->fields, meta_off, attr_offsets, nattrs, &wm->dfields);
+  if (r) return r;
+  wm->meta_bound = true;
   return 0;
 }
 
@@ -907,7 +966,7 @@ int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
 int bg_wm_classify_window(bg_wm *wm, const void *d_frames, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,
                           uint16_t *d_gates, bg_stream_t stream) {
-  if (wm->has_attr) return no_attr_datapath();
+  if (wm->has_attr && !wm->meta_bound) return no_attr_datapath();
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");

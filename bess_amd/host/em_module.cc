@@ -129,8 +129,16 @@ class ExactMatch final : public Module {
     *writeback = false;
   }
 
+  // P15: attr fields read the metadata area the slot carries at meta_off
+  int BindMeta(int meta_off, const std::vector<std::string> &names,
+               const std::vector<int32_t> &offsets) override {
+    std::vector<int32_t> off = AttrOffsets(names, offsets);
+    return bg_em_bind_meta(table_, meta_off, off.data(), (int)off.size());
+  }
+
   int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n, int win_off,
                           uint16_t *d_ogates, void *stream) override {
+    if (!all_attrs().empty()) return -ENOTSUP;  // staged windows: no metadata
     int rc = bg_em_sync(table_, device_, stream);
     if (rc < 0) return rc;
     return bg_em_classify_window(table_, d_win, wstride, n, win_off,

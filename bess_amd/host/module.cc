@@ -146,6 +146,24 @@ int bg_module_set_igate(bg_module *h, uint16_t igate) {
   return 0;
 }
 
+int bg_module_bind_meta(bg_module *h, int meta_off, const char *const *names,
+                        const int32_t *offsets, int n) {
+  if (n < 0 || (n > 0 && (!names || !offsets))) return fail(EINVAL, "bad arguments");
+  std::vector<std::string> nm;
+  std::vector<int32_t> off;
+  for (int i = 0; i < n; i++) {
+    nm.emplace_back(names[i] ? names[i] : "");
+    off.push_back(offsets[i]);
+  }
+  std::lock_guard<std::mutex> lk(h->mu);
+  bg::g_err.clear();
+  int r = h->m->BindMeta(meta_off, nm, off);
+  if (r == -ENOTSUP && bg::g_err.empty())
+    return fail(ENOTSUP, "'%s' has no metadata fields on its datapath",
+                h->mclass.c_str());
+  return r;
+}
+
 int bg_module_desc(const bg_module *h, char *buf, size_t len) {
   std::string d = h->m->GetDesc();
   if (buf && len) {

@@ -161,6 +161,26 @@ class Module {
     if (win_off != 0) return -EINVAL;
     return ProcessDevice(d_win, wstride, n, d_ogates, stream);
   }
+  // attr_name fields: metadata area at slot offset meta_off, attribute
+  // offsets by name (bg_module_bind_meta). Modules without attr fields on
+  // their datapath: ENOTSUP.
+  virtual int BindMeta(int meta_off, const std::vector<std::string> &names,
+                       const std::vector<int32_t> &offsets) {
+    (void)meta_off;
+    (void)names;
+    (void)offsets;
+    return -ENOTSUP;
+  }
+  // offsets of this module's attributes (by id) from a name -> offset list;
+  // -1 for names not given
+  std::vector<int32_t> AttrOffsets(const std::vector<std::string> &names,
+                                   const std::vector<int32_t> &offsets) const {
+    std::vector<int32_t> r(attrs_.size(), -1);
+    for (size_t i = 0; i < attrs_.size(); i++)
+      for (size_t j = 0; j < names.size(); j++)
+        if (names[j] == attrs_[i].name) r[i] = offsets[j];
+    return r;
+  }
   void set_device(int d) { device_ = d; }
   int device() const { return device_; }
   // ctx->current_igate of the calls that follow (core/module.h:59-75)

@@ -97,6 +97,16 @@ class Module:
     def set_device(self, device):
         lib().bg_module_set_device(self.h, device)
 
+    def bind_meta(self, meta_off, attr_offsets):
+        """attr_name fields (ExactMatch, WildcardMatch): each slot carries
+        the packet's metadata area at byte meta_off; attr_offsets maps an
+        attribute name to the metadata offset the pipeline assigned it
+        (Module::attr_offset, core/module.h)."""
+        names = list(attr_offsets)
+        arr = (C.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        offs = (C.c_int32 * max(len(names), 1))(*[int(attr_offsets[n]) for n in names])
+        _check(lib().bg_module_bind_meta(self.h, meta_off, arr, offs, len(names)))
+
     def set_igate(self, igate):
         """the input gate the following process calls arrive on
         (ctx->current_igate, core/module.h:59-75)"""

@@ -88,6 +88,17 @@ int bg_em_iter(const bg_em *em, size_t *cursor, uint8_t *key_out,
                uint16_t *gate_out);
 /* Rebuild/upload the device table if rules changed (control path). */
 int bg_em_sync(bg_em *em, int device, bg_stream_t stream);
+/* attr_name fields (exact_match.cc:230-236 reads
+ * ptr_attr(this, attr_id, pkt) = the packet's metadata area + the
+ * attribute's offset that bessd's metadata allocator assigned,
+ * core/module.h:679-684). On the device each slot carries that metadata
+ * area at byte meta_off; attr_offsets[attr_id] is attr_offset(attr_id)
+ * (nattrs entries, < 0: none -> EINVAL, where the reference would
+ * dereference a null attribute pointer). Until bound, classify returns
+ * ENOTSUP for tables with attr fields; host staging paths never carry
+ * metadata and keep returning ENOTSUP. */
+int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
+                    int nattrs);
 /* Device-resident classify: d_gates[i] = gate for frame i (default_gate on
  * a miss). Calls bg_em_sync implicitly when needed (not capturable then). */
 int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
@@ -133,6 +144,10 @@ size_t bg_wm_tuple_count(const bg_wm *wm, int t);
 int bg_wm_iter(const bg_wm *wm, int t, size_t *cursor, uint8_t *key_out,
                int32_t *priority, uint16_t *gate);
 int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream);
+/* as bg_em_bind_meta (wildcard_match.cc:177-195: buffer +
+ * mt_offset_to_databuf_offset(attr_offset(attr_id)), packet.h:189-191) */
+int bg_wm_bind_meta(bg_wm *wm, int meta_off, const int32_t *attr_offsets,
+                    int nattrs);
 int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
                    uint16_t default_gate, uint16_t *d_gates, bg_stream_t stream);
 int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
@@ -277,6 +292,11 @@ int bg_module_set_device(bg_module *m, int device);
 /* the input gate the next process calls arrive on (ctx->current_igate:
  * ACL emits on it, StaticNAT picks its direction by it); default 0 */
 int bg_module_set_igate(bg_module *m, uint16_t igate);
+/* Metadata layout for attr_name fields (ExactMatch, WildcardMatch): the
+ * slot offset of each packet's metadata area and, by attribute name, the
+ * offsets the pipeline assigned (Module::attr_offset, core/module.h). */
+int bg_module_bind_meta(bg_module *m, int meta_off, const char *const *names,
+                        const int32_t *offsets, int n);
 /* GetDesc() (exact_match.cc:246-249, wildcard_match.cc:205-213) */
 int bg_module_desc(const bg_module *m, char *buf, size_t len);
 

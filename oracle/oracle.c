@@ -533,9 +533,22 @@ void or_em_make_key(const or_em *em, const uint8_t *head, uint64_t key[8]) {
   }
 }
 
-/* MakeKeys 239-263 + ExactMatch::ProcessBatch 224-244 + Find 273-278 */
-void or_em_process_batch(const or_em *em, const uint8_t *const *heads, int cnt,
-                         uint16_t default_gate, uint16_t *gates) {
+/* An attr_name field reads its metadata attribute: ExactMatch::ProcessBatch's
+ * buffer_fn (exact_match.cc:230-236) returns ptr_attr(this, attr_id, pkt) =
+ * the packet's metadata + attr_offset(attr_id) (module.h:679-684). The
+ * offset is whatever the pipeline's metadata allocator assigned; it is
+ * bound here. */
+void or_em_bind_attr(or_em *em, int idx, int mt_offset) {
+  em->fields[idx].attr_id = 0;
+  em->fields[idx].offset = mt_offset;
+}
+
+/* MakeKeys 239-263 + ExactMatch::ProcessBatch 224-244 + Find 273-278;
+ * metas[j]: packet j's metadata area (attr fields), may be NULL without
+ * attr fields */
+static void em_process_batch_meta(const or_em *em, const uint8_t *const *heads,
+                                  const uint8_t *const *metas, int cnt,
+                                  uint16_t default_gate, uint16_t *gates) {
   uint64_t keys[OR_MAX_BURST][8];
   if (em->total_key_size == 0) {
     /* no fields: the reference indexes u64_arr[(0-1)/8] (UB); with no
@@ -549,8 +562,9 @@ void or_em_process_batch(const or_em *em, const uint8_t *const *heads, int cnt,
     uint64_t mask = em->fields[f].mask;
     int pos = em->fields[f].pos;
     int off = em->fields[f].offset;
+    const int attr = em->fields[f].attr_id >= 0;
     for (int j = 0; j < cnt; j++) {
-      uint64_t v = ld64(heads[j] + off) & mask;
+      uint64_t v = ld64((attr ? metas[j] : heads[j]) + off) & mask;
       memcpy((uint8_t *)keys[j] + pos, &v, 8);
     }
   }
@@ -566,14 +580,30 @@ void or_em_process_batch(const or_em *em, const uint8_t *const *heads, int cnt,
   }
 }
 
-void or_em_process(const or_em *em, const uint8_t *base, size_t stride,
-                   size_t n, uint16_t default_gate, uint16_t *gates) {
-  const uint8_t *heads[OR_MAX_BURST];
+void or_em_process_batch(const or_em *em, const uint8_t *const *heads, int cnt,
+                         uint16_t default_gate, uint16_t *gates) {
+  em_process_batch_meta(em, heads, NULL, cnt, default_gate, gates);
+}
+
+/* n packets: frame i at base + i*stride, its metadata area at
+ * meta + i*meta_stride (meta may be NULL without attr fields) */
+void or_em_process_meta(const or_em *em, const uint8_t *base, size_t stride,
+                        const uint8_t *meta, size_t meta_stride, size_t n,
+                        uint16_t default_gate, uint16_t *gates) {
+  const uint8_t *heads[OR_MAX_BURST], *metas[OR_MAX_BURST];
   for (size_t i = 0; i < n; i += OR_MAX_BURST) {
     int cnt = (int)((n - i) < OR_MAX_BURST ? (n - i) : OR_MAX_BURST);
-    for (int j = 0; j < cnt; j++) heads[j] = base + (i + (size_t)j) * stride;
-    or_em_process_batch(em, heads, cnt, default_gate, gates + i);
+    for (int j = 0; j < cnt; j++) {
+      heads[j] = base + (i + (size_t)j) * stride;
+      metas[j] = meta ? meta + (i + (size_t)j) * meta_stride : NULL;
+    }
+    em_process_batch_meta(em, heads, metas, cnt, default_gate, gates + i);
   }
+}
+
+void or_em_process(const or_em *em, const uint8_t *base, size_t stride,
+                   size_t n, uint16_t default_gate, uint16_t *gates) {
+  or_em_process_meta(em, base, stride, NULL, 0, n, default_gate, gates);
 }
 
 /* ====================================================================== */
@@ -753,8 +783,16 @@ static uint16_t wm_lookup(const or_wm *wm, const uint64_t *key,
 }
 
 /* ProcessBatch 159-203 (offset fields: raw unmasked 8-byte loads) */
-void or_wm_process_batch(const or_wm *wm, const uint8_t *const *heads, int cnt,
-                         uint16_t default_gate, uint16_t *gates) {
+/* attr fields: ProcessBatch 177-195 reads buffer + mt_offset_to_databuf_
+ * offset(attr_offset(attr_id)) -- the metadata attribute (packet.h:189-191) */
+void or_wm_bind_attr(or_wm *wm, int idx, int mt_offset) {
+  wm->fields[idx].attr_id = 0;
+  wm->fields[idx].offset = mt_offset;
+}
+
+static void wm_process_batch_meta(const or_wm *wm, const uint8_t *const *heads,
+                                  const uint8_t *const *metas, int cnt,
+                                  uint16_t default_gate, uint16_t *gates) {
   uint64_t keys[OR_MAX_BURST][8];
   if (wm->total_key_size == 0) {
     for (int i = 0; i < cnt; i++) gates[i] = default_gate;
@@ -763,22 +801,37 @@ void or_wm_process_batch(const or_wm *wm, const uint8_t *const *heads, int cnt,
   memset(keys, 0, sizeof(keys));
   for (int f = 0; f < wm->nfields; f++) {
     int off = wm->fields[f].offset, pos = wm->fields[f].pos;
+    const int attr = wm->fields[f].attr_id >= 0;
     for (int j = 0; j < cnt; j++) {
-      uint64_t v = ld64(heads[j] + off);
+      uint64_t v = ld64((attr ? metas[j] : heads[j]) + off);
       memcpy((uint8_t *)keys[j] + pos, &v, 8);
     }
   }
   for (int i = 0; i < cnt; i++) gates[i] = wm_lookup(wm, keys[i], default_gate);
 }
 
-void or_wm_process(const or_wm *wm, const uint8_t *base, size_t stride,
-                   size_t n, uint16_t default_gate, uint16_t *gates) {
-  const uint8_t *heads[OR_MAX_BURST];
+void or_wm_process_batch(const or_wm *wm, const uint8_t *const *heads, int cnt,
+                         uint16_t default_gate, uint16_t *gates) {
+  wm_process_batch_meta(wm, heads, NULL, cnt, default_gate, gates);
+}
+
+void or_wm_process_meta(const or_wm *wm, const uint8_t *base, size_t stride,
+                        const uint8_t *meta, size_t meta_stride, size_t n,
+                        uint16_t default_gate, uint16_t *gates) {
+  const uint8_t *heads[OR_MAX_BURST], *metas[OR_MAX_BURST];
   for (size_t i = 0; i < n; i += OR_MAX_BURST) {
     int cnt = (int)((n - i) < OR_MAX_BURST ? (n - i) : OR_MAX_BURST);
-    for (int j = 0; j < cnt; j++) heads[j] = base + (i + (size_t)j) * stride;
-    or_wm_process_batch(wm, heads, cnt, default_gate, gates + i);
+    for (int j = 0; j < cnt; j++) {
+      heads[j] = base + (i + (size_t)j) * stride;
+      metas[j] = meta ? meta + (i + (size_t)j) * meta_stride : NULL;
+    }
+    wm_process_batch_meta(wm, heads, metas, cnt, default_gate, gates + i);
   }
+}
+
+void or_wm_process(const or_wm *wm, const uint8_t *base, size_t stride,
+                   size_t n, uint16_t default_gate, uint16_t *gates) {
+  or_wm_process_meta(wm, base, stride, NULL, 0, n, default_gate, gates);
 }
 
 /* ====================================================================== */

@@ -69,6 +69,10 @@ void or_em_make_key(const or_em *em, const uint8_t *head, uint64_t key[8]);
 /* the same over n packets at base + i*stride, in kMaxBurst batches */
 void or_em_process(const or_em *em, const uint8_t *base, size_t stride,
                    size_t n, uint16_t default_gate, uint16_t *gates);
+void or_em_bind_attr(or_em *em, int idx, int mt_offset);
+void or_em_process_meta(const or_em *em, const uint8_t *base, size_t stride,
+                        const uint8_t *meta, size_t meta_stride, size_t n,
+                        uint16_t default_gate, uint16_t *gates);
 
 /* ---- WildcardMatch ----------------------------------------------------- */
 typedef struct or_wm or_wm;
@@ -101,6 +105,10 @@ void or_wm_process_batch(const or_wm *wm, const uint8_t *const *heads, int cnt,
                          uint16_t default_gate, uint16_t *gates);
 void or_wm_process(const or_wm *wm, const uint8_t *base, size_t stride,
                    size_t n, uint16_t default_gate, uint16_t *gates);
+void or_wm_bind_attr(or_wm *wm, int idx, int mt_offset);
+void or_wm_process_meta(const or_wm *wm, const uint8_t *base, size_t stride,
+                        const uint8_t *meta, size_t meta_stride, size_t n,
+                        uint16_t default_gate, uint16_t *gates);
 
 /* ---- checksums (checksum.h) ------------------------------------------- */
 uint32_t or_calculate_sum(const void *buf, size_t len);           /* 52-181 */

@@ -65,6 +65,9 @@ def lib():
             "or_em_iter": (C.c_int, [C.c_void_p, C.POINTER(sz), C.c_void_p,
                                      C.POINTER(C.c_uint16)]),
             "or_em_process": (None, [C.c_void_p, u8p, sz, sz, C.c_uint16, u16p]),
+            "or_em_bind_attr": (None, [C.c_void_p, C.c_int, C.c_int]),
+            "or_em_process_meta": (None, [C.c_void_p, u8p, sz, u8p, sz, sz,
+                                          C.c_uint16, u16p]),
             "or_em_bench": (C.c_double, [C.c_void_p, u8p, sz, sz, C.c_uint16,
                                          u16p, C.c_int, C.c_int]),
             "or_wm_new": (C.c_void_p, []),
@@ -84,6 +87,9 @@ def lib():
                                      C.c_void_p, C.POINTER(C.c_int32),
                                      C.POINTER(C.c_uint16)]),
             "or_wm_process": (None, [C.c_void_p, u8p, sz, sz, C.c_uint16, u16p]),
+            "or_wm_bind_attr": (None, [C.c_void_p, C.c_int, C.c_int]),
+            "or_wm_process_meta": (None, [C.c_void_p, u8p, sz, u8p, sz, sz,
+                                          C.c_uint16, u16p]),
             "or_wm_bench": (C.c_double, [C.c_void_p, u8p, sz, sz, C.c_uint16,
                                          u16p, C.c_int, C.c_int]),
             "or_calculate_sum": (C.c_uint32, [C.c_void_p, sz]),
@@ -362,16 +368,25 @@ class OracleExactMatch:
         for r in rules:
             self.add(fields=r.get("fields", []), gate=r.get("gate", 0))
 
-    def process(self, frames, stride, n):
+    def process(self, frames, stride, n, meta_off=None, attr_offsets=None):
         """ExactMatch::ProcessBatch over n frames at frames + i*stride (32-
-        packet batches). frames: writable buffer; returns list of gates."""
+        packet batches). frames: writable buffer; returns list of gates.
+        attr_name fields read packet i's metadata area, taken to sit at
+        frames + i*stride + meta_off, at the attribute's metadata offset
+        attr_offsets[name] (what the pipeline's allocator assigned)."""
         import numpy as np
         gates = np.zeros(n, dtype=np.uint16)
-        if any(f["attr_name"] is not None for f in
-               (self.field(i) for i in range(self.num_fields()))):
-            raise OracleError(errno.ENOTSUP, "attr_name fields: no datapath")
-        lib().or_em_process(self.h, _ptr(frames), stride, n, self.default_gate,
-                            gates.ctypes.data)
+        fl = [self.field(i) for i in range(self.num_fields())]
+        meta = None
+        if any(f["attr_name"] is not None for f in fl):
+            if meta_off is None or attr_offsets is None:
+                raise OracleError(errno.ENOTSUP, "attr_name fields: no metadata")
+            for i, f in enumerate(fl):
+                if f["attr_name"] is not None:
+                    lib().or_em_bind_attr(self.h, i, attr_offsets[f["attr_name"]])
+            meta = _ptr(frames) + meta_off
+        lib().or_em_process_meta(self.h, _ptr(frames), stride, meta, stride, n,
+                                 self.default_gate, gates.ctypes.data)
         return gates
 
 
@@ -536,13 +551,21 @@ class OracleWildcardMatch:
             self.add(gate=r.get("gate", 0), priority=r.get("priority", 0),
                      values=r.get("values", []), masks=r.get("masks", []))
 
-    def process(self, frames, stride, n):
+    def process(self, frames, stride, n, meta_off=None, attr_offsets=None):
+        """WildcardMatch::ProcessBatch (wildcard_match.cc:159-203); attr_name
+        fields as in OracleExactMatch.process"""
         import numpy as np
+        meta = None
         if any(f["attr_name"] is not None for f in self.fields):
-            raise OracleError(errno.ENOTSUP, "attr_name fields: no datapath")
+            if meta_off is None or attr_offsets is None:
+                raise OracleError(errno.ENOTSUP, "attr_name fields: no metadata")
+            for i, f in enumerate(self.fields):
+                if f["attr_name"] is not None:
+                    lib().or_wm_bind_attr(self.h, i, attr_offsets[f["attr_name"]])
+            meta = _ptr(frames) + meta_off
         gates = np.zeros(n, dtype=np.uint16)
-        lib().or_wm_process(self.h, _ptr(frames), stride, n, self.default_gate,
-                            gates.ctypes.data)
+        lib().or_wm_process_meta(self.h, _ptr(frames), stride, meta, stride, n,
+                                 self.default_gate, gates.ctypes.data)
         return gates
 
 

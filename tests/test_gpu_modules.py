@@ -106,7 +106,7 @@ def test_em_module_random_traffic_vs_oracle():
     assert (want != 77).mean() > 0.2
 
 
-def test_attr_fields_have_no_device_datapath():
+def test_attr_fields_host_path_carries_no_metadata():
     m = ExactMatch(fields=[{"attr_name": "foo", "num_bytes": 2}])
     m.add(fields=[{"value_bin": b"\x01\x02"}], gate=1)
     with pytest.raises(ModuleError) as e:
