@@ -192,7 +192,8 @@ void relayout(TableLayout &L, uint32_t nbp) {
   L.nbp = nbp;
   L.keys_off = align256((uint64_t)nbp * 4);
   L.vals_off = align256(L.keys_off + (uint64_t)nbp * kSlots * L.kw * 8);
-  L.part_bytes = align256(L.vals_off + (uint64_t)nbp * kSlots * L.val_bytes);
+  L.part_bytes =
+      align256(L.vals_off + (L.vik ? 0 : (uint64_t)nbp * kSlots * L.val_bytes));
 }
 
 int DevTable::upload(int dev, const std::vector<uint8_t> &img,
@@ -245,6 +246,7 @@ TableRef DevTable::ref() const {
   const uint64_t tb = filt_words ? filt_off : bytes;
   t.bytes_total = (uint32_t)std::min<uint64_t>(tb, 0xFFFFFFFFu);
   t.filt_words = filt_words;
+  t.vik = L.vik;
   t.filt_off = filt_off;
   t.lds = tb <= kLdsTableMax ? kLdsTable
           : tags_lds       ? kLdsTags
@@ -258,16 +260,16 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
                 const std::vector<uint64_t> &keys,
                 const std::vector<uint8_t> &vals,
                 const std::vector<uint64_t> &hashes, std::vector<uint8_t> *img,
-                TableLayout *out_layout, double max_load) {
+                TableLayout *out_layout, double max_load, bool vik) {
   const size_t n = hashes.size();
   // count entries per partition to size the layout
   std::vector<std::vector<size_t>> members(nparts);
-  TableLayout L = plan_layout(0, kw, val_bytes, nparts, kDefaultSeed);
+  TableLayout L = plan_layout(0, kw, val_bytes, nparts, kDefaultSeed, 0.75, vik);
   for (size_t i = 0; i < n; i++)
     members[split_hash(hashes[i], nparts, 2).part].push_back(i);
   size_t maxc = 0;
   for (auto &m : members) maxc = std::max(maxc, m.size());
-  L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load);
+  L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load, vik);
   for (int attempt = 0; attempt < 8; attempt++) {
     img->assign((size_t)L.part_bytes * nparts, 0);
     bool ok = true;
@@ -347,6 +349,7 @@ struct bg_em {
   std::vector<bg_field> dfields;
   bool meta_bound = false;
   uint32_t key_size = 0;  // total_key_size_
+  uint32_t raw_size = 0;  // raw_key_size_ (sum of field sizes)
   uint32_t kw = 1;        // device key words (1, 2, 4, 8)
   std::unordered_map<Key, uint16_t, KeyHash> rules;
   bool dirty = true;
@@ -426,6 +429,7 @@ int bg_em_create(const bg_field *fields, int nfields, bg_em **out) {
   for (int i = 0; i < nfields; i++) em->has_attr |= fields[i].attr_id >= 0;
   int acc = 0;
   for (int i = 0; i < nfields; i++) acc += fields[i].size;
+  em->raw_size = (uint32_t)acc;
   em->key_size = (uint32_t)((acc + 7) / 8 * 8);
   em->kw = round_kw(em->key_size);
   *out = em;
@@ -493,13 +497,22 @@ static void em_entries(const bg_em *em, std::vector<uint64_t> *keys,
   }
 }
 
+// the gate fits in the key's unused top bytes (A/B knob BG_EM_VIK=0)
+static bool em_vik(const bg_em *em) {
+  static const bool on = [] {
+    const char *e = getenv("BG_EM_VIK");
+    return !(e && *e && atoi(e) == 0);
+  }();
+  return on && em->raw_size + 2 <= em->kw * 8;
+}
+
 static int em_sync_locked(bg_em *em, int device, hipStream_t s) {
   if (!em->dirty && em->dev.valid && em->dev.device == device) return 0;
   std::vector<uint64_t> keys, seeds;
   std::vector<uint8_t> vals, img;
   em_entries(em, &keys, &vals, &seeds);
   TableLayout L;
-  int r = build_image(em->kw, 2, 1, keys, vals, seeds, &img, &L);
+  int r = build_image(em->kw, 2, 1, keys, vals, seeds, &img, &L, 0.75, em_vik(em));
   if (r) return r;
   r = em->dev.upload(device, img, L, s);
   if (r) return r;
@@ -671,7 +684,8 @@ int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes) {
     cnt[split_hash(h, (uint32_t)nparts, 2).part]++;
   }
   size_t maxc = *std::max_element(cnt.begin(), cnt.end());
-  em->planned = plan_layout(maxc, em->kw, 2, (uint32_t)nparts, kDefaultSeed);
+  em->planned = plan_layout(maxc, em->kw, 2, (uint32_t)nparts, kDefaultSeed,
+                            0.75, em_vik(em));
   em->planned_valid = true;
   *part_bytes = em->planned.part_bytes;
   return 0;

@@ -85,6 +85,7 @@ struct TableRef {
   uint32_t nparts, nbp, kw, lds;  // lds: kLds* above
   uint32_t bytes_total;           // table bytes (LDS copy length)
   uint32_t filt_words;            // 0: no filter
+  uint32_t vik;                   // EM value in the key's top 2 bytes
   uint64_t filt_off;              // byte offset of the filter in the image
 };
 

@@ -49,6 +49,24 @@ __device__ __forceinline__ bool key_eq(const uint8_t *slot_key,
   }
 }
 
+template <int KW>
+__device__ __forceinline__ void load_key(const uint8_t *p, uint64_t (&o)[KW]) {
+  if constexpr (KW % 2 == 0) {
+    const uint4 *s = reinterpret_cast<const uint4 *>(p);
+#pragma unroll
+    for (int j = 0; j < KW / 2; j++) {
+      const uint4 v = s[j];
+      o[2 * j] = (uint64_t)v.y << 32 | v.x;
+      o[2 * j + 1] = (uint64_t)v.w << 32 | v.z;
+    }
+  } else {
+    const uint64_t *s = reinterpret_cast<const uint64_t *>(p);
+#pragma unroll
+    for (int j = 0; j < KW; j++) o[j] = s[j];
+  }
+}
+
+
 // Look one key up: the two tag words, then for each fingerprint match the
 // slot's key AND value, loaded together (one dependent round trip per
 // candidate instead of two). `tab` is either the global image or its LDS
@@ -64,6 +82,22 @@ __device__ __forceinline__ uint32_t em_lookup(const uint8_t *tab,
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(pb);
   uint32_t cand = tag_match(tags[p.b1], p.tag) |
                   (tag_match(tags[p.b2], p.tag) << 4);
+  if (t.vik) {  // the gate rides in the key's top two bytes: one read
+    while (cand) {
+      const int s = __builtin_ctz(cand);
+      cand &= cand - 1;
+      const uint32_t slot = (s < 4 ? p.b1 : p.b2) * kSlots + (s & 3);
+      uint64_t sk[KW];
+      load_key<KW>(pb + t.keys_off + (uint64_t)slot * KW * 8, sk);
+      const uint32_t v = (uint32_t)(sk[KW - 1] >> 48);
+      sk[KW - 1] &= 0x0000FFFFFFFFFFFFULL;
+      bool eq = true;
+#pragma unroll
+      for (int j = 0; j < KW; j++) eq &= sk[j] == k[j];
+      if (eq) return v;
+    }
+    return dflt;
+  }
   const uint16_t *vals = reinterpret_cast<const uint16_t *>(pb + t.vals_off);
   while (cand) {
     const int s = __builtin_ctz(cand);
@@ -325,23 +359,6 @@ __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
 // WildcardMatch: tuple-space search over <= 8 masks in one combined table;
 // the best (priority, later-tuple-on-tie) entry wins (LookupEntry 136-157).
 // ---------------------------------------------------------------------------
-template <int KW>
-__device__ __forceinline__ void load_key(const uint8_t *p, uint64_t (&o)[KW]) {
-  if constexpr (KW % 2 == 0) {
-    const uint4 *s = reinterpret_cast<const uint4 *>(p);
-#pragma unroll
-    for (int j = 0; j < KW / 2; j++) {
-      const uint4 v = s[j];
-      o[2 * j] = (uint64_t)v.y << 32 | v.x;
-      o[2 * j + 1] = (uint64_t)v.w << 32 | v.z;
-    }
-  } else {
-    const uint64_t *s = reinterpret_cast<const uint64_t *>(p);
-#pragma unroll
-    for (int j = 0; j < KW; j++) o[j] = s[j];
-  }
-}
-
 // WildcardMatch entry value: priority | gate << 32 | tuple << 48. A slot
 // matches tuple `tu` when its tuple field is tu and its key is k & mask.
 template <int KW>

@@ -13,8 +13,9 @@ namespace bg {
 
 TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
                         uint32_t val_bytes, uint32_t nparts, uint64_t seed,
-                        double max_load) {
+                        double max_load, bool vik) {
   TableLayout L;
+  L.vik = vik && val_bytes == 2 ? 1u : 0u;
   L.kw = kw;
   L.val_bytes = val_bytes;
   L.nparts = nparts;
@@ -25,7 +26,7 @@ TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
   L.nbp = nbp;
   L.keys_off = align256((uint64_t)nbp * 4);
   L.vals_off = align256(L.keys_off + (uint64_t)nbp * kSlots * kw * 8);
-  L.part_bytes = align256(L.vals_off + (uint64_t)nbp * kSlots * val_bytes);
+  L.part_bytes = align256(L.vals_off + (L.vik ? 0 : (uint64_t)nbp * kSlots * val_bytes));
   return L;
 }
 
@@ -95,8 +96,15 @@ bool build_partition(const TableLayout &L, uint32_t part, size_t n,
     uint32_t b = sl / kSlots, s = sl % kSlots;
     tags[b] |= pr[e].tag << (8 * s);
     memcpy(kslots + (uint64_t)sl * L.kw, keys + (uint64_t)e * L.kw, L.kw * 8);
-    memcpy(vslots + (uint64_t)sl * L.val_bytes, vals + (uint64_t)e * L.val_bytes,
-           L.val_bytes);
+    if (L.vik) {  // value in the key's last two bytes
+      uint16_t v;
+      memcpy(&v, vals + (uint64_t)e * 2, 2);
+      uint64_t &last = kslots[(uint64_t)sl * L.kw + L.kw - 1];
+      last = (last & 0x0000FFFFFFFFFFFFULL) | ((uint64_t)v << 48);
+    } else {
+      memcpy(vslots + (uint64_t)sl * L.val_bytes, vals + (uint64_t)e * L.val_bytes,
+             L.val_bytes);
+    }
   }
   return true;
 }

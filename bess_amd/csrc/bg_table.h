@@ -44,6 +44,10 @@ struct TableLayout {
   uint64_t keys_off;   // byte offset of keys within a partition
   uint64_t vals_off;   // byte offset of values within a partition
   uint64_t seed;       // hash seed
+  // 1: the u16 value sits in the top two bytes of the key's last word (the
+  // key has >= 2 bytes past its raw size, which are 0 in every packet key,
+  // P4), so one key read also yields the value; no value array
+  uint32_t vik;
 };
 
 BG_HD uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -129,7 +133,7 @@ BG_HD FilterProbe filter_probe(uint64_t h, uint32_t nwords) {
 
 TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
                         uint32_t val_bytes, uint32_t nparts, uint64_t seed,
-                        double max_load = 0.75);
+                        double max_load = 0.75, bool vik = false);
 
 // Lay out the partition image of `part` at `dst` (layout.part_bytes bytes)
 // from the given entries (keys[i*kw .. ], vals[i*val_bytes ..]) that hash

@@ -78,7 +78,8 @@ def _keys_off(img):
     for nbp in (2 ** k for k in range(1, 25)):
         ko = (nbp * 4 + 255) // 256 * 256
         vo = (ko + nbp * 4 * 2 * 8 + 255) // 256 * 256
-        pbytes = (vo + nbp * 4 * 2 + 255) // 256 * 256
-        if pbytes == n:
-            return nbp * 4
+        # value array, or none when the gate rides in the key (vik)
+        for pbytes in ((vo + nbp * 4 * 2 + 255) // 256 * 256, vo):
+            if pbytes == n:
+                return nbp * 4
     raise AssertionError("layout not found")
