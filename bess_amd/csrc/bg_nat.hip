@@ -28,21 +28,19 @@ __device__ __forceinline__ uint32_t upd_ck(uint32_t ck, uint32_t incr) {
   return ~s & 0xFFFFu;
 }
 
-// the u16 at even line byte offset `pos` (< 64) of d[], read / replaced
-__device__ __forceinline__ uint32_t get16(const uint32_t (&d)[16], uint32_t pos) {
-  uint32_t v = 0;
-#pragma unroll
-  for (int j = 0; j < 16; j++)
-    if ((pos >> 2) == (uint32_t)j) v = (d[j] >> ((pos & 2) * 8)) & 0xFFFFu;
-  return v;
+// The L4 checksum word sits at line byte l4 + 16 (TCP) or l4 + 6 (UDP),
+// l4 = 14 + 4 * IHL: inside the 64-byte line for TCP with IHL <= 8 (the
+// upper half of dword 7 + IHL) and UDP with IHL <= 10 (the lower half of
+// dword 5 + IHL). Per-lane positions differ, so the word is picked and put
+// back with constant-index selects over those dwords (a variable index into
+// d[] would put the line in scratch memory).
+constexpr int kL4Lo = 10, kL4Hi = 15;
+
+__device__ __forceinline__ bool l4_hi_at(int j, uint32_t ihl, bool tcp) {
+  return tcp && (uint32_t)j == 7u + ihl;
 }
-__device__ __forceinline__ void set16(uint32_t (&d)[16], uint32_t pos, uint32_t v) {
-#pragma unroll
-  for (int j = 0; j < 16; j++)
-    if ((pos >> 2) == (uint32_t)j) {
-      const uint32_t sh = (pos & 2) * 8;
-      d[j] = (d[j] & ~(0xFFFFu << sh)) | (v << sh);
-    }
+__device__ __forceinline__ bool l4_lo_at(int j, uint32_t ihl, bool udp) {
+  return udp && (uint32_t)j == 5u + ihl;
 }
 
 struct NatOp {
@@ -81,18 +79,30 @@ struct NatOp {
     d[6] = (d[6] & 0xFFFF0000u) | upd_ck(d[6] & 0xFFFFu, incr);
     const uint32_t ihl = (d[3] >> 16) & 0x0F, proto = d[5] >> 24;
     const uint32_t l4 = 14 + 4 * ihl;
-    if (proto == 6 || proto == 17) {
-      const uint32_t pos = l4 + (proto == 6 ? 16u : 6u);
-      uint32_t ck;
+    const bool tcp = proto == 6, udp = proto == 17;
+    if (tcp || udp) {
+      const uint32_t pos = l4 + (tcp ? 16u : 6u);
       const bool in_line = pos + 2 <= 64;
       const bool in_slot = pos + 2 <= x.stride;
-      if (in_line) ck = get16(d, pos);
-      else ck = in_slot ? *reinterpret_cast<const uint16_t *>(f + pos) : 0u;
-      if (proto == 6 || ck != 0) {
+      uint32_t ck = 0;
+#pragma unroll
+      for (int j = kL4Lo; j <= kL4Hi; j++) {
+        ck = l4_hi_at(j, ihl, tcp) ? d[j] >> 16 : ck;
+        ck = l4_lo_at(j, ihl, udp) ? d[j] & 0xFFFFu : ck;
+      }
+      if (!in_line) ck = in_slot ? *reinterpret_cast<const uint16_t *>(f + pos) : 0u;
+      if (tcp || ck != 0) {
         uint32_t nck = upd_ck(ck, incr);
-        if (proto == 17 && nck == 0) nck = 0xFFFF;
-        if (in_line) set16(d, pos, nck);
-        else if (in_slot) *reinterpret_cast<uint16_t *>(f + pos) = (uint16_t)nck;
+        if (udp && nck == 0) nck = 0xFFFF;
+        if (in_line) {
+#pragma unroll
+          for (int j = kL4Lo; j <= kL4Hi; j++) {
+            d[j] = l4_hi_at(j, ihl, tcp) ? (d[j] & 0xFFFFu) | (nck << 16) : d[j];
+            d[j] = l4_lo_at(j, ihl, udp) ? (d[j] & 0xFFFF0000u) | nck : d[j];
+          }
+        } else if (in_slot) {
+          *reinterpret_cast<uint16_t *>(f + pos) = (uint16_t)nck;
+        }
       }
     }
     // the address itself (src 26..29 / dst 30..33)
