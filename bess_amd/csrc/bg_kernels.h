@@ -175,6 +175,18 @@ struct NatArgs {
   uint32_t npairs, dir;
 };
 
+// IPEncap (core/modules/ip_encap.cc): slot i at slots + i*stride, its data
+// at + head[i], metadata area at + meta_off; offs: attr offsets of ip_src,
+// ip_dst, ip_proto, ip_nexthop, ether_type (< 0: invalid).
+struct EncapArgs {
+  uint8_t *slots;
+  uint64_t stride, n;
+  int32_t meta_off, offs[5];
+  uint16_t *head;  // data_off, in/out
+  uint32_t *len;   // pkt_len, in/out
+  uint16_t *out;
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -185,6 +197,7 @@ hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_encap(const EncapArgs &a, int num_cus, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword

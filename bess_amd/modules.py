@@ -235,6 +235,24 @@ class StaticNAT(Module):
         return self.command("get_initial_arg")
 
 
+# IPEncap attribute order (ip_encap.cc:36-40)
+IP_ENCAP_ATTRS = ("ip_src", "ip_dst", "ip_proto", "ip_nexthop", "ether_type")
+
+
+def ip_encap(d_slots, stride, n, meta_off, attr_offsets, d_head, d_len, d_out,
+             device=0, stream=None):
+    """core/modules/ip_encap.cc on the GPU (bg_ip_encap): torch tensors
+    d_slots (uint8 slab), d_head (int16: data_off), d_len (int32: pkt_len),
+    d_out (int16 gates); attr_offsets maps IP_ENCAP_ATTRS names to the
+    attribute offsets in the metadata area (missing: invalid)."""
+    from .flowtable import _stream_ptr
+    offs = (C.c_int32 * 5)(*[int(attr_offsets.get(k, -1)) for k in IP_ENCAP_ATTRS])
+    _check(lib().bg_ip_encap(device, C.c_void_p(d_slots.data_ptr()), stride, n,
+                             meta_off, offs, C.c_void_p(d_head.data_ptr()),
+                             C.c_void_p(d_len.data_ptr()),
+                             C.c_void_p(d_out.data_ptr()), _stream_ptr(stream)))
+
+
 class Pipe:
     """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
     are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered

@@ -267,6 +267,18 @@ size_t bg_snat_count(const bg_snat *h);
 int bg_snat_classify(bg_snat *h, void *d_frames, size_t stride, size_t n,
                      int dir, uint16_t *d_out, bg_stream_t stream);
 
+/* ---- IPEncap (core/modules/ip_encap.cc) -------------------------------- */
+/* ProcessBatch 40-80 on a device slab: packet i's slot at d_slots +
+ * i*stride, its data at slot + d_head[i] (the mbuf's data_off), pkt_len
+ * d_len[i], its metadata area at slot + meta_off. attr_offsets[5]: the
+ * attr_offset() of ip_src, ip_dst, ip_proto (read) and ip_nexthop,
+ * ether_type (written); < 0 = invalid (reads give 0, writes are skipped).
+ * A 20-byte IPv4 header is prepended in place (d_head -= 20, d_len += 20)
+ * unless the headroom is < 20; d_out[i] = 0 for every packet. */
+int bg_ip_encap(int device, void *d_slots, size_t stride, size_t n,
+                int meta_off, const int32_t *attr_offsets, uint16_t *d_head,
+                uint32_t *d_len, uint16_t *d_out, bg_stream_t stream);
+
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".

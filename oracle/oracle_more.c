@@ -418,3 +418,49 @@ void or_static_nat_process(const uint32_t *int_addr, const uint32_t *ext_addr,
     out[i] = dir == 0 ? 1 : 0;
   }
 }
+
+/* ====================================================================== */
+/* IPEncap (core/modules/ip_encap.cc)                                      */
+/* ====================================================================== */
+/* ProcessBatch 40-80 over a slab: slot i at base + i*stride; the packet's
+ * data at slot + head[i] (data_off), pkt_len len[i]; its metadata area at
+ * slot + meta_off; offs[0..4] = attr_offset() of ip_src, ip_dst, ip_proto
+ * (read), ip_nexthop, ether_type (write), < 0 when invalid (get_attr gives
+ * 0, set_attr does nothing: core/module.h:686-705). head/len are updated as
+ * Packet::prepend does (packet.h:145-154); a packet whose headroom is < 20
+ * is left alone. Every packet goes on (RunNextModule: gate 0). */
+void or_ip_encap_process(uint8_t *base, size_t stride, size_t n, int meta_off,
+                         const int32_t *offs, uint16_t *head, uint32_t *len,
+                         uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    uint8_t *slot = base + i * stride, *meta = slot + meta_off;
+    uint8_t src[4] = {0}, dst[4] = {0}, proto = 0;
+    if (offs[0] >= 0) memcpy(src, meta + offs[0], 4);
+    if (offs[1] >= 0) memcpy(dst, meta + offs[1], 4);
+    if (offs[2] >= 0) proto = meta[offs[2]];
+    uint16_t total_len = (uint16_t)(len[i] + 20);
+    out[i] = 0;
+    if (head[i] < 20) continue; /* prepend() returned nullptr */
+    head[i] -= 20;
+    len[i] += 20;
+    uint8_t *ip = slot + head[i];
+    ip[0] = 0x45;              /* version 4, header_length 5 */
+    ip[1] = 0;                 /* type_of_service */
+    ip[2] = (uint8_t)(total_len >> 8);
+    ip[3] = (uint8_t)total_len;
+    /* id (4-5) is not written: the headroom's bytes stay */
+    ip[6] = 0x40;              /* fragment_offset = kDF */
+    ip[7] = 0;
+    ip[8] = 64;                /* ttl */
+    ip[9] = proto;
+    memcpy(ip + 12, src, 4);
+    memcpy(ip + 16, dst, 4);
+    uint16_t ck = or_ipv4_checksum(ip); /* CalculateIpv4NoOptChecksum */
+    memcpy(ip + 10, &ck, 2);
+    if (offs[3] >= 0) memcpy(meta + offs[3], dst, 4);
+    if (offs[4] >= 0) {
+      meta[offs[4]] = 0x08;    /* be16(Ethernet::Type::kIpv4) */
+      meta[offs[4] + 1] = 0x00;
+    }
+  }
+}

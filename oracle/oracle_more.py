@@ -1,5 +1,5 @@
 """TEST INFRASTRUCTURE ONLY: control-plane restatements of the SURVEY §8f
-modules (HashLB, ACL, IPLookup, UpdateTTL, StaticNAT) around oracle_more.c. Only
+modules (HashLB, ACL, IPLookup, UpdateTTL, StaticNAT, IPEncap) around oracle_more.c. Only
 tests/, smoke() and bench.py's cpu_baseline leg import this. Each method
 cites the reference file:line it follows; errors raise OracleError(errno,
 message) with the reference's text."""
@@ -29,6 +29,7 @@ _SIGS = {
     "or_update_ttl_process": (None, [_vp, _sz, _sz, _vp]),
     "or_static_nat_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_int,
                                      _vp]),
+    "or_ip_encap_process": (None, [_vp, _sz, _sz, C.c_int, _vp, _vp, _vp, _vp]),
     "or_lpm_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_uint16,
                               _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
@@ -341,3 +342,15 @@ class OracleStaticNAT:
                                      _ptr(frames), stride, n,
                                      0 if igate == 0 else 1, out.ctypes.data)
         return out
+
+
+def ip_encap_process(slots, stride, n, meta_off, offs, head, length):
+    """IPEncap::ProcessBatch (ip_encap.cc:40-80) in place on a slab; offs:
+    5 attribute offsets (ip_src, ip_dst, ip_proto, ip_nexthop, ether_type),
+    < 0 invalid; head (uint16) / length (uint32) updated -> gates"""
+    o = np.ascontiguousarray(offs, np.int32)
+    out = np.empty(n, np.uint16)
+    mlib().or_ip_encap_process(_ptr(slots), stride, n, meta_off, o.ctypes.data,
+                               head.ctypes.data, length.ctypes.data,
+                               out.ctypes.data)
+    return out
