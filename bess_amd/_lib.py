@@ -121,6 +121,11 @@ _SIGS = {
     "bg_lpm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
     "bg_update_ttl": (_int, [_int, _vp, _sz, _sz, _vp, _vp]),
     "bg_ip_encap": (_int, [_int, _vp, _sz, _sz, _int, _vp, _vp, _vp, _vp, _vp]),
+    "bg_dnat_create": (_int, [_vp, _int, _vp, _vp, _vp, _vp, C.c_uint64,
+                              C.POINTER(_vp)]),
+    "bg_dnat_destroy": (None, [_vp]),
+    "bg_dnat_count": (_sz, [_vp]),
+    "bg_dnat_process": (_int, [_vp, _vp, _sz, _sz, _int, C.c_uint64, _vp, _vp]),
     "bg_snat_create": (_int, [C.POINTER(_vp)]),
     "bg_snat_destroy": (None, [_vp]),
     "bg_snat_add": (_int, [_vp, C.c_uint32, C.c_uint32, C.c_uint32]),

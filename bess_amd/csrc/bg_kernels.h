@@ -187,6 +187,27 @@ struct EncapArgs {
   uint16_t *out;
 };
 
+// NAT (core/modules/nat.cc): endpoint keys (addr raw | port raw << 32 |
+// proto << 48), per-packet entry indices (or kDnatMiss / kDnatInvalid),
+// the entries' translated endpoints and forward timestamps.
+constexpr uint32_t kDnatMiss = 0xFFFFFFFFu;
+constexpr uint32_t kDnatInvalid = 0xFFFFFFFEu;  // every code >= this drops
+constexpr uint16_t kDropGate = 8192;
+struct DnatArgs {
+  uint8_t *frames;
+  uint64_t stride, n;
+  uint32_t dir, refresh;
+  uint64_t now;
+  TableRef t;        // endpoint -> entry index (u32 values), KW = 1
+  uint64_t *keys;    // per packet: the endpoint key
+  uint32_t *res;     // per packet: entry / kDnatMiss / kDnatInvalid
+  uint32_t *nmiss;   // forward misses of the batch
+  const uint64_t *ent;  // per entry: translated endpoint
+  uint64_t *ts;      // per entry: last_refresh
+  uint64_t nent;     // entries the two arrays hold
+  uint16_t *out;
+};
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -198,6 +219,8 @@ hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_encap(const EncapArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_dnat_find(const DnatArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword

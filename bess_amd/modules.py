@@ -235,6 +235,51 @@ class StaticNAT(Module):
         return self.command("get_initial_arg")
 
 
+def _nat_arrays(ext_addrs):
+    """NATArg.ext_addrs (module_msg.proto) -> flat C arrays"""
+    addrs, nr, beg, end, sus = [], [], [], [], []
+    for a in ext_addrs:
+        addrs.append(str(a.get("ext_addr", "")).encode())
+        rl = a.get("port_ranges", [])
+        nr.append(len(rl))
+        for r in rl:
+            beg.append(int(r.get("begin", 0)))
+            end.append(int(r.get("end", 0)))
+            sus.append(1 if r.get("suspended", False) else 0)
+    k = max(len(beg), 1)
+    return ((C.c_char_p * max(len(addrs), 1))(*addrs), len(addrs),
+            (C.c_int32 * max(len(nr), 1))(*nr), (C.c_int64 * k)(*beg),
+            (C.c_int64 * k)(*end), (C.c_uint8 * k)(*sus))
+
+
+class NAT:
+    """core/modules/nat.cc on the GPU (bg_dnat_*): NAT(ext_addrs=[{'ext_addr':
+    '1.2.3.4', 'port_ranges': [{'begin': b, 'end': e, 'suspended': s}]}],
+    seed=...) -- the reference seeds its port search from rdtsc."""
+
+    def __init__(self, ext_addrs=(), seed=0x5EED):
+        a, n, nr, b, e, s = _nat_arrays(ext_addrs)
+        h = C.c_void_p()
+        _check(lib().bg_dnat_create(a, n, nr, b, e, s, seed, C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_dnat_destroy(self.h)
+            self.h = None
+
+    def desc(self):
+        return "%d entries" % lib().bg_dnat_count(self.h)
+
+    def process_device(self, d_frames, stride, n, d_ogates, now, igate=0,
+                       stream=None):
+        from .flowtable import _stream_ptr
+        _check(lib().bg_dnat_process(self.h, C.c_void_p(d_frames.data_ptr()), stride,
+                                     n, 0 if igate == 0 else 1, now,
+                                     C.c_void_p(d_ogates.data_ptr()),
+                                     _stream_ptr(stream)))
+
+
 # IPEncap attribute order (ip_encap.cc:36-40)
 IP_ENCAP_ATTRS = ("ip_src", "ip_dst", "ip_proto", "ip_nexthop", "ether_type")
 

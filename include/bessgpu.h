@@ -267,6 +267,28 @@ size_t bg_snat_count(const bg_snat *h);
 int bg_snat_classify(bg_snat *h, void *d_frames, size_t stride, size_t n,
                      int dir, uint16_t *d_out, bg_stream_t stream);
 
+/* ---- NAT (core/modules/nat.{h,cc}): dynamic address/port translation --- */
+/* Init (nat.cc:46-96): naddr external addresses (dotted strings) with
+ * nranges[i] port ranges each, flattened in begin / end / suspended (end
+ * exclusive as in PortRange; no ranges = [0, 65535)); errors and messages as
+ * the reference. seed: the Random the port search draws from (the
+ * reference seeds it from rdtsc). */
+typedef struct bg_dnat bg_dnat;
+int bg_dnat_create(const char *const *addrs, int naddr, const int32_t *nranges,
+                   const int64_t *begin, const int64_t *end,
+                   const uint8_t *suspended, uint64_t seed, bg_dnat **out);
+void bg_dnat_destroy(bg_dnat *h);
+/* GetDesc: mappings (map entries / 2) */
+size_t bg_dnat_count(const bg_dnat *h);
+/* DoProcessBatch<dir> (nat.cc:321-363) on a device slab in place: dir 0
+ * (input gate 0) maps internal sources, creating mappings, and emits on
+ * gate 1; dir 1 maps external destinations and emits on 0; unknown
+ * endpoints and other protocols: DROP_GATE. now: ctx->current_ns. A batch
+ * with new forward flows is decided on the host in packet order (the port
+ * search is sequential); synchronous. */
+int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
+                    int dir, uint64_t now, uint16_t *d_out, bg_stream_t stream);
+
 /* ---- IPEncap (core/modules/ip_encap.cc) -------------------------------- */
 /* ProcessBatch 40-80 on a device slab: packet i's slot at d_slots +
  * i*stride, its data at slot + d_head[i] (the mbuf's data_off), pkt_len

@@ -464,3 +464,253 @@ void or_ip_encap_process(uint8_t *base, size_t stride, size_t n, int meta_off,
     }
   }
 }
+
+/* ====================================================================== */
+/* NAT (core/modules/nat.{h,cc}): dynamic address/port translation         */
+/* ====================================================================== */
+/* Endpoint (nat.h:48-78) as its 8 bytes: addr raw be32 | port raw be16 <<
+ * 32 | protocol << 48; NatEntry {endpoint, last_refresh}. CuckooMap lookup
+ * semantics only (a key maps to one entry; Insert overwrites). The port
+ * search draws from bess::utils::Random (random.h:38-70), seeded here
+ * (the reference seeds it from rdtsc). */
+typedef struct {
+  uint64_t key, ep, ts;
+  int used;
+} or_nat_slot;
+
+typedef struct or_nat {
+  uint32_t naddr;
+  uint32_t addrs[64];          /* ext_addrs_ (raw be32), sorted by value */
+  uint32_t nranges[64];
+  uint16_t rbeg[64][16], rend[64][16];
+  uint8_t rsusp[64][16];       /* port_ranges_[i] (Init order, not sorted) */
+  uint64_t seed;               /* Random::seed_ */
+  size_t cap, count, tomb;
+  or_nat_slot *tab;            /* open addressing, power-of-two capacity */
+} or_nat;
+
+static uint64_t nat_mix(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+  return x;
+}
+
+static or_nat_slot *nat_find(or_nat *m, uint64_t key) {
+  size_t i = nat_mix(key) & (m->cap - 1);
+  for (;;) {
+    or_nat_slot *s = &m->tab[i];
+    if (s->used == 0) return NULL;
+    if (s->used == 1 && s->key == key) return s;
+    i = (i + 1) & (m->cap - 1);
+  }
+}
+
+static void nat_grow(or_nat *m);
+/* HashTable::Insert: overwrite or add */
+static or_nat_slot *nat_insert(or_nat *m, uint64_t key, uint64_t ep) {
+  or_nat_slot *s = nat_find(m, key);
+  if (s) { s->ep = ep; return s; }
+  if ((m->count + m->tomb + 1) * 2 > m->cap) nat_grow(m);
+  size_t i = nat_mix(key) & (m->cap - 1);
+  while (m->tab[i].used == 1) i = (i + 1) & (m->cap - 1);
+  if (m->tab[i].used == 2) m->tomb--;
+  m->tab[i].used = 1;
+  m->tab[i].key = key;
+  m->tab[i].ep = ep;
+  m->tab[i].ts = 0;
+  m->count++;
+  return &m->tab[i];
+}
+
+static void nat_grow(or_nat *m) {
+  size_t oc = m->cap;
+  or_nat_slot *ot = m->tab;
+  m->cap = oc ? (m->count * 4 > oc ? oc * 2 : oc) : 1024;
+  m->tab = (or_nat_slot *)calloc(m->cap, sizeof(or_nat_slot));
+  m->count = 0;
+  m->tomb = 0;
+  for (size_t i = 0; i < oc; i++)
+    if (ot[i].used == 1) {
+      or_nat_slot *s = nat_insert(m, ot[i].key, ot[i].ep);
+      s->ts = ot[i].ts;
+    }
+  free(ot);
+}
+
+/* HashTable::Remove: tombstone (used = 2) */
+static void nat_remove(or_nat *m, uint64_t key) {
+  or_nat_slot *s = nat_find(m, key);
+  if (s) { s->used = 2; m->count--; m->tomb++; }
+}
+
+or_nat *or_nat_new(uint64_t seed) {
+  or_nat *m = (or_nat *)calloc(1, sizeof(or_nat));
+  m->seed = seed;
+  nat_grow(m);
+  return m;
+}
+void or_nat_free(or_nat *m) { if (m) { free(m->tab); free(m); } }
+size_t or_nat_count(const or_nat *m) { return m->count; }
+
+/* Init 46-96 after validation: addresses in the argument's order with their
+ * range lists; ext_addrs_ is then sorted (be32_t compares values) while
+ * port_ranges_ keeps the argument's order. */
+void or_nat_init(or_nat *m, const uint32_t *addrs_host, uint32_t naddr,
+                 const uint32_t *nranges, const uint16_t *beg, const uint16_t *end,
+                 const uint8_t *susp) {
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < naddr; i++) {
+    if (nranges[i] == 0) {
+      m->nranges[i] = 1;
+      m->rbeg[i][0] = 0; m->rend[i][0] = 65535; m->rsusp[i][0] = 0;
+    } else {
+      m->nranges[i] = nranges[i];
+      for (uint32_t r = 0; r < nranges[i]; r++, k++) {
+        m->rbeg[i][r] = beg[k]; m->rend[i][r] = end[k]; m->rsusp[i][r] = susp[k];
+      }
+    }
+  }
+  uint32_t v[64];
+  memcpy(v, addrs_host, naddr * 4);
+  for (uint32_t i = 1; i < naddr; i++)   /* insertion sort by value */
+    for (uint32_t j = i; j > 0 && v[j - 1] > v[j]; j--) {
+      uint32_t t = v[j]; v[j] = v[j - 1]; v[j - 1] = t;
+    }
+  for (uint32_t i = 0; i < naddr; i++) m->addrs[i] = __builtin_bswap32(v[i]);
+  m->naddr = naddr;
+}
+
+/* Random::GetRange (random.h:58-75) */
+static uint32_t nat_get_range(or_nat *m, uint32_t range) {
+  m->seed = m->seed * 1103515245 + 12345;
+  union { uint64_t i; double d; } t;
+  t.i = (m->seed >> 12) | 0x3ff0000000000000ULL;
+  return (uint32_t)((t.d - 1.0) * range);
+}
+
+static uint64_t ep_make(uint32_t addr_raw, uint16_t port_raw, uint16_t proto) {
+  return (uint64_t)addr_raw | (uint64_t)port_raw << 32 | (uint64_t)proto << 48;
+}
+
+/* CreateNewEntry 180-258 -> the forward entry, or NULL */
+static or_nat_slot *nat_create(or_nat *m, uint64_t in, uint64_t now) {
+  const uint32_t in_addr = (uint32_t)in;
+  const uint16_t in_port = (uint16_t)(in >> 32), proto = (uint16_t)(in >> 48);
+  const uint32_t hashed = _mm_crc32_u32(0, in_addr); /* rte_hash_crc(&addr, 4, 0) */
+  const uint32_t idx = hashed % m->naddr;
+  const uint16_t in_port_host = __builtin_bswap16(in_port);
+  for (uint32_t r = 0; r < m->nranges[idx]; r++) {
+    uint16_t min, range;
+    if (m->rsusp[idx][r]) continue;
+    if (proto == 1) {
+      min = m->rbeg[idx][r];
+      range = (uint16_t)(m->rend[idx][r] - m->rbeg[idx][r]);
+    } else if (in_port_host == 0) {
+      return NULL;
+    } else if (in_port_host & ~1023u) {
+      if (m->rend[idx][r] <= 1024u) continue;
+      min = m->rbeg[idx][r] > 1024 ? m->rbeg[idx][r] : 1024;
+      range = (uint16_t)(m->rend[idx][r] - min + 1);
+    } else {
+      if (m->rbeg[idx][r] >= 1023u) continue;
+      min = m->rbeg[idx][r];
+      range = (uint16_t)((m->rend[idx][r] < 1023 ? m->rend[idx][r] : 1023) - min);
+    }
+    const uint16_t start = (uint16_t)(min + nat_get_range(m, range));
+    uint16_t port = start;
+    int trials = 0;
+    do {
+      const uint64_t ext = ep_make(m->addrs[idx], __builtin_bswap16(port), proto);
+      or_nat_slot *rev = nat_find(m, ext);
+      int take = rev == NULL;
+      if (!take) {
+        or_nat_slot *fwd = nat_find(m, rev->ep);
+        if (now - fwd->ts > 300ull * 1000 * 1000 * 1000) { /* kTimeOutNs */
+          nat_remove(m, fwd->key);
+          nat_remove(m, rev->key);
+          take = 1;
+        }
+      }
+      if (take) {
+        nat_insert(m, ext, in);
+        return nat_insert(m, in, ext);
+      }
+      port++;
+      trials++;
+      if (port == 0 || port >= min + range) port = min;
+    } while (port != start && trials < 128); /* kMaxTrials */
+  }
+  return NULL;
+}
+
+/* UpdateChecksumWithIncrement / ChecksumIncrement16/32 (checksum.h:520-549) */
+static uint16_t nat_upd(uint16_t ck, uint32_t incr) {
+  return or_fold_checksum((uint32_t)(~ck & 0xFFFF) + incr);
+}
+static uint32_t nat_inc32(uint32_t o, uint32_t n) {
+  return (~o >> 16) + (~o & 0xFFFF) + (n >> 16) + (n & 0xFFFF);
+}
+static uint32_t nat_inc16(uint16_t o, uint16_t n) { return (uint32_t)(~o & 0xFFFF) + n; }
+
+/* DoProcessBatch<dir> 321-363 with ExtractEndpoint 120-160 and Stamp
+ * 262-319, over n packets (32-packet batches give the same result: every
+ * packet is decided in order) */
+void or_nat_process(or_nat *m, uint8_t *base, size_t stride, size_t n, int dir,
+                    uint64_t now, uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    uint8_t *ip = base + i * stride + 14;
+    uint8_t *l4 = ip + ((ip[0] & 0x0F) << 2);
+    const uint8_t proto = ip[9];
+    uint16_t port;
+    int valid = 0;
+    if (proto == 6 || proto == 17) {
+      memcpy(&port, l4 + (dir == 0 ? 0 : 2), 2);
+      valid = 1;
+    } else if (proto == 1) {
+      const uint8_t t = l4[0];
+      if (t == 0 || t == 8 || t == 13 || t == 15 || t == 16) {
+        memcpy(&port, l4 + 4, 2); /* icmp->ident */
+        valid = 1;
+      }
+    }
+    if (!valid) { out[i] = 8192; continue; } /* DropPacket */
+    uint32_t addr;
+    memcpy(&addr, ip + (dir == 0 ? 12 : 16), 4);
+    const uint64_t before = ep_make(addr, port, proto);
+    or_nat_slot *e = nat_find(m, before);
+    if (!e) {
+      if (dir != 0 || !(e = nat_create(m, before, now))) { out[i] = 8192; continue; }
+    }
+    if (dir == 0) e->ts = now;
+    /* Stamp<dir> */
+    const uint32_t na = (uint32_t)e->ep;
+    const uint16_t np = (uint16_t)(e->ep >> 32);
+    memcpy(ip + (dir == 0 ? 12 : 16), &na, 4);
+    const uint32_t l3 = nat_inc32(addr, na);
+    uint16_t ck;
+    memcpy(&ck, ip + 10, 2);
+    ck = nat_upd(ck, l3);
+    memcpy(ip + 10, &ck, 2);
+    const uint32_t l4inc = l3 + nat_inc16(port, np);
+    if (proto == 6 || proto == 17) {
+      memcpy(l4 + (dir == 0 ? 0 : 2), &np, 2);
+      if (proto == 6) {
+        memcpy(&ck, l4 + 16, 2);
+        ck = nat_upd(ck, l4inc);
+        memcpy(l4 + 16, &ck, 2);
+      } else {
+        memcpy(&ck, l4 + 6, 2);
+        if (ck != 0) {
+          ck = nat_upd(ck, l4inc);
+          if (ck == 0) ck = 0xFFFF;
+          memcpy(l4 + 6, &ck, 2);
+        }
+      }
+    } else {
+      memcpy(l4 + 4, &np, 2);
+      memcpy(&ck, l4 + 2, 2);
+      ck = nat_upd(ck, nat_inc16(port, np)); /* UpdateChecksum16 */
+      memcpy(l4 + 2, &ck, 2);
+    }
+    out[i] = dir == 0 ? 1 : 0;
+  }
+}

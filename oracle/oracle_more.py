@@ -1,5 +1,5 @@
 """TEST INFRASTRUCTURE ONLY: control-plane restatements of the SURVEY §8f
-modules (HashLB, ACL, IPLookup, UpdateTTL, StaticNAT, IPEncap) around oracle_more.c. Only
+modules (HashLB, ACL, IPLookup, UpdateTTL, StaticNAT, IPEncap, NAT) around oracle_more.c. Only
 tests/, smoke() and bench.py's cpu_baseline leg import this. Each method
 cites the reference file:line it follows; errors raise OracleError(errno,
 message) with the reference's text."""
@@ -30,6 +30,11 @@ _SIGS = {
     "or_static_nat_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_int,
                                      _vp]),
     "or_ip_encap_process": (None, [_vp, _sz, _sz, C.c_int, _vp, _vp, _vp, _vp]),
+    "or_nat_new": (_vp, [C.c_uint64]),
+    "or_nat_free": (None, [_vp]),
+    "or_nat_count": (_sz, [_vp]),
+    "or_nat_init": (None, [_vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp]),
+    "or_nat_process": (None, [_vp, _vp, _sz, _sz, C.c_int, C.c_uint64, _vp]),
     "or_lpm_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_uint16,
                               _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
@@ -354,3 +359,55 @@ def ip_encap_process(slots, stride, n, meta_off, offs, head, length):
                                head.ctypes.data, length.ctypes.data,
                                out.ctypes.data)
     return out
+
+
+class OracleNAT:
+    """core/modules/nat.{h,cc}; seed: the module's Random (rdtsc in the
+    reference)"""
+
+    def __init__(self, ext_addrs=(), seed=0x5EED):
+        # Init 46-96: every range is checked before any address
+        for a in ext_addrs:
+            for r in a.get("port_ranges", []):
+                b, e = int(r.get("begin", 0)), int(r.get("end", 0))
+                if b >= e or b > 65535 or e > 65535:
+                    raise OracleError(E.EINVAL, "Port range for address %s is "
+                                      "malformed" % a.get("ext_addr", ""))
+        addrs, nr, beg, end, sus = [], [], [], [], []
+        for a in ext_addrs:
+            v = _ipv4(a.get("ext_addr", ""))
+            if v is None:
+                raise OracleError(E.EINVAL, "invalid IP address %s"
+                                  % a.get("ext_addr", ""))
+            addrs.append(v)
+            rl = a.get("port_ranges", [])
+            nr.append(len(rl))
+            for r in rl:
+                beg.append(int(r["begin"]))
+                end.append(int(r["end"]))
+                sus.append(1 if r.get("suspended", False) else 0)
+        if not addrs:
+            raise OracleError(E.EINVAL,
+                              "at least one external IP address must be specified")
+        self.h = mlib().or_nat_new(seed)
+        A = np.array(addrs, np.uint32)
+        N = np.array(nr, np.uint32)
+        B = np.array(beg or [0], np.uint16)
+        En = np.array(end or [0], np.uint16)
+        S = np.array(sus or [0], np.uint8)
+        mlib().or_nat_init(self.h, A.ctypes.data, len(addrs), N.ctypes.data,
+                           B.ctypes.data, En.ctypes.data, S.ctypes.data)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            mlib().or_nat_free(self.h)
+            self.h = None
+
+    def desc(self):
+        return "%d entries" % (mlib().or_nat_count(self.h) // 2)
+
+    def process(self, frames, stride, n, igate, now):
+        out = np.empty(n, np.uint16)
+        mlib().or_nat_process(self.h, _ptr(frames), stride, n,
+                              0 if igate == 0 else 1, now, out.ctypes.data)
+        return out

@@ -1,0 +1,173 @@
+"""NAT (core/modules/nat.{h,cc}): dynamic address/port translation. The
+oracle restates Init, CreateNewEntry (port search from the module's Random,
+eviction of expired mappings), ExtractEndpoint and Stamp; the GPU datapath
+(bg_dnat: device lookup + rewrite, new mappings decided on the host in
+packet order) must leave every packet byte and gate equal to the oracle's,
+batch after batch: new flows, established flows (the device-only path),
+reverse traffic, ICMP queries, protocols NAT drops, port 0, ports below
+1024, suspended and exhausted ranges, and expiry after 300 s. The
+reference seeds its Random from rdtsc; both sides take the same seed."""
+import errno
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import oracle_more as OM
+
+EXT = [{"ext_addr": "10.9.0.2", "port_ranges": [
+           {"begin": 2000, "end": 2100},
+           {"begin": 100, "end": 200, "suspended": True},
+           {"begin": 5, "end": 900}]},
+       {"ext_addr": "10.9.0.1"},
+       {"ext_addr": "8.8.8.8", "port_ranges": [{"begin": 1024, "end": 1040}]}]
+STRIDE = 128
+T0 = 10**12
+
+
+def flows(n, rng):
+    """internal endpoints: (src ip, port, proto, icmp type)"""
+    src = (0xC0A80000 | rng.integers(0, 1 << 16, n)).astype(np.uint64)
+    r = rng.random(n)
+    proto = np.where(r < 0.45, 6, np.where(r < 0.85, 17, np.where(r < 0.95, 1, 47)))
+    port = rng.integers(1024, 65536, n)
+    low = rng.random(n) < 0.15
+    port[low] = rng.integers(1, 1024, int(low.sum()))
+    port[rng.random(n) < 0.02] = 0
+    itype = rng.choice([0, 8, 13, 15, 16, 3, 11], n)
+    return src, port, proto, itype
+
+
+def frames(src, sport, dst, dport, proto, itype, rng, ihl=None):
+    """Eth / IPv4 (IHL 5..7) / TCP, UDP or ICMP; valid checksums"""
+    n = len(src)
+    f = np.zeros((n, STRIDE), np.uint8)
+    f[:, 12:14] = [0x08, 0x00]
+    if ihl is None:
+        ihl = np.where(rng.random(n) < 0.8, 5, rng.integers(6, 8, n))
+    f[:, 14] = 0x40 | ihl
+    l4 = 14 + 4 * ihl
+    for i in range(n):
+        o = 14 + 20
+        f[i, o:l4[i]] = rng.integers(0, 256, l4[i] - o)  # options
+        pl = {6: 20, 17: 8, 1: 8}.get(int(proto[i]), 8) + 16
+        iplen = 4 * ihl[i] + pl
+        f[i, 16:18] = [iplen >> 8, iplen & 255]
+        f[i, 18:20] = rng.integers(0, 256, 2)
+        f[i, 22] = 64
+        f[i, 23] = proto[i]
+        f[i, 26:30] = np.frombuffer(int(src[i]).to_bytes(4, "big"), np.uint8)
+        f[i, 30:34] = np.frombuffer(int(dst[i]).to_bytes(4, "big"), np.uint8)
+        L = l4[i]
+        f[i, L + 8:L + pl] = rng.integers(0, 256, pl - 8)
+        if proto[i] in (6, 17):
+            f[i, L:L + 2] = [sport[i] >> 8, sport[i] & 255]
+            f[i, L + 2:L + 4] = [dport[i] >> 8, dport[i] & 255]
+            if proto[i] == 17:
+                f[i, L + 4:L + 6] = [pl >> 8, pl & 255]
+            else:
+                f[i, L + 12] = 0x50
+        elif proto[i] == 1:
+            f[i, L] = itype[i]
+            f[i, L + 2:L + 4] = rng.integers(0, 256, 2)  # checksum: any
+            f[i, L + 4:L + 6] = [sport[i] >> 8, sport[i] & 255]  # ident
+    O.cksum_process(f, STRIDE, n, 3, False)
+    udp0 = np.nonzero((proto == 17) & (rng.random(n) < 0.1))[0]
+    for i in udp0:  # UDP checksum 0: left alone
+        f[i, l4[i] + 6:l4[i] + 8] = 0
+    return f
+
+
+def ext_side(g):
+    """(addr, port) NAT gave each forwarded packet (its new source)"""
+    ihl = g[:, 14] & 15
+    l4 = 14 + 4 * ihl
+    addr = np.array([int.from_bytes(g[i, 26:30].tobytes(), "big") for i in range(len(g))])
+    port = np.array([int.from_bytes(g[i, l4[i]:l4[i] + 2].tobytes(), "big")
+                     if g[i, 23] in (6, 17) else
+                     int.from_bytes(g[i, l4[i] + 4:l4[i] + 6].tobytes(), "big")
+                     for i in range(len(g))])
+    return addr, port
+
+
+def test_init_errors_match_oracle():
+    from bess_amd.modules import NAT, ModuleError
+    bad = [[{"ext_addr": "1.2.3.4", "port_ranges": [{"begin": 5, "end": 5}]}],
+           [{"ext_addr": "1.2.3.4", "port_ranges": [{"begin": 5, "end": 70000}]}],
+           [{"ext_addr": "1.2.3"}],
+           [{"ext_addr": "bad", "port_ranges": [{"begin": 9, "end": 5}]}],
+           []]
+    for arg in bad:
+        with pytest.raises(OM.OracleError) as eo:
+            OM.OracleNAT(ext_addrs=arg)
+        with pytest.raises(ModuleError) as em:
+            NAT(ext_addrs=arg)
+        assert em.value.code == eo.value.code == errno.EINVAL
+        assert em.value.errmsg == eo.value.msg
+    assert NAT(ext_addrs=EXT).desc() == OM.OracleNAT(ext_addrs=EXT).desc() == "0 entries"
+
+
+def test_oracle_translation_keeps_checksums_valid():
+    """Stamp's incremental updates leave valid IPv4 and TCP/UDP checksums
+    (the reference's pin for incremental updates, checksum_test.cc:408-457)"""
+    rng = np.random.default_rng(1)
+    s, p, pr, it = flows(2000, rng)
+    pr[:] = np.where(pr == 6, 6, 17)
+    p[p == 0] = 4000
+    f = frames(s, p, np.full(2000, 0x08080404), rng.integers(1, 65536, 2000), pr, it,
+               rng, ihl=np.full(2000, 5))
+    o = OM.OracleNAT(ext_addrs=EXT, seed=7)
+    g = f.copy()
+    out = o.process(g, STRIDE, 2000, 0, T0)
+    ok = out == 1
+    assert ok.sum() > 500  # the small ranges run out (drops)
+    ipg, l4g = O.cksum_process(g, STRIDE, 2000, 3, True)
+    assert (ipg[ok] == 0).all() and (l4g[ok] == 0).all()
+
+
+@pytest.mark.gpu
+def test_gpu_batches_vs_oracle():
+    import torch
+    from bess_amd.modules import NAT
+    rng = np.random.default_rng(11)
+    m, o = NAT(ext_addrs=EXT, seed=0xABC), OM.OracleNAT(ext_addrs=EXT, seed=0xABC)
+
+    def run(f, igate, now):
+        ref = f.copy()
+        want = o.process(ref, STRIDE, len(f), igate, now)
+        d = torch.from_numpy(f.reshape(-1).copy()).cuda()
+        og = torch.zeros(len(f), dtype=torch.int16, device="cuda")
+        m.process_device(d, STRIDE, len(f), og, now, igate=igate)
+        got = d.cpu().numpy().reshape(len(f), STRIDE)
+        assert (og.cpu().numpy().view(np.uint16) == want).all()
+        bad = np.nonzero((got != ref).any(1))[0]
+        assert len(bad) == 0, bad[:5]
+        assert m.desc() == o.desc()
+        return ref, want
+
+    n = 6000
+    s, p, pr, it = flows(1500, rng)
+    pick = rng.integers(0, 1500, n)
+    dst = rng.integers(1, 1 << 32, n)
+    dport = rng.integers(1, 65536, n)
+    fa = frames(s[pick], p[pick], dst, dport, pr[pick], it[pick], rng)
+    ga, out_a = run(fa, 0, T0)                            # new flows (host walk)
+    mapped = out_a == 1
+    assert 0.5 < mapped.mean() < 1.0 and int(m.desc().split()[0]) > 500
+    run(fa[mapped], 0, T0 + 1000)                         # established: device only
+    ea, ep = ext_side(ga[mapped])                         # reverse traffic
+    k = int(mapped.sum())
+    prm = pr[pick][mapped]
+    # reverse endpoint: (dst, dst port) for TCP/UDP, (dst, ident) for ICMP
+    rev = frames(dst[mapped], np.where(prm == 1, ep, dport[mapped]), ea, ep, prm,
+                 it[pick][mapped], rng)
+    unk = frames(rng.integers(1, 1 << 32, 500), rng.integers(1, 65536, 500),
+                 rng.integers(1, 1 << 32, 500), rng.integers(1, 65536, 500),
+                 np.full(500, 6), np.zeros(500, int), rng)
+    run(np.concatenate([rev, unk]), 1, T0 + 2000)         # reverse hits + drops
+    # 301 s later: new flows evict expired mappings where ports collide
+    s2, p2, pr2, it2 = flows(3000, rng)
+    fb = frames(s2, p2, rng.integers(1, 1 << 32, 3000), rng.integers(1, 65536, 3000),
+                pr2, it2, rng)
+    run(fb, 0, T0 + 301 * 10**9)
+    run(rev[:2000], 1, T0 + 302 * 10**9)                  # some mappings now gone
