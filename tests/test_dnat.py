@@ -171,3 +171,76 @@ def test_gpu_batches_vs_oracle():
                 pr2, it2, rng)
     run(fb, 0, T0 + 301 * 10**9)
     run(rev[:2000], 1, T0 + 302 * 10**9)                  # some mappings now gone
+
+
+# ---- bessctl/module_tests/nat.py, restated (scapy is absent: packets are
+# built field by field with scapy's defaults and fresh checksums)
+def scapy_pkt(src, dst, kind, sport=0, dport=0, udp_ck0=False, icmp_id=0):
+    import struct
+    l7 = b"helloworld"
+    if kind == "udp":
+        l4 = struct.pack(">HHHH", sport, dport, 8 + len(l7), 0) + l7
+        proto = 17
+    elif kind == "tcp":  # seq 0, ack 0, dataofs 5, flags S, window 8192
+        l4 = struct.pack(">HHIIBBHHH", sport, dport, 0, 0, 0x50, 0x02, 8192, 0, 0) + l7
+        proto = 6
+    else:                # echo-request, code 0, id, seq 0
+        l4 = struct.pack(">BBHHH", 8, 0, 0, icmp_id, 0) + l7
+        proto = 1
+    ip = struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + len(l4), 1, 0, 64, proto, 0,
+                     bytes(int(x) for x in src.split(".")),
+                     bytes(int(x) for x in dst.split(".")))
+    eth = bytes.fromhex("06163e1b7232" "021e679f4dae" "0800")
+    f = np.zeros((1, STRIDE), np.uint8)
+    b = eth + ip + l4
+    f[0, :len(b)] = np.frombuffer(b, np.uint8)
+    O.cksum_process(f, STRIDE, 1, 3, False)  # IPv4 + TCP/UDP checksums
+    if kind == "icmp":
+        ck = O.lib().or_generic_checksum(f[0, 34:].ctypes.data, len(l4))
+        f[0, 36:38] = [ck & 255, ck >> 8]
+    if udp_ck0:
+        f[0, 40:42] = 0
+    return f, len(b)
+
+
+CASES = [("udp", 56797, 53, False), ("udp", 56797, 53, True),
+         ("tcp", 52428, 80, False), ("icmp", 0, 0, False)]
+
+
+def module_test_case(kind, sport, dport, ck0, process):
+    """nat.py _test_l4: orig -> natted (= a fresh packet from the rule
+    address and the chosen port) -> reply -> unnatted (= the swapped
+    original)"""
+    f, ln = scapy_pkt("172.16.0.2", "8.8.8.8", kind, sport, dport, ck0)
+    g = f.copy()
+    assert list(process(g, 0)) == [1]
+    l4 = 34
+    chosen = int.from_bytes(g[0, l4 + (4 if kind == "icmp" else 0):][:2].tobytes(), "big")
+    want, _ = scapy_pkt("192.168.1.1", "8.8.8.8", kind, chosen, dport, ck0, chosen)
+    assert (g[0, :ln] == want[0, :ln]).all(), kind
+    rep, _ = scapy_pkt("8.8.8.8", "192.168.1.1", kind, dport, chosen, ck0, chosen)
+    assert list(process(rep, 1)) == [0]
+    unn, _ = scapy_pkt("8.8.8.8", "172.16.0.2", kind, dport, sport, ck0, 0)
+    assert (rep[0, :ln] == unn[0, :ln]).all(), kind
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_vs_reference_module_test(case):
+    o = OM.OracleNAT(ext_addrs=[{"ext_addr": "192.168.1.1"}], seed=3)
+    module_test_case(*case, lambda f, g: o.process(f, STRIDE, 1, g, T0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_gpu_vs_reference_module_test(case):
+    import torch
+    from bess_amd.modules import NAT
+    m = NAT(ext_addrs=[{"ext_addr": "192.168.1.1"}], seed=3)
+
+    def process(f, igate):
+        d = torch.from_numpy(f.reshape(-1).copy()).cuda()
+        og = torch.zeros(1, dtype=torch.int16, device="cuda")
+        m.process_device(d, STRIDE, 1, og, T0, igate=igate)
+        f[:] = d.cpu().numpy().reshape(f.shape)
+        return og.cpu().numpy().view(np.uint16)
+    module_test_case(*case, process)
