@@ -9,6 +9,7 @@
 //   em32    : bytes 16..47 of every 64 B slot (two 16 B loads per lane, lane
 //             = slot) + one 2-byte store per slot -- the C2 ExactMatch shape
 //   slot64  : all 64 B of every slot (four 16 B loads per lane, lane = slot)
+//   half32  : bytes 16..47 of every slot, two lanes per slot, lanes contiguous
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
 // bytes read (median of 5 rounds of 20 back-to-back launches).
 #include <hip/hip_runtime.h>
@@ -58,6 +59,21 @@ __global__ __launch_bounds__(512) void slot64(const u32x4 *src, size_t nslots,
   }
 }
 
+// bytes 16..47 of every slot with lane-paired loads: lanes 2j, 2j+1 read
+// chunks 1 and 2 of slot j (32 contiguous bytes per slot, the other 32
+// skipped) -- the ExactMatch 5-tuple window only
+__global__ __launch_bounds__(512) void half32(const u32x4 *src, size_t nslots,
+                                              uint16_t *gates) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x; u < nslots * 2;
+       u += step) {
+    const size_t slot = u >> 1;
+    u32x4 a = ldnt(src + 4 * slot + 1 + (u & 1));
+    const uint32_t x = a.x ^ a.w;
+    if ((u & 1) == 0) gates[slot] = (uint16_t)x;
+  }
+}
+
 #define CK(x)                                                            \
   do {                                                                   \
     hipError_t e = (x);                                                  \
@@ -83,8 +99,8 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char *names[3] = {"full16", "em32", "slot64"};
-  for (int shape = 0; shape < 3; shape++) {
+  const char *names[4] = {"full16", "em32", "slot64", "half32"};
+  for (int shape = 0; shape < 4; shape++) {
     for (int bpc : {1, 2, 4, 8}) {
       const int blocks = cus * bpc;
       auto launch = [&]() {
@@ -94,8 +110,11 @@ int main(int argc, char **argv) {
         else if (shape == 1)
           hipLaunchKernelGGL(em32, dim3(blocks), dim3(512), 0, 0, src, nslots,
                              gates);
-        else
+        else if (shape == 2)
           hipLaunchKernelGGL(slot64, dim3(blocks), dim3(512), 0, 0, src,
+                             nslots, gates);
+        else
+          hipLaunchKernelGGL(half32, dim3(blocks), dim3(512), 0, 0, src,
                              nslots, gates);
       };
       for (int w = 0; w < 20; w++) launch();
