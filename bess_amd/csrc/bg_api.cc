@@ -541,6 +541,26 @@ static int em_launch(bg_em *em, const void *d_frames, size_t stride, size_t n,
   return 0;
 }
 
+// Every byte a classify kernel reads for packet i lies in its slot, so the
+// last packet's reads stay inside the slab: the staged window
+// [win_lo, win_lo + 16 * nch), or in direct mode each field's dwords.
+static int check_extent(const std::vector<bg_field> &fields, int shift,
+                        size_t stride) {
+  if (fields.empty()) return 0;
+  const FieldPlan p = make_plan(fields, false, shift);
+  int hi = 0;
+  if (!p.direct) {
+    hi = p.win_lo + 16 * p.nch;
+  } else {
+    for (int i = 0; i < p.nf; i++)
+      hi = std::max(hi, (fspec_d(p.fspec[i]) + fspec_nd(p.fspec[i])) * 4);
+  }
+  if (hi > (int)stride || p.win_lo < 0)
+    return fail(EINVAL, "fields read bytes up to %d, past the %zu-byte slot", hi,
+                stride);
+  return 0;
+}
+
 static int no_attr_datapath() {
   return fail(ENOTSUP, "metadata-attribute (attr_name) fields need the "
               "packets' metadata in the slot: bind its layout first "
@@ -595,6 +615,7 @@ int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
+  if (int r = check_extent(em->dfields, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
   int dev = em->dev.valid ? em->dev.device : 0;
   if (!em->dev.valid || em->dirty) {
@@ -984,6 +1005,7 @@ int bg_wm_classify_window(bg_wm *wm, const void *d_frames, size_t stride,
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
   if (stride % 16 || ((uintptr_t)d_frames & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
+  if (int r = check_extent(wm->dfields, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
   if (!wm->dev.valid || wm->dirty) {
     int cur = 0;

@@ -83,3 +83,22 @@ def _keys_off(img):
             if pbytes == n:
                 return nbp * 4
     raise AssertionError("layout not found")
+
+
+def test_classify_rejects_reads_past_the_slot():
+    """a slab whose slots are shorter than the fields' read window is
+    refused before any device work (the last packet would read past the
+    slab): EM at offset 60..63 in 64-byte slots passes the check (then
+    fails for want of a device), at 100 it is refused"""
+    import ctypes as C
+    frames = np.zeros(64 * 4, np.uint8)
+    gates = np.zeros(4, np.uint16)
+    for fields, ok in (([(60, 4)], True), ([(100, 4)], False),
+                       ([(26, 4), (1020, 2)], False)):
+        t = F.EmTable([(o, s, (1 << (8 * s)) - 1) for o, s in fields])
+        t.add_many(np.zeros((1, sum(s for _, s in fields)), np.uint8),
+                   np.zeros(1, np.uint16))
+        rc = F.lib().bg_em_classify(t.h, C.c_void_p(frames.ctypes.data), 64, 4, 0,
+                                    C.c_void_p(gates.ctypes.data), None)
+        assert rc < 0
+        assert (rc == -22) != ok, (fields, rc, F.lib().bg_last_error())
