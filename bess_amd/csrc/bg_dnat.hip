@@ -12,6 +12,9 @@
 // Lane = packet; header fields past the first bytes are reached through
 // the frame pointer (any IHL).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "bg_kernels.h"
 #include "bg_keys_dev.h"
@@ -21,16 +24,41 @@ namespace {
 
 constexpr int kNatBlock = 256;
 
-__device__ __forceinline__ uint32_t ld_u16(const uint8_t *p) {
-  return (uint32_t)p[0] | (uint32_t)p[1] << 8;
-}
-__device__ __forceinline__ void st_u16(uint8_t *p, uint32_t v) {
-  p[0] = (uint8_t)v;
-  p[1] = (uint8_t)(v >> 8);
-}
-__device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {
-  return ld_u16(p) | ld_u16(p + 2) << 16;
-}
+// Frame byte access. Header fields sit at even offsets (the IPv4 header
+// starts at 14, L4 at 14 + 4 * IHL), so a u16 never straddles a dword or a
+// 16-byte stage chunk. Bytes past the slot read as 0 and writes to them are
+// dropped (the reference reads on into its 2 KB buffer; a slot holds the
+// frame only).
+struct GlobalFrame {  // the frame in HBM (any stride)
+  uint8_t *p;
+  uint32_t lim;
+  __device__ uint32_t u8(uint32_t o) const { return o < lim ? p[o] : 0u; }
+  __device__ uint32_t u16(uint32_t o) const {
+    return o + 2 <= lim ? (uint32_t)p[o] | (uint32_t)p[o + 1] << 8 : 0u;
+  }
+  __device__ void put16(uint32_t o, uint32_t v) const {
+    if (o + 2 > lim) return;
+    p[o] = (uint8_t)v;
+    p[o + 1] = (uint8_t)(v >> 8);
+  }
+};
+
+// This lane's 64-byte slot in the wave's swizzled LDS stage (slot s keeps
+// chunk q at unit 4s + ((q + s/4) & 3), as line_slab_kernel)
+struct StageSlot {
+  uint8_t *stage;  // the wave's 4 KB stage
+  uint32_t slot;
+  __device__ uint32_t at(uint32_t o) const {
+    return (slot * 4 + (((o >> 4) + (slot >> 2)) & 3)) * 16 + (o & 15);
+  }
+  __device__ uint32_t u8(uint32_t o) const { return o < 64 ? stage[at(o)] : 0u; }
+  __device__ uint32_t u16(uint32_t o) const {
+    return o + 2 <= 64 ? *reinterpret_cast<const uint16_t *>(stage + at(o)) : 0u;
+  }
+  __device__ void put16(uint32_t o, uint32_t v) const {
+    if (o + 2 <= 64) *reinterpret_cast<uint16_t *>(stage + at(o)) = (uint16_t)v;
+  }
+};
 
 // fold(~ck + incr) (UpdateChecksumWithIncrement, checksum.h:535-538)
 __device__ __forceinline__ uint32_t upd_ck(uint32_t ck, uint32_t incr) {
@@ -40,49 +68,116 @@ __device__ __forceinline__ uint32_t upd_ck(uint32_t ck, uint32_t incr) {
   return ~s & 0xFFFFu;
 }
 
-// ExtractEndpoint: the endpoint key (addr raw | port raw << 32 | proto <<
-// 48) or ~0 for a protocol NAT does not handle
-__device__ __forceinline__ uint64_t endpoint(const uint8_t *ip, int dir) {
-  const uint8_t *l4 = ip + ((ip[0] & 0x0Fu) << 2);
-  const uint32_t proto = ip[9];
+// ExtractEndpoint (nat.cc:120-160): the endpoint key (addr raw | port raw
+// << 32 | proto << 48) or ~0 for a protocol NAT does not handle
+template <class F>
+__device__ __forceinline__ uint64_t endpoint(const F &f, uint32_t dir) {
+  const uint32_t l4 = 14 + ((f.u8(14) & 0x0Fu) << 2);
+  const uint32_t proto = f.u8(23);
   uint32_t port;
   if (proto == 6 || proto == 17) {
-    port = ld_u16(l4 + (dir == 0 ? 0 : 2));
+    port = f.u16(l4 + (dir == 0 ? 0 : 2));
   } else if (proto == 1) {
-    const uint32_t t = l4[0];
+    const uint32_t t = f.u8(l4);
     if (!(t == 0 || t == 8 || t == 13 || t == 15 || t == 16)) return ~0ull;
-    port = ld_u16(l4 + 4);  // icmp->ident
+    port = f.u16(l4 + 4);  // icmp->ident
   } else {
     return ~0ull;
   }
-  const uint32_t addr = ld_u32(ip + (dir == 0 ? 12 : 16));
+  const uint32_t ao = dir == 0 ? 26 : 30;
+  const uint32_t addr = f.u16(ao) | f.u16(ao + 2) << 16;
   return (uint64_t)addr | (uint64_t)port << 32 | (uint64_t)proto << 48;
+}
+
+// endpoint -> table slot, or ~0u. A slot's key is two words: the
+// endpoint and its translated endpoint (so a hit needs no entry read); the
+// slot's value is the entry index (for the timestamp). The first candidate
+// slot's 16-byte key and its value are read together.
+struct SlotHit {
+  uint32_t slot, entry;
+  uint64_t ep;
+};
+__device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(a.t.base);
+  const u32x4 *kv = reinterpret_cast<const u32x4 *>(a.t.base + a.t.keys_off);
+  const uint32_t *vals = reinterpret_cast<const uint32_t *>(a.t.base + a.t.vals_off);
+  const Probe p = split_hash(hash_words(&key, 1, a.t.seed), 1, a.t.nbp);
+  uint32_t c = tag_match(tags[p.b1], p.tag) | (tag_match(tags[p.b2], p.tag) << 4);
+  SlotHit h;
+  h.slot = ~0u;
+  h.entry = 0;
+  h.ep = 0;
+  while (c) {
+    const int s = __builtin_ctz(c);
+    c &= c - 1;
+    const uint32_t slot = (s < 4 ? p.b1 : p.b2) * kSlots + (s & 3);
+    const u32x4 k = kv[slot];
+    const uint32_t e = vals[slot];
+    if ((k.x | (uint64_t)k.y << 32) == key) {
+      h.slot = slot;
+      h.entry = e;
+      h.ep = k.z | (uint64_t)k.w << 32;
+      break;
+    }
+  }
+  return h;
+}
+// endpoint -> entry index, or kDnatMiss
+__device__ __forceinline__ uint32_t lookup(const DnatArgs &a, uint64_t key) {
+  const SlotHit h = lookup_hit(a, key);
+  return h.slot == ~0u ? kDnatMiss : h.entry;
+}
+
+// Stamp<dir> (nat.cc:262-319): `before` -> `after` endpoint, IPv4 and
+// TCP / UDP / ICMP checksums updated incrementally (RFC 1624)
+template <class F>
+__device__ __forceinline__ void stamp(const F &f, uint64_t before, uint64_t after,
+                                      uint32_t dir) {
+  const uint32_t l4 = 14 + ((f.u8(14) & 0x0Fu) << 2);
+  const uint32_t oa = (uint32_t)before, na = (uint32_t)after;
+  const uint32_t op = (uint32_t)(before >> 32) & 0xFFFFu,
+                 np = (uint32_t)(after >> 32) & 0xFFFFu;
+  const uint32_t proto = f.u8(23);
+  const uint32_t ao = dir == 0 ? 26 : 30;
+  f.put16(ao, na & 0xFFFFu);
+  f.put16(ao + 2, na >> 16);
+  // ChecksumIncrement32(before.addr, after.addr)
+  const uint32_t l3 = (~oa >> 16) + (~oa & 0xFFFFu) + (na >> 16) + (na & 0xFFFFu);
+  f.put16(24, upd_ck(f.u16(24), l3));
+  const uint32_t inc16 = (~op & 0xFFFFu) + np;  // ChecksumIncrement16
+  if (proto == 6 || proto == 17) {
+    f.put16(l4 + (dir == 0 ? 0 : 2), np);
+    if (proto == 6) {
+      f.put16(l4 + 16, upd_ck(f.u16(l4 + 16), l3 + inc16));
+    } else {
+      const uint32_t ck = f.u16(l4 + 6);
+      if (ck != 0) {
+        const uint32_t nck = upd_ck(ck, l3 + inc16);
+        f.put16(l4 + 6, nck ? nck : 0xFFFFu);
+      }
+    }
+  } else {  // ICMP: ident, checksum over the ICMP message only
+    f.put16(l4 + 4, np);
+    f.put16(l4 + 2, upd_ck(f.u16(l4 + 2), inc16));
+  }
+}
+
+__device__ __forceinline__ GlobalFrame frame_of(const DnatArgs &a, uint64_t i) {
+  GlobalFrame f;
+  f.p = a.frames + i * a.stride;
+  f.lim = (uint32_t)(a.stride < 4096 ? a.stride : 4096);
+  return f;
 }
 
 __global__ __launch_bounds__(kNatBlock) void dnat_find_kernel(DnatArgs a) {
   const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
-  const uint32_t *tags = reinterpret_cast<const uint32_t *>(a.t.base);
-  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
-  const uint32_t *vals = reinterpret_cast<const uint32_t *>(a.t.base + a.t.vals_off);
   for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < a.n;
        i += step) {
-    const uint8_t *ip = a.frames + i * a.stride + 14;
-    const uint64_t key = endpoint(ip, a.dir);
+    const uint64_t key = endpoint(frame_of(a, i), a.dir);
     a.keys[i] = key;
     uint32_t r = kDnatInvalid;
     if (key != ~0ull) {
-      r = kDnatMiss;
-      const Probe p = split_hash(hash_words(&key, 1, a.t.seed), 1, a.t.nbp);
-      uint32_t c = tag_match(tags[p.b1], p.tag) | (tag_match(tags[p.b2], p.tag) << 4);
-      while (c) {
-        const int s = __builtin_ctz(c);
-        c &= c - 1;
-        const uint32_t slot = (s < 4 ? p.b1 : p.b2) * kSlots + (s & 3);
-        if (keys[slot] == key) {
-          r = vals[slot];
-          break;
-        }
-      }
+      r = lookup(a, key);
       // a forward miss needs a new mapping (CreateNewEntry); a reverse
       // miss is dropped
       if (r == kDnatMiss && a.dir == 0) atomicAdd(a.nmiss, 1u);
@@ -91,45 +186,127 @@ __global__ __launch_bounds__(kNatBlock) void dnat_find_kernel(DnatArgs a) {
   }
 }
 
+// Rewrites packets from entry indices: every packet of the batch (n > 0,
+// res[i] per packet) or, with a.list, the nlist packets idx[k] = res[k]
+// with entries mres[k] and endpoints keys[k].
 __global__ __launch_bounds__(kNatBlock) void dnat_apply_kernel(DnatArgs a) {
   const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < a.n;
-       i += step) {
-    const uint32_t e = a.res[i];
+  const uint64_t cnt = a.list ? a.nlist : a.n;
+  for (uint64_t k = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; k < cnt;
+       k += step) {
+    const uint64_t i = a.list ? a.res[k] : k;
+    const uint32_t e = a.list ? a.mres[k] : a.res[k];
     if (e >= kDnatInvalid || e >= a.nent) {  // drop codes (bound: never)
       a.out[i] = kDropGate;
       continue;
     }
     if (a.refresh) a.ts[e] = a.now;  // forward packets only (rfc4787 REQ-6)
-    uint8_t *ip = a.frames + i * a.stride + 14;
-    uint8_t *l4 = ip + ((ip[0] & 0x0Fu) << 2);
-    const uint64_t before = a.keys[i], after = a.ent[e];
-    const uint32_t oa = (uint32_t)before, na = (uint32_t)after;
-    const uint32_t op = (uint32_t)(before >> 32) & 0xFFFFu, np = (uint32_t)(after >> 32) & 0xFFFFu;
-    const uint32_t proto = ip[9];
-    uint8_t *pa = ip + (a.dir == 0 ? 12 : 16);
-    st_u16(pa, na & 0xFFFFu);
-    st_u16(pa + 2, na >> 16);
-    // ChecksumIncrement32(before.addr, after.addr)
-    const uint32_t l3 = (~oa >> 16) + (~oa & 0xFFFFu) + (na >> 16) + (na & 0xFFFFu);
-    st_u16(ip + 10, upd_ck(ld_u16(ip + 10), l3));
-    const uint32_t inc16 = (~op & 0xFFFFu) + np;  // ChecksumIncrement16
-    if (proto == 6 || proto == 17) {
-      st_u16(l4 + (a.dir == 0 ? 0 : 2), np);
-      if (proto == 6) {
-        st_u16(l4 + 16, upd_ck(ld_u16(l4 + 16), l3 + inc16));
-      } else {
-        const uint32_t ck = ld_u16(l4 + 6);
-        if (ck != 0) {
-          const uint32_t nck = upd_ck(ck, l3 + inc16);
-          st_u16(l4 + 6, nck ? nck : 0xFFFFu);
-        }
-      }
-    } else {  // ICMP: ident, checksum over the ICMP message only
-      st_u16(l4 + 4, np);
-      st_u16(l4 + 2, upd_ck(ld_u16(l4 + 2), inc16));
-    }
+    stamp(frame_of(a, i), a.keys[k], a.ent[e], a.dir);
     a.out[i] = a.dir == 0 ? 1 : 0;
+  }
+}
+
+// One packet's whole decision when no mapping can be evicted by this batch
+// (bg_dnat_process): lookup; a hit is stamped and its forward timestamp
+// refreshed; an invalid protocol or a reverse miss drops; a forward miss is
+// appended to the miss list (wave-aggregated) for the host's in-order
+// CreateNewEntry walk.
+template <class F>
+__device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
+                                          uint64_t i, bool live) {
+  uint64_t key = ~0ull;
+  SlotHit h;
+  h.slot = ~0u;
+  if (live) {
+    key = endpoint(f, a.dir);
+    if (key != ~0ull) h = lookup_hit(a, key);
+  }
+  const bool fmiss = live && key != ~0ull && h.slot == ~0u && a.dir == 0;
+  const uint64_t m = __ballot(fmiss);
+  if (m) {
+    const int lead = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == lead) base = atomicAdd(a.nmiss, (uint32_t)__popcll(m));
+    base = __shfl(base, lead);
+    if (fmiss) {
+      const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(m >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      a.res[pos] = (uint32_t)i;
+      a.keys[pos] = key;
+    }
+  }
+  if (!live) return;
+  if (h.slot == ~0u) {
+    a.out[i] = kDropGate;  // the host's walk decides forward misses
+    return;
+  }
+  stamp(f, key, h.ep, a.dir);
+  a.out[i] = a.dir == 0 ? 1 : 0;
+  // forward timestamp refresh. A scattered 8-byte store is a partial-line
+  // write; an entry an earlier packet of the flow already stamped with
+  // `now` is left alone (measured: 0.73-0.80 -> 0.69 ms per 16 M packets)
+  if (a.dir == 0 && a.ts[h.entry] != a.now) a.ts[h.entry] = a.now;
+}
+
+// any stride: lane = packet, header bytes straight from HBM
+__global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
+  const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
+  const uint64_t n_pad = (a.n + 63) & ~63ull;  // whole waves reach the ballot
+  for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < n_pad;
+       i += step)
+    fused_one(a, frame_of(a, i < a.n ? i : 0), i, i < a.n);
+}
+
+// dense 64-byte slots: a wave's 64 slots (4 KB) come in with lane-contiguous
+// 16-byte loads into its swizzled LDS stage (next tile in flight), each lane
+// decides and stamps its slot in LDS, and the tile goes back whole with
+// lane-contiguous 16-byte stores (no partial-line writes).
+constexpr int kNatSlabBlock = 512;
+__global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kWaves = kNatSlabBlock / 64;
+  uint4 *stage = reinterpret_cast<uint4 *>(lds) + wid * 256;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  uint4 *src = reinterpret_cast<uint4 *>(a.frames);
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  uint4 v[4];
+  auto units_of = [&](uint64_t tile) {
+    const uint64_t p0 = tile * 64;
+    return (uint32_t)((a.n - p0 < 64 ? a.n - p0 : 64) * 4);
+  };
+  auto load_tile = [&](uint64_t tile) {
+    const uint32_t units = units_of(tile);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      v[c] = u < units ? ld_stream(src + tile * 256 + u) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  StageSlot me;
+  me.stage = reinterpret_cast<uint8_t *>(stage);
+  me.slot = (uint32_t)lane;
+  if (t < ntiles) load_tile(t);
+  for (; t < ntiles; t += nwaves) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      stage[(u >> 2) * 4 + (((u & 3) + (u >> 4)) & 3)] = v[c];
+    }
+    lds_fence();
+    const uint32_t units = units_of(t);
+    if (t + nwaves < ntiles) load_tile(t + nwaves);
+    const uint64_t idx = t * 64 + lane;
+    fused_one(a, me, idx, idx < a.n);
+    lds_fence();
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t u = c * 64 + lane;
+      if (u < units) src[t * 256 + u] = stage[(u >> 2) * 4 + (((u & 3) + (u >> 4)) & 3)];
+    }
+    lds_fence();  // stage reads retire before the next tile's writes
   }
 }
 
@@ -149,8 +326,29 @@ hipError_t launch_dnat_find(const DnatArgs &a, int num_cus, hipStream_t s) {
 }
 
 hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s) {
+  const uint64_t cnt = a.list ? a.nlist : a.n;
+  if (cnt == 0) return hipSuccess;
+  hipLaunchKernelGGL(dnat_apply_kernel, dim3((unsigned)grid_of(cnt, num_cus)),
+                     dim3(kNatBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(dnat_apply_kernel, dim3((unsigned)grid_of(a.n, num_cus)),
+  if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 && !getenv("BG_NO_SLAB")) {
+    const size_t lds = (size_t)(kNatSlabBlock / 64) * 4096;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, reinterpret_cast<const void *>(dnat_fused_slab_kernel),
+            kNatSlabBlock, lds) != hipSuccess || occ <= 0)
+      occ = 1;
+    const uint64_t need = (a.n + kNatSlabBlock - 1) / kNatSlabBlock;
+    const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
+    hipLaunchKernelGGL(dnat_fused_slab_kernel, dim3((unsigned)blocks),
+                       dim3(kNatSlabBlock), lds, s, a);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(dnat_fused_kernel, dim3((unsigned)grid_of(a.n, num_cus)),
                      dim3(kNatBlock), 0, s, a);
   return hipGetLastError();
 }

@@ -3,19 +3,27 @@
 // The NAT map (core/modules/nat.h:129-175: endpoint -> NatEntry, forward and
 // reverse entries) lives on the host, where new mappings are made; the
 // device keeps a lookup copy (bg_table.h image, entry index values), the
-// entries' translated endpoints and their forward timestamps. A batch:
-//   1. dnat_find_kernel: endpoint + lookup per packet, forward misses counted;
-//   2. no forward miss (the steady state): dnat_apply_kernel rewrites every
-//      packet from its lookup result and refreshes forward timestamps;
-//   3. otherwise the batch is decided on the host in packet order --
-//      CreateNewEntry (nat.cc:180-258) draws ports from the module's Random
-//      and may evict expired mappings that later packets of the same batch
-//      would have hit -- with the device's timestamps read back first; the
-//      device copy is rebuilt, and dnat_apply_kernel rewrites the packets
-//      from the host's per-packet decisions.
+// entries' translated endpoints and their forward timestamps.
+// CreateNewEntry (nat.cc:180-258) draws ports from the module's Random and
+// may evict an expired mapping that a later packet of the same batch would
+// have hit. The host tracks bounds on the forward timestamps, so it knows
+// when no mapping can expire at `now` (and reverse traffic never creates
+// one). Then a batch is
+//   1. dnat_fused_kernel (dnat_fused_slab_kernel for 64-byte slots): lookup
+//      and Stamp of every hit in one pass over the header line, forward
+//      timestamps refreshed, forward misses listed;
+//   2. only if the list is not empty: the misses walked in packet order on
+//      the host (find or CreateNewEntry), the device copy rebuilt, and
+//      dnat_apply_kernel stamps the listed packets.
+// When a mapping may expire, the whole batch is classified first
+// (dnat_find_kernel); with no forward miss dnat_apply_kernel rewrites it,
+// otherwise every packet is decided on the host in packet order, with the
+// device's timestamps read back first, and dnat_apply_kernel rewrites the
+// batch from the host's decisions.
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -73,18 +81,22 @@ struct bg_dnat {
   std::unordered_map<uint64_t, uint32_t> map;
   std::vector<uint64_t> ent_ep, ent_ts;
   std::vector<uint32_t> free_idx;
+  std::vector<uint8_t> ent_fwd;  // live forward entry (its ts can expire)
+  // bounds on the forward entries' timestamps: lb exact after every host
+  // walk (device refreshes only raise them), ub = the latest `now` seen
+  uint64_t ts_lb = ~0ull, ts_ub = 0;
   bool dirty = true;
   int device = -1;
   DevTable dev;
   uint64_t *d_ent = nullptr, *d_ts = nullptr;
   size_t d_cap = 0;  // entries the device arrays hold
   uint64_t *d_keys = nullptr;
-  uint32_t *d_res = nullptr, *d_nmiss = nullptr;
+  uint32_t *d_res = nullptr, *d_nmiss = nullptr, *d_mres = nullptr;
   size_t d_n = 0;
   std::mutex mu;
   ~bg_dnat() {
     for (void *p : {(void *)d_ent, (void *)d_ts, (void *)d_keys, (void *)d_res,
-                    (void *)d_nmiss})
+                    (void *)d_nmiss, (void *)d_mres})
       if (p) (void)hipFree(p);
   }
 
@@ -100,10 +112,12 @@ struct bg_dnat {
       free_idx.pop_back();
       ent_ep[idx] = ep;
       ent_ts[idx] = 0;
+      ent_fwd[idx] = 0;
     } else {
       idx = (uint32_t)ent_ep.size();
       ent_ep.push_back(ep);
       ent_ts.push_back(0);
+      ent_fwd.push_back(0);
     }
     map.emplace(key, idx);
     dirty = true;
@@ -113,6 +127,7 @@ struct bg_dnat {
     auto it = map.find(key);
     if (it == map.end()) return;
     free_idx.push_back(it->second);
+    ent_fwd[it->second] = 0;
     map.erase(it);
     dirty = true;
   }
@@ -170,7 +185,9 @@ struct bg_dnat {
         }
         if (take) {
           insert(ext_ep, in);
-          return insert(in, ext_ep);
+          const uint32_t e = insert(in, ext_ep);
+          ent_fwd[e] = 1;
+          return e;
         }
         port++;
         trials++;
@@ -182,13 +199,30 @@ struct bg_dnat {
 
   int ensure_batch(size_t n) {
     if (n <= d_n) return 0;
-    for (void *p : {(void *)d_keys, (void *)d_res})
+    for (void *p : {(void *)d_keys, (void *)d_res, (void *)d_mres})
       if (p) (void)hipFree(p);
     d_n = std::max<size_t>(n, 4096);
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_keys), d_n * 8));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_res), d_n * 4));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_mres), d_n * 4));
     if (!d_nmiss) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_nmiss), 4));
     return 0;
+  }
+
+  // Can CreateNewEntry evict a mapping at `now`? Only a forward entry with
+  // now - ts > kTimeOutNs (u64 arithmetic, nat.cc:217) can go; with every
+  // forward ts in [lb, ub], none can when ub <= now and now - lb <= timeout.
+  bool may_evict(uint64_t now) const {
+    if (ts_lb == ~0ull) return false;  // no forward entry
+    return now < ts_ub || now - ts_lb > kTimeOutNs;
+  }
+  void exact_bounds() {  // host timestamps are exact here
+    ts_lb = ~0ull;
+    for (size_t e = 0; e < ent_fwd.size(); e++)
+      if (ent_fwd[e]) {
+        ts_lb = std::min(ts_lb, ent_ts[e]);
+        ts_ub = std::max(ts_ub, ent_ts[e]);
+      }
   }
 
   // device copy of the map, entries and timestamps
@@ -198,13 +232,14 @@ struct bg_dnat {
     if (r) return r;
     std::vector<uint64_t> keys, hashes;
     std::vector<uint8_t> vals, img;
-    for (auto &kv : map) {
+    for (auto &kv : map) {  // key words: the endpoint, its translation
       keys.push_back(kv.first);
+      keys.push_back(ent_ep[kv.second]);
       hashes.push_back(hash_words(&kv.first, 1, kDefaultSeed));
       for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(kv.second >> (8 * b)));
     }
     TableLayout L;
-    r = build_image(1, 4, 1, keys, vals, hashes, &img, &L);
+    r = build_image(2, 4, 1, keys, vals, hashes, &img, &L);
     if (r) return r;
     r = dev.upload(dev_id, img, L, s);
     if (r) return r;
@@ -302,10 +337,66 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.out = d_out;
   HIP_TRY(hipMemsetAsync(h->d_nmiss, 0, 4, s));
   const int ncu = num_cus(dev);
+  if (dir == 1 || !h->may_evict(now)) {
+    // Nothing this batch creates can change another packet's mapping, so
+    // hits are final: one pass stamps them and lists the forward misses.
+    // Reverse traffic never creates a mapping (a miss drops).
+    HIP_TRY(launch_dnat_fused(a, ncu, s));
+    if (dir == 1) return 0;
+    h->ts_ub = std::max(h->ts_ub, now);
+    uint32_t nmiss = 0;
+    HIP_TRY(hipMemcpyAsync(&nmiss, h->d_nmiss, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (nmiss == 0) return 0;
+    // new flows: CreateNewEntry in packet order on the host
+    std::vector<uint32_t> idx(nmiss), ent(nmiss);
+    std::vector<uint64_t> key(nmiss);
+    HIP_TRY(hipMemcpyAsync(idx.data(), h->d_res, nmiss * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(key.data(), h->d_keys, nmiss * 8, hipMemcpyDeviceToHost, s));
+    if (!h->ent_ts.empty())  // forward refreshes made on the device
+      HIP_TRY(hipMemcpyAsync(h->ent_ts.data(), h->d_ts, h->ent_ts.size() * 8,
+                             hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint32_t> ord(nmiss);
+    for (uint32_t k = 0; k < nmiss; k++) ord[k] = k;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
+    std::vector<uint32_t> sidx(nmiss);
+    std::vector<uint64_t> skey(nmiss);
+    for (uint32_t k = 0; k < nmiss; k++) {
+      sidx[k] = idx[ord[k]];
+      skey[k] = key[ord[k]];
+      int64_t e = h->find(skey[k]);
+      if (e < 0) e = h->create(skey[k], now);
+      if (e >= 0) h->ent_ts[e] = now;
+      ent[k] = e < 0 ? kDnatMiss : (uint32_t)e;
+    }
+    h->exact_bounds();
+    h->dirty = true;
+    r = h->sync(dev, s);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(h->d_res, sidx.data(), nmiss * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(h->d_keys, skey.data(), nmiss * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(h->d_mres, ent.data(), nmiss * 4, hipMemcpyHostToDevice, s));
+    a.t = h->dev.ref();
+    a.ent = h->d_ent;
+    a.ts = h->d_ts;
+    a.nent = h->ent_ep.size();
+    a.refresh = 0;
+    a.list = 1;
+    a.nlist = nmiss;
+    a.mres = h->d_mres;
+    HIP_TRY(launch_dnat_apply(a, ncu, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the host vectors outlive the copies
+    return 0;
+  }
+  // An expired mapping may be evicted by a new flow, which changes what a
+  // later packet of the batch maps to: classify first, and if any forward
+  // packet misses, decide the whole batch in packet order on the host.
   HIP_TRY(launch_dnat_find(a, ncu, s));
   uint32_t nmiss = 0;
   HIP_TRY(hipMemcpyAsync(&nmiss, h->d_nmiss, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  h->ts_ub = std::max(h->ts_ub, now);
   if (nmiss == 0) {  // every valid packet has a mapping
     a.refresh = dir == 0;
     HIP_TRY(launch_dnat_apply(a, ncu, s));
@@ -323,7 +414,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   for (size_t i = 0; i < n; i++) {
     if (res[i] == kDnatInvalid) continue;  // DropPacket
     int64_t e = h->find(keys[i]);
-    if (e < 0 && dir == 0) e = h->create(keys[i], now);
+    if (e < 0) e = h->create(keys[i], now);
     if (e < 0) {
       res[i] = kDnatMiss;  // DropPacket
       continue;
@@ -331,6 +422,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
     if (dir == 0) h->ent_ts[e] = now;
     res[i] = (uint32_t)e;
   }
+  h->exact_bounds();
   h->dirty = true;  // timestamps (and maybe entries) changed
   r = h->sync(dev, s);
   if (r) return r;

@@ -206,6 +206,11 @@ struct DnatArgs {
   uint64_t *ts;      // per entry: last_refresh
   uint64_t nent;     // entries the two arrays hold
   uint16_t *out;
+  // apply over a packet list: res[k] = packet, mres[k] = entry, keys[k] =
+  // its endpoint, k < nlist (the fused kernel's forward misses)
+  uint32_t list;
+  uint64_t nlist;
+  const uint32_t *mres;
 };
 
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
@@ -221,6 +226,9 @@ hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_encap(const EncapArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_dnat_find(const DnatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s);
+// lookup + stamp in one pass; forward misses listed in res/keys (count in
+// *nmiss) -- only when the batch cannot evict a mapping
+hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword

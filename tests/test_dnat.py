@@ -38,10 +38,12 @@ def flows(n, rng):
     return src, port, proto, itype
 
 
-def frames(src, sport, dst, dport, proto, itype, rng, ihl=None):
-    """Eth / IPv4 (IHL 5..7) / TCP, UDP or ICMP; valid checksums"""
+def frames(src, sport, dst, dport, proto, itype, rng, ihl=None, stride=STRIDE):
+    """Eth / IPv4 (IHL 5..7) / TCP, UDP or ICMP; valid checksums. In 64-byte
+    slots the L4 payload is empty, so every frame fits its slot."""
     n = len(src)
-    f = np.zeros((n, STRIDE), np.uint8)
+    f = np.zeros((n, stride), np.uint8)
+    extra = 16 if stride > 64 else 0
     f[:, 12:14] = [0x08, 0x00]
     if ihl is None:
         ihl = np.where(rng.random(n) < 0.8, 5, rng.integers(6, 8, n))
@@ -50,7 +52,7 @@ def frames(src, sport, dst, dport, proto, itype, rng, ihl=None):
     for i in range(n):
         o = 14 + 20
         f[i, o:l4[i]] = rng.integers(0, 256, l4[i] - o)  # options
-        pl = {6: 20, 17: 8, 1: 8}.get(int(proto[i]), 8) + 16
+        pl = {6: 20, 17: 8, 1: 8}.get(int(proto[i]), 8) + extra
         iplen = 4 * ihl[i] + pl
         f[i, 16:18] = [iplen >> 8, iplen & 255]
         f[i, 18:20] = rng.integers(0, 256, 2)
@@ -71,7 +73,7 @@ def frames(src, sport, dst, dport, proto, itype, rng, ihl=None):
             f[i, L] = itype[i]
             f[i, L + 2:L + 4] = rng.integers(0, 256, 2)  # checksum: any
             f[i, L + 4:L + 6] = [sport[i] >> 8, sport[i] & 255]  # ident
-    O.cksum_process(f, STRIDE, n, 3, False)
+    O.cksum_process(f, stride, n, 3, False)
     udp0 = np.nonzero((proto == 17) & (rng.random(n) < 0.1))[0]
     for i in udp0:  # UDP checksum 0: left alone
         f[i, l4[i] + 6:l4[i] + 8] = 0
@@ -126,19 +128,26 @@ def test_oracle_translation_keeps_checksums_valid():
 
 
 @pytest.mark.gpu
-def test_gpu_batches_vs_oracle():
+@pytest.mark.parametrize("stride", [STRIDE, 64])
+def test_gpu_batches_vs_oracle(stride):
+    """stride 64 runs the slab kernel (dnat_fused_slab_kernel); batches
+    where no mapping can expire take the fused path (new flows listed and
+    walked on the host, mixed with hits), the batch 301 s later the
+    classify-then-decide path"""
+    import functools
     import torch
     from bess_amd.modules import NAT
     rng = np.random.default_rng(11)
     m, o = NAT(ext_addrs=EXT, seed=0xABC), OM.OracleNAT(ext_addrs=EXT, seed=0xABC)
+    frames_ = functools.partial(frames, stride=stride)
 
     def run(f, igate, now):
         ref = f.copy()
-        want = o.process(ref, STRIDE, len(f), igate, now)
+        want = o.process(ref, stride, len(f), igate, now)
         d = torch.from_numpy(f.reshape(-1).copy()).cuda()
         og = torch.zeros(len(f), dtype=torch.int16, device="cuda")
-        m.process_device(d, STRIDE, len(f), og, now, igate=igate)
-        got = d.cpu().numpy().reshape(len(f), STRIDE)
+        m.process_device(d, stride, len(f), og, now, igate=igate)
+        got = d.cpu().numpy().reshape(len(f), stride)
         assert (og.cpu().numpy().view(np.uint16) == want).all()
         bad = np.nonzero((got != ref).any(1))[0]
         assert len(bad) == 0, bad[:5]
@@ -150,24 +159,29 @@ def test_gpu_batches_vs_oracle():
     pick = rng.integers(0, 1500, n)
     dst = rng.integers(1, 1 << 32, n)
     dport = rng.integers(1, 65536, n)
-    fa = frames(s[pick], p[pick], dst, dport, pr[pick], it[pick], rng)
+    fa = frames_(s[pick], p[pick], dst, dport, pr[pick], it[pick], rng)
     ga, out_a = run(fa, 0, T0)                            # new flows (host walk)
     mapped = out_a == 1
     assert 0.5 < mapped.mean() < 1.0 and int(m.desc().split()[0]) > 500
     run(fa[mapped], 0, T0 + 1000)                         # established: device only
+    s3, p3, pr3, it3 = flows(800, rng)                    # hits mixed with new flows
+    fc = frames_(s3, p3, rng.integers(1, 1 << 32, 800), rng.integers(1, 65536, 800),
+                 pr3, it3, rng)
+    mix = np.concatenate([fa[mapped][:1200], fc])
+    run(mix[rng.permutation(len(mix))], 0, T0 + 1500)
     ea, ep = ext_side(ga[mapped])                         # reverse traffic
     k = int(mapped.sum())
     prm = pr[pick][mapped]
     # reverse endpoint: (dst, dst port) for TCP/UDP, (dst, ident) for ICMP
-    rev = frames(dst[mapped], np.where(prm == 1, ep, dport[mapped]), ea, ep, prm,
+    rev = frames_(dst[mapped], np.where(prm == 1, ep, dport[mapped]), ea, ep, prm,
                  it[pick][mapped], rng)
-    unk = frames(rng.integers(1, 1 << 32, 500), rng.integers(1, 65536, 500),
+    unk = frames_(rng.integers(1, 1 << 32, 500), rng.integers(1, 65536, 500),
                  rng.integers(1, 1 << 32, 500), rng.integers(1, 65536, 500),
                  np.full(500, 6), np.zeros(500, int), rng)
     run(np.concatenate([rev, unk]), 1, T0 + 2000)         # reverse hits + drops
     # 301 s later: new flows evict expired mappings where ports collide
     s2, p2, pr2, it2 = flows(3000, rng)
-    fb = frames(s2, p2, rng.integers(1, 1 << 32, 3000), rng.integers(1, 65536, 3000),
+    fb = frames_(s2, p2, rng.integers(1, 1 << 32, 3000), rng.integers(1, 65536, 3000),
                 pr2, it2, rng)
     run(fb, 0, T0 + 301 * 10**9)
     run(rev[:2000], 1, T0 + 302 * 10**9)                  # some mappings now gone
