@@ -783,7 +783,7 @@ def run_dnat(args, dev, torch):
                         "%d pkts per call over %d mappings" % (n, nflow),
             "pkts": n, "ms_per_step": round(ms, 4),
             "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-            "roofline": _roof(130, n, ms),
+            "roofline": _roof(130, n, ms, "dnat"),
             "note": "per call: fused lookup+rewrite kernel (64 B slab), "
                     "4-byte miss count read back",
             "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
