@@ -246,7 +246,8 @@ __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
   // forward timestamp refresh. A scattered 8-byte store is a partial-line
   // write; an entry an earlier packet of the flow already stamped with
   // `now` is left alone (measured: 0.73-0.80 -> 0.69 ms per 16 M packets)
-  if (a.dir == 0 && a.ts[h.entry] != a.now) a.ts[h.entry] = a.now;
+  // (a.ts is null only under the BG_NAT_AB_NOTS measurement knob)
+  if (a.dir == 0 && a.ts && a.ts[h.entry] != a.now) a.ts[h.entry] = a.now;
 }
 
 // any stride: lane = packet, header bytes straight from HBM
@@ -333,8 +334,12 @@ hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s) {
-  if (a.n == 0) return hipSuccess;
+hipError_t launch_dnat_fused(const DnatArgs &a0, int num_cus, hipStream_t s) {
+  if (a0.n == 0) return hipSuccess;
+  DnatArgs a = a0;
+  // measurement only: skip the forward timestamp refresh (breaks parity;
+  // scripts A/B the cost of the dependent ts read)
+  if (getenv("BG_NAT_AB_NOTS")) a.ts = nullptr;
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 && !getenv("BG_NO_SLAB")) {
     const size_t lds = (size_t)(kNatSlabBlock / 64) * 4096;
     int occ = 0;
@@ -342,6 +347,7 @@ hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s) {
             &occ, reinterpret_cast<const void *>(dnat_fused_slab_kernel),
             kNatSlabBlock, lds) != hipSuccess || occ <= 0)
       occ = 1;
+    if (const char *e = getenv("BG_NAT_OCC")) occ = std::max(1, atoi(e));  // A/B knob
     const uint64_t need = (a.n + kNatSlabBlock - 1) / kNatSlabBlock;
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
     hipLaunchKernelGGL(dnat_fused_slab_kernel, dim3((unsigned)blocks),
