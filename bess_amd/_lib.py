@@ -14,6 +14,10 @@ BG_DROP_GATE = 8192
 BG_GATE_NONE = 0xFFFF
 BG_CK_IP = 1
 BG_CK_L4 = 2
+BG_PATH_FORCE_LDS = 1
+BG_PATH_NO_LDS = 2
+BG_PATH_NO_SLAB = 4
+BG_PATH_WM_NO_TAGS = 8
 KEY_BYTES = 64
 
 
@@ -79,6 +83,9 @@ _SIGS = {
     "bg_module_command": (_int, [_vp, C.c_char_p, _vp, _sz, _vp,
                                  C.POINTER(_sz)]),
     "bg_module_process": (_int, [_vp, _vp, _sz, _vp]),
+    "bg_module_process_batches": (_int, [_vp, _vp, _sz, _vp, _vp, _vp, _vp,
+                                         C.POINTER(_sz), C.POINTER(_sz)]),
+    "bg_module_connect": (_int, [_vp, _u16, _int]),
     "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
     "bg_module_set_device": (_int, [_vp, _int]),
     "bg_module_set_igate": (_int, [_vp, _u16]),
@@ -86,6 +93,9 @@ _SIGS = {
     "bg_em_bind_meta": (_int, [_vp, _int, _vp, _int]),
     "bg_wm_bind_meta": (_int, [_vp, _int, _vp, _int]),
     "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
+    "bg_set_path_flags": (_int, [C.c_uint32]),
+    "bg_get_path_flags": (C.c_uint32, []),
+    "bg_is_ab_build": (_int, []),
     "bg_debug_key": (_int, [C.POINTER(bg_field), _int, _int, _vp, _vp]),
     "bg_em_classify_window": (_int, [_vp, _vp, _sz, _sz, _int, _u16, _vp, _vp]),
     "bg_em_window": (None, [_vp, C.POINTER(_int), C.POINTER(_int)]),
@@ -153,6 +163,24 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+class kernel_paths:
+    """Context manager: run the enclosed calls with bg_set_path_flags(flags)
+    (which of several result-identical kernels serve them), restoring the
+    previous flags afterwards."""
+
+    def __init__(self, flags):
+        self.flags = flags
+
+    def __enter__(self):
+        self.old = lib().bg_get_path_flags()
+        check(lib().bg_set_path_flags(self.flags))
+        return self
+
+    def __exit__(self, *exc):
+        lib().bg_set_path_flags(self.old)
+        return False
 
 
 def check(rc):

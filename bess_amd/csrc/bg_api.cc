@@ -16,6 +16,7 @@
 #include "../../include/bessgpu.h"
 #include "bg_internal.h"
 #include "bg_kernels.h"
+#include "bg_launch.h"
 #include "bg_table.h"
 
 namespace bg {
@@ -33,16 +34,15 @@ int fail(int code, const char *fmt, ...) {
 }
 
 int num_cus(int device) {
-  static std::mutex mu;
-  static std::unordered_map<int, int> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = cache.find(device);
-  if (it != cache.end()) return it->second;
-  int v = 0;
+  // launch path: a lock-free per-device cache (the answer never changes)
+  static std::atomic<int> cache[64];
+  if (device < 0 || device >= 64) return 256;
+  int v = cache[device].load(std::memory_order_relaxed);
+  if (v > 0) return v;
   if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount,
                             device) != hipSuccess || v <= 0)
     v = 256;
-  cache[device] = v;
+  cache[device].store(v, std::memory_order_relaxed);
   return v;
 }
 
@@ -325,6 +325,25 @@ int Staging::ensure(int dev, size_t in_bytes, size_t out_bytes) {
   return 0;
 }
 
+namespace {
+struct ThreadStage {
+  Staging st;
+  hipStream_t streams[16] = {};
+};
+thread_local ThreadStage t_stage;
+}  // namespace
+
+Staging &thread_staging() { return t_stage.st; }
+
+hipStream_t thread_stream(int device, hipStream_t given) {
+  if (given) return given;
+  if (device < 0 || device >= 16) return nullptr;
+  hipStream_t &s = t_stage.streams[device];
+  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+    s = nullptr;  // fall back to the legacy stream
+  return s;
+}
+
 void Staging::release() {
   if (h_in) (void)hipHostFree(h_in);
   if (d_in) (void)hipFree(d_in);
@@ -352,12 +371,13 @@ struct bg_em {
   uint32_t raw_size = 0;  // raw_key_size_ (sum of field sizes)
   uint32_t kw = 1;        // device key words (1, 2, 4, 8)
   std::unordered_map<Key, uint16_t, KeyHash> rules;
-  bool dirty = true;
+  // set by rule changes (THREAD_UNSAFE commands, workers paused); cleared,
+  // after the device image is published, by the sync that rebuilt it
+  std::atomic<bool> dirty{true};
   DevTable dev;
-  Staging stage;
   TableLayout planned;  // sharded build
   bool planned_valid = false;
-  std::mutex mu;  // serialises sync/staging (lookups from many workers)
+  std::mutex mu;  // serialises sync (lookups from many workers never lock)
 };
 
 static Key em_key(const bg_em *em, const uint8_t *key) {
@@ -439,7 +459,6 @@ int bg_em_create(const bg_field *fields, int nfields, bg_em **out) {
 void bg_em_destroy(bg_em *em) {
   if (!em) return;
   em->dev.release();
-  em->stage.release();
   delete em;
 }
 
@@ -497,13 +516,10 @@ static void em_entries(const bg_em *em, std::vector<uint64_t> *keys,
   }
 }
 
-// the gate fits in the key's unused top bytes (A/B knob BG_EM_VIK=0)
+// the gate fits in the key's unused top bytes (A/B knob BG_EM_VIK=0 of
+// libbessgpu_ab.so)
 static bool em_vik(const bg_em *em) {
-  static const bool on = [] {
-    const char *e = getenv("BG_EM_VIK");
-    return !(e && *e && atoi(e) == 0);
-  }();
-  return on && em->raw_size + 2 <= em->kw * 8;
+  return knob("BG_EM_VIK", 1) && em->raw_size + 2 <= em->kw * 8;
 }
 
 static int em_sync_locked(bg_em *em, int device, hipStream_t s) {
@@ -521,6 +537,10 @@ static int em_sync_locked(bg_em *em, int device, hipStream_t s) {
 }
 
 int bg_em_sync(bg_em *em, int device, bg_stream_t stream) {
+  // fast path for the per-batch calls of many workers: no lock
+  if (!em->dirty.load(std::memory_order_acquire) && em->dev.valid &&
+      em->dev.device == device)
+    return 0;
   std::lock_guard<std::mutex> lk(em->mu);
   return em_sync_locked(em, device, (hipStream_t)stream);
 }
@@ -617,16 +637,15 @@ int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   if (int r = check_extent(em->dfields, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
-  int dev = em->dev.valid ? em->dev.device : 0;
-  if (!em->dev.valid || em->dirty) {
+  // acquire: a clean flag publishes the device image the sync built
+  if (em->dirty.load(std::memory_order_acquire) || !em->dev.valid) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     std::lock_guard<std::mutex> lk(em->mu);
     int r = em_sync_locked(em, em->dev.valid ? em->dev.device : cur, s);
     if (r) return r;
-    dev = em->dev.device;
   }
-  int r = set_device(dev);
+  int r = set_device(em->dev.device);
   if (r) return r;
   return em_launch(em, d_frames, stride, n, default_gate, d_gates, -win_off, s);
 }
@@ -636,6 +655,7 @@ int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
 static int stage_windows(const std::vector<bg_field> &fields,
                          const uint8_t *const *heads, size_t n, Staging &st,
                          int dev, int *shift, size_t *wstride) {
+  // +64 B: the last window's 16-byte loads may run past its slot
   int lo = 1 << 30, hi = 0;
   for (auto &f : fields) {
     lo = std::min(lo, f.offset);
@@ -643,7 +663,7 @@ static int stage_windows(const std::vector<bg_field> &fields,
   }
   if (fields.empty()) lo = hi = 0;
   const size_t w = std::max<size_t>(16, (size_t)(hi - lo + 15) / 16 * 16);
-  int r = st.ensure(dev, n * w, n * 2);
+  int r = st.ensure(dev, n * w + 64, n * 2);
   if (r) return r;
   for (size_t i = 0; i < n; i++)
     memcpy(st.h_in + i * w, heads[i] + lo, (size_t)(hi - lo));
@@ -652,31 +672,39 @@ static int stage_windows(const std::vector<bg_field> &fields,
   return 0;
 }
 
+// Many workers may call this on one table at once (core/module.h:485,
+// exact_match.h:55): each calling thread stages into its own pinned buffers
+// and, unless it passes a stream, runs on its own HIP stream; the table lock
+// is taken only when the device image must be (re)built.
 int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
                        uint16_t default_gate, uint16_t *gates,
                        bg_stream_t stream) {
   if (em->has_attr) return no_attr_datapath();
   if (n == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  std::lock_guard<std::mutex> lk(em->mu);
-  int cur = 0;
-  (void)hipGetDevice(&cur);
-  int dev = em->dev.valid ? em->dev.device : cur;
-  int r = em_sync_locked(em, dev, s);
+  if (em->dirty.load(std::memory_order_acquire) || !em->dev.valid) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    std::lock_guard<std::mutex> lk(em->mu);
+    int r = em_sync_locked(em, em->dev.valid ? em->dev.device : cur,
+                           thread_stream(cur, (hipStream_t)stream));
+    if (r) return r;
+  }
+  const int dev = em->dev.device;
+  int r = set_device(dev);
   if (r) return r;
+  hipStream_t s = thread_stream(dev, (hipStream_t)stream);
+  Staging &st = thread_staging();
   int shift;
   size_t w;
-  r = stage_windows(em->fields, heads, n, em->stage, dev, &shift, &w);
+  r = stage_windows(em->fields, heads, n, st, dev, &shift, &w);
   if (r) return r;
-  HIP_TRY(hipMemcpyAsync(em->stage.d_in, em->stage.h_in, n * w,
-                         hipMemcpyHostToDevice, s));
-  r = em_launch(em, em->stage.d_in, w, n, default_gate,
-                reinterpret_cast<uint16_t *>(em->stage.d_out), shift, s);
+  HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
+  r = em_launch(em, st.d_in, w, n, default_gate,
+                reinterpret_cast<uint16_t *>(st.d_out), shift, s);
   if (r) return r;
-  HIP_TRY(hipMemcpyAsync(em->stage.h_out, em->stage.d_out, n * 2,
-                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 2, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  memcpy(gates, em->stage.h_out, n * 2);
+  memcpy(gates, st.h_out, n * 2);
   return 0;
 }
 
@@ -774,9 +802,9 @@ struct bg_wm {
   uint32_t key_size = 0;
   uint32_t kw = 1;
   std::vector<WmTupleH> tuples;
-  bool dirty = true;
+  std::atomic<bool> dirty{true};  // as bg_em::dirty
+  bool built_no_tags = false;     // BG_PATH_WM_NO_TAGS when the image was built
   DevTable dev;
-  Staging stage;
   std::mutex mu;
 };
 
@@ -819,7 +847,6 @@ int bg_wm_create(const bg_field *fields, int nfields, bg_wm **out) {
 void bg_wm_destroy(bg_wm *wm) {
   if (!wm) return;
   wm->dev.release();
-  wm->stage.release();
   delete wm;
 }
 
@@ -888,8 +915,13 @@ int bg_wm_iter(const bg_wm *wm, int t, size_t *cursor, uint8_t *key_out,
   return 0;
 }
 
+static bool wm_want_no_tags() { return (path_flags() & kPathWmNoTags) != 0; }
+
 static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
-  if (!wm->dirty && wm->dev.valid && wm->dev.device == device) return 0;
+  const bool no_tags = wm_want_no_tags();
+  if (!wm->dirty && wm->dev.valid && wm->dev.device == device &&
+      wm->built_no_tags == no_tags)
+    return 0;
   std::vector<uint64_t> keys, seeds;
   std::vector<uint8_t> vals, img;
   for (size_t t = 0; t < wm->tuples.size(); t++) {
@@ -912,8 +944,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   // higher load factor if need be: the bucketized 2x4 cuckoo table inserts
   // well past 0.9) keeps them there (bg_wm.hip) and needs no key filter.
   bool tags_lds = false;
-  const char *etg = getenv("BG_WM_TAGS");  // A/B knob (variants.py)
-  if (img.size() > kLdsTableMax && !(etg && *etg && atoi(etg) == 0)) {
+  if (img.size() > kLdsTableMax && !no_tags && knob("BG_WM_TAGS", 1)) {
     for (double load : {0.75, 0.93}) {
       std::vector<uint8_t> img2;
       TableLayout L2;
@@ -930,8 +961,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   // key, 64 KB by default so two workgroups fit a CU -- measured faster
   // than 128 KB at one workgroup per CU) that the kernel stages in LDS.
   uint32_t fw = 0;
-  const char *ekb = getenv("BG_WM_FILTER_KB");  // A/B knob (variants.py)
-  const int kb = (ekb && *ekb) ? atoi(ekb) : 64;
+  const int kb = knob("BG_WM_FILTER_KB", 64);  // A/B knob (variants.py)
   if (img.size() > kLdsTableMax && !tags_lds && kb > 0 && nkeys > 0) {
     const uint32_t cap = std::min<uint32_t>(kFilterMaxWords, (uint32_t)kb * 256);
     fw = 1024;
@@ -954,11 +984,15 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   wm->dev.filt_off = foff;
   wm->dev.filt_words = fw;
   wm->dev.tags_lds = tags_lds;
+  wm->built_no_tags = no_tags;
   wm->dirty = false;
   return 0;
 }
 
 int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream) {
+  if (!wm->dirty.load(std::memory_order_acquire) && wm->dev.valid &&
+      wm->dev.device == device && wm->built_no_tags == wm_want_no_tags())
+    return 0;
   std::lock_guard<std::mutex> lk(wm->mu);
   return wm_sync_locked(wm, device, (hipStream_t)stream);
 }
@@ -1007,7 +1041,8 @@ int bg_wm_classify_window(bg_wm *wm, const void *d_frames, size_t stride,
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   if (int r = check_extent(wm->dfields, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
-  if (!wm->dev.valid || wm->dirty) {
+  if (wm->dirty.load(std::memory_order_acquire) || !wm->dev.valid ||
+      wm->built_no_tags != wm_want_no_tags()) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     std::lock_guard<std::mutex> lk(wm->mu);
@@ -1024,26 +1059,31 @@ int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
                        bg_stream_t stream) {
   if (wm->has_attr) return no_attr_datapath();
   if (n == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  std::lock_guard<std::mutex> lk(wm->mu);
-  int cur = 0;
-  (void)hipGetDevice(&cur);
-  int dev = wm->dev.valid ? wm->dev.device : cur;
-  int r = wm_sync_locked(wm, dev, s);
+  if (wm->dirty.load(std::memory_order_acquire) || !wm->dev.valid ||
+      wm->built_no_tags != wm_want_no_tags()) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    std::lock_guard<std::mutex> lk(wm->mu);
+    int r = wm_sync_locked(wm, wm->dev.valid ? wm->dev.device : cur,
+                           thread_stream(cur, (hipStream_t)stream));
+    if (r) return r;
+  }
+  const int dev = wm->dev.device;
+  int r = set_device(dev);
   if (r) return r;
+  hipStream_t s = thread_stream(dev, (hipStream_t)stream);
+  Staging &st = thread_staging();
   int shift;
   size_t w;
-  r = stage_windows(wm->fields, heads, n, wm->stage, dev, &shift, &w);
+  r = stage_windows(wm->fields, heads, n, st, dev, &shift, &w);
   if (r) return r;
-  HIP_TRY(hipMemcpyAsync(wm->stage.d_in, wm->stage.h_in, n * w,
-                         hipMemcpyHostToDevice, s));
-  r = wm_launch(wm, wm->stage.d_in, w, n, default_gate,
-                reinterpret_cast<uint16_t *>(wm->stage.d_out), shift, s);
+  HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
+  r = wm_launch(wm, st.d_in, w, n, default_gate,
+                reinterpret_cast<uint16_t *>(st.d_out), shift, s);
   if (r) return r;
-  HIP_TRY(hipMemcpyAsync(wm->stage.h_out, wm->stage.d_out, n * 2,
-                         hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 2, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  memcpy(gates, wm->stage.h_out, n * 2);
+  memcpy(gates, st.h_out, n * 2);
   return 0;
 }
 
@@ -1086,11 +1126,11 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
                           uint16_t *ip_gates, uint16_t *l4_gates,
                           bg_stream_t stream) {
   if (n == 0) return 0;
-  static thread_local Staging st;
-  hipStream_t s = (hipStream_t)stream;
+  Staging &st = thread_staging();
   const size_t w = (span + 15) / 16 * 16;
   int r = set_device(device);
   if (r) return r;
+  hipStream_t s = thread_stream(device, (hipStream_t)stream);
   r = st.ensure(device, n * w, n * 4);
   if (r) return r;
   for (size_t i = 0; i < n; i++) {
@@ -1099,7 +1139,7 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
   }
   HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
   uint16_t *dg = reinterpret_cast<uint16_t *>(st.d_out);
-  r = bg_cksum(device, st.d_in, w, n, mode, verify, dg, dg + n, stream);
+  r = bg_cksum(device, st.d_in, w, n, mode, verify, dg, dg + n, s);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.h_in, st.d_in, n * w, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 4, hipMemcpyDeviceToHost, s));

@@ -4,20 +4,20 @@
 // the NAT map, then Stamp<dir> (262-319): the address and port rewritten,
 // IPv4 and TCP/UDP/ICMP checksums updated incrementally (RFC 1624).
 //
-// dnat_find_kernel classifies a batch (entry index, or a miss / an
-// invalid protocol) and counts the forward misses, which need a new
-// mapping; dnat_apply_kernel rewrites every packet from a per-packet entry
-// index (the lookup result itself when there was no forward miss, else the
-// host's in-order walk, bg_dnat_api.cc) and refreshes forward timestamps.
+// dnat_fused_*_kernel look every packet up and Stamp the final hits (any
+// reverse hit; a forward hit on a mapping that has not expired at `now`),
+// refreshing forward timestamps, and list the rest of the forward packets
+// (misses, hits on expired mappings) for the host's in-order walk
+// (bg_dnat_api.cc); dnat_apply_kernel then rewrites the listed packets from
+// the walk's entry indices.
 // Lane = packet; header fields past the first bytes are reached through
 // the frame pointer (any IHL).
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
-
 #include <algorithm>
 
 #include "bg_kernels.h"
 #include "bg_keys_dev.h"
+#include "bg_launch.h"
 
 namespace bg {
 namespace {
@@ -169,23 +169,6 @@ __device__ __forceinline__ GlobalFrame frame_of(const DnatArgs &a, uint64_t i) {
   return f;
 }
 
-__global__ __launch_bounds__(kNatBlock) void dnat_find_kernel(DnatArgs a) {
-  const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < a.n;
-       i += step) {
-    const uint64_t key = endpoint(frame_of(a, i), a.dir);
-    a.keys[i] = key;
-    uint32_t r = kDnatInvalid;
-    if (key != ~0ull) {
-      r = lookup(a, key);
-      // a forward miss needs a new mapping (CreateNewEntry); a reverse
-      // miss is dropped
-      if (r == kDnatMiss && a.dir == 0) atomicAdd(a.nmiss, 1u);
-    }
-    a.res[i] = r;
-  }
-}
-
 // Rewrites packets from entry indices: every packet of the batch (n > 0,
 // res[i] per packet) or, with a.list, the nlist packets idx[k] = res[k]
 // with entries mres[k] and endpoints keys[k].
@@ -206,22 +189,27 @@ __global__ __launch_bounds__(kNatBlock) void dnat_apply_kernel(DnatArgs a) {
   }
 }
 
-// One packet's whole decision when no mapping can be evicted by this batch
-// (bg_dnat_process): lookup; a hit is stamped and its forward timestamp
-// refreshed; an invalid protocol or a reverse miss drops; a forward miss is
-// appended to the miss list (wave-aggregated) for the host's in-order
-// CreateNewEntry walk.
+// One packet's decision (bg_dnat_process): lookup; a final hit is stamped
+// and its forward timestamp refreshed; an invalid protocol or a reverse
+// miss drops; a forward miss, or a forward hit on an expired mapping (a new
+// flow earlier in the batch may evict it: CreateNewEntry, nat.cc:224-231),
+// is appended to the list (wave-aggregated) for the host's in-order walk.
 template <class F>
 __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
                                           uint64_t i, bool live) {
   uint64_t key = ~0ull;
   SlotHit h;
   h.slot = ~0u;
+  uint64_t ts = 0;
   if (live) {
     key = endpoint(f, a.dir);
     if (key != ~0ull) h = lookup_hit(a, key);
+    if (h.slot != ~0u && a.dir == 0) ts = a.ts[h.entry];
   }
-  const bool fmiss = live && key != ~0ull && h.slot == ~0u && a.dir == 0;
+  // only a forward entry's timestamp decides expiry (nat.cc:222-226)
+  const bool expired = h.slot != ~0u && a.dir == 0 && a.now - ts > a.timeout;
+  const bool fmiss =
+      live && key != ~0ull && a.dir == 0 && (h.slot == ~0u || expired);
   const uint64_t m = __ballot(fmiss);
   if (m) {
     const int lead = __builtin_ctzll(m);
@@ -237,8 +225,8 @@ __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
     }
   }
   if (!live) return;
-  if (h.slot == ~0u) {
-    a.out[i] = kDropGate;  // the host's walk decides forward misses
+  if (h.slot == ~0u || expired) {
+    a.out[i] = kDropGate;  // the host's walk decides listed packets
     return;
   }
   stamp(f, key, h.ep, a.dir);
@@ -246,8 +234,18 @@ __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
   // forward timestamp refresh. A scattered 8-byte store is a partial-line
   // write; an entry an earlier packet of the flow already stamped with
   // `now` is left alone (measured: 0.73-0.80 -> 0.69 ms per 16 M packets)
-  // (a.ts is null only under the BG_NAT_AB_NOTS measurement knob)
-  if (a.dir == 0 && a.ts && a.ts[h.entry] != a.now) a.ts[h.entry] = a.now;
+  if (a.dir == 0 && ts != a.now) a.ts[h.entry] = a.now;
+}
+
+// the entries a host walk changed: ent[idx] = ep, ts[idx] = ts
+__global__ __launch_bounds__(kNatBlock) void dnat_scatter_kernel(
+    const uint64_t *up, uint64_t k, uint64_t *ent, uint64_t *ts) {
+  const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < k; i += step) {
+    const uint64_t e = up[i];
+    ent[e] = up[k + i];
+    ts[e] = up[2 * k + i];
+  }
 }
 
 // any stride: lane = packet, header bytes straight from HBM
@@ -319,10 +317,11 @@ uint64_t grid_of(uint64_t n, int num_cus) {
 
 }  // namespace
 
-hipError_t launch_dnat_find(const DnatArgs &a, int num_cus, hipStream_t s) {
-  if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(dnat_find_kernel, dim3((unsigned)grid_of(a.n, num_cus)),
-                     dim3(kNatBlock), 0, s, a);
+hipError_t launch_dnat_scatter(const uint64_t *d_up, size_t k, uint64_t *ent,
+                               uint64_t *ts, hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  hipLaunchKernelGGL(dnat_scatter_kernel, dim3((unsigned)grid_of(k, 256)),
+                     dim3(kNatBlock), 0, s, d_up, (uint64_t)k, ent, ts);
   return hipGetLastError();
 }
 
@@ -336,18 +335,13 @@ hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s) {
 
 hipError_t launch_dnat_fused(const DnatArgs &a0, int num_cus, hipStream_t s) {
   if (a0.n == 0) return hipSuccess;
-  DnatArgs a = a0;
-  // measurement only: skip the forward timestamp refresh (breaks parity;
-  // scripts A/B the cost of the dependent ts read)
-  if (getenv("BG_NAT_AB_NOTS")) a.ts = nullptr;
-  if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 && !getenv("BG_NO_SLAB")) {
+  const DnatArgs &a = a0;
+  if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
+      !(path_flags() & kPathNoSlab)) {
     const size_t lds = (size_t)(kNatSlabBlock / 64) * 4096;
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void *>(dnat_fused_slab_kernel),
-            kNatSlabBlock, lds) != hipSuccess || occ <= 0)
-      occ = 1;
-    if (const char *e = getenv("BG_NAT_OCC")) occ = std::max(1, atoi(e));  // A/B knob
+    int occ = occupancy(reinterpret_cast<const void *>(dnat_fused_slab_kernel),
+                        kNatSlabBlock, lds, 1);
+    occ = std::max(1, knob("BG_NAT_OCC", occ));
     const uint64_t need = (a.n + kNatSlabBlock - 1) / kNatSlabBlock;
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
     hipLaunchKernelGGL(dnat_fused_slab_kernel, dim3((unsigned)blocks),

@@ -6,20 +6,21 @@
 // entries' translated endpoints and their forward timestamps.
 // CreateNewEntry (nat.cc:180-258) draws ports from the module's Random and
 // may evict an expired mapping that a later packet of the same batch would
-// have hit. The host tracks bounds on the forward timestamps, so it knows
-// when no mapping can expire at `now` (and reverse traffic never creates
-// one). Then a batch is
+// have hit. A hit on a mapping that has NOT expired at `now` is final for the
+// whole batch (only expired mappings can be evicted, and a hit refreshes its
+// mapping), so every batch is
 //   1. dnat_fused_kernel (dnat_fused_slab_kernel for 64-byte slots): lookup
-//      and Stamp of every hit in one pass over the header line, forward
-//      timestamps refreshed, forward misses listed;
-//   2. only if the list is not empty: the misses walked in packet order on
-//      the host (find or CreateNewEntry), the device copy rebuilt, and
-//      dnat_apply_kernel stamps the listed packets.
-// When a mapping may expire, the whole batch is classified first
-// (dnat_find_kernel); with no forward miss dnat_apply_kernel rewrites it,
-// otherwise every packet is decided on the host in packet order, with the
-// device's timestamps read back first, and dnat_apply_kernel rewrites the
-// batch from the host's decisions.
+//      and Stamp of every final hit in one pass over the header line,
+//      forward timestamps refreshed; forward misses AND forward hits on
+//      expired mappings are listed instead;
+//   2. only if the list is not empty: the listed packets walked in packet
+//      order on the host (find, or CreateNewEntry with its eviction), the
+//      device copy updated, and dnat_apply_kernel stamps the listed packets.
+// Reverse traffic never creates a mapping, so a reverse batch is step 1.
+// The host's forward timestamps are lower bounds of the device's (only the
+// device refreshes between walks): a mapping the host sees as unexpired is
+// unexpired; one it sees as expired is re-read from the device before the
+// port search may evict it.
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -79,14 +80,16 @@ struct bg_dnat {
   uint64_t seed;                           // Random::seed_
   // the map: key -> entry index; entries: translated endpoint, timestamp
   std::unordered_map<uint64_t, uint32_t> map;
+  // per entry: translated endpoint, forward timestamp (a lower bound of the
+  // device's unless `exact`), whether the current walk set it
   std::vector<uint64_t> ent_ep, ent_ts;
+  std::vector<uint32_t> exact_walk;  // walk that made ent_ts exact
+  uint32_t walk = 1;
   std::vector<uint32_t> free_idx;
-  std::vector<uint8_t> ent_fwd;  // live forward entry (its ts can expire)
-  // bounds on the forward entries' timestamps: lb exact after every host
-  // walk (device refreshes only raise them), ub = the latest `now` seen
-  uint64_t ts_lb = ~0ull, ts_ub = 0;
-  bool dirty = true;
+  std::vector<uint32_t> changed;  // entries to push to the device
+  bool map_dirty = true;          // the lookup image must be rebuilt
   int device = -1;
+  hipStream_t walk_stream = nullptr;
   DevTable dev;
   uint64_t *d_ent = nullptr, *d_ts = nullptr;
   size_t d_cap = 0;  // entries the device arrays hold
@@ -104,6 +107,8 @@ struct bg_dnat {
     auto it = map.find(key);
     if (it != map.end()) {
       ent_ep[it->second] = ep;
+      changed.push_back(it->second);
+      map_dirty = true;  // the image carries the translation
       return it->second;
     }
     uint32_t idx;
@@ -112,24 +117,39 @@ struct bg_dnat {
       free_idx.pop_back();
       ent_ep[idx] = ep;
       ent_ts[idx] = 0;
-      ent_fwd[idx] = 0;
+      exact_walk[idx] = walk;
     } else {
       idx = (uint32_t)ent_ep.size();
       ent_ep.push_back(ep);
       ent_ts.push_back(0);
-      ent_fwd.push_back(0);
+      exact_walk.push_back(walk);
     }
     map.emplace(key, idx);
-    dirty = true;
+    changed.push_back(idx);
+    map_dirty = true;
     return idx;
   }
   void remove(uint64_t key) {
     auto it = map.find(key);
     if (it == map.end()) return;
     free_idx.push_back(it->second);
-    ent_fwd[it->second] = 0;
     map.erase(it);
-    dirty = true;
+    map_dirty = true;
+  }
+  // now - last_refresh > kTimeOutNs (nat.cc:217, u64 arithmetic) with the
+  // entry's current timestamp: a host value that says "expired" may be
+  // stale, so it is re-read from the device first
+  bool expired(uint32_t e, uint64_t now) {
+    if (now - ent_ts[e] <= kTimeOutNs) return false;
+    if (exact_walk[e] != walk && d_ts && e < d_cap) {
+      uint64_t t = 0;
+      if (hipMemcpyAsync(&t, d_ts + e, 8, hipMemcpyDeviceToHost, walk_stream) ==
+              hipSuccess &&
+          hipStreamSynchronize(walk_stream) == hipSuccess)
+        ent_ts[e] = std::max(ent_ts[e], t);
+      exact_walk[e] = walk;
+    }
+    return now - ent_ts[e] > kTimeOutNs;
   }
   int64_t find(uint64_t key) const {
     auto it = map.find(key);
@@ -177,7 +197,7 @@ struct bg_dnat {
         bool take = rev < 0;
         if (!take) {
           const int64_t fwd = find(ent_ep[rev]);  // the internal endpoint
-          if (fwd >= 0 && now - ent_ts[fwd] > kTimeOutNs) {
+          if (fwd >= 0 && expired((uint32_t)fwd, now)) {
             remove(ent_ep[rev]);
             remove(ext_ep);
             take = true;
@@ -185,9 +205,7 @@ struct bg_dnat {
         }
         if (take) {
           insert(ext_ep, in);
-          const uint32_t e = insert(in, ext_ep);
-          ent_fwd[e] = 1;
-          return e;
+          return insert(in, ext_ep);
         }
         port++;
         trials++;
@@ -209,57 +227,67 @@ struct bg_dnat {
     return 0;
   }
 
-  // Can CreateNewEntry evict a mapping at `now`? Only a forward entry with
-  // now - ts > kTimeOutNs (u64 arithmetic, nat.cc:217) can go; with every
-  // forward ts in [lb, ub], none can when ub <= now and now - lb <= timeout.
-  bool may_evict(uint64_t now) const {
-    if (ts_lb == ~0ull) return false;  // no forward entry
-    return now < ts_ub || now - ts_lb > kTimeOutNs;
-  }
-  void exact_bounds() {  // host timestamps are exact here
-    ts_lb = ~0ull;
-    for (size_t e = 0; e < ent_fwd.size(); e++)
-      if (ent_fwd[e]) {
-        ts_lb = std::min(ts_lb, ent_ts[e]);
-        ts_ub = std::max(ts_ub, ent_ts[e]);
-      }
-  }
-
-  // device copy of the map, entries and timestamps
+  // Device copy: the lookup image (rebuilt when the map changed) and the
+  // per-entry arrays, grown by doubling with their device contents kept
+  // (the device's timestamps are newer than the host's), then the entries
+  // the walk changed scattered in (dnat_scatter_kernel).
   int sync(int dev_id, hipStream_t s) {
-    if (!dirty && device == dev_id && dev.valid) return 0;
     int r = set_device(dev_id);
     if (r) return r;
-    std::vector<uint64_t> keys, hashes;
-    std::vector<uint8_t> vals, img;
-    for (auto &kv : map) {  // key words: the endpoint, its translation
-      keys.push_back(kv.first);
-      keys.push_back(ent_ep[kv.second]);
-      hashes.push_back(hash_words(&kv.first, 1, kDefaultSeed));
-      for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(kv.second >> (8 * b)));
+    if (device != dev_id && device >= 0)
+      return fail(EINVAL, "NAT map bound to device %d", device);
+    if (map_dirty || !dev.valid) {
+      std::vector<uint64_t> keys, hashes;
+      std::vector<uint8_t> vals, img;
+      for (auto &kv : map) {  // key words: the endpoint, its translation
+        keys.push_back(kv.first);
+        keys.push_back(ent_ep[kv.second]);
+        hashes.push_back(hash_words(&kv.first, 1, kDefaultSeed));
+        for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(kv.second >> (8 * b)));
+      }
+      TableLayout L;
+      r = build_image(2, 4, 1, keys, vals, hashes, &img, &L);
+      if (r) return r;
+      r = dev.upload(dev_id, img, L, s);
+      if (r) return r;
+      map_dirty = false;
     }
-    TableLayout L;
-    r = build_image(2, 4, 1, keys, vals, hashes, &img, &L);
-    if (r) return r;
-    r = dev.upload(dev_id, img, L, s);
-    if (r) return r;
     const size_t ne = std::max<size_t>(ent_ep.size(), 1);
-    if (ne > d_cap || device != dev_id) {
-      if (d_ent) (void)hipFree(d_ent);
-      if (d_ts) (void)hipFree(d_ts);
-      d_cap = std::max<size_t>(ne * 2, 1024);
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_ent), d_cap * 8));
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_ts), d_cap * 8));
+    if (ne > d_cap) {
+      const size_t cap = std::max<size_t>(ne * 2, 1024);
+      uint64_t *ne_ep = nullptr, *ne_ts = nullptr;
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ne_ep), cap * 8));
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&ne_ts), cap * 8));
+      if (d_cap) {
+        HIP_TRY(hipMemcpyAsync(ne_ep, d_ent, d_cap * 8, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ne_ts, d_ts, d_cap * 8, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(d_ent);
+        (void)hipFree(d_ts);
+      }
+      d_ent = ne_ep;
+      d_ts = ne_ts;
+      d_cap = cap;
     }
-    if (!ent_ep.empty()) {
-      HIP_TRY(hipMemcpyAsync(d_ent, ent_ep.data(), ent_ep.size() * 8,
-                             hipMemcpyHostToDevice, s));
-      HIP_TRY(hipMemcpyAsync(d_ts, ent_ts.data(), ent_ts.size() * 8,
-                             hipMemcpyHostToDevice, s));
+    if (!changed.empty()) {
+      std::sort(changed.begin(), changed.end());
+      changed.erase(std::unique(changed.begin(), changed.end()), changed.end());
+      const size_t k = changed.size();
+      std::vector<uint64_t> up(3 * k);  // idx | ep | ts
+      for (size_t i = 0; i < k; i++) {
+        up[i] = changed[i];
+        up[k + i] = ent_ep[changed[i]];
+        up[2 * k + i] = ent_ts[changed[i]];
+      }
+      uint64_t *d_up = nullptr;
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_up), up.size() * 8));
+      HIP_TRY(hipMemcpyAsync(d_up, up.data(), up.size() * 8, hipMemcpyHostToDevice, s));
+      HIP_TRY(launch_dnat_scatter(d_up, k, d_ent, d_ts, s));
+      HIP_TRY(hipStreamSynchronize(s));  // `up` is host memory
+      (void)hipFree(d_up);
+      changed.clear();
     }
-    HIP_TRY(hipStreamSynchronize(s));
     device = dev_id;
-    dirty = false;
     return 0;
   }
 };
@@ -311,11 +339,11 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
                     int dir, uint64_t now, uint16_t *d_out, bg_stream_t stream) {
   if (dir != 0 && dir != 1) return fail(EINVAL, "dir %d", dir);
   if (n == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
   std::lock_guard<std::mutex> lk(h->mu);
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (h->device >= 0) dev = h->device;
+  hipStream_t s = thread_stream(dev, (hipStream_t)stream);
   int r = h->sync(dev, s);
   if (r) return r;
   r = h->ensure_batch(n);
@@ -327,6 +355,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.n = n;
   a.dir = (uint32_t)dir;
   a.now = now;
+  a.timeout = kTimeOutNs;
   a.t = h->dev.ref();
   a.keys = h->d_keys;
   a.res = h->d_res;
@@ -337,103 +366,53 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.out = d_out;
   HIP_TRY(hipMemsetAsync(h->d_nmiss, 0, 4, s));
   const int ncu = num_cus(dev);
-  if (dir == 1 || !h->may_evict(now)) {
-    // Nothing this batch creates can change another packet's mapping, so
-    // hits are final: one pass stamps them and lists the forward misses.
-    // Reverse traffic never creates a mapping (a miss drops).
-    HIP_TRY(launch_dnat_fused(a, ncu, s));
-    if (dir == 1) return 0;
-    h->ts_ub = std::max(h->ts_ub, now);
-    uint32_t nmiss = 0;
-    HIP_TRY(hipMemcpyAsync(&nmiss, h->d_nmiss, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (nmiss == 0) return 0;
-    // new flows: CreateNewEntry in packet order on the host
-    std::vector<uint32_t> idx(nmiss), ent(nmiss);
-    std::vector<uint64_t> key(nmiss);
-    HIP_TRY(hipMemcpyAsync(idx.data(), h->d_res, nmiss * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(key.data(), h->d_keys, nmiss * 8, hipMemcpyDeviceToHost, s));
-    if (!h->ent_ts.empty())  // forward refreshes made on the device
-      HIP_TRY(hipMemcpyAsync(h->ent_ts.data(), h->d_ts, h->ent_ts.size() * 8,
-                             hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    std::vector<uint32_t> ord(nmiss);
-    for (uint32_t k = 0; k < nmiss; k++) ord[k] = k;
-    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
-    std::vector<uint32_t> sidx(nmiss);
-    std::vector<uint64_t> skey(nmiss);
-    for (uint32_t k = 0; k < nmiss; k++) {
-      sidx[k] = idx[ord[k]];
-      skey[k] = key[ord[k]];
-      int64_t e = h->find(skey[k]);
-      if (e < 0) e = h->create(skey[k], now);
-      if (e >= 0) h->ent_ts[e] = now;
-      ent[k] = e < 0 ? kDnatMiss : (uint32_t)e;
-    }
-    h->exact_bounds();
-    h->dirty = true;
-    r = h->sync(dev, s);
-    if (r) return r;
-    HIP_TRY(hipMemcpyAsync(h->d_res, sidx.data(), nmiss * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(h->d_keys, skey.data(), nmiss * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(h->d_mres, ent.data(), nmiss * 4, hipMemcpyHostToDevice, s));
-    a.t = h->dev.ref();
-    a.ent = h->d_ent;
-    a.ts = h->d_ts;
-    a.nent = h->ent_ep.size();
-    a.refresh = 0;
-    a.list = 1;
-    a.nlist = nmiss;
-    a.mres = h->d_mres;
-    HIP_TRY(launch_dnat_apply(a, ncu, s));
-    HIP_TRY(hipStreamSynchronize(s));  // the host vectors outlive the copies
-    return 0;
-  }
-  // An expired mapping may be evicted by a new flow, which changes what a
-  // later packet of the batch maps to: classify first, and if any forward
-  // packet misses, decide the whole batch in packet order on the host.
-  HIP_TRY(launch_dnat_find(a, ncu, s));
-  uint32_t nmiss = 0;
-  HIP_TRY(hipMemcpyAsync(&nmiss, h->d_nmiss, 4, hipMemcpyDeviceToHost, s));
+  // final hits stamped on the device; forward misses and forward hits on
+  // expired mappings listed (reverse traffic never creates a mapping)
+  HIP_TRY(launch_dnat_fused(a, ncu, s));
+  uint32_t nlist = 0;
+  if (dir == 0)
+    HIP_TRY(hipMemcpyAsync(&nlist, h->d_nmiss, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  h->ts_ub = std::max(h->ts_ub, now);
-  if (nmiss == 0) {  // every valid packet has a mapping
-    a.refresh = dir == 0;
-    HIP_TRY(launch_dnat_apply(a, ncu, s));
-    return 0;
-  }
-  // in packet order on the host (DoProcessBatch 321-363)
-  std::vector<uint64_t> keys(n);
-  std::vector<uint32_t> res(n);
-  HIP_TRY(hipMemcpyAsync(keys.data(), h->d_keys, n * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(res.data(), h->d_res, n * 4, hipMemcpyDeviceToHost, s));
-  if (!h->ent_ts.empty())  // forward refreshes made on the device
-    HIP_TRY(hipMemcpyAsync(h->ent_ts.data(), h->d_ts, h->ent_ts.size() * 8,
-                           hipMemcpyDeviceToHost, s));
+  if (nlist == 0) return 0;
+  // the listed packets in packet order on the host (DoProcessBatch 321-363)
+  std::vector<uint32_t> idx(nlist), ent(nlist);
+  std::vector<uint64_t> key(nlist);
+  HIP_TRY(hipMemcpyAsync(idx.data(), h->d_res, nlist * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(key.data(), h->d_keys, nlist * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  for (size_t i = 0; i < n; i++) {
-    if (res[i] == kDnatInvalid) continue;  // DropPacket
-    int64_t e = h->find(keys[i]);
-    if (e < 0) e = h->create(keys[i], now);
-    if (e < 0) {
-      res[i] = kDnatMiss;  // DropPacket
-      continue;
+  std::vector<uint32_t> ord(nlist);
+  for (uint32_t k = 0; k < nlist; k++) ord[k] = k;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
+  std::vector<uint32_t> sidx(nlist);
+  std::vector<uint64_t> skey(nlist);
+  h->walk++;  // no host timestamp is known exact yet
+  h->walk_stream = s;
+  for (uint32_t k = 0; k < nlist; k++) {
+    sidx[k] = idx[ord[k]];
+    skey[k] = key[ord[k]];
+    int64_t e = h->find(skey[k]);
+    if (e < 0) e = h->create(skey[k], now);
+    if (e >= 0) {  // forward refresh (rfc4787 REQ-6)
+      h->ent_ts[e] = now;
+      h->exact_walk[e] = h->walk;
+      h->changed.push_back((uint32_t)e);
     }
-    if (dir == 0) h->ent_ts[e] = now;
-    res[i] = (uint32_t)e;
+    ent[k] = e < 0 ? kDnatMiss : (uint32_t)e;
   }
-  h->exact_bounds();
-  h->dirty = true;  // timestamps (and maybe entries) changed
   r = h->sync(dev, s);
   if (r) return r;
-  HIP_TRY(hipMemcpyAsync(h->d_res, res.data(), n * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(h->d_res, sidx.data(), nlist * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(h->d_keys, skey.data(), nlist * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(h->d_mres, ent.data(), nlist * 4, hipMemcpyHostToDevice, s));
   a.t = h->dev.ref();
   a.ent = h->d_ent;
   a.ts = h->d_ts;
   a.nent = h->ent_ep.size();
-  a.refresh = 0;
+  a.list = 1;
+  a.nlist = nlist;
+  a.mres = h->d_mres;
   HIP_TRY(launch_dnat_apply(a, ncu, s));
-  HIP_TRY(hipStreamSynchronize(s));  // res (host memory) outlives the copy
+  HIP_TRY(hipStreamSynchronize(s));  // the host vectors outlive the copies
   return 0;
 }
 

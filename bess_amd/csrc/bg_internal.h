@@ -81,6 +81,14 @@ struct Staging {
   ~Staging() { release(); }
 };
 
+// The synchronous host paths (bg_*_process_host, Module::ProcessPackets)
+// may be entered by many worker threads on one table or module at once
+// (core/module.h:485): each thread stages into its own pinned buffers and,
+// when the caller passes no stream, runs on its own non-blocking stream per
+// device (never the legacy stream, which would serialise the workers).
+Staging &thread_staging();
+hipStream_t thread_stream(int device, hipStream_t given);
+
 }  // namespace bg
 
 #endif  // BESS_AMD_BG_INTERNAL_H_

@@ -197,7 +197,7 @@ struct DnatArgs {
   uint8_t *frames;
   uint64_t stride, n;
   uint32_t dir, refresh;
-  uint64_t now;
+  uint64_t now, timeout;  // a forward hit with now - ts > timeout is listed
   TableRef t;        // endpoint -> entry index (u32 values), KW = 1
   uint64_t *keys;    // per packet: the endpoint key
   uint32_t *res;     // per packet: entry / kDnatMiss / kDnatInvalid
@@ -224,11 +224,13 @@ hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_encap(const EncapArgs &a, int num_cus, hipStream_t s);
-hipError_t launch_dnat_find(const DnatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s);
-// lookup + stamp in one pass; forward misses listed in res/keys (count in
-// *nmiss) -- only when the batch cannot evict a mapping
+// lookup + stamp of the final hits in one pass; forward misses and forward
+// hits on expired mappings listed in res/keys (count in *nmiss)
 hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s);
+// up = [idx x k | ep x k | ts x k]: ent[idx[i]] = ep[i], ts[idx[i]] = ts[i]
+hipError_t launch_dnat_scatter(const uint64_t *d_up, size_t k, uint64_t *ent,
+                               uint64_t *ts, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword

@@ -8,17 +8,14 @@
 // All integer work; HBM-bound streaming over resident packet slabs (frame i
 // at frames + i*stride). No MFMA: there is no contraction on this path.
 #include <hip/hip_runtime.h>
-
-#include <mutex>
-#include <vector>
 #include <limits.h>
 #include <stddef.h>
-#include <stdlib.h>
 
 #include <algorithm>
 
 #include "bg_kernels.h"
 #include "bg_keys_dev.h"
+#include "bg_launch.h"
 
 namespace bg {
 namespace {
@@ -172,6 +169,7 @@ void em_classify_kernel(EmArgs a) {
   em_body<KW, NCH, PPL>(a, lds);
 }
 
+#ifdef BG_AB
 // next grid-stride packet's window prefetched (A/B experiments: BG_EM_PF=1)
 template <int KW, int NCH>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
@@ -196,6 +194,7 @@ void em_classify_pf_kernel(EmArgs a) {
     a.gates[idx] = (uint16_t)g;
   }
 }
+#endif  // BG_AB
 
 // ---------------------------------------------------------------------------
 // ExactMatch over a dense 64-byte-slot slab (stride 64, key window inside
@@ -280,6 +279,7 @@ void em_slab_kernel(EmArgs a) {
   }
 }
 
+#ifdef BG_AB
 // Compact-stage slab kernel: only the NCH chunks of each slot's key window
 // are loaded and staged (64 x NCH x 16 B per wave instead of 4 KB), so a
 // workgroup of BLOCK threads fits beside the LDS table at twice the
@@ -354,6 +354,7 @@ __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   em_body<KW, NCH, PPL>(a, lds);
 }
+#endif  // BG_AB
 
 // ---------------------------------------------------------------------------
 // WildcardMatch: tuple-space search over <= 8 masks in one combined table;
@@ -441,6 +442,9 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
   return gate;
 }
 
+#ifdef BG_AB
+// Batched-rounds lookup (A/B variant V = 2; measured slower than the
+// sequential resolve, which the product uses)
 template <int KW, bool FILT, int G>
 __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
                                               const WmArgs &a,
@@ -544,6 +548,7 @@ __device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
   }
   return gate;
 }
+#endif  // BG_AB
 
 // lookup variant: V 1 = wm_lookup_seq, 2 = batched rounds over groups of G
 template <int KW, bool FILT, int V, int G>
@@ -551,10 +556,10 @@ __device__ __forceinline__ uint32_t wm_lookup_v(const uint8_t *tab,
                                                 const WmArgs &a,
                                                 const uint64_t (&k)[KW],
                                                 const uint32_t *filt) {
-  if constexpr (V == 1)
-    return wm_lookup_seq<KW, FILT>(tab, a, k, filt);
-  else
-    return wm_lookup<KW, FILT, G>(tab, a, k, filt);
+#ifdef BG_AB
+  if constexpr (V == 2) return wm_lookup<KW, FILT, G>(tab, a, k, filt);
+#endif
+  return wm_lookup_seq<KW, FILT>(tab, a, k, filt);
 }
 
 template <int KW, bool FILT, int V, int G>
@@ -615,6 +620,7 @@ void wm_classify_kernel(WmArgs a) {
   wm_body<KW, NCH, PPL, 1, 8, true>(a, lds);
 }
 
+#ifdef BG_AB
 // 1024-thread workgroups: one LDS key-filter copy serves 16 waves
 // (A/B: BG_WM_BLOCK=1024)
 template <int PPL>
@@ -631,6 +637,7 @@ void wm_classify_exp_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   wm_body<2, 2, PPL, V, G, PF>(a, lds);
 }
+#endif  // BG_AB
 
 // ---------------------------------------------------------------------------
 // IPChecksum + L4Checksum, one wave per frame.
@@ -1207,10 +1214,12 @@ template <bool RELOAD, int DEPTH>
 __global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
 void cksum_kernel(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
 
+#ifdef BG_AB
 template <bool RELOAD, int DEPTH>
 __global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
 __attribute__((amdgpu_waves_per_eu(5, 8)))
 void cksum_kernel_w5(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
+#endif
 
 // any stride: frame chunks loaded after the header walk, one frame at a time
 __global__ __launch_bounds__(kCkBlock) void cksum_kernel_generic(CkArgs a) {
@@ -1232,49 +1241,22 @@ __global__ __launch_bounds__(kCkBlock) void cksum_kernel_generic(CkArgs a) {
   }
 }
 
-// Launch-time knobs (defaults measured on MI355X; env overrides are for
-// A/B experiments in scripts/em_variants.py).
-int env_int(const char *name, int dflt) {
-  const char *v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
 
 // Packets per workgroup below which staging the table into LDS costs more
 // than probing it in L2 (a 40 KB table fill vs. 64 B of header per packet).
 constexpr uint64_t kLdsMinPktsPerBlock = 4096;
 
-// hipOccupancyMaxActiveBlocksPerMultiprocessor, memoised per (kernel, LDS
-// bytes, block) -- it is not free and the answer never changes
-int occupancy(const void *kernel, int block, size_t lds, int dflt) {
-  struct Ent {
-    const void *k;
-    size_t lds;
-    int block, occ;
-  };
-  static std::mutex mu;
-  static std::vector<Ent> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const Ent &e : cache)
-    if (e.k == kernel && e.lds == lds && e.block == block) return e.occ;
-  int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block, lds) !=
-          hipSuccess ||
-      occ <= 0)
-    occ = dflt;
-  cache.push_back({kernel, lds, block, occ});
-  return occ;
-}
-
 template <typename Args, typename K>
 hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
                            int ppl, int block = kEmBlock) {
   if (a.n == 0) return hipSuccess;
-  if (env_int("BG_NOLDS", 0)) a.t.lds = 0;
+  const uint32_t pf = path_flags();
+  if (pf & kPathNoLds) a.t.lds = kLdsNone;
   const uint64_t need = (a.n + (uint64_t)block * ppl - 1) / ((uint64_t)block * ppl);
   // Measured on MI355X (scripts/variants.py): with the table in LDS two
   // 512-thread blocks per CU (16 waves) stream fastest -- fewer LDS table
   // fills; with the table in L2/MALL, twice the resident grid.
-  int per_cu = env_int("BG_BLOCKS_PER_CU", 0);
+  const int per_cu = knob("BG_BLOCKS_PER_CU", 0);
   for (int pass = 0; pass < 2; pass++) {
     const size_t lds = a.t.lds == kLdsTable    ? a.t.bytes_total
                        : a.t.lds == kLdsFilter ? (size_t)a.t.filt_words * 4
@@ -1284,13 +1266,13 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
       const int occ =
           occupancy(reinterpret_cast<const void *>(kernel), block, lds, 2);
       pc = a.t.lds ? std::min(occ, 2) : occ * 2;
-      pc *= std::max(1, env_int("BG_GRID_MULT", 1));
+      pc *= std::max(1, knob("BG_GRID_MULT", 1));
     }
     const uint64_t cap = (uint64_t)num_cus * pc;
     const uint64_t blocks = need > cap ? cap : need;
     if (a.t.lds && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
-        !env_int("BG_FORCE_LDS", 0)) {
-      a.t.lds = 0;  // small launch: probe the table in L2 instead
+        !(pf & kPathForceLds)) {
+      a.t.lds = kLdsNone;  // small launch: probe the table in L2 instead
       continue;
     }
     hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(block), lds, s, a);
@@ -1304,11 +1286,15 @@ hipError_t dispatch(const Args &a, int num_cus, hipStream_t s, int dflt_ppl) {
   int maxops = 0;
   for (int q = 0; q < a.fp.nkd; q++) maxops = std::max(maxops, kd_nops_of(a.fp, q));
   const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 && maxops <= 2 ? 2 : 4);
-  const int ppl = env_int("BG_PPL", dflt_ppl);
+  const int ppl = knob("BG_PPL", dflt_ppl);
 #define BG_CASE(KW, NCH, PPL)                                                   \
   if (a.t.kw == KW && nch == NCH && ppl == PPL)                                 \
     return launch_classify(Sel<KW, NCH, PPL>::kernel(), a, num_cus, s, PPL);
+#ifdef BG_AB
 #define BG_PPLS(KW, NCH) BG_CASE(KW, NCH, 1) BG_CASE(KW, NCH, 2)
+#else
+#define BG_PPLS(KW, NCH) BG_CASE(KW, NCH, 1)
+#endif
 #define BG_NCHS(KW) BG_PPLS(KW, 0) BG_PPLS(KW, 2) BG_PPLS(KW, 4)
   BG_NCHS(1) BG_NCHS(2) BG_NCHS(4) BG_NCHS(8)
 #undef BG_NCHS
@@ -1326,6 +1312,52 @@ struct WmSel {
   static auto kernel() { return wm_classify_kernel<KW, NCH, PPL>; }
 };
 
+// Dense 64 B slots with the key window inside the slot: the coalesced slab
+// kernel. LDS = table (if staged) + the per-wave stage.
+template <typename K>
+hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
+                       size_t stage) {
+  const uint32_t pf = path_flags();
+  if (pf & kPathNoLds) a.t.lds = kLdsNone;
+  const uint64_t need = (a.n + block - 1) / block;
+  for (int pass = 0; pass < 2; pass++) {
+    const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
+    const size_t lds = tab + stage;
+    int pc = knob("BG_BLOCKS_PER_CU", 0);
+    if (pc <= 0) pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
+    const uint64_t cap = (uint64_t)num_cus * pc;
+    const uint64_t blocks = need > cap ? cap : need;
+    if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
+        !(pf & kPathForceLds)) {
+      a.t.lds = kLdsNone;  // small launch: probe the table in L2 instead
+      continue;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(block), lds, s, a);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int KW, int NCH>
+hipError_t launch_em_slab(const EmArgs &a, int num_cus, hipStream_t s) {
+  constexpr size_t kStage = (size_t)(kEmBlock / 64) * 4096;
+#ifdef BG_AB
+  const int v2 = knob("BG_SLAB2", 0);
+  if (v2 == 512)
+    return launch_slab(em_slab2_kernel<KW, NCH, 512>, a, num_cus, s, 512,
+                       (size_t)8 * 64 * NCH * 16);
+  if (v2 == 1024)
+    return launch_slab(em_slab2_kernel<KW, NCH, 1024>, a, num_cus, s, 1024,
+                       (size_t)16 * 64 * NCH * 16);
+  // prefetch depth (tiles ahead)
+  const int pf = std::min(2, std::max(0, knob("BG_SLAB_PF", 1)));
+  if (pf == 0) return launch_slab(em_slab_kernel<KW, NCH, 0>, a, num_cus, s, kEmBlock, kStage);
+  if (pf == 2) return launch_slab(em_slab_kernel<KW, NCH, 2>, a, num_cus, s, kEmBlock, kStage);
+#endif
+  // one tile ahead: measured on MI355X (scripts/variants.py) against 0 and 2
+  return launch_slab(em_slab_kernel<KW, NCH, 1>, a, num_cus, s, kEmBlock, kStage);
+}
+
 }  // namespace
 
 bool fits_nch2(const FieldPlan &fp) {
@@ -1335,70 +1367,14 @@ bool fits_nch2(const FieldPlan &fp) {
   return true;
 }
 
-// Dense 64 B slots with the key window inside the slot: the coalesced
-// slab kernel (em_slab_kernel). LDS = table (if staged) + 4 KB per wave.
-template <int KW, int NCH, int BLOCK>
-hipError_t launch_em_slab2(EmArgs a, int num_cus, hipStream_t s) {
-  auto kern = em_slab2_kernel<KW, NCH, BLOCK>;
-  const uint64_t need = (a.n + BLOCK - 1) / BLOCK;
-  constexpr size_t kStage = (size_t)(BLOCK / 64) * 64 * NCH * 16;
-  for (int pass = 0; pass < 2; pass++) {
-    const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
-    const size_t lds = tab + kStage;
-    int pc = env_int("BG_BLOCKS_PER_CU", 0);
-    if (pc <= 0) pc = occupancy(reinterpret_cast<const void *>(kern), BLOCK, lds, 1);
-    const uint64_t cap = (uint64_t)num_cus * pc;
-    const uint64_t blocks = need > cap ? cap : need;
-    if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
-        !env_int("BG_FORCE_LDS", 0)) {
-      a.t.lds = kLdsNone;  // small launch: probe the table in L2 instead
-      continue;
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), lds, s, a);
-    return hipGetLastError();
-  }
-  return hipErrorInvalidValue;
-}
-
-template <int KW, int NCH>
-hipError_t launch_em_slab(EmArgs a, int num_cus, hipStream_t s) {
-  if (env_int("BG_NOLDS", 0)) a.t.lds = kLdsNone;
-  const int v2 = env_int("BG_SLAB2", 0);
-  if (v2 == 512) return launch_em_slab2<KW, NCH, 512>(a, num_cus, s);
-  if (v2 == 1024) return launch_em_slab2<KW, NCH, 1024>(a, num_cus, s);
-  // prefetch depth (tiles ahead), measured on MI355X: scripts/variants.py
-  const int pf = std::min(2, std::max(0, env_int("BG_SLAB_PF", 1)));
-  using K = void (*)(EmArgs);
-  const K kern = pf == 2   ? em_slab_kernel<KW, NCH, 2>
-                 : pf == 1 ? em_slab_kernel<KW, NCH, 1>
-                           : em_slab_kernel<KW, NCH, 0>;
-  const uint64_t need = (a.n + kEmBlock - 1) / kEmBlock;
-  constexpr size_t kStage = (size_t)(kEmBlock / 64) * 4096;
-  for (int pass = 0; pass < 2; pass++) {
-    const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
-    const size_t lds = tab + kStage;
-    int pc = env_int("BG_BLOCKS_PER_CU", 0);
-    if (pc <= 0) pc = occupancy(reinterpret_cast<const void *>(kern), kEmBlock, lds, 1);
-    const uint64_t cap = (uint64_t)num_cus * pc;
-    const uint64_t blocks = need > cap ? cap : need;
-    if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
-        !env_int("BG_FORCE_LDS", 0)) {
-      a.t.lds = kLdsNone;  // small launch: probe the table in L2 instead
-      continue;
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kEmBlock), lds, s, a);
-    return hipGetLastError();
-  }
-  return hipErrorInvalidValue;
-}
-
 bool slab_ok(const EmArgs &a) {
   return a.stride == 64 && !a.fp.direct && a.fp.win_lo >= 0 &&
          a.fp.win_lo + 16 * a.fp.nch <= 64 && ((uintptr_t)a.frames & 15) == 0 &&
-         !env_int("BG_NO_SLAB", 0);
+         !(path_flags() & kPathNoSlab);
 }
 
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
   if (slab_ok(a)) {
     const bool two = fits_nch2(a.fp);
 #define BG_SLAB(KW)                                                        \
@@ -1408,32 +1384,37 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
     BG_SLAB(1) BG_SLAB(2) BG_SLAB(4) BG_SLAB(8)
 #undef BG_SLAB
   }
-  if (env_int("BG_EM_PF", 0) && a.t.kw == 2 && fits_nch2(a.fp))
+#ifdef BG_AB
+  if (knob("BG_EM_PF", 0) && a.t.kw == 2 && fits_nch2(a.fp))
     return launch_classify(em_classify_pf_kernel<2, 2>, a, num_cus, s, 1);
-  if (env_int("BG_FAT", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {
-    if (env_int("BG_PPL", kDefaultPpl) == 2)
+  if (knob("BG_FAT", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {
+    if (knob("BG_PPL", kDefaultPpl) == 2)
       return launch_classify(em_classify_fat_kernel<2, 2, 2>, a, num_cus, s, 2);
     return launch_classify(em_classify_fat_kernel<2, 2, 1>, a, num_cus, s, 1);
   }
+#endif
   return dispatch<EmSel>(a, num_cus, s, kDefaultPpl);
 }
 
 hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
   if (a.t.lds == kLdsTags) {
-    if (!a.fp.direct && a.fp.nch <= 4) return launch_wm_tags(a, num_cus, s);
+    if (!a.fp.direct && a.fp.nch <= 4 && !(path_flags() & kPathNoLds))
+      return launch_wm_tags(a, num_cus, s);
     WmArgs b = a;  // fields too far apart for a window: probe in L2
     b.t.lds = kLdsNone;
     return dispatch<WmSel>(b, num_cus, s, 1);
   }
-  if (env_int("BG_WM_BLOCK", 512) == 1024 && a.t.kw == 2 && fits_nch2(a.fp)) {
-    if (env_int("BG_PPL", 1) == 2)
+#ifdef BG_AB
+  if (knob("BG_WM_BLOCK", 512) == 1024 && a.t.kw == 2 && fits_nch2(a.fp)) {
+    if (knob("BG_PPL", 1) == 2)
       return launch_classify(wm_classify_k1024_kernel<2>, a, num_cus, s, 2, 1024);
     return launch_classify(wm_classify_k1024_kernel<1>, a, num_cus, s, 1, 1024);
   }
-  const int v = env_int("BG_WM_V", 0), g = env_int("BG_WM_G", 4);
+  const int v = knob("BG_WM_V", 0), g = knob("BG_WM_G", 4);
   if (v && a.t.kw == 2 && fits_nch2(a.fp)) {
-    const int ppl = env_int("BG_PPL", 2);
-    const bool pf = env_int("BG_WM_PF", 0) != 0;
+    const int ppl = knob("BG_PPL", 2);
+    const bool pf = knob("BG_WM_PF", 0) != 0;
 #define BG_WMX(P, V, G, PF)                                                \
   if (ppl == P && v == V && (V == 1 || g == G) && pf == PF)                \
     return launch_classify(wm_classify_exp_kernel<P, V, G, PF>, a, num_cus, s, P);
@@ -1443,33 +1424,37 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
 #undef BG_WMX
     return hipErrorInvalidValue;
   }
+#endif
   return dispatch<WmSel>(a, num_cus, s, 1);
 }
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const bool tiled =
-      a.stride >= 128 && a.stride <= 2048 && !env_int("BG_CK_GENERIC", 0);
+  const bool tiled = a.stride >= 128 && a.stride <= 2048 &&
+                     !(path_flags() & kPathNoSlab) && !knob("BG_CK_GENERIC", 0);
   using CkKern = void (*)(CkArgs);
   CkKern kfn = cksum_kernel_generic;
   if (tiled) {
     // measured on MI355X (scripts/variants.py): re-reading the header line
     // in phase 3 beats holding it in registers; prefetch depth 2
-    switch (env_int("BG_CK_TILED", 0)) {
+    kfn = cksum_kernel<true, 2>;
+#ifdef BG_AB
+    switch (knob("BG_CK_TILED", 0)) {
       case 1: kfn = cksum_kernel<false, 1>; break;
       case 2: kfn = cksum_kernel<true, 1>; break;
       case 3: kfn = cksum_kernel<true, 3>; break;
       case 4: kfn = cksum_kernel<false, 2>; break;
       case 5: kfn = cksum_kernel_w5<true, 2>; break;
       case 6: kfn = cksum_kernel_w5<true, 3>; break;
-      default: kfn = cksum_kernel<true, 2>; break;
+      default: break;
     }
+#endif
   }
   const void *kern = reinterpret_cast<const void *>(kfn);
-  int per_cu = env_int("BG_CK_BLOCKS_PER_CU", 0);
+  int per_cu = knob("BG_CK_BLOCKS_PER_CU", 0);
   if (per_cu <= 0) {
     const int occ = occupancy(kern, kCkBlock, 0, 7);
-    per_cu = occ * std::max(1, env_int("BG_CK_GRID_MULT", 4));
+    per_cu = occ * std::max(1, knob("BG_CK_GRID_MULT", 4));
   }
   const uint64_t waves_per_block = kCkBlock / 64;
   const uint64_t max_waves = (uint64_t)num_cus * per_cu * waves_per_block;

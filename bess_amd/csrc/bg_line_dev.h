@@ -31,12 +31,12 @@
 #define BESS_AMD_BG_LINE_DEV_H_
 
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
 
 #include <algorithm>
 
 #include "bg_kernels.h"
 #include "bg_keys_dev.h"
+#include "bg_launch.h"
 
 namespace bg {
 namespace {
@@ -181,12 +181,7 @@ __device__ __forceinline__ uint32_t ip_dst_le(uint32_t (&d)[16]) {
 }
 
 inline int line_occupancy(const void *kern, size_t lds) {
-  int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kLineBlock, lds) !=
-          hipSuccess ||
-      occ <= 0)
-    occ = 1;
-  return occ;
+  return occupancy(kern, kLineBlock, lds, 1);
 }
 
 // Residency-sized grid; the slab shape for dense 64-byte slots.
@@ -195,7 +190,8 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const size_t tab = (Op::lds_bytes(a) + 15) & ~(size_t)15;
   const uint64_t need = (a.n + kLineBlock - 1) / kLineBlock;
-  if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 && !getenv("BG_NO_SLAB")) {
+  if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
+      !(path_flags() & kPathNoSlab)) {
     auto kern = line_slab_kernel<Op>;
     const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
     const int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);

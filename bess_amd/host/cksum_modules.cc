@@ -26,33 +26,6 @@ class ChecksumModule : public Module {
     return CommandSuccess();
   }
 
-  void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override {
-    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
-  }
-
-  int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                     size_t cnt) override {
-    if (cnt == 0) return 0;
-    heads_.resize(cnt);
-    gates_.resize(cnt);
-    uint32_t span = 0xFFFFFFFFu;
-    for (size_t i = 0; i < cnt; i++) {
-      heads_[i] = pkts[i]->head_data<uint8_t *>();
-      span = std::min(span, pkts[i]->span());
-    }
-    uint16_t *ipg = kMode == BG_CK_IP ? gates_.data() : nullptr;
-    uint16_t *l4g = kMode == BG_CK_L4 ? gates_.data() : nullptr;
-    int rc = bg_cksum_process_host(device_, heads_.data(), cnt, span, kMode,
-                                   verify_ ? 1 : 0, ipg, l4g, nullptr);
-    if (rc < 0) {
-      for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
-      return rc;
-    }
-    for (size_t i = 0; i < cnt; i++)
-      if (gates_[i] != BG_GATE_NONE) EmitPacket(ctx, pkts[i], gates_[i]);
-    return 0;
-  }
-
   // the whole frame goes to the device; the recomputed checksum words come
   // back (bg_pipe writes the header line back into the packet buffer)
   void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
@@ -70,8 +43,6 @@ class ChecksumModule : public Module {
 
  private:
   bool verify_ = false;
-  std::vector<uint8_t *> heads_;
-  std::vector<uint16_t> gates_;
 };
 
 template <int kMode>

@@ -92,30 +92,6 @@ class ExactMatch final : public Module {
     return buf;
   }
 
-  // exact_match.cc:224-244 on the GPU: the key window of every packet is
-  // staged, classified by em_classify_kernel, and each packet is emitted on
-  // its gate (default gate on a miss).
-  void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override {
-    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
-  }
-
-  int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                     size_t cnt) override {
-    if (cnt == 0) return 0;
-    const gate_idx_t default_gate = default_gate_;  // ACCESS_ONCE
-    heads_.resize(cnt);
-    gates_.resize(cnt);
-    for (size_t i = 0; i < cnt; i++) heads_[i] = pkts[i]->head_data<uint8_t *>();
-    int rc = bg_em_process_host(table_, heads_.data(), cnt, default_gate,
-                                gates_.data(), nullptr);
-    if (rc < 0) {
-      for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
-      return rc;
-    }
-    for (size_t i = 0; i < cnt; i++) EmitPacket(ctx, pkts[i], gates_[i]);
-    return 0;
-  }
-
   int ProcessDevice(void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     int rc = bg_em_sync(table_, device_, stream);
@@ -354,8 +330,6 @@ class ExactMatch final : public Module {
   gate_idx_t default_gate_ = DROP_GATE;
   bool empty_masks_ = true;
   bg_em *table_ = nullptr;
-  std::vector<const uint8_t *> heads_;
-  std::vector<uint16_t> gates_;
 };
 
 // exact_match.cc:45-60

@@ -118,40 +118,6 @@ class HashLB final : public Module {
     return buf;
   }
 
-  void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override {
-    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
-  }
-
-  // synchronous host path: stage the hash window, classify, emit
-  int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                     size_t cnt) override {
-    if (cnt == 0) return 0;
-    int lo, hi;
-    bool wb;
-    DeviceWindow(&lo, &hi, &wb);
-    const size_t w = ((size_t)(hi - lo) + 15) / 16 * 16;
-    std::vector<uint8_t> h((cnt + 4) * w, 0);
-    for (size_t i = 0; i < cnt; i++)
-      memcpy(h.data() + i * w, pkts[i]->head_data<uint8_t *>() + lo, (size_t)(hi - lo));
-    void *d_in = nullptr, *d_out = nullptr;
-    int rc = bg_malloc(device_, h.size(), &d_in);
-    if (rc == 0) rc = bg_malloc(device_, cnt * 2, &d_out);
-    if (rc == 0) rc = bg_memcpy_h2d(d_in, h.data(), h.size(), nullptr);
-    if (rc == 0)
-      rc = bg_hlb_classify(h_, d_in, w, cnt, lo, static_cast<uint16_t *>(d_out), nullptr);
-    std::vector<uint16_t> g(cnt);
-    if (rc == 0) rc = bg_memcpy_d2h(g.data(), d_out, cnt * 2, nullptr);
-    if (rc == 0) rc = bg_stream_sync(nullptr);
-    if (d_in) bg_free(d_in);
-    if (d_out) bg_free(d_out);
-    if (rc < 0) {
-      for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
-      return rc;
-    }
-    for (size_t i = 0; i < cnt; i++) EmitPacket(ctx, pkts[i], g[i]);
-    return 0;
-  }
-
   int ProcessDevice(void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_hlb_classify(h_, d_frames, stride, n, 0, d_ogates, stream);

@@ -112,38 +112,6 @@ class IPLookup final : public Module {
     return CommandSuccess();
   }
 
-  void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override {
-    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
-  }
-
-  // synchronous host path: stage bytes [0, 64), classify, emit
-  int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                     size_t cnt) override {
-    if (cnt == 0) return 0;
-    const size_t w = 64;
-    std::vector<uint8_t> h(cnt * w);
-    for (size_t i = 0; i < cnt; i++)
-      memcpy(h.data() + i * w, pkts[i]->head_data<uint8_t *>(), w);
-    void *d_in = nullptr, *d_out = nullptr;
-    int rc = bg_malloc(device_, h.size(), &d_in);
-    if (rc == 0) rc = bg_malloc(device_, cnt * 2, &d_out);
-    if (rc == 0) rc = bg_memcpy_h2d(d_in, h.data(), h.size(), nullptr);
-    if (rc == 0)
-      rc = bg_lpm_classify(lpm_, d_in, w, cnt, default_gate_,
-                           static_cast<uint16_t *>(d_out), nullptr);
-    std::vector<uint16_t> g(cnt);
-    if (rc == 0) rc = bg_memcpy_d2h(g.data(), d_out, cnt * 2, nullptr);
-    if (rc == 0) rc = bg_stream_sync(nullptr);
-    if (d_in) bg_free(d_in);
-    if (d_out) bg_free(d_out);
-    if (rc < 0) {
-      for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
-      return rc;
-    }
-    for (size_t i = 0; i < cnt; i++) EmitPacket(ctx, pkts[i], g[i]);
-    return 0;
-  }
-
   int ProcessDevice(void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_lpm_classify(lpm_, d_frames, stride, n, default_gate_, d_ogates,

@@ -6,8 +6,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <mutex>
+#include <shared_mutex>
 
 #include "../../include/bessgpu.h"
 #include "../csrc/bg_internal.h"
@@ -66,6 +69,59 @@ std::vector<std::string> ModuleBuilder::Classes() {
 
 using bg::fail;
 
+// The synchronous host datapath shared by every module (see module.h).
+int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) {
+  if (cnt == 0) return 0;
+  int lo, hi;
+  bool wb;
+  DeviceWindow(&lo, &hi, &wb);
+  uint32_t span = 0xFFFFFFFFu;
+  for (size_t i = 0; i < cnt; i++) span = std::min(span, pkts[i]->span());
+  if (hi > (int)span) hi = (int)span;
+  if (hi <= lo) hi = lo + 1;
+  const size_t len = (size_t)(hi - lo);
+  const size_t w = (len + 15) / 16 * 16;
+  const size_t line = std::min<size_t>(w, 128);  // header line written back
+  int r = bg::set_device(device_);
+  auto drop_all = [&](int rc) {
+    for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
+    return rc;
+  };
+  if (r) return drop_all(r);
+  bg::Staging &st = bg::thread_staging();
+  // +64 B: the last window's 16-byte loads may run past its slot
+  r = st.ensure(device_, cnt * w + 64, cnt * 2);
+  if (r) return drop_all(r);
+  hipStream_t s = bg::thread_stream(device_, nullptr);
+  for (size_t i = 0; i < cnt; i++) {
+    uint8_t *dst = st.h_in + i * w;
+    memcpy(dst, pkts[i]->head_data<uint8_t *>() + lo, len);
+    if (w > len) memset(dst + len, 0, w - len);
+  }
+  uint16_t *d_g = reinterpret_cast<uint16_t *>(st.d_out);
+  hipError_t e = hipMemcpyAsync(st.d_in, st.h_in, cnt * w, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return drop_all(fail(EIO, "H2D: %s", hipGetErrorString(e)));
+  r = ProcessDeviceWindow(st.d_in, w, cnt, lo, d_g, s);
+  if (r < 0) {
+    (void)hipStreamSynchronize(s);
+    return drop_all(r);
+  }
+  e = hipMemcpyAsync(st.h_out, d_g, cnt * 2, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && wb)
+    e = hipMemcpy2DAsync(st.h_in, line, st.d_in, w, line, cnt,
+                         hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return drop_all(fail(EIO, "D2H: %s", hipGetErrorString(e)));
+  const uint16_t *g = reinterpret_cast<const uint16_t *>(st.h_out);
+  for (size_t i = 0; i < cnt; i++) {
+    if (wb && lo == 0)
+      memcpy(pkts[i]->head_data<uint8_t *>(), st.h_in + i * line,
+             std::min(line, len));
+    if (g[i] != BG_GATE_NONE) EmitPacket(ctx, pkts[i], g[i]);
+  }
+  return 0;
+}
+
 static int respond(const CommandResponse &r) {
   if (r.code() != 0) return fail(r.code(), "%s", r.errmsg().c_str());
   bg::g_err.clear();
@@ -93,10 +149,15 @@ void bg_module_destroy(bg_module *m) { delete m; }
 // ModuleBuilder::RunCommand (core/module.cc:92-116)
 int bg_module_command(bg_module *h, const char *cmd, const void *arg,
                       size_t arg_len, void *out, size_t *out_len) {
-  std::lock_guard<std::mutex> lk(h->mu);
   const std::string user_cmd = cmd ? cmd : "";
   for (const Command &c : h->m->cmds()) {
     if (c.cmd != user_cmd) continue;
+    std::shared_lock<std::shared_mutex> shared(h->mu, std::defer_lock);
+    std::unique_lock<std::shared_mutex> excl(h->mu, std::defer_lock);
+    if (c.mt_safe == Command::THREAD_SAFE)
+      shared.lock();
+    else
+      excl.lock();
     CommandResponse r = c.func(h->m.get(), arg, arg_len);
     if (r.code() != 0) return respond(r);
     const std::string &d = r.data();
@@ -114,9 +175,9 @@ int bg_module_command(bg_module *h, const char *cmd, const void *arg,
               user_cmd.c_str());
 }
 
-int bg_module_process(bg_module *h, uint8_t *const *heads, size_t cnt,
-                      uint16_t *ogates) {
-  std::lock_guard<std::mutex> lk(h->mu);
+static int process(bg_module *h, uint8_t *const *heads, size_t cnt,
+                   uint16_t *ogates, EmitLog *log) {
+  std::shared_lock<std::shared_mutex> lk(h->mu);  // many workers at once
   for (size_t i = 0; i < cnt; i++) ogates[i] = BG_GATE_NONE;
   std::vector<bess::Packet> pkts(cnt);
   std::vector<bess::Packet *> ptrs(cnt);
@@ -126,9 +187,40 @@ int bg_module_process(bg_module *h, uint8_t *const *heads, size_t cnt,
   }
   Context ctx;
   ctx.ogates = ogates;
+  ctx.log = log;
   bg::g_err.clear();
-  int r = h->m->ProcessPackets(&ctx, ptrs.data(), cnt);
-  return r;
+  return h->m->ProcessPackets(&ctx, ptrs.data(), cnt);
+}
+
+int bg_module_process(bg_module *h, uint8_t *const *heads, size_t cnt,
+                      uint16_t *ogates) {
+  return process(h, heads, cnt, ogates, nullptr);
+}
+
+int bg_module_process_batches(bg_module *h, uint8_t *const *heads, size_t cnt,
+                              uint16_t *ogates, uint16_t *batch_gate,
+                              uint32_t *batch_len, uint32_t *pkt_idx,
+                              size_t *nbatches, size_t *ndead) {
+  EmitLog log;
+  int r = process(h, heads, cnt, ogates, &log);
+  if (r < 0) return r;
+  size_t k = 0;
+  for (size_t b = 0; b < log.batches.size(); b++) {
+    batch_gate[b] = log.batches[b].gate;
+    batch_len[b] = (uint32_t)log.batches[b].pkts.size();
+    for (uint32_t i : log.batches[b].pkts) pkt_idx[k++] = i;
+  }
+  for (uint32_t i : log.dead) pkt_idx[k++] = i;
+  *nbatches = log.batches.size();
+  *ndead = log.dead.size();
+  return 0;
+}
+
+int bg_module_connect(bg_module *h, uint16_t ogate, int connected) {
+  if (ogate >= MAX_GATES) return fail(EINVAL, "ogate %hu not in [0,%d)", ogate, MAX_GATES);
+  std::unique_lock<std::shared_mutex> lk(h->mu);
+  h->m->ConnectOGate(ogate, connected != 0);
+  return 0;
 }
 
 int bg_module_process_device(bg_module *h, void *d_frames, size_t stride,
@@ -155,7 +247,7 @@ int bg_module_bind_meta(bg_module *h, int meta_off, const char *const *names,
     nm.emplace_back(names[i] ? names[i] : "");
     off.push_back(offsets[i]);
   }
-  std::lock_guard<std::mutex> lk(h->mu);
+  std::unique_lock<std::shared_mutex> lk(h->mu);
   bg::g_err.clear();
   int r = h->m->BindMeta(meta_off, nm, off);
   if (r == -ENOTSUP && bg::g_err.empty())

@@ -21,7 +21,7 @@
 #include <functional>
 #include <map>
 #include <memory>
-#include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -71,10 +71,26 @@ class PacketBatch {
 
 }  // namespace bess
 
-// Per-call context (core/module.h:59-75): here it records where each packet
-// was emitted.
+// The batches a Task would run after one ProcessBatch call: EmitPacket
+// appends each packet to its output gate's batch and starts a new batch
+// when that one holds kMaxBurst packets (core/module.h:543-594; the igate
+// batches go onto the task's run list in the order they were started,
+// Task::AddToRun); DropPacket collects the dead batch (534-541).
+struct EmitLog {
+  struct Batch {
+    gate_idx_t gate;
+    std::vector<uint32_t> pkts;  // Packet::index() of each packet, in order
+  };
+  std::vector<Batch> batches;    // AddToRun order
+  std::vector<uint32_t> dead;    // dropped packets, in drop order
+  std::map<gate_idx_t, size_t> open;  // gate -> its batch being filled
+};
+
+// Per-call context (core/module.h:59-75): where each packet went.
 struct Context {
-  uint16_t *ogates = nullptr;  // indexed by Packet::index()
+  uint16_t *ogates = nullptr;  // indexed by Packet::index(); DROP_GATE: dropped
+  EmitLog *log = nullptr;      // optional: the gate batches
+  uint64_t deadends = 0;       // deadends_[ctx->wid] (module.h:455)
 };
 
 class CommandResponse {
@@ -127,19 +143,20 @@ std::function<CommandResponse(Module *, const void *, size_t)> ModuleCmdFunc(
 class Module {
  public:
   virtual ~Module() = default;
-  virtual void ProcessBatch(Context *ctx, bess::PacketBatch *batch) = 0;
-  // Any number of packets in one call (the GPU modules run them as one
-  // device batch; BESS hands ProcessBatch <= 32). Returns 0 or -errno.
-  virtual int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                             size_t cnt) {
-    for (size_t i = 0; i < cnt; i += bess::PacketBatch::kMaxBurst) {
-      bess::PacketBatch b;
-      for (size_t j = i; j < cnt && j < i + bess::PacketBatch::kMaxBurst; j++)
-        b.add(pkts[j]);
-      ProcessBatch(ctx, &b);
-    }
-    return 0;
+  // core/module.h:226: every module runs its batch on the device through
+  // ProcessPackets
+  virtual void ProcessBatch(Context *ctx, bess::PacketBatch *batch) {
+    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
   }
+  // Any number of packets in one synchronous call (BESS hands ProcessBatch
+  // <= 32): the DeviceWindow bytes of each packet are staged in the calling
+  // thread's pinned buffers, ProcessDeviceWindow runs on the thread's own
+  // stream, the gates (and, for writing modules, the header lines) come
+  // back, then each packet is emitted on its gate (BG_GATE_NONE: not
+  // emitted). Re-entrant: many workers may run it on one module at once
+  // (module.cc). Returns 0 or -errno (every packet dropped).
+  virtual int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
+                             size_t cnt);
   virtual std::string GetDesc() const { return ""; }
   virtual const Commands &cmds() const = 0;
   // Device-resident datapath over a frame slab (libbessgpu.so).
@@ -204,18 +221,53 @@ class Module {
   }
   const std::vector<Attribute> &all_attrs() const { return attrs_; }
 
-  // core/module.h:543-594: the chosen gate is recorded for the packet.
-  void EmitPacket(Context *ctx, bess::Packet *pkt, gate_idx_t ogate) {
-    ctx->ogates[pkt->index()] = ogate;
+  // Output gates the pipeline connected (ConnectModules). Until the first
+  // ConnectOGate every gate < MAX_GATES counts as connected.
+  void ConnectOGate(gate_idx_t g, bool on) {
+    if (!explicit_ogates_) {
+      ogates_.clear();
+      explicit_ogates_ = true;
+    }
+    if (g >= ogates_.size()) ogates_.resize((size_t)g + 1, false);
+    ogates_[g] = on;
   }
+  bool OGateConnected(gate_idx_t g) const {
+    if (!explicit_ogates_) return g < MAX_GATES;
+    return g < ogates_.size() && ogates_[g];
+  }
+
+  // core/module.h:543-594: a gate that is out of range or not connected
+  // drops the packet (546-549); otherwise the packet joins the gate's batch.
+  void EmitPacket(Context *ctx, bess::Packet *pkt, gate_idx_t ogate) {
+    if (!OGateConnected(ogate)) {
+      DropPacket(ctx, pkt);
+      return;
+    }
+    ctx->ogates[pkt->index()] = ogate;
+    if (EmitLog *l = ctx->log) {
+      auto it = l->open.find(ogate);
+      if (it == l->open.end() ||
+          l->batches[it->second].pkts.size() >= bess::PacketBatch::kMaxBurst) {
+        l->batches.push_back(EmitLog::Batch{ogate, {}});
+        l->open[ogate] = l->batches.size() - 1;
+        it = l->open.find(ogate);
+      }
+      l->batches[it->second].pkts.push_back(pkt->index());
+    }
+  }
+  // core/module.h:534-541
   void DropPacket(Context *ctx, bess::Packet *pkt) {
     ctx->ogates[pkt->index()] = DROP_GATE;
+    ctx->deadends++;
+    if (ctx->log) ctx->log->dead.push_back(pkt->index());
   }
 
  protected:
   int device_ = 0;
   gate_idx_t igate_ = 0;
   std::vector<Attribute> attrs_;
+  std::vector<bool> ogates_;
+  bool explicit_ogates_ = false;
 };
 
 // ModuleBuilder (core/module.h:108-172): class name -> factory taking the
@@ -263,7 +315,10 @@ ModuleBuilder::Factory MakeFactory() {
 struct bg_module {
   std::unique_ptr<Module> m;
   std::string mclass;
-  std::mutex mu;  // commands vs. process (THREAD_UNSAFE commands)
+  // ProcessBatch calls and THREAD_SAFE commands share it; THREAD_UNSAFE
+  // commands (which bessd runs only with workers paused,
+  // core/module.cc:97-101) take it exclusively
+  std::shared_mutex mu;
 };
 
 #endif  // BESS_AMD_HOST_MODULE_H_

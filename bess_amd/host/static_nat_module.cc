@@ -92,42 +92,6 @@ class StaticNAT final : public Module {
   CommandResponse GetRuntimeConfig(const EmptyArg &) { return CommandSuccess(); }
   CommandResponse SetRuntimeConfig(const EmptyArg &) { return CommandSuccess(); }
 
-  void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override {
-    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
-  }
-
-  // synchronous host path: the header (first 128 bytes) round-trips
-  int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                     size_t cnt) override {
-    if (cnt == 0) return 0;
-    const size_t w = 128;
-    std::vector<uint8_t> h(cnt * w);
-    for (size_t i = 0; i < cnt; i++)
-      memcpy(h.data() + i * w, pkts[i]->head_data<uint8_t *>(), w);
-    void *d_in = nullptr, *d_out = nullptr;
-    int rc = bg_malloc(device_, h.size(), &d_in);
-    if (rc == 0) rc = bg_malloc(device_, cnt * 2, &d_out);
-    if (rc == 0) rc = bg_memcpy_h2d(d_in, h.data(), h.size(), nullptr);
-    if (rc == 0)
-      rc = bg_snat_classify(h_, d_in, w, cnt, igate_ ? 1 : 0,
-                            static_cast<uint16_t *>(d_out), nullptr);
-    std::vector<uint16_t> g(cnt);
-    if (rc == 0) rc = bg_memcpy_d2h(g.data(), d_out, cnt * 2, nullptr);
-    if (rc == 0) rc = bg_memcpy_d2h(h.data(), d_in, h.size(), nullptr);
-    if (rc == 0) rc = bg_stream_sync(nullptr);
-    if (d_in) bg_free(d_in);
-    if (d_out) bg_free(d_out);
-    if (rc < 0) {
-      for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
-      return rc;
-    }
-    for (size_t i = 0; i < cnt; i++) {
-      memcpy(pkts[i]->head_data<uint8_t *>(), h.data() + i * w, w);
-      EmitPacket(ctx, pkts[i], g[i]);
-    }
-    return 0;
-  }
-
   int ProcessDevice(void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_snat_classify(h_, d_frames, stride, n, igate_ ? 1 : 0, d_ogates,

@@ -82,28 +82,6 @@ class WildcardMatch final : public Module {
     return buf;
   }
 
-  // wildcard_match.cc:159-203 on the GPU
-  void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override {
-    ProcessPackets(ctx, batch->pkts(), (size_t)batch->cnt());
-  }
-
-  int ProcessPackets(Context *ctx, bess::Packet *const *pkts,
-                     size_t cnt) override {
-    if (cnt == 0) return 0;
-    const gate_idx_t default_gate = default_gate_;
-    heads_.resize(cnt);
-    gates_.resize(cnt);
-    for (size_t i = 0; i < cnt; i++) heads_[i] = pkts[i]->head_data<uint8_t *>();
-    int rc = bg_wm_process_host(table_, heads_.data(), cnt, default_gate,
-                                gates_.data(), nullptr);
-    if (rc < 0) {
-      for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
-      return rc;
-    }
-    for (size_t i = 0; i < cnt; i++) EmitPacket(ctx, pkts[i], gates_[i]);
-    return 0;
-  }
-
   int ProcessDevice(void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     int rc = bg_wm_sync(table_, device_, stream);
@@ -301,8 +279,6 @@ class WildcardMatch final : public Module {
   size_t total_key_size_ = 0;
   std::vector<WmField> fields_;
   bg_wm *table_ = nullptr;
-  std::vector<const uint8_t *> heads_;
-  std::vector<uint16_t> gates_;
 };
 
 // wildcard_match.cc:58-73

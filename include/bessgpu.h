@@ -24,7 +24,10 @@
  *             per-packet EmitPacket gate (core/module.h:543).
  *
  * Device pointers (d_*) are HIP device memory on the handle's device;
- * `stream` is a hipStream_t (NULL = the legacy default stream).
+ * `stream` is a hipStream_t. NULL means the legacy default stream for the
+ * device-slab calls, and the calling thread's own non-blocking stream for
+ * the synchronous host paths (*_process_host, bg_module_process), so that
+ * worker threads never serialise on one stream.
  * Frame slabs: frame i starts at d_frames + i*stride (= Packet::head_data(),
  * core/packet.h:84-94); stride must be a multiple of 16 and d_frames 16-byte
  * aligned.
@@ -175,6 +178,22 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
                           uint16_t *ip_gates, uint16_t *l4_gates,
                           bg_stream_t stream);
 
+/* ---- kernel paths (parity tests) ---------------------------------------- */
+/* Several kernels compute each result (flow table staged in LDS or probed in
+ * L2; coalesced 64-byte-slot slab shape or one packet per lane; for
+ * WildcardMatch tag words in LDS or a key filter). bg_set_path_flags picks
+ * among them process-wide so the parity tests can run every path against
+ * the oracle; no result depends on the flags. 0 = the measured defaults.
+ * The product library reads no environment variable. */
+#define BG_PATH_FORCE_LDS 1
+#define BG_PATH_NO_LDS 2
+#define BG_PATH_NO_SLAB 4
+#define BG_PATH_WM_NO_TAGS 8
+int bg_set_path_flags(uint32_t flags);
+uint32_t bg_get_path_flags(void);
+/* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */
+int bg_is_ab_build(void);
+
 /* ---- diagnostics ------------------------------------------------------- */
 /* The key the classify kernels build for `frame` from `fields` (em_masks 1:
  * ExactMatch field masks applied; 0: WildcardMatch raw field bytes), run on
@@ -316,9 +335,27 @@ void bg_module_destroy(bg_module *m);
 int bg_module_command(bg_module *m, const char *cmd, const void *arg,
                       size_t arg_len, void *out, size_t *out_len);
 /* ProcessBatch over cnt <= any packets: heads[i] = head_data() of packet i;
- * ogates[i] = the gate EmitPacket would receive (BG_GATE_NONE: none). */
+ * ogates[i] = the output gate packet i left on, BG_DROP_GATE if it was
+ * dropped (DropPacket, or EmitPacket to a gate that is out of range or not
+ * connected, core/module.h:546-549), BG_GATE_NONE if it was not emitted.
+ * Synchronous; may be called from many worker threads at once (each stages
+ * into its own pinned buffers on its own HIP stream; core/module.h:485). */
 int bg_module_process(bg_module *m, uint8_t *const *heads, size_t cnt,
                       uint16_t *ogates);
+/* bg_module_process plus the batches the Task would run next
+ * (core/module.h:543-618): per output gate, packets in emission order cut
+ * into batches of <= 32 (PacketBatch::kMaxBurst), in the order the batches
+ * were started (Task::AddToRun). batch_gate / batch_len get *nbatches
+ * entries; pkt_idx lists the batches' packet indices back to back, then the
+ * *ndead dropped packets in drop order. Capacities: cnt each. */
+int bg_module_process_batches(bg_module *m, uint8_t *const *heads, size_t cnt,
+                              uint16_t *ogates, uint16_t *batch_gate,
+                              uint32_t *batch_len, uint32_t *pkt_idx,
+                              size_t *nbatches, size_t *ndead);
+/* Output gate `ogate` connected (1) or not (0) to a next module
+ * (ConnectModules). Until the first call every gate < BG_MAX_GATES counts
+ * as connected. EmitPacket to an unconnected gate drops the packet. */
+int bg_module_connect(bg_module *m, uint16_t ogate, int connected);
 /* Device-resident ProcessBatch over a slab. */
 int bg_module_process_device(bg_module *m, void *d_frames, size_t stride,
                              size_t n, uint16_t *d_ogates, bg_stream_t stream);

@@ -2,9 +2,11 @@
 """A/B launch variants of the classify / checksum kernels in ONE process,
 interleaved over several rounds (cdna_hip_programming.md §5.4 rule 24).
 
-Variants are selected through the BG_* environment knobs read by the
-launchers in bess_amd/csrc/bg_kernels.hip. Prints one JSON line per kernel
-family with median / min milliseconds per launch for each variant.
+Variants are selected through the BG_* environment knobs, which only the
+measurement build libbessgpu_ab.so reads (`make -C bess_amd/csrc ab`; the
+product libbessgpu.so has no knobs and no A/B kernels). Prints one JSON line
+per kernel family with median / min milliseconds per launch for each
+variant.
 """
 import json
 import os
@@ -16,6 +18,11 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+from bess_amd import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.path.join(ROOT, "bess_amd", "libbessgpu_ab.so")
+assert _lib.lib().bg_is_ab_build() == 1, "variants.py needs libbessgpu_ab.so"
 
 from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402

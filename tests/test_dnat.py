@@ -258,3 +258,48 @@ def test_gpu_vs_reference_module_test(case):
         f[:] = d.cpu().numpy().reshape(f.shape)
         return og.cpu().numpy().view(np.uint16)
     module_test_case(*case, process)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["hit_first", "new_first", "interleaved"])
+def test_gpu_expired_hits_in_order(order):
+    """Every batch takes the fused pass: a forward hit on a
+    mapping that has expired at `now` is not final -- a new flow earlier in
+    the batch may evict it (CreateNewEntry, nat.cc:224-231), and a hit
+    earlier in the batch refreshes it so that it can no longer be evicted
+    (nat.cc:350-352) -- so such hits are listed and walked in packet order
+    with the misses. Three external ports (3000..3002), three mappings of
+    which two have idled past 300 s, and a new flow that must take a port."""
+    import torch
+    from bess_amd.modules import NAT
+    ext = [{"ext_addr": "10.9.0.9", "port_ranges": [{"begin": 3000, "end": 3002}]}]
+    rng = np.random.default_rng(5)
+    for seed in range(6):
+        m, o = NAT(ext_addrs=ext, seed=seed), OM.OracleNAT(ext_addrs=ext, seed=seed)
+        src = np.array([0xC0A80001, 0xC0A80002, 0xC0A80003, 0xC0A80004], np.uint64)
+        sport = np.array([4001, 4002, 4003, 4004])
+        dst = np.full(4, 0x08080808, np.uint64)
+        dport = np.full(4, 53)
+        proto = np.full(4, 17)
+        f = frames(src, sport, dst, dport, proto, np.zeros(4, int), rng,
+                   ihl=np.full(4, 5))
+        A, B, C, D = (f[i:i + 1] for i in range(4))
+
+        def run(batch, now):
+            ref = batch.copy()
+            want = o.process(ref, STRIDE, len(batch), 0, now)
+            d = torch.from_numpy(batch.reshape(-1).copy()).cuda()
+            og = torch.zeros(len(batch), dtype=torch.int16, device="cuda")
+            m.process_device(d, STRIDE, len(batch), og, now, igate=0)
+            got = d.cpu().numpy().reshape(len(batch), STRIDE)
+            assert (og.cpu().numpy().view(np.uint16) == want).all(), (order, seed)
+            assert (got == ref).all(), (order, seed)
+            return want
+
+        assert list(run(np.concatenate([A, B, C]), T0)) == [1, 1, 1]
+        run(A, T0 + 100 * 10**9)                      # A stays fresh
+        now = T0 + 350 * 10**9                        # B and C have expired
+        batch = {"hit_first": [B, D, C, B], "new_first": [D, B, C, B],
+                 "interleaved": [C, D, B, A, D, C]}[order]
+        run(np.concatenate(batch), now)
+        run(np.concatenate([A, B, C, D]), now + 1)

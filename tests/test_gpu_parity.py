@@ -4,7 +4,6 @@ Marked gpu: runs on a real MI355X. Every comparison is bit-exact (gates,
 checksum words, whole frames after in-place checksum writes).
 """
 import ctypes as C
-import os
 
 import numpy as np
 import pytest
@@ -13,6 +12,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from bess_amd import _lib as LB  # noqa: E402
 from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 from oracle import oracle as O  # noqa: E402
@@ -28,34 +28,25 @@ def to_dev(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).to(dev)
 
 
-# launcher choices (BG_* knobs of bg_kernels.hip): where the table is probed
-# -- its own choice (LDS for tables <= 40 KB on launches with >= 4096 packets
-# per workgroup, else L2), forced LDS, forced L2 -- and, for dense 64 B
-# slots, the coalesced slab kernel (default) or the one-slot-per-lane one
-TABLE_PATHS = ({}, {"BG_FORCE_LDS": "1"}, {"BG_NOLDS": "1"},
-               {"BG_NO_SLAB": "1"}, {"BG_NO_SLAB": "1", "BG_FORCE_LDS": "1"})
+# kernel paths (bg_set_path_flags): where the table is probed -- its own
+# choice (LDS for tables <= 40 KB on launches with >= 4096 packets per
+# workgroup, else L2), forced LDS, forced L2 -- and, for dense 64 B slots,
+# the coalesced slab kernel (default) or the one-slot-per-lane one
+TABLE_PATHS = (0, LB.BG_PATH_FORCE_LDS, LB.BG_PATH_NO_LDS, LB.BG_PATH_NO_SLAB,
+               LB.BG_PATH_NO_SLAB | LB.BG_PATH_FORCE_LDS)
 
 
 def classify_all_paths(t, d_frames, stride, n, default_gate, dev):
     """Gates from every table path; asserts they agree, returns them."""
     outs = []
-    for env in TABLE_PATHS:
-        old = {k: os.environ.get(k)
-               for k in ("BG_FORCE_LDS", "BG_NOLDS", "BG_NO_SLAB")}
-        os.environ.update(env)
-        try:
+    for flags in TABLE_PATHS:
+        with LB.kernel_paths(flags):
             d_g = torch.zeros(n, dtype=torch.int16, device=dev)
             t.classify(d_frames, stride, n, default_gate, d_g)
             torch.cuda.synchronize()
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
         outs.append(d_g.cpu().numpy().view(np.uint16))
-    for o, env in zip(outs[1:], TABLE_PATHS[1:]):
-        assert (o == outs[0]).all(), env
+    for o, flags in zip(outs[1:], TABLE_PATHS[1:]):
+        assert (o == outs[0]).all(), flags
     return outs[0]
 
 
@@ -208,6 +199,21 @@ def test_em_sharded_build_matches_single(dev):
 
 
 # ---------------------------------------------------------- WildcardMatch
+def classify_all_paths_wm(t, d_frames, stride, n, default_gate, dev, tags):
+    """classify_all_paths with BG_PATH_WM_NO_TAGS kept on (tags == 0)"""
+    keep = 0 if tags else LB.BG_PATH_WM_NO_TAGS
+    outs = []
+    for flags in TABLE_PATHS:
+        with LB.kernel_paths(flags | keep):
+            d_g = torch.zeros(n, dtype=torch.int16, device=dev)
+            t.classify(d_frames, stride, n, default_gate, d_g)
+            torch.cuda.synchronize()
+        outs.append(d_g.cpu().numpy().view(np.uint16))
+    for o, flags in zip(outs[1:], TABLE_PATHS[1:]):
+        assert (o == outs[0]).all(), flags
+    return outs[0]
+
+
 def oracle_wm(fields, rkeys, rmasks, prio, gates):
     L = O.lib()
     wm = L.or_wm_new()
@@ -247,11 +253,10 @@ def test_wm_module_kat(golden, dev):
 @pytest.mark.parametrize("n_rules,n_pkts,tags", [
     (64, 4096, 1), (5000, 65536, 1), (5000, 65536, 0), (100000, 131072, 1),
     (100000, 131072, 0), (300000, 65536, 1)])
-def test_wm_vs_oracle(n_rules, n_pkts, tags, dev, monkeypatch):
+def test_wm_vs_oracle(n_rules, n_pkts, tags, dev):
     """tags 1: tables past the whole-table LDS size keep their tag words in
-    LDS (bg_wm.hip) when they fit; 0 (BG_WM_TAGS=0): the key-filter path;
-    300 K rules: tags too big for LDS, the key-filter path either way"""
-    monkeypatch.setenv("BG_WM_TAGS", str(tags))
+    LDS (bg_wm.hip) when they fit; 0 (BG_PATH_WM_NO_TAGS): the key-filter
+    path; 300 K rules: tags too big for LDS, the key-filter path either way"""
     rk, rm, prio, gates, frames, _ = P.wm_workload(n_rules, n_pkts,
                                                   seed=n_rules, stride=64,
                                                   sizes=((60, 1),))
@@ -259,7 +264,9 @@ def test_wm_vs_oracle(n_rules, n_pkts, tags, dev, monkeypatch):
     for k, m, p, g in zip(rk, rm, prio, gates):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
     assert t.num_tuples() == 8
-    got = classify_all_paths(t, to_dev(frames, dev), 64, n_pkts, 77, dev)
+    with LB.kernel_paths(0 if tags else LB.BG_PATH_WM_NO_TAGS):
+        got = classify_all_paths_wm(t, to_dev(frames, dev), 64, n_pkts, 77,
+                                    dev, tags)
     wm = oracle_wm(P.FIVE_TUPLE, rk, rm, prio, gates)
     want = np.zeros(n_pkts, np.uint16)
     O.lib().or_wm_process(wm, frames.ctypes.data, 64, n_pkts, 77,
