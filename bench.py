@@ -11,17 +11,28 @@ resident slab.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rules R]
     torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
 
-N > 1: every rank owns its own 16 M packets (weak scaling, no data-path
-collective). The rule table is built sharded: rank r builds partition r of
-the flow table and an RCCL all-gather over xGMI assembles the replicated
-table on every GPU (the only collective; control path, timed separately).
+`--gpus N` without torchrun starts the N ranks itself (torch.distributed.run
+as a child process, before anything touches a GPU) and exits with its code;
+under torchrun WORLD_SIZE must equal N.
 
-Rank 0 prints ONE JSON line. Secondary configs (C3 checksum, C4 wildcard,
-batch-size sweep) are measured at N = 1 only, as extra keys.
+N > 1: every rank owns its own 16 M packets (weak scaling, no data-path
+collective). The headline stays C2 at every N so the driver's per-N values
+compare like with like. The line also carries C5 at that N: 1 M rules
+sharded over the N GPUs -- rank r inserts only partition r's rules, the
+ranks agree on the layout with an all-reduce, build their partition, and
+one RCCL all-gather over xGMI assembles the replicated table on every GPU
+(the only collective; control path, timed separately) -- then every rank
+classifies its own 16 M packets through the gathered 1 M-rule table.
+
+Rank 0 prints ONE JSON line. Secondary configs (C1 CPU plumbing, C3
+checksum, C4 wildcard, the §8f modules, batch-size sweeps, host legs) are
+measured at N = 1 only, as extra keys.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -53,7 +64,13 @@ def parse():
                     help="skip the host end-to-end legs (16 launching threads "
                          "crash rocprofv3's kernel tracer)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
-    ap.add_argument("--only", default="", help="cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|pipe (profiling runs)")
+    ap.add_argument("--cpu-table-only", action="store_true",
+                    help="no GPU: the N-rank sharded table build of C5 over "
+                         "gloo (CPU tests of the multi-GPU launch and control "
+                         "path); prints the line with value null")
+    ap.add_argument("--c5-rules", type=int, default=1 << 20,
+                    help="rules of the sharded C5 table in the N > 1 line")
+    ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|pipe (profiling runs)")
     return ap.parse_args()
 
 
@@ -103,7 +120,7 @@ def em_setup(args, rank, world, dev, torch, dist):
     from bess_amd import flowtable as F
     from bess_amd import packets as P
     t0 = time.time()
-    # same rules on every rank, rank-specific packets
+    # same rule set on every rank, rank-specific packets
     keys, gates, frames = P.em_workload(args.rules, args.pkts, seed=0x5EED,
                                         pkt_seed=0x5EED + 7919 * rank)
     log("[rank %d] workload generated in %.1fs" % (rank, time.time() - t0))
@@ -112,9 +129,12 @@ def em_setup(args, rank, world, dev, torch, dist):
     d_gates = torch.empty(args.pkts, dtype=torch.int16, device=dev)
     t = F.EmTable(P.em_fields_5tuple())
     t0 = time.time()
-    t.add_many(keys, gates)
+    if world > 1:  # this rank's partition only
+        t.add_many(keys, gates, part=rank, nparts=world)
+    else:
+        t.add_many(keys, gates)
     log("[rank %d] %d rules inserted in %.1fs" % (rank, len(t), time.time() - t0))
-    table = {"rules": len(t)}
+    table = {"rules": len(keys)}
     if world > 1:
         # sharded build + RCCL all-gather of the partition images
         from bess_amd import dist as D
@@ -138,34 +158,57 @@ def em_parity_sample(t, d_frames, d_gates, keys, gates, n, torch):
     frames = d_frames[:n * 64].cpu().numpy()
     got = d_gates[:n].cpu().numpy().view(np.uint16)
     L = O.lib()
-    em = L.or_em_new()
-    for i, (off, size) in enumerate(P.FIVE_TUPLE):
-        L.or_em_add_field(em, off, size, 0, i, None, 0)
-    sizes = [s for _, s in P.FIVE_TUPLE]
-    pos = np.cumsum([0] + sizes)
-    ptrs = (C.c_void_p * 5)()
-    lens = (C.c_size_t * 5)(*sizes)
-    keys = np.ascontiguousarray(keys)
-    for k, g in zip(keys, gates):
-        for j in range(5):
-            ptrs[j] = k.ctypes.data + int(pos[j])
-        L.or_em_add_rule(em, int(g), ptrs, lens, 5, None, 0)
+    em = oracle_em_bulk(keys, gates)
     want = np.zeros(n, np.uint16)
     L.or_em_process(em, frames.ctypes.data, 64, n, 8192, want.ctypes.data)
     L.or_em_free(em)
     return bool((got == want).all())
 
 
-def cpu_rate(bench, n, seconds):
+def cpu_info():
+    """The host CPUs a CPU baseline may use: every CPU of the affinity mask
+    within the lease's CPU share (the GPU pool sets OMP_NUM_THREADS to the
+    CPUs it grants one GPU's job; nproc reports the whole machine). Returns
+    (threads, record for the JSON line)."""
+    aff = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    share = int(share) if share and share.isdigit() and int(share) > 0 else aff
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    threads = max(1, min(aff, share))
+    return threads, {"nproc": os.cpu_count(), "affinity_cpus": aff,
+                     "lease_cpu_share": share, "cpu_model": model}
+
+
+def cpu_baseline(res, threads, sample, kind="port", unit="Mpps"):
+    """cpu_baseline object: `res` {threads: rate} at 1 and T threads"""
+    _, info = cpu_info()
+    out = {"value": round(res[threads], 2), "unit": unit, "cores": threads,
+           "kind": kind, "single_core_mpps": round(res[1], 2), "sample": sample}
+    out.update(info)
+    return out
+
+
+def cpu_rate(bench, n, seconds, threads=None, max_reps=None):
     """Time the oracle's pthread bench driver `bench(nthreads, reps)` (returns
-    seconds) at 1 thread and at T = min(16, usable cores) threads; about
-    `seconds` of CPU work in total. Returns (T, {threads: Mpps})."""
-    from oracle import oracle as O
-    threads = max(1, min(16, O.lib().or_num_cpus()))
+    seconds) at 1 thread and at T threads (default: every CPU the lease
+    grants, cpu_info); about `seconds` of CPU work in total. Returns
+    (T, {threads: Mpps})."""
+    if threads is None:
+        threads, _ = cpu_info()
     res = {}
     for nt in sorted({1, threads}):
         t1 = bench(nt, 1)
         reps = max(1, int(seconds / 2 / max(t1, 1e-6)))
+        if max_reps:
+            reps = min(reps, max_reps)
         res[nt] = n * reps / bench(nt, reps) / 1e6
     return threads, res
 
@@ -195,20 +238,14 @@ def cpu_baseline_em(keys, gates, seconds):
     snb[:, 512:512 + 64] = frames
     base = snb.ctypes.data + 512
     out = np.zeros(n, np.uint16)
-    threads = max(1, min(16, L.or_num_cpus()))
-    res = {}
-    for nt in sorted({1, threads}):
-        t1 = L.or_em_bench(em, base, 2624, n, 8192, out.ctypes.data, nt, 1)
-        reps = max(1, int(seconds / 2 / max(t1, 1e-6)))
-        dt = L.or_em_bench(em, base, 2624, n, 8192, out.ctypes.data, nt, reps)
-        res[nt] = n * reps / dt / 1e6
+    threads, res = cpu_rate(
+        lambda nt, reps: L.or_em_bench(em, base, 2624, n, 8192, out.ctypes.data,
+                                       nt, reps), n, seconds)
     L.or_em_free(em)
-    return {"value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
-            "kind": "port",
-            "single_core_mpps": round(res[1], 2),
-            "sample": "%d 64B pkts x reps, 1K-rule 5-tuple ExactMatch, snbuf "
-                      "layout (2624 B stride), 32-pkt batches, %d pinned "
-                      "threads" % (n, threads)}
+    return cpu_baseline(res, threads,
+                        "%d 64B pkts x reps, 1K-rule 5-tuple ExactMatch, snbuf "
+                        "layout (2624 B stride), 32-pkt batches, %d pinned "
+                        "threads" % (n, threads))
 
 
 def run_em(args, rank, world, dev, torch, dist):
@@ -354,11 +391,9 @@ def run_cksum(args, dev, torch):
             lambda nt, reps: L.or_cksum_bench(cpu_frames.ctypes.data, 2048, cn,
                                               3, 0, g.ctypes.data, nt, reps),
             cn, args.cpu_seconds / 2)
-        out["cpu_baseline"] = {
-            "value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
-            "kind": "port", "single_core_mpps": round(res[1], 2),
-            "sample": "%d 1496B frames x reps in 2048B slots, IPChecksum->"
-                      "L4Checksum (AVX2/adc CalculateSum restated)" % cn}
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d 1496B frames x reps in 2048B slots, IPChecksum->"
+                          "L4Checksum (AVX2/adc CalculateSum restated)" % cn)
     return out
 
 
@@ -574,12 +609,9 @@ def run_hashlb(args, dev, torch):
                 lambda nt, reps: L.or_hashlb_bench(
                     o.mode, None, 0, gt.ctypes.data, 8, snb.ctypes.data + 512,
                     2624, cn, og.ctypes.data, nt, reps), cn, args.cpu_seconds / 3)
-            out[name]["cpu_baseline"] = {
-                "value": round(res[threads], 2), "unit": "Mpps",
-                "cores": threads, "kind": "port",
-                "single_core_mpps": round(res[1], 2),
-                "sample": "%d 64B pkts x reps in snbuf layout, HashLB l4 "
-                          "(SSE4.2 CRC32C)" % cn}
+            out[name]["cpu_baseline"] = cpu_baseline(
+                res, threads, "%d 64B pkts x reps in snbuf layout, HashLB l4 "
+                              "(SSE4.2 CRC32C)" % cn)
     return out
 
 
@@ -616,10 +648,9 @@ def run_acl(args, dev, torch):
             threads, res = cpu_rate(
                 lambda nt, reps: o.bench(snb.ctypes.data + 512, 2624, cn, nt, reps),
                 cn, args.cpu_seconds / 4)
-            e["cpu_baseline"] = {
-                "value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
-                "kind": "port", "single_core_mpps": round(res[1], 2),
-                "sample": "%d 64B pkts x reps in snbuf layout, %d-rule ACL" % (cn, nr)}
+            e["cpu_baseline"] = cpu_baseline(
+                res, threads, "%d 64B pkts x reps in snbuf layout, %d-rule ACL"
+                              % (cn, nr))
         out["rules_%d" % nr] = e
         del d
     return out
@@ -654,6 +685,20 @@ def run_iplookup(args, dev, torch):
            "ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
            "roofline": _roof(EM_BYTES_PER_PKT, n, ms, "iplookup"),
            "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}
+    if not args.no_cpu:
+        from oracle import oracle_more as OM
+        cn = 1 << 18
+        snb = _snbuf_sample(frames, cn)
+        tab = o.dir24()
+        og = np.zeros(cn, np.uint16)
+        threads, res = cpu_rate(
+            lambda nt, reps: OM.mlib().or_dir24_bench(
+                tab, snb.ctypes.data + 512, 2624, cn, o.default_gate,
+                og.ctypes.data, nt, reps), cn, args.cpu_seconds / 3)
+        OM.mlib().or_dir24_free(tab)
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d 64B pkts x reps in snbuf layout, 10K routes, "
+                          "rte_lpm's DIR-24-8 lookup restated (DPDK absent)" % cn)
     return out
 
 
@@ -683,12 +728,24 @@ def run_update_ttl(args, dev, torch):
     warm = max(3, args.warmup // 4)
     assert reps + warm + 1 < 199
     ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
-    return {"workload": "UpdateTTL: 64B pkts (64B slots), %d resident pkts, in "
-                        "place" % n, "pkts": n, "ms_per_step": round(ms, 4),
-            "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-            "roofline": _roof(130, n, ms, "ttl"),
-            "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
-                      if parity else "MISMATCH"}
+    out = {"workload": "UpdateTTL: 64B pkts (64B slots), %d resident pkts, in "
+                       "place" % n, "pkts": n, "ms_per_step": round(ms, 4),
+           "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+           "roofline": _roof(130, n, ms, "ttl"),
+           "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
+                     if parity else "MISMATCH"}
+    if not args.no_cpu:
+        cn = 1 << 18
+        snb = _snbuf_sample(ref, cn)
+        snb[:, 512 + 22] = 255  # every rep decrements (<= 250 reps)
+        og = np.zeros(cn, np.uint16)
+        threads, res = cpu_rate(
+            lambda nt, reps: OM.mlib().or_update_ttl_bench(
+                snb.ctypes.data + 512, 2624, cn, og.ctypes.data, nt, reps),
+            cn, args.cpu_seconds / 3, max_reps=120)
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d 64B pkts x reps in snbuf layout, in place" % cn)
+    return out
 
 
 def nat_pairs():
@@ -731,13 +788,24 @@ def run_static_nat(args, dev, torch):
     parity = bool((g[:k].cpu().numpy().view(np.uint16) == want).all() and
                   (d[:k * 64].cpu().numpy().reshape(k, 64) == ref).all())
     ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
-    return {"workload": "StaticNAT forward: 64B pkts (64B slots), %d resident "
-                        "pkts, 16 pairs, 50%% translated, in place" % n,
-            "pkts": n, "ms_per_step": round(ms, 4),
-            "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-            "roofline": _roof(130, n, ms, "nat"),
-            "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
-                      if parity else "MISMATCH"}
+    out = {"workload": "StaticNAT forward: 64B pkts (64B slots), %d resident "
+                       "pkts, 16 pairs, 50%% translated, in place" % n,
+           "pkts": n, "ms_per_step": round(ms, 4),
+           "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+           "roofline": _roof(130, n, ms, "nat"),
+           "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
+                     if parity else "MISMATCH"}
+    if not args.no_cpu:
+        cn = 1 << 18
+        snb = _snbuf_sample(frames, cn)
+        o = OM.OracleStaticNAT(pairs=nat_pairs())
+        threads, res = cpu_rate(
+            lambda nt, reps: o.bench(snb.ctypes.data + 512, 2624, cn, nt, reps),
+            cn, args.cpu_seconds / 3)
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d 64B pkts x reps in snbuf layout, 16 pairs, in "
+                          "place (translations flip back and forth)" % cn)
+    return out
 
 
 def run_dnat(args, dev, torch):
@@ -779,7 +847,29 @@ def run_dnat(args, dev, torch):
     for i in range(reps):
         m.process_device(copies[i + 1], 64, n, g, t0 + 2 + i)
     ms = timer.stop_ms() / reps
-    return {"workload": "NAT forward, established flows: 64B pkts (64B slots), "
+    cpu = None
+    if not args.no_cpu:
+        # one worker (the reference NAT map is not shared between workers):
+        # fresh copies of the sample per pass, copies untimed
+        cn = 1 << 18
+        snb0 = _snbuf_sample(slab, cn)
+        snb = snb0.copy()
+        og = np.zeros(cn, np.uint16)
+        busy, done, i = 0.0, 0, 0
+        while busy < args.cpu_seconds / 3 or i < 2:
+            snb[:] = snb0
+            t0c = time.perf_counter()
+            OM.mlib().or_nat_process(o.h, snb.ctypes.data + 512, 2624, cn, 0,
+                                     t0 + 100 + i, og.ctypes.data)
+            busy += time.perf_counter() - t0c
+            done += cn
+            i += 1
+        rate = done / busy / 1e6
+        cpu = cpu_baseline({1: rate}, 1, "%d 64B pkts x %d passes in snbuf "
+                           "layout, established flows, 1 worker (one NAT map)"
+                           % (cn, i))
+    return {"cpu_baseline": cpu,
+            "workload": "NAT forward, established flows: 64B pkts (64B slots), "
                         "%d pkts per call over %d mappings" % (n, nflow),
             "pkts": n, "ms_per_step": round(ms, 4),
             "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
@@ -861,22 +951,48 @@ def run_wm(args, dev, torch):
             lambda nt, reps: L.or_wm_bench(ow, sample.ctypes.data, 2048, cn,
                                            8192, g.ctypes.data, nt, reps),
             cn, args.cpu_seconds / 2)
-        out["cpu_baseline"] = {
-            "value": round(res[threads], 2), "unit": "Mpps", "cores": threads,
-            "kind": "port", "single_core_mpps": round(res[1], 2),
-            "sample": "%d IMIX frames x reps in 2048B slots, 100K-rule "
-                      "WildcardMatch (8 CuckooMap tuples, CRC32C)" % cn}
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d IMIX frames x reps in 2048B slots, 100K-rule "
+                          "WildcardMatch (8 CuckooMap tuples, CRC32C)" % cn)
     L.or_wm_free(ow)
     return out
 
 
+def oracle_em_bulk(keys, gates):
+    """the oracle ExactMatch (CuckooMap restatement) holding every rule"""
+    from bess_amd import packets as P
+    from oracle import oracle as O
+    L = O.lib()
+    em = L.or_em_new()
+    for i, (off, size) in enumerate(P.FIVE_TUPLE):
+        L.or_em_add_field(em, off, size, 0, i, None, 0)
+    k = np.ascontiguousarray(keys)
+    g = np.ascontiguousarray(gates, dtype=np.uint16)
+    rc = L.or_em_add_rules(em, k.ctypes.data, len(k), k.shape[1], g.ctypes.data)
+    if rc:
+        raise RuntimeError("oracle rule insert failed: %d" % rc)
+    return em
+
+
+def c5_parity(keys, gates, sample, got):
+    from oracle import oracle as O
+    L = O.lib()
+    em = oracle_em_bulk(keys, gates)
+    want = np.zeros(sample.shape[0], np.uint16)
+    L.or_em_process(em, sample.ctypes.data, 64, sample.shape[0], 8192,
+                    want.ctypes.data)
+    L.or_em_free(em)
+    return bool((got == want).all())
+
+
 def run_c5(args, dev, torch):
     """C5 on one GPU: 1M-rule 5-tuple ExactMatch (table in HBM / MALL, not
-    LDS), 16M resident 64 B packets. The multi-GPU form builds the table
-    sharded and all-gathers it (dist.sharded_em_table); here the 8-way
-    partition build is timed on the host as it would run per rank."""
+    LDS), 16M resident 64 B packets. The multi-GPU form (run_c5_multi) is
+    in the N > 1 line; here the 8-way partition build is timed on the host
+    as one rank of 8 runs it (inserting only its partition's rules)."""
     from bess_amd import flowtable as F
     from bess_amd import packets as P
+    from oracle import oracle as O
     n, nr = 16 << 20, 1 << 20
     keys, gates, frames = P.em_workload(nr, n, seed=0xC5, pkt_seed=0xC55)
     d = torch.from_numpy(frames.reshape(-1)).to(dev)
@@ -889,33 +1005,16 @@ def run_c5(args, dev, torch):
     t.sync(dev.index)
     build_s = time.perf_counter() - t0
     t0 = time.perf_counter()
-    pb = t.plan(8)
-    part = t.build_part(0, pb)
+    t8 = F.EmTable(P.em_fields_5tuple())
+    t8.add_many(keys, gates, part=0, nparts=8)
+    pb = t8.plan_count(8, t8.part_count(0, 8))
+    part = t8.build_part(0, pb)
     part_s = time.perf_counter() - t0
-    del part
-    t.sync(dev.index)  # back to the single-device image
+    del part, t8
     t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
-    # parity on the first 256K packets
-    from oracle import oracle as O
-    import ctypes as C
-    L = O.lib()
-    em = L.or_em_new()
-    for i, (off, size) in enumerate(P.FIVE_TUPLE):
-        L.or_em_add_field(em, off, size, 0, i, None, 0)
-    sizes = [s for _, s in P.FIVE_TUPLE]
-    pos = np.cumsum([0] + sizes)
-    ptrs = (C.c_void_p * 5)()
-    lens = (C.c_size_t * 5)(*sizes)
-    for k, g in zip(np.ascontiguousarray(keys), gates):
-        for j in range(5):
-            ptrs[j] = k.ctypes.data + int(pos[j])
-        L.or_em_add_rule(em, int(g), ptrs, lens, 5, None, 0)
     ns = sample.shape[0]
-    want = np.zeros(ns, np.uint16)
-    L.or_em_process(em, sample.ctypes.data, 64, ns, 8192, want.ctypes.data)
-    L.or_em_free(em)
-    parity = bool((dg[:ns].cpu().numpy().view(np.uint16) == want).all())
+    parity = c5_parity(keys, gates, sample, dg[:ns].cpu().numpy().view(np.uint16))
     for _ in range(args.warmup):
         t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
@@ -927,28 +1026,221 @@ def run_c5(args, dev, torch):
     mpps = n / (ms * 1e-3) / 1e6
     gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
     nbytes, in_lds = t.table_info()
-    return {"workload": "C5 (1 GPU): 64B pkts, 1M-rule 5-tuple ExactMatch, "
-                        "16M resident pkts, table in HBM/MALL",
-            "pkts": n, "rules": nr, "ms_per_step": round(ms, 4),
-            "Mpps": round(mpps, 1), "table_bytes": nbytes,
-            "host_table_build_s": round(build_s, 2),
-            "host_partition_build_s_per_rank_of_8": round(part_s, 3),
-            "partition_bytes": pb,
+    out = {"workload": "C5 (1 GPU): 64B pkts, 1M-rule 5-tuple ExactMatch, "
+                       "16M resident pkts, table in HBM/MALL",
+           "pkts": n, "rules": nr, "ms_per_step": round(ms, 4),
+           "Mpps": round(mpps, 1), "table_bytes": nbytes,
+           "host_table_build_s": round(build_s, 2),
+           "host_partition_build_s_per_rank_of_8": round(part_s, 3),
+           "partition_bytes": pb,
+           "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(gbs / HBM_PEAK_GBS, 4),
+                        "traffic": traffic_gbs("c5", ms),
+                        "traffic_bytes_per_launch": load_traffic("c5")},
+           "parity": "bit-exact vs oracle on 256K-pkt sample" if parity
+                     else "MISMATCH"}
+    if not args.no_cpu:
+        L = O.lib()
+        em = oracle_em_bulk(keys, gates)
+        cn = ns
+        snb = np.zeros((cn, 2624), np.uint8)
+        snb[:, 512:512 + 64] = sample
+        og = np.zeros(cn, np.uint16)
+        threads, res = cpu_rate(
+            lambda nt, reps: L.or_em_bench(em, snb.ctypes.data + 512, 2624, cn,
+                                           8192, og.ctypes.data, nt, reps),
+            cn, args.cpu_seconds / 3)
+        L.or_em_free(em)
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d 64B pkts x reps in snbuf layout, 1M-rule 5-tuple "
+                          "ExactMatch (CuckooMap/CRC32C restated)" % cn)
+    return out
+
+
+def run_c5_multi(args, rank, world, dev, torch, dist):
+    """C5 at N = world GPUs: 1M rules sharded over the ranks (rank r inserts
+    only partition r's rules; all-reduce MAX of the partition sizes fixes
+    the layout; each rank builds its partition; one all-gather of the
+    partition images over RCCL/xGMI assembles the replicated table), then
+    every rank classifies its own 16M packets through the 1M-rule table."""
+    from bess_amd import dist as D
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    n, nr = args.pkts, args.c5_rules
+    keys, gates, frames = P.em_workload(nr, n, seed=0xC5,
+                                        pkt_seed=0xC55 + 7919 * rank)
+    d = torch.from_numpy(frames.reshape(-1)).to(dev)
+    sample = np.ascontiguousarray(frames[:1 << 18])
+    del frames
+    dg = torch.empty(n, dtype=torch.int16, device=dev)
+    t = F.EmTable(P.em_fields_5tuple())
+    dist.barrier()
+    t0 = time.perf_counter()
+    t.add_many(keys, gates, part=rank, nparts=world)
+    insert_s = time.perf_counter() - t0
+    held = len(t)
+    _, st = D.sharded_em_table(t, rank, world, device=dev)
+    t.classify(d, 64, n, 8192, dg)
+    torch.cuda.synchronize()
+    ns = sample.shape[0]
+    parity = c5_parity(keys, gates, sample, dg[:ns].cpu().numpy().view(np.uint16))
+    for _ in range(args.warmup):
+        t.classify(d, 64, n, 8192, dg)
+    torch.cuda.synchronize()
+    timer = Timer(torch)
+    dist.barrier()
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    timer.start()
+    for _ in range(args.steps):
+        t.classify(d, 64, n, 8192, dg)
+    kern_ms = timer.stop_ms() / args.steps
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - w0
+    per = torch.tensor([wall, kern_ms, insert_s * 1e3, st["build_ms"],
+                        st["allgather_ms"], held, 1.0 if parity else 0.0],
+                       dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(per) for _ in range(world)]
+    dist.all_gather(allr, per)
+    allr = [x.tolist() for x in allr]
+    wall = max(x[0] for x in allr)
+    kern = max(x[1] for x in allr)
+    gbs = EM_BYTES_PER_PKT * n / (kern * 1e-3) / 1e9
+    nbytes, _ = t.table_info()
+    return {"workload": "C5: 64B pkts, %d-rule 5-tuple ExactMatch sharded over %d "
+                        "GPUs (RCCL all-gather of the partition images), %d "
+                        "resident pkts per GPU" % (nr, world, n),
+            "n_gpus": world, "rules": nr, "pkts_per_gpu": n,
+            "value": round(n * world * args.steps / wall / 1e6, 1), "unit": "Mpps",
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "per_rank_Mpps": [round(n / (x[1] * 1e-3) / 1e6, 1) for x in allr],
+            "rules_inserted_per_rank": [int(x[5]) for x in allr],
+            "insert_ms_per_rank": [round(x[2], 1) for x in allr],
+            "part_build_ms": round(max(x[3] for x in allr), 2),
+            "allgather_ms": round(max(x[4] for x in allr), 3),
+            "allgather_bytes": st["bytes"], "table_bytes": nbytes,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
-                         "traffic": traffic_gbs("c5", ms),
-                         "traffic_bytes_per_launch": load_traffic("c5")},
-            "parity": "bit-exact vs oracle on 256K-pkt sample" if parity
-                      else "MISMATCH"}
+                         "per": "GPU (slowest rank's kernel)"},
+            "parity": "bit-exact vs oracle on 256K pkts per rank"
+                      if all(x[6] for x in allr) else "MISMATCH"}
+
+
+def run_c1(args):
+    """C1 (bessctl/conf/samples/exactmatch.bess shape, CPU only): Source ->
+    ExactMatch(1 rule, 5-tuple) -> Sink on the host, 60 B frames (64 B
+    packets) from a pool of snbuf-like buffers, 32-packet batches, gate 0
+    connected to the Sink, default DROP_GATE. The oracle restatement of the
+    reference path (MakeKeys + CuckooMap::Find + EmitPacket's per-gate
+    batches + Sink) is timed; no GPU (plumbing)."""
+    from bess_amd import packets as P
+    from oracle import oracle as O
+    import ctypes as C
+    L = O.lib()
+    n = 1 << 18
+    keys, gates, frames = P.em_workload(1, n, hit_frac=1.0, seed=0xC1)
+    em = oracle_em_bulk(keys, np.zeros(1, np.uint16))
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + 64] = frames
+    og = np.zeros(n, np.uint16)
+    sunk = C.c_uint64()
+    threads, res = cpu_rate(
+        lambda nt, reps: L.or_c1_bench(em, snb.ctypes.data + 512, 2624, n, 8192,
+                                       1, og.ctypes.data, nt, reps,
+                                       C.byref(sunk)),
+        n, args.cpu_seconds / 3)
+    L.or_c1_bench(em, snb.ctypes.data + 512, 2624, n, 8192, 1, og.ctypes.data,
+                  1, 1, C.byref(sunk))
+    L.or_em_free(em)
+    ok = bool((og == 0).all() and sunk.value == n)
+    return {"workload": "C1: Source -> ExactMatch(1 rule, 5-tuple) -> Sink on "
+                        "CPU, 60B frames (64B pkts), 32-pkt batches",
+            "Mpps": round(res[threads], 2), "unit": "Mpps",
+            "cpu_baseline": cpu_baseline(
+                res, threads, "%d 64B pkts x reps in snbuf layout; per batch: "
+                              "MakeKeys, CuckooMap::Find, EmitPacket per-gate "
+                              "batches, Sink" % n),
+            "parity": "every packet to gate 0 and the sink" if ok else "MISMATCH"}
+
+
+def run_table_only(args, rank, world):
+    """--cpu-table-only: the C5 control path of an N-rank run on CPU (gloo):
+    rank r inserts only partition r's rules, all-reduce MAX, build, all-gather
+    of the partition images; rank 0 checks the gathered image is byte-equal
+    to a single-process build of the whole rule set."""
+    import torch.distributed as dist
+    from bess_amd import dist as D
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    nr = args.c5_rules
+    keys, gates, _ = P.em_workload(nr, 1, seed=0xC5)
+    t = F.EmTable(P.em_fields_5tuple())
+    t0 = time.perf_counter()
+    t.add_many(keys, gates, part=rank, nparts=world)
+    insert_ms = (time.perf_counter() - t0) * 1e3
+    if world > 1:
+        full, st = D.sharded_em_table(t, rank, world)
+    else:
+        pb = t.plan(1)
+        full, st = t.build_part(0, pb), {"part_bytes": pb, "bytes": pb,
+                                         "build_ms": 0.0, "allgather_ms": 0.0}
+    same = None
+    if rank == 0:
+        ref = F.EmTable(P.em_fields_5tuple())
+        ref.add_many(keys, gates)
+        same = bool(np.array_equal(np.asarray(full), D.local_image(ref, world)))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "Mpps + %HBM-roofline, device-resident parse+match, "
+                      "64B/1500B, 1/2/4/8 GPU", "value": None, "unit": "Mpps",
+            "n_gpus": world, "mode": "cpu-table-only (gloo, no GPU)",
+            "C5_table": {"rules": nr, "rules_inserted_rank0": len(t),
+                         "insert_ms_rank0": round(insert_ms, 1),
+                         "part_bytes": st["part_bytes"], "bytes": st["bytes"],
+                         "part_build_ms": round(st["build_ms"], 2),
+                         "allgather_ms": round(st["allgather_ms"], 3),
+                         "image_equals_single_build": same}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if same in (None, True) else 1
+
+
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # start the N ranks (one process per GPU) before anything touches a
+        # GPU, and exit with their exit code
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               "--nproc-per-node=%d" % args.gpus, "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.abspath(__file__)]
+        cmd += sys.argv[1:]
+        log("bench.py: starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+        sys.exit(subprocess.call(cmd))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+        sys.exit(2)
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_table_only:
+        return run_table_only(args, rank, world)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -960,35 +1252,19 @@ def main():
     import bess_amd
     bess_amd.lib()  # fail loudly if the HIP library is missing
 
-    if args.only == "cksum":
-        log(json.dumps(run_cksum(args, dev, torch)))
-        return
-    if args.only == "wm":
-        log(json.dumps(run_wm(args, dev, torch)))
-        return
-    if args.only == "c5":
-        log(json.dumps(run_c5(args, dev, torch)))
-        return
-    if args.only == "ttl":
-        log(json.dumps(run_update_ttl(args, dev, torch)))
-        return
-    if args.only == "dnat":
-        log(json.dumps(run_dnat(args, dev, torch)))
-        return
-    if args.only == "nat":
-        log(json.dumps(run_static_nat(args, dev, torch)))
-        return
-    if args.only == "iplookup":
-        log(json.dumps(run_iplookup(args, dev, torch)))
-        return
-    if args.only == "acl":
-        log(json.dumps(run_acl(args, dev, torch)))
-        return
-    if args.only == "hashlb":
-        log(json.dumps(run_hashlb(args, dev, torch)))
-        return
-    if args.only == "pipe":
-        log(json.dumps(run_e2e_pipe(args, torch)))
+    only = {"cksum": lambda: run_cksum(args, dev, torch),
+            "wm": lambda: run_wm(args, dev, torch),
+            "c5": lambda: run_c5(args, dev, torch),
+            "ttl": lambda: run_update_ttl(args, dev, torch),
+            "dnat": lambda: run_dnat(args, dev, torch),
+            "nat": lambda: run_static_nat(args, dev, torch),
+            "iplookup": lambda: run_iplookup(args, dev, torch),
+            "acl": lambda: run_acl(args, dev, torch),
+            "hashlb": lambda: run_hashlb(args, dev, torch),
+            "pipe": lambda: run_e2e_pipe(args, torch),
+            "c1": lambda: run_c1(args)}
+    if args.only:
+        log(json.dumps(only[args.only]()))
         return
 
     r = run_em(args, rank, world, dev, torch, dist)
@@ -1025,12 +1301,24 @@ def main():
                   else "MISMATCH",
         "cpu_baseline": None,
     }
+    if world > 1:
+        del r
+        torch.cuda.empty_cache()
+        try:
+            out["C5"] = run_c5_multi(args, rank, world, dev, torch, dist)
+        except Exception as e:  # report, do not hide
+            out["C5"] = "failed: %r" % (e,)
     if rank == 0 and world == 1 and not args.no_extra:
         try:
             out["batch_sweep_mpps"] = em_sweep(r, torch)
         except Exception as e:  # report, do not hide
             out["batch_sweep_mpps"] = "failed: %r" % (e,)
         out["extra_configs"] = {}
+        if not args.no_cpu:
+            try:
+                out["extra_configs"]["C1"] = run_c1(args)
+            except Exception as e:
+                out["extra_configs"]["C1"] = "failed: %r" % (e,)
         if not args.no_e2e:
             try:
                 out["e2e_host"] = run_e2e_host(r, args, torch)
@@ -1062,4 +1350,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -57,6 +57,9 @@ _SIGS = {
     "bg_em_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
     "bg_em_process_host": (_int, [_vp, _vp, _sz, _u16, _vp, _vp]),
     "bg_em_plan": (_int, [_vp, _int, C.POINTER(C.c_uint64)]),
+    "bg_em_add_many": (_int, [_vp, _vp, _sz, _sz, _vp, _int, _int]),
+    "bg_em_part_count": (_int, [_vp, _int, _int, C.POINTER(C.c_uint64)]),
+    "bg_em_plan_count": (_int, [_vp, _int, C.c_uint64, C.POINTER(C.c_uint64)]),
     "bg_em_build_part": (_int, [_vp, _int, _vp]),
     "bg_em_attach": (_int, [_vp, _int, _vp]),
     "bg_em_table_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
@@ -86,6 +89,7 @@ _SIGS = {
     "bg_module_process_batches": (_int, [_vp, _vp, _sz, _vp, _vp, _vp, _vp,
                                          C.POINTER(_sz), C.POINTER(_sz)]),
     "bg_module_connect": (_int, [_vp, _u16, _int]),
+    "bg_module_run": (_int, [_vp, _vp, _sz, _sz, _vp]),
     "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
     "bg_module_set_device": (_int, [_vp, _int]),
     "bg_module_set_igate": (_int, [_vp, _u16]),

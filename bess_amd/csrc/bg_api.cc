@@ -724,36 +724,89 @@ void bg_em_window(const bg_em *em, int *lo, int *hi) {
   fields_window(em->fields, lo, hi);
 }
 
-int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes) {
+static int check_nparts(int nparts) {
   if (nparts < 1 || nparts > 8 || (nparts & (nparts - 1)))
     return fail(EINVAL, "nparts must be 1, 2, 4 or 8");
-  std::vector<size_t> cnt(nparts, 0);
-  for (auto &kv : em->rules) {
-    uint64_t h = hash_words(kv.first.w, (int)em->kw, kDefaultSeed);
-    cnt[split_hash(h, (uint32_t)nparts, 2).part]++;
+  return 0;
+}
+
+static uint32_t key_part(const bg_em *em, const uint64_t *w, int nparts) {
+  return split_hash(hash_words(w, (int)em->kw, kDefaultSeed), (uint32_t)nparts, 2).part;
+}
+
+int bg_em_add_many(bg_em *em, const uint8_t *keys, size_t n, size_t key_stride,
+                   const uint16_t *gates, int part, int nparts) {
+  if (em->key_size == 0) return fail(EINVAL, "rule has no fields");
+  if (part >= 0) {
+    if (int r = check_nparts(nparts)) return r;
+    if (part >= nparts) return fail(EINVAL, "part %d out of range", part);
   }
+  em->rules.reserve(em->rules.size() + n);
+  for (size_t i = 0; i < n; i++) {
+    const Key k = em_key(em, keys + i * key_stride);
+    if (part >= 0 && key_part(em, k.w, nparts) != (uint32_t)part) continue;
+    em->rules[k] = gates[i];
+  }
+  em->dirty = true;
+  return 0;
+}
+
+int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes) {
+  if (int r = check_nparts(nparts)) return r;
+  std::vector<size_t> cnt(nparts, 0);
+  for (auto &kv : em->rules) cnt[key_part(em, kv.first.w, nparts)]++;
   size_t maxc = *std::max_element(cnt.begin(), cnt.end());
-  em->planned = plan_layout(maxc, em->kw, 2, (uint32_t)nparts, kDefaultSeed,
-                            0.75, em_vik(em));
+  return bg_em_plan_count(em, nparts, maxc, part_bytes);
+}
+
+int bg_em_part_count(const bg_em *em, int part, int nparts, uint64_t *count) {
+  if (int r = check_nparts(nparts)) return r;
+  uint64_t c = 0;
+  for (auto &kv : em->rules) c += key_part(em, kv.first.w, nparts) == (uint32_t)part;
+  *count = c;
+  return 0;
+}
+
+int bg_em_plan_count(bg_em *em, int nparts, uint64_t max_part_entries,
+                     uint64_t *part_bytes) {
+  if (int r = check_nparts(nparts)) return r;
+  em->planned = plan_layout(max_part_entries, em->kw, 2, (uint32_t)nparts,
+                            kDefaultSeed, 0.75, em_vik(em));
   em->planned_valid = true;
   *part_bytes = em->planned.part_bytes;
   return 0;
 }
 
+// The partition's entries in (hash, key) order: the image depends only on
+// the rule set, not on how (or on which rank) the rules were inserted.
 int bg_em_build_part(bg_em *em, int part, void *host_dst) {
   if (!em->planned_valid) return fail(EINVAL, "bg_em_plan first");
   const TableLayout &L = em->planned;
   if (part < 0 || (uint32_t)part >= L.nparts)
     return fail(EINVAL, "part %d out of range", part);
-  std::vector<uint64_t> keys, seeds;
-  std::vector<uint8_t> vals;
+  struct Ent {
+    uint64_t h;
+    const Key *k;
+    uint16_t g;
+  };
+  std::vector<Ent> ents;
   for (auto &kv : em->rules) {
     uint64_t h = hash_words(kv.first.w, (int)em->kw, kDefaultSeed);
     if (split_hash(h, L.nparts, L.nbp).part != (uint32_t)part) continue;
-    keys.insert(keys.end(), kv.first.w, kv.first.w + em->kw);
-    vals.push_back((uint8_t)kv.second);
-    vals.push_back((uint8_t)(kv.second >> 8));
-    seeds.push_back(h);
+    ents.push_back(Ent{h, &kv.first, kv.second});
+  }
+  std::sort(ents.begin(), ents.end(), [&](const Ent &a, const Ent &b) {
+    if (a.h != b.h) return a.h < b.h;
+    return memcmp(a.k->w, b.k->w, sizeof(a.k->w)) < 0;
+  });
+  std::vector<uint64_t> keys, seeds;
+  std::vector<uint8_t> vals;
+  keys.reserve(ents.size() * em->kw);
+  for (const Ent &e : ents) {
+    keys.insert(keys.end(), e.k->w, e.k->w + em->kw);
+    vals.push_back((uint8_t)e.g);
+    vals.push_back((uint8_t)(e.g >> 8));
+    seeds.push_back(e.h);
   }
   if (!build_partition(L, (uint32_t)part, seeds.size(), keys.data(),
                        vals.data(), seeds.data(),

@@ -65,13 +65,28 @@ class EmTable:
     def add(self, key, gate):
         check(lib().bg_em_add(self.h, bytes(key).ljust(64, b"\0"), gate))
 
-    def add_many(self, keys, gates):
-        """keys: (n, key_size) uint8 array; gates: (n,) ints."""
+    def add_many(self, keys, gates, part=-1, nparts=1):
+        """keys: (n, key_size) uint8 array; gates: (n,) ints. part >= 0:
+        keep only the rules of partition `part` of an nparts-way sharded
+        table (a multi-GPU rank's share)."""
         keys = np.ascontiguousarray(keys, dtype=np.uint8)
-        buf = np.zeros(64, np.uint8)
-        for k, g in zip(keys, np.asarray(gates)):
-            buf[:keys.shape[1]] = k
-            check(lib().bg_em_add(self.h, buf.ctypes.data, int(g)))
+        if keys.shape[1] < self.key_size:
+            keys = np.ascontiguousarray(np.pad(
+                keys, ((0, 0), (0, self.key_size - keys.shape[1]))))
+        g = np.ascontiguousarray(gates, dtype=np.uint16)
+        check(lib().bg_em_add_many(self.h, keys.ctypes.data, len(keys),
+                                   keys.shape[1], g.ctypes.data, part, nparts))
+
+    def part_count(self, part, nparts):
+        c = C.c_uint64()
+        check(lib().bg_em_part_count(self.h, part, nparts, C.byref(c)))
+        return c.value
+
+    def plan_count(self, nparts, max_part_entries):
+        pb = C.c_uint64()
+        check(lib().bg_em_plan_count(self.h, nparts, max_part_entries,
+                                     C.byref(pb)))
+        return pb.value
 
     def delete(self, key):
         check(lib().bg_em_delete(self.h, bytes(key).ljust(64, b"\0")))

@@ -216,6 +216,18 @@ int bg_module_process_batches(bg_module *h, uint8_t *const *heads, size_t cnt,
   return 0;
 }
 
+// A worker's loop over this module with the synchronous drop-in path:
+// ProcessBatch on each `burst` of packets in turn (Source -> module -> Sink).
+int bg_module_run(bg_module *h, uint8_t *const *heads, size_t n, size_t burst,
+                  uint16_t *ogates) {
+  if (burst < 1) return fail(EINVAL, "burst must be >= 1");
+  for (size_t i = 0; i < n; i += burst) {
+    int r = process(h, heads + i, std::min(burst, n - i), ogates + i, nullptr);
+    if (r < 0) return r;
+  }
+  return 0;
+}
+
 int bg_module_connect(bg_module *h, uint16_t ogate, int connected) {
   if (ogate >= MAX_GATES) return fail(EINVAL, "ogate %hu not in [0,%d)", ogate, MAX_GATES);
   std::unique_lock<std::shared_mutex> lk(h->mu);

@@ -123,6 +123,40 @@ class Module:
         _check(lib().bg_module_process(self.h, heads, n, og.ctypes.data))
         return og
 
+    def process_batches(self, frames, stride, n):
+        """process() plus the batches the Task would run next
+        (core/module.h:543-618): -> (ogates, [(gate, [packet index, ...])],
+        [dropped packet index, ...])"""
+        base = frames.ctypes.data
+        heads = (C.c_void_p * n)(*[base + i * stride for i in range(n)])
+        og = np.full(n, BG_GATE_NONE, np.uint16)
+        bg_ = np.zeros(max(n, 1), np.uint16)
+        bl = np.zeros(max(n, 1), np.uint32)
+        idx = np.zeros(max(n, 1), np.uint32)
+        nb, nd = C.c_size_t(), C.c_size_t()
+        _check(lib().bg_module_process_batches(
+            self.h, heads, n, og.ctypes.data, bg_.ctypes.data, bl.ctypes.data,
+            idx.ctypes.data, C.byref(nb), C.byref(nd)))
+        batches, k = [], 0
+        for b in range(nb.value):
+            batches.append((int(bg_[b]), [int(x) for x in idx[k:k + bl[b]]]))
+            k += int(bl[b])
+        return og, batches, [int(x) for x in idx[k:k + nd.value]]
+
+    def run(self, heads, burst=32):
+        """a worker's synchronous loop (bg_module_run) over head addresses
+        (numpy uintp) in bursts; -> gates"""
+        heads = np.ascontiguousarray(heads, dtype=np.uintp)
+        og = np.full(len(heads), BG_GATE_NONE, np.uint16)
+        _check(lib().bg_module_run(self.h, heads.ctypes.data, len(heads), burst,
+                                   og.ctypes.data))
+        return og
+
+    def connect(self, ogate, connected=True):
+        """ogate connected to a next module or not (ConnectModules); until
+        the first call every gate counts as connected"""
+        _check(lib().bg_module_connect(self.h, ogate, 1 if connected else 0))
+
     def process_device(self, d_frames, stride, n, d_ogates, stream=None):
         """Device-resident ProcessBatch over a torch uint8 slab."""
         from .flowtable import _stream_ptr

@@ -111,10 +111,23 @@ int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
 int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
                        uint16_t default_gate, uint16_t *gates,
                        bg_stream_t stream);
+/* n rules at once: rule i's key at keys + i*key_stride, its gate gates[i]
+ * (bg_em_add each). part >= 0: only the rules that fall into partition
+ * `part` of an nparts-way sharded table are kept (a rank of a multi-GPU
+ * build inserts its own share only). */
+int bg_em_add_many(bg_em *em, const uint8_t *keys, size_t n, size_t key_stride,
+                   const uint16_t *gates, int part, int nparts);
 /* Sharded table build (multi-GPU): fix a layout of `nparts` partitions for
  * the current rules, export the host image of one partition, and attach an
- * externally assembled (all-gathered) device image. */
+ * externally assembled (all-gathered) device image. bg_em_plan_count fixes
+ * the layout from the largest partition's entry count, which a rank that
+ * holds only its own partition learns from the other ranks (all-reduce
+ * MAX of bg_em_part_count). A partition image depends only on the rule
+ * set, not on insertion order. */
 int bg_em_plan(bg_em *em, int nparts, uint64_t *part_bytes);
+int bg_em_part_count(const bg_em *em, int part, int nparts, uint64_t *count);
+int bg_em_plan_count(bg_em *em, int nparts, uint64_t max_part_entries,
+                     uint64_t *part_bytes);
 int bg_em_build_part(bg_em *em, int part, void *host_dst);
 int bg_em_attach(bg_em *em, int device, const void *d_image);
 /* bytes of the current device table image and whether it lives in LDS */
@@ -352,6 +365,10 @@ int bg_module_process_batches(bg_module *m, uint8_t *const *heads, size_t cnt,
                               uint16_t *ogates, uint16_t *batch_gate,
                               uint32_t *batch_len, uint32_t *pkt_idx,
                               size_t *nbatches, size_t *ndead);
+/* A worker's loop with the synchronous path: bg_module_process on each
+ * `burst` packets of heads[0..n) in turn (ogates as bg_module_process). */
+int bg_module_run(bg_module *m, uint8_t *const *heads, size_t n, size_t burst,
+                  uint16_t *ogates);
 /* Output gate `ogate` connected (1) or not (0) to a next module
  * (ConnectModules). Until the first call every gate < BG_MAX_GATES counts
  * as connected. EmitPacket to an unconnected gate drops the packet. */

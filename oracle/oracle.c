@@ -490,6 +490,27 @@ int or_em_add_rule(or_em *em, uint16_t gate, const uint8_t *const *vals,
   return 0;
 }
 
+/* n rules at once (test helper): rule i's field values are the
+ * raw_key_size bytes at keys + i * key_stride, cut at the fields' sizes in
+ * field order, i.e. or_em_add_rule with value_bin fields. */
+int or_em_add_rules(or_em *em, const uint8_t *keys, size_t n, size_t key_stride,
+                    const uint16_t *gates) {
+  const uint8_t *vals[OR_MAX_FIELDS];
+  size_t lens[OR_MAX_FIELDS];
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *k = keys + i * key_stride;
+    size_t pos = 0;
+    for (size_t f = 0; f < em->num_fields; f++) {
+      vals[f] = k + pos;
+      lens[f] = (size_t)em->fields[f].size;
+      pos += lens[f];
+    }
+    int err = or_em_add_rule(em, gates[i], vals, lens, em->num_fields, NULL, 0);
+    if (err) return err;
+  }
+  return 0;
+}
+
 /* DeleteRule 198-217 */
 int or_em_delete_rule(or_em *em, const uint8_t *const *vals, const size_t *lens,
                       size_t nvals, char *msg, size_t msglen) {
@@ -1139,12 +1160,52 @@ typedef struct {
   uint16_t *gates;
   int mode, verify, reps, cpu;
   pthread_barrier_t *bar;
+  uint64_t connected, sunk;  /* C1 pipeline */
 } bench_arg;
 
 static double now_s(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* Config C1 (bessctl/conf/samples/exactmatch.bess): Source -> ExactMatch
+ * -> Sink on one worker. Per 32-packet batch (Source::RunTask,
+ * source.cc:83-101, packets from the pool): ExactMatch::ProcessBatch
+ * (exact_match.cc:224-244), then EmitPacket of each packet into its gate's
+ * batch (core/module.h:543-594: a gate that is not connected drops; a full
+ * batch of kMaxBurst goes to the next module), the Task running the
+ * connected gates' batches into Sink (sink.cc:33-35, which frees them:
+ * counted here) at the end of the call (ProcessOGates, 596-618). Returns
+ * the packets the sink received. `connected`: gates 0..63 bitmap. */
+static uint64_t c1_batches(const or_em *em, const uint8_t *base, size_t stride,
+                           size_t n, uint16_t default_gate, uint64_t connected,
+                           uint16_t *gates) {
+  const uint8_t *heads[OR_MAX_BURST];
+  uint64_t sunk = 0, dead = 0;
+  int fill[64];
+  for (size_t i = 0; i < n; i += OR_MAX_BURST) {
+    int cnt = (int)((n - i) < OR_MAX_BURST ? (n - i) : OR_MAX_BURST);
+    for (int j = 0; j < cnt; j++) heads[j] = base + (i + (size_t)j) * stride;
+    uint16_t *g = gates + i;
+    or_em_process_batch(em, heads, cnt, default_gate, g);
+    memset(fill, 0, sizeof(fill));
+    for (int j = 0; j < cnt; j++) {
+      const uint16_t o = g[j];
+      if (o >= 64 || !((connected >> o) & 1)) {  /* DropPacket */
+        dead++;
+        continue;
+      }
+      if (fill[o] >= OR_MAX_BURST) {  /* full: to the next module */
+        sunk += (uint64_t)fill[o];
+        fill[o] = 0;
+      }
+      fill[o]++;
+    }
+    for (int o = 0; o < 64; o++) sunk += (uint64_t)fill[o];  /* Sink */
+  }
+  (void)dead;
+  return sunk;
 }
 
 static void *bench_thread(void *p) {
@@ -1164,6 +1225,9 @@ static void *bench_thread(void *p) {
       or_em_process((const or_em *)a->obj, b, a->stride, n, a->default_gate, g);
     else if (a->kind == 1)
       or_wm_process((const or_wm *)a->obj, b, a->stride, n, a->default_gate, g);
+    else if (a->kind == 3)
+      a->sunk += c1_batches((const or_em *)a->obj, b, a->stride, n,
+                            a->default_gate, a->connected, g);
     else
       or_cksum_process(b, a->stride, n, a->mode, a->verify, NULL, g);
   }
@@ -1177,9 +1241,10 @@ int or_num_cpus(void) {
   return CPU_COUNT(&set);
 }
 
-static double run_bench(int kind, const void *obj, uint8_t *base, size_t stride,
-                        size_t n, uint16_t dg, uint16_t *gates, int mode,
-                        int verify, int nthreads, int reps) {
+static double run_bench_c1(int kind, const void *obj, uint8_t *base,
+                           size_t stride, size_t n, uint16_t dg, uint16_t *gates,
+                           int mode, int verify, int nthreads, int reps,
+                           uint64_t connected, uint64_t *sunk) {
   if (nthreads < 1) nthreads = 1;
   cpu_set_t set;
   int cpus[1024], ncpu = 0;
@@ -1208,6 +1273,8 @@ static double run_bench(int kind, const void *obj, uint8_t *base, size_t stride,
     a->mode = mode;
     a->verify = verify;
     a->reps = reps;
+    a->connected = connected;
+    a->sunk = 0;
     a->cpu = ncpu ? cpus[t % ncpu] : -1;
     a->bar = &bar;
     pthread_create(&th[t], NULL, bench_thread, a);
@@ -1217,10 +1284,28 @@ static double run_bench(int kind, const void *obj, uint8_t *base, size_t stride,
   pthread_barrier_wait(&bar);
   double t1 = now_s();
   for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  if (sunk) {
+    *sunk = 0;
+    for (int t = 0; t < nthreads; t++) *sunk += args[t].sunk;
+  }
   pthread_barrier_destroy(&bar);
   free(th);
   free(args);
   return t1 - t0;
+}
+
+static double run_bench(int kind, const void *obj, uint8_t *base, size_t stride,
+                        size_t n, uint16_t dg, uint16_t *gates, int mode,
+                        int verify, int nthreads, int reps) {
+  return run_bench_c1(kind, obj, base, stride, n, dg, gates, mode, verify,
+                      nthreads, reps, 0, NULL);
+}
+
+double or_c1_bench(const or_em *em, const uint8_t *base, size_t stride,
+                   size_t n, uint16_t default_gate, uint64_t connected,
+                   uint16_t *gates, int nthreads, int reps, uint64_t *sunk) {
+  return run_bench_c1(3, em, (uint8_t *)base, stride, n, default_gate, gates, 0,
+                      0, nthreads, reps, connected, sunk);
 }
 
 double or_em_bench(const or_em *em, const uint8_t *base, size_t stride,

@@ -53,6 +53,8 @@ size_t or_em_total_key_size(const or_em *em);
 /* ExactMatchTable::AddRule / DeleteRule (exact_match_table.h:175-217) */
 int or_em_add_rule(or_em *em, uint16_t gate, const uint8_t *const *vals,
                    const size_t *lens, size_t nvals, char *msg, size_t msglen);
+int or_em_add_rules(or_em *em, const uint8_t *keys, size_t n, size_t key_stride,
+                    const uint16_t *gates);
 int or_em_delete_rule(or_em *em, const uint8_t *const *vals, const size_t *lens,
                       size_t nvals, char *msg, size_t msglen);
 void or_em_clear(or_em *em);
@@ -190,6 +192,11 @@ void or_update_ttl_process(uint8_t *base, size_t stride, size_t n, uint16_t *out
  * 32 over base + i*stride) and sweeps it `reps` times; threads are pinned to
  * the first `nthreads` CPUs of the process affinity mask. Returns wall
  * seconds of the timed region. */
+/* C1: Source -> ExactMatch -> Sink (gates 0..63 bitmap `connected`); the
+ * packets the sink received in *sunk */
+double or_c1_bench(const or_em *em, const uint8_t *base, size_t stride,
+                   size_t n, uint16_t default_gate, uint64_t connected,
+                   uint16_t *gates, int nthreads, int reps, uint64_t *sunk);
 double or_em_bench(const or_em *em, const uint8_t *base, size_t stride,
                    size_t n, uint16_t default_gate, uint16_t *gates,
                    int nthreads, int reps);

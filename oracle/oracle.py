@@ -58,6 +58,12 @@ def lib():
             "or_em_total_key_size": (sz, [C.c_void_p]),
             "or_em_add_rule": (C.c_int, [C.c_void_p, C.c_uint16, C.c_void_p,
                                          C.c_void_p, sz, C.c_char_p, sz]),
+            "or_em_add_rules": (C.c_int, [C.c_void_p, C.c_void_p, sz, sz,
+                                          C.c_void_p]),
+            "or_c1_bench": (C.c_double, [C.c_void_p, C.c_void_p, sz, sz,
+                                         C.c_uint16, C.c_uint64, C.c_void_p,
+                                         C.c_int, C.c_int,
+                                         C.POINTER(C.c_uint64)]),
             "or_em_delete_rule": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p,
                                             sz, C.c_char_p, sz]),
             "or_em_clear": (None, [C.c_void_p]),
@@ -581,3 +587,33 @@ def cksum_process(frames, stride, n, mode, verify):
     lib().or_cksum_process(_ptr(frames), stride, n, mode, 1 if verify else 0,
                            ipg.ctypes.data, l4g.ctypes.data)
     return ipg, l4g
+
+
+def emit_packets(gates, connected=None, none=0xFFFF, drop_gate=8192, burst=32):
+    """Module::EmitPacket / DropPacket (core/module.h:534-594) for packets
+    0..n-1 in order, packet i emitted on gates[i] (`none`: the module never
+    emits it): a gate >= the ogate count or not connected drops the packet
+    (546-549); otherwise it joins its gate's batch, and a new batch is
+    started (Task::AddToRun) when the current one holds kMaxBurst packets.
+    connected: set of connected gates (None: every gate < 8192).
+    Returns (per-packet gate or drop_gate, [(gate, [idx...])] in AddToRun
+    order, [dropped idx...])."""
+    out, batches, dead, cur = [], [], [], {}
+    for i, g in enumerate(gates):
+        g = int(g)
+        if g == none:
+            out.append(none)
+            continue
+        ok = g < 8192 if connected is None else g in connected
+        if not ok:
+            out.append(drop_gate)
+            dead.append(i)
+            continue
+        out.append(g)
+        b = cur.get(g)
+        if b is None or len(batches[b][1]) >= burst:
+            batches.append((g, []))
+            cur[g] = len(batches) - 1
+            b = cur[g]
+        batches[b][1].append(i)
+    return out, batches, dead

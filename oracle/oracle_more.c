@@ -714,3 +714,144 @@ void or_nat_process(or_nat *m, uint8_t *base, size_t stride, size_t n, int dir,
     out[i] = dir == 0 ? 1 : 0;
   }
 }
+
+/* ====================================================================== */
+/* CPU baselines (bench.py cpu_baseline legs)                              */
+/* ====================================================================== */
+
+/* IPLookup's CPU cost is rte_lpm's lookup (DPDK 19.11, absent here):
+ * DIR-24-8 -- one 2^24-entry table indexed by the top 24 address bits,
+ * and 256-entry groups for /24 blocks that hold deeper rules. This is a
+ * restatement of that structure (rte_lpm.c's rte_lpm_lookup_bulk fast
+ * path), used only to time the reference's lookup on the host; results are
+ * checked equal to or_lpm_process. Entry: 0 none, 0x80000000 | group, else
+ * next hop + 1. Rules are applied in ascending depth (deeper overrides). */
+typedef struct or_dir24 {
+  uint32_t *tbl24;
+  uint32_t *tbl8;
+  size_t ngroups;
+} or_dir24;
+
+static int dir24_cmp_depth(const void *a, const void *b) {
+  return (int)((const uint32_t *)a)[1] - (int)((const uint32_t *)b)[1];
+}
+
+or_dir24 *or_dir24_build(const uint32_t *ips, const uint8_t *depths,
+                         const uint32_t *nhs, size_t nrules) {
+  or_dir24 *t = (or_dir24 *)calloc(1, sizeof(or_dir24));
+  t->tbl24 = (uint32_t *)calloc((size_t)1 << 24, 4);
+  uint32_t(*r)[3] = (uint32_t(*)[3])malloc((nrules + 1) * sizeof(*r));
+  for (size_t i = 0; i < nrules; i++) {
+    r[i][0] = ips[i] & lpm_mask(depths[i]);
+    r[i][1] = depths[i];
+    r[i][2] = nhs[i];
+  }
+  qsort(r, nrules, sizeof(*r), dir24_cmp_depth);  /* stable enough: distinct (ip, depth) */
+  size_t cap = 0;
+  for (size_t i = 0; i < nrules; i++) {
+    const uint32_t ip = r[i][0], d = r[i][1], v = r[i][2] + 1;
+    if (d <= 24) {
+      const uint32_t b = ip >> 8, cnt = 1u << (24 - d);
+      for (uint32_t k = b; k < b + cnt; k++) {
+        if (t->tbl24[k] & 0x80000000u) {  /* deeper block: fill its group */
+          uint32_t *g = t->tbl8 + (size_t)(t->tbl24[k] & 0x7FFFFFFFu) * 256;
+          for (int j = 0; j < 256; j++) g[j] = v;  /* rules come by depth */
+        } else {
+          t->tbl24[k] = v;
+        }
+      }
+    } else {
+      const uint32_t b = ip >> 8;
+      if (!(t->tbl24[b] & 0x80000000u)) {
+        if (t->ngroups == cap) {
+          cap = cap ? cap * 2 : 64;
+          t->tbl8 = (uint32_t *)realloc(t->tbl8, cap * 256 * 4);
+        }
+        uint32_t *g = t->tbl8 + t->ngroups * 256;
+        for (int j = 0; j < 256; j++) g[j] = t->tbl24[b];
+        t->tbl24[b] = 0x80000000u | (uint32_t)t->ngroups++;
+      }
+      uint32_t *g = t->tbl8 + (size_t)(t->tbl24[b] & 0x7FFFFFFFu) * 256;
+      const uint32_t lo = ip & 0xFF, cnt = 1u << (32 - d);
+      for (uint32_t j = lo; j < lo + cnt; j++) g[j] = v;
+    }
+  }
+  free(r);
+  return t;
+}
+
+void or_dir24_free(or_dir24 *t) {
+  if (!t) return;
+  free(t->tbl24);
+  free(t->tbl8);
+  free(t);
+}
+
+void or_dir24_process(const or_dir24 *t, const uint8_t *base, size_t stride,
+                      size_t n, uint16_t default_gate, uint16_t *out) {
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t dst = be32(base + i * stride + 30);
+    uint32_t e = t->tbl24[dst >> 8];
+    if (e & 0x80000000u) e = t->tbl8[(size_t)(e & 0x7FFFFFFFu) * 256 + (dst & 0xFF)];
+    out[i] = e ? (uint16_t)(e - 1) : default_gate;
+  }
+}
+
+typedef struct {
+  const or_dir24 *t;
+  const uint8_t *base;
+  size_t stride;
+  uint16_t dg;
+  uint16_t *out;
+} dir24_ctx;
+
+static void dir24_slice(void *p, size_t b, size_t e) {
+  dir24_ctx *c = (dir24_ctx *)p;
+  or_dir24_process(c->t, c->base + b * c->stride, c->stride, e - b, c->dg, c->out + b);
+}
+
+double or_dir24_bench(const or_dir24 *t, const uint8_t *base, size_t stride,
+                      size_t n, uint16_t default_gate, uint16_t *out,
+                      int nthreads, int reps) {
+  dir24_ctx c = {t, base, stride, default_gate, out};
+  return run_slices(dir24_slice, &c, n, nthreads, reps);
+}
+
+typedef struct {
+  uint8_t *base;
+  size_t stride;
+  uint16_t *out;
+} ttl_ctx;
+
+static void ttl_slice(void *p, size_t b, size_t e) {
+  ttl_ctx *c = (ttl_ctx *)p;
+  or_update_ttl_process(c->base + b * c->stride, c->stride, e - b, c->out + b);
+}
+
+double or_update_ttl_bench(uint8_t *base, size_t stride, size_t n, uint16_t *out,
+                           int nthreads, int reps) {
+  ttl_ctx c = {base, stride, out};
+  return run_slices(ttl_slice, &c, n, nthreads, reps);
+}
+
+typedef struct {
+  const uint32_t *ia, *ea, *sz;
+  size_t np;
+  uint8_t *base;
+  size_t stride;
+  uint16_t *out;
+} snat_ctx;
+
+static void snat_slice(void *p, size_t b, size_t e) {
+  snat_ctx *c = (snat_ctx *)p;
+  or_static_nat_process(c->ia, c->ea, c->sz, c->np, c->base + b * c->stride,
+                        c->stride, e - b, 0, c->out + b);
+}
+
+double or_static_nat_bench(const uint32_t *int_addr, const uint32_t *ext_addr,
+                           const uint32_t *size, size_t npairs, uint8_t *base,
+                           size_t stride, size_t n, uint16_t *out, int nthreads,
+                           int reps) {
+  snat_ctx c = {int_addr, ext_addr, size, npairs, base, stride, out};
+  return run_slices(snat_slice, &c, n, nthreads, reps);
+}

@@ -38,6 +38,14 @@ _SIGS = {
     "or_lpm_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_uint16,
                               _vp]),
     "or_hash_range": (C.c_uint16, [C.c_uint32, C.c_uint16]),
+    "or_dir24_build": (_vp, [_vp, _vp, _vp, _sz]),
+    "or_dir24_free": (None, [_vp]),
+    "or_dir24_process": (None, [_vp, _vp, _sz, _sz, C.c_uint16, _vp]),
+    "or_dir24_bench": (C.c_double, [_vp, _vp, _sz, _sz, C.c_uint16, _vp,
+                                    C.c_int, C.c_int]),
+    "or_update_ttl_bench": (C.c_double, [_vp, _sz, _sz, _vp, C.c_int, C.c_int]),
+    "or_static_nat_bench": (C.c_double, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, _vp,
+                                         C.c_int, C.c_int]),
     "or_hashlb_process": (None, [C.c_int, _vp, _sz, _vp, _sz, _vp, _sz, _sz,
                                  _vp]),
     "or_hashlb_bench": (C.c_double, [C.c_int, _vp, _sz, _vp, _sz, _vp, _sz,
@@ -272,6 +280,16 @@ class OracleIPLookup:
     def clear(self):
         self.rules = {}
 
+    def dir24(self):
+        """rte_lpm's DIR-24-8 lookup structure over the current rules (the
+        CPU baseline's lookup; or_dir24_free it)"""
+        k = list(self.rules.items())
+        ips = np.array([x[0][0] for x in k] or [0], np.uint32)
+        ds = np.array([x[0][1] for x in k] or [0], np.uint8)
+        nh = np.array([x[1] for x in k] or [0], np.uint32)
+        return mlib().or_dir24_build(ips.ctypes.data, ds.ctypes.data,
+                                     nh.ctypes.data, len(k))
+
     def process(self, frames, stride, n):
         out = np.empty(n, np.uint16)
         k = list(self.rules.items())
@@ -334,6 +352,16 @@ class OracleStaticNAT:
         return {"pairs": [{"int_range": {"start": f(i), "end": f(i + z)},
                            "ext_range": {"start": f(e), "end": f(e + z)}}
                           for i, e, z in self.pairs_]}
+
+    def bench(self, base, stride, n, threads, reps):
+        """forward ProcessBatch timed over `threads` pinned threads (CPU
+        baseline); in place; returns seconds"""
+        k = self.pairs_ or [(0, 0, 0)]
+        self._b = [np.array([x[j] for x in k], np.uint32) for j in range(3)]
+        out = np.empty(n, np.uint16)
+        return mlib().or_static_nat_bench(
+            self._b[0].ctypes.data, self._b[1].ctypes.data, self._b[2].ctypes.data,
+            len(self.pairs_), base, stride, n, out.ctypes.data, threads, reps)
 
     def process(self, frames, stride, n, igate=0):
         """ProcessBatch 179-187 (igate 0 forward, else reverse), in place"""

@@ -1,0 +1,206 @@
+"""BASELINE configs C4 and C5 at their own sizes through the HIP path,
+bit-exact against the oracle; the drop-in module path under concurrent
+workers; EmitPacket's per-gate batches and drops (core/module.h:534-618).
+
+  C5: 1,048,576-rule 5-tuple ExactMatch (table in HBM/MALL), as one image
+      and as 8 partitions attached as one image (the multi-GPU build);
+  C4: 100K-rule WildcardMatch over 8 masks on IMIX frames in 2 KB slots
+      (tag words in LDS, and the key-filter path).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from bess_amd import _lib as LB  # noqa: E402
+from bess_amd import flowtable as F  # noqa: E402
+from bess_amd import packets as P  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).cuda()
+
+
+def oracle_em_bulk(keys, gates):
+    L = O.lib()
+    em = L.or_em_new()
+    for i, (off, size) in enumerate(P.FIVE_TUPLE):
+        assert L.or_em_add_field(em, off, size, 0, i, None, 0) == 0
+    k = np.ascontiguousarray(keys)
+    g = np.ascontiguousarray(gates, dtype=np.uint16)
+    assert L.or_em_add_rules(em, k.ctypes.data, len(k), k.shape[1], g.ctypes.data) == 0
+    return em
+
+
+def oracle_em_gates(keys, gates, frames, stride, default_gate=8192):
+    em = oracle_em_bulk(keys, gates)
+    want = np.zeros(len(frames), np.uint16)
+    O.lib().or_em_process(em, frames.ctypes.data, stride, len(frames),
+                          default_gate, want.ctypes.data)
+    O.lib().or_em_free(em)
+    return want
+
+
+@pytest.fixture(scope="module")
+def c5():
+    keys, gates, frames = P.em_workload(1 << 20, 1 << 21, seed=0xC5,
+                                        pkt_seed=0xC55)
+    want = oracle_em_gates(keys, gates, frames, 64)
+    assert 0.4 < (want != 8192).mean() < 0.6
+    return keys, gates, frames, want
+
+
+# ------------------------------------------------------------------- C5
+@pytest.mark.parametrize("flags", [0, LB.BG_PATH_NO_SLAB])
+def test_c5_1m_rules_single_image(c5, flags):
+    keys, gates, frames, want = c5
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    assert len(t) == 1 << 20
+    d_g = torch.zeros(len(frames), dtype=torch.int16, device="cuda")
+    with LB.kernel_paths(flags):
+        t.classify(to_dev(frames), 64, len(frames), 8192, d_g)
+        torch.cuda.synchronize()
+    nbytes, in_lds = t.table_info()
+    assert not in_lds and nbytes > 16 << 20
+    assert (d_g.cpu().numpy().view(np.uint16) == want).all()
+
+
+def test_c5_8_partitions_attached(c5):
+    """the multi-GPU table: 8 partitions, each holding only its rules (as
+    each rank inserts them), built separately and attached as one image"""
+    keys, gates, frames, want = c5
+    parts, counts = [], []
+    for r in range(8):
+        t = F.EmTable(P.em_fields_5tuple())
+        t.add_many(keys, gates, part=r, nparts=8)
+        parts.append(t)
+        counts.append(t.part_count(r, 8))
+    assert sum(counts) == 1 << 20
+    pb = [t.plan_count(8, max(counts)) for t in parts]
+    assert len(set(pb)) == 1
+    img = np.concatenate([t.build_part(r, pb[0]) for r, t in enumerate(parts)])
+    full = F.EmTable(P.em_fields_5tuple())
+    full.add_many(keys, gates)
+    assert full.plan(8) == pb[0]
+    d_img = to_dev(img)
+    full.attach(0, d_img)
+    d_g = torch.zeros(len(frames), dtype=torch.int16, device="cuda")
+    full.classify(to_dev(frames), 64, len(frames), 8192, d_g)
+    assert (d_g.cpu().numpy().view(np.uint16) == want).all()
+
+
+# ------------------------------------------------------------------- C4
+@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_TAGS])
+def test_c4_imix_2k_slots(flags):
+    n = 1 << 18
+    rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n, stride=2048)
+    assert set(np.unique(flen)) == {60, 590, 1514}
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    assert t.num_tuples() == 8
+    d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
+    with LB.kernel_paths(flags):
+        t.classify(to_dev(frames), 2048, n, 8192, d_g)
+        torch.cuda.synchronize()
+        in_lds = t.table_info()[1]
+    assert in_lds == (2 if flags else 3)  # key filter / tag words in LDS
+    L = O.lib()
+    ow = L.or_wm_new()
+    for off, size in P.FIVE_TUPLE:
+        L.or_wm_add_field(ow, off, size, None, 0)
+    L.or_wm_init_done(ow)
+    kb = np.zeros(64, np.uint8)
+    mb = np.zeros(64, np.uint8)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        kb[:16] = k
+        mb[:16] = m
+        assert L.or_wm_add(ow, kb.ctypes.data, mb.ctypes.data, int(p), int(g)) == 0
+    want = np.zeros(n, np.uint16)
+    L.or_wm_process(ow, frames.ctypes.data, 2048, n, 8192, want.ctypes.data)
+    L.or_wm_free(ow)
+    assert (d_g.cpu().numpy().view(np.uint16) == want).all()
+    assert (want != 8192).mean() > 0.3
+
+
+# ------------------------------------------- concurrent workers, one module
+def _em_module_and_oracle(n_rules, n_pkts, seed):
+    from bess_amd.modules import ExactMatch
+    keys, gates, frames = P.em_workload(n_rules, n_pkts, seed=seed)
+    fields = [{"offset": o, "num_bytes": s} for o, s in P.FIVE_TUPLE]
+    m = ExactMatch(fields=fields)
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    for k, g in zip(keys, gates):
+        kb = k.tobytes()
+        m.add(fields=[{"value_bin": kb[a:c]} for a, c in cut], gate=int(g))
+    want = oracle_em_gates(keys, gates, frames, 64)
+    return m, frames, want
+
+
+def test_concurrent_workers_one_module():
+    """8 worker threads run the synchronous drop-in path (ProcessBatch of 32
+    packets, bg_module_run) on ONE ExactMatch module at the same time, and 8
+    more each drive their own bg_pipe over it; every gate equals the
+    oracle's (core/module.h:485: lookups from many workers at once)."""
+    from bess_amd.modules import Pipe
+    m, frames, want = _em_module_and_oracle(1000, 1 << 16, seed=21)
+    snb = np.zeros((len(frames), 2624), np.uint8)  # snbuf-like buffers
+    snb[:, 512:512 + 64] = frames
+    heads = snb.ctypes.data + 512 + 2624 * np.arange(len(frames), dtype=np.uintp)
+    outs, errs = {}, []
+
+    def sync_worker(w):
+        try:
+            rot = np.roll(np.arange(len(frames)), -w * 977)
+            g = m.run(heads[rot], burst=32)
+            outs[("sync", w)] = (rot, g)
+        except Exception as e:  # reported below
+            errs.append(e)
+
+    def pipe_worker(w):
+        try:
+            rot = np.roll(np.arange(len(frames)), -w * 1231)
+            p = Pipe(m, batch=2048, depth=3)
+            g = p.run(heads[rot])
+            p.close()
+            outs[("pipe", w)] = (rot, g)
+        except Exception as e:
+            errs.append(e)
+
+    ths = [threading.Thread(target=sync_worker, args=(w,)) for w in range(8)]
+    ths += [threading.Thread(target=pipe_worker, args=(w,)) for w in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=300)
+    assert not errs, errs
+    assert len(outs) == 16
+    for key, (rot, g) in outs.items():
+        assert (g == want[rot]).all(), key
+
+
+# ----------------------------------------------------- EmitPacket batches
+def test_emit_batches_and_unconnected_gates():
+    """Module::EmitPacket (core/module.h:543-594): packets join their
+    gate's batch in order, a new batch starts at 32; a gate that is out of
+    range (the default DROP_GATE 8192 on a miss) or not connected drops the
+    packet (546-549)."""
+    m, frames, want = _em_module_and_oracle(200, 3000, seed=23)
+    n = len(frames)
+    og, batches, dead = m.process_batches(frames, 64, n)
+    w_og, w_b, w_dead = O.emit_packets(want)
+    assert list(og) == w_og and batches == w_b and dead == w_dead
+    assert dead and all(len(b) <= 32 for _, b in batches)
+    conn = {0, 1, 2, 5}
+    for g in conn:
+        m.connect(g)
+    og, batches, dead = m.process_batches(frames, 64, n)
+    w_og, w_b, w_dead = O.emit_packets(want, connected=conn)
+    assert list(og) == w_og and batches == w_b and dead == w_dead
+    assert set(g for g, _ in batches) <= conn

@@ -75,3 +75,32 @@ def test_control_surface_matches_reference():
         (22, "Invalid prefix length: 33")
     assert _outcome(lambda: o.add(prefix="22.22.22.0", prefix_len=16, gate=0)) == \
         (22, "Invalid IP prefix 22.22.22.0/16 16161600 ffff0000")
+
+
+def test_cpu_baseline_dir24_equals_oracle():
+    """The CPU baseline times rte_lpm's DIR-24-8 lookup (restated in
+    oracle_more.c, DPDK being absent); it must give the oracle's longest-
+    prefix results (an independent per-depth search) on nested routes."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    o = OM.OracleIPLookup(max_rules=5000, max_tbl8s=2000)
+    for _ in range(3000):
+        d = int(rng.choice([8, 12, 16, 20, 24, 25, 28, 30, 32]))
+        ip = int(rng.integers(0, 1 << 32)) & ((0xFFFFFFFF << (32 - d)) & 0xFFFFFFFF)
+        o.add(prefix="%d.%d.%d.%d" % tuple(ip.to_bytes(4, "big")), prefix_len=d,
+              gate=int(rng.integers(0, 8000)))
+    n = 20000
+    frames = np.zeros((n, 64), np.uint8)
+    keys = [ip for ip, _ in o.rules]
+    dst = np.where(rng.random(n) < 0.7,
+                   np.array(keys)[rng.integers(0, len(keys), n)] +
+                   rng.integers(0, 256, n), rng.integers(0, 1 << 32, n)) & 0xFFFFFFFF
+    frames[:, 30:34] = dst.astype(">u4").view(np.uint8).reshape(n, 4)
+    want = o.process(frames, 64, n)
+    t = o.dir24()
+    got = np.zeros(n, np.uint16)
+    OM.mlib().or_dir24_process(t, frames.ctypes.data, 64, n, o.default_gate,
+                               got.ctypes.data)
+    OM.mlib().or_dir24_free(t)
+    assert (got == want).all()
+    assert (want != o.default_gate).mean() > 0.3
