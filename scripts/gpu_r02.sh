@@ -21,11 +21,11 @@ if [[ "$MODE" == *info* ]] || [ "$MODE" = all ]; then
   echo "OMP_NUM_THREADS=$OMP_NUM_THREADS" >> "$OUT/nproc.txt"
 fi
 if [[ "$MODE" == *tests* ]] || [ "$MODE" = all ]; then
-  step tests 1500 python -u -m pytest tests -m gpu -x -v -rf --timeout 400 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"}
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step tests 600 python -u -m pytest tests -m gpu -x -v -rf --timeout 400 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"}
+  step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ "$MODE" == *bench* ]] || [ "$MODE" = all ]; then
-  step bench 900 python bench.py ${BENCH_ARGS}
+  step bench 700 python bench.py ${BENCH_ARGS}
 fi
 if [[ "$MODE" == *prof* ]]; then
   step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-e2e
