@@ -612,6 +612,34 @@ static int bind_meta(const std::vector<bg_field> &fields, int meta_off,
   return 0;
 }
 
+}  // extern "C"
+
+namespace bg {
+// The device plan of a table for launches outside this file (the persistent
+// ring, bg_ring.cc): table synced to `device`, field plan of the slot layout.
+int em_device_plan(bg_em *em, int device, hipStream_t s, FieldPlan *fp,
+                   TableRef *t, int *read_end) {
+  if (em->has_attr && !em->meta_bound) return no_attr_datapath();
+  {
+    std::lock_guard<std::mutex> lk(em->mu);
+    if (int r = em_sync_locked(em, device, s)) return r;
+  }
+  *fp = make_plan(em->dfields, true, 0);
+  *t = em->dev.ref();
+  int hi = 0;  // bytes of a slot the kernel reads (check_extent)
+  if (!fp->direct) {
+    hi = fp->nf ? fp->win_lo + 16 * fp->nch : 0;
+  } else {
+    for (int i = 0; i < fp->nf; i++)
+      hi = std::max(hi, (fspec_d(fp->fspec[i]) + fspec_nd(fp->fspec[i])) * 4);
+  }
+  *read_end = hi;
+  return 0;
+}
+}  // namespace bg
+
+extern "C" {
+
 int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
                     int nattrs) {
   std::lock_guard<std::mutex> lk(em->mu);

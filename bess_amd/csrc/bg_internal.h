@@ -87,6 +87,9 @@ struct Staging {
 // when the caller passes no stream, runs on its own non-blocking stream per
 // device (never the legacy stream, which would serialise the workers).
 Staging &thread_staging();
+// bg_api.cc: a table's field plan (slot layout) and synced device table
+int em_device_plan(bg_em *em, int device, hipStream_t s, FieldPlan *fp,
+                   TableRef *t, int *read_end);
 hipStream_t thread_stream(int device, hipStream_t given);
 
 }  // namespace bg

@@ -213,6 +213,32 @@ struct DnatArgs {
   const uint32_t *mres;
 };
 
+// Persistent ExactMatch kernel fed by a ring of batch descriptors
+// (bg_ring.cc). Descriptor of ticket t at desc + (t % nslots) * 4: four
+// 8-byte words, each carrying the tag (t + 1) & 0xFFFF in its top 16 bits
+// (one untorn 8-byte store each, so a reader that sees four matching tags
+// sees the whole descriptor, no fence):
+//   w0 frames address | tag << 48     w1 gates address | tag << 48
+//   w2 n | stride << 32 | tag << 48   w3 default gate | tag << 48
+// A workgroup claims tickets from *head (one atomic add), waits for the
+// descriptor, classifies the batch, then publishes done[t % nslots] = t + 1
+// (system scope, after a system release of its gate stores). A workgroup
+// that waits longer than idle_ticks (s_memrealtime, 100 MHz) sets *stop;
+// every workgroup that sees *stop re-checks its descriptor once and exits
+// if it is still unpublished. The host relaunches from its oldest
+// unfinished ticket (re-classifying a finished batch is harmless).
+struct RingArgs {
+  const uint64_t *desc;   // host memory (mapped)
+  uint32_t *done;         // host memory (mapped)
+  uint32_t *stop;         // host memory (mapped)
+  unsigned long long *head;  // device memory: next ticket to claim
+  uint32_t nslots, pad;
+  uint64_t idle_ticks;
+  FieldPlan fp;
+  TableRef t;
+};
+constexpr int kRingBlock = 256;
+
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -231,6 +257,8 @@ hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s);
 // up = [idx x k | ep x k | ts x k]: ent[idx[i]] = ep[i], ts[idx[i]] = ts[i]
 hipError_t launch_dnat_scatter(const uint64_t *d_up, size_t k, uint64_t *ent,
                                uint64_t *ts, hipStream_t s);
+// the persistent ring kernel: `blocks` workgroups
+hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword

@@ -357,6 +357,90 @@ __global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
 #endif  // BG_AB
 
 // ---------------------------------------------------------------------------
+// Persistent ExactMatch over a ring of batch descriptors (RingArgs,
+// bg_kernels.h): BESS hands a module <= 32 packets per ProcessBatch
+// (core/pktbatch.h:70); one launch drains any number of such batches.
+// Lane = packet inside the batch; the table stays in LDS for the whole run.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// all four words of the slot carry `tag`: the descriptor is complete
+__device__ __forceinline__ bool ring_read(const uint64_t *d, uint64_t tag,
+                                          uint64_t (&w)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) w[i] = ld_sys(d + i);
+  return (w[0] >> 48) == tag && (w[1] >> 48) == tag && (w[2] >> 48) == tag &&
+         (w[3] >> 48) == tag;
+}
+
+template <int KW, int NCH>
+__global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
+void em_ring_kernel(RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ uint64_t sh_w[4];
+  __shared__ uint64_t sh_t;
+  __shared__ uint32_t sh_go;
+  copy_table_to_lds(lds, a.t);  // (ends with a barrier)
+  const uint64_t mask48 = (1ull << 48) - 1;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t t = atomicAdd(a.head, 1ull);
+      const uint64_t tag = (t + 1) & 0xFFFF;
+      const uint64_t *d = a.desc + (t % a.nslots) * 4;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t w[4];
+      uint32_t go = 0;
+      for (;;) {
+        if (ring_read(d, tag, w)) {
+          go = 1;
+          break;
+        }
+        const uint32_t st = __hip_atomic_load(a.stop, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if (st || __builtin_amdgcn_s_memrealtime() - t0 > a.idle_ticks) {
+          if (!st)  // idle: the whole grid drains, the host relaunches
+            __hip_atomic_store(a.stop, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          go = ring_read(d, tag, w) ? 1u : 0u;  // published meanwhile?
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) sh_w[i] = w[i];
+      sh_t = t;
+      sh_go = go;
+    }
+    __syncthreads();
+    if (!sh_go) return;
+    const uint8_t *frames = reinterpret_cast<const uint8_t *>(sh_w[0] & mask48);
+    uint16_t *gates = reinterpret_cast<uint16_t *>(sh_w[1] & mask48);
+    const uint32_t n = (uint32_t)sh_w[2];
+    const uint64_t stride = (sh_w[2] >> 32) & 0xFFFF;
+    const uint32_t dflt = (uint32_t)(sh_w[3] & 0xFFFF);
+    const uint64_t t = sh_t;
+    for (uint32_t i = threadIdx.x; i < n; i += kRingBlock) {
+      uint64_t k[1][KW];
+      build_keys<KW, NCH, 1>(frames, stride, n, i, a.fp, k);
+      gates[i] = (uint16_t)(a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, k[0], dflt)
+                                                 : em_lookup<KW>(a.t.base, a.t, k[0], dflt));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // the batch's gates leave the L2 before the host can see `done`
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.done + (t % a.nslots), (uint32_t)(t + 1),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();  // sh_* are rewritten for the next ticket
+  }
+}
+
+// ---------------------------------------------------------------------------
 // WildcardMatch: tuple-space search over <= 8 masks in one combined table;
 // the best (priority, later-tuple-on-tie) entry wins (LookupEntry 136-157).
 // ---------------------------------------------------------------------------
@@ -1359,6 +1443,24 @@ hipError_t launch_em_slab(const EmArgs &a, int num_cus, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s) {
+  int maxops = 0;
+  for (int q = 0; q < a.fp.nkd; q++) maxops = std::max(maxops, kd_nops_of(a.fp, q));
+  const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 && maxops <= 2 ? 2 : 4);
+  const size_t lds = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
+#define BG_RING(KW, NCH)                                                     \
+  if (a.t.kw == KW && nch == NCH) {                                          \
+    hipLaunchKernelGGL((em_ring_kernel<KW, NCH>), dim3((unsigned)blocks),     \
+                       dim3(kRingBlock), lds, s, a);                         \
+    return hipGetLastError();                                                \
+  }
+#define BG_RINGS(KW) BG_RING(KW, 0) BG_RING(KW, 2) BG_RING(KW, 4)
+  BG_RINGS(1) BG_RINGS(2) BG_RINGS(4) BG_RINGS(8)
+#undef BG_RINGS
+#undef BG_RING
+  return hipErrorInvalidValue;
+}
 
 bool fits_nch2(const FieldPlan &fp) {
   if (fp.direct || fp.nch > 2) return false;

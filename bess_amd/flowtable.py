@@ -11,7 +11,7 @@ import numpy as np
 from . import _lib
 from ._lib import BessGpuError, bg_field, check, lib
 
-__all__ = ["EmTable", "WmTable", "cksum", "cksum_host", "resolve_em_fields",
+__all__ = ["EmTable", "Ring", "WmTable", "cksum", "cksum_host", "resolve_em_fields",
            "resolve_wm_fields", "BessGpuError"]
 
 
@@ -132,6 +132,47 @@ class EmTable:
         b, l = C.c_uint64(), C.c_int()
         check(lib().bg_em_table_info(self.h, C.byref(b), C.byref(l)))
         return b.value, bool(l.value)
+
+
+class Ring:
+    """bg_ring: one persistent ExactMatch kernel draining batch descriptors
+    (the table as of creation, in LDS for the kernel's whole run)."""
+
+    def __init__(self, table, device=0, slots=1024, blocks=0, idle_us=200000):
+        h = C.c_void_p()
+        check(lib().bg_em_ring_create(table.h, device, slots, blocks, idle_us,
+                                      C.byref(h)))
+        self.h = h
+        self.table = table
+
+    def close(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_ring_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def submit(self, frames, stride, n, default_gate, gates, offset=0):
+        """frames / gates: device tensors; batch = packets [offset, offset+n)"""
+        t = lib().bg_ring_submit(self.h, C.c_void_p(frames.data_ptr() + offset * stride),
+                                 stride, n, default_gate,
+                                 C.c_void_p(gates.data_ptr() + 2 * offset))
+        return check(t)
+
+    def wait(self, ticket):
+        check(lib().bg_ring_wait(self.h, ticket))
+
+    def completed(self):
+        return check(lib().bg_ring_completed(self.h))
+
+    def run(self, frames, stride, n, burst, default_gate, gates):
+        check(lib().bg_ring_run(self.h, _dev_ptr(frames), stride, n, burst,
+                                default_gate, _dev_ptr(gates)))
+
+    def info(self):
+        launches, blocks = C.c_uint64(), C.c_int()
+        lib().bg_ring_info(self.h, C.byref(launches), C.byref(blocks))
+        return launches.value, blocks.value
 
 
 class WmTable:

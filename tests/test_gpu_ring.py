@@ -1,0 +1,86 @@
+"""The persistent classify kernel (bg_ring, em_ring_kernel): batches of the
+sizes BESS hands a module (32 ... 4096 packets, ragged tails) through one
+running kernel, bit-exact against the oracle; idle exit and relaunch; the
+table snapshot; a 1M-rule table probed in L2."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from bess_amd import flowtable as F  # noqa: E402
+from bess_amd import packets as P  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def oracle_gates(keys, gates, frames, default_gate=8192):
+    L = O.lib()
+    em = L.or_em_new()
+    for i, (off, size) in enumerate(P.FIVE_TUPLE):
+        L.or_em_add_field(em, off, size, 0, i, None, 0)
+    k = np.ascontiguousarray(keys)
+    g = np.ascontiguousarray(gates, dtype=np.uint16)
+    assert L.or_em_add_rules(em, k.ctypes.data, len(k), k.shape[1], g.ctypes.data) == 0
+    want = np.zeros(len(frames), np.uint16)
+    L.or_em_process(em, frames.ctypes.data, 64, len(frames), default_gate,
+                    want.ctypes.data)
+    L.or_em_free(em)
+    return want
+
+
+@pytest.mark.parametrize("n_rules", [1000, 1 << 20])
+def test_ring_batches_vs_oracle(n_rules):
+    n = 1 << 18
+    keys, gates, frames = P.em_workload(n_rules, n, seed=n_rules, pkt_seed=3)
+    want = oracle_gates(keys, gates, frames)
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    d = torch.from_numpy(frames.reshape(-1)).cuda()
+    ring = F.Ring(t, slots=256)
+    for burst in (32, 100, 4096):
+        dg = torch.full((n,), -1, dtype=torch.int16, device="cuda")
+        ring.run(d, 64, n, burst, 8192, dg)
+        torch.cuda.synchronize()
+        assert (dg.cpu().numpy().view(np.uint16) == want).all(), burst
+    # individual tickets, out-of-order waits, a 1-packet batch
+    dg = torch.full((n,), -1, dtype=torch.int16, device="cuda")
+    tickets = [ring.submit(d, 64, 1, 8192, dg, offset=0)]
+    tickets += [ring.submit(d, 64, 32, 8192, dg, offset=1 + 32 * i) for i in range(50)]
+    ring.wait(tickets[-1])
+    ring.wait(tickets[0])
+    assert ring.completed() >= tickets[-1] + 1
+    got = dg[:1 + 32 * 50].cpu().numpy().view(np.uint16)
+    assert (got == want[:1 + 32 * 50]).all()
+    launches, blocks = ring.info()
+    assert launches >= 1 and blocks > 0
+    ring.close()
+
+
+def test_ring_idle_exit_relaunch_and_snapshot():
+    n = 1 << 14
+    keys, gates, frames = P.em_workload(1000, n, seed=5)
+    want = oracle_gates(keys, gates, frames)
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    d = torch.from_numpy(frames.reshape(-1)).cuda()
+    ring = F.Ring(t, slots=64, idle_us=2000)
+    dg = torch.zeros(n, dtype=torch.int16, device="cuda")
+    ring.run(d, 64, n, 256, 8192, dg)
+    assert (dg.cpu().numpy().view(np.uint16) == want).all()
+    time.sleep(0.05)  # > idle: the grid has stopped itself
+    t.clear()  # a rule change: the ring keeps its snapshot (and memory)
+    t.sync(0)
+    dg.zero_()
+    ring.run(d, 64, n, 512, 8192, dg)
+    assert (dg.cpu().numpy().view(np.uint16) == want).all()
+    launches, _ = ring.info()
+    assert launches >= 2
+    ring.close()
+    # a new ring sees the cleared table
+    ring = F.Ring(t, slots=64)
+    ring.run(d, 64, n, 512, 8192, dg)
+    assert (dg.cpu().numpy().view(np.uint16) == 8192).all()
+    ring.close()
