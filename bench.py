@@ -1284,7 +1284,9 @@ def main():
             "acl": lambda: run_acl(args, dev, torch),
             "hashlb": lambda: run_hashlb(args, dev, torch),
             "pipe": lambda: run_e2e_pipe(args, torch),
-            "c1": lambda: run_c1(args)}
+            "c1": lambda: run_c1(args),
+            "sweep": lambda: em_sweep(run_em(args, rank, world, dev, torch,
+                                             dist), torch)}
     if args.only:
         log(json.dumps(only[args.only]()))
         return

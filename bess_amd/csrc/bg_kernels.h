@@ -220,18 +220,24 @@ struct DnatArgs {
 // sees the whole descriptor, no fence):
 //   w0 frames address | tag << 48     w1 gates address | tag << 48
 //   w2 n | stride << 32 | tag << 48   w3 default gate | tag << 48
-// A workgroup claims tickets from *head (one atomic add), waits for the
-// descriptor, classifies the batch, then publishes done[t % nslots] = t + 1
-// (system scope, after a system release of its gate stores). A workgroup
-// that waits longer than idle_ticks (s_memrealtime, 100 MHz) sets *stop;
-// every workgroup that sees *stop re-checks its descriptor once and exits
-// if it is still unpublished. The host relaunches from its oldest
+// The host then raises *pub (host memory) to t + 1. Workgroup 0 is the
+// dispatcher: one lane polls *pub over PCIe and mirrors it into dev[1]
+// (device memory), so the other workgroups poll L2, not PCIe. A worker
+// workgroup claims a ticket from dev[0] (one atomic add), waits until
+// dev[1] > t, reads the descriptor, classifies the batch and publishes
+// done[t % nslots] = t + 1 (system scope, after a system release of its
+// gate stores). When *pub has not moved for idle_ticks (s_memrealtime,
+// 100 MHz), or the host sets *stop, the dispatcher sets dev[2]: every
+// worker re-checks dev[1] once and exits if its ticket is still
+// unpublished, and the grid ends. The host relaunches from its oldest
 // unfinished ticket (re-classifying a finished batch is harmless).
 struct RingArgs {
   const uint64_t *desc;   // host memory (mapped)
   uint32_t *done;         // host memory (mapped)
-  uint32_t *stop;         // host memory (mapped)
-  unsigned long long *head;  // device memory: next ticket to claim
+  const uint64_t *pub;    // host memory: tickets published
+  const uint32_t *stop;   // host memory: the owner stops the grid
+  unsigned long long *dev;  // device memory: [0] next ticket to claim,
+                            // [1] published (mirror), [2] stop
   uint32_t nslots, pad;
   uint64_t idle_ticks;
   FieldPlan fp;

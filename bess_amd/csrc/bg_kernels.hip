@@ -375,6 +375,77 @@ __device__ __forceinline__ bool ring_read(const uint64_t *d, uint64_t tag,
          (w[3] >> 48) == tag;
 }
 
+__device__ __forceinline__ uint64_t ld_agent(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long *p, uint64_t v) {
+  __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// workgroup 0, one lane: *pub (PCIe) -> dev[1] (L2) until idle or stopped
+__device__ __forceinline__ void ring_dispatch(const RingArgs &a) {
+  uint64_t last = ld_agent(a.dev + 1);
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint64_t p = ld_sys(a.pub);
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (p != last) {
+      st_agent(a.dev + 1, p);
+      last = p;
+      t0 = now;
+    }
+    const uint32_t st = __hip_atomic_load(a.stop, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+    if (st || now - t0 > a.idle_ticks) {
+      st_agent(a.dev + 2, 1);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int KW, int NCH>
+__device__ __forceinline__ void ring_key1(const uint8_t *frames, uint64_t stride,
+                                          uint32_t n, uint32_t i,
+                                          const FieldPlan &fp,
+                                          uint32_t (&w)[NCH * 4 + 2]) {
+#pragma unroll
+  for (int q = 0; q < NCH * 4 + 2; q++) w[q] = 0;
+  if (i < n) load_window<NCH>(frames + (uint64_t)i * stride, fp, w);
+}
+
+template <int KW, int NCH>
+__device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride,
+                                          uint32_t n, uint32_t base,
+                                          const FieldPlan &fp, uint64_t (&k0)[KW],
+                                          uint64_t (&k1)[KW], uint64_t (&k2)[KW],
+                                          uint64_t (&k3)[KW]) {
+  if constexpr (NCH > 0) {
+    uint32_t w0[NCH * 4 + 2], w1[NCH * 4 + 2], w2[NCH * 4 + 2], w3[NCH * 4 + 2];
+    ring_key1<KW, NCH>(frames, stride, n, base, fp, w0);
+    ring_key1<KW, NCH>(frames, stride, n, base + kRingBlock, fp, w1);
+    ring_key1<KW, NCH>(frames, stride, n, base + 2 * kRingBlock, fp, w2);
+    ring_key1<KW, NCH>(frames, stride, n, base + 3 * kRingBlock, fp, w3);
+    extract_key<KW, NCH>(w0, fp, k0);
+    extract_key<KW, NCH>(w1, fp, k1);
+    extract_key<KW, NCH>(w2, fp, k2);
+    extract_key<KW, NCH>(w3, fp, k3);
+  } else {  // fields too far apart for a window: per-field loads
+    uint64_t (*ks[4])[KW] = {&k0, &k1, &k2, &k3};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t i = base + j * kRingBlock;
+      if (i < n) {
+        direct_key<KW>(frames + (uint64_t)i * stride, fp, *ks[j]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < KW; q++) (*ks[j])[q] = 0;
+      }
+    }
+  }
+}
+
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
@@ -382,31 +453,33 @@ void em_ring_kernel(RingArgs a) {
   __shared__ uint64_t sh_w[4];
   __shared__ uint64_t sh_t;
   __shared__ uint32_t sh_go;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) ring_dispatch(a);
+    return;
+  }
   copy_table_to_lds(lds, a.t);  // (ends with a barrier)
   const uint64_t mask48 = (1ull << 48) - 1;
+  constexpr int kPpl = 4;  // packets per lane per round, loads in flight
   for (;;) {
     if (threadIdx.x == 0) {
-      const uint64_t t = atomicAdd(a.head, 1ull);
-      const uint64_t tag = (t + 1) & 0xFFFF;
-      const uint64_t *d = a.desc + (t % a.nslots) * 4;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      uint64_t w[4];
+      const uint64_t t = atomicAdd(a.dev, 1ull);
       uint32_t go = 0;
       for (;;) {
-        if (ring_read(d, tag, w)) {
+        if (ld_agent(a.dev + 1) > t) {
           go = 1;
           break;
         }
-        const uint32_t st = __hip_atomic_load(a.stop, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_SYSTEM);
-        if (st || __builtin_amdgcn_s_memrealtime() - t0 > a.idle_ticks) {
-          if (!st)  // idle: the whole grid drains, the host relaunches
-            __hip_atomic_store(a.stop, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-          go = ring_read(d, tag, w) ? 1u : 0u;  // published meanwhile?
+        if (ld_agent(a.dev + 2)) {  // stopping: published meanwhile?
+          go = ld_agent(a.dev + 1) > t ? 1u : 0u;
           break;
         }
-        __builtin_amdgcn_s_sleep(4);
+        __builtin_amdgcn_s_sleep(2);
+      }
+      uint64_t w[4] = {0, 0, 0, 0};
+      if (go) {
+        const uint64_t tag = (t + 1) & 0xFFFF;
+        const uint64_t *d = a.desc + (t % a.nslots) * 4;
+        while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
       for (int i = 0; i < 4; i++) sh_w[i] = w[i];
@@ -421,11 +494,23 @@ void em_ring_kernel(RingArgs a) {
     const uint64_t stride = (sh_w[2] >> 32) & 0xFFFF;
     const uint32_t dflt = (uint32_t)(sh_w[3] & 0xFFFF);
     const uint64_t t = sh_t;
-    for (uint32_t i = threadIdx.x; i < n; i += kRingBlock) {
-      uint64_t k[1][KW];
-      build_keys<KW, NCH, 1>(frames, stride, n, i, a.fp, k);
-      gates[i] = (uint16_t)(a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, k[0], dflt)
-                                                 : em_lookup<KW>(a.t.base, a.t, k[0], dflt));
+    for (uint32_t base = threadIdx.x; base < n; base += kRingBlock * kPpl) {
+      // kPpl packets per lane, their header windows loaded before any key
+      // is built; one named window array per packet (a 2-D array indexed
+      // by the plan's runtime dword index would live in scratch)
+      uint64_t k0[KW], k1[KW], k2[KW], k3[KW];
+      ring_keys<KW, NCH>(frames, stride, n, base, a.fp, k0, k1, k2, k3);
+      const uint64_t *kk[kPpl] = {k0, k1, k2, k3};
+#pragma unroll
+      for (int j = 0; j < kPpl; j++) {
+        const uint32_t i = base + j * kRingBlock;
+        uint64_t k[KW];
+#pragma unroll
+        for (int q = 0; q < KW; q++) k[q] = kk[j][q];
+        const uint32_t g = a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, k, dflt)
+                                                : em_lookup<KW>(a.t.base, a.t, k, dflt);
+        if (i < n) gates[i] = (uint16_t)g;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -9,10 +9,13 @@
 // once, claims tickets in order, classifies each batch and publishes
 // done[t % slots] = t + 1 in host memory, which wait/poll read.
 //
-// Liveness: a workgroup that waits longer than the idle time for an
-// unpublished descriptor stops the grid, so the kernel always drains on
-// its own (also when the owner never destroys the ring); submit and wait
-// relaunch it from the oldest unfinished ticket when it has ended.
+// One lane of the grid (the dispatcher) polls the host's published count
+// over PCIe and mirrors it in device memory, where the other workgroups
+// wait: hundreds of waiting workgroups poll L2 instead of all issuing
+// PCIe reads. Liveness: when nothing is published for
+// the idle time the dispatcher stops the grid, so the kernel always drains
+// on its own (also when the owner never destroys the ring); submit and
+// wait relaunch it from the oldest unfinished ticket when it has ended.
 // Descriptor words carry the ticket's tag (bg_kernels.h RingArgs), so a
 // descriptor is read whole without fences.
 #include <errno.h>
@@ -41,8 +44,9 @@ struct bg_ring {
   uint64_t *h_desc = nullptr;  // nslots x 4 words, host (coherent, mapped)
   uint32_t *h_done = nullptr;  // nslots, host
   uint32_t *h_stop = nullptr;  // 1 word, host
-  uint64_t *h_head = nullptr;  // pinned source of the head reset
-  unsigned long long *d_head = nullptr;
+  uint64_t *h_pub = nullptr;   // tickets published, host
+  uint64_t *h_reset = nullptr;  // pinned source of the device words' reset
+  unsigned long long *d_dev = nullptr;  // next ticket, published, stop
   uint8_t *d_table = nullptr;  // the ring's own copy of the table image
   RingArgs a{};
   uint64_t next = 0;      // next ticket to publish
@@ -87,8 +91,10 @@ int ensure_running(bg_ring *r) {
   int rc = set_device(r->device);
   if (rc) return rc;
   __atomic_store_n(r->h_stop, 0u, __ATOMIC_RELEASE);
-  *r->h_head = r->done_upto;
-  HIP_TRY(hipMemcpyAsync(r->d_head, r->h_head, 8, hipMemcpyHostToDevice, r->st));
+  r->h_reset[0] = r->done_upto;  // claims restart at the oldest unfinished
+  r->h_reset[1] = r->done_upto;  // the dispatcher picks up *pub at once
+  r->h_reset[2] = 0;
+  HIP_TRY(hipMemcpyAsync(r->d_dev, r->h_reset, 24, hipMemcpyHostToDevice, r->st));
   HIP_TRY(launch_em_ring(r->a, r->blocks, r->st));
   HIP_TRY(hipEventRecord(r->ev, r->st));
   r->running = true;
@@ -102,8 +108,9 @@ void ring_release(bg_ring *r) {
   if (r->h_desc) (void)hipHostFree(r->h_desc);
   if (r->h_done) (void)hipHostFree(r->h_done);
   if (r->h_stop) (void)hipHostFree(r->h_stop);
-  if (r->h_head) (void)hipHostFree(r->h_head);
-  if (r->d_head) (void)hipFree(r->d_head);
+  if (r->h_pub) (void)hipHostFree(r->h_pub);
+  if (r->h_reset) (void)hipHostFree(r->h_reset);
+  if (r->d_dev) (void)hipFree(r->d_dev);
   if (r->d_table) (void)hipFree(r->d_table);
   if (r->ev) (void)hipEventDestroy(r->ev);
   if (r->st) (void)hipStreamDestroy(r->st);
@@ -137,14 +144,16 @@ int bg_em_ring_create(bg_em *em, int device, int slots, int blocks,
   bg_ring *r = new bg_ring();
   r->device = device;
   r->nslots = (uint32_t)slots;
-  r->blocks = blocks > 0 ? blocks : 2 * num_cus(device);
+  // workers + the dispatcher
+  r->blocks = (blocks > 0 ? blocks : 2 * num_cus(device)) + 1;
   hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
   if (e == hipSuccess) e = host_alloc(&r->h_desc, (size_t)slots * 32);
   if (e == hipSuccess) e = host_alloc(&r->h_done, (size_t)slots * 4);
   if (e == hipSuccess) e = host_alloc(&r->h_stop, 64);
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&r->h_head), 64);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->d_head), 8);
+  if (e == hipSuccess) e = host_alloc(&r->h_pub, 64);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&r->h_reset), 64);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->d_dev), 64);
   if (e != hipSuccess) {
     ring_release(r);
     delete r;
@@ -153,14 +162,16 @@ int bg_em_ring_create(bg_em *em, int device, int slots, int blocks,
   memset(r->h_desc, 0, (size_t)slots * 32);  // tag 0: no ticket's
   memset(r->h_done, 0, (size_t)slots * 4);
   *r->h_stop = 0;
+  *r->h_pub = 0;
   RingArgs &a = r->a;
   a.desc = dev_alias(r->h_desc);
   a.done = dev_alias(r->h_done);
   a.stop = dev_alias(r->h_stop);
-  a.head = r->d_head;
+  a.pub = dev_alias(r->h_pub);
+  a.dev = r->d_dev;
   a.nslots = (uint32_t)slots;
   a.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
-  if (!a.desc || !a.done || !a.stop) {
+  if (!a.desc || !a.done || !a.stop || !a.pub) {
     ring_release(r);
     delete r;
     return fail(EIO, "no device address for the ring's host memory");
@@ -220,7 +231,8 @@ int64_t bg_ring_submit(bg_ring *r, const void *frames, size_t stride, size_t n,
   __atomic_store_n(d + 0, ((uint64_t)(uintptr_t)frames & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 1, ((uint64_t)(uintptr_t)gates & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 2, (uint64_t)n | ((uint64_t)stride << 32) | tag, __ATOMIC_RELAXED);
-  __atomic_store_n(d + 3, (uint64_t)default_gate | tag, __ATOMIC_RELEASE);
+  __atomic_store_n(d + 3, (uint64_t)default_gate | tag, __ATOMIC_RELAXED);
+  __atomic_store_n(r->h_pub, t + 1, __ATOMIC_RELEASE);
   r->next = t + 1;
   if (int rc = ensure_running(r)) return rc;
   return (int64_t)t;
@@ -261,7 +273,7 @@ int bg_ring_run(bg_ring *r, const void *frames, size_t stride, size_t n,
 
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks) {
   if (launches) *launches = r->launches;
-  if (blocks) *blocks = r->blocks;
+  if (blocks) *blocks = r->blocks - 1;  // workers
   return 0;
 }
 
