@@ -68,6 +68,8 @@ def parse():
                     help="no GPU: the N-rank sharded table build of C5 over "
                          "gloo (CPU tests of the multi-GPU launch and control "
                          "path); prints the line with value null")
+    ap.add_argument("--wm-layout", default="both", choices=("both", "slab", "2k"),
+                    help="C4 layouts to time (PMC passes time one at a time)")
     ap.add_argument("--c5-rules", type=int, default=1 << 20,
                     help="rules of the sharded C5 table in the N > 1 line")
     ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|pipe (profiling runs)")
@@ -915,12 +917,6 @@ def run_wm(args, dev, torch):
     t = F.WmTable(P.FIVE_TUPLE)
     for k, m, p, g in zip(rk, rm, prio, gates):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
-    d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
-    d = d0.repeat(rep)
-    del d0
-    dg = torch.empty(n, dtype=torch.int16, device=dev)
-    t.classify(d, 2048, n, 8192, dg)
-    torch.cuda.synchronize()
     # parity: oracle WildcardMatch on the first 64K frames
     L = O.lib()
     ow = L.or_wm_new()
@@ -937,23 +933,57 @@ def run_wm(args, dev, torch):
     sample = np.ascontiguousarray(frames[:ns])
     want = np.zeros(ns, np.uint16)
     L.or_wm_process(ow, sample.ctypes.data, 2048, ns, 8192, want.ctypes.data)
-    got = dg.cpu().numpy().view(np.uint16)
-    parity = bool((got[:ns] == want).all() and
-                  (got.reshape(rep, n0) == got[:n0]).all())
-    for _ in range(args.warmup):
+
+    def timed(slab, stride, gates):
+        for _ in range(args.warmup):
+            t.classify(slab, stride, n, 8192, gates)
+        torch.cuda.synchronize()
+        timer = Timer(torch)
+        timer.start()
+        for _ in range(args.steps):
+            t.classify(slab, stride, n, 8192, gates)
+        return timer.stop_ms() / args.steps
+
+    def check(gates_t):
+        got = gates_t.cpu().numpy().view(np.uint16)
+        return bool((got[:ns] == want).all() and
+                    (got.reshape(rep, n0) == got[:n0]).all()), got[:n0]
+
+    nan = float("nan")
+    parity, ms2k, g2k = True, nan, None
+    if args.wm_layout != "slab":  # the frames in 2 KB slots
+        d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
+        d = d0.repeat(rep)
+        del d0
+        dg = torch.empty(n, dtype=torch.int16, device=dev)
         t.classify(d, 2048, n, 8192, dg)
-    torch.cuda.synchronize()
-    timer = Timer(torch)
-    timer.start()
-    for _ in range(args.steps):
-        t.classify(d, 2048, n, 8192, dg)
-    ms = timer.stop_ms() / args.steps
+        torch.cuda.synchronize()
+        parity, g2k = check(dg)
+        ms2k = timed(d, 2048, dg)
+        del d, dg
+    gbs2k = EM_BYTES_PER_PKT * n / (ms2k * 1e-3) / 1e9
+    # The same packets' header lines in a dense 64 B slab: the layout the
+    # north star asks for ("batches laid out for coalesced HBM reads of
+    # header bytes"), which the host ingress (bg_pipe) stages anyway.
+    ms, parity_h = nan, True
+    if args.wm_layout != "2k":
+        h0 = torch.from_numpy(np.ascontiguousarray(frames[:, :64]).reshape(-1)).to(dev)
+        hs = h0.repeat(rep)
+        del h0
+        dgh = torch.empty(n, dtype=torch.int16, device=dev)
+        t.classify(hs, 64, n, 8192, dgh)
+        torch.cuda.synchronize()
+        parity_h, gh = check(dgh)
+        if g2k is not None:
+            parity_h = parity_h and bool((gh == g2k).all())
+        ms = timed(hs, 64, dgh)
+        del hs, dgh
     mpps = n / (ms * 1e-3) / 1e6
     gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
     nbytes, in_lds = t.table_info()
     out = {"workload": "C4: 100K-rule WildcardMatch over 8 masks (tuple-space,"
-                       " priority ties), 5-tuple, header lines of IMIX frames "
-                       "in 2KB slots",
+                       " priority ties), 5-tuple, IMIX frames' header lines in "
+                       "a dense 64B slab (beside: the frames in 2KB slots)",
            "pkts": n, "ms_per_step": round(ms, 4), "Mpps": round(mpps, 1),
            "table_bytes": nbytes,
            "table_in_lds": {0: "no (L2/MALL)", 1: "whole table",
@@ -964,8 +994,16 @@ def run_wm(args, dev, torch):
                         "frac": round(gbs / HBM_PEAK_GBS, 4),
                         "traffic": traffic_gbs("wm", ms),
                         "traffic_bytes_per_launch": load_traffic("wm")},
-           "parity": "bit-exact vs oracle on 64K-pkt sample" if parity
-                     else "MISMATCH"}
+           "parity": "bit-exact vs oracle on 64K-pkt samples of both layouts; "
+                     "header-slab gates == 2KB-slot gates on all %d pkts" % n0
+                     if parity and parity_h else "MISMATCH",
+           "slots_2k": {"ms_per_step": round(ms2k, 4),
+                        "Mpps": round(n / (ms2k * 1e-3) / 1e6, 1),
+                        "roofline": {"bound": "hbm", "achieved": round(gbs2k, 1),
+                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(gbs2k / HBM_PEAK_GBS, 4),
+                                     "traffic": traffic_gbs("wm2k", ms2k),
+                                     "traffic_bytes_per_launch": load_traffic("wm2k")}}}
     if not args.no_cpu:
         cn = 1 << 16
         g = np.zeros(cn, np.uint16)
