@@ -14,13 +14,14 @@
 //      fingerprint match is appended to a per-wave LDS queue as
 //      (slot, lane, tuple) with a ballot + mbcnt prefix, so the key checks
 //      run on dense lanes instead of on whichever lanes happen to match;
-//   3. each full 64-entry batch of the queue (and the remainder at the end
-//      of the tile) is checked in one round trip: a lane loads the slot's
-//      key and value from L2, compares it with its packet's masked key
-//      (fetched from the owning lane with ds_bpermute) and folds a hit into
-//      the packet's best with a 64-bit LDS atomic max over
-//      (priority, tuple, gate) -- the highest priority wins and an equal
-//      priority goes to the later tuple, LookupEntry's '>=' (P5);
+//   3. at the end of the tile the queued entries are checked in one round
+//      trip, two per lane (the queue holds 256; only a tile with more than
+//      two candidates per packet checks a 64-entry batch early): a lane
+//      loads each entry's slot key and value from L2, compares it with its
+//      packet's masked key (fetched from the owning lane with ds_bpermute)
+//      and folds a hit into the packet's best with a 64-bit LDS atomic max
+//      over (priority, tuple, gate) -- the highest priority wins and an
+//      equal priority goes to the later tuple, LookupEntry's '>=' (P5);
 //   4. gate = the best's gate, or the default gate when nothing matched.
 //
 // One 1024-thread workgroup per CU (tags <= 128 KB + 1 KB per wave).
@@ -35,46 +36,84 @@ namespace {
 
 constexpr int kWmBlock = 1024;
 constexpr int kWaves = kWmBlock / 64;
-constexpr uint32_t kQueue = 128;        // entries per wave (ring)
+constexpr uint32_t kQueue = 256;        // entries per wave (ring)
 constexpr uint32_t kWaveLds = 64 * 8 + kQueue * 4;  // best[64] + queue
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
-// Check queue entries [head, head + m), one per lane: slot | lane << 20 |
-// tuple << 26.
+// The owning lane's key for queue entry e (every lane takes part in the
+// permutes)
+template <int KW>
+__device__ __forceinline__ void owner_key(uint32_t e, const uint64_t (&k)[KW],
+                                          uint64_t (&kk)[KW]) {
+  const int pl = (int)((e >> 20) & 63u);
+#pragma unroll
+  for (int j = 0; j < KW; j++) {
+    const uint32_t lo = shfl32((uint32_t)k[j], pl);
+    const uint32_t hi = shfl32((uint32_t)(k[j] >> 32), pl);
+    kk[j] = (uint64_t)hi << 32 | lo;
+  }
+}
+
+// fold a hit of entry e (slot value v) into its packet's best
+__device__ __forceinline__ void wm_fold(uint64_t *best, uint32_t e, uint64_t v) {
+  const uint32_t pl = (e >> 20) & 63u, tu = e >> 26;
+  // (priority as unsigned order, valid bit, tuple, gate)
+  const uint64_t comb = ((uint64_t)((uint32_t)v ^ 0x80000000u) << 32) |
+                        (1u << 19) | (tu << 16) | ((uint32_t)(v >> 32) & 0xFFFFu);
+  atomicMax(reinterpret_cast<unsigned long long *>(best + pl),
+            (unsigned long long)comb);
+}
+
+template <int KW>
+__device__ __forceinline__ bool wm_hit(const uint64_t *mlds, uint32_t e,
+                                       uint64_t v, const uint64_t (&sk)[KW],
+                                       const uint64_t (&kk)[KW]) {
+  const uint32_t tu = e >> 26;
+  bool hit = (uint32_t)(v >> 48) == tu;
+#pragma unroll
+  for (int j = 0; j < KW; j++) hit &= sk[j] == (kk[j] & mlds[tu * KW + j]);
+  return hit;
+}
+
+// Check queue entries [head, head + m), m <= 128: lane l takes entries l
+// and l + 64; an entry is slot | lane << 20 | tuple << 26. Both entries'
+// key and value loads are issued before either is compared (one L2 round
+// trip for up to two candidates per packet of the tile).
 template <int KW>
 __device__ __forceinline__ void wm_check(const WmArgs &a, const uint64_t *mlds,
                                          uint64_t *best, const uint32_t *q,
                                          uint32_t head, uint32_t m, int lane,
                                          const uint64_t (&k)[KW]) {
-  const uint32_t e = q[(head + lane) & (kQueue - 1)];
-  const uint32_t slot = e & 0xFFFFFu, pl = (e >> 20) & 63u, tu = e >> 26;
-  // the owning lane's key (every lane takes part in the permutes)
-  uint64_t kk[KW];
+  const uint32_t e0 = q[(head + lane) & (kQueue - 1)];
+  const uint32_t e1 = q[(head + 64 + lane) & (kQueue - 1)];
+  uint64_t kk0[KW], kk1[KW];
+  owner_key<KW>(e0, k, kk0);
+  const bool two = m > 64;  // wave-uniform
+  if (two) owner_key<KW>(e1, k, kk1);
+  const uint8_t *tab = a.t.base;
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(tab + a.t.keys_off);
+  const bool l0 = (uint32_t)lane < m, l1 = two && (uint32_t)lane + 64 < m;
+  uint64_t v0 = 0, v1 = 0, sk0[KW], sk1[KW];
 #pragma unroll
-  for (int j = 0; j < KW; j++) {
-    const uint32_t lo = shfl32((uint32_t)k[j], (int)pl);
-    const uint32_t hi = shfl32((uint32_t)(k[j] >> 32), (int)pl);
-    kk[j] = (uint64_t)hi << 32 | lo;
-  }
-  if ((uint32_t)lane < m) {
-    const uint8_t *tab = a.t.base;
-    const uint64_t v = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off)[slot];
-    const uint64_t *sk =
-        reinterpret_cast<const uint64_t *>(tab + a.t.keys_off) + (uint64_t)slot * KW;
-    bool hit = (uint32_t)(v >> 48) == tu;
+  for (int j = 0; j < KW; j++) sk0[j] = sk1[j] = 0;
+  if (l0) {
+    const uint32_t slot = e0 & 0xFFFFFu;
+    v0 = vals[slot];
 #pragma unroll
-    for (int j = 0; j < KW; j++) hit &= sk[j] == (kk[j] & mlds[tu * KW + j]);
-    if (hit) {
-      // (priority as unsigned order, valid bit, tuple, gate)
-      const uint64_t comb = ((uint64_t)((uint32_t)v ^ 0x80000000u) << 32) |
-                            (1u << 19) | (tu << 16) | ((uint32_t)(v >> 32) & 0xFFFFu);
-      atomicMax(reinterpret_cast<unsigned long long *>(best + pl),
-                (unsigned long long)comb);
-    }
+    for (int j = 0; j < KW; j++) sk0[j] = keys[(uint64_t)slot * KW + j];
   }
+  if (l1) {
+    const uint32_t slot = e1 & 0xFFFFFu;
+    v1 = vals[slot];
+#pragma unroll
+    for (int j = 0; j < KW; j++) sk1[j] = keys[(uint64_t)slot * KW + j];
+  }
+  if (l0 && wm_hit<KW>(mlds, e0, v0, sk0, kk0)) wm_fold(best, e0, v0);
+  if (l1 && wm_hit<KW>(mlds, e1, v1, sk1, kk1)) wm_fold(best, e1, v1);
 }
 
 template <int KW, int NCH>
@@ -166,7 +205,7 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
                 slot | ((uint32_t)lane << 20) | ((uint32_t)tu << 26);
           }
           qlen += (uint32_t)__popcll(bal);
-          if (qlen >= 64) {
+          if (qlen > kQueue - 64) {  // room for one more ballot round
             lds_fence();
             wm_check<KW>(a, mlds, best, q, head, 64, lane, k);
             head += 64;
@@ -175,9 +214,12 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
         }
       }
     }
-    if (qlen) {
+    while (qlen) {
       lds_fence();
-      wm_check<KW>(a, mlds, best, q, head, qlen, lane, k);
+      const uint32_t m = qlen < 128 ? qlen : 128;
+      wm_check<KW>(a, mlds, best, q, head, m, lane, k);
+      head += m;
+      qlen -= m;
     }
     lds_fence();
     const uint64_t b = best[lane];
