@@ -68,6 +68,8 @@ def parse():
                     help="no GPU: the N-rank sharded table build of C5 over "
                          "gloo (CPU tests of the multi-GPU launch and control "
                          "path); prints the line with value null")
+    ap.add_argument("--pipe-threads", default="1,4,16",
+                    help="worker threads of the bg_pipe legs")
     ap.add_argument("--wm-layout", default="both", choices=("both", "slab", "2k"),
                     help="C4 layouts to time (PMC passes time one at a time)")
     ap.add_argument("--c5-rules", type=int, default=1 << 20,
@@ -528,7 +530,7 @@ def run_e2e_pipe(args, torch):
         em["parity_batch%d" % batch] = bool((p.run(heads) == want).all())
         p.close()
         rates = {}
-        for th in (1, 4, 16):
+        for th in [int(x) for x in args.pipe_threads.split(",")]:
             rates[str(th)] = _pipe_rate(
                 lambda: Pipe(m, batch=batch, depth=4), heads, None, th,
                 reps=2 if th == 1 else 4)
@@ -551,7 +553,7 @@ def run_e2e_pipe(args, torch):
     ck = {"parity": bool((g == l4w).all() and
                          (snb[:, 512:512 + 1496] == ref[:, :1496]).all())}
     rates = {}
-    for th in (1, 4, 16):
+    for th in [int(x) for x in args.pipe_threads.split(",")]:
         rates[str(th)] = _pipe_rate(
             lambda: Pipe(mk, batch=8192, depth=4, span=1504), heads, lens, th,
             reps=4)

@@ -1093,6 +1093,7 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
   a.t = wm->dev.ref();
   for (size_t t = 0; t < wm->tuples.size(); t++)
     for (uint32_t j = 0; j < wm->kw; j++) a.tmask[t][j] = wm->tuples[t].mask.w[j];
+  a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
   HIP_TRY(launch_wm(a, num_cus(wm->dev.device), s));
   return 0;
 }

@@ -106,6 +106,7 @@ struct WmArgs {
   FieldPlan fp;
   TableRef t;
   uint64_t tmask[kMaxTuples][kMaxKeyWords];
+  uint32_t ab_phase, pad2;  // A/B build only: stop after a phase (timing)
 };
 
 struct CkArgs {

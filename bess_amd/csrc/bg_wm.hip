@@ -156,6 +156,12 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
       load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
     uint64_t k[KW];
     extract_key<KW, NCH>(w, a.fp, k);
+#ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
+    if (a.ab_phase == 1) {
+      if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
+      continue;
+    }
+#endif
     const kconst_u64 tm = tuple_masks(a);  // laundered per tile: no hoisting
 
     // A. every tuple's hash and both tag words (16 LDS reads in flight)
@@ -177,6 +183,15 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
         tw2[tu] = tags[p.b2];
       }
     }
+#ifdef BG_AB  // phase timing: + hashes and tag reads
+    if (a.ab_phase == 2) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int tu = 0; tu < kMaxTuples; tu++) x ^= tw1[tu] ^ tw2[tu];
+      if (live) a.gates[idx] = (uint16_t)x;
+      continue;
+    }
+#endif
     // B. fingerprint matches -> queue; full batches checked on the way
     uint32_t head = 0, qlen = 0;  // wave-uniform
 #pragma unroll

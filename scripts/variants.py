@@ -28,6 +28,7 @@ from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
+         "BG_WM_PHASE",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2"]
@@ -161,7 +162,28 @@ def main():
             r[k]["GBps_1502B"] = round(1502 * n / (r[k]["median_ms"] * 1e-3) / 1e9, 1)
         out["ck"] = r
         del d
-    if "wm" in which:
+    if "wmphase" in which:
+        # C4 on the dense header slab, timed up to each phase of
+        # wm_tags_kernel (BG_WM_PHASE: 1 header read + key, 2 + the 8
+        # tuple hashes and tag reads, 0 everything)
+        n = 1 << 23
+        rk, rm, prio, gates, frames, _ = P.wm_workload(100000, 1 << 20, stride=64,
+                                                      sizes=((60, 1),))
+        d = torch.from_numpy(frames.reshape(-1)).to(dev).repeat(8)
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        t = F.WmTable(P.FIVE_TUPLE)
+        for k, m, p, gg in zip(rk, rm, prio, gates):
+            t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
+        t.sync(0)
+        variants = {"full": {}, "read_key": {"BG_WM_PHASE": 1},
+                    "hash_tags": {"BG_WM_PHASE": 2}}
+        r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants,
+                          reps=20)
+        for k in r:
+            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+        out["wmphase"] = r
+        del d, g
+    if "wm" in which.split(","):
         n = 1 << 22
         rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n, stride=64,
                                                       sizes=((60, 1),))
