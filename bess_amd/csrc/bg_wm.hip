@@ -11,20 +11,22 @@
 //      P4), the next tile's window in flight;
 //   2. per tuple (wave-uniform): key & mask, hash, both tag words from
 //      LDS (all tuples' reads issued before any is used); every
-//      fingerprint match is appended to a per-wave LDS queue as
+//      fingerprint match is appended to the tile's per-wave LDS queue as
 //      (slot, lane, tuple) with a ballot + mbcnt prefix, so the key checks
 //      run on dense lanes instead of on whichever lanes happen to match;
-//   3. at the end of the tile the queued entries are checked in one round
-//      trip, two per lane (the queue holds 256; only a tile with more than
-//      two candidates per packet checks a 64-entry batch early): a lane
-//      loads each entry's slot key and value from L2, compares it with its
-//      packet's masked key (fetched from the owning lane with ds_bpermute)
-//      and folds a hit into the packet's best with a 64-bit LDS atomic max
-//      over (priority, tuple, gate) -- the highest priority wins and an
-//      equal priority goes to the later tuple, LookupEntry's '>=' (P5);
+//   3. the tile's queued entries are checked two per lane: a lane loads
+//      each entry's slot key and value from L2 and the owning lane's key
+//      comes over with ds_bpermute. Those loads are software-pipelined: they
+//      are issued at the end of tile t and consumed after steps 1-2 of tile
+//      t + 1, so the L2 round trip overlaps the next tile's hashing. A hit
+//      is folded into the packet's best with a 64-bit LDS atomic max over
+//      (priority, tuple, gate) -- the highest priority wins and an equal
+//      priority goes to the later tuple, LookupEntry's '>=' (P5). (A tile
+//      with more than 128 candidates checks 64 of them at once.)
 //   4. gate = the best's gate, or the default gate when nothing matched.
 //
-// One 1024-thread workgroup per CU (tags <= 128 KB + 1 KB per wave).
+// One 960-thread workgroup per CU: tags <= 128 KB + per wave two queues of
+// 128 entries and two best arrays (tiles t and t + 1), 2 KB.
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
@@ -34,10 +36,10 @@
 namespace bg {
 namespace {
 
-constexpr int kWmBlock = 1024;
+constexpr int kWmBlock = 960;           // 15 waves: LDS for the tags + 2 KB each
 constexpr int kWaves = kWmBlock / 64;
-constexpr uint32_t kQueue = 256;        // entries per wave (ring)
-constexpr uint32_t kWaveLds = 64 * 8 + kQueue * 4;  // best[64] + queue
+constexpr uint32_t kQueue = 128;        // entries per wave per tile (ring)
+constexpr uint32_t kWaveLds = 2 * (64 * 8 + kQueue * 4);  // 2 x (best + queue)
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
@@ -78,42 +80,53 @@ __device__ __forceinline__ bool wm_hit(const uint64_t *mlds, uint32_t e,
   return hit;
 }
 
-// Check queue entries [head, head + m), m <= 128: lane l takes entries l
-// and l + 64; an entry is slot | lane << 20 | tuple << 26. Both entries'
-// key and value loads are issued before either is compared (one L2 round
-// trip for up to two candidates per packet of the tile).
+// Up to 128 queued entries of one tile in flight: lane l holds entries l
+// and l + 64 (an entry is slot | lane << 20 | tuple << 26), the owning
+// lanes' keys and the slots' keys and values being loaded.
 template <int KW>
-__device__ __forceinline__ void wm_check(const WmArgs &a, const uint64_t *mlds,
-                                         uint64_t *best, const uint32_t *q,
+struct Pending {
+  uint32_t e0, e1, m;  // m: entries (wave-uniform), 0 = none
+  uint64_t v0, v1, sk0[KW], sk1[KW], kk0[KW], kk1[KW];
+};
+
+// Issue the loads of queue entries [head, head + m), m <= 128.
+template <int KW>
+__device__ __forceinline__ void wm_issue(const WmArgs &a, const uint32_t *q,
                                          uint32_t head, uint32_t m, int lane,
-                                         const uint64_t (&k)[KW]) {
-  const uint32_t e0 = q[(head + lane) & (kQueue - 1)];
-  const uint32_t e1 = q[(head + 64 + lane) & (kQueue - 1)];
-  uint64_t kk0[KW], kk1[KW];
-  owner_key<KW>(e0, k, kk0);
-  const bool two = m > 64;  // wave-uniform
-  if (two) owner_key<KW>(e1, k, kk1);
+                                         const uint64_t (&k)[KW], Pending<KW> &p) {
+  p.m = m;
+  p.e0 = q[(head + lane) & (kQueue - 1)];
+  p.e1 = q[(head + 64 + lane) & (kQueue - 1)];
+  owner_key<KW>(p.e0, k, p.kk0);
+  if (m > 64) owner_key<KW>(p.e1, k, p.kk1);  // wave-uniform
   const uint8_t *tab = a.t.base;
   const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(tab + a.t.keys_off);
-  const bool l0 = (uint32_t)lane < m, l1 = two && (uint32_t)lane + 64 < m;
-  uint64_t v0 = 0, v1 = 0, sk0[KW], sk1[KW];
+  p.v0 = p.v1 = 0;
 #pragma unroll
-  for (int j = 0; j < KW; j++) sk0[j] = sk1[j] = 0;
-  if (l0) {
-    const uint32_t slot = e0 & 0xFFFFFu;
-    v0 = vals[slot];
+  for (int j = 0; j < KW; j++) p.sk0[j] = p.sk1[j] = 0;
+  if ((uint32_t)lane < m) {
+    const uint32_t slot = p.e0 & 0xFFFFFu;
+    p.v0 = vals[slot];
 #pragma unroll
-    for (int j = 0; j < KW; j++) sk0[j] = keys[(uint64_t)slot * KW + j];
+    for (int j = 0; j < KW; j++) p.sk0[j] = keys[(uint64_t)slot * KW + j];
   }
-  if (l1) {
-    const uint32_t slot = e1 & 0xFFFFFu;
-    v1 = vals[slot];
+  if ((uint32_t)lane + 64 < m) {
+    const uint32_t slot = p.e1 & 0xFFFFFu;
+    p.v1 = vals[slot];
 #pragma unroll
-    for (int j = 0; j < KW; j++) sk1[j] = keys[(uint64_t)slot * KW + j];
+    for (int j = 0; j < KW; j++) p.sk1[j] = keys[(uint64_t)slot * KW + j];
   }
-  if (l0 && wm_hit<KW>(mlds, e0, v0, sk0, kk0)) wm_fold(best, e0, v0);
-  if (l1 && wm_hit<KW>(mlds, e1, v1, sk1, kk1)) wm_fold(best, e1, v1);
+}
+
+// Compare the loaded entries and fold the hits into `best`.
+template <int KW>
+__device__ __forceinline__ void wm_resolve(const uint64_t *mlds, uint64_t *best,
+                                           int lane, const Pending<KW> &p) {
+  if ((uint32_t)lane < p.m && wm_hit<KW>(mlds, p.e0, p.v0, p.sk0, p.kk0))
+    wm_fold(best, p.e0, p.v0);
+  if ((uint32_t)lane + 64 < p.m && wm_hit<KW>(mlds, p.e1, p.v1, p.sk1, p.kk1))
+    wm_fold(best, p.e1, p.v1);
 }
 
 template <int KW, int NCH>
@@ -134,9 +147,12 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + wid * kWaveLds;
-  uint64_t *best = reinterpret_cast<uint64_t *>(wl);
-  uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
-  best[lane] = 0;
+  // two buffers: the tile being hashed (cur) and the one whose key checks
+  // are in flight (cur ^ 1)
+  uint64_t *bests = reinterpret_cast<uint64_t *>(wl);            // [2][64]
+  uint32_t *queues = reinterpret_cast<uint32_t *>(wl + 2 * 64 * 8);  // [2][kQueue]
+  bests[lane] = 0;
+  bests[64 + lane] = 0;
   __syncthreads();
 
   const uint64_t ntiles = (a.n + 63) / 64;
@@ -145,6 +161,20 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   uint32_t wn[NCH * 4 + 2];
   if (t < ntiles && t * 64 + lane < a.n)
     load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
+  Pending<KW> pend;
+  pend.m = 0;
+  int cur = 0;
+  uint64_t prev_idx = 0;
+  bool prev_live = false, have_prev = false;
+  // the previous tile: its checks resolved, its gates out
+  auto finish_prev = [&]() {
+    uint64_t *best = bests + (cur ^ 1) * 64;
+    wm_resolve<KW>(mlds, best, lane, pend);
+    lds_fence();
+    const uint64_t b = best[lane];
+    best[lane] = 0;
+    if (prev_live) a.gates[prev_idx] = b ? (uint16_t)b : (uint16_t)a.default_gate;
+  };
   for (; t < ntiles; t += nw) {
     const uint64_t idx = t * 64 + lane;
     const bool live = idx < a.n;
@@ -192,7 +222,11 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
       continue;
     }
 #endif
-    // B. fingerprint matches -> queue; full batches checked on the way
+    // B. fingerprint matches -> this tile's queue (a full queue checks 64
+    // entries at once)
+    uint64_t *best = bests + cur * 64;
+    const uint32_t *qc = queues + cur * kQueue;
+    uint32_t *q = queues + cur * kQueue;
     uint32_t head = 0, qlen = 0;  // wave-uniform
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
@@ -222,25 +256,26 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
           qlen += (uint32_t)__popcll(bal);
           if (qlen > kQueue - 64) {  // room for one more ballot round
             lds_fence();
-            wm_check<KW>(a, mlds, best, q, head, 64, lane, k);
+            Pending<KW> now;
+            wm_issue<KW>(a, qc, head, 64, lane, k, now);
+            wm_resolve<KW>(mlds, best, lane, now);
             head += 64;
             qlen -= 64;
           }
         }
       }
     }
-    while (qlen) {
-      lds_fence();
-      const uint32_t m = qlen < 128 ? qlen : 128;
-      wm_check<KW>(a, mlds, best, q, head, m, lane, k);
-      head += m;
-      qlen -= m;
-    }
+    // C. the previous tile's checks (loads issued one tile ago) and gates
+    if (have_prev) finish_prev();
+    // D. this tile's checks go in flight
     lds_fence();
-    const uint64_t b = best[lane];
-    best[lane] = 0;
-    if (live) a.gates[idx] = b ? (uint16_t)b : (uint16_t)a.default_gate;
+    wm_issue<KW>(a, qc, head, qlen, lane, k, pend);
+    prev_idx = idx;
+    prev_live = live;
+    have_prev = true;
+    cur ^= 1;
   }
+  if (have_prev) finish_prev();
 }
 
 template <int KW, int NCH>
