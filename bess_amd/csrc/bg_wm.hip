@@ -10,23 +10,24 @@
 //   1. header window -> raw key (WildcardMatch's unmasked 8-byte loads,
 //      P4), the next tile's window in flight;
 //   2. per tuple (wave-uniform): key & mask, hash, both tag words from
-//      LDS (all tuples' reads issued before any is used); every
-//      fingerprint match is appended to the tile's per-wave LDS queue as
-//      (slot, lane, tuple) with a ballot + mbcnt prefix, so the key checks
-//      run on dense lanes instead of on whichever lanes happen to match;
-//   3. the tile's queued entries are checked two per lane: a lane loads
-//      each entry's slot key and value from L2 and the owning lane's key
-//      comes over with ds_bpermute. Those loads are software-pipelined: they
-//      are issued at the end of tile t and consumed after steps 1-2 of tile
-//      t + 1, so the L2 round trip overlaps the next tile's hashing. A hit
-//      is folded into the packet's best with a 64-bit LDS atomic max over
-//      (priority, tuple, gate) -- the highest priority wins and an equal
-//      priority goes to the later tuple, LookupEntry's '>=' (P5). (A tile
-//      with more than 128 candidates checks 64 of them at once.)
-//   4. gate = the best's gate, or the default gate when nothing matched.
+//      LDS (all tuples' reads issued before any is used);
+//   3. every fingerprint match goes into a per-wave LDS queue as (slot,
+//      lane, tuple): each lane counts its matches, a bit-sliced wave prefix
+//      sum (one ballot + mbcnt per count bit) gives each lane its first
+//      queue position, and each lane writes its own entries -- so the key
+//      checks run on dense lanes instead of on whichever lanes matched
+//      (measured: the per-tuple ballot loop this replaces took a third of
+//      the kernel);
+//   4. the queue (<= 256 entries; more go in further rounds) is checked
+//      with up to four entries per lane, all their loads in flight at
+//      once: a lane loads each entry's slot key and value from L2 and the
+//      owning lane's key comes over with ds_bpermute; a hit is folded into
+//      the packet's best with a 64-bit LDS atomic max over (priority,
+//      tuple, gate) -- the highest priority wins and an equal priority
+//      goes to the later tuple, LookupEntry's '>=' (P5);
+//   5. gate = the best's gate, or the default gate when nothing matched.
 //
-// One 960-thread workgroup per CU: tags <= 128 KB + per wave two queues of
-// 128 entries and two best arrays (tiles t and t + 1), 2 KB.
+// One 1024-thread workgroup per CU (tags <= 128 KB + 1.5 KB per wave).
 #include <hip/hip_runtime.h>
 #include <limits.h>
 
@@ -36,10 +37,11 @@
 namespace bg {
 namespace {
 
-constexpr int kWmBlock = 960;           // 15 waves: LDS for the tags + 2 KB each
+constexpr int kWmBlock = 1024;
 constexpr int kWaves = kWmBlock / 64;
-constexpr uint32_t kQueue = 128;        // entries per wave per tile (ring)
-constexpr uint32_t kWaveLds = 2 * (64 * 8 + kQueue * 4);  // 2 x (best + queue)
+constexpr uint32_t kQueue = 256;        // entries per wave per round
+constexpr int kPerLane = kQueue / 64;   // entries a lane checks per round
+constexpr uint32_t kWaveLds = 64 * 8 + kQueue * 4;  // best[64] + queue
 
 __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
@@ -80,53 +82,57 @@ __device__ __forceinline__ bool wm_hit(const uint64_t *mlds, uint32_t e,
   return hit;
 }
 
-// Up to 128 queued entries of one tile in flight: lane l holds entries l
-// and l + 64 (an entry is slot | lane << 20 | tuple << 26), the owning
-// lanes' keys and the slots' keys and values being loaded.
+// Check queue entries [0, m), m <= kQueue: lane l takes entries l, l + 64,
+// ... (an entry is slot | lane << 20 | tuple << 26); every entry's key and
+// value loads are issued before any is compared (one L2 round trip).
 template <int KW>
-struct Pending {
-  uint32_t e0, e1, m;  // m: entries (wave-uniform), 0 = none
-  uint64_t v0, v1, sk0[KW], sk1[KW], kk0[KW], kk1[KW];
-};
-
-// Issue the loads of queue entries [head, head + m), m <= 128.
-template <int KW>
-__device__ __forceinline__ void wm_issue(const WmArgs &a, const uint32_t *q,
-                                         uint32_t head, uint32_t m, int lane,
-                                         const uint64_t (&k)[KW], Pending<KW> &p) {
-  p.m = m;
-  p.e0 = q[(head + lane) & (kQueue - 1)];
-  p.e1 = q[(head + 64 + lane) & (kQueue - 1)];
-  owner_key<KW>(p.e0, k, p.kk0);
-  if (m > 64) owner_key<KW>(p.e1, k, p.kk1);  // wave-uniform
-  const uint8_t *tab = a.t.base;
-  const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
-  const uint64_t *keys = reinterpret_cast<const uint64_t *>(tab + a.t.keys_off);
-  p.v0 = p.v1 = 0;
+__device__ __forceinline__ void wm_check(const WmArgs &a, const uint64_t *mlds,
+                                         uint64_t *best, const uint32_t *q,
+                                         uint32_t m, int lane,
+                                         const uint64_t (&k)[KW]) {
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
+  uint32_t e[kPerLane];
+  uint64_t v[kPerLane], sk[kPerLane][KW], kk[kPerLane][KW];
 #pragma unroll
-  for (int j = 0; j < KW; j++) p.sk0[j] = p.sk1[j] = 0;
-  if ((uint32_t)lane < m) {
-    const uint32_t slot = p.e0 & 0xFFFFFu;
-    p.v0 = vals[slot];
+  for (int r = 0; r < kPerLane; r++) {
+    const uint32_t i = (uint32_t)lane + 64u * r;
+    e[r] = 0;
+    v[r] = 0;
 #pragma unroll
-    for (int j = 0; j < KW; j++) p.sk0[j] = keys[(uint64_t)slot * KW + j];
+    for (int j = 0; j < KW; j++) sk[r][j] = kk[r][j] = 0;
+    if (64u * r < m) {  // wave-uniform: the permutes need every lane
+      e[r] = q[i];
+      owner_key<KW>(e[r], k, kk[r]);
+      if (i < m) {
+        const uint32_t slot = e[r] & 0xFFFFFu;
+        v[r] = vals[slot];
+#pragma unroll
+        for (int j = 0; j < KW; j++) sk[r][j] = keys[(uint64_t)slot * KW + j];
+      }
+    }
   }
-  if ((uint32_t)lane + 64 < m) {
-    const uint32_t slot = p.e1 & 0xFFFFFu;
-    p.v1 = vals[slot];
 #pragma unroll
-    for (int j = 0; j < KW; j++) p.sk1[j] = keys[(uint64_t)slot * KW + j];
+  for (int r = 0; r < kPerLane; r++) {
+    const uint32_t i = (uint32_t)lane + 64u * r;
+    if (i < m && wm_hit<KW>(mlds, e[r], v[r], sk[r], kk[r])) wm_fold(best, e[r], v[r]);
   }
 }
 
-// Compare the loaded entries and fold the hits into `best`.
-template <int KW>
-__device__ __forceinline__ void wm_resolve(const uint64_t *mlds, uint64_t *best,
-                                           int lane, const Pending<KW> &p) {
-  if ((uint32_t)lane < p.m && wm_hit<KW>(mlds, p.e0, p.v0, p.sk0, p.kk0))
-    wm_fold(best, p.e0, p.v0);
-  if ((uint32_t)lane + 64 < p.m && wm_hit<KW>(mlds, p.e1, p.v1, p.sk1, p.kk1))
-    wm_fold(best, p.e1, p.v1);
+// Exclusive wave prefix sum of small per-lane counts (< 128): one ballot +
+// mbcnt per bit. *total: the wave's sum.
+__device__ __forceinline__ uint32_t wave_excl_scan7(uint32_t c, uint32_t *total) {
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < 7; b++) {
+    const uint64_t bal = __ballot((c >> b) & 1u);
+    off += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))
+           << b;
+    tot += (uint32_t)__popcll(bal) << b;
+  }
+  *total = tot;
+  return off;
 }
 
 template <int KW, int NCH>
@@ -147,12 +153,9 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + wid * kWaveLds;
-  // two buffers: the tile being hashed (cur) and the one whose key checks
-  // are in flight (cur ^ 1)
-  uint64_t *bests = reinterpret_cast<uint64_t *>(wl);            // [2][64]
-  uint32_t *queues = reinterpret_cast<uint32_t *>(wl + 2 * 64 * 8);  // [2][kQueue]
-  bests[lane] = 0;
-  bests[64 + lane] = 0;
+  uint64_t *best = reinterpret_cast<uint64_t *>(wl);
+  uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
+  best[lane] = 0;
   __syncthreads();
 
   const uint64_t ntiles = (a.n + 63) / 64;
@@ -161,20 +164,6 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   uint32_t wn[NCH * 4 + 2];
   if (t < ntiles && t * 64 + lane < a.n)
     load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
-  Pending<KW> pend;
-  pend.m = 0;
-  int cur = 0;
-  uint64_t prev_idx = 0;
-  bool prev_live = false, have_prev = false;
-  // the previous tile: its checks resolved, its gates out
-  auto finish_prev = [&]() {
-    uint64_t *best = bests + (cur ^ 1) * 64;
-    wm_resolve<KW>(mlds, best, lane, pend);
-    lds_fence();
-    const uint64_t b = best[lane];
-    best[lane] = 0;
-    if (prev_live) a.gates[prev_idx] = b ? (uint16_t)b : (uint16_t)a.default_gate;
-  };
   for (; t < ntiles; t += nw) {
     const uint64_t idx = t * 64 + lane;
     const bool live = idx < a.n;
@@ -194,12 +183,12 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
 #endif
     const kconst_u64 tm = tuple_masks(a);  // laundered per tile: no hoisting
 
-    // A. every tuple's hash and both tag words (16 LDS reads in flight)
-    uint32_t b1[kMaxTuples], b2[kMaxTuples], tw1[kMaxTuples], tw2[kMaxTuples],
-        tb[kMaxTuples];
+    // A. every tuple's hash and both tag words (16 LDS reads in flight);
+    // fingerprint matches as bit 7 of each matching tag byte
+    uint32_t b1[kMaxTuples], b2[kMaxTuples], c1[kMaxTuples], c2[kMaxTuples];
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
-      b1[tu] = b2[tu] = tw1[tu] = tw2[tu] = tb[tu] = 0;
+      b1[tu] = b2[tu] = c1[tu] = c2[tu] = 0;
       if (tu < (int)a.ntuples) {
         uint64_t km[KW];
 #pragma unroll
@@ -208,74 +197,63 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
             hash_join(hash_words_h1(km, KW, tuple_seed(a.t.seed, tu))), 1, a.t.nbp);
         b1[tu] = p.b1;
         b2[tu] = p.b2;
-        tb[tu] = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
-        tw1[tu] = tags[p.b1];
-        tw2[tu] = tags[p.b2];
+        const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
+        c1[tu] = tags[p.b1] ^ tb;  // zero bytes = matches (below)
+        c2[tu] = tags[p.b2] ^ tb;
       }
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      c1[tu] = zero_bytes(c1[tu]);
+      c2[tu] = zero_bytes(c2[tu]);
+      if (!live) c1[tu] = c2[tu] = 0;
+      cnt += __popc(c1[tu]) + __popc(c2[tu]);
     }
 #ifdef BG_AB  // phase timing: + hashes and tag reads
     if (a.ab_phase == 2) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int tu = 0; tu < kMaxTuples; tu++) x ^= tw1[tu] ^ tw2[tu];
-      if (live) a.gates[idx] = (uint16_t)x;
+      if (live) a.gates[idx] = (uint16_t)cnt;
       continue;
     }
 #endif
-    // B. fingerprint matches -> this tile's queue (a full queue checks 64
-    // entries at once)
-    uint64_t *best = bests + cur * 64;
-    const uint32_t *qc = queues + cur * kQueue;
-    uint32_t *q = queues + cur * kQueue;
-    uint32_t head = 0, qlen = 0;  // wave-uniform
+    // B. queue positions: a wave prefix sum of the per-lane match counts
+    uint32_t total;
+    const uint32_t off = wave_excl_scan7(cnt, &total);
+    // C. in rounds of kQueue entries (one round unless the tile has more
+    // than four candidates per packet): each lane writes its entries that
+    // fall into the round, then the round is checked
+    for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
+      uint32_t pos = off;
 #pragma unroll
-    for (int tu = 0; tu < kMaxTuples; tu++) {
-      if (tu < (int)a.ntuples) {
-        // bytes of the tag words equal to the fingerprint: bit 7 of each
-        uint32_t c1 = zero_bytes(tw1[tu] ^ tb[tu]);
-        uint32_t c2 = zero_bytes(tw2[tu] ^ tb[tu]);
-        if (!live) c1 = c2 = 0;
-        for (;;) {
-          const bool has = (c1 | c2) != 0;
-          const uint64_t bal = __ballot(has);
-          if (!bal) break;
-          if (has) {
-            uint32_t slot;
-            if (c1) {
-              slot = b1[tu] * kSlots + (__builtin_ctz(c1) >> 3);
-              c1 &= c1 - 1;
-            } else {
-              slot = b2[tu] * kSlots + (__builtin_ctz(c2) >> 3);
-              c2 &= c2 - 1;
-            }
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-            q[(head + qlen + rank) & (kQueue - 1)] =
-                slot | ((uint32_t)lane << 20) | ((uint32_t)tu << 26);
+      for (int tu = 0; tu < kMaxTuples; tu++) {
+        uint32_t m1 = c1[tu], m2 = c2[tu];
+        while (m1 | m2) {
+          uint32_t slot;
+          if (m1) {
+            slot = b1[tu] * kSlots + (__builtin_ctz(m1) >> 3);
+            m1 &= m1 - 1;
+          } else {
+            slot = b2[tu] * kSlots + (__builtin_ctz(m2) >> 3);
+            m2 &= m2 - 1;
           }
-          qlen += (uint32_t)__popcll(bal);
-          if (qlen > kQueue - 64) {  // room for one more ballot round
-            lds_fence();
-            Pending<KW> now;
-            wm_issue<KW>(a, qc, head, 64, lane, k, now);
-            wm_resolve<KW>(mlds, best, lane, now);
-            head += 64;
-            qlen -= 64;
-          }
+          if (pos - r0 < kQueue)
+            q[pos - r0] = slot | ((uint32_t)lane << 20) | ((uint32_t)tu << 26);
+          pos++;
         }
       }
+      lds_fence();
+#ifdef BG_AB  // phase timing: queue built, no key checks
+      if (a.ab_phase == 3) continue;
+#endif
+      const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
+      wm_check<KW>(a, mlds, best, q, m, lane, k);
+      lds_fence();  // the queue is rewritten by the next round
     }
-    // C. the previous tile's checks (loads issued one tile ago) and gates
-    if (have_prev) finish_prev();
-    // D. this tile's checks go in flight
     lds_fence();
-    wm_issue<KW>(a, qc, head, qlen, lane, k, pend);
-    prev_idx = idx;
-    prev_live = live;
-    have_prev = true;
-    cur ^= 1;
+    const uint64_t bb = best[lane];
+    best[lane] = 0;
+    if (live) a.gates[idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
   }
-  if (have_prev) finish_prev();
 }
 
 template <int KW, int NCH>

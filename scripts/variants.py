@@ -176,7 +176,8 @@ def main():
             t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
         t.sync(0)
         variants = {"full": {}, "read_key": {"BG_WM_PHASE": 1},
-                    "hash_tags": {"BG_WM_PHASE": 2}}
+                    "hash_tags": {"BG_WM_PHASE": 2},
+                    "enqueue": {"BG_WM_PHASE": 3}}
         r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants,
                           reps=20)
         for k in r:
