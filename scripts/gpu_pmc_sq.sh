@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
 P2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum"
 for W in ${WL:-wm}; do
-  if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --no-cpu --steps 3 --warmup 1"; fi
+  if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; elif [ $W = wm ]; then ARGS="--only wm --wm-layout slab --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --no-cpu --steps 3 --warmup 1"; fi
   i=0
   for C in "$P1" "$P2"; do
     i=$((i+1))
