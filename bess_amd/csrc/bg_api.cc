@@ -260,16 +260,17 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
                 const std::vector<uint64_t> &keys,
                 const std::vector<uint8_t> &vals,
                 const std::vector<uint64_t> &hashes, std::vector<uint8_t> *img,
-                TableLayout *out_layout, double max_load, bool vik) {
+                TableLayout *out_layout, double max_load, bool vik,
+                uint32_t probe) {
   const size_t n = hashes.size();
   // count entries per partition to size the layout
   std::vector<std::vector<size_t>> members(nparts);
-  TableLayout L = plan_layout(0, kw, val_bytes, nparts, kDefaultSeed, 0.75, vik);
   for (size_t i = 0; i < n; i++)
-    members[split_hash(hashes[i], nparts, 2).part].push_back(i);
+    members[probe ? 0 : split_hash(hashes[i], nparts, 2).part].push_back(i);
   size_t maxc = 0;
   for (auto &m : members) maxc = std::max(maxc, m.size());
-  L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load, vik);
+  TableLayout L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load, vik);
+  L.probe = probe;
   for (int attempt = 0; attempt < 8; attempt++) {
     img->assign((size_t)L.part_bytes * nparts, 0);
     bool ok = true;
@@ -998,28 +999,41 @@ int bg_wm_iter(const bg_wm *wm, int t, size_t *cursor, uint8_t *key_out,
 
 static bool wm_want_no_tags() { return (path_flags() & kPathWmNoTags) != 0; }
 
+// bit d: the tuple's mask has a nonzero dword d (wm_hash covers it)
+static uint32_t wm_cover(const bg_wm *wm, size_t t) {
+  uint32_t c = 0;
+  for (uint32_t d = 0; d < 2 * wm->kw; d++) {
+    uint32_t m;
+    memcpy(&m, reinterpret_cast<const uint8_t *>(wm->tuples[t].mask.w) + 4 * d, 4);
+    if (m) c |= 1u << d;
+  }
+  return c;
+}
+
 static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   const bool no_tags = wm_want_no_tags();
   if (!wm->dirty && wm->dev.valid && wm->dev.device == device &&
       wm->built_no_tags == no_tags)
     return 0;
-  std::vector<uint64_t> keys, seeds;
+  std::vector<uint64_t> keys, hashes;
   std::vector<uint8_t> vals, img;
   for (size_t t = 0; t < wm->tuples.size(); t++) {
+    const uint32_t cover = wm_cover(wm, t);
+    const uint32_t seed = wm_seed32(tuple_seed(kDefaultSeed, (uint32_t)t));
     for (auto &kv : wm->tuples[t].ht) {
       keys.insert(keys.end(), kv.first.w, kv.first.w + wm->kw);
       uint64_t v = (uint64_t)(uint32_t)kv.second.priority |
                    ((uint64_t)kv.second.gate << 32) | ((uint64_t)t << 48);
       for (int b = 0; b < 8; b++) vals.push_back((uint8_t)(v >> (8 * b)));
-      seeds.push_back(tuple_seed(kDefaultSeed, (uint32_t)t));
+      // the stored key is already masked: wm_hash of its dwords
+      uint32_t kd[2 * kMaxKeyWords];
+      memcpy(kd, kv.first.w, sizeof(kd));
+      hashes.push_back(wm_hash(kd, cover, 2 * (int)wm->kw, seed));
     }
   }
-  const size_t nkeys = seeds.size();
-  std::vector<uint64_t> hashes(nkeys);
-  for (size_t i = 0; i < nkeys; i++)
-    hashes[i] = hash_words(&keys[i * wm->kw], (int)wm->kw, seeds[i]);
+  const size_t nkeys = hashes.size();
   TableLayout L;
-  int r = build_image(wm->kw, 8, 1, keys, vals, hashes, &img, &L);
+  int r = build_image(wm->kw, 8, 1, keys, vals, hashes, &img, &L, 0.75, false, 1);
   if (r) return r;
   // Past the whole-table LDS size, a table whose tag words fit LDS (at a
   // higher load factor if need be: the bucketized 2x4 cuckoo table inserts
@@ -1029,7 +1043,8 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
     for (double load : {0.75, 0.93}) {
       std::vector<uint8_t> img2;
       TableLayout L2;
-      if (build_image(wm->kw, 8, 1, keys, vals, hashes, &img2, &L2, load) == 0 &&
+      if (build_image(wm->kw, 8, 1, keys, vals, hashes, &img2, &L2, load, false,
+                      1) == 0 &&
           (uint64_t)L2.nbp * 4 <= kTagsLdsMax) {
         img.swap(img2);
         L = L2;
@@ -1055,8 +1070,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
     img.resize(foff + (uint64_t)fw * 4, 0);
     uint32_t *f = reinterpret_cast<uint32_t *>(img.data() + foff);
     for (size_t i = 0; i < nkeys; i++) {
-      const FilterProbe q =
-          filter_probe(hash_words(&keys[i * wm->kw], (int)wm->kw, seeds[i]), fw);
+      const FilterProbe q = filter_probe(hashes[i], fw);
       f[q.word] |= q.bits;
     }
   }
@@ -1091,8 +1105,11 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
   a.ntuples = (uint32_t)wm->tuples.size();
   a.fp = make_plan(wm->dfields, false, shift);
   a.t = wm->dev.ref();
-  for (size_t t = 0; t < wm->tuples.size(); t++)
+  for (size_t t = 0; t < wm->tuples.size(); t++) {
     for (uint32_t j = 0; j < wm->kw; j++) a.tmask[t][j] = wm->tuples[t].mask.w[j];
+    a.tcover[t] = wm_cover(wm, t);
+    a.tseed[t] = wm_seed32(tuple_seed(a.t.seed, (uint32_t)t));
+  }
   a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
   HIP_TRY(launch_wm(a, num_cus(wm->dev.device), s));
   return 0;

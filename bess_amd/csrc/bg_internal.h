@@ -54,7 +54,7 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
                 const std::vector<uint8_t> &vals,
                 const std::vector<uint64_t> &hashes, std::vector<uint8_t> *img,
                 TableLayout *out_layout, double max_load = 0.75,
-                bool vik = false);
+                bool vik = false, uint32_t probe = 0);
 
 struct DevTable {
   int device = -1;

@@ -106,6 +106,8 @@ struct WmArgs {
   FieldPlan fp;
   TableRef t;
   uint64_t tmask[kMaxTuples][kMaxKeyWords];
+  uint32_t tcover[kMaxTuples];  // per tuple: the dwords wm_hash covers
+  uint32_t tseed[kMaxTuples];   // per tuple: wm_seed32(tuple_seed(seed, tu))
   uint32_t ab_phase, pad2;  // A/B build only: stop after a phase (timing)
 };
 

@@ -549,6 +549,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
                                                   const uint64_t (&k)[KW],
                                                   const uint32_t *filt) {
   const kconst_u64 tm = tuple_masks(a);
+  const uint32_t lg = 31 - __builtin_clz(a.t.nbp);
   uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples];
   uint32_t w1[kMaxTuples], w2[kMaxTuples];
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
@@ -558,17 +559,14 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
     tg[tu] = 1;  // fingerprints are never 0, so empty (0) tag words never match
     w1[tu] = w2[tu] = 0;
     if (tu < (int)a.ntuples) {
-      uint64_t km[KW];
-#pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
-      const uint32_t h1 = hash_words_h1(km, KW, tuple_seed(a.t.seed, tu));
+      const uint32_t h = wm_tuple_hash<KW>(k, tm, tu, a.tcover[tu], a.tseed[tu]);
       bool pass = true;
       if (FILT) {
-        const FilterProbe q = filter_probe(h1, a.t.filt_words);
+        const FilterProbe q = filter_probe(h, a.t.filt_words);
         pass = (filt[q.word] & q.bits) == q.bits;
       }
-      if (pass) {  // the second hash only for tuples the filter lets through
-        const Probe p = split_hash(hash_join(h1), 1, a.t.nbp);
+      if (pass) {
+        const Probe p = wm_probe(h, lg);
         b1[tu] = p.b1;
         b2[tu] = p.b2;
         tg[tu] = p.tag;
@@ -611,123 +609,12 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
   return gate;
 }
 
-#ifdef BG_AB
-// Batched-rounds lookup (A/B variant V = 2; measured slower than the
-// sequential resolve, which the product uses)
-template <int KW, bool FILT, int G>
-__device__ __forceinline__ uint32_t wm_lookup(const uint8_t *tab,
-                                              const WmArgs &a,
-                                              const uint64_t (&k)[KW],
-                                              const uint32_t *filt) {
-  const kconst_u64 tm = tuple_masks(a);
-  // Three batched rounds, each issuing every tuple's reads before any is
-  // consumed (the WildcardMatch table has a single partition):
-  //   A. hash per tuple, LDS key filter, both tag words (<= 16 loads);
-  //   B. for each tuple's first fingerprint match, its key and value;
-  //   C. resolve in tuple order (LookupEntry order, '>=' tie-break);
-  //      further fingerprint matches of a tuple (rare) are probed there.
-  uint32_t w1[kMaxTuples], w2[kMaxTuples];
-  const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
-  const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
-  const uint8_t *keys = tab + a.t.keys_off;
-#pragma unroll
-  for (int tu = 0; tu < kMaxTuples; tu++) {
-    w1[tu] = w2[tu] = 0;  // 0: four empty slots
-    if (tu < (int)a.ntuples) {
-      uint64_t km[KW];
-#pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
-      const uint64_t h = hash_words(km, KW, tuple_seed(a.t.seed, tu));
-      bool pass = true;
-      if (FILT) {  // key filter in LDS: skip tuples that cannot match
-        const FilterProbe q = filter_probe(h, a.t.filt_words);
-        pass = (filt[q.word] & q.bits) == q.bits;
-      }
-      if (pass) {
-        const Probe p = split_hash(h, 1, a.t.nbp);
-        w1[tu] = tags[p.b1];
-        w2[tu] = tags[p.b2];
-      }
-    }
-  }
-  int32_t best = INT_MIN;
-  uint32_t gate = a.default_gate;
-  // rounds B and C run over groups of G tuples (register budget)
-#pragma unroll
-  for (int g0 = 0; g0 < kMaxTuples; g0 += G) {
-  // cand: bit 8 = the tuple had a fingerprint match, bits 0-7 = the
-  // matches not yet probed (bits 0-3 bucket b1's slots, 4-7 bucket b2's)
-  uint32_t cand[G];
-  uint64_t v1[G], sk1[G][KW];
-#pragma unroll
-  for (int gi = 0; gi < G; gi++) {
-    const int tu = g0 + gi;
-    cand[gi] = 0;
-    v1[gi] = 0;
-#pragma unroll
-    for (int j = 0; j < KW; j++) sk1[gi][j] = 0;
-    if (tu < (int)a.ntuples && (w1[tu] | w2[tu])) {
-      uint64_t km[KW];
-#pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
-      const Probe p =
-          split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)), 1, a.t.nbp);
-      uint32_t c = tag_match(w1[tu], p.tag) | (tag_match(w2[tu], p.tag) << 4);
-      if (c) {
-        const int sl = __builtin_ctz(c);
-        const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
-        v1[gi] = vals[slot];
-        load_key<KW>(keys + (uint64_t)slot * KW * 8, sk1[gi]);
-        cand[gi] = 0x100u | (c & (c - 1));
-      }
-    }
-  }
-#pragma unroll
-  for (int gi = 0; gi < G; gi++) {
-    const int tu = g0 + gi;
-    if (tu < (int)a.ntuples && (cand[gi] & 0x100u)) {
-      uint64_t km[KW];
-#pragma unroll
-      for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
-      bool hit = wm_slot_hit<KW>(v1[gi], sk1[gi], km, tu);
-      uint64_t v = v1[gi];
-      uint32_t c = cand[gi] & 0xFFu;
-      if (!hit && c) {  // another fingerprint match in this tuple (rare)
-        const Probe p = split_hash(hash_words(km, KW, tuple_seed(a.t.seed, tu)),
-                                   1, a.t.nbp);
-        while (c && !hit) {
-          const int sl = __builtin_ctz(c);
-          c &= c - 1;
-          const uint32_t slot = (sl < 4 ? p.b1 : p.b2) * kSlots + (sl & 3);
-          uint64_t sk[KW];
-          v = vals[slot];
-          load_key<KW>(keys + (uint64_t)slot * KW * 8, sk);
-          hit = wm_slot_hit<KW>(v, sk, km, tu);
-        }
-      }
-      if (hit) {
-        const int32_t prio = (int32_t)(uint32_t)v;
-        if (prio >= best) {  // '>=': the later tuple wins a tie (P5)
-          best = prio;
-          gate = (uint32_t)(v >> 32) & 0xFFFFu;
-        }
-      }
-    }
-  }
-  }
-  return gate;
-}
-#endif  // BG_AB
-
 // lookup variant: V 1 = wm_lookup_seq, 2 = batched rounds over groups of G
 template <int KW, bool FILT, int V, int G>
 __device__ __forceinline__ uint32_t wm_lookup_v(const uint8_t *tab,
                                                 const WmArgs &a,
                                                 const uint64_t (&k)[KW],
                                                 const uint32_t *filt) {
-#ifdef BG_AB
-  if constexpr (V == 2) return wm_lookup<KW, FILT, G>(tab, a, k, filt);
-#endif
   return wm_lookup_seq<KW, FILT>(tab, a, k, filt);
 }
 
@@ -1598,16 +1485,13 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
       return launch_classify(wm_classify_k1024_kernel<2>, a, num_cus, s, 2, 1024);
     return launch_classify(wm_classify_k1024_kernel<1>, a, num_cus, s, 1, 1024);
   }
-  const int v = knob("BG_WM_V", 0), g = knob("BG_WM_G", 4);
-  if (v && a.t.kw == 2 && fits_nch2(a.fp)) {
+  if (knob("BG_WM_V", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {
     const int ppl = knob("BG_PPL", 2);
     const bool pf = knob("BG_WM_PF", 0) != 0;
-#define BG_WMX(P, V, G, PF)                                                \
-  if (ppl == P && v == V && (V == 1 || g == G) && pf == PF)                \
-    return launch_classify(wm_classify_exp_kernel<P, V, G, PF>, a, num_cus, s, P);
-    BG_WMX(1, 1, 8, false) BG_WMX(2, 1, 8, false) BG_WMX(1, 2, 8, false)
-    BG_WMX(1, 2, 4, false) BG_WMX(2, 2, 4, false) BG_WMX(1, 1, 8, true)
-    BG_WMX(1, 2, 4, true) BG_WMX(1, 2, 8, true)
+#define BG_WMX(P, PF) \
+  if (ppl == P && pf == PF) \
+    return launch_classify(wm_classify_exp_kernel<P, 1, 8, PF>, a, num_cus, s, P);
+    BG_WMX(1, false) BG_WMX(2, false) BG_WMX(1, true)
 #undef BG_WMX
     return hipErrorInvalidValue;
   }

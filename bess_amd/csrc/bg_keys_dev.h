@@ -49,6 +49,29 @@ __device__ __forceinline__ kconst_u64 tuple_masks(const WmArgs &) {
   return p;
 }
 
+// The tuple's hash of packet key k (bg_table.h wm_hash over k & mask):
+// uniform branches skip the dwords the tuple's mask clears.
+template <int KW>
+__device__ __forceinline__ uint32_t wm_tuple_hash(const uint64_t (&k)[KW],
+                                                  kconst_u64 tm, int tu,
+                                                  uint32_t cover, uint32_t seed) {
+  uint32_t h = seed;
+#pragma unroll
+  for (int d = 0; d < 2 * KW; d++) {
+    if ((cover >> d) & 1u) {
+      const uint64_t mw = tm[tu * kMaxKeyWords + d / 2];
+      const uint32_t x = (uint32_t)(k[d / 2] >> (32 * (d & 1))) &
+                         (uint32_t)(mw >> (32 * (d & 1)));
+      h = (h ^ x) * 0x9E3779B1u;
+      h ^= h >> 15;
+    }
+  }
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  return h;
+}
+
 __device__ __forceinline__ void lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }

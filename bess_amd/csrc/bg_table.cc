@@ -16,6 +16,7 @@ TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
                         double max_load, bool vik) {
   TableLayout L;
   L.vik = vik && val_bytes == 2 ? 1u : 0u;
+  L.probe = 0;
   L.kw = kw;
   L.val_bytes = val_bytes;
   L.nparts = nparts;
@@ -49,8 +50,10 @@ bool build_partition(const TableLayout &L, uint32_t part, size_t n,
   if (n > nslots) return false;
   std::vector<int32_t> occ(nslots, -1);
   std::vector<Probe> pr(n);
+  const uint32_t lg = log2_pow2(L.nbp);
   for (size_t i = 0; i < n; i++) {
-    pr[i] = split_hash(hashes[i], L.nparts, L.nbp);
+    pr[i] = L.probe ? wm_probe((uint32_t)hashes[i], lg)
+                    : split_hash(hashes[i], L.nparts, L.nbp);
     if (pr[i].part != part) return false;  // caller filtered wrongly
   }
   Xorshift rng{(L.seed ^ (0x9E3779B97F4A7C15ULL * (part + 1))) | 1};

@@ -48,6 +48,9 @@ struct TableLayout {
   // key has >= 2 bytes past its raw size, which are 0 in every packet key,
   // P4), so one key read also yields the value; no value array
   uint32_t vik;
+  // 0: split_hash of a 64-bit hash_words value (ExactMatch, NAT);
+  // 1: wm_probe of a 32-bit wm_hash value (WildcardMatch, one partition)
+  uint32_t probe;
 };
 
 BG_HD uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
@@ -98,6 +101,49 @@ BG_HD uint64_t tuple_seed(uint64_t seed, uint32_t tuple) {
 struct Probe {
   uint32_t part, b1, b2, tag;
 };
+
+// WildcardMatch tuple hash: one multiply-xorshift step per key dword the
+// tuple's mask covers (`cover` bit d: mask dword d is not zero -- a masked
+// key is 0 everywhere else, so those dwords carry nothing), then a
+// one-multiply finalizer. A packet is probed in all (<= 8) tuples, so the
+// multiplies (quarter-rate on gfx950) are what bounds the kernel: this
+// spends 1 per covered dword + 1, where hash_words + hash_join spend 1 per
+// dword + 4.
+BG_HD uint32_t wm_seed32(uint64_t tuple_seed) {
+  return (uint32_t)tuple_seed ^ (uint32_t)(tuple_seed >> 32);
+}
+BG_HD uint32_t wm_hash(const uint32_t *kd, uint32_t cover, int ndw, uint32_t seed) {
+  uint32_t h = seed;
+  for (int d = 0; d < ndw; d++) {
+    if (!((cover >> d) & 1u)) continue;
+    h = (h ^ kd[d]) * 0x9E3779B1u;
+    h ^= h >> 15;
+  }
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  return h;
+}
+
+// first bucket from the low bits, fingerprint from the top byte, second
+// bucket from the top bits of one more product (nbp = 2^lg, lg >= 1)
+BG_HD Probe wm_probe(uint32_t h, uint32_t lg) {
+  Probe p;
+  const uint32_t m = (1u << lg) - 1;
+  p.part = 0;
+  p.b1 = h & m;
+  p.b2 = (h * 0xC2B2AE35u) >> (32 - lg);
+  if (p.b2 == p.b1) p.b2 = (p.b1 ^ 1u) & m;
+  const uint32_t t = h >> 24;
+  p.tag = t ? t : 1u;
+  return p;
+}
+
+BG_HD uint32_t log2_pow2(uint32_t x) {
+  uint32_t l = 0;
+  while ((1u << l) < x) l++;
+  return l;
+}
 
 // h1: first bucket (low bits) and fingerprint (top byte); h2: second
 // bucket (low bits) and partition (top 3 bits). Buckets per partition are

@@ -158,6 +158,7 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   best[lane] = 0;
   __syncthreads();
 
+  const uint32_t lg = 31 - __builtin_clz(a.t.nbp);
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
@@ -190,11 +191,8 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
     for (int tu = 0; tu < kMaxTuples; tu++) {
       b1[tu] = b2[tu] = c1[tu] = c2[tu] = 0;
       if (tu < (int)a.ntuples) {
-        uint64_t km[KW];
-#pragma unroll
-        for (int j = 0; j < KW; j++) km[j] = k[j] & tm[tu * kMaxKeyWords + j];
-        const Probe p = split_hash(
-            hash_join(hash_words_h1(km, KW, tuple_seed(a.t.seed, tu))), 1, a.t.nbp);
+        const Probe p = wm_probe(
+            wm_tuple_hash<KW>(k, tm, tu, a.tcover[tu], a.tseed[tu]), lg);
         b1[tu] = p.b1;
         b2[tu] = p.b2;
         const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte

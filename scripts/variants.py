@@ -30,7 +30,7 @@ from bess_amd import packets as P  # noqa: E402
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_WM_PHASE",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
-         "BG_CK_TILED", "BG_WM_V", "BG_WM_G", "BG_WM_PF", "BG_EM_PF",
+         "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2"]
 
 
@@ -202,9 +202,6 @@ def main():
         variants = {"default": (64, {}),
                     "seq_pf": (64, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "seq_p2": (64, {"BG_WM_V": 1, "BG_PPL": 2}),
-                    "g4_pf": (64, {"BG_WM_V": 2, "BG_WM_G": 4, "BG_WM_PF": 1, "BG_PPL": 1}),
-                    "g8_pf": (64, {"BG_WM_V": 2, "BG_WM_G": 8, "BG_WM_PF": 1, "BG_PPL": 1}),
-                    "g4_p1": (64, {"BG_WM_V": 2, "BG_WM_G": 4, "BG_PPL": 1}),
                     "seq_pf_f128": (128, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "nofilter_seq_pf": (0, {"BG_WM_V": 1, "BG_WM_PF": 1, "BG_PPL": 1}),
                     "k1024": (64, {"BG_WM_BLOCK": 1024}),
