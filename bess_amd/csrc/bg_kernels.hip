@@ -559,7 +559,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
     tg[tu] = 1;  // fingerprints are never 0, so empty (0) tag words never match
     w1[tu] = w2[tu] = 0;
     if (tu < (int)a.ntuples) {
-      const uint32_t h = wm_tuple_hash<KW>(k, tm, tu, a.tcover[tu], a.tseed[tu]);
+      const uint32_t h = wm_tuple_hash<KW>(k, tm, tu, a);
       bool pass = true;
       if (FILT) {
         const FilterProbe q = filter_probe(h, a.t.filt_words);

@@ -49,13 +49,26 @@ __device__ __forceinline__ kconst_u64 tuple_masks(const WmArgs &) {
   return p;
 }
 
+typedef const uint32_t __attribute__((address_space(4))) *kconst_u32;
+// tcover / tseed / ntuples the same way (read per tile: hoisted, the
+// per-dword branch conditions would become lane masks spilled to VGPR lanes)
+__device__ __forceinline__ kconst_u32 tuple_words(const WmArgs &, size_t off) {
+  const __attribute__((address_space(4))) uint8_t *ka =
+      (const __attribute__((address_space(4))) uint8_t *)
+          __builtin_amdgcn_kernarg_segment_ptr();
+  kconst_u32 p = (kconst_u32)(ka + off);
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // The tuple's hash of packet key k (bg_table.h wm_hash over k & mask):
 // uniform branches skip the dwords the tuple's mask clears.
 template <int KW>
 __device__ __forceinline__ uint32_t wm_tuple_hash(const uint64_t (&k)[KW],
                                                   kconst_u64 tm, int tu,
-                                                  uint32_t cover, uint32_t seed) {
-  uint32_t h = seed;
+                                                  const WmArgs &a) {
+  const uint32_t cover = tuple_words(a, offsetof(WmArgs, tcover))[tu];
+  uint32_t h = tuple_words(a, offsetof(WmArgs, tseed))[tu];
 #pragma unroll
   for (int d = 0; d < 2 * KW; d++) {
     if ((cover >> d) & 1u) {

@@ -47,12 +47,17 @@ __device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 
+// Queue entry: bucket (bits 0-14; tags <= 128 KB, so < 2^15 buckets) |
+// lane << 15 | tuple << 21 | fingerprint << 24.
+__device__ __forceinline__ uint32_t entry_lane(uint32_t e) { return (e >> 15) & 63u; }
+__device__ __forceinline__ uint32_t entry_tuple(uint32_t e) { return (e >> 21) & 7u; }
+
 // The owning lane's key for queue entry e (every lane takes part in the
 // permutes)
 template <int KW>
 __device__ __forceinline__ void owner_key(uint32_t e, const uint64_t (&k)[KW],
                                           uint64_t (&kk)[KW]) {
-  const int pl = (int)((e >> 20) & 63u);
+  const int pl = (int)entry_lane(e);
 #pragma unroll
   for (int j = 0; j < KW; j++) {
     const uint32_t lo = shfl32((uint32_t)k[j], pl);
@@ -63,11 +68,11 @@ __device__ __forceinline__ void owner_key(uint32_t e, const uint64_t (&k)[KW],
 
 // fold a hit of entry e (slot value v) into its packet's best
 __device__ __forceinline__ void wm_fold(uint64_t *best, uint32_t e, uint64_t v) {
-  const uint32_t pl = (e >> 20) & 63u, tu = e >> 26;
   // (priority as unsigned order, valid bit, tuple, gate)
   const uint64_t comb = ((uint64_t)((uint32_t)v ^ 0x80000000u) << 32) |
-                        (1u << 19) | (tu << 16) | ((uint32_t)(v >> 32) & 0xFFFFu);
-  atomicMax(reinterpret_cast<unsigned long long *>(best + pl),
+                        (1u << 19) | (entry_tuple(e) << 16) |
+                        ((uint32_t)(v >> 32) & 0xFFFFu);
+  atomicMax(reinterpret_cast<unsigned long long *>(best + entry_lane(e)),
             (unsigned long long)comb);
 }
 
@@ -75,29 +80,41 @@ template <int KW>
 __device__ __forceinline__ bool wm_hit(const uint64_t *mlds, uint32_t e,
                                        uint64_t v, const uint64_t (&sk)[KW],
                                        const uint64_t (&kk)[KW]) {
-  const uint32_t tu = e >> 26;
+  const uint32_t tu = entry_tuple(e);
   bool hit = (uint32_t)(v >> 48) == tu;
 #pragma unroll
   for (int j = 0; j < KW; j++) hit &= sk[j] == (kk[j] & mlds[tu * KW + j]);
   return hit;
 }
 
+// fingerprint matches of entry e's tag in its bucket: bit 7 of each byte
+__device__ __forceinline__ uint32_t entry_matches(const uint32_t *tags, uint32_t e) {
+  return zero_bytes(tags[e & 0x7FFFu] ^ __builtin_amdgcn_perm(0u, e >> 24, 0u));
+}
+
+__device__ __forceinline__ uint32_t match_slot(uint32_t e, uint32_t z) {
+  return (e & 0x7FFFu) * kSlots + (__builtin_ctz(z) >> 3);
+}
+
 // Check queue entries [0, m), m <= kQueue: lane l takes entries l, l + 64,
-// ... (an entry is slot | lane << 20 | tuple << 26); every entry's key and
-// value loads are issued before any is compared (one L2 round trip).
+// ... Each entry is a (packet, tuple, bucket) whose tag word holds the
+// packet's fingerprint: the lane re-reads the tag word, and the first
+// matching slot's key and value loads of every entry are issued before any
+// is compared (one L2 round trip). An entry whose first match is not the
+// key (a fingerprint collision) tries its further matches (rare).
 template <int KW>
-__device__ __forceinline__ void wm_check(const WmArgs &a, const uint64_t *mlds,
-                                         uint64_t *best, const uint32_t *q,
-                                         uint32_t m, int lane,
+__device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
+                                         const uint64_t *mlds, uint64_t *best,
+                                         const uint32_t *q, uint32_t m, int lane,
                                          const uint64_t (&k)[KW]) {
   const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
-  uint32_t e[kPerLane];
+  uint32_t e[kPerLane], z[kPerLane];
   uint64_t v[kPerLane], sk[kPerLane][KW], kk[kPerLane][KW];
 #pragma unroll
   for (int r = 0; r < kPerLane; r++) {
     const uint32_t i = (uint32_t)lane + 64u * r;
-    e[r] = 0;
+    e[r] = z[r] = 0;
     v[r] = 0;
 #pragma unroll
     for (int j = 0; j < KW; j++) sk[r][j] = kk[r][j] = 0;
@@ -105,34 +122,55 @@ __device__ __forceinline__ void wm_check(const WmArgs &a, const uint64_t *mlds,
       e[r] = q[i];
       owner_key<KW>(e[r], k, kk[r]);
       if (i < m) {
-        const uint32_t slot = e[r] & 0xFFFFFu;
+        z[r] = entry_matches(tags, e[r]);
+        const uint32_t slot = match_slot(e[r], z[r]);
+#ifdef BG_AB  // phase timing: checks without their L2 loads
+        if (a.ab_phase == 3) continue;
+#endif
         v[r] = vals[slot];
 #pragma unroll
         for (int j = 0; j < KW; j++) sk[r][j] = keys[(uint64_t)slot * KW + j];
       }
     }
   }
+  bool more = false;
 #pragma unroll
   for (int r = 0; r < kPerLane; r++) {
     const uint32_t i = (uint32_t)lane + 64u * r;
-    if (i < m && wm_hit<KW>(mlds, e[r], v[r], sk[r], kk[r])) wm_fold(best, e[r], v[r]);
+    if (i < m) {
+      if (wm_hit<KW>(mlds, e[r], v[r], sk[r], kk[r])) {
+        wm_fold(best, e[r], v[r]);
+        z[r] = 0;
+      } else {
+        z[r] &= z[r] - 1;  // the matches not tried yet
+      }
+    } else {
+      z[r] = 0;
+    }
+    more |= z[r] != 0;
+  }
+  if (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform, rare
+#pragma unroll
+    for (int r = 0; r < kPerLane; r++) {
+      while (z[r]) {
+        const uint32_t slot = match_slot(e[r], z[r]);
+        z[r] &= z[r] - 1;
+        const uint64_t vv = vals[slot];
+        uint64_t s2[KW];
+#pragma unroll
+        for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * KW + j];
+        if (wm_hit<KW>(mlds, e[r], vv, s2, kk[r])) {
+          wm_fold(best, e[r], vv);
+          z[r] = 0;
+        }
+      }
+    }
   }
 }
 
-// Exclusive wave prefix sum of small per-lane counts (< 128): one ballot +
-// mbcnt per bit. *total: the wave's sum.
-__device__ __forceinline__ uint32_t wave_excl_scan7(uint32_t c, uint32_t *total) {
-  uint32_t off = 0, tot = 0;
-#pragma unroll
-  for (int b = 0; b < 7; b++) {
-    const uint64_t bal = __ballot((c >> b) & 1u);
-    off += __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))
-           << b;
-    tot += (uint32_t)__popcll(bal) << b;
-  }
-  *total = tot;
-  return off;
+// any byte of x zero (the SWAR test of zero_bytes, as a predicate)
+__device__ __forceinline__ bool has_zero_byte(uint32_t x) {
+  return ((x - 0x01010101u) & ~x & 0x80808080u) != 0;
 }
 
 template <int KW, int NCH>
@@ -183,69 +221,55 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
     }
 #endif
     const kconst_u64 tm = tuple_masks(a);  // laundered per tile: no hoisting
+    const int ntu = (int)tuple_words(a, offsetof(WmArgs, ntuples))[0];
 
-    // A. every tuple's hash and both tag words (16 LDS reads in flight);
-    // fingerprint matches as bit 7 of each matching tag byte
-    uint32_t b1[kMaxTuples], b2[kMaxTuples], c1[kMaxTuples], c2[kMaxTuples];
+    // A. every tuple's hash and both tag words (16 LDS reads in flight)
+    uint32_t b[2 * kMaxTuples], c[2 * kMaxTuples], et[kMaxTuples];
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
-      b1[tu] = b2[tu] = c1[tu] = c2[tu] = 0;
-      if (tu < (int)a.ntuples) {
-        const Probe p = wm_probe(
-            wm_tuple_hash<KW>(k, tm, tu, a.tcover[tu], a.tseed[tu]), lg);
-        b1[tu] = p.b1;
-        b2[tu] = p.b2;
+      b[2 * tu] = b[2 * tu + 1] = 0;
+      c[2 * tu] = c[2 * tu + 1] = 0xFFFFFFFFu;  // no zero byte: no match
+      et[tu] = 0;
+      if (tu < ntu) {
+        const Probe p = wm_probe(wm_tuple_hash<KW>(k, tm, tu, a), lg);
+        b[2 * tu] = p.b1;
+        b[2 * tu + 1] = p.b2;
         const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
-        c1[tu] = tags[p.b1] ^ tb;  // zero bytes = matches (below)
-        c2[tu] = tags[p.b2] ^ tb;
+        c[2 * tu] = tags[p.b1] ^ tb;  // zero bytes = fingerprint matches
+        c[2 * tu + 1] = tags[p.b2] ^ tb;
+        et[tu] = ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24);
       }
     }
-    uint32_t cnt = 0;
+    // B/C. queue entries, one per (packet, tuple, bucket) with a
+    // fingerprint match, bucket-major: for each bucket word the wave's
+    // mask of matching lanes gives each lane its position (a scalar base +
+    // mbcnt) and the base advances by the mask's popcount. The entries
+    // that fall into [r0, r0 + kQueue) are written, then checked; the
+    // first round's base ends as the tile's total (more rounds are rare:
+    // over four candidate buckets per packet).
+    const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
+    uint32_t total = 0;
+    for (uint32_t r0 = 0;; r0 += kQueue) {
+      uint32_t base = 0;
 #pragma unroll
-    for (int tu = 0; tu < kMaxTuples; tu++) {
-      c1[tu] = zero_bytes(c1[tu]);
-      c2[tu] = zero_bytes(c2[tu]);
-      if (!live) c1[tu] = c2[tu] = 0;
-      cnt += __popc(c1[tu]) + __popc(c2[tu]);
-    }
-#ifdef BG_AB  // phase timing: + hashes and tag reads
-    if (a.ab_phase == 2) {
-      if (live) a.gates[idx] = (uint16_t)cnt;
-      continue;
-    }
+      for (int x = 0; x < 2 * kMaxTuples; x++) {
+        const bool hz = live && has_zero_byte(c[x]);
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(hz) & livemask;
+        const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, base));
+        if (hz && pos - r0 < kQueue) q[pos - r0] = b[x] | et[x / 2];
+        base += (uint32_t)__popcll(mk);
+      }
+      total = base;
+#ifdef BG_AB  // phase timing: + hashes, tag reads and the queue writes
+      if (a.ab_phase == 2) break;
 #endif
-    // B. queue positions: a wave prefix sum of the per-lane match counts
-    uint32_t total;
-    const uint32_t off = wave_excl_scan7(cnt, &total);
-    // C. in rounds of kQueue entries (one round unless the tile has more
-    // than four candidates per packet): each lane writes its entries that
-    // fall into the round, then the round is checked
-    for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
-      uint32_t pos = off;
-#pragma unroll
-      for (int tu = 0; tu < kMaxTuples; tu++) {
-        uint32_t m1 = c1[tu], m2 = c2[tu];
-        while (m1 | m2) {
-          uint32_t slot;
-          if (m1) {
-            slot = b1[tu] * kSlots + (__builtin_ctz(m1) >> 3);
-            m1 &= m1 - 1;
-          } else {
-            slot = b2[tu] * kSlots + (__builtin_ctz(m2) >> 3);
-            m2 &= m2 - 1;
-          }
-          if (pos - r0 < kQueue)
-            q[pos - r0] = slot | ((uint32_t)lane << 20) | ((uint32_t)tu << 26);
-          pos++;
-        }
-      }
+      if (total <= r0) break;
       lds_fence();
-#ifdef BG_AB  // phase timing: queue built, no key checks
-      if (a.ab_phase == 3) continue;
-#endif
       const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
-      wm_check<KW>(a, mlds, best, q, m, lane, k);
+      wm_check<KW>(a, tags, mlds, best, q, m, lane, k);
       lds_fence();  // the queue is rewritten by the next round
+      if (total <= r0 + kQueue) break;
     }
     lds_fence();
     const uint64_t bb = best[lane];
@@ -271,7 +295,7 @@ hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
 
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   const bool n2 = fits_nch2(a.fp);
-  if (a.fp.direct || a.fp.nch > 4) return hipErrorInvalidValue;
+  if (a.fp.direct || a.fp.nch > 4 || a.t.nbp > (1u << 15)) return hipErrorInvalidValue;
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
     return n2 ? launch_tags<KW, 2>(a, num_cus, s) : launch_tags<KW, 4>(a, num_cus, s);

@@ -33,8 +33,13 @@ if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
   i=0
   for C in ${PMC_SETS:-"FETCH_SIZE" "WRITE_SIZE"}; do
     i=$((i+1))
-    for W in ${PMC_WL:-em cksum wm c5 hashlb acl iplookup ttl nat dnat}; do
-      if [ $W = em ]; then ARGS="--no-extra --no-cpu --steps 3 --warmup 1"; else ARGS="--only $W --no-cpu --steps 3 --warmup 1"; fi
+    for W in ${PMC_WL:-em cksum wm wm2k c5 hashlb acl iplookup ttl nat dnat}; do
+      case $W in
+        em) ARGS="--no-extra --no-cpu --steps 3 --warmup 1" ;;
+        wm) ARGS="--only wm --wm-layout slab --no-cpu --steps 3 --warmup 1" ;;
+        wm2k) ARGS="--only wm --wm-layout 2k --no-cpu --steps 3 --warmup 1" ;;
+        *) ARGS="--only $W --no-cpu --steps 3 --warmup 1" ;;
+      esac
       step pmc_${W}_$i 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
     done
   done

@@ -165,7 +165,8 @@ def main():
     if "wmphase" in which:
         # C4 on the dense header slab, timed up to each phase of
         # wm_tags_kernel (BG_WM_PHASE: 1 header read + key, 2 + the 8
-        # tuple hashes and tag reads, 0 everything)
+        # tuple hashes, tag reads and queue writes, 3 everything but the
+        # checks' L2 loads, 0 everything)
         n = 1 << 23
         rk, rm, prio, gates, frames, _ = P.wm_workload(100000, 1 << 20, stride=64,
                                                       sizes=((60, 1),))
@@ -176,8 +177,8 @@ def main():
             t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
         t.sync(0)
         variants = {"full": {}, "read_key": {"BG_WM_PHASE": 1},
-                    "hash_tags": {"BG_WM_PHASE": 2},
-                    "enqueue": {"BG_WM_PHASE": 3}}
+                    "enqueue": {"BG_WM_PHASE": 2},
+                    "checks_no_l2": {"BG_WM_PHASE": 3}}
         r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants,
                           reps=20)
         for k in r:
