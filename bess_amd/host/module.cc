@@ -250,6 +250,11 @@ int bg_module_set_igate(bg_module *h, uint16_t igate) {
   return 0;
 }
 
+int bg_module_set_now(bg_module *h, uint64_t now_ns) {
+  h->m->set_now(now_ns);
+  return 0;
+}
+
 int bg_module_bind_meta(bg_module *h, int meta_off, const char *const *names,
                         const int32_t *offsets, int n) {
   if (n < 0 || (n > 0 && (!names || !offsets))) return fail(EINVAL, "bad arguments");

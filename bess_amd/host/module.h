@@ -203,6 +203,12 @@ class Module {
   // ctx->current_igate of the calls that follow (core/module.h:59-75)
   void set_igate(gate_idx_t g) { igate_ = g; }
   gate_idx_t igate() const { return igate_; }
+  // ctx->current_ns of the calls that follow (NAT's mapping clock); until
+  // set, modules that need it read CLOCK_MONOTONIC per call
+  void set_now(uint64_t ns) {
+    now_ = ns;
+    now_set_ = true;
+  }
 
   // Module::AddMetadataAttr (core/module.cc:248-285): per-module metadata
   // attributes; returns the attribute id or -errno.
@@ -265,6 +271,8 @@ class Module {
  protected:
   int device_ = 0;
   gate_idx_t igate_ = 0;
+  uint64_t now_ = 0;
+  bool now_set_ = false;
   std::vector<Attribute> attrs_;
   std::vector<bool> ogates_;
   bool explicit_ogates_ = false;

@@ -444,5 +444,35 @@ void StaticNATArg::Write(Writer &w) const {
   for (auto &x : pairs_) write_msg(w, 1, x);
 }
 
+bool NATArg_PortRange::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_u32(r, wt, &begin_);
+  if (field == 2) return read_u32(r, wt, &end_);
+  if (field == 3) return read_bool(r, wt, &suspended_);
+  return r.skip(wt);
+}
+void NATArg_PortRange::Write(Writer &w) const {
+  if (begin_) w.varint_field(1, begin_);
+  if (end_) w.varint_field(2, end_);
+  if (suspended_) w.varint_field(3, 1);
+}
+
+bool NATArg_ExternalAddress::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_str(r, wt, &ext_addr_);
+  if (field == 2) return read_msg(r, wt, ranges_.Add());
+  return r.skip(wt);
+}
+void NATArg_ExternalAddress::Write(Writer &w) const {
+  write_str(w, 1, ext_addr_);
+  for (auto &x : ranges_) write_msg(w, 2, x);
+}
+
+bool NATArg::MergeField(Reader &r, uint32_t field, uint32_t wt) {
+  if (field == 1) return read_msg(r, wt, addrs_.Add());
+  return r.skip(wt);
+}
+void NATArg::Write(Writer &w) const {
+  for (auto &x : addrs_) write_msg(w, 1, x);
+}
+
 }  // namespace pb
 }  // namespace bess

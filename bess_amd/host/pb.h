@@ -483,6 +483,48 @@ class StaticNATArg : public Message {
   Repeated<StaticNATArg_AddressRangePair> pairs_;
 };
 
+// module_msg.proto:697-708
+class NATArg_PortRange : public Message {
+ public:
+  uint32_t begin() const { return begin_; }
+  uint32_t end() const { return end_; }
+  bool suspended() const { return suspended_; }
+  void set_begin(uint32_t v) { begin_ = v; }
+  void set_end(uint32_t v) { end_ = v; }
+  void set_suspended(bool v) { suspended_ = v; }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  uint32_t begin_ = 0, end_ = 0;
+  bool suspended_ = false;
+};
+
+class NATArg_ExternalAddress : public Message {
+ public:
+  const std::string &ext_addr() const { return ext_addr_; }
+  void set_ext_addr(const std::string &v) { ext_addr_ = v; }
+  const Repeated<NATArg_PortRange> &port_ranges() const { return ranges_; }
+  NATArg_PortRange *add_port_ranges() { return ranges_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  std::string ext_addr_;
+  Repeated<NATArg_PortRange> ranges_;
+};
+
+class NATArg : public Message {
+ public:
+  const Repeated<NATArg_ExternalAddress> &ext_addrs() const { return addrs_; }
+  NATArg_ExternalAddress *add_ext_addrs() { return addrs_.Add(); }
+  bool MergeField(Reader &r, uint32_t field, uint32_t wt) override;
+  void Write(Writer &w) const override;
+
+ private:
+  Repeated<NATArg_ExternalAddress> addrs_;
+};
+
 }  // namespace pb
 }  // namespace bess
 

@@ -99,6 +99,17 @@ _MESSAGES = [
         ("ext_range", 2, _F.TYPE_MESSAGE, 1, ".bess.pb.StaticNATArg_AddressRange", None)]),
     ("StaticNATArg", [("pairs", 1, _F.TYPE_MESSAGE, 3,
                        ".bess.pb.StaticNATArg_AddressRangePair", None)]),
+    # module_msg.proto:697-708 (nested messages as top-level ones)
+    ("NATArg_PortRange", [("begin", 1, _F.TYPE_UINT32, 1, None, None),
+                          ("end", 2, _F.TYPE_UINT32, 1, None, None),
+                          ("suspended", 3, _F.TYPE_BOOL, 1, None, None)]),
+    ("NATArg_ExternalAddress", [
+        ("ext_addr", 1, _F.TYPE_STRING, 1, None, None),
+        ("port_ranges", 2, _F.TYPE_MESSAGE, 3, ".bess.pb.NATArg_PortRange", None)]),
+    ("NATArg", [("ext_addrs", 1, _F.TYPE_MESSAGE, 3, ".bess.pb.NATArg_ExternalAddress",
+                 None)]),
+    # module_msg.proto:603-604
+    ("IPEncapArg", []),
 ]
 
 

@@ -332,10 +332,18 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
 int bg_ip_encap(int device, void *d_slots, size_t stride, size_t n,
                 int meta_off, const int32_t *attr_offsets, uint16_t *d_head,
                 uint32_t *d_len, uint16_t *d_out, bg_stream_t stream);
+/* Host packets: slots[i] = packet i's buffer (metadata area at meta_off,
+ * data at slots[i] + head[i], len[i] bytes; all within slot_bytes), staged
+ * through the calling thread's pinned buffers and written back with the
+ * updated head / len. Synchronous; stream as the other host paths. */
+int bg_ip_encap_host(int device, uint8_t *const *slots, size_t slot_bytes, size_t n,
+                     int meta_off, const int32_t *attr_offsets, uint16_t *head,
+                     uint32_t *len, uint16_t *out, bg_stream_t stream);
 
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
-/* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum".
+/* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum",
+ * "HashLB", "ACL", "IPLookup", "UpdateTTL", "StaticNAT", "NAT".
  * arg: serialized bess.pb.<mclass>Arg. On failure returns -errno and the
  * reference's message via bg_last_error(). */
 int bg_module_create(const char *mclass, const void *arg, size_t arg_len,
@@ -380,6 +388,9 @@ int bg_module_set_device(bg_module *m, int device);
 /* the input gate the next process calls arrive on (ctx->current_igate:
  * ACL emits on it, StaticNAT picks its direction by it); default 0 */
 int bg_module_set_igate(bg_module *m, uint16_t igate);
+/* ctx->current_ns of the process calls that follow (NAT's mapping clock,
+ * nat.cc:321-363); until set, CLOCK_MONOTONIC at each call */
+int bg_module_set_now(bg_module *m, uint64_t now_ns);
 /* Metadata layout for attr_name fields (ExactMatch, WildcardMatch): the
  * slot offset of each packet's metadata area and, by attribute name, the
  * offsets the pipeline assigned (Module::attr_offset, core/module.h). */

@@ -1,0 +1,242 @@
+// A minimal stand-in for bessd's core headers, exposing exactly the names
+// the integration/bessd/*_gpu.cc plugin wrappers use, so that the wrappers
+// compile and register here as they would inside bessd (tests only):
+//
+//   Module, Context, bess::Packet / PacketBatch       core/module.h, packet.h
+//   Command / Commands, THREAD_SAFE / THREAD_UNSAFE   core/commands.h:54-72
+//   MODULE_CMD_FUNC / MODULE_INIT_FUNC                core/module.h:82-102
+//   CommandResponse, CommandSuccess / CommandFailure  core/message.h:44-53
+//   EmitPacket / DropPacket                           core/module.h:534-594
+//   ADD_MODULE -> ModuleBuilder::RegisterModuleClass  core/module.h:719-733
+//   gate_idx_t, MAX_GATES, DROP_GATE, SNBUF_*         core/gate.h, snbuf_layout.h
+//
+// EmitPacket keeps bessd's rule (module.h:546-549): an out-of-range or
+// unconnected output gate drops the packet.
+#ifndef BESSD_SHELL_MODULE_H_
+#define BESSD_SHELL_MODULE_H_
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "pb/module_msg.pb.h"
+
+typedef uint16_t gate_idx_t;
+#define MAX_GATES 8192
+#define DROP_GATE MAX_GATES
+
+#define SNBUF_MBUF 128
+#define SNBUF_IMMUTABLE 64
+#define SNBUF_METADATA 128
+#define SNBUF_SCRATCHPAD 64
+#define SNBUF_HEADROOM 128
+#define SNBUF_DATA 2048
+#define SNBUF_METADATA_OFF (SNBUF_MBUF + SNBUF_IMMUTABLE)
+#define SNBUF_HEADROOM_OFF (SNBUF_METADATA_OFF + SNBUF_METADATA + SNBUF_SCRATCHPAD)
+#define SNBUF_SIZE (SNBUF_HEADROOM_OFF + SNBUF_HEADROOM + SNBUF_DATA)
+
+namespace bess {
+
+// an snbuf: the packet object at the start of its slot, its data at
+// SNBUF_HEADROOM_OFF + data_off
+class Packet {
+ public:
+  template <typename T = void *>
+  T head_data() {
+    return reinterpret_cast<T>(reinterpret_cast<uint8_t *>(this) + SNBUF_HEADROOM_OFF +
+                               data_off_);
+  }
+  uint16_t data_off() const { return data_off_; }
+  void set_data_off(uint16_t v) { data_off_ = v; }
+  uint32_t total_len() const { return total_len_; }
+  void set_total_len(uint32_t v) { total_len_ = v; }
+  uint16_t data_len() const { return data_len_; }
+  void set_data_len(uint16_t v) { data_len_ = v; }
+
+ private:
+  uint16_t data_off_ = SNBUF_HEADROOM;
+  uint16_t data_len_ = 0;
+  uint32_t total_len_ = 0;
+};
+
+class PacketBatch {
+ public:
+  static const size_t kMaxBurst = 32;
+  int cnt() const { return cnt_; }
+  Packet **pkts() { return pkts_; }
+  void clear() { cnt_ = 0; }
+  void add(Packet *p) { pkts_[cnt_++] = p; }
+
+ private:
+  int cnt_ = 0;
+  Packet *pkts_[kMaxBurst];
+};
+
+}  // namespace bess
+
+struct Context {
+  uint64_t current_tsc = 0;
+  uint64_t current_ns = 0;
+  int wid = 0;
+  gate_idx_t current_igate = 0;
+  // where each packet went (the shell's stand-in for the task's batches)
+  std::vector<std::pair<bess::Packet *, gate_idx_t>> emitted;
+  std::vector<bess::Packet *> dropped;
+};
+
+class CommandResponse {
+ public:
+  bool has_error() const { return code_ != 0; }
+  int code() const { return code_; }
+  const std::string &errmsg() const { return msg_; }
+  const std::string &data() const { return data_; }
+  void set_error(int c, const std::string &m) {
+    code_ = c;
+    msg_ = m;
+  }
+  void set_data(const std::string &d) { data_ = d; }
+
+ private:
+  int code_ = 0;
+  std::string msg_, data_;
+};
+
+inline CommandResponse CommandSuccess() { return CommandResponse(); }
+inline CommandResponse CommandSuccess(const google::protobuf::Message &m) {
+  CommandResponse r;
+  r.set_data(m.SerializeAsString());
+  return r;
+}
+inline CommandResponse CommandFailure(int code, const char *fmt = nullptr, ...) {
+  CommandResponse r;
+  char b[512] = "";
+  if (fmt) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof(b), fmt, ap);
+    va_end(ap);
+  }
+  r.set_error(code, b);
+  return r;
+}
+
+class Module;
+using module_cmd_func_t =
+    std::function<CommandResponse(Module *, const google::protobuf::Any &)>;
+
+struct Command {
+  enum ThreadSafety { THREAD_UNSAFE = 0, THREAD_SAFE = 1 };
+  std::string cmd;
+  std::string arg_type;
+  module_cmd_func_t func;
+  ThreadSafety mt_safe;
+};
+using Commands = std::vector<Command>;
+
+template <typename T, typename M>
+static inline module_cmd_func_t MODULE_CMD_FUNC(CommandResponse (M::*fn)(const T &)) {
+  return [fn](Module *m, const google::protobuf::Any &arg) {
+    T a;
+    arg.UnpackTo(&a);
+    return (static_cast<M *>(m)->*fn)(a);
+  };
+}
+#define MODULE_INIT_FUNC MODULE_CMD_FUNC
+
+class Module {
+ public:
+  static const gate_idx_t kNumIGates = 1;
+  static const gate_idx_t kNumOGates = 1;
+  static const Commands cmds;
+
+  virtual ~Module() = default;
+  // modules without an Init of their own (e.g. UpdateTTL) take EmptyArg
+  CommandResponse Init(const bess::pb::EmptyArg &) { return CommandSuccess(); }
+  virtual void DeInit() {}
+  virtual void ProcessBatch(Context *, bess::PacketBatch *) {}
+  virtual std::string GetDesc() const { return ""; }
+
+  // ConnectModules: the output gates with a next module
+  void ConnectOGate(gate_idx_t g) {
+    if (g >= ogates_.size()) ogates_.resize((size_t)g + 1, false);
+    ogates_[g] = true;
+  }
+  void EmitPacket(Context *ctx, bess::Packet *pkt, gate_idx_t ogate = 0) {
+    if (ogates_.size() <= ogate || !ogates_[ogate]) {  // module.h:546-549
+      DropPacket(ctx, pkt);
+      return;
+    }
+    ctx->emitted.push_back({pkt, ogate});
+  }
+  void DropPacket(Context *ctx, bess::Packet *pkt) { ctx->dropped.push_back(pkt); }
+  // core/module.h:530-532: the whole batch to output gate 0
+  void RunNextModule(Context *ctx, bess::PacketBatch *batch) {
+    for (int i = 0; i < batch->cnt(); i++) EmitPacket(ctx, batch->pkts()[i], 0);
+  }
+
+  // Module::AddMetadataAttr / attr_offset (core/module.h:640-700); the
+  // shell's pipeline places attribute i at metadata offset 4 * i
+  enum class AccessMode { kRead = 0, kWrite, kUpdate };
+  int AddMetadataAttr(const std::string &name, size_t size, AccessMode) {
+    attrs_.push_back(name);
+    (void)size;
+    return (int)attrs_.size() - 1;
+  }
+  int32_t attr_offset(int attr_id) const { return 4 * attr_id; }
+  size_t num_attrs() const { return attrs_.size(); }
+
+ private:
+  std::vector<bool> ogates_;
+  std::vector<std::string> attrs_;
+};
+inline const Commands Module::cmds = {};
+
+// ModuleBuilder::RegisterModuleClass (core/module.h:108-172): what bessd
+// records per class, kept for inspection
+struct ModuleClass {
+  std::function<Module *()> make;
+  std::string name_template, help;
+  gate_idx_t igates, ogates;
+  Commands cmds;
+  module_cmd_func_t init;
+};
+inline std::map<std::string, ModuleClass> &module_classes() {
+  static std::map<std::string, ModuleClass> m;
+  return m;
+}
+struct ModuleBuilder {
+  static bool RegisterModuleClass(std::function<Module *()> make, const std::string &cls,
+                                  const std::string &tmpl, const std::string &help,
+                                  gate_idx_t ig, gate_idx_t og, const Commands &cmds,
+                                  module_cmd_func_t init) {
+    return module_classes()
+        .emplace(cls, ModuleClass{make, tmpl, help, ig, og, cmds, init})
+        .second;
+  }
+  static bool DeregisterModuleClass(const std::string &cls) {
+    return module_classes().erase(cls) > 0;
+  }
+};
+
+#define DEF_MODULE(_MOD, _NAME_TEMPLATE, _HELP)                                        \
+  class _MOD##_class {                                                                 \
+   public:                                                                             \
+    _MOD##_class() {                                                                   \
+      ModuleBuilder::RegisterModuleClass([]() -> Module * { return new _MOD(); }, #_MOD, \
+                                         _NAME_TEMPLATE, _HELP, _MOD::kNumIGates,      \
+                                         _MOD::kNumOGates, _MOD::cmds,                 \
+                                         MODULE_INIT_FUNC(&_MOD::Init));               \
+    }                                                                                  \
+    ~_MOD##_class() { ModuleBuilder::DeregisterModuleClass(#_MOD); }                   \
+  };
+
+#define ADD_MODULE(_MOD, _NAME_TEMPLATE, _HELP) \
+  DEF_MODULE(_MOD, _NAME_TEMPLATE, _HELP);      \
+  static _MOD##_class _MOD##_singleton;
+
+#endif  // BESSD_SHELL_MODULE_H_
