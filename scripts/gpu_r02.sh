@@ -30,7 +30,11 @@ fi
 if [[ "$MODE" == *prof* ]]; then
   step prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-e2e
 fi
-if [[ "$MODE" == *pipetrace* ]]; then
+if [[ "$MODE" == *pipetrace1* ]]; then
+  # one launching thread: the traced pipe path (the multi-threaded legs
+  # crash the tracer, profiles/README.md)
+  step prof_pipe1 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_pipe1" -o pipe -- python3 "$GRAFT_REPO_ROOT/bench.py" --only pipe --pipe-threads 1
+elif [[ "$MODE" == *pipetrace* ]]; then
   step prof_pipe 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_pipe" -o pipe -- python3 "$GRAFT_REPO_ROOT/bench.py" --only pipe
 fi
 echo done >> "$OUT/steps.log"
