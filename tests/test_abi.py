@@ -18,6 +18,20 @@ def test_library_exports_every_declared_symbol():
     assert missing == []
 
 
+def test_library_exports_only_the_c_abi():
+    """nothing but bg_* leaves the library (exports.map): its C++ module
+    classes carry the reference's names and must not interpose on bessd's"""
+    import os
+    import subprocess
+    so = os.path.join(_lib.HERE, "libbessgpu.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True,
+                         text=True, check=True).stdout
+    names = [ln.split()[-1] for ln in out.splitlines() if ln.strip()]
+    assert names and all(n.startswith("bg_") for n in names), \
+        [n for n in names if not n.startswith("bg_")][:5]
+    assert set(_lib.declared_symbols()) <= set(names)
+
+
 def test_header_is_plain_c():
     import os
     hdr = open(os.path.join(os.path.dirname(_lib.HERE), "include",
