@@ -18,6 +18,8 @@ BG_PATH_FORCE_LDS = 1
 BG_PATH_NO_LDS = 2
 BG_PATH_NO_SLAB = 4
 BG_PATH_WM_NO_TAGS = 8
+BG_PATH_ACL_SCAN = 16
+BG_PATH_ACL_BV = 32
 KEY_BYTES = 64
 
 

@@ -3,7 +3,7 @@
 // whose src/dst prefixes and non-zero ports match decides -- emit on the
 // input gate unless the rule drops; no match drops.
 //
-// The rule list is the same for every packet, so rules are read with
+// Two forms. The rule scan: the rule list is the same for every packet, so rules are read with
 // wave-uniform (scalar) loads and each rule costs a handful of VALU ops per
 // 64 packets; a wave stops scanning once all its lanes have matched. The
 // packet side comes from the header line (IHL at byte 14, addresses at
@@ -59,9 +59,144 @@ struct AclOp {
   static constexpr uint32_t kDropGateDev = 8192;  // DROP_GATE
 };
 
+// (v ^ a) & m in one instruction (v_bitop3_b32, truth table 0x48 over
+// (a, m, v)); the compiler otherwise spends an xor and an and
+__device__ __forceinline__ uint32_t masked_ne(uint32_t v, uint32_t a, uint32_t m) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x48" : "=v"(r) : "v"(a), "v"(m), "v"(v));
+  return r;
+}
+
+// The rule scan with the rule list in LDS: each rule reaches the lanes as
+// two broadcast ds_read_b128 (no bank conflicts), so its three masked
+// compares are single v_bitop3 instructions on VGPRs -- from scalar
+// registers each needed a v_mov first (one scalar operand per VOP3). The
+// first match is kept as a minimum over keys (rule index, plus bit 31 when
+// the rule misses): no lane-mask bookkeeping per rule, whose scalar
+// instructions share one scalar unit per CU. Per rule: 3 bitop3, or3, min,
+// lshl_or, min; a wave leaves the scan once every lane has matched.
+struct AclLdsOp {
+  using Args = AclArgs;
+  static constexpr bool kWrites = false;
+  static constexpr int c0 = 0, c1 = 4;
+  static size_t lds_bytes(const AclArgs &a) { return (size_t)a.nrules * 32; }
+  __device__ static void stage(uint32_t *lds, const AclArgs &a) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.rules);
+    uint4 *dst = reinterpret_cast<uint4 *>(lds);
+    for (uint32_t i = threadIdx.x; i < a.nrules * 2; i += blockDim.x) dst[i] = src[i];
+  }
+  __device__ static uint32_t decide(const AclArgs &x, const uint32_t *lds,
+                                    uint32_t (&d)[16], uint8_t *f) {
+    const uint32_t sip = ip_src_le(d), dip = ip_dst_le(d);
+    const uint32_t ports = l4_ports(d, f, x.stride);
+    const uint4 *R = reinterpret_cast<const uint4 *>(lds);
+    uint32_t best = 0xFFFFFFFFu;
+    // nrules is a multiple of 4; the padding repeats the last rule, which
+    // can never be a first match the rule before it was not
+    for (uint32_t r = 0; r < x.nrules; r += 4) {
+      uint4 A[4], B[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        A[j] = R[2 * (r + j)];
+        B[j] = R[2 * (r + j) + 1];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t miss = masked_ne(sip, A[j].x, A[j].y) | masked_ne(dip, A[j].z, A[j].w) |
+                              masked_ne(ports, B[j].x, B[j].y);
+        best = min(best, (min(miss, 1u) << 31) | (r + (uint32_t)j));
+      }
+      if ((r & 12) == 12 && __all(best < 0x80000000u)) break;  // every 16 rules
+    }
+    if (best >= 0x80000000u) return kDropGateDev;
+    return R[2 * best + 1].z ? kDropGateDev : x.igate;
+  }
+  static constexpr uint32_t kDropGateDev = 8192;  // DROP_GATE
+};
+
+// LDS the scan may take for its rule list (32 B per rule)
+constexpr size_t kAclLdsRules = 48 << 10;
+
+// The same decision from per-dimension bit vectors (Lakshman-Stiliadis
+// style, with a summary word per interval): a packet finds its interval in
+// each of the four dimensions -- two binary searches over the address
+// interval starts in LDS, two 64 K-entry port tables -- ANDs the four
+// summary words, and for each set summary bit (lowest first) ANDs the
+// four rule words of that group: the lowest set bit is the first rule, in
+// list order, that matches in all four dimensions, which is the rule the
+// ordered scan stops at. A summary bit that no single rule backs only
+// costs one more group (rare). The work per packet no longer grows with
+// the rule count, beyond the searches' log2 steps.
+struct AclBvOp {
+  using Args = AclArgs;
+  static constexpr bool kWrites = false;
+  static constexpr int c0 = 0, c1 = 4;
+  static size_t lds_bytes(const AclArgs &a) { return (size_t)(a.k0 + a.k1) * 4; }
+  __device__ static void stage(uint32_t *lds, const AclArgs &a) {
+    const uint32_t nb = a.k0 + a.k1;  // B_0 then B_1, adjacent in bv
+    const uint32_t *src = a.bv + a.b_off[0];
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) lds[i] = src[i];
+  }
+  // the last interval start <= v (B[0] == 0)
+  __device__ static uint32_t search(const uint32_t *B, uint32_t k, uint32_t lg,
+                                    uint32_t v) {
+    uint32_t lo = 0;
+    for (uint32_t step = lg ? 1u << (lg - 1) : 0u; step; step >>= 1) {
+      const uint32_t j = lo + step;
+      lo = (j < k && B[j] <= v) ? j : lo;
+    }
+    return lo;
+  }
+  __device__ static uint32_t decide(const AclArgs &x, const uint32_t *lds,
+                                    uint32_t (&d)[16], uint8_t *f) {
+    const uint32_t sip = __builtin_bswap32(ip_src_le(d));
+    const uint32_t dip = __builtin_bswap32(ip_dst_le(d));
+    const uint32_t ports = l4_ports(d, f, x.stride);  // raw frame bytes
+    const uint32_t i0 = search(lds, x.k0, x.lg0, sip);
+    const uint32_t i1 = search(lds + x.k0, x.k1, x.lg1, dip);
+    const uint16_t *P2 = reinterpret_cast<const uint16_t *>(x.bv + x.p_off[0]);
+    const uint16_t *P3 = reinterpret_cast<const uint16_t *>(x.bv + x.p_off[1]);
+    const uint32_t i2 = P2[ports & 0xFFFFu], i3 = P3[ports >> 16];
+    const uint32_t *bv = x.bv;
+    uint32_t s = bv[x.s_off[0] + i0] & bv[x.s_off[1] + i1] & bv[x.s_off[2] + i2] &
+                 bv[x.s_off[3] + i3];
+    const uint32_t *V0 = bv + x.v_off[0] + (size_t)i0 * x.nw;
+    const uint32_t *V1 = bv + x.v_off[1] + (size_t)i1 * x.nw;
+    const uint32_t *V2 = bv + x.v_off[2] + (size_t)i2 * x.nw;
+    const uint32_t *V3 = bv + x.v_off[3] + (size_t)i3 * x.nw;
+    uint32_t res = kDropGateDev;
+    while (s) {
+      const uint32_t g = __builtin_ctz(s);
+      s &= s - 1;
+      const uint32_t w1 = min((g + 1) * x.grp, x.nw);
+      for (uint32_t w = g * x.grp; w < w1; w++) {
+        const uint32_t m = V0[w] & V1[w] & V2[w] & V3[w];
+        if (m) {
+          const uint32_t b = __builtin_ctz(m);
+          res = ((bv[x.d_off + w] >> b) & 1u) ? kDropGateDev : x.igate;
+          s = 0;
+          break;
+        }
+      }
+    }
+    return res;
+  }
+  static constexpr uint32_t kDropGateDev = 8192;  // DROP_GATE
+};
+
 }  // namespace
 
 hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s) {
+  const uint32_t pf = path_flags();
+  // measured (scripts/acl_paths.py, 16 M packets): bit vectors 0.41 ms at
+  // 100 rules (4 words per vector) against 0.50 for the LDS scan; at 1000
+  // rules (32 words) 0.77 against 0.49 -- wildcards fill the summaries, so
+  // a packet that matches late or not at all ANDs every word
+  const bool bv = a.bv && (a.nw <= 4 || (pf & kPathAclBv)) &&
+                  !(pf & (kPathAclScan | kPathNoLds));
+  if (bv) return launch_line<AclBvOp>(a, num_cus, s);
+  if (!(pf & (kPathAclScan | kPathNoLds)) && (size_t)a.nrules * 32 <= kAclLdsRules)
+    return launch_line<AclLdsOp>(a, num_cus, s);
   return launch_line<AclOp>(a, num_cus, s);
 }
 

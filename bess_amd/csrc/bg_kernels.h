@@ -145,6 +145,18 @@ struct AclArgs {
   uint16_t *out;
   const uint32_t *rules;
   uint32_t nrules, igate;
+  // Bit-vector form (bg_acl.hip AclBvOp; bv == nullptr: the rule scan).
+  // Per dimension d (0 src addr, 1 dst addr, 2 src port, 3 dst port) the
+  // values fall into elementary intervals; interval i of dimension d has a
+  // bit vector V_d[i] of the rules that match there (nw words, bit r = rule
+  // r) and a summary word S_d[i] (bit g: some rule of words [gG, gG + G)).
+  // Addresses: the interval is found by binary search over the sorted
+  // interval starts B_0 / B_1 (staged in LDS, k0 / k1 entries, host byte
+  // order); ports: a 64 K-entry u16 table indexed by the port's raw frame
+  // bytes. Word offsets into bv:
+  const uint32_t *bv;
+  uint32_t k0, k1, lg0, lg1, nw, grp;
+  uint32_t b_off[2], s_off[4], v_off[4], p_off[2], d_off;
 };
 
 // IPLookup (core/modules/ip_lookup.cc): DIR-24-8 longest-prefix match on

@@ -28,7 +28,9 @@ constexpr uint32_t kPathForceLds = 1;   // stage tables in LDS even for small la
 constexpr uint32_t kPathNoLds = 2;      // probe tables in L2 (never LDS)
 constexpr uint32_t kPathNoSlab = 4;     // lane-per-packet kernels, never the slab shape
 constexpr uint32_t kPathWmNoTags = 8;   // WildcardMatch: key filter, not tag words
-constexpr uint32_t kPathAll = 15;
+constexpr uint32_t kPathAclScan = 16;   // ACL: the rule scan with scalar rule loads
+constexpr uint32_t kPathAclBv = 32;     // ACL: per-dimension bit vectors
+constexpr uint32_t kPathAll = 63;
 
 uint32_t path_flags();
 

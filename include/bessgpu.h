@@ -202,6 +202,8 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_NO_LDS 2
 #define BG_PATH_NO_SLAB 4
 #define BG_PATH_WM_NO_TAGS 8
+#define BG_PATH_ACL_SCAN 16 /* ACL: rule scan with scalar loads (not LDS) */
+#define BG_PATH_ACL_BV 32   /* ACL: per-dimension bit vectors */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */

@@ -9,6 +9,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from bess_amd import _lib as LB  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 from bess_amd.modules import ACL, Pipe  # noqa: E402
 from oracle import oracle_more as OM  # noqa: E402
@@ -66,24 +67,76 @@ def workload(nrules, npkts, seed, stride=64):
     return rules, P.build_frames(pk, 60, stride)
 
 
-@pytest.mark.parametrize("nrules", [0, 1, 10, 300, 3000])
-def test_random_rules_vs_oracle(nrules):
+# the default choice (bit vectors up to 128 rules, else the rule scan from
+# LDS), the scan with scalar rule loads, bit vectors forced, and the LDS
+# forbidden (the scan with scalar loads)
+PATHS = [0, LB.BG_PATH_ACL_SCAN, LB.BG_PATH_ACL_BV, LB.BG_PATH_NO_LDS]
+
+
+@pytest.mark.parametrize("flags", PATHS)
+@pytest.mark.parametrize("nrules", [0, 1, 10, 31, 32, 33, 300, 3000])
+def test_random_rules_vs_oracle(nrules, flags):
     rules, f = workload(nrules, 50000, seed=nrules)
     m = ACL(rules=rules)
     o = OM.OracleACL(rules=rules)
     want = o.process(f, 64, len(f))
-    assert (device_gates(m, f, 64) == want).all()
+    with LB.kernel_paths(flags):
+        assert (device_gates(m, f, 64) == want).all()
     if nrules >= 10:
         assert (want == 0).any() and (want == 8192).any()
 
 
-def test_ihl_and_stride():
+def test_rule_lists_past_the_lds_bit_vector_limit():
+    """40 K rules: neither the rule list nor the address interval starts
+    fit the LDS; the scan with scalar rule loads serves them -- same gates"""
+    rules, f = workload(40000, 20000, seed=41)
+    m = ACL(rules=rules)
+    o = OM.OracleACL(rules=rules)
+    want = o.process(f, 64, len(f))
+    for flags in PATHS:
+        with LB.kernel_paths(flags):
+            assert (device_gates(m, f, 64) == want).all()
+
+
+def test_wide_rules_and_many_groups():
+    """2500 rules (79 rule words, summary groups of 3 words) where most
+    packets match several rules and the first match lies deep in the list:
+    summary bits without a single backing rule, later groups"""
+    rng = np.random.default_rng(17)
+    rules = []
+    for i in range(2500):
+        r = {"drop": bool(i % 3 == 0)}
+        if i < 2400:  # narrow decoys: each dimension matches, not together
+            r["src_ip"] = "10.%d.0.0/16" % (i % 50)
+            r["dst_ip"] = "20.%d.0.0/16" % ((i + 7) % 50)
+            r["dst_port"] = 80 + (i % 5)
+        else:
+            r["src_ip"] = "10.0.0.0/8"
+            r["dst_port"] = 80 + (i % 7)
+        rules.append(r)
+    t = P.random_tuples(30000, rng)
+    t["sip"][:] = (10 << 24) | rng.integers(0, 1 << 24, 30000)
+    t["dip"][:] = (20 << 24) | rng.integers(0, 1 << 24, 30000)
+    t["dport"][:] = 80 + rng.integers(0, 8, 30000)
+    f = P.build_frames(t, 60, 64)
+    m = ACL(rules=rules)
+    o = OM.OracleACL(rules=rules)
+    want = o.process(f, 64, len(f))
+    assert (want == 0).any() and (want == 8192).any()
+    for flags in PATHS:
+        with LB.kernel_paths(flags):
+            assert (device_gates(m, f, 64) == want).all()
+
+
+@pytest.mark.parametrize("flags", PATHS)
+def test_ihl_and_stride(flags):
     rules, f = workload(200, 20000, seed=7, stride=128)
     rng = np.random.default_rng(8)
     f[:, 14] = 0x40 | rng.integers(0, 16, len(f), dtype=np.uint8)
     m = ACL(rules=rules)
     o = OM.OracleACL(rules=rules)
-    assert (device_gates(m, f, 128) == o.process(f, 128, len(f))).all()
+    with LB.kernel_paths(flags):
+        assert (device_gates(m, f, 128) == o.process(f, 128, len(f))).all()
 
 
 def test_reference_module_tests(golden):
