@@ -20,6 +20,7 @@ BG_PATH_NO_SLAB = 4
 BG_PATH_WM_NO_TAGS = 8
 BG_PATH_ACL_SCAN = 16
 BG_PATH_ACL_BV = 32
+BG_PATH_ACL_LDS = 64
 KEY_BYTES = 64
 
 
@@ -135,6 +136,7 @@ _SIGS = {
     "bg_acl_clear": (None, [_vp]),
     "bg_acl_count": (_sz, [_vp]),
     "bg_acl_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
+    "bg_acl_tree": (_int, [_vp, _vp, _sz, C.POINTER(_sz), _vp, C.POINTER(C.c_int)]),
     "bg_lpm_create": (_int, [C.c_uint32, C.c_uint32, C.POINTER(_vp)]),
     "bg_lpm_destroy": (None, [_vp]),
     "bg_lpm_add": (_int, [_vp, C.c_uint32, _int, C.c_uint32]),

@@ -184,19 +184,79 @@ struct AclBvOp {
   static constexpr uint32_t kDropGateDev = 8192;  // DROP_GATE
 };
 
+// The same decision from a decision tree in LDS (bit cuts, HiCuts-style;
+// built by bg_acl_api.cc build_tree, layout in AclArgs): a lane walks from
+// the root, each internal node taking a bit field of one dimension of its
+// packet as the index into the node's child array (one LDS read per level),
+// to a leaf of a few rule records that it checks in order. A leaf holds, in
+// list order, only the rules that intersect its box, cut after the first
+// one that covers the whole box, so the first of them to match is the
+// reference's first match (acl.cc:80-88) for every packet in the box.
+struct AclTreeOp {
+  using Args = AclArgs;
+  static constexpr bool kWrites = false;
+  static constexpr int c0 = 0, c1 = 4;
+  static size_t lds_bytes(const AclArgs &a) { return (size_t)a.tree_words * 4; }
+  __device__ static void stage(uint32_t *lds, const AclArgs &a) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.tree);
+    uint4 *dst = reinterpret_cast<uint4 *>(lds);
+    for (uint32_t i = threadIdx.x; i < a.tree_words / 4; i += blockDim.x) dst[i] = src[i];
+  }
+  __device__ static uint32_t decide(const AclArgs &x, const uint32_t *lds,
+                                    uint32_t (&d)[16], uint8_t *f) {
+    const uint32_t sip = __builtin_bswap32(ip_src_le(d));
+    const uint32_t dip = __builtin_bswap32(ip_dst_le(d));
+    const uint32_t raw = l4_ports(d, f, x.stride);
+    // host-order src port in the low half, dst port in the high half
+    const uint32_t ports = ((raw & 0x00FF00FFu) << 8) | ((raw >> 8) & 0x00FF00FFu);
+    // best: the matched record's last word (rule index in the top bits)
+    uint32_t best = 0xFFFFFFFFu;
+    for (uint32_t t = 0; t < x.ntrees; t++) {
+      uint32_t ref = x.roots[t];
+      while (!(ref >> 31)) {
+        const uint32_t dim = ref >> 25;
+        const uint32_t v = dim == 0 ? sip : (dim == 1 ? dip : ports);
+        ref = lds[(ref & 0xFFFFu) +
+                  __builtin_amdgcn_ubfe(v, (ref >> 16) & 31u, (ref >> 21) & 15u)];
+      }
+      const uint4 *rec = reinterpret_cast<const uint4 *>(lds) + (ref & 0xFFFFu);
+      const uint32_t cnt = (ref >> 16) & 0xFFu;
+      for (uint32_t i = 0; i < cnt; i++) {
+        const uint4 r = rec[i];
+        if (r.w >= best) break;  // records ascend by rule index
+        const uint32_t pmask = ((0u - ((r.w >> 12) & 1u)) & 0xFFFFu) |
+                               ((0u - ((r.w >> 13) & 1u)) << 16);
+        // the top len bits of (value ^ rule): zero iff the prefix matches
+        // (len 0 shifts every bit out)
+        const uint32_t miss =
+            (uint32_t)(((uint64_t)(sip ^ r.x) << (r.w & 63u)) >> 32) |
+            (uint32_t)(((uint64_t)(dip ^ r.y) << ((r.w >> 6) & 63u)) >> 32) |
+            ((ports ^ r.z) & pmask);
+        if (miss == 0) {
+          best = r.w;
+          break;
+        }
+      }
+    }
+    if (best == 0xFFFFFFFFu || ((best >> 14) & 1u)) return kDropGateDev;
+    return x.igate;
+  }
+  static constexpr uint32_t kDropGateDev = 8192;  // DROP_GATE
+};
+
 }  // namespace
 
 hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s) {
   const uint32_t pf = path_flags();
+  if (pf & (kPathAclScan | kPathNoLds)) return launch_line<AclOp>(a, num_cus, s);
+  if (a.bv && (pf & kPathAclBv)) return launch_line<AclBvOp>(a, num_cus, s);
+  if (a.tree && !(pf & kPathAclLds)) return launch_line<AclTreeOp>(a, num_cus, s);
   // measured (scripts/acl_paths.py, 16 M packets): bit vectors 0.41 ms at
   // 100 rules (4 words per vector) against 0.50 for the LDS scan; at 1000
   // rules (32 words) 0.77 against 0.49 -- wildcards fill the summaries, so
   // a packet that matches late or not at all ANDs every word
-  const bool bv = a.bv && (a.nw <= 4 || (pf & kPathAclBv)) &&
-                  !(pf & (kPathAclScan | kPathNoLds));
-  if (bv) return launch_line<AclBvOp>(a, num_cus, s);
-  if (!(pf & (kPathAclScan | kPathNoLds)) && (size_t)a.nrules * 32 <= kAclLdsRules)
-    return launch_line<AclLdsOp>(a, num_cus, s);
+  if (a.bv && a.nw <= 4 && !(pf & kPathAclLds)) return launch_line<AclBvOp>(a, num_cus, s);
+  if ((size_t)a.nrules * 32 <= kAclLdsRules) return launch_line<AclLdsOp>(a, num_cus, s);
   return launch_line<AclOp>(a, num_cus, s);
 }
 

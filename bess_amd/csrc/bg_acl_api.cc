@@ -1,12 +1,17 @@
 // bg_acl_api.cc -- C ABI of the ACL datapath (include/bessgpu.h bg_acl_*):
-// the ordered rule list, compiled to the frame's byte order and uploaded
-// when it changes (bg_acl.hip reads it with wave-uniform loads).
+// the ordered rule list, compiled when it changes into the forms bg_acl.hip
+// classifies with (the list in the frame's byte order for the scans, the
+// per-dimension bit vectors, the decision tree) and uploaded.
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "bg_internal.h"
@@ -22,10 +27,14 @@ struct bg_acl {
   uint32_t *d_bv = nullptr;  // the bit-vector form (bv_args), or none
   size_t bv_cap = 0;         // words
   AclArgs bv_args{};         // its geometry and offsets (bv = d_bv)
+  uint32_t *d_tree = nullptr;  // the decision tree (tree_words, root), or none
+  size_t tree_cap = 0;         // words
+  uint32_t tree_words = 0, ntrees = 0, roots[4] = {};
   std::mutex mu;
   ~bg_acl() {
     if (d_rules) (void)hipFree(d_rules);
     if (d_bv) (void)hipFree(d_bv);
+    if (d_tree) (void)hipFree(d_tree);
   }
 };
 
@@ -134,6 +143,212 @@ static bool build_bv(const std::vector<bg_acl_rule> &R, std::vector<uint32_t> *i
   return true;
 }
 
+// ---- decision trees (AclArgs tree fields, bg_acl.hip AclTreeOp) ---------
+//
+// Every ACL field is a prefix: the addresses by their prefix length
+// (Ipv4Prefix), a port exact (length 16) or 0 = any (length 0). A node is
+// the box of packets that agree on the first c[d] bits of each dimension d;
+// it cuts k more bits of one dimension into 2^k children. A rule goes to the
+// children its prefix allows (all of them when its length is <= c[d]).
+// A node's list keeps the list order and ends at the first rule that covers
+// its box (length <= c[d] in every dimension): later rules can never be the
+// first match there. Lists of <= kLeafMax rules become leaves. Children
+// with equal lists share one subtree (equal lists imply equal subtrees: a
+// rule in two siblings has no bits left to test in the cut dimension).
+//
+// One tree over all rules replicates the rules that are wild in the cut
+// dimension into every child: 1000 random rules (bench lists) needed up to
+// 600 KB. So the rules are split by which address is specific (prefix
+// length >= kSpecific; EffiCuts' separation), one tree per class, and the
+// packet takes the lowest rule index any tree matches (records carry it).
+// A rule that matches every packet ends every class's list.
+
+namespace {
+
+constexpr int kTreeW[4] = {32, 32, 16, 16};
+constexpr size_t kAclTreeLdsBytes = 112 << 10;  // + 32 KB stage <= 160 KB
+constexpr uint32_t kLeafMax = 8;
+constexpr int kCutMax = 8;              // up to 256 children per node
+constexpr size_t kTreeMaxRules = 8192;  // larger lists: the scans
+constexpr int kSpecific = 8;
+
+struct TreeRule {
+  uint32_t v[4];   // host-order value, masked to its prefix
+  uint8_t len[4];  // prefix length
+  bool drop;
+};
+
+bool prefix_len(uint32_t mask, uint8_t *len) {
+  const uint32_t inv = ~mask;
+  if (inv & (inv + 1)) return false;  // not a prefix mask
+  *len = (uint8_t)__builtin_popcount(mask);
+  return true;
+}
+
+typedef std::array<uint8_t, 4> Box;  // bits fixed per dimension
+
+struct TreeBuilder {
+  std::vector<TreeRule> R;
+  std::vector<uint32_t> recs;   // leaf records, 4 words each
+  std::vector<uint32_t> nodes;  // child arrays; internal refs node-relative
+  std::unordered_map<std::string, uint32_t> memo;
+  size_t budget_words = kAclTreeLdsBytes / 4;
+  bool overflow = false;
+
+  uint32_t bits_of(const TreeRule &r, int d, int c, int k) const {
+    return (r.v[d] >> (kTreeW[d] - c - k)) & ((1u << k) - 1);
+  }
+  bool covers(const TreeRule &r, const Box &c) const {
+    for (int d = 0; d < 4; d++)
+      if (r.len[d] > c[d]) return false;
+    return true;
+  }
+  // the 2^k children of (lst, c) cut on k bits of d, truncated
+  void cut(const std::vector<uint32_t> &lst, const Box &c, int d, int k,
+           std::vector<std::vector<uint32_t>> *ch, Box *c2) const {
+    const uint32_t nc = 1u << k;
+    *c2 = c;
+    (*c2)[d] = (uint8_t)(c[d] + k);
+    ch->assign(nc, {});
+    std::vector<uint8_t> closed(nc, 0);
+    auto put = [&](uint32_t j, uint32_t r) {
+      if (closed[j]) return;
+      (*ch)[j].push_back(r);
+      if (covers(R[r], *c2)) closed[j] = 1;
+    };
+    for (uint32_t r : lst) {
+      const TreeRule &x = R[r];
+      if (x.len[d] <= c[d]) {
+        for (uint32_t j = 0; j < nc; j++) put(j, r);
+      } else if (x.len[d] >= c[d] + k) {
+        put(bits_of(x, d, c[d], k), r);
+      } else {
+        const int span = c[d] + k - x.len[d];
+        const uint32_t base = bits_of(x, d, c[d], k) & ~((1u << span) - 1);
+        for (uint32_t j = 0; j < (1u << span); j++) put(base + j, r);
+      }
+    }
+  }
+  static std::string key_of(const std::vector<uint32_t> &lst, const Box &c) {
+    std::string s(reinterpret_cast<const char *>(c.data()), 4);
+    s.append(reinterpret_cast<const char *>(lst.data()), lst.size() * 4);
+    return s;
+  }
+  uint32_t leaf(const std::vector<uint32_t> &lst) {
+    const uint32_t off = (uint32_t)(recs.size() / 4);
+    for (uint32_t r : lst) {
+      const TreeRule &x = R[r];
+      recs.push_back(x.v[0]);
+      recs.push_back(x.v[1]);
+      recs.push_back(x.v[2] | (x.v[3] << 16));
+      recs.push_back((uint32_t)x.len[0] | ((uint32_t)x.len[1] << 6) |
+                     ((uint32_t)(x.len[2] != 0) << 12) | ((uint32_t)(x.len[3] != 0) << 13) |
+                     ((uint32_t)x.drop << 14) | (r << 16));
+    }
+    return 0x80000000u | ((uint32_t)lst.size() << 16) | off;
+  }
+  uint32_t build(const std::vector<uint32_t> &lst, const Box &c) {
+    if (overflow) return 0;
+    const std::string key = key_of(lst, c);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+    uint32_t ref;
+    int best_d = -1, best_k = 0;
+    size_t best_mx = 0, best_mem = 0;
+    if (lst.size() > kLeafMax) {
+      std::vector<std::vector<uint32_t>> ch;
+      Box c2;
+      for (int d = 0; d < 4; d++) {
+        bool useful = false;
+        for (uint32_t r : lst) useful |= R[r].len[d] > c[d];
+        if (!useful) continue;
+        for (int k = 1; k <= std::min(kCutMax, kTreeW[d] - (int)c[d]); k++) {
+          cut(lst, c, d, k, &ch, &c2);
+          std::unordered_set<std::string> uniq;
+          size_t mx = 0, mem = (size_t)1 << k;
+          for (auto &x : ch) {
+            mx = std::max(mx, x.size());
+            if (uniq.insert(key_of(x, c2)).second) mem += x.size() * 4;
+          }
+          // wider cuts only while they stay within a space factor
+          if (k > 1 && mem > 16 * lst.size() + 64) break;
+          if (best_d < 0 || mx < best_mx || (mx == best_mx && mem < best_mem)) {
+            best_d = d;
+            best_k = k;
+            best_mx = mx;
+            best_mem = mem;
+          }
+        }
+      }
+    }
+    // no useful cut: every rule is covered, so the list is one rule long
+    if (best_d < 0) {
+      ref = leaf(lst);
+    } else {
+      std::vector<std::vector<uint32_t>> ch;
+      Box c2;
+      cut(lst, c, best_d, best_k, &ch, &c2);
+      const uint32_t nc = 1u << best_k;
+      const uint32_t at = (uint32_t)nodes.size();
+      nodes.resize(nodes.size() + nc);
+      const int shift = kTreeW[best_d] - c2[best_d] + (best_d == 3 ? 16 : 0);
+      ref = ((uint32_t)std::min(best_d, 2) << 25) | ((uint32_t)best_k << 21) |
+            ((uint32_t)shift << 16) | at;
+      for (uint32_t j = 0; j < nc && !overflow; j++) {
+        const uint32_t child = build(ch[j], c2);  // may grow nodes
+        nodes[at + j] = child;
+      }
+    }
+    if (recs.size() + nodes.size() > budget_words) overflow = true;
+    memo.emplace(key, ref);
+    return ref;
+  }
+};
+
+}  // namespace
+
+// The trees' image [leaf records][child arrays] and their roots, or false
+// (no trees: masks that are not prefixes, too many rules, or an image past
+// the LDS budget).
+static bool build_tree(const std::vector<bg_acl_rule> &rules, std::vector<uint32_t> *img,
+                       uint32_t *roots, uint32_t *ntrees) {
+  if (rules.empty() || rules.size() > kTreeMaxRules) return false;
+  TreeBuilder b;
+  for (const bg_acl_rule &x : rules) {
+    TreeRule t;
+    if (!prefix_len(x.src_mask, &t.len[0]) || !prefix_len(x.dst_mask, &t.len[1]))
+      return false;
+    t.v[0] = x.src_addr & x.src_mask;
+    t.v[1] = x.dst_addr & x.dst_mask;
+    t.v[2] = x.src_port;
+    t.v[3] = x.dst_port;
+    t.len[2] = x.src_port ? 16 : 0;
+    t.len[3] = x.dst_port ? 16 : 0;
+    t.drop = x.drop != 0;
+    b.R.push_back(t);
+  }
+  // classes: src address specific x dst address specific
+  std::vector<uint32_t> cls[4];
+  for (uint32_t i = 0; i < rules.size(); i++) {
+    const TreeRule &t = b.R[i];
+    cls[(t.len[0] >= kSpecific ? 0 : 2) + (t.len[1] >= kSpecific ? 0 : 1)].push_back(i);
+    if (b.covers(t, {0, 0, 0, 0})) break;  // matches every packet
+  }
+  std::vector<uint32_t> r;
+  for (auto &l : cls)
+    if (!l.empty()) r.push_back(b.build(l, {0, 0, 0, 0}));
+  if (b.overflow) return false;
+  const uint32_t base = (uint32_t)b.recs.size();  // a multiple of 4
+  auto fix = [&](uint32_t ref) { return (ref >> 31) ? ref : ref + base; };
+  img->assign(b.recs.begin(), b.recs.end());
+  for (uint32_t w : b.nodes) img->push_back(fix(w));
+  while (img->size() % 4) img->push_back(0);
+  if (img->size() * 4 > kAclTreeLdsBytes || img->size() > 0xFFFF) return false;
+  *ntrees = (uint32_t)r.size();
+  for (size_t i = 0; i < r.size(); i++) roots[i] = fix(r[i]);
+  return true;
+}
+
 static int acl_sync_locked(bg_acl *h, int dev, hipStream_t s) {
   if (!h->dirty && h->device == dev && (h->d_rules || h->rules.empty())) return 0;
   int r = set_device(dev);
@@ -179,6 +394,18 @@ static int acl_sync_locked(bg_acl *h, int dev, hipStream_t s) {
     HIP_TRY(hipMemcpyAsync(h->d_bv, bv.data(), bv.size() * 4, hipMemcpyHostToDevice, s));
     h->bv_args.bv = h->d_bv;
   }
+  std::vector<uint32_t> tree;
+  h->tree_words = 0;
+  if (build_tree(h->rules, &tree, h->roots, &h->ntrees)) {
+    if (!h->d_tree || h->tree_cap < tree.size() || h->device != dev) {
+      if (h->d_tree) (void)hipFree(h->d_tree);
+      h->d_tree = nullptr;
+      h->tree_cap = tree.size();
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tree), h->tree_cap * 4));
+    }
+    HIP_TRY(hipMemcpyAsync(h->d_tree, tree.data(), tree.size() * 4, hipMemcpyHostToDevice, s));
+    h->tree_words = (uint32_t)tree.size();
+  }
   HIP_TRY(hipStreamSynchronize(s));
   h->device = dev;
   h->dirty = false;
@@ -211,6 +438,23 @@ void bg_acl_clear(bg_acl *h) {
 
 size_t bg_acl_count(const bg_acl *h) { return h->rules.size(); }
 
+int bg_acl_tree(bg_acl *h, uint32_t *img, size_t cap, size_t *words, uint32_t *roots,
+                int *ntrees) {
+  if (!words || !roots || !ntrees) return fail(EINVAL, "bad arguments");
+  std::vector<uint32_t> t;
+  uint32_t nt = 0;
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!build_tree(h->rules, &t, roots, &nt))
+      return fail(ENOENT, "no decision tree for this rule list");
+  }
+  *ntrees = (int)nt;
+  *words = t.size();
+  if (img && cap >= t.size()) memcpy(img, t.data(), t.size() * 4);
+  else if (img) return fail(ENOBUFS, "tree needs %zu words", t.size());
+  return 0;
+}
+
 int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
                     uint16_t igate, uint16_t *d_out, bg_stream_t stream) {
   if (stride % 16 || stride < 64 || ((uintptr_t)d_frames & 15))
@@ -228,6 +472,12 @@ int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
     if (r) return r;
     a = h->bv_args;  // the bit-vector form, when it was built
     a.rules = h->d_rules;
+    if (h->tree_words) {
+      a.tree = h->d_tree;
+      a.tree_words = h->tree_words;
+      a.ntrees = h->ntrees;
+      memcpy(a.roots, h->roots, sizeof(a.roots));
+    }
     a.nrules = (uint32_t)((h->rules.size() + 3) / 4 * 4);
   }
   int r = set_device(dev);

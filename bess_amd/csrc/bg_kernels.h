@@ -157,6 +157,23 @@ struct AclArgs {
   const uint32_t *bv;
   uint32_t k0, k1, lg0, lg1, nw, grp;
   uint32_t b_off[2], s_off[4], v_off[4], p_off[2], d_off;
+  // Decision-tree form (AclTreeOp; tree == nullptr: none): ntrees trees
+  // (one per class of rules, bg_acl_api.cc build_tree) in one image of
+  // tree_words dwords, staged whole in LDS: 16-byte leaf rule records, then
+  // the internal nodes' child arrays. A node reference (roots, children):
+  //   leaf      bit 31 | count << 16 | first record (16-byte units)
+  //   internal  dim << 25 | k << 21 | shift << 16 | child array (dword)
+  // where the child taken is bits [shift, shift + k) of the dimension's
+  // value: 0 src addr, 1 dst addr (host order), 2 the ports (src port in
+  // the low half, dst port in the high half, host order).
+  // A record: {src addr, dst addr, ports (as above), src prefix length |
+  // dst prefix length << 6 | src port exact << 12 | dst port exact << 13 |
+  // drop << 14 | rule index << 16}; a leaf's records are, in list order,
+  // the class's rules that can still be the first match in its box, cut
+  // after one that covers it. The packet's rule: the lowest index matched.
+  const uint32_t *tree;
+  uint32_t tree_words, ntrees;
+  uint32_t roots[4];
 };
 
 // IPLookup (core/modules/ip_lookup.cc): DIR-24-8 longest-prefix match on

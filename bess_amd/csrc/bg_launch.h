@@ -30,7 +30,8 @@ constexpr uint32_t kPathNoSlab = 4;     // lane-per-packet kernels, never the sl
 constexpr uint32_t kPathWmNoTags = 8;   // WildcardMatch: key filter, not tag words
 constexpr uint32_t kPathAclScan = 16;   // ACL: the rule scan with scalar rule loads
 constexpr uint32_t kPathAclBv = 32;     // ACL: per-dimension bit vectors
-constexpr uint32_t kPathAll = 63;
+constexpr uint32_t kPathAclLds = 64;    // ACL: the rule scan from LDS (not the tree)
+constexpr uint32_t kPathAll = 127;
 
 uint32_t path_flags();
 

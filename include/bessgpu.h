@@ -204,6 +204,7 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_WM_NO_TAGS 8
 #define BG_PATH_ACL_SCAN 16 /* ACL: rule scan with scalar loads (not LDS) */
 #define BG_PATH_ACL_BV 32   /* ACL: per-dimension bit vectors */
+#define BG_PATH_ACL_LDS 64  /* ACL: rule scan from LDS (not the decision tree) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */
@@ -260,6 +261,14 @@ size_t bg_acl_count(const bg_acl *h);
  * BG_DROP_GATE (it drops, or no rule matches). Stride >= 64. */
 int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
                     uint16_t igate, uint16_t *d_out, bg_stream_t stream);
+/* Diagnostic (host only, no device): the decision-tree image the classify
+ * kernel stages in LDS for the current rule list (layout: AclArgs in
+ * bess_amd/csrc/bg_kernels.h) into img (capacity cap words; *words = its
+ * size) and the roots of its *ntrees (<= 4) trees. -ENOENT when the list
+ * gets no trees (masks that are not prefixes, > 8192 rules, or an image
+ * past 112 KB). */
+int bg_acl_tree(bg_acl *h, uint32_t *img, size_t cap, size_t *words, uint32_t *roots,
+                int *ntrees);
 
 /* ---- IPLookup (core/modules/ip_lookup.cc) ----------------------------- */
 /* Longest-prefix match on the IPv4 destination with rte_lpm's table

@@ -67,10 +67,32 @@ def workload(nrules, npkts, seed, stride=64):
     return rules, P.build_frames(pk, 60, stride)
 
 
-# the default choice (bit vectors up to 128 rules, else the rule scan from
-# LDS), the scan with scalar rule loads, bit vectors forced, and the LDS
-# forbidden (the scan with scalar loads)
-PATHS = [0, LB.BG_PATH_ACL_SCAN, LB.BG_PATH_ACL_BV, LB.BG_PATH_NO_LDS]
+# the default choice (the decision trees while their image fits), the rule
+# scan from LDS, the scan with scalar rule loads, bit vectors forced, and
+# the LDS forbidden (the scan with scalar loads)
+PATHS = [0, LB.BG_PATH_ACL_LDS, LB.BG_PATH_ACL_SCAN, LB.BG_PATH_ACL_BV,
+         LB.BG_PATH_NO_LDS]
+
+
+def no_catch_all(rules):
+    """the list without rules that match nearly everything (no address
+    prefix): every tree class is populated and no scan ends early"""
+    return [r for r in rules if r.get("src_ip") or r.get("dst_ip")]
+
+
+@pytest.mark.parametrize("nrules", [100, 1000, 3000, 8000])
+def test_trees_without_catch_all_vs_oracle(nrules):
+    rules, f = workload(nrules, 60000, seed=500 + nrules)
+    rules = no_catch_all(rules)
+    m = ACL(rules=rules)
+    o = OM.OracleACL(rules=rules)
+    want = o.process(f, 64, len(f))
+    assert (want == 0).any() and (want == 8192).any()
+    for flags in (0, LB.BG_PATH_ACL_LDS):
+        with LB.kernel_paths(flags):
+            assert (device_gates(m, f, 64) == want).all()
+    with LB.kernel_paths(LB.BG_PATH_NO_SLAB):  # lane-per-packet kernel
+        assert (device_gates(m, f, 64) == want).all()
 
 
 @pytest.mark.parametrize("flags", PATHS)
