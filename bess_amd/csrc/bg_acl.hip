@@ -3,12 +3,11 @@
 // whose src/dst prefixes and non-zero ports match decides -- emit on the
 // input gate unless the rule drops; no match drops.
 //
-// Two forms. The rule scan: the rule list is the same for every packet, so rules are read with
-// wave-uniform (scalar) loads and each rule costs a handful of VALU ops per
-// 64 packets; a wave stops scanning once all its lanes have matched. The
-// packet side comes from the header line (IHL at byte 14, addresses at
-// 26..33, ports at 14 + 4*IHL), via bg_line_dev.h (coalesced slab kernel
-// for 64 B slots).
+// Four forms (launch_acl picks): decision trees in LDS (AclTreeOp, the
+// default), per-dimension bit vectors (AclBvOp), and the ordered rule scan
+// from LDS (AclLdsOp) or with scalar loads (AclOp). The packet side comes
+// from the header line (IHL at byte 14, addresses at 26..33, ports at
+// 14 + 4*IHL), via bg_line_dev.h (coalesced slab kernel for 64 B slots).
 #include <hip/hip_runtime.h>
 
 #include "bg_kernels.h"
@@ -17,6 +16,10 @@
 namespace bg {
 namespace {
 
+// The rule scan with scalar loads: the rule list is the same for every
+// packet, so rules are read with wave-uniform (scalar) loads and each rule
+// costs a handful of VALU ops per 64 packets; a wave stops scanning once
+// all its lanes have matched.
 struct AclOp {
   using Args = AclArgs;
   static constexpr bool kWrites = false;
