@@ -21,6 +21,7 @@ BG_PATH_WM_NO_TAGS = 8
 BG_PATH_ACL_SCAN = 16
 BG_PATH_ACL_BV = 32
 BG_PATH_ACL_LDS = 64
+BG_PATH_LPM_DIR24 = 128
 KEY_BYTES = 64
 
 

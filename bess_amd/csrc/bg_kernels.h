@@ -186,6 +186,12 @@ struct LpmArgs {
   const uint16_t *tbl24;  // 2^24 entries
   const uint16_t *tbl8;   // groups x 256 entries
   uint32_t default_gate, pad;
+  // DIR-16-8-8, the same entries with tbl24 folded (null: DIR-24-8): tbl16
+  // (2^16 entries) per /16 block either the value every /24 of the block
+  // has in tbl24, or 0x8000 | g for tbl2 group g (256 entries: the block's
+  // tbl24 entries, which may extend into tbl8 as before)
+  const uint16_t *tbl16;
+  const uint16_t *tbl2;
 };
 
 // UpdateTTL (core/modules/update_ttl.cc): in place on the frames.

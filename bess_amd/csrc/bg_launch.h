@@ -31,7 +31,8 @@ constexpr uint32_t kPathWmNoTags = 8;   // WildcardMatch: key filter, not tag wo
 constexpr uint32_t kPathAclScan = 16;   // ACL: the rule scan with scalar rule loads
 constexpr uint32_t kPathAclBv = 32;     // ACL: per-dimension bit vectors
 constexpr uint32_t kPathAclLds = 64;    // ACL: the rule scan from LDS (not the tree)
-constexpr uint32_t kPathAll = 127;
+constexpr uint32_t kPathLpmDir24 = 128;  // IPLookup: DIR-24-8 (not DIR-16-8-8)
+constexpr uint32_t kPathAll = 255;
 
 uint32_t path_flags();
 

@@ -47,8 +47,8 @@ __device__ __forceinline__ uint32_t line_stage_unit(uint32_t slot, uint32_t q) {
   return slot * 4 + ((q + (slot >> 2)) & 3);
 }
 
-template <class Op>
-__global__ __launch_bounds__(kLineBlock) void line_kernel(typename Op::Args a) {
+template <class Op, int kBlock = kLineBlock>
+__global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   Op::stage(lds, a);
   __syncthreads();
@@ -204,6 +204,20 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
   const int occ = line_occupancy(reinterpret_cast<const void *>(kern), tab);
   const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLineBlock), tab, s, a);
+  return hipGetLastError();
+}
+
+// One packet per lane in 1024-thread workgroups, for ops whose LDS tables
+// leave room for one workgroup per CU and no slab stage: 16 waves per CU
+template <class Op>
+hipError_t launch_line_wide(const typename Op::Args &a, int num_cus, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  const size_t tab = (Op::lds_bytes(a) + 15) & ~(size_t)15;
+  auto kern = line_kernel<Op, 1024>;
+  const int occ = occupancy(reinterpret_cast<const void *>(kern), 1024, tab, 1);
+  const uint64_t need = (a.n + 1023) / 1024;
+  const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), tab, s, a);
   return hipGetLastError();
 }
 

@@ -35,10 +35,15 @@ struct bg_lpm {
   int device = -1;
   uint16_t *d_tbl24 = nullptr, *d_tbl8 = nullptr;
   size_t d_cap8 = 0;  // groups
+  uint16_t *d_tbl16 = nullptr, *d_tbl2 = nullptr;  // DIR-16-8-8 (or none)
+  size_t d_cap2 = 0;  // groups
+  bool has16 = false;
   std::mutex mu;
   ~bg_lpm() {
     if (d_tbl24) (void)hipFree(d_tbl24);
     if (d_tbl8) (void)hipFree(d_tbl8);
+    if (d_tbl16) (void)hipFree(d_tbl16);
+    if (d_tbl2) (void)hipFree(d_tbl2);
   }
 };
 
@@ -84,6 +89,41 @@ static int lpm_sync_locked(bg_lpm *h, int dev, hipStream_t s) {
   }
   HIP_TRY(hipMemcpyAsync(h->d_tbl24, t24.data(), (size_t)kTbl24 * 2,
                          hipMemcpyHostToDevice, s));
+  // DIR-16-8-8: a /16 block whose 256 tbl24 entries are one plain value
+  // keeps it in tbl16; any other block gets a tbl2 group (its entries)
+  std::vector<uint16_t> t16(1u << 16), t2;
+  h->has16 = true;
+  for (uint32_t b = 0; b < (1u << 16) && h->has16; b++) {
+    const uint16_t *seg = t24.data() + (size_t)b * 256;
+    const bool flat = !(seg[0] & 0x8000u) && std::all_of(seg, seg + 256, [&](uint16_t v) {
+      return v == seg[0];
+    });
+    if (flat) {
+      t16[b] = seg[0];
+    } else if (t2.size() / 256 >= kMaxGroups) {
+      h->has16 = false;  // past 15-bit group indices: DIR-24-8 only
+    } else {
+      t16[b] = (uint16_t)(0x8000u | (t2.size() / 256));
+      t2.insert(t2.end(), seg, seg + 256);
+    }
+  }
+  if (h->has16) {
+    if (!h->d_tbl16 || h->device != dev) {
+      if (h->d_tbl16) (void)hipFree(h->d_tbl16);
+      h->d_tbl16 = nullptr;
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl16), t16.size() * 2));
+    }
+    const size_t ng2 = std::max<size_t>(t2.size() / 256, 1);
+    if (!h->d_tbl2 || h->d_cap2 < ng2 || h->device != dev) {
+      if (h->d_tbl2) (void)hipFree(h->d_tbl2);
+      h->d_tbl2 = nullptr;
+      h->d_cap2 = std::max<size_t>(ng2, 64);
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl2), h->d_cap2 * 512));
+    }
+    HIP_TRY(hipMemcpyAsync(h->d_tbl16, t16.data(), t16.size() * 2, hipMemcpyHostToDevice, s));
+    if (!t2.empty())
+      HIP_TRY(hipMemcpyAsync(h->d_tbl2, t2.data(), t2.size() * 2, hipMemcpyHostToDevice, s));
+  }
   if (g)
     HIP_TRY(hipMemcpyAsync(h->d_tbl8, t8.data(), t8.size() * 2,
                            hipMemcpyHostToDevice, s));
@@ -178,6 +218,8 @@ int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
     if (r) return r;
     a.tbl24 = h->d_tbl24;
     a.tbl8 = h->d_tbl8;
+    a.tbl16 = h->has16 ? h->d_tbl16 : nullptr;
+    a.tbl2 = h->d_tbl2;
   }
   int r = set_device(dev);
   if (r) return r;

@@ -205,6 +205,7 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_ACL_SCAN 16 /* ACL: rule scan with scalar loads (not LDS) */
 #define BG_PATH_ACL_BV 32   /* ACL: per-dimension bit vectors */
 #define BG_PATH_ACL_LDS 64  /* ACL: rule scan from LDS (not the decision tree) */
+#define BG_PATH_LPM_DIR24 128 /* IPLookup: DIR-24-8 tables (not DIR-16-8-8) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */

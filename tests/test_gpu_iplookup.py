@@ -1,4 +1,4 @@
-"""IPLookup on the GPU (DIR-24-8 kernel via the module surface): gates
+"""IPLookup on the GPU (DIR-16-8-8 and DIR-24-8 kernels via the module surface): gates
 bit-exact against the oracle's longest-prefix match and the reference's
 module tests; route tables of every depth mix, deletes revealing shorter
 prefixes, default-gate changes, device slabs, the host path and the pipe."""
@@ -9,6 +9,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from bess_amd import _lib as LB  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 from bess_amd.modules import IPLookup, Pipe  # noqa: E402
 from oracle import oracle_more as OM  # noqa: E402
@@ -78,9 +79,16 @@ def build(rt, max_rules=0, max_tbl8s=0):
     return m, o
 
 
+# DIR-16-8-8 with tbl16 in LDS (the default), with tbl16 in L2 (slab and
+# lane-per-packet kernels), and DIR-24-8
+PATHS = [0, LB.BG_PATH_NO_LDS, LB.BG_PATH_NO_LDS | LB.BG_PATH_NO_SLAB,
+         LB.BG_PATH_LPM_DIR24]
+
+
+@pytest.mark.parametrize("flags", PATHS)
 @pytest.mark.parametrize("nroutes,deep", [(1, 0.0), (100, 0.1), (5000, 0.05),
-                                          (50000, 0.002)])
-def test_random_routes_vs_oracle(nroutes, deep):
+                                          (50000, 0.002), (150000, 0.0)])
+def test_random_routes_vs_oracle(nroutes, deep, flags):
     rng = np.random.default_rng(nroutes)
     rt = routes(nroutes, rng, deep)
     m, o = build(rt, max_rules=nroutes + 10, max_tbl8s=4096)
@@ -89,11 +97,13 @@ def test_random_routes_vs_oracle(nroutes, deep):
     inside = dsts_inside(rt, 40000, rng)
     f = frames_to(np.concatenate([inside, rnd]))
     want = o.process(f, 64, len(f))
-    assert (device_gates(m, f, 64) == want).all()
+    with LB.kernel_paths(flags):
+        assert (device_gates(m, f, 64) == want).all()
     assert (want != 8192).mean() > 0.4
 
 
-def test_delete_reveals_shorter_prefix_and_default_gate():
+@pytest.mark.parametrize("flags", PATHS)
+def test_delete_reveals_shorter_prefix_and_default_gate(flags):
     m, o = build([("10.0.0.0", 8, 1), ("10.1.0.0", 16, 2), ("10.1.1.0", 24, 3),
                   ("10.1.1.128", 25, 4), ("10.1.1.192", 26, 5), ("10.1.1.200", 32, 6)])
     dst = [0x0A0101C8, 0x0A0101C1, 0x0A010181, 0x0A010101, 0x0A010201, 0x0A020202,
@@ -110,7 +120,8 @@ def test_delete_reveals_shorter_prefix_and_default_gate():
         if st:
             getattr(m, st[0])(**st[1])
             getattr(o, st[0])(**st[1])
-        assert (device_gates(m, f, 128) == o.process(f, 128, len(f))).all(), st
+        with LB.kernel_paths(flags):
+            assert (device_gates(m, f, 128) == o.process(f, 128, len(f))).all(), st
 
 
 def test_reference_module_tests(golden):
