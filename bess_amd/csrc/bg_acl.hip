@@ -253,7 +253,14 @@ hipError_t launch_acl(const AclArgs &a, int num_cus, hipStream_t s) {
   const uint32_t pf = path_flags();
   if (pf & (kPathAclScan | kPathNoLds)) return launch_line<AclOp>(a, num_cus, s);
   if (a.bv && (pf & kPathAclBv)) return launch_line<AclBvOp>(a, num_cus, s);
-  if (a.tree && !(pf & kPathAclLds)) return launch_line<AclTreeOp>(a, num_cus, s);
+  if (a.tree && !(pf & kPathAclLds)) {
+    // trees past 48 KB would leave one 512-thread slab workgroup per CU;
+    // 1024-thread lane-per-packet workgroups keep 16 waves (3000 rules
+    // without catch-alls: 0.36 ms against 0.68)
+    if ((size_t)a.tree_words * 4 > kAclLdsRules && !(pf & kPathNoSlab))
+      return launch_line_wide<AclTreeOp>(a, num_cus, s);
+    return launch_line<AclTreeOp>(a, num_cus, s);
+  }
   // measured (scripts/acl_paths.py, 16 M packets): bit vectors 0.41 ms at
   // 100 rules (4 words per vector) against 0.50 for the LDS scan; at 1000
   // rules (32 words) 0.77 against 0.49 -- wildcards fill the summaries, so

@@ -15,6 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from bess_amd import _lib as LB  # noqa: E402
+
+if len(sys.argv) > 1:  # another build of the library (A/B on one box)
+    LB.LIB_PATH = os.path.abspath(sys.argv[1])
 from bess_amd.modules import ACL  # noqa: E402
 from test_gpu_acl import workload  # noqa: E402
 
