@@ -22,7 +22,7 @@ from collections import defaultdict
 KERNELS = {"em": "em_slab_kernel", "cksum": "cksum_kernel",
            "wm": "wm_tags_kernel", "wm2k": "wm_tags_kernel",
            "c5": "em_slab_kernel",
-           "hashlb": "HlbOp<2>", "acl": "AclOp", "iplookup": "LpmOp",
+           "hashlb": "HlbOp<2>", "acl": "AclTreeOp", "iplookup": "Lpm16LdsOp",
            "ttl": "TtlOp<4>", "nat": "NatOp", "dnat": "dnat_fused_slab_kernel"}
 # algorithmic bytes per launch of each bench workload
 ALGO = {"em": 66 * (16 << 20), "cksum": 1502 * (1 << 20),
