@@ -44,14 +44,22 @@ def main():
             best = min(best, e0.elapsed_time(e1) / 10)
         return round(best, 4), g.cpu().numpy().view(np.uint16)[:n0].copy()
 
+    flags = int(os.environ.get("WM_AB_FLAGS", "0"), 0)
     h = torch.from_numpy(np.ascontiguousarray(frames[:, :64]).reshape(-1)).cuda().repeat(rep)
     g = torch.empty(n, dtype=torch.int16, device="cuda")
-    out["slab_ms"], gh = timed(h, 64, g)
+    ref = None
+    for name, fl in (("default", 0), ("flags", flags)) if flags else (("default", 0),):
+        with _lib.kernel_paths(fl):
+            out[name + "_slab_ms"], gh = timed(h, 64, g)
+        ref = gh if ref is None else ref
+        out[name + "_same_as_default"] = bool((gh == ref).all())
     del h
     d = torch.from_numpy(frames.reshape(-1)).cuda().repeat(rep)
-    out["slots2k_ms"], g2 = timed(d, 2048, g)
-    out["same_gates"] = bool((gh == g2).all())
-    out["gates_crc"] = int(np.bitwise_xor.reduce(gh.astype(np.uint64) * np.arange(1, n0 + 1, dtype=np.uint64)))
+    for name, fl in (("default", 0), ("flags", flags)) if flags else (("default", 0),):
+        with _lib.kernel_paths(fl):
+            out[name + "_slots2k_ms"], g2 = timed(d, 2048, g)
+        out[name + "_2k_same"] = bool((g2 == ref).all())
+    out["gates_crc"] = int(np.bitwise_xor.reduce(ref.astype(np.uint64) * np.arange(1, n0 + 1, dtype=np.uint64)))
     print(json.dumps(out))
 
 
