@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "bg_internal.h"
+#include "bg_launch.h"
 
 using namespace bg;
 
@@ -239,11 +240,15 @@ struct bg_dnat {
     if (map_dirty || !dev.valid) {
       std::vector<uint64_t> keys, hashes;
       std::vector<uint8_t> vals, img;
-      for (auto &kv : map) {  // key words: the endpoint, its translation
-        keys.push_back(kv.first);
-        keys.push_back(ent_ep[kv.second]);
+      if (ent_ep.size() > (1u << 24))
+        return fail(ENOSPC, "NAT map past 2^24 entries");
+      for (auto &kv : map) {  // key words: the endpoint, its translation,
+        // the entry index in their spare top bits (bg_dnat.hip lookup_hit)
+        const uint64_t e = kv.second;
+        keys.push_back(kv.first | (e >> 16) << 56);
+        keys.push_back((ent_ep[e] & 0xFFFFFFFFFFFFull) | (e & 0xFFFF) << 48);
         hashes.push_back(hash_words(&kv.first, 1, kDefaultSeed));
-        for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(kv.second >> (8 * b)));
+        for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(e >> (8 * b)));
       }
       TableLayout L;
       r = build_image(2, 4, 1, keys, vals, hashes, &img, &L);
@@ -364,6 +369,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.ts = h->d_ts;
   a.nent = h->ent_ep.size();
   a.out = d_out;
+  a.ab_phase = (uint32_t)knob("BG_NAT_PHASE", 0);
   HIP_TRY(hipMemsetAsync(h->d_nmiss, 0, 4, s));
   const int ncu = num_cus(dev);
   // final hits stamped on the device; forward misses and forward hits on

@@ -247,6 +247,7 @@ struct DnatArgs {
   // apply over a packet list: res[k] = packet, mres[k] = entry, keys[k] =
   // its endpoint, k < nlist (the fused kernel's forward misses)
   uint32_t list;
+  uint32_t ab_phase;  // A/B build only (timing): 1 = no timestamp read/refresh
   uint64_t nlist;
   const uint32_t *mres;
 };

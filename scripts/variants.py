@@ -31,7 +31,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_WM_PHASE",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
-         "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2"]
+         "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE"]
 
 
 def set_env(v):
@@ -162,6 +162,46 @@ def main():
             r[k]["GBps_1502B"] = round(1502 * n / (r[k]["median_ms"] * 1e-3) / 1e9, 1)
         out["ck"] = r
         del d
+    if "natphase" in which:
+        # NAT established flows as bench.py times them (16 M packets of 64 K
+        # flows, fresh copies, `now` advancing): everything vs. without the
+        # forward timestamp read and refresh (BG_NAT_PHASE=1)
+        from bess_amd.modules import NAT
+        nflow, n = 1 << 16, 1 << 24
+        _, _, flows = P.em_workload(16, nflow, seed=0x5EED, pkt_seed=17)
+        zero = (flows[:, 34] == 0) & (flows[:, 35] == 0)
+        flows[zero, 35] = 1
+        rng = np.random.default_rng(17)
+        slab = flows[rng.integers(0, nflow, n)]
+        m = NAT(ext_addrs=[{"ext_addr": "100.64.0.1"}, {"ext_addr": "100.64.0.2"}],
+                seed=0x5EED)
+        t0 = 10 ** 12
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        m.process_device(torch.from_numpy(flows.reshape(-1).copy()).to(dev), 64, nflow, g, t0)
+        src = torch.from_numpy(slab.reshape(-1)).to(dev)
+        now = [t0]
+        phases = (("full", {}), ("no_timestamp", {"BG_NAT_PHASE": 1}),
+                  ("no_lookup", {"BG_NAT_PHASE": 2}), ("tags_only", {"BG_NAT_PHASE": 3}),
+                  ("no_value_read", {"BG_NAT_PHASE": 4}))
+        res = {name: [] for name, _ in phases}
+        for _ in range(3):
+            for name, env in phases:
+                set_env(env)
+                copies = [src.clone() for _ in range(8)]
+                torch.cuda.synchronize()
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record()
+                for c in copies:
+                    now[0] += 1
+                    m.process_device(c, 64, n, g, now[0])
+                b.record()
+                b.synchronize()
+                res[name].append(a.elapsed_time(b) / len(copies))
+                del copies
+        set_env({})
+        out["natphase"] = {k: {"median_ms": round(statistics.median(v), 4),
+                               "min_ms": round(min(v), 4)} for k, v in res.items()}
     if "wmphase" in which:
         # C4 on the dense header slab, timed up to each phase of
         # wm_tags_kernel (BG_WM_PHASE: 1 header read + key, 2 + the 8
