@@ -165,7 +165,8 @@ def main():
     if "natphase" in which:
         # NAT established flows as bench.py times them (16 M packets of 64 K
         # flows, fresh copies, `now` advancing): everything vs. without the
-        # forward timestamp read and refresh (BG_NAT_PHASE=1)
+        # forward timestamp read and refresh (BG_NAT_PHASE=1) vs. without
+        # the table lookup (2)
         from bess_amd.modules import NAT
         nflow, n = 1 << 16, 1 << 24
         _, _, flows = P.em_workload(16, nflow, seed=0x5EED, pkt_seed=17)
@@ -181,8 +182,7 @@ def main():
         src = torch.from_numpy(slab.reshape(-1)).to(dev)
         now = [t0]
         phases = (("full", {}), ("no_timestamp", {"BG_NAT_PHASE": 1}),
-                  ("no_lookup", {"BG_NAT_PHASE": 2}), ("tags_only", {"BG_NAT_PHASE": 3}),
-                  ("no_value_read", {"BG_NAT_PHASE": 4}))
+                  ("no_lookup", {"BG_NAT_PHASE": 2}))
         res = {name: [] for name, _ in phases}
         for _ in range(3):
             for name, env in phases:
