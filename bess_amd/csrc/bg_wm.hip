@@ -173,7 +173,47 @@ __device__ __forceinline__ bool has_zero_byte(uint32_t x) {
   return ((x - 0x01010101u) & ~x & 0x80808080u) != 0;
 }
 
-template <int KW, int NCH>
+// Dense 64 B header slab (PAIR): the two 16-byte window chunks of a slot
+// are loaded by a lane pair -- load 0 of lanes 2m, 2m+1 holds chunks q0,
+// q0+1 of slot m, load 1 those of slot 32+m -- so each load instruction
+// covers 32 B of each of 32 adjacent slots (half the cache lines per
+// instruction of one 16 B chunk per lane at a 64 B stride). One DPP swap
+// per dword completes the windows: lane 2m takes slot m, lane 2m+1 slot
+// 32+m.
+__device__ __forceinline__ uint64_t pair_slot(int lane) {
+  return (lane & 1) ? 32u + (lane >> 1) : (uint32_t)(lane >> 1);
+}
+
+__device__ __forceinline__ void load_pair(const uint8_t *__restrict__ frames,
+                                          uint64_t n, uint64_t p0, int lane,
+                                          uint32_t win_lo, uint32_t (&r)[8]) {
+  const uint64_t s0 = p0 + (lane >> 1), s1 = s0 + 32;
+  const uint32_t off = win_lo + (lane & 1) * 16;
+  uint4 x = make_uint4(0, 0, 0, 0), y = x;
+  if (s0 < n) x = ld_stream(reinterpret_cast<const uint4 *>(frames + s0 * 64 + off));
+  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(frames + s1 * 64 + off));
+  r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+  r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
+}
+
+template <int NCH>
+__device__ __forceinline__ void pair_window(const uint32_t (&r)[8], int lane,
+                                            uint32_t (&w)[NCH * 4 + 2]) {
+  static_assert(NCH == 2, "pair loads carry two chunks");
+  const bool odd = lane & 1;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    const uint32_t src = odd ? r[d] : r[4 + d];
+    // quad_perm [1,0,3,2]: swap with the neighbouring lane
+    const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)src, 0xB1, 0xF, 0xF, false);
+    w[d] = odd ? recv : r[d];
+    w[4 + d] = odd ? r[4 + d] : recv;
+  }
+  w[8] = 0;
+  w[9] = 0;
+}
+
+template <int KW, int NCH, int PAIR>
 __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
@@ -200,18 +240,27 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
-  uint32_t wn[NCH * 4 + 2];
-  if (t < ntiles && t * 64 + lane < a.n)
-    load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
+  uint32_t wn[PAIR ? 8 : NCH * 4 + 2];
+  if constexpr (PAIR) {
+    if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, wn);
+  } else {
+    if (t < ntiles && t * 64 + lane < a.n)
+      load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
+  }
   for (; t < ntiles; t += nw) {
-    const uint64_t idx = t * 64 + lane;
+    const uint64_t idx = t * 64 + (PAIR ? pair_slot(lane) : (uint64_t)lane);
     const bool live = idx < a.n;
     uint32_t w[NCH * 4 + 2];
+    if constexpr (PAIR) {
+      pair_window<NCH>(wn, lane, w);
+      if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, wn);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
-    const uint64_t nidx = (t + nw) * 64 + lane;
-    if (t + nw < ntiles && nidx < a.n)
-      load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
+      for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
+      const uint64_t nidx = (t + nw) * 64 + lane;
+      if (t + nw < ntiles && nidx < a.n)
+        load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
+    }
     uint64_t k[KW];
     extract_key<KW, NCH>(w, a.fp, k);
 #ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
@@ -278,7 +327,7 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   }
 }
 
-template <int KW, int NCH>
+template <int KW, int NCH, int PAIR>
 hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   const size_t lds = ((a.t.nbp * 4 + 15) & ~(size_t)15) + kMaxTuples * KW * 8 +
                      (size_t)kWaves * kWaveLds;
@@ -286,7 +335,7 @@ hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((wm_tags_kernel<KW, NCH>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((wm_tags_kernel<KW, NCH, PAIR>), dim3((unsigned)blocks),
                      dim3(kWmBlock), lds, s, a);
   return hipGetLastError();
 }
@@ -296,9 +345,13 @@ hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   const bool n2 = fits_nch2(a.fp);
   if (a.fp.direct || a.fp.nch > 4 || a.t.nbp > (1u << 15)) return hipErrorInvalidValue;
+  // the pair loads: dense 64 B slots whose window is two chunks inside the slot
+  const bool pair = n2 && a.stride == 64 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64;
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
-    return n2 ? launch_tags<KW, 2>(a, num_cus, s) : launch_tags<KW, 4>(a, num_cus, s);
+    return pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                     \
+                : n2 ? launch_tags<KW, 2, 0>(a, num_cus, s)                \
+                     : launch_tags<KW, 4, 0>(a, num_cus, s);
   BG_WT(1) BG_WT(2) BG_WT(4) BG_WT(8)
 #undef BG_WT
   return hipErrorInvalidValue;

@@ -252,11 +252,12 @@ def test_wm_module_kat(golden, dev):
 
 @pytest.mark.parametrize("n_rules,n_pkts,tags", [
     (64, 4096, 1), (5000, 65536, 1), (5000, 65536, 0), (100000, 131072, 1),
-    (100000, 131072, 0), (300000, 65536, 1)])
+    (100000, 131072, 0), (100000, 131051, 1), (100000, 45, 1), (300000, 65536, 1)])
 def test_wm_vs_oracle(n_rules, n_pkts, tags, dev):
     """tags 1: tables past the whole-table LDS size keep their tag words in
     LDS (bg_wm.hip) when they fit; 0 (BG_PATH_WM_NO_TAGS): the key-filter
-    path; 300 K rules: tags too big for LDS, the key-filter path either way"""
+    path; 300 K rules: tags too big for LDS, the key-filter path either way.
+    Ragged counts end in a partial tile (the 64 B slab's pair loads, bg_wm.hip)"""
     rk, rm, prio, gates, frames, _ = P.wm_workload(n_rules, n_pkts,
                                                   seed=n_rules, stride=64,
                                                   sizes=((60, 1),))
