@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""C5 ExactMatch (1 M rules, table in HBM/MALL, 16 M resident 64 B packets)
-timed through a given build of libbessgpu.so (argv[1]; default the product
-library). Run once per library in separate processes on one box to compare
+"""ExactMatch over 16 M resident 64 B packets -- C5 (1 M rules, table in
+HBM/MALL) or, with argv[2] = 1000, C2 (table in LDS) -- timed through a
+given build of libbessgpu.so (argv[1]; default the product library). Run once per library in separate processes on one box to compare
 kernel versions. Prints one JSON line with a checksum of the gates."""
 import json
 import os
@@ -21,7 +21,7 @@ from bess_amd import packets as P  # noqa: E402
 
 
 def main():
-    n, nr = 16 << 20, 1 << 20
+    n, nr = 16 << 20, int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     keys, gates, frames = P.em_workload(nr, n, seed=0xC5, pkt_seed=0xC55)
     d = torch.from_numpy(frames.reshape(-1)).cuda()
     del frames
@@ -43,7 +43,7 @@ def main():
     got = g.cpu().numpy().view(np.uint16)
     crc = int(np.bitwise_xor.reduce(got.astype(np.uint64) *
                                      np.arange(1, n + 1, dtype=np.uint64)))
-    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "c5_ms": round(best, 4),
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "rules": nr, "ms": round(best, 4),
                       "frac": round(66 * n / (best * 1e-3) / 8e12, 4), "gates_crc": crc}))
 
 
