@@ -74,6 +74,10 @@ def parse():
                     help="C4 layouts to time (PMC passes time one at a time)")
     ap.add_argument("--c5-rules", type=int, default=1 << 20,
                     help="rules of the sharded C5 table in the N > 1 line")
+    ap.add_argument("--no-churn", action="store_true",
+                    help="NAT: skip the new-flow batch stream (PMC passes)")
+    ap.add_argument("--lib", default="",
+                    help="time another build of libbessgpu.so (same-box A/B)")
     ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|pipe (profiling runs)")
     return ap.parse_args()
 
@@ -933,7 +937,10 @@ def run_dnat(args, dev, torch):
         cpu = cpu_baseline({1: rate}, 1, "%d 64B pkts x %d passes in snbuf "
                            "layout, established flows, 1 worker (one NAT map)"
                            % (cn, i))
+    del copies, src
+    churn = None if args.no_churn else dnat_new_flows(m, o, flows, t0 + 1000, dev, torch)
     return {"cpu_baseline": cpu,
+            "new_flows": churn,
             "workload": "NAT forward, established flows: 64B pkts (64B slots), "
                         "%d pkts per call over %d mappings" % (n, nflow),
             "pkts": n, "ms_per_step": round(ms, 4),
@@ -943,6 +950,53 @@ def run_dnat(args, dev, torch):
                     "4-byte miss count read back",
             "parity": "bit-exact (gates + frame bytes) vs oracle on %d pkts" % k
                       if parity else "MISMATCH"}
+
+
+def dnat_new_flows(m, o, flows, t0, dev, torch, nb=20, bn=1 << 16, frac=0.01):
+    """NAT with a steady rate of new flows: nb forward batches of bn 64 B
+    packets, `frac` of them from flows never seen before (each needs the
+    host's port search), the rest from the established mappings. Per call:
+    the fused pass, the new flows walked on the host in packet order, only
+    the changed map words and entries sent to the device, then their
+    packets stamped. Every batch checked against the oracle run on the same
+    sequence (gates and frame bytes)."""
+    from bess_amd import packets as P
+    rng = np.random.default_rng(29)
+    nnew = int(bn * frac)
+    batches = []
+    for b in range(nb):
+        x = flows[rng.integers(0, flows.shape[0], bn)].copy()
+        _, _, fresh = P.em_workload(16, nnew, seed=0x5EED, pkt_seed=1000 + b)
+        zero = (fresh[:, 34] == 0) & (fresh[:, 35] == 0)
+        fresh[zero, 35] = 1
+        x[rng.choice(bn, nnew, replace=False)] = fresh
+        batches.append(x)
+    d = [torch.from_numpy(x.reshape(-1).copy()).to(dev) for x in batches]
+    g = torch.empty(bn, dtype=torch.int16, device=dev)
+    outs = []
+    torch.cuda.synchronize()
+    ms = []
+    for b in range(nb):
+        t = time.perf_counter()
+        m.process_device(d[b], 64, bn, g, t0 + b)
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t) * 1e3)
+        outs.append((g.cpu().numpy().view(np.uint16).copy(), d[b].cpu().numpy()))
+    ok = True
+    for b in range(nb):
+        ref = batches[b].copy()
+        want = o.process(ref, 64, bn, 0, t0 + b)
+        ok &= bool((outs[b][0] == want).all() and (outs[b][1] == ref.reshape(-1)).all())
+    med = float(np.median(ms))
+    return {"workload": "%d batches of %d 64B pkts, %.0f%% new flows each "
+                        "(%d), the rest established; map grows from %d"
+                        % (nb, bn, frac * 100, nnew, flows.shape[0]),
+            "ms_per_batch_median": round(med, 4),
+            "ms_per_batch_max": round(max(ms), 4),
+            "Mpps": round(bn / (med * 1e-3) / 1e6, 1),
+            "timing": "host wall per synchronous call (fused pass, host walk of "
+                      "the new flows, word-level map update, stamp pass)",
+            "parity": "bit-exact vs oracle, all batches" if ok else "MISMATCH"}
 
 
 def run_wm(args, dev, torch):
@@ -1323,6 +1377,9 @@ def _free_port():
 
 def main():
     args = parse()
+    if args.lib:
+        from bess_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         # start the N ranks (one process per GPU) before anything touches a

@@ -243,7 +243,7 @@ TableRef DevTable::ref() const {
   t.nparts = L.nparts;
   t.nbp = L.nbp;
   t.kw = L.kw;
-  const uint64_t tb = filt_words ? filt_off : bytes;
+  const uint64_t tb = filt_words ? filt_off : aux_off ? aux_off : bytes;
   t.bytes_total = (uint32_t)std::min<uint64_t>(tb, 0xFFFFFFFFu);
   t.filt_words = filt_words;
   t.vik = L.vik;
@@ -887,6 +887,10 @@ struct bg_wm {
   std::atomic<bool> dirty{true};  // as bg_em::dirty
   bool built_no_tags = false;     // BG_PATH_WM_NO_TAGS when the image was built
   DevTable dev;
+  // direct tuples of the image (WmArgs::ndirect ...), set with it
+  uint32_t ndirect = 0;
+  uint32_t dtu[kMaxDirect] = {}, dspec[kMaxDirect] = {};
+  uint64_t doff[kMaxDirect] = {};
   std::mutex mu;
 };
 
@@ -1010,6 +1014,86 @@ static uint32_t wm_cover(const bg_wm *wm, size_t t) {
   return c;
 }
 
+// A tuple whose mask covers one or two key bytes can be a direct tuple
+// (WmArgs::ndirect): *spec = direct_index's byte positions and masks.
+static bool wm_direct_spec(const bg_wm *wm, size_t t, uint32_t *spec) {
+  const uint8_t *m = reinterpret_cast<const uint8_t *>(wm->tuples[t].mask.w);
+  uint32_t pos[2] = {0, 0}, msk[2] = {0, 0}, nb = 0;
+  for (uint32_t b = 0; b < 8 * wm->kw; b++) {
+    if (!m[b]) continue;
+    if (nb == 2) return false;
+    pos[nb] = b;
+    msk[nb++] = m[b];
+  }
+  if (nb == 0) return false;
+  if (nb == 1) pos[1] = pos[0];
+  *spec = pos[0] | pos[1] << 8 | msk[0] << 16 | msk[1] << 24;
+  return true;
+}
+
+// The direct tuples of a tag-word image: up to kMaxDirect tuples of one or
+// two mask bytes, one-byte masks first (their 2 KB tables stay in L2),
+// then the tuples with the most entries (each saves a hash, two tag reads
+// and its queue entries for every packet it matches).
+static void wm_pick_direct(bg_wm *wm) {
+  struct Cand {
+    bool two;  // two mask bytes
+    size_t n;  // entries
+    uint32_t t;
+  };
+  std::vector<Cand> cand;
+  for (size_t t = 0; t < wm->tuples.size(); t++) {
+    uint32_t spec;
+    if (!wm_direct_spec(wm, t, &spec) || wm->tuples[t].ht.empty()) continue;
+    cand.push_back({(spec >> 24) != 0, wm->tuples[t].ht.size(), (uint32_t)t});
+  }
+  std::sort(cand.begin(), cand.end(), [](const Cand &a, const Cand &b) {
+    if (a.two != b.two) return !a.two;
+    if (a.n != b.n) return a.n > b.n;
+    return a.t < b.t;
+  });
+  wm->ndirect = 0;
+  for (auto &c : cand) {
+    if (wm->ndirect == (uint32_t)kMaxDirect) break;
+    uint32_t spec = 0;
+    wm_direct_spec(wm, c.t, &spec);
+    wm->dtu[wm->ndirect] = c.t;
+    wm->dspec[wm->ndirect] = spec;
+    wm->ndirect++;
+  }
+  std::sort(wm->dtu, wm->dtu + wm->ndirect);  // specs follow their tuples
+  for (uint32_t d = 0; d < wm->ndirect; d++) wm_direct_spec(wm, wm->dtu[d], &wm->dspec[d]);
+}
+
+static bool wm_is_direct(const bg_wm *wm, size_t t) {
+  for (uint32_t d = 0; d < wm->ndirect; d++)
+    if (wm->dtu[d] == t) return true;
+  return false;
+}
+
+// the hashed table's entries (all tuples but the direct ones)
+static void wm_entries(const bg_wm *wm, std::vector<uint64_t> *keys,
+                       std::vector<uint8_t> *vals, std::vector<uint64_t> *hashes) {
+  keys->clear();
+  vals->clear();
+  hashes->clear();
+  for (size_t t = 0; t < wm->tuples.size(); t++) {
+    if (wm_is_direct(wm, t)) continue;
+    const uint32_t cover = wm_cover(wm, t);
+    const uint32_t seed = wm_seed32(tuple_seed(kDefaultSeed, (uint32_t)t));
+    for (auto &kv : wm->tuples[t].ht) {
+      keys->insert(keys->end(), kv.first.w, kv.first.w + wm->kw);
+      uint64_t v = (uint64_t)(uint32_t)kv.second.priority |
+                   ((uint64_t)kv.second.gate << 32) | ((uint64_t)t << 48);
+      for (int b = 0; b < 8; b++) vals->push_back((uint8_t)(v >> (8 * b)));
+      // the stored key is already masked: wm_hash of its dwords
+      uint32_t kd[2 * kMaxKeyWords];
+      memcpy(kd, kv.first.w, sizeof(kd));
+      hashes->push_back(wm_hash(kd, cover, 2 * (int)wm->kw, seed));
+    }
+  }
+}
+
 static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   const bool no_tags = wm_want_no_tags();
   if (!wm->dirty && wm->dev.valid && wm->dev.device == device &&
@@ -1017,29 +1101,22 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
     return 0;
   std::vector<uint64_t> keys, hashes;
   std::vector<uint8_t> vals, img;
-  for (size_t t = 0; t < wm->tuples.size(); t++) {
-    const uint32_t cover = wm_cover(wm, t);
-    const uint32_t seed = wm_seed32(tuple_seed(kDefaultSeed, (uint32_t)t));
-    for (auto &kv : wm->tuples[t].ht) {
-      keys.insert(keys.end(), kv.first.w, kv.first.w + wm->kw);
-      uint64_t v = (uint64_t)(uint32_t)kv.second.priority |
-                   ((uint64_t)kv.second.gate << 32) | ((uint64_t)t << 48);
-      for (int b = 0; b < 8; b++) vals.push_back((uint8_t)(v >> (8 * b)));
-      // the stored key is already masked: wm_hash of its dwords
-      uint32_t kd[2 * kMaxKeyWords];
-      memcpy(kd, kv.first.w, sizeof(kd));
-      hashes.push_back(wm_hash(kd, cover, 2 * (int)wm->kw, seed));
-    }
-  }
-  const size_t nkeys = hashes.size();
+  wm->ndirect = 0;
+  wm_entries(wm, &keys, &vals, &hashes);
   TableLayout L;
   int r = build_image(wm->kw, 8, 1, keys, vals, hashes, &img, &L, 0.75, false, 1);
   if (r) return r;
   // Past the whole-table LDS size, a table whose tag words fit LDS (at a
   // higher load factor if need be: the bucketized 2x4 cuckoo table inserts
-  // well past 0.9) keeps them there (bg_wm.hip) and needs no key filter.
+  // well past 0.9) keeps them there (bg_wm.hip) and needs no key filter;
+  // its one- and two-byte tuples become direct tuples (WmArgs::ndirect).
   bool tags_lds = false;
+  uint64_t aux_off = 0;
   if (img.size() > kLdsTableMax && !no_tags && knob("BG_WM_TAGS", 1)) {
+    if (knob("BG_WM_DIRECT", 1)) {
+      wm_pick_direct(wm);
+      wm_entries(wm, &keys, &vals, &hashes);
+    }
     for (double load : {0.75, 0.93}) {
       std::vector<uint8_t> img2;
       TableLayout L2;
@@ -1052,7 +1129,30 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
         break;
       }
     }
+    if (!tags_lds && wm->ndirect) {  // back to the full table
+      wm->ndirect = 0;
+      wm_entries(wm, &keys, &vals, &hashes);
+      r = build_image(wm->kw, 8, 1, keys, vals, hashes, &img, &L, 0.75, false, 1);
+      if (r) return r;
+    }
+    if (wm->ndirect) {  // the direct tables after the hashed image
+      aux_off = align256(img.size());
+      uint64_t off = aux_off;
+      for (uint32_t d = 0; d < wm->ndirect; d++) {
+        const size_t nent = (wm->dspec[d] >> 24) ? 65536 : 256;
+        wm->doff[d] = off;
+        img.resize(off + nent * 8, 0xFF);  // empty: all ones (tuple 0xFFFF)
+        uint64_t *tab = reinterpret_cast<uint64_t *>(img.data() + off);
+        const uint32_t t = wm->dtu[d];
+        for (auto &kv : wm->tuples[t].ht)
+          tab[direct_index(kv.first.w, wm->dspec[d])] =
+              (uint64_t)(uint32_t)kv.second.priority |
+              ((uint64_t)kv.second.gate << 32) | ((uint64_t)t << 48);
+        off = align256(off + nent * 8);
+      }
+    }
   }
+  const size_t nkeys = hashes.size();
   // Tables too big for LDS get a blocked Bloom filter (up to 16 bits per
   // key, 64 KB by default so two workgroups fit a CU -- measured faster
   // than 128 KB at one workgroup per CU) that the kernel stages in LDS.
@@ -1076,6 +1176,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   }
   r = wm->dev.upload(device, img, L, s);
   if (r) return r;
+  wm->dev.aux_off = aux_off;
   wm->dev.filt_off = foff;
   wm->dev.filt_words = fw;
   wm->dev.tags_lds = tags_lds;
@@ -1109,6 +1210,12 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
     for (uint32_t j = 0; j < wm->kw; j++) a.tmask[t][j] = wm->tuples[t].mask.w[j];
     a.tcover[t] = wm_cover(wm, t);
     a.tseed[t] = wm_seed32(tuple_seed(a.t.seed, (uint32_t)t));
+  }
+  a.ndirect = wm->ndirect;
+  for (uint32_t d = 0; d < wm->ndirect; d++) {
+    a.dtu[d] = wm->dtu[d];
+    a.dspec[d] = wm->dspec[d];
+    a.doff[d] = wm->doff[d];
   }
   a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
   HIP_TRY(launch_wm(a, num_cus(wm->dev.device), s));

@@ -260,6 +260,14 @@ __global__ __launch_bounds__(kNatBlock) void dnat_scatter_kernel(
   }
 }
 
+// the lookup-image words a host walk changed: img[up[i]] = up[k + i]
+__global__ __launch_bounds__(kNatBlock) void dnat_image_kernel(
+    const uint64_t *up, uint64_t k, uint64_t *img) {
+  const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < k; i += step)
+    img[up[i]] = up[k + i];
+}
+
 // any stride: lane = packet, header bytes straight from HBM
 __global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
   const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
@@ -334,6 +342,14 @@ hipError_t launch_dnat_scatter(const uint64_t *d_up, size_t k, uint64_t *ent,
   if (k == 0) return hipSuccess;
   hipLaunchKernelGGL(dnat_scatter_kernel, dim3((unsigned)grid_of(k, 256)),
                      dim3(kNatBlock), 0, s, d_up, (uint64_t)k, ent, ts);
+  return hipGetLastError();
+}
+
+hipError_t launch_dnat_image(const uint64_t *d_up, size_t k, uint64_t *img,
+                             hipStream_t s) {
+  if (k == 0) return hipSuccess;
+  hipLaunchKernelGGL(dnat_image_kernel, dim3((unsigned)grid_of(k, 256)),
+                     dim3(kNatBlock), 0, s, d_up, (uint64_t)k, img);
   return hipGetLastError();
 }
 

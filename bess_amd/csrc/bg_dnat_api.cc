@@ -73,6 +73,129 @@ bool parse_ipv4(const char *s, uint32_t *host) {  // ParseIpv4Address
   return true;
 }
 
+// Host mirror of the device lookup image, kept in step with the map so that
+// a batch that adds or evicts mappings sends the device only the 8-byte
+// words it changed (dnat_image_kernel) instead of a rebuilt image. Slot key
+// words as in bg_dnat.hip lookup_hit: the endpoint with the entry index's
+// top byte in bits 56-63, its translation with the index's low half in bits
+// 48-63. New keys go in by cuckoo insertion (the builder's placement rule:
+// a free slot of b1, then b2, then a random-walk eviction path); past the
+// load limit or an insertion failure the next sync rebuilds the image.
+struct ImageMirror {
+  std::vector<uint8_t> img;
+  TableLayout L{};
+  std::vector<uint64_t> occ;                   // per slot: endpoint or kFree
+  std::unordered_map<uint64_t, uint32_t> at;   // endpoint -> slot
+  std::vector<uint32_t> dirty;                 // changed 8-byte words
+  uint64_t rng = 0x9E3779B97F4A7C15ull;
+  bool valid = false;
+  static constexpr uint64_t kFree = ~0ull;
+  static constexpr double kMaxLoad = 0.9;
+
+  Probe probe(uint64_t key) const {
+    return split_hash(hash_words(&key, 1, L.seed), 1, L.nbp);
+  }
+  uint32_t *tags() { return reinterpret_cast<uint32_t *>(img.data()); }
+  uint64_t *kwords() { return reinterpret_cast<uint64_t *>(img.data() + L.keys_off); }
+  uint32_t *vals() { return reinterpret_cast<uint32_t *>(img.data() + L.vals_off); }
+  void mark(const void *p) {
+    dirty.push_back((uint32_t)((reinterpret_cast<const uint8_t *>(p) - img.data()) / 8));
+  }
+  // write (or clear, e = ~0u) one slot
+  void write_slot(uint32_t slot, uint64_t key, uint32_t e, uint64_t ep) {
+    const uint32_t b = slot / kSlots, sh = 8 * (slot % kSlots);
+    uint32_t &tw = tags()[b];
+    tw &= ~(0xFFu << sh);
+    uint64_t *kw = kwords() + (uint64_t)slot * 2;
+    if (e == ~0u) {
+      kw[0] = kw[1] = 0;
+      vals()[slot] = 0;
+      occ[slot] = kFree;
+    } else {
+      tw |= probe(key).tag << sh;
+      kw[0] = key | (uint64_t)(e >> 16) << 56;
+      kw[1] = (ep & 0xFFFFFFFFFFFFull) | (uint64_t)(e & 0xFFFF) << 48;
+      vals()[slot] = e;
+      occ[slot] = key;
+      at[key] = slot;
+    }
+    mark(&tw);
+    mark(kw);
+    mark(kw + 1);
+    mark(&vals()[slot]);
+  }
+  // after a full build: which slot holds which endpoint
+  void index(const std::vector<uint8_t> &image, const TableLayout &lay) {
+    img = image;
+    L = lay;
+    occ.assign((size_t)L.nbp * kSlots, kFree);
+    at.clear();
+    dirty.clear();
+    const uint64_t *kw = kwords();
+    for (uint32_t sl = 0; sl < occ.size(); sl++) {
+      if (!((tags()[sl / kSlots] >> (8 * (sl % kSlots))) & 0xFFu)) continue;
+      const uint64_t key = kw[(uint64_t)sl * 2] & 0x00FFFFFFFFFFFFFFull;
+      occ[sl] = key;
+      at[key] = sl;
+    }
+    valid = true;
+  }
+  // insert or update; false: the image must be rebuilt
+  bool put(uint64_t key, uint32_t e, uint64_t ep, const std::vector<uint64_t> &ent_ep) {
+    if (!valid) return false;
+    auto it = at.find(key);
+    if (it != at.end()) {
+      write_slot(it->second, key, e, ep);
+      return true;
+    }
+    if ((double)(at.size() + 1) > kMaxLoad * (double)occ.size()) return false;
+    uint64_t cur = key;
+    uint32_t ce = e;
+    uint64_t cep = ep;
+    Probe p = probe(cur);
+    for (uint32_t b : {p.b1, p.b2})
+      for (int s = 0; s < kSlots; s++)
+        if (occ[b * kSlots + s] == kFree) {
+          write_slot(b * kSlots + s, cur, ce, cep);
+          return true;
+        }
+    uint32_t bucket = (rng_next() & 1) ? p.b2 : p.b1;
+    for (int step = 0; step < 500; step++) {
+      for (int s = 0; s < kSlots; s++)
+        if (occ[bucket * kSlots + s] == kFree) {
+          write_slot(bucket * kSlots + s, cur, ce, cep);
+          return true;
+        }
+      const uint32_t slot = bucket * kSlots + (uint32_t)(rng_next() % kSlots);
+      const uint64_t vkey = occ[slot];
+      const uint32_t ve = vals()[slot];
+      at.erase(vkey);
+      write_slot(slot, cur, ce, cep);
+      cur = vkey;
+      ce = ve;
+      cep = ent_ep[ve];
+      const Probe q = probe(cur);
+      bucket = q.b1 == bucket ? q.b2 : q.b1;
+    }
+    valid = false;  // the displaced key has no slot: rebuild
+    return false;
+  }
+  void erase(uint64_t key) {
+    if (!valid) return;
+    auto it = at.find(key);
+    if (it == at.end()) return;
+    const uint32_t slot = it->second;
+    at.erase(it);
+    write_slot(slot, 0, ~0u, 0);
+  }
+  uint64_t rng_next() {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return rng;
+  }
+};
+
 }  // namespace
 
 struct bg_dnat {
@@ -89,6 +212,7 @@ struct bg_dnat {
   std::vector<uint32_t> free_idx;
   std::vector<uint32_t> changed;  // entries to push to the device
   bool map_dirty = true;          // the lookup image must be rebuilt
+  ImageMirror mirror;             // the image, for word-level updates
   int device = -1;
   hipStream_t walk_stream = nullptr;
   DevTable dev;
@@ -97,10 +221,12 @@ struct bg_dnat {
   uint64_t *d_keys = nullptr;
   uint32_t *d_res = nullptr, *d_nmiss = nullptr, *d_mres = nullptr;
   size_t d_n = 0;
+  uint64_t *d_up = nullptr;  // update lists (ensure_up)
+  size_t d_upcap = 0;
   std::mutex mu;
   ~bg_dnat() {
     for (void *p : {(void *)d_ent, (void *)d_ts, (void *)d_keys, (void *)d_res,
-                    (void *)d_nmiss, (void *)d_mres})
+                    (void *)d_nmiss, (void *)d_mres, (void *)d_up})
       if (p) (void)hipFree(p);
   }
 
@@ -109,7 +235,8 @@ struct bg_dnat {
     if (it != map.end()) {
       ent_ep[it->second] = ep;
       changed.push_back(it->second);
-      map_dirty = true;  // the image carries the translation
+      // the image carries the translation
+      if (!mirror.put(key, it->second, ep, ent_ep)) map_dirty = true;
       return it->second;
     }
     uint32_t idx;
@@ -127,7 +254,7 @@ struct bg_dnat {
     }
     map.emplace(key, idx);
     changed.push_back(idx);
-    map_dirty = true;
+    if (idx >= (1u << 24) || !mirror.put(key, idx, ep, ent_ep)) map_dirty = true;
     return idx;
   }
   void remove(uint64_t key) {
@@ -135,7 +262,7 @@ struct bg_dnat {
     if (it == map.end()) return;
     free_idx.push_back(it->second);
     map.erase(it);
-    map_dirty = true;
+    mirror.erase(key);
   }
   // now - last_refresh > kTimeOutNs (nat.cc:217, u64 arithmetic) with the
   // entry's current timestamp: a host value that says "expired" may be
@@ -216,6 +343,17 @@ struct bg_dnat {
     return -1;
   }
 
+  // the device buffer of a sync's update lists (grown, never shrunk: a
+  // hipMalloc + hipFree per batch cost more than the whole walk)
+  int ensure_up(size_t words) {
+    if (words <= d_upcap) return 0;
+    if (d_up) (void)hipFree(d_up);
+    d_up = nullptr;
+    d_upcap = std::max<size_t>(words * 2, 4096);
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_up), d_upcap * 8));
+    return 0;
+  }
+
   int ensure_batch(size_t n) {
     if (n <= d_n) return 0;
     for (void *p : {(void *)d_keys, (void *)d_res, (void *)d_mres})
@@ -255,7 +393,24 @@ struct bg_dnat {
       if (r) return r;
       r = dev.upload(dev_id, img, L, s);
       if (r) return r;
+      mirror.index(img, L);
       map_dirty = false;
+    } else if (!mirror.dirty.empty()) {  // the changed words only
+      std::vector<uint32_t> &w = mirror.dirty;
+      std::sort(w.begin(), w.end());
+      w.erase(std::unique(w.begin(), w.end()), w.end());
+      const size_t k = w.size();
+      std::vector<uint64_t> up(2 * k);  // word index | value
+      const uint64_t *src = reinterpret_cast<const uint64_t *>(mirror.img.data());
+      for (size_t i = 0; i < k; i++) {
+        up[i] = w[i];
+        up[k + i] = src[w[i]];
+      }
+      if (int e = ensure_up(up.size())) return e;
+      HIP_TRY(hipMemcpyAsync(d_up, up.data(), up.size() * 8, hipMemcpyHostToDevice, s));
+      HIP_TRY(launch_dnat_image(d_up, k, reinterpret_cast<uint64_t *>(dev.d_image), s));
+      HIP_TRY(hipStreamSynchronize(s));  // `up` is host memory
+      w.clear();
     }
     const size_t ne = std::max<size_t>(ent_ep.size(), 1);
     if (ne > d_cap) {
@@ -284,12 +439,10 @@ struct bg_dnat {
         up[k + i] = ent_ep[changed[i]];
         up[2 * k + i] = ent_ts[changed[i]];
       }
-      uint64_t *d_up = nullptr;
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_up), up.size() * 8));
+      if (int e = ensure_up(up.size())) return e;
       HIP_TRY(hipMemcpyAsync(d_up, up.data(), up.size() * 8, hipMemcpyHostToDevice, s));
       HIP_TRY(launch_dnat_scatter(d_up, k, d_ent, d_ts, s));
       HIP_TRY(hipStreamSynchronize(s));  // `up` is host memory
-      (void)hipFree(d_up);
       changed.clear();
     }
     device = dev_id;

@@ -66,6 +66,7 @@ struct DevTable {
   uint64_t filt_off = 0;    // key filter appended to the image (WM)
   uint32_t filt_words = 0;
   bool tags_lds = false;    // tag words staged in LDS (WM, bg_wm.hip)
+  uint64_t aux_off = 0;     // direct-tuple tables appended to the image (WM)
   int upload(int dev, const std::vector<uint8_t> &img, const TableLayout &lay,
              hipStream_t s);
   void release();

@@ -11,6 +11,7 @@ namespace bg {
 
 constexpr int kMaxFields = 8;
 constexpr int kMaxTuples = 8;
+constexpr int kMaxDirect = 2;  // direct tuples per WildcardMatch image (WmArgs)
 constexpr int kMaxWindowChunks = 4;      // 16-byte chunks staged per packet
 constexpr uint32_t kLdsTableMax = 40960;  // tables up to this size go to LDS
 constexpr uint16_t kGateNone = 0xFFFF;
@@ -98,6 +99,14 @@ struct EmArgs {
   TableRef t;
 };
 
+// a direct tuple's table index: the masked key bytes a and b (WmArgs::dspec)
+BG_HD uint32_t direct_index(const uint64_t *k, uint32_t spec) {
+  const uint32_t pa = spec & 63, pb = (spec >> 8) & 63;
+  const uint32_t ba = (uint32_t)(k[pa >> 3] >> ((pa & 7) * 8)) & (spec >> 16) & 0xFFu;
+  const uint32_t bb = (uint32_t)(k[pb >> 3] >> ((pb & 7) * 8)) & (spec >> 24) & 0xFFu;
+  return ba | bb << 8;
+}
+
 struct WmArgs {
   const uint8_t *frames;
   uint64_t stride, n;
@@ -108,6 +117,15 @@ struct WmArgs {
   uint64_t tmask[kMaxTuples][kMaxKeyWords];
   uint32_t tcover[kMaxTuples];  // per tuple: the dwords wm_hash covers
   uint32_t tseed[kMaxTuples];   // per tuple: wm_seed32(tuple_seed(seed, tu))
+  // Direct tuples (tag-word images only, <= kMaxDirect): a tuple whose mask
+  // covers one or two key bytes is not in the hashed table; its entries sit
+  // in a table indexed by those masked bytes (256 or 65536 values of the
+  // hashed table's format, empty = all ones), one read per packet, no hash,
+  // no fingerprint, no key compare.
+  uint32_t ndirect;
+  uint32_t dtu[kMaxDirect];    // tuple index
+  uint32_t dspec[kMaxDirect];  // key byte a | byte b << 8 | mask a << 16 | mask b << 24
+  uint64_t doff[kMaxDirect];   // the table's byte offset in the image
   uint32_t ab_phase, pad2;  // A/B build only: stop after a phase (timing)
 };
 
@@ -296,6 +314,8 @@ hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_encap(const EncapArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_dnat_image(const uint64_t *d_up, size_t k, uint64_t *img,
+                             hipStream_t s);
 // lookup + stamp of the final hits in one pass; forward misses and forward
 // hits on expired mappings listed in res/keys (count in *nmiss)
 hipError_t launch_dnat_fused(const DnatArgs &a, int num_cus, hipStream_t s);

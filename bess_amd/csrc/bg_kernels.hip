@@ -553,12 +553,19 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
   uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples];
   uint32_t w1[kMaxTuples], w2[kMaxTuples];
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
+  uint64_t dv[kMaxDirect];  // direct tuples' values (global, issued first)
+#pragma unroll
+  for (int d = 0; d < kMaxDirect; d++) {
+    dv[d] = ~0ull;
+    if ((uint32_t)d < a.ndirect)
+      dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + a.doff[d])[direct_index_k<KW>(k, a.dspec[d])];
+  }
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
     b1[tu] = b2[tu] = 0;
     tg[tu] = 1;  // fingerprints are never 0, so empty (0) tag words never match
     w1[tu] = w2[tu] = 0;
-    if (tu < (int)a.ntuples) {
+    if (tu < (int)a.ntuples && direct_of(a, tu) < 0) {
       const uint32_t h = wm_tuple_hash<KW>(k, tm, tu, a);
       bool pass = true;
       if (FILT) {
@@ -580,7 +587,17 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
   const uint64_t *vals = reinterpret_cast<const uint64_t *>(tab + a.t.vals_off);
 #pragma unroll
   for (int tu = 0; tu < kMaxTuples; tu++) {
-    if (tu < (int)a.ntuples) {
+    const int d = direct_of(a, tu);
+    if (d >= 0) {  // direct tuple: its value or empty
+#pragma unroll
+      for (int e = 0; e < kMaxDirect; e++) {
+        const uint64_t v = dv[e];
+        if (e == d && (uint32_t)(v >> 48) == (uint32_t)tu && (int32_t)(uint32_t)v >= best) {
+          best = (int32_t)(uint32_t)v;
+          gate = (uint32_t)(v >> 32) & 0xFFFFu;
+        }
+      }
+    } else if (tu < (int)a.ntuples) {
       uint32_t cand = tag_match(w1[tu], tg[tu]) | (tag_match(w2[tu], tg[tu]) << 4);
       if (cand) {
         uint64_t km[KW];

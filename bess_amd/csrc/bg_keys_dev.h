@@ -85,6 +85,32 @@ __device__ __forceinline__ uint32_t wm_tuple_hash(const uint64_t (&k)[KW],
   return h;
 }
 
+// direct_index (bg_kernels.h) over a key held in registers: the key words
+// are picked with selects on the uniform byte positions (no register-array
+// indexing)
+template <int KW>
+__device__ __forceinline__ uint32_t direct_index_k(const uint64_t (&k)[KW], uint32_t spec) {
+  const uint32_t pa = spec & 63, pb = (spec >> 8) & 63;
+  uint64_t wa = 0, wb = 0;
+#pragma unroll
+  for (int j = 0; j < KW; j++) {
+    if ((uint32_t)j == pa >> 3) wa = k[j];
+    if ((uint32_t)j == pb >> 3) wb = k[j];
+  }
+  const uint32_t ba = (uint32_t)(wa >> ((pa & 7) * 8)) & (spec >> 16) & 0xFFu;
+  const uint32_t bb = (uint32_t)(wb >> ((pb & 7) * 8)) & (spec >> 24) & 0xFFu;
+  return ba | bb << 8;
+}
+
+// the direct-tuple slot of tuple tu (WmArgs::ndirect), or -1 (uniform)
+__device__ __forceinline__ int direct_of(const WmArgs &a, int tu) {
+  int r = -1;
+#pragma unroll
+  for (int d = 0; d < kMaxDirect; d++)
+    if ((uint32_t)d < a.ndirect && a.dtu[d] == (uint32_t)tu) r = d;
+  return r;
+}
+
 __device__ __forceinline__ void lds_fence() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }

@@ -263,6 +263,21 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
     }
     uint64_t k[KW];
     extract_key<KW, NCH>(w, a.fp, k);
+    // direct tuples: one value read each, issued now, folded at the end
+    const kconst_u32 dtu = tuple_words(a, offsetof(WmArgs, dtu));
+    const uint32_t ndir = tuple_words(a, offsetof(WmArgs, ndirect))[0];
+    uint64_t dv[kMaxDirect];
+#pragma unroll
+    for (int d = 0; d < kMaxDirect; d++) {
+      dv[d] = ~0ull;
+      if ((uint32_t)d < ndir && live) {
+        const uint32_t spec = tuple_words(a, offsetof(WmArgs, dspec))[d];
+        const uint64_t off =
+            reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
+                tuple_words(a, offsetof(WmArgs, doff)))[d];
+        dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)[direct_index_k<KW>(k, spec)];
+      }
+    }
 #ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
     if (a.ab_phase == 1) {
       if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
@@ -279,7 +294,10 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
       b[2 * tu] = b[2 * tu + 1] = 0;
       c[2 * tu] = c[2 * tu + 1] = 0xFFFFFFFFu;  // no zero byte: no match
       et[tu] = 0;
-      if (tu < ntu) {
+      bool direct = false;
+#pragma unroll
+      for (int d = 0; d < kMaxDirect; d++) direct |= (uint32_t)d < ndir && dtu[d] == (uint32_t)tu;
+      if (tu < ntu && !direct) {
         const Probe p = wm_probe(wm_tuple_hash<KW>(k, tm, tu, a), lg);
         b[2 * tu] = p.b1;
         b[2 * tu + 1] = p.b2;
@@ -321,8 +339,17 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
       if (total <= r0 + kQueue) break;
     }
     lds_fence();
-    const uint64_t bb = best[lane];
+    uint64_t bb = best[lane];
     best[lane] = 0;
+#pragma unroll
+    for (int d = 0; d < kMaxDirect; d++) {
+      const uint32_t tu = (uint32_t)d < ndir ? dtu[d] : 0xFFFFu;
+      if ((uint32_t)(dv[d] >> 48) == tu) {  // same order as wm_fold
+        const uint64_t comb = ((uint64_t)((uint32_t)dv[d] ^ 0x80000000u) << 32) |
+                              (1u << 19) | (tu << 16) | ((uint32_t)(dv[d] >> 32) & 0xFFFFu);
+        bb = comb > bb ? comb : bb;
+      }
+    }
     if (live) a.gates[idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
   }
 }

@@ -38,6 +38,7 @@ if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
         em) ARGS="--no-extra --no-cpu --steps 3 --warmup 1" ;;
         wm) ARGS="--only wm --wm-layout slab --no-cpu --steps 3 --warmup 1" ;;
         wm2k) ARGS="--only wm --wm-layout 2k --no-cpu --steps 3 --warmup 1" ;;
+        dnat) ARGS="--only dnat --no-churn --no-cpu --steps 3 --warmup 1" ;;
         *) ARGS="--only $W --no-cpu --steps 3 --warmup 1" ;;
       esac
       step pmc_${W}_$i 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${W}_$i" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS
