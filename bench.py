@@ -1084,6 +1084,7 @@ def run_wm(args, dev, torch):
            "table_in_lds": {0: "no (L2/MALL)", 1: "whole table",
                             2: "key filter (table in L2/MALL)",
                             3: "tag words (keys/values in L2/MALL)"}[int(in_lds)],
+           "direct_tuples": t.direct_tuples(),
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),

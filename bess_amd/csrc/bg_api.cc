@@ -1300,7 +1300,8 @@ void bg_wm_window(const bg_wm *wm, int *lo, int *hi) {
 int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds) {
   if (!wm->dev.valid) return fail(EINVAL, "no device table yet");
   *bytes = wm->dev.bytes;
-  *in_lds = (int)wm->dev.ref().lds;  // 2: key filter in LDS
+  // 2: key filter in LDS, 3: tag words in LDS; bits 8+: direct tuples
+  *in_lds = (int)wm->dev.ref().lds | (int)(wm->ndirect << 8);
   return 0;
 }
 

@@ -224,7 +224,14 @@ class WmTable:
     def table_info(self):
         b, l = C.c_uint64(), C.c_int()
         check(lib().bg_wm_table_info(self.h, C.byref(b), C.byref(l)))
-        return b.value, l.value  # 0 L2/MALL, 1 table in LDS, 2 key filter in LDS
+        # 0 L2/MALL, 1 table in LDS, 2 key filter in LDS, 3 tag words in LDS
+        return b.value, l.value & 0xFF
+
+    def direct_tuples(self):
+        """tuples of the device image read by index (one- or two-byte masks)"""
+        b, l = C.c_uint64(), C.c_int()
+        check(lib().bg_wm_table_info(self.h, C.byref(b), C.byref(l)))
+        return l.value >> 8
 
 
 def cksum(frames, stride, n, mode, verify, ip_gates=None, l4_gates=None,

@@ -169,7 +169,9 @@ int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
 int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
                        uint16_t default_gate, uint16_t *gates,
                        bg_stream_t stream);
-/* in_lds: 0 table probed in L2/MALL, 1 table in LDS, 2 key filter in LDS */
+/* in_lds: 0 table probed in L2/MALL, 1 table in LDS, 2 key filter in LDS,
+ * 3 tag words in LDS; bits 8 and up: the image's direct tuples (one- or
+ * two-byte masks read by index, not hashed) */
 int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds);
 int bg_wm_classify_window(bg_wm *wm, const void *d_win, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,

@@ -277,6 +277,47 @@ def test_wm_vs_oracle(n_rules, n_pkts, tags, dev):
     assert (want != 77).mean() > 0.3
 
 
+def test_wm_direct_tuples_vs_oracle(dev):
+    """Tuples whose masks cover one or two key bytes -- whole and partial
+    bytes -- are direct tuples of the tag-word image (bg_wm.hip, WmArgs::
+    ndirect; two at most, the rest hashed), mixed with hashed tuples under
+    frequent priority ties; then a third of the direct tuples' rules are
+    deleted and the image resynced. Every table path, against the oracle."""
+    masks = [P._m(proto=0x0F), P._m(sport=0xFF00), P._m(dip=0xFF000000),
+             P._m(dport=0xFFF0), P._m(sip=0xFFFFFFFF, dport=0xFFFF),
+             P._m(sip=0xFFFF0000, dip=0xFFFF0000), P._m(sport=0xFFFF)]
+    n = 65536
+    rk, rm, prio, gates, frames, _ = P.wm_workload(60000, n, seed=77, stride=64,
+                                                  sizes=((60, 1),), prio_range=20,
+                                                  masks=masks)
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    d_frames = to_dev(frames, dev)
+
+    def check(keep):
+        got = classify_all_paths_wm(t, d_frames, 64, n, 77, dev, 1)
+        wm = oracle_wm(P.FIVE_TUPLE, rk[keep], rm[keep], prio[keep], gates[keep])
+        want = np.zeros(n, np.uint16)
+        O.lib().or_wm_process(wm, frames.ctypes.data, 64, n, 77, want.ctypes.data)
+        O.lib().or_wm_free(wm)
+        assert (got == want).all()
+        return want
+
+    want = check(np.ones(len(rk), bool))
+    assert t.table_info()[1] == 3 and t.direct_tuples() == 2
+    assert (want != 77).mean() > 0.5
+    # delete a third of the one- and two-byte tuples' (mask, key) entries
+    rng = np.random.default_rng(5)
+    few = np.array([np.count_nonzero(m) <= 2 for m in rm])
+    pairs = {(k.tobytes(), m.tobytes()) for k, m in zip(rk[few], rm[few])}
+    gone = {x for x in pairs if rng.random() < 1 / 3}
+    for k, m in gone:
+        t.delete(k, m)
+    keep = np.array([(k.tobytes(), m.tobytes()) not in gone for k, m in zip(rk, rm)])
+    check(keep)
+
+
 @pytest.mark.parametrize("filler", [0, 5000])
 def test_wm_priority_ties(dev, filler):
     """filler: extra rules in the third tuple make the table too big for
