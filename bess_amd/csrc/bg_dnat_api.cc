@@ -211,11 +211,15 @@ struct bg_dnat {
   uint32_t walk = 1;
   std::vector<uint32_t> free_idx;
   std::vector<uint32_t> changed;  // entries to push to the device
-  bool map_dirty = true;          // the lookup image must be rebuilt
-  ImageMirror mirror;             // the image, for word-level updates
+  bool map_dirty = true;          // the lookup images must be rebuilt
+  // Two lookup images -- forward entries (internal endpoint -> external)
+  // and reverse entries -- since a batch has one direction: its lookups
+  // touch half the keys (half the L2 footprint of one combined table)
+  std::vector<uint8_t> ent_rev;   // per entry: 1 = reverse entry
+  DevTable tab[2];
+  ImageMirror mirror[2];          // the images, for word-level updates
   int device = -1;
   hipStream_t walk_stream = nullptr;
-  DevTable dev;
   uint64_t *d_ent = nullptr, *d_ts = nullptr;
   size_t d_cap = 0;  // entries the device arrays hold
   uint64_t *d_keys = nullptr;
@@ -230,13 +234,18 @@ struct bg_dnat {
       if (p) (void)hipFree(p);
   }
 
-  uint32_t insert(uint64_t key, uint64_t ep) {  // HashTable::Insert
+  // HashTable::Insert; rev: a reverse entry (external endpoint -> internal)
+  uint32_t insert(uint64_t key, uint64_t ep, bool rev) {
     auto it = map.find(key);
     if (it != map.end()) {
       ent_ep[it->second] = ep;
       changed.push_back(it->second);
       // the image carries the translation
-      if (!mirror.put(key, it->second, ep, ent_ep)) map_dirty = true;
+      if (ent_rev[it->second] != rev) {  // the key changes direction
+        mirror[ent_rev[it->second]].erase(key);
+        ent_rev[it->second] = rev;
+      }
+      if (!mirror[rev].put(key, it->second, ep, ent_ep)) map_dirty = true;
       return it->second;
     }
     uint32_t idx;
@@ -246,23 +255,25 @@ struct bg_dnat {
       ent_ep[idx] = ep;
       ent_ts[idx] = 0;
       exact_walk[idx] = walk;
+      ent_rev[idx] = rev;
     } else {
       idx = (uint32_t)ent_ep.size();
       ent_ep.push_back(ep);
       ent_ts.push_back(0);
       exact_walk.push_back(walk);
+      ent_rev.push_back(rev);
     }
     map.emplace(key, idx);
     changed.push_back(idx);
-    if (idx >= (1u << 24) || !mirror.put(key, idx, ep, ent_ep)) map_dirty = true;
+    if (idx >= (1u << 24) || !mirror[rev].put(key, idx, ep, ent_ep)) map_dirty = true;
     return idx;
   }
   void remove(uint64_t key) {
     auto it = map.find(key);
     if (it == map.end()) return;
     free_idx.push_back(it->second);
+    mirror[ent_rev[it->second]].erase(key);
     map.erase(it);
-    mirror.erase(key);
   }
   // now - last_refresh > kTimeOutNs (nat.cc:217, u64 arithmetic) with the
   // entry's current timestamp: a host value that says "expired" may be
@@ -332,8 +343,8 @@ struct bg_dnat {
           }
         }
         if (take) {
-          insert(ext_ep, in);
-          return insert(in, ext_ep);
+          insert(ext_ep, in, true);
+          return insert(in, ext_ep, false);
         }
         port++;
         trials++;
@@ -375,40 +386,45 @@ struct bg_dnat {
     if (r) return r;
     if (device != dev_id && device >= 0)
       return fail(EINVAL, "NAT map bound to device %d", device);
-    if (map_dirty || !dev.valid) {
-      std::vector<uint64_t> keys, hashes;
-      std::vector<uint8_t> vals, img;
+    if (map_dirty || !tab[0].valid || !tab[1].valid) {
       if (ent_ep.size() > (1u << 24))
         return fail(ENOSPC, "NAT map past 2^24 entries");
-      for (auto &kv : map) {  // key words: the endpoint, its translation,
-        // the entry index in their spare top bits (bg_dnat.hip lookup_hit)
-        const uint64_t e = kv.second;
-        keys.push_back(kv.first | (e >> 16) << 56);
-        keys.push_back((ent_ep[e] & 0xFFFFFFFFFFFFull) | (e & 0xFFFF) << 48);
-        hashes.push_back(hash_words(&kv.first, 1, kDefaultSeed));
-        for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(e >> (8 * b)));
+      for (int rev = 0; rev < 2; rev++) {  // forward, reverse
+        std::vector<uint64_t> keys, hashes;
+        std::vector<uint8_t> vals, img;
+        for (auto &kv : map) {  // key words: the endpoint, its translation,
+          // the entry index in their spare top bits (bg_dnat.hip lookup_hit)
+          const uint64_t e = kv.second;
+          if (ent_rev[e] != rev) continue;
+          keys.push_back(kv.first | (e >> 16) << 56);
+          keys.push_back((ent_ep[e] & 0xFFFFFFFFFFFFull) | (e & 0xFFFF) << 48);
+          hashes.push_back(hash_words(&kv.first, 1, kDefaultSeed));
+          for (int b = 0; b < 4; b++) vals.push_back((uint8_t)(e >> (8 * b)));
+        }
+        TableLayout L;
+        r = build_image(2, 4, 1, keys, vals, hashes, &img, &L);
+        if (r) return r;
+        r = tab[rev].upload(dev_id, img, L, s);
+        if (r) return r;
+        mirror[rev].index(img, L);
       }
-      TableLayout L;
-      r = build_image(2, 4, 1, keys, vals, hashes, &img, &L);
-      if (r) return r;
-      r = dev.upload(dev_id, img, L, s);
-      if (r) return r;
-      mirror.index(img, L);
       map_dirty = false;
-    } else if (!mirror.dirty.empty()) {  // the changed words only
-      std::vector<uint32_t> &w = mirror.dirty;
+    }
+    for (int rev = 0; rev < 2; rev++) {
+      if (mirror[rev].dirty.empty()) continue;  // the changed words only
+      std::vector<uint32_t> &w = mirror[rev].dirty;
       std::sort(w.begin(), w.end());
       w.erase(std::unique(w.begin(), w.end()), w.end());
       const size_t k = w.size();
       std::vector<uint64_t> up(2 * k);  // word index | value
-      const uint64_t *src = reinterpret_cast<const uint64_t *>(mirror.img.data());
+      const uint64_t *src = reinterpret_cast<const uint64_t *>(mirror[rev].img.data());
       for (size_t i = 0; i < k; i++) {
         up[i] = w[i];
         up[k + i] = src[w[i]];
       }
       if (int e = ensure_up(up.size())) return e;
       HIP_TRY(hipMemcpyAsync(d_up, up.data(), up.size() * 8, hipMemcpyHostToDevice, s));
-      HIP_TRY(launch_dnat_image(d_up, k, reinterpret_cast<uint64_t *>(dev.d_image), s));
+      HIP_TRY(launch_dnat_image(d_up, k, reinterpret_cast<uint64_t *>(tab[rev].d_image), s));
       HIP_TRY(hipStreamSynchronize(s));  // `up` is host memory
       w.clear();
     }
@@ -514,7 +530,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.dir = (uint32_t)dir;
   a.now = now;
   a.timeout = kTimeOutNs;
-  a.t = h->dev.ref();
+  a.t = h->tab[dir].ref();
   a.keys = h->d_keys;
   a.res = h->d_res;
   a.nmiss = h->d_nmiss;
@@ -563,7 +579,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   HIP_TRY(hipMemcpyAsync(h->d_res, sidx.data(), nlist * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->d_keys, skey.data(), nlist * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->d_mres, ent.data(), nlist * 4, hipMemcpyHostToDevice, s));
-  a.t = h->dev.ref();
+  a.t = h->tab[dir].ref();
   a.ent = h->d_ent;
   a.ts = h->d_ts;
   a.nent = h->ent_ep.size();
