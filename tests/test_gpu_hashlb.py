@@ -78,11 +78,14 @@ FIELDSETS = [
 ]
 
 
-@pytest.mark.parametrize("fi", range(len(FIELDSETS)))
-def test_fields_vs_oracle(fi):
+@pytest.mark.parametrize("fi,stride", [(fi, 1040 if fi == 3 else 128)
+                                       for fi in range(len(FIELDSETS))] +
+                         [(0, 64), (1, 64), (2, 64), (4, 64)])
+def test_fields_vs_oracle(fi, stride):
+    """hlb_fields_kernel at slot strides 64 (a ragged last tile), 128 and
+    1040 (fields too far apart for one window)"""
     fl = FIELDSETS[fi]
-    stride = 1040 if fi == 3 else 128
-    f = frames(8000, stride, seed=10 + fi)
+    f = frames(8001, stride, seed=10 + fi)
     g = list(range(37))
     m = HashLB(gates=g, fields=fl)
     o = OM.OracleHashLB(gates=g, fields=fl)
