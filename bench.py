@@ -580,6 +580,36 @@ def run_e2e_pipe(args, torch):
         em["Mpps_by_threads_batch%d" % batch] = rates
     out["ExactMatch_64B"] = em
     del snb
+    # WildcardMatch, C4 rules (100 K over 8 masks), IMIX frames: the heavier
+    # classifier, where the device's per-packet work outweighs the gather
+    # (compare the C4 entry's cpu_baseline on the same cores)
+    from bess_amd.modules import WildcardMatch
+    n = 1 << 18
+    rk, rm, prio, wg, wf, _ = P.wm_workload(100000, n, stride=2048)
+    mw = WildcardMatch(fields=fields)
+    ow = O.OracleWildcardMatch(fields=fields)
+    for k, mk, pr, g in zip(rk, rm, prio, wg):
+        kb, mb = k.tobytes(), mk.tobytes()
+        kw = dict(gate=int(g), priority=int(pr),
+                  values=[{"value_bin": kb[a:c]} for a, c in cut],
+                  masks=[{"value_bin": mb[a:c]} for a, c in cut])
+        mw.add(**kw)
+        ow.add(**kw)
+    want = ow.process(wf, 2048, n)
+    snb = np.zeros((n, 2624), np.uint8)
+    snb[:, 512:512 + 2048] = wf
+    del wf
+    heads = snb.ctypes.data + 512 + 2624 * np.arange(n, dtype=np.uintp)
+    p = Pipe(mw, batch=65536, depth=4)
+    wmr = {"parity": bool((p.run(heads) == want).all())}
+    p.close()
+    rates = {}
+    for th in [int(x) for x in args.pipe_threads.split(",")]:
+        rates[str(th)] = _pipe_rate(lambda: Pipe(mw, batch=65536, depth=4), heads,
+                                    None, th, reps=4)
+    wmr["Mpps_by_threads_batch65536"] = rates
+    out["WildcardMatch_IMIX_100K"] = wmr
+    del snb
     # L4Checksum (recompute), 1500 B packets: frames H2D, header lines back
     n = 1 << 17
     cf = P.cksum_workload(n, frame_len=1496)
