@@ -1,11 +1,15 @@
-"""BASELINE configs C4 and C5 at their own sizes through the HIP path,
-bit-exact against the oracle; the drop-in module path under concurrent
-workers; EmitPacket's per-gate batches and drops (core/module.h:534-618).
+"""BASELINE configs at their own sizes through the HIP path, bit-exact
+against the oracle; the drop-in module path under concurrent workers;
+EmitPacket's per-gate batches and drops (core/module.h:534-618).
 
+  C2: 1K-rule 5-tuple ExactMatch over the bench's 16,777,216 64 B packets;
+  C3: IPChecksum -> L4Checksum over 1,048,576 1500 B frames in 2 KB slots,
+      every byte of every frame compared;
   C5: 1,048,576-rule 5-tuple ExactMatch (table in HBM/MALL), as one image
       and as 8 partitions attached as one image (the multi-GPU build);
   C4: 100K-rule WildcardMatch over 8 masks on IMIX frames in 2 KB slots
-      (tag words in LDS, and the key-filter path).
+      (tag words in LDS, and the key-filter path), and the bench's 8 M
+      header-slab packets.
 """
 import threading
 
@@ -53,6 +57,39 @@ def c5():
     want = oracle_em_gates(keys, gates, frames, 64)
     assert 0.4 < (want != 8192).mean() < 0.6
     return keys, gates, frames, want
+
+
+# ------------------------------------------------------------------- C2
+def test_c2_full_size():
+    """the bench's C2 workload, all 16 M gates"""
+    n = 16 << 20
+    keys, gates, frames = P.em_workload(1000, n, seed=0x5EED)
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
+    t.classify(to_dev(frames), 64, n, 8192, d_g)
+    torch.cuda.synchronize()
+    assert t.table_info()[1] == 1  # table in LDS
+    want = oracle_em_gates(keys, gates, frames, 64)
+    assert (d_g.cpu().numpy().view(np.uint16) == want).all()
+    assert 0.4 < (want != 8192).mean() < 0.6
+
+
+# ------------------------------------------------------------------- C3
+def test_c3_full_size():
+    """1 M 1500 B frames, IPChecksum -> L4Checksum recompute in one pass:
+    both gate arrays and every frame byte"""
+    n = 1 << 20
+    cf = P.cksum_workload(n, frame_len=1496)
+    d = to_dev(cf)
+    ipg = torch.zeros(n, dtype=torch.int16, device="cuda")
+    l4g = torch.zeros(n, dtype=torch.int16, device="cuda")
+    F.cksum(d, 2048, n, 3, False, ipg, l4g)
+    torch.cuda.synchronize()
+    wip, wl4 = O.cksum_process(cf, 2048, n, 3, False)  # in place on the host copy
+    assert (ipg.cpu().numpy().view(np.uint16) == wip).all()
+    assert (l4g.cpu().numpy().view(np.uint16) == wl4).all()
+    assert (d.cpu().numpy() == cf.reshape(-1)).all()
 
 
 # ------------------------------------------------------------------- C5
@@ -127,6 +164,37 @@ def test_c4_imix_2k_slots(flags):
     L.or_wm_free(ow)
     assert (d_g.cpu().numpy().view(np.uint16) == want).all()
     assert (want != 8192).mean() > 0.3
+
+
+def test_c4_header_slab_full_size():
+    """the bench's C4 slab: 1 M IMIX frames' header lines, 8 copies (8 M
+    packets), against the oracle on the frames themselves"""
+    n0, rep = 1 << 20, 8
+    rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n0, stride=2048)
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    L = O.lib()
+    ow = L.or_wm_new()
+    for off, size in P.FIVE_TUPLE:
+        L.or_wm_add_field(ow, off, size, None, 0)
+    L.or_wm_init_done(ow)
+    kb = np.zeros(64, np.uint8)
+    mb = np.zeros(64, np.uint8)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        kb[:16] = k
+        mb[:16] = m
+        assert L.or_wm_add(ow, kb.ctypes.data, mb.ctypes.data, int(p), int(g)) == 0
+    want = np.zeros(n0, np.uint16)
+    L.or_wm_process(ow, frames.ctypes.data, 2048, n0, 8192, want.ctypes.data)
+    L.or_wm_free(ow)
+    h = to_dev(np.ascontiguousarray(frames[:, :64])).repeat(rep)
+    del frames
+    d_g = torch.zeros(n0 * rep, dtype=torch.int16, device="cuda")
+    t.classify(h, 64, n0 * rep, 8192, d_g)
+    torch.cuda.synchronize()
+    assert t.table_info()[1] == 3 and t.direct_tuples() == 2
+    assert (d_g.cpu().numpy().view(np.uint16).reshape(rep, n0) == want).all()
 
 
 # ------------------------------------------- concurrent workers, one module
