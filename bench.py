@@ -78,7 +78,7 @@ def parse():
                     help="NAT: skip the new-flow batch stream (PMC passes)")
     ap.add_argument("--lib", default="",
                     help="time another build of libbessgpu.so (same-box A/B)")
-    ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|pipe (profiling runs)")
+    ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|rewrite|pipe (profiling runs)")
     return ap.parse_args()
 
 
@@ -847,6 +847,56 @@ def run_update_ttl(args, dev, torch):
     return out
 
 
+def run_rewrite(args, dev, torch):
+    """Rewrite (core/modules/rewrite.cc) over 16M packet slots: 4 templates
+    of 60 B (the Source -> Rewrite front of a BESS pipeline), round robin;
+    slots of 192 B (128 B headroom + data). Bytes/pkt: the 64 B the
+    reference's 32-byte-block copy writes + data_off (2 B) + length (4 B) =
+    70, all writes."""
+    from bess_amd import packets as P
+    from bess_amd.modules import Rewrite
+    from oracle import oracle_more as OM
+    n, stride = args.pkts, 192
+    _, _, fr = P.em_workload(4, 4, seed=0x5EED, pkt_seed=3)
+    ts = [fr[i, :60].tobytes() for i in range(4)]
+    m, o = Rewrite(templates=ts), OM.OracleRewrite(ts)
+    d = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    dh = torch.zeros(n, dtype=torch.int16, device=dev)
+    dl = torch.zeros(n, dtype=torch.int32, device=dev)
+    k = min(n, 1 << 18)
+    m.process_device(d, stride, k, dh, dl)
+    torch.cuda.synchronize()
+    ref = np.zeros((k, stride), np.uint8)
+    oh, ol = np.zeros(k, np.uint16), np.zeros(k, np.uint32)
+    o.process(ref, stride, k, oh, ol)
+    parity = bool((d[:k * stride].cpu().numpy().reshape(k, stride) == ref).all() and
+                  (dh[:k].cpu().numpy().view(np.uint16) == oh).all() and
+                  (dl[:k].cpu().numpy().view(np.uint32) == ol).all())
+    ms = _time_steps(lambda: m.process_device(d, stride, n, dh, dl), args, torch)
+    out = {"workload": "Rewrite: 4 templates of 60B round robin into %d resident "
+                       "192B packet slots" % n, "pkts": n, "ms_per_step": round(ms, 4),
+           "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+           "roofline": _roof(70, n, ms),
+           "parity": "bit-exact (slots, data_off, lengths) vs oracle on %d pkts" % k
+                     if parity else "MISMATCH"}
+    if not args.no_cpu:
+        cn = 1 << 18
+        snb = np.zeros((cn, 2624), np.uint8)
+        hh, ll = np.zeros(cn, np.uint16), np.zeros(cn, np.uint32)
+        busy, done, i = 0.0, 0, 0
+        while busy < args.cpu_seconds / 3 or i < 2:
+            t0 = time.perf_counter()
+            OM.mlib().or_rewrite_process(o.h, snb.ctypes.data, 2624, cn, 128,
+                                         hh.ctypes.data, ll.ctypes.data)
+            busy += time.perf_counter() - t0
+            done += cn
+            i += 1
+        out["cpu_baseline"] = cpu_baseline({1: done / busy / 1e6}, 1,
+                                           "%d packets x %d passes in snbuf layout, "
+                                           "1 thread" % (cn, i))
+    return out
+
+
 def nat_pairs():
     """16 pairs: 8 /16s 10.i.0.0 -> 100.i.0.0 then their images mapped
     back, so every launch translates the same packets again (steady state)"""
@@ -1446,6 +1496,7 @@ def main():
             "c5": lambda: run_c5(args, dev, torch),
             "ttl": lambda: run_update_ttl(args, dev, torch),
             "dnat": lambda: run_dnat(args, dev, torch),
+            "rewrite": lambda: run_rewrite(args, dev, torch),
             "nat": lambda: run_static_nat(args, dev, torch),
             "iplookup": lambda: run_iplookup(args, dev, torch),
             "acl": lambda: run_acl(args, dev, torch),
@@ -1524,7 +1575,7 @@ def main():
                          ("IPLookup", run_iplookup),
                          ("UpdateTTL", run_update_ttl),
                          ("StaticNAT", run_static_nat),
-                         ("NAT", run_dnat)):
+                         ("NAT", run_dnat), ("Rewrite", run_rewrite)):
             try:
                 out["extra_configs"][name] = fn(args, dev, torch)
             except Exception as e:

@@ -147,6 +147,15 @@ _SIGS = {
     "bg_lpm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
     "bg_update_ttl": (_int, [_int, _vp, _sz, _sz, _vp, _vp]),
     "bg_ip_encap": (_int, [_int, _vp, _sz, _sz, _int, _vp, _vp, _vp, _vp, _vp]),
+    "bg_rewrite_create": (_int, [C.POINTER(_vp)]),
+    "bg_rewrite_destroy": (None, [_vp]),
+    "bg_rewrite_add": (_int, [_vp, _vp, _vp, _int]),
+    "bg_rewrite_clear": (None, [_vp]),
+    "bg_rewrite_count": (_sz, [_vp]),
+    "bg_rewrite_add_pb": (_int, [_vp, _vp, _sz]),
+    "bg_rewrite_process": (_int, [_vp, _int, _vp, _sz, _sz, C.c_uint32, _vp, _vp, _vp]),
+    "bg_rewrite_process_host": (_int, [_vp, _int, _vp, _sz, _sz, C.c_uint32, _vp,
+                                       _vp, _vp]),
     "bg_dnat_create": (_int, [_vp, _int, _vp, _vp, _vp, _vp, C.c_uint64,
                               C.POINTER(_vp)]),
     "bg_dnat_destroy": (None, [_vp]),
@@ -170,6 +179,15 @@ def lib():
             raise ImportError(
                 "bess_amd: %s missing -- build it (python -c 'import "
                 "__graft_entry__ as g; g.build()')" % LIB_PATH)
+        # One HIP runtime per process: PyTorch-ROCm ships its own
+        # libamdhip64; when it is present it is loaded first so that
+        # libbessgpu.so binds to the same runtime (loaded the other way
+        # round, the library's runtime reports no device once torch holds
+        # the GPU -- measured on the MI355X box)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name, None)

@@ -243,6 +243,25 @@ struct EncapArgs {
   uint16_t *out;
 };
 
+// Rewrite (core/modules/rewrite.cc): packet i becomes template (start + i) %
+// ntempl: its bytes at slot + headroom in whole 16-byte chunks up to the
+// size rounded to 32 (the reference's sloppy 32-byte block copy; the
+// template buffer is zero past its size), head[i] = headroom, len[i] = size
+constexpr uint32_t kRwMaxTemplates = 32;   // PacketBatch::kMaxBurst
+constexpr uint32_t kRwMaxSize = 1536;      // Rewrite::kMaxTemplateSize
+struct RewriteArgs {
+  uint8_t *slots;
+  uint64_t stride, n;
+  const uint8_t *tmpl;    // ntempl x kRwMaxSize, zero past each size
+  const uint16_t *tsize;  // ntempl
+  uint32_t ntempl, start, headroom;
+  uint32_t lpp_log2;      // lanes per packet = 2^lpp_log2 (<= 64)
+  uint32_t units;         // 16-byte chunks of the largest rounded template
+  uint32_t pad;
+  uint16_t *head;         // data_off, out
+  uint32_t *len;          // pkt_len, out
+};
+
 // NAT (core/modules/nat.cc): endpoint keys (addr raw | port raw << 32 |
 // proto << 48), per-packet entry indices (or kDnatMiss / kDnatInvalid),
 // the entries' translated endpoints and forward timestamps.
@@ -313,6 +332,7 @@ hipError_t launch_lpm(const LpmArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_nat(const NatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_encap(const EncapArgs &a, int num_cus, hipStream_t s);
+hipError_t launch_rewrite(const RewriteArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_dnat_apply(const DnatArgs &a, int num_cus, hipStream_t s);
 hipError_t launch_dnat_image(const uint64_t *d_up, size_t k, uint64_t *img,
                              hipStream_t s);

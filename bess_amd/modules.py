@@ -332,6 +332,60 @@ def ip_encap(d_slots, stride, n, meta_off, attr_offsets, d_head, d_len, d_out,
                              C.c_void_p(d_out.data_ptr()), _stream_ptr(stream)))
 
 
+class Rewrite:
+    """core/modules/rewrite.{h,cc} on the GPU (bg_rewrite_*): Init(arg) =
+    add(arg.templates); the add / clear commands; ProcessBatch over a device
+    slab of packet slots or over host packet buffers."""
+    mclass = "Rewrite"
+    cmds = {"add": ("RewriteArg", "EmptyArg"), "clear": ("EmptyArg", "EmptyArg")}
+    SNBUF_HEADROOM = 128
+
+    def __init__(self, templates=()):
+        h = C.c_void_p()
+        _check(lib().bg_rewrite_create(C.byref(h)))
+        self.h = h
+        self.add(templates=templates)
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_rewrite_destroy(self.h)
+            self.h = None
+
+    def add(self, templates=()):
+        """RewriteArg.templates: bytes"""
+        ts = [bytes(t) for t in templates]
+        bufs = [C.create_string_buffer(t, max(len(t), 1)) for t in ts]
+        ptrs = (C.c_void_p * max(len(ts), 1))(*[C.addressof(b) for b in bufs])
+        lens = (C.c_uint32 * max(len(ts), 1))(*[len(t) for t in ts])
+        _check(lib().bg_rewrite_add(self.h, ptrs, lens, len(ts)))
+
+    def clear(self):
+        lib().bg_rewrite_clear(self.h)
+
+    def __len__(self):
+        return lib().bg_rewrite_count(self.h)
+
+    def process_device(self, d_slots, stride, n, d_head, d_len,
+                       headroom=SNBUF_HEADROOM, device=0, stream=None):
+        """torch tensors: d_slots (uint8 slab), d_head (int16: data_off),
+        d_len (int32: pkt_len)"""
+        from .flowtable import _stream_ptr
+        _check(lib().bg_rewrite_process(self.h, device, C.c_void_p(d_slots.data_ptr()),
+                                        stride, n, headroom,
+                                        C.c_void_p(d_head.data_ptr()),
+                                        C.c_void_p(d_len.data_ptr()), _stream_ptr(stream)))
+
+    def process_host(self, slots, slot_bytes, head, length, headroom=SNBUF_HEADROOM,
+                     device=0):
+        """slots: array of buffer addresses (uintp); head uint16 / length
+        uint32 numpy arrays, written"""
+        n = len(slots)
+        ptrs = np.ascontiguousarray(slots, dtype=np.uintp)
+        _check(lib().bg_rewrite_process_host(self.h, device, ptrs.ctypes.data, slot_bytes,
+                                             n, headroom, head.ctypes.data,
+                                             length.ctypes.data, None))
+
+
 class Pipe:
     """Asynchronous host ingress/egress for a module (bg_pipe_*): packets
     are submitted in BESS-sized batches (<= 32 per ProcessBatch), gathered

@@ -335,6 +335,37 @@ size_t bg_dnat_count(const bg_dnat *h);
 int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
                     int dir, uint64_t now, uint16_t *d_out, bg_stream_t stream);
 
+/* ---- Rewrite (core/modules/rewrite.{h,cc}) ----------------------------- */
+/* The template set and the round-robin turn. add = CommandAdd (25-61):
+ * all or nothing, -EINVAL "max 32 packet templates can be used %zu %d" /
+ * "template is too big" (> 1536 bytes); clear = CommandClear (63-67).
+ * Init(arg) is add(arg.templates). */
+typedef struct bg_rewrite bg_rewrite;
+int bg_rewrite_create(bg_rewrite **out);
+void bg_rewrite_destroy(bg_rewrite *h);
+int bg_rewrite_add(bg_rewrite *h, const uint8_t *const *templates,
+                   const uint32_t *lens, int n);
+void bg_rewrite_clear(bg_rewrite *h);
+size_t bg_rewrite_count(const bg_rewrite *h);
+/* add() from a serialized bess.pb.RewriteArg (repeated bytes templates = 1),
+ * as a bessd plugin receives its Init / add argument */
+int bg_rewrite_add_pb(bg_rewrite *h, const void *arg, size_t len);
+/* ProcessBatch (72-113) over n packets in one call, as consecutive batches:
+ * packet i (slot d_slots + i*stride) gets template (turn + i) % count at
+ * slot + headroom, d_head[i] = headroom (data_off), d_len[i] = its size;
+ * the turn advances by n. Whole 32-byte blocks are written, as the
+ * reference's sloppy copy does (bytes past the size are the template's
+ * zero padding), so headroom + the largest size rounded up to 32 must fit
+ * the slot. No template: packets untouched. stream NULL: synchronous. */
+int bg_rewrite_process(bg_rewrite *h, int device, void *d_slots, size_t stride,
+                       size_t n, uint32_t headroom, uint16_t *d_head, uint32_t *d_len,
+                       bg_stream_t stream);
+/* Host packets: slots[i] = packet i's buffer (slot_bytes each); written at
+ * headroom through the calling thread's pinned staging. Synchronous. */
+int bg_rewrite_process_host(bg_rewrite *h, int device, uint8_t *const *slots,
+                            size_t slot_bytes, size_t n, uint32_t headroom,
+                            uint16_t *head, uint32_t *len, bg_stream_t stream);
+
 /* ---- IPEncap (core/modules/ip_encap.cc) -------------------------------- */
 /* ProcessBatch 40-80 on a device slab: packet i's slot at d_slots +
  * i*stride, its data at slot + d_head[i] (the mbuf's data_off), pkt_len

@@ -855,3 +855,86 @@ double or_static_nat_bench(const uint32_t *int_addr, const uint32_t *ext_addr,
   snat_ctx c = {int_addr, ext_addr, size, npairs, base, stride, out};
   return run_slices(snat_slice, &c, n, nthreads, reps);
 }
+
+/* ------------------------------------------------------------------------
+ * Rewrite (core/modules/rewrite.{h,cc}): kNumSlots = 2 * kMaxBurst - 1 = 63
+ * template slots of kMaxTemplateSize = 1536 bytes; CommandAdd (25-61) fills
+ * slots [curr, curr + k) and replicates template i % n into every later
+ * slot so that a batch reads templates_[start + i] without a modulo;
+ * ProcessBatch (105-113) -> DoRewriteSingle (72-86) / DoRewrite (88-103)
+ * per batch of <= kMaxBurst packets: data_off = SNBUF_HEADROOM, lengths =
+ * the template's size, CopyInlined(..., sloppy = true) -- whole 32-byte
+ * AVX2 blocks (copy.h:145-231), so up to 31 bytes past the size come from
+ * the template slot too. next_turn_ = jump_[start + cnt]: jump_[i] is
+ * written only for i >= n (its value i % n), so for start + cnt < n the
+ * reference reads an unset entry; restated as start + cnt (its meaning).
+ * ------------------------------------------------------------------------ */
+#define OR_RW_SLOTS 63
+#define OR_RW_MAX 1536
+#define OR_RW_BURST 32
+
+typedef struct {
+  uint8_t t[OR_RW_SLOTS][OR_RW_MAX];
+  uint16_t size[OR_RW_SLOTS];
+  size_t jump[OR_RW_SLOTS + 1];
+  size_t n, next;
+} or_rewrite;
+
+or_rewrite *or_rewrite_new(void) { return (or_rewrite *)calloc(1, sizeof(or_rewrite)); }
+void or_rewrite_free(or_rewrite *r) { free(r); }
+
+/* CommandAdd: 0, -EINVAL with the reference's message in msg */
+int or_rewrite_add(or_rewrite *r, const uint8_t *const *tmpl, const uint32_t *len,
+                   int k, char *msg, size_t msglen) {
+  size_t curr = r->n;
+  if (curr + (size_t)k > OR_RW_BURST) {
+    snprintf(msg, msglen, "max %zu packet templates can be used %zu %d",
+             (size_t)OR_RW_BURST, curr, k);
+    return -EINVAL;
+  }
+  for (int i = 0; i < k; i++) {
+    if (len[i] > OR_RW_MAX) {
+      snprintf(msg, msglen, "template is too big");
+      return -EINVAL;
+    }
+    memset(r->t[curr + i], 0, OR_RW_MAX);
+    memcpy(r->t[curr + i], tmpl[i], len[i]);
+    r->size[curr + i] = (uint16_t)len[i];
+  }
+  r->n = curr + (size_t)k;
+  if (r->n == 0) return 0;
+  for (size_t i = r->n; i < OR_RW_SLOTS; i++) {
+    size_t j = i % r->n;
+    memcpy(r->t[i], r->t[j], r->size[j]);
+    r->size[i] = r->size[j];
+    r->jump[i] = j;
+  }
+  r->jump[OR_RW_SLOTS] = OR_RW_SLOTS % r->n;
+  return 0;
+}
+
+void or_rewrite_clear(or_rewrite *r) {
+  r->next = 0;
+  r->n = 0;
+}
+
+/* n packets in slots of `stride` bytes (data at slot + head[i]), processed
+ * as consecutive batches of <= 32: head[i] = headroom, len[i] = size */
+void or_rewrite_process(or_rewrite *r, uint8_t *slots, size_t stride, size_t n,
+                        uint32_t headroom, uint16_t *head, uint32_t *len) {
+  for (size_t b = 0; b < n; b += OR_RW_BURST) {
+    const size_t cnt = n - b < OR_RW_BURST ? n - b : OR_RW_BURST;
+    if (r->n == 0) continue;
+    const size_t start = r->n == 1 ? 0 : r->next;
+    for (size_t i = 0; i < cnt; i++) {
+      const size_t s = start + i;
+      const uint16_t size = r->size[s];
+      uint8_t *dst = slots + (b + i) * stride + headroom;
+      size_t blocks = ((size_t)size + 31) / 32;  /* sloppy: whole 32 B blocks */
+      memcpy(dst, r->t[s], blocks * 32);
+      head[b + i] = (uint16_t)headroom;
+      len[b + i] = size;
+    }
+    if (r->n > 1) r->next = start + cnt < r->n ? start + cnt : r->jump[start + cnt];
+  }
+}

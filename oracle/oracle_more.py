@@ -30,6 +30,11 @@ _SIGS = {
     "or_static_nat_process": (None, [_vp, _vp, _vp, _sz, _vp, _sz, _sz, C.c_int,
                                      _vp]),
     "or_ip_encap_process": (None, [_vp, _sz, _sz, C.c_int, _vp, _vp, _vp, _vp]),
+    "or_rewrite_new": (_vp, []),
+    "or_rewrite_free": (None, [_vp]),
+    "or_rewrite_add": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_char_p, _sz]),
+    "or_rewrite_clear": (None, [_vp]),
+    "or_rewrite_process": (None, [_vp, _vp, _sz, _sz, C.c_uint32, _vp, _vp]),
     "or_nat_new": (_vp, [C.c_uint64]),
     "or_nat_free": (None, [_vp]),
     "or_nat_count": (_sz, [_vp]),
@@ -387,6 +392,39 @@ def ip_encap_process(slots, stride, n, meta_off, offs, head, length):
                                head.ctypes.data, length.ctypes.data,
                                out.ctypes.data)
     return out
+
+
+class OracleRewrite:
+    """core/modules/rewrite.{h,cc}: Init = add; add / clear; ProcessBatch
+    over a slab of packet slots (data at slot + head[i]) in batches of 32."""
+    SNBUF_HEADROOM = 128
+
+    def __init__(self, templates=()):
+        self.h = mlib().or_rewrite_new()
+        self.add(templates)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            mlib().or_rewrite_free(self.h)
+            self.h = None
+
+    def add(self, templates):
+        """templates: bytes objects -> raises ValueError(errno, msg)"""
+        k = len(templates)
+        bufs = [C.create_string_buffer(bytes(t), max(len(t), 1)) for t in templates]
+        ptrs = (C.c_void_p * max(k, 1))(*[C.addressof(b) for b in bufs])
+        lens = (C.c_uint32 * max(k, 1))(*[len(t) for t in templates])
+        msg = C.create_string_buffer(256)
+        r = mlib().or_rewrite_add(self.h, ptrs, lens, k, msg, 256)
+        if r:
+            raise ValueError(-r, msg.value.decode())
+
+    def clear(self):
+        mlib().or_rewrite_clear(self.h)
+
+    def process(self, slots, stride, n, head, length, headroom=SNBUF_HEADROOM):
+        mlib().or_rewrite_process(self.h, _ptr(slots), stride, n, headroom,
+                                  head.ctypes.data, length.ctypes.data)
 
 
 class OracleNAT:

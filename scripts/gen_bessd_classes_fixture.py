@@ -18,7 +18,7 @@ MODULES = {  # class -> reference file stem (core/modules/<stem>.{h,cc})
     "IPChecksum": "ip_checksum", "L4Checksum": "l4_checksum",
     "HashLB": "hash_lb", "ACL": "acl", "IPLookup": "ip_lookup",
     "UpdateTTL": "update_ttl", "StaticNAT": "static_nat", "NAT": "nat",
-    "IPEncap": "ip_encap",
+    "IPEncap": "ip_encap", "Rewrite": "rewrite",
 }
 
 

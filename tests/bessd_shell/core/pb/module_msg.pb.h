@@ -66,6 +66,7 @@ BESSD_SHELL_MSG(IPLookupCommandDeleteArg)
 BESSD_SHELL_MSG(StaticNATArg)
 BESSD_SHELL_MSG(NATArg)
 BESSD_SHELL_MSG(IPEncapArg)
+BESSD_SHELL_MSG(RewriteArg)
 #undef BESSD_SHELL_MSG
 
 }  // namespace pb

@@ -63,7 +63,7 @@ def test_classes_equal_reference(drive):
                                     check=True).stdout)
     with open(os.path.join(ROOT, "tests", "golden", "bessd_classes.json")) as f:
         want = json.load(f)
-    assert set(got) == set(want) and len(got) == 11
+    assert set(got) == set(want) and len(got) == 12
     for cls in want:
         assert got[cls] == want[cls], cls
 
@@ -253,3 +253,57 @@ def test_nat_wrapper_forward_and_reverse(drive, tmp_path):
         assert int.from_bytes(b[30:34], "big") == int(src[i])
         assert int.from_bytes(b[36:38], "big") == int(sport[i])
         assert int.from_bytes(b[26:30], "big") == int(dst[i])
+
+
+def _rewrite_arg(templates):
+    """bess.pb.RewriteArg wire bytes: repeated bytes templates = 1"""
+    out = b""
+    for t in templates:
+        n, ln = len(t), b""
+        while True:
+            b = n & 0x7F
+            n >>= 7
+            ln += bytes([b | (0x80 if n else 0)])
+            if not n:
+                break
+        out += b"\x0a" + ln + t
+    return out.hex() if out else "-"
+
+
+def test_rewrite_commands_through_wrapper(drive):
+    """Rewrite's Init / add / clear through its wrapper answer as
+    CommandAdd does (rewrite.cc:25-61): the template count and size
+    checks with their messages, all or nothing"""
+    out = run(drive, ["create Rewrite " + _rewrite_arg([b"x"] * 33)])
+    assert rc(out[0]) == (22, "max 32 packet templates can be used 0 33")
+    out = run(drive, ["create Rewrite " + _rewrite_arg([b"a" * 60, b"b" * 100]),
+                      "cmd add " + _rewrite_arg([b"c"] * 31),
+                      "cmd add " + _rewrite_arg([b"d", b"e" * 1537]),
+                      "cmd clear -",
+                      "cmd add " + _rewrite_arg([b"f" * 1536])])
+    assert rc(out[0]) == (0, "")
+    assert rc(out[1], True) == (22, "max 32 packet templates can be used 2 31")
+    assert rc(out[2], True) == (22, "template is too big")
+    assert rc(out[3], True) == (0, "") and rc(out[4], True) == (0, "")
+
+
+@pytest.mark.gpu
+def test_rewrite_wrapper_rewrites(drive, tmp_path):
+    """Rewrite through its wrapper on the GPU: packet i of the run carries
+    template i % 3 (the turn crosses the 32-packet batches), its length,
+    and goes on to gate 0 (RunNextModule)"""
+    ts = [bytes(range(60)), bytes([7]) * 100, bytes(range(200, 250))]
+    n = 70
+    frames = np.zeros((n, 64), np.uint8)
+    path = tmp_path / "f.bin"
+    frames.tofile(path)
+    out = run(drive, ["create Rewrite " + _rewrite_arg(ts), "connect 0",
+                      "frames %s 64 %d" % (path, n), "process 0 0"])
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == ["0"] * n
+    data = [x.split() for x in out if x.startswith("data")]
+    assert len(data) == n
+    for i, (_, ln, h) in enumerate(data):
+        t = ts[i % 3]
+        assert int(ln) == len(t)
+        assert bytes.fromhex(h)[:min(64, len(t))] == t[:64]
