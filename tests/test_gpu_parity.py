@@ -295,9 +295,23 @@ def test_wm_direct_tuples_vs_oracle(dev):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
     d_frames = to_dev(frames, dev)
 
+    order = {}  # tuple order: each mask's first add (deletes keep tuples)
+    for m in rm:
+        order.setdefault(m.tobytes(), len(order))
+
     def check(keep):
         got = classify_all_paths_wm(t, d_frames, 64, n, 77, dev, 1)
-        wm = oracle_wm(P.FIVE_TUPLE, rk[keep], rm[keep], prio[keep], gates[keep])
+        # the oracle gets the kept rules, each mask's first kept rule added
+        # up front in the table's tuple order (equal priorities go to the
+        # later tuple, P5), then all of them in order (the later add of a
+        # (mask, key) wins, as in the table)
+        idx = np.nonzero(keep)[0]
+        first = {}
+        for i in idx:
+            first.setdefault(rm[i].tobytes(), i)
+        lead = [first[m] for m in sorted(first, key=order.get)]
+        sel = np.concatenate([np.array(lead, np.int64), idx])
+        wm = oracle_wm(P.FIVE_TUPLE, rk[sel], rm[sel], prio[sel], gates[sel])
         want = np.zeros(n, np.uint16)
         O.lib().or_wm_process(wm, frames.ctypes.data, 64, n, 77, want.ctypes.data)
         O.lib().or_wm_free(wm)
@@ -311,7 +325,7 @@ def test_wm_direct_tuples_vs_oracle(dev):
     rng = np.random.default_rng(5)
     few = np.array([np.count_nonzero(m) <= 2 for m in rm])
     pairs = {(k.tobytes(), m.tobytes()) for k, m in zip(rk[few], rm[few])}
-    gone = {x for x in pairs if rng.random() < 1 / 3}
+    gone = {x for x in sorted(pairs) if rng.random() < 1 / 3}
     for k, m in gone:
         t.delete(k, m)
     keep = np.array([(k.tobytes(), m.tobytes()) not in gone for k, m in zip(rk, rm)])
