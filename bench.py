@@ -698,7 +698,7 @@ def run_hashlb(args, dev, torch):
                                        "hashlb" if name == "l4" else None),
                      "parity": "bit-exact vs oracle on %d pkts" % k
                                if parity else "MISMATCH"}
-        if name == "l4" and not args.no_cpu:
+        if not args.no_cpu:
             cn = 1 << 18
             snb = _snbuf_sample(frames, cn)
             og = np.zeros(cn, np.uint16)
@@ -706,11 +706,11 @@ def run_hashlb(args, dev, torch):
             L = OM.mlib()
             threads, res = cpu_rate(
                 lambda nt, reps: L.or_hashlb_bench(
-                    o.mode, None, 0, gt.ctypes.data, 8, snb.ctypes.data + 512,
+                    o.mode, o._em, o.hash_len, gt.ctypes.data, 8, snb.ctypes.data + 512,
                     2624, cn, og.ctypes.data, nt, reps), cn, args.cpu_seconds / 3)
             out[name]["cpu_baseline"] = cpu_baseline(
-                res, threads, "%d 64B pkts x reps in snbuf layout, HashLB l4 "
-                              "(SSE4.2 CRC32C)" % cn)
+                res, threads, "%d 64B pkts x reps in snbuf layout, HashLB %s "
+                              "(SSE4.2 CRC32C)" % (cn, name))
     return out
 
 
