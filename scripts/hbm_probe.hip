@@ -10,6 +10,11 @@
 //             = slot) + one 2-byte store per slot -- the C2 ExactMatch shape
 //   slot64  : all 64 B of every slot (four 16 B loads per lane, lane = slot)
 //   half32  : bytes 16..47 of every slot, two lanes per slot, lanes contiguous
+// Write shapes (`./hbm_probe GiB w`; TB/s of bytes written):
+//   wfull16 : every byte, 16 B per lane per store, lanes contiguous
+//   w64s192 : 64 B at +128 of every 192 B slot, 4 lanes per slot (the
+//             Rewrite bench's shape: a 60 B template in 32 B blocks)
+//   w64s128 : 64 B at +64 of every 128 B slot (one half line per slot)
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
 // bytes read (median of 5 rounds of 20 back-to-back launches).
 #include <hip/hip_runtime.h>
@@ -74,6 +79,22 @@ __global__ __launch_bounds__(512) void half32(const u32x4 *src, size_t nslots,
   }
 }
 
+__global__ __launch_bounds__(512) void wfull16(u32x4 *dst, size_t n16) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += step)
+    dst[i] = u32x4{(uint32_t)i, 1u, 2u, 3u};
+}
+
+// 64 B of every `slot`-byte slot at offset `off`: lane u writes chunk u & 3
+// of slot u >> 2
+__global__ __launch_bounds__(512) void w64(u32x4 *dst, size_t nslots, uint32_t slot,
+                                           uint32_t off) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x; u < nslots * 4;
+       u += step)
+    dst[((u >> 2) * slot + off) / 16 + (u & 3)] = u32x4{(uint32_t)u, 1u, 2u, 3u};
+}
+
 #define CK(x)                                                            \
   do {                                                                   \
     hipError_t e = (x);                                                  \
@@ -99,10 +120,15 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char *names[4] = {"full16", "em32", "slot64", "half32"};
-  for (int shape = 0; shape < 4; shape++) {
+  const bool wr = argc > 2 && argv[2][0] == 'w';
+  const char *names[7] = {"full16", "em32", "slot64", "half32",
+                          "wfull16", "w64s192", "w64s128"};
+  for (int shape = wr ? 4 : 0; shape < (wr ? 7 : 4); shape++) {
     for (int bpc : {1, 2, 4, 8}) {
       const int blocks = cus * bpc;
+      double moved = (double)bytes;  // bytes read or written per launch
+      if (shape == 5) moved = (double)(bytes / 192) * 64;
+      if (shape == 6) moved = (double)(bytes / 128) * 64;
       auto launch = [&]() {
         if (shape == 0)
           hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
@@ -113,9 +139,17 @@ int main(int argc, char **argv) {
         else if (shape == 2)
           hipLaunchKernelGGL(slot64, dim3(blocks), dim3(512), 0, 0, src,
                              nslots, gates);
-        else
+        else if (shape == 3)
           hipLaunchKernelGGL(half32, dim3(blocks), dim3(512), 0, 0, src,
                              nslots, gates);
+        else if (shape == 4)
+          hipLaunchKernelGGL(wfull16, dim3(blocks), dim3(512), 0, 0, src, bytes / 16);
+        else if (shape == 5)
+          hipLaunchKernelGGL(w64, dim3(blocks), dim3(512), 0, 0, src, bytes / 192,
+                             192u, 128u);
+        else
+          hipLaunchKernelGGL(w64, dim3(blocks), dim3(512), 0, 0, src, bytes / 128,
+                             128u, 64u);
       };
       for (int w = 0; w < 20; w++) launch();
       CK(hipDeviceSynchronize());
@@ -132,8 +166,8 @@ int main(int argc, char **argv) {
       std::sort(ms.begin(), ms.end());
       const double t = ms[2] * 1e-3;
       printf("{\"shape\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, "
-             "\"slab_TBps\": %.3f}\n",
-             names[shape], bpc, ms[2], bytes / t / 1e12);
+             "\"TBps\": %.3f}\n",
+             names[shape], bpc, ms[2], moved / t / 1e12);
       fflush(stdout);
     }
   }
