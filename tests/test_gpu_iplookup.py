@@ -85,6 +85,21 @@ PATHS = [0, LB.BG_PATH_NO_LDS, LB.BG_PATH_NO_LDS | LB.BG_PATH_NO_SLAB,
          LB.BG_PATH_LPM_DIR24]
 
 
+@pytest.mark.parametrize("n", [1, 5, 63, 64, 65, 2047, 64 * 1000 + 37])
+def test_ragged_counts_vs_oracle(n):
+    """partial last waves and workgroups (1024-thread lane-per-packet kernel,
+    tbl16 in LDS; the L2 slab kernel's partial tiles)"""
+    rng = np.random.default_rng(n)
+    rt = routes(3000, rng, 0.05)
+    m, o = build(rt, max_rules=3010, max_tbl8s=4096)
+    f = frames_to(np.concatenate([dsts_inside(rt, n - n // 2, rng),
+                                  rng.integers(0, 1 << 32, n // 2, dtype=np.uint64)]))
+    want = o.process(f, 64, n)
+    for flags in (0, LB.BG_PATH_NO_LDS):
+        with LB.kernel_paths(flags):
+            assert (device_gates(m, f, 64) == want).all(), flags
+
+
 @pytest.mark.parametrize("flags", PATHS)
 @pytest.mark.parametrize("nroutes,deep", [(1, 0.0), (100, 0.1), (5000, 0.05),
                                           (50000, 0.002), (150000, 0.0)])
