@@ -126,14 +126,15 @@ BG_HD uint32_t wm_hash(const uint32_t *kd, uint32_t cover, int ndw, uint32_t see
 }
 
 // first bucket from the low bits, fingerprint from the top byte, second
-// bucket from the top bits of one more product (nbp = 2^lg, lg >= 1)
+// bucket the first XOR an odd number from the top bits of one more product
+// (nbp = 2^lg, lg >= 1)
 BG_HD Probe wm_probe(uint32_t h, uint32_t lg) {
   Probe p;
   const uint32_t m = (1u << lg) - 1;
   p.part = 0;
   p.b1 = h & m;
-  p.b2 = (h * 0xC2B2AE35u) >> (32 - lg);
-  if (p.b2 == p.b1) p.b2 = (p.b1 ^ 1u) & m;
+  // b1 XOR an odd offset: never b1, no compare-and-fix
+  p.b2 = p.b1 ^ (((h * 0xC2B2AE35u) >> (32 - lg)) | 1u);
   const uint32_t t = h >> 24;
   p.tag = t ? t : 1u;
   return p;
