@@ -34,6 +34,24 @@ class BessGpuError(RuntimeError):
         self.msg = msg
 
 
+class bg_ctx(C.Structure):
+    """a ProcessBatch's Context (core/module.h:59-75): current_ns,
+    current_igate, the device of the call (-1: the module's), wid"""
+    _fields_ = [("now_ns", C.c_uint64), ("igate", C.c_uint16),
+                ("device", C.c_int16), ("wid", C.c_uint32)]
+
+
+def make_ctx(igate=0, now=None, device=-1, wid=0):
+    """a bg_ctx pointer argument; now None = the library's monotonic clock
+    (then the whole ctx is NULL when igate and device are defaults too)"""
+    if now is None and igate == 0 and device == -1 and wid == 0:
+        return None
+    if now is None:
+        import time
+        now = time.monotonic_ns()
+    return C.byref(bg_ctx(int(now), int(igate), int(device), int(wid)))
+
+
 class bg_field(C.Structure):
     _fields_ = [("offset", C.c_int32), ("size", C.c_int32), ("pos", C.c_int32),
                 ("attr_id", C.c_int32), ("mask", C.c_uint64)]
@@ -89,14 +107,13 @@ _SIGS = {
     "bg_module_destroy": (None, [_vp]),
     "bg_module_command": (_int, [_vp, C.c_char_p, _vp, _sz, _vp,
                                  C.POINTER(_sz)]),
-    "bg_module_process": (_int, [_vp, _vp, _sz, _vp]),
-    "bg_module_process_batches": (_int, [_vp, _vp, _sz, _vp, _vp, _vp, _vp,
+    "bg_module_process": (_int, [_vp, _vp, _vp, _sz, _vp]),
+    "bg_module_process_batches": (_int, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp,
                                          C.POINTER(_sz), C.POINTER(_sz)]),
     "bg_module_connect": (_int, [_vp, _u16, _int]),
-    "bg_module_run": (_int, [_vp, _vp, _sz, _sz, _vp]),
-    "bg_module_process_device": (_int, [_vp, _vp, _sz, _sz, _vp, _vp]),
+    "bg_module_run": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "bg_module_process_device": (_int, [_vp, _vp, _vp, _sz, _sz, _vp, _vp]),
     "bg_module_set_device": (_int, [_vp, _int]),
-    "bg_module_set_igate": (_int, [_vp, _u16]),
     "bg_module_bind_meta": (_int, [_vp, _int, _vp, _vp, _int]),
     "bg_em_bind_meta": (_int, [_vp, _int, _vp, _int]),
     "bg_wm_bind_meta": (_int, [_vp, _int, _vp, _int]),
@@ -113,11 +130,11 @@ _SIGS = {
     "bg_pipe_destroy": (None, [_vp]),
     "bg_pipe_window": (_int, [_vp, C.POINTER(_int), C.POINTER(_int),
                               C.POINTER(_sz)]),
-    "bg_pipe_submit": (_int, [_vp, _vp, _vp, _vp, _sz]),
+    "bg_pipe_submit": (_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
     "bg_pipe_flush": (_int, [_vp]),
     "bg_pipe_poll": (C.c_long, [_vp, _int, _vp, _vp, _sz]),
     "bg_pipe_pending": (_sz, [_vp]),
-    "bg_pipe_run": (_int, [_vp, _vp, _vp, _sz, _sz, _vp]),
+    "bg_pipe_run": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
     "bg_em_ring_create": (_int, [_vp, _int, _int, _int, C.c_uint32, C.POINTER(_vp)]),
     "bg_ring_destroy": (None, [_vp]),
     "bg_ring_submit": (C.c_int64, [_vp, _vp, _sz, _sz, _u16, _vp]),

@@ -91,10 +91,13 @@ class ACL final : public Module {
     return CommandSuccess();
   }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  // acl.cc:70: a packet the first matching rule forwards leaves on the
+  // input gate it came in on -- the call's, ctx->current_igate
+  int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
-    return bg_acl_classify(h_, d_frames, stride, n, igate_, d_ogates, stream);
+    return bg_acl_classify(h_, d_frames, stride, n, c.igate, d_ogates, stream);
   }
+  unsigned CtxUse() const override { return kCtxIgate; }
 
   void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
     *lo = 0;

@@ -34,9 +34,9 @@ class ChecksumModule : public Module {
     *writeback = true;
   }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
-    return bg_cksum(device_, d_frames, stride, n, kMode, verify_ ? 1 : 0,
+    return bg_cksum(c.device, d_frames, stride, n, kMode, verify_ ? 1 : 0,
                     kMode == BG_CK_IP ? d_ogates : nullptr,
                     kMode == BG_CK_L4 ? d_ogates : nullptr, stream);
   }

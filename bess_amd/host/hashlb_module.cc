@@ -118,7 +118,7 @@ class HashLB final : public Module {
     return buf;
   }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  int ProcessDevice(const bg_ctx &, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_hlb_classify(h_, d_frames, stride, n, 0, d_ogates, stream);
   }
@@ -129,8 +129,8 @@ class HashLB final : public Module {
     *writeback = false;
   }
 
-  int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n, int win_off,
-                          uint16_t *d_ogates, void *stream) override {
+  int ProcessDeviceWindow(const bg_ctx &, void *d_win, size_t wstride, size_t n,
+                          int win_off, uint16_t *d_ogates, void *stream) override {
     return bg_hlb_classify(h_, d_win, wstride, n, win_off, d_ogates, stream);
   }
 

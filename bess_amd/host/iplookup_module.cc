@@ -112,7 +112,7 @@ class IPLookup final : public Module {
     return CommandSuccess();
   }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  int ProcessDevice(const bg_ctx &, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_lpm_classify(lpm_, d_frames, stride, n, default_gate_, d_ogates,
                            stream);

@@ -5,6 +5,7 @@
 
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime.h>
 
@@ -69,6 +70,22 @@ std::vector<std::string> ModuleBuilder::Classes() {
 
 using bg::fail;
 
+// A call's context with its defaults filled in (bg_ctx, include/bessgpu.h):
+// no ctx = input gate 0 and the monotonic clock now; device -1 = the
+// module's.
+bg_ctx ResolveCtx(const bg_ctx *c, int module_device) {
+  bg_ctx r{};
+  if (c) {
+    r = *c;
+  } else {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    r.now_ns = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+  }
+  if (r.device < 0) r.device = (int16_t)module_device;
+  return r;
+}
+
 // The synchronous host datapath shared by every module (see module.h).
 int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) {
   if (cnt == 0) return 0;
@@ -82,7 +99,8 @@ int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) 
   const size_t len = (size_t)(hi - lo);
   const size_t w = (len + 15) / 16 * 16;
   const size_t line = std::min<size_t>(w, 128);  // header line written back
-  int r = bg::set_device(device_);
+  const bg_ctx &c = ctx->call;
+  int r = bg::set_device(c.device);
   auto drop_all = [&](int rc) {
     for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
     return rc;
@@ -90,9 +108,9 @@ int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) 
   if (r) return drop_all(r);
   bg::Staging &st = bg::thread_staging();
   // +64 B: the last window's 16-byte loads may run past its slot
-  r = st.ensure(device_, cnt * w + 64, cnt * 2);
+  r = st.ensure(c.device, cnt * w + 64, cnt * 2);
   if (r) return drop_all(r);
-  hipStream_t s = bg::thread_stream(device_, nullptr);
+  hipStream_t s = bg::thread_stream(c.device, nullptr);
   for (size_t i = 0; i < cnt; i++) {
     uint8_t *dst = st.h_in + i * w;
     memcpy(dst, pkts[i]->head_data<uint8_t *>() + lo, len);
@@ -101,7 +119,7 @@ int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) 
   uint16_t *d_g = reinterpret_cast<uint16_t *>(st.d_out);
   hipError_t e = hipMemcpyAsync(st.d_in, st.h_in, cnt * w, hipMemcpyHostToDevice, s);
   if (e != hipSuccess) return drop_all(fail(EIO, "H2D: %s", hipGetErrorString(e)));
-  r = ProcessDeviceWindow(st.d_in, w, cnt, lo, d_g, s);
+  r = ProcessDeviceWindow(c, st.d_in, w, cnt, lo, d_g, s);
   if (r < 0) {
     (void)hipStreamSynchronize(s);
     return drop_all(r);
@@ -175,8 +193,8 @@ int bg_module_command(bg_module *h, const char *cmd, const void *arg,
               user_cmd.c_str());
 }
 
-static int process(bg_module *h, uint8_t *const *heads, size_t cnt,
-                   uint16_t *ogates, EmitLog *log) {
+static int process(bg_module *h, const bg_ctx *call, uint8_t *const *heads,
+                   size_t cnt, uint16_t *ogates, EmitLog *log) {
   std::shared_lock<std::shared_mutex> lk(h->mu);  // many workers at once
   for (size_t i = 0; i < cnt; i++) ogates[i] = BG_GATE_NONE;
   std::vector<bess::Packet> pkts(cnt);
@@ -186,23 +204,25 @@ static int process(bg_module *h, uint8_t *const *heads, size_t cnt,
     ptrs[i] = &pkts[i];
   }
   Context ctx;
+  ctx.call = ResolveCtx(call, h->m->device());
   ctx.ogates = ogates;
   ctx.log = log;
   bg::g_err.clear();
   return h->m->ProcessPackets(&ctx, ptrs.data(), cnt);
 }
 
-int bg_module_process(bg_module *h, uint8_t *const *heads, size_t cnt,
-                      uint16_t *ogates) {
-  return process(h, heads, cnt, ogates, nullptr);
+int bg_module_process(bg_module *h, const bg_ctx *ctx, uint8_t *const *heads,
+                      size_t cnt, uint16_t *ogates) {
+  return process(h, ctx, heads, cnt, ogates, nullptr);
 }
 
-int bg_module_process_batches(bg_module *h, uint8_t *const *heads, size_t cnt,
+int bg_module_process_batches(bg_module *h, const bg_ctx *ctx,
+                              uint8_t *const *heads, size_t cnt,
                               uint16_t *ogates, uint16_t *batch_gate,
                               uint32_t *batch_len, uint32_t *pkt_idx,
                               size_t *nbatches, size_t *ndead) {
   EmitLog log;
-  int r = process(h, heads, cnt, ogates, &log);
+  int r = process(h, ctx, heads, cnt, ogates, &log);
   if (r < 0) return r;
   size_t k = 0;
   for (size_t b = 0; b < log.batches.size(); b++) {
@@ -218,11 +238,11 @@ int bg_module_process_batches(bg_module *h, uint8_t *const *heads, size_t cnt,
 
 // A worker's loop over this module with the synchronous drop-in path:
 // ProcessBatch on each `burst` of packets in turn (Source -> module -> Sink).
-int bg_module_run(bg_module *h, uint8_t *const *heads, size_t n, size_t burst,
-                  uint16_t *ogates) {
+int bg_module_run(bg_module *h, const bg_ctx *ctx, uint8_t *const *heads,
+                  size_t n, size_t burst, uint16_t *ogates) {
   if (burst < 1) return fail(EINVAL, "burst must be >= 1");
   for (size_t i = 0; i < n; i += burst) {
-    int r = process(h, heads + i, std::min(burst, n - i), ogates + i, nullptr);
+    int r = process(h, ctx, heads + i, std::min(burst, n - i), ogates + i, nullptr);
     if (r < 0) return r;
   }
   return 0;
@@ -235,23 +255,21 @@ int bg_module_connect(bg_module *h, uint16_t ogate, int connected) {
   return 0;
 }
 
-int bg_module_process_device(bg_module *h, void *d_frames, size_t stride,
-                             size_t n, uint16_t *d_ogates, bg_stream_t stream) {
-  return h->m->ProcessDevice(d_frames, stride, n, d_ogates, stream);
+int bg_module_process_device(bg_module *h, const bg_ctx *ctx, void *d_frames,
+                             size_t stride, size_t n, uint16_t *d_ogates,
+                             bg_stream_t stream) {
+  std::shared_lock<std::shared_mutex> lk(h->mu);
+  const bg_ctx c = ResolveCtx(ctx, h->m->device());
+  int r = bg::set_device(c.device);
+  if (r) return r;
+  return h->m->ProcessDevice(c, d_frames, stride, n, d_ogates, stream);
 }
 
 int bg_module_set_device(bg_module *h, int device) {
+  int r = bg::set_device(device);
+  if (r) return r;
+  std::unique_lock<std::shared_mutex> lk(h->mu);
   h->m->set_device(device);
-  return 0;
-}
-
-int bg_module_set_igate(bg_module *h, uint16_t igate) {
-  h->m->set_igate(igate);
-  return 0;
-}
-
-int bg_module_set_now(bg_module *h, uint64_t now_ns) {
-  h->m->set_now(now_ns);
   return 0;
 }
 

@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/bessgpu.h"
 #include "pb.h"
 
 typedef uint16_t gate_idx_t;
@@ -86,12 +87,19 @@ struct EmitLog {
   std::map<gate_idx_t, size_t> open;  // gate -> its batch being filled
 };
 
-// Per-call context (core/module.h:59-75): where each packet went.
+// Per-call context (core/module.h:59-75): the batch's input gate, the
+// worker's clock and the device of this call (bg_ctx: never module state),
+// and where each packet went.
 struct Context {
+  bg_ctx call{};               // current_igate, current_ns, device, wid
   uint16_t *ogates = nullptr;  // indexed by Packet::index(); DROP_GATE: dropped
   EmitLog *log = nullptr;      // optional: the gate batches
   uint64_t deadends = 0;       // deadends_[ctx->wid] (module.h:455)
 };
+
+// bg_ctx with its defaults filled in (NULL: igate 0, the monotonic clock
+// now; device -1: module_device)
+bg_ctx ResolveCtx(const bg_ctx *c, int module_device);
 
 class CommandResponse {
  public:
@@ -159,9 +167,15 @@ class Module {
                              size_t cnt);
   virtual std::string GetDesc() const { return ""; }
   virtual const Commands &cmds() const = 0;
-  // Device-resident datapath over a frame slab (libbessgpu.so).
-  virtual int ProcessDevice(void *d_frames, size_t stride, size_t n,
-                            uint16_t *d_ogates, void *stream) = 0;
+  // Device-resident datapath over a frame slab (libbessgpu.so) for one
+  // call's context: c.device is resolved (>= 0) and is the calling thread's
+  // current HIP device; c.igate / c.now_ns are the batch's.
+  virtual int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride,
+                            size_t n, uint16_t *d_ogates, void *stream) = 0;
+  // Which context fields the device datapath reads (a bg_pipe slot holds
+  // packets of one value of them).
+  enum : unsigned { kCtxIgate = 1, kCtxNow = 2 };
+  virtual unsigned CtxUse() const { return 0; }
   // Host ingress/egress staging (bg_pipe, bess_amd/host/pipe.cc): the frame
   // bytes [*lo, *hi) the device datapath reads, and whether it writes frame
   // bytes that must go back into the packet buffers.
@@ -172,11 +186,11 @@ class Module {
   }
   // ProcessDevice over staged windows: byte 0 of window i is frame offset
   // `win_off` of packet i.
-  virtual int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n,
-                                  int win_off, uint16_t *d_ogates,
+  virtual int ProcessDeviceWindow(const bg_ctx &c, void *d_win, size_t wstride,
+                                  size_t n, int win_off, uint16_t *d_ogates,
                                   void *stream) {
     if (win_off != 0) return -EINVAL;
-    return ProcessDevice(d_win, wstride, n, d_ogates, stream);
+    return ProcessDevice(c, d_win, wstride, n, d_ogates, stream);
   }
   // attr_name fields: metadata area at slot offset meta_off, attribute
   // offsets by name (bg_module_bind_meta). Modules without attr fields on
@@ -198,17 +212,9 @@ class Module {
         if (names[j] == attrs_[i].name) r[i] = offsets[j];
     return r;
   }
+  // the device of calls whose bg_ctx says -1 (control path)
   void set_device(int d) { device_ = d; }
   int device() const { return device_; }
-  // ctx->current_igate of the calls that follow (core/module.h:59-75)
-  void set_igate(gate_idx_t g) { igate_ = g; }
-  gate_idx_t igate() const { return igate_; }
-  // ctx->current_ns of the calls that follow (NAT's mapping clock); until
-  // set, modules that need it read CLOCK_MONOTONIC per call
-  void set_now(uint64_t ns) {
-    now_ = ns;
-    now_set_ = true;
-  }
 
   // Module::AddMetadataAttr (core/module.cc:248-285): per-module metadata
   // attributes; returns the attribute id or -errno.
@@ -270,9 +276,6 @@ class Module {
 
  protected:
   int device_ = 0;
-  gate_idx_t igate_ = 0;
-  uint64_t now_ = 0;
-  bool now_set_ = false;
   std::vector<Attribute> attrs_;
   std::vector<bool> ogates_;
   bool explicit_ogates_ = false;

@@ -1,9 +1,9 @@
 // nat_module.cc -- NAT (core/modules/nat.{h,cc}): dynamic address/port
 // translation with its ProcessBatch on the GPU (bg_dnat_*, bg_dnat.hip).
 // Same class name, commands table, Init argument, error codes and
-// messages; two input gates (the input gate picks the direction,
-// bg_module_set_igate) and ctx->current_ns as the mapping clock
-// (bg_module_set_now).
+// messages; two input gates (each call's input gate, bg_ctx::igate, picks
+// the direction) and the call's ctx->current_ns (bg_ctx::now_ns) as the
+// mapping clock.
 #include <errno.h>
 #include <stdio.h>
 #include <time.h>
@@ -113,12 +113,13 @@ class NAT final : public Module {
 
   // DoProcessBatch<dir> (nat.cc:321-363). The mapping table is the
   // module's state: batches go through it one at a time.
-  int ProcessDevice(void *d_frames, size_t stride, size_t n, uint16_t *d_ogates,
-                    void *stream) override {
+  int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
+                    uint16_t *d_ogates, void *stream) override {
     std::lock_guard<std::mutex> g(mu_);
-    return bg_dnat_process(h_, d_frames, stride, n, igate_ ? 1 : 0, clock_ns(),
+    return bg_dnat_process(h_, d_frames, stride, n, c.igate ? 1 : 0, c.now_ns,
                            d_ogates, stream);
   }
+  unsigned CtxUse() const override { return kCtxIgate | kCtxNow; }
 
   void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
     *lo = 0;
@@ -131,12 +132,6 @@ class NAT final : public Module {
     uint16_t begin, end;
     bool suspended;
   };
-  uint64_t clock_ns() const {
-    if (now_set_) return now_;
-    timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-  }
   std::vector<uint32_t> ext_addrs_;
   std::vector<std::vector<Range>> ranges_;
   bg_dnat *h_ = nullptr;

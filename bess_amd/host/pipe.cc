@@ -52,6 +52,7 @@ struct Slot {
   std::vector<void *> cookies;
   size_t n = 0;
   bool inflight = false;
+  bg_ctx ctx{};  // the context of the slot's packets (Module::CtxUse fields)
 };
 
 }  // namespace
@@ -63,6 +64,7 @@ struct bg_pipe {
   int lo = 0, hi = 0;    // staged frame bytes [lo, hi)
   size_t w = 0;          // staged stride (16-byte multiple)
   bool writeback = false;
+  unsigned ctx_use = 0;  // Module::CtxUse(): the context fields a slot fixes
   std::vector<Slot> slots;
   size_t fill = 0;       // slot being filled
   size_t oldest = 0;     // oldest in-flight slot
@@ -91,7 +93,9 @@ static int launch_slot(bg_pipe *p) {
   Slot &s = p->slots[p->fill];
   const size_t n = s.n;
   HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
-  int r = p->mod->m->ProcessDeviceWindow(s.d_in, p->w, n, p->lo, s.d_g, s.st);
+  bg_ctx c = s.ctx;
+  c.device = (int16_t)p->device;
+  int r = p->mod->m->ProcessDeviceWindow(c, s.d_in, p->w, n, p->lo, s.d_g, s.st);
   if (r < 0) return r;
   HIP_TRY(hipMemcpyAsync(s.h_g, s.d_g, n * 2, hipMemcpyDeviceToHost, s.st));
   if (p->writeback) {
@@ -149,7 +153,7 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
   if (span && p->lo == 0 && (int)span < p->hi) p->hi = (int)span;
   if (p->hi <= p->lo) p->hi = p->lo + 1;
   p->w = ((size_t)(p->hi - p->lo) + 15) / 16 * 16;
-  m->m->set_device(device);
+  p->ctx_use = m->m->CtxUse();
   p->slots.resize((size_t)depth);
   for (Slot &s : p->slots) {
     // +64 B: window loads of the last packet may run past its slot
@@ -192,17 +196,33 @@ int bg_pipe_window(const bg_pipe *p, int *lo, int *hi, size_t *stride) {
   return 0;
 }
 
-int bg_pipe_submit(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
-                   void *const *cookies, size_t cnt) {
+// Whether two contexts agree on every field the module's device path reads.
+static bool same_ctx(unsigned use, const bg_ctx &a, const bg_ctx &b) {
+  if ((use & Module::kCtxIgate) && a.igate != b.igate) return false;
+  if ((use & Module::kCtxNow) && a.now_ns != b.now_ns) return false;
+  return true;
+}
+
+int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                   const uint16_t *lens, void *const *cookies, size_t cnt) {
   if (p->err) return p->err;
   int r = bg::set_device(p->device);
   if (r) return r;
+  const bg_ctx c = ResolveCtx(ctx, p->device);
   const size_t span = (size_t)(p->hi - p->lo);
   size_t i = 0;
   while (i < cnt) {
     Slot &s = p->slots[p->fill];
     if (s.inflight) {  // ring full: backpressure until the oldest retires
       r = retire_oldest(p, true);
+      if (r < 0) return p->err = r;
+      continue;
+    }
+    if (s.n == 0) {
+      s.ctx = c;
+    } else if (!same_ctx(p->ctx_use, s.ctx, c)) {
+      // the slot's packets run with their own context: launch them first
+      r = launch_slot(p);
       if (r < 0) return p->err = r;
       continue;
     }
@@ -274,8 +294,8 @@ size_t bg_pipe_pending(const bg_pipe *p) { return p->pending; }
 // A BESS worker's loop over this module (Source -> module -> Sink, SURVEY
 // §3A): ProcessBatch-sized submits of `burst` packets, completions polled
 // after every submit and emitted into ogates[packet index].
-int bg_pipe_run(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
-                size_t n, size_t burst, uint16_t *ogates) {
+int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                const uint16_t *lens, size_t n, size_t burst, uint16_t *ogates) {
   if (burst < 1) return fail(EINVAL, "burst must be >= 1");
   std::vector<void *> ck(burst), done(std::max<size_t>(p->batch, 4096));
   std::vector<uint16_t> g(done.size());
@@ -292,7 +312,7 @@ int bg_pipe_run(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
     // while this batch is gathered
     for (size_t j = i + c; j < std::min(n, i + c + burst); j++)
       __builtin_prefetch(heads[j] + p->lo);
-    int r = bg_pipe_submit(p, heads + i, lens ? lens + i : nullptr, ck.data(), c);
+    int r = bg_pipe_submit(p, ctx, heads + i, lens ? lens + i : nullptr, ck.data(), c);
     if (r < 0) return r;
     if (p->inflight && (r = emit(0)) < 0) return r;
   }

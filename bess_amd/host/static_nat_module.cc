@@ -1,7 +1,7 @@
 // static_nat_module.cc -- StaticNAT (core/modules/static_nat.{h,cc}) with
 // its ProcessBatch on the GPU (bg_snat_*, bg_nat.hip). Same class name,
 // commands table, Init argument, error codes and messages; two input gates
-// (the input gate picks the direction, bg_module_set_igate).
+// (the input gate of each call, bg_ctx::igate, picks the direction).
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
@@ -92,11 +92,14 @@ class StaticNAT final : public Module {
   CommandResponse GetRuntimeConfig(const EmptyArg &) { return CommandSuccess(); }
   CommandResponse SetRuntimeConfig(const EmptyArg &) { return CommandSuccess(); }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  // static_nat.cc:146-181: input gate 0 translates the source, 1 the
+  // destination -- the call's gate, ctx->current_igate
+  int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
-    return bg_snat_classify(h_, d_frames, stride, n, igate_ ? 1 : 0, d_ogates,
+    return bg_snat_classify(h_, d_frames, stride, n, c.igate ? 1 : 0, d_ogates,
                             stream);
   }
+  unsigned CtxUse() const override { return kCtxIgate; }
 
   void DeviceWindow(int *lo, int *hi, bool *writeback) const override {
     *lo = 0;

@@ -16,9 +16,9 @@ class UpdateTTL final : public Module {
 
   CommandResponse Init(const bess::pb::EmptyArg &) { return CommandSuccess(); }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
-    return bg_update_ttl(device_, d_frames, stride, n, d_ogates, stream);
+    return bg_update_ttl(c.device, d_frames, stride, n, d_ogates, stream);
   }
 
   void DeviceWindow(int *lo, int *hi, bool *writeback) const override {

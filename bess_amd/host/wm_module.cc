@@ -82,9 +82,9 @@ class WildcardMatch final : public Module {
     return buf;
   }
 
-  int ProcessDevice(void *d_frames, size_t stride, size_t n,
+  int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
-    int rc = bg_wm_sync(table_, device_, stream);
+    int rc = bg_wm_sync(table_, c.device, stream);
     if (rc < 0) return rc;
     return bg_wm_classify(table_, d_frames, stride, n, default_gate_, d_ogates,
                           stream);
@@ -102,10 +102,10 @@ class WildcardMatch final : public Module {
     return bg_wm_bind_meta(table_, meta_off, off.data(), (int)off.size());
   }
 
-  int ProcessDeviceWindow(void *d_win, size_t wstride, size_t n, int win_off,
-                          uint16_t *d_ogates, void *stream) override {
+  int ProcessDeviceWindow(const bg_ctx &c, void *d_win, size_t wstride, size_t n,
+                          int win_off, uint16_t *d_ogates, void *stream) override {
     if (!all_attrs().empty()) return -ENOTSUP;  // staged windows: no metadata
-    int rc = bg_wm_sync(table_, device_, stream);
+    int rc = bg_wm_sync(table_, c.device, stream);
     if (rc < 0) return rc;
     return bg_wm_classify_window(table_, d_win, wstride, n, win_off,
                                  default_gate_, d_ogates, stream);

@@ -16,7 +16,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib, pb
-from ._lib import BG_GATE_NONE, lib
+from ._lib import BG_GATE_NONE, lib, make_ctx
 
 # command -> (argument message, response message or None); module cmds
 # tables: exact_match.cc:45-60, wildcard_match.cc:58-73
@@ -107,23 +107,21 @@ class Module:
         offs = (C.c_int32 * max(len(names), 1))(*[int(attr_offsets[n]) for n in names])
         _check(lib().bg_module_bind_meta(self.h, meta_off, arr, offs, len(names)))
 
-    def set_igate(self, igate):
-        """the input gate the following process calls arrive on
-        (ctx->current_igate, core/module.h:59-75)"""
-        lib().bg_module_set_igate(self.h, igate)
-
-    def process(self, frames, stride, n):
+    def process(self, frames, stride, n, igate=0, now=None, device=-1):
         """ProcessBatch over host frames (numpy uint8 slab, frame i at
         i*stride, each with >= 2048 accessible bytes for the checksum
-        modules). Returns per-packet EmitPacket gates (BG_GATE_NONE: not
-        emitted). Checksum modules rewrite frames in place."""
+        modules) with the call's context (ctx->current_igate, current_ns,
+        core/module.h:59-75; now None = the library's clock). Returns
+        per-packet EmitPacket gates (BG_GATE_NONE: not emitted). Checksum
+        modules rewrite frames in place."""
         base = frames.ctypes.data
         heads = (C.c_void_p * n)(*[base + i * stride for i in range(n)])
         og = np.full(n, BG_GATE_NONE, np.uint16)
-        _check(lib().bg_module_process(self.h, heads, n, og.ctypes.data))
+        _check(lib().bg_module_process(self.h, make_ctx(igate, now, device), heads,
+                                       n, og.ctypes.data))
         return og
 
-    def process_batches(self, frames, stride, n):
+    def process_batches(self, frames, stride, n, igate=0, now=None):
         """process() plus the batches the Task would run next
         (core/module.h:543-618): -> (ogates, [(gate, [packet index, ...])],
         [dropped packet index, ...])"""
@@ -135,7 +133,7 @@ class Module:
         idx = np.zeros(max(n, 1), np.uint32)
         nb, nd = C.c_size_t(), C.c_size_t()
         _check(lib().bg_module_process_batches(
-            self.h, heads, n, og.ctypes.data, bg_.ctypes.data, bl.ctypes.data,
+            self.h, make_ctx(igate, now), heads, n, og.ctypes.data, bg_.ctypes.data, bl.ctypes.data,
             idx.ctypes.data, C.byref(nb), C.byref(nd)))
         batches, k = [], 0
         for b in range(nb.value):
@@ -143,12 +141,13 @@ class Module:
             k += int(bl[b])
         return og, batches, [int(x) for x in idx[k:k + nd.value]]
 
-    def run(self, heads, burst=32):
+    def run(self, heads, burst=32, igate=0, now=None, device=-1):
         """a worker's synchronous loop (bg_module_run) over head addresses
         (numpy uintp) in bursts; -> gates"""
         heads = np.ascontiguousarray(heads, dtype=np.uintp)
         og = np.full(len(heads), BG_GATE_NONE, np.uint16)
-        _check(lib().bg_module_run(self.h, heads.ctypes.data, len(heads), burst,
+        _check(lib().bg_module_run(self.h, make_ctx(igate, now, device),
+                                   heads.ctypes.data, len(heads), burst,
                                    og.ctypes.data))
         return og
 
@@ -157,11 +156,13 @@ class Module:
         the first call every gate counts as connected"""
         _check(lib().bg_module_connect(self.h, ogate, 1 if connected else 0))
 
-    def process_device(self, d_frames, stride, n, d_ogates, stream=None):
-        """Device-resident ProcessBatch over a torch uint8 slab."""
+    def process_device(self, d_frames, stride, n, d_ogates, stream=None, igate=0,
+                       now=None):
+        """Device-resident ProcessBatch over a torch uint8 slab (on the
+        module's device)."""
         from .flowtable import _stream_ptr
         _check(lib().bg_module_process_device(
-            self.h, C.c_void_p(d_frames.data_ptr()), stride, n,
+            self.h, make_ctx(igate, now), C.c_void_p(d_frames.data_ptr()), stride, n,
             C.c_void_p(d_ogates.data_ptr()), _stream_ptr(stream)))
 
 
@@ -412,8 +413,9 @@ class Pipe:
         lib().bg_pipe_window(self.h, C.byref(lo), C.byref(hi), C.byref(st))
         return lo.value, hi.value, st.value
 
-    def submit(self, heads, lens=None, cookies=None):
-        """heads: numpy uintp array of head_data() addresses."""
+    def submit(self, heads, lens=None, cookies=None, igate=0, now=None):
+        """heads: numpy uintp array of head_data() addresses; igate / now:
+        the ProcessBatch's context."""
         heads = np.ascontiguousarray(heads, dtype=np.uintp)
         n = len(heads)
         lp = None
@@ -424,7 +426,8 @@ class Pipe:
         if cookies is not None:
             cookies = np.ascontiguousarray(cookies, dtype=np.uintp)
             cp = cookies.ctypes.data
-        _check(lib().bg_pipe_submit(self.h, heads.ctypes.data, lp, cp, n))
+        _check(lib().bg_pipe_submit(self.h, make_ctx(igate, now), heads.ctypes.data,
+                                    lp, cp, n))
 
     def flush(self):
         _check(lib().bg_pipe_flush(self.h))
@@ -440,7 +443,7 @@ class Pipe:
     def pending(self):
         return lib().bg_pipe_pending(self.h)
 
-    def run(self, heads, lens=None, burst=32):
+    def run(self, heads, lens=None, burst=32, igate=0, now=None):
         """native worker loop over all packets (bg_pipe_run); -> gates"""
         heads = np.ascontiguousarray(heads, dtype=np.uintp)
         n = len(heads)
@@ -449,7 +452,8 @@ class Pipe:
         if lens is not None:
             lens = np.ascontiguousarray(lens, dtype=np.uint16)
             lp = lens.ctypes.data
-        _check(lib().bg_pipe_run(self.h, heads.ctypes.data, lp, n, burst,
+        _check(lib().bg_pipe_run(self.h, make_ctx(igate, now), heads.ctypes.data,
+                                 lp, n, burst,
                                  og.ctypes.data))
         return og
 

@@ -387,6 +387,25 @@ int bg_ip_encap_host(int device, uint8_t *const *slots, size_t slot_bytes, size_
 
 /* ---- BESS module surface (protobuf arguments) -------------------------- */
 typedef struct bg_module bg_module;
+
+/* The per-call context of a ProcessBatch: what bessd's Context
+ * (core/module.h:59-75) carries into Module::ProcessBatch(ctx, batch) --
+ * the input gate the batch arrived on (ctx->current_igate: ACL emits on it,
+ * acl.cc:70; StaticNAT and NAT pick their direction by it, static_nat.cc:
+ * 146-181, nat.cc:321-363), the worker's clock (ctx->current_ns: NAT's
+ * mapping timestamps) and the worker (ctx->wid). It is passed with every
+ * datapath call and never stored in the module, so workers that feed one
+ * module through different input gates at the same time cannot see each
+ * other's values. `device`: the HIP device this call's work runs on (the
+ * module keeps a table replica per device); -1 = the module's device
+ * (bg_module_set_device, default 0). A NULL bg_ctx means igate 0, now =
+ * CLOCK_MONOTONIC at the call, device -1. */
+typedef struct bg_ctx {
+  uint64_t now_ns;
+  uint16_t igate;
+  int16_t device;
+  uint32_t wid;
+} bg_ctx;
 /* mclass: "ExactMatch", "WildcardMatch", "IPChecksum", "L4Checksum",
  * "HashLB", "ACL", "IPLookup", "UpdateTTL", "StaticNAT", "NAT".
  * arg: serialized bess.pb.<mclass>Arg. On failure returns -errno and the
@@ -405,37 +424,36 @@ int bg_module_command(bg_module *m, const char *cmd, const void *arg,
  * dropped (DropPacket, or EmitPacket to a gate that is out of range or not
  * connected, core/module.h:546-549), BG_GATE_NONE if it was not emitted.
  * Synchronous; may be called from many worker threads at once (each stages
- * into its own pinned buffers on its own HIP stream; core/module.h:485). */
-int bg_module_process(bg_module *m, uint8_t *const *heads, size_t cnt,
-                      uint16_t *ogates);
+ * into its own pinned buffers on its own HIP stream; core/module.h:485),
+ * each with its own ctx. */
+int bg_module_process(bg_module *m, const bg_ctx *ctx, uint8_t *const *heads,
+                      size_t cnt, uint16_t *ogates);
 /* bg_module_process plus the batches the Task would run next
  * (core/module.h:543-618): per output gate, packets in emission order cut
  * into batches of <= 32 (PacketBatch::kMaxBurst), in the order the batches
  * were started (Task::AddToRun). batch_gate / batch_len get *nbatches
  * entries; pkt_idx lists the batches' packet indices back to back, then the
  * *ndead dropped packets in drop order. Capacities: cnt each. */
-int bg_module_process_batches(bg_module *m, uint8_t *const *heads, size_t cnt,
+int bg_module_process_batches(bg_module *m, const bg_ctx *ctx,
+                              uint8_t *const *heads, size_t cnt,
                               uint16_t *ogates, uint16_t *batch_gate,
                               uint32_t *batch_len, uint32_t *pkt_idx,
                               size_t *nbatches, size_t *ndead);
 /* A worker's loop with the synchronous path: bg_module_process on each
  * `burst` packets of heads[0..n) in turn (ogates as bg_module_process). */
-int bg_module_run(bg_module *m, uint8_t *const *heads, size_t n, size_t burst,
-                  uint16_t *ogates);
+int bg_module_run(bg_module *m, const bg_ctx *ctx, uint8_t *const *heads,
+                  size_t n, size_t burst, uint16_t *ogates);
 /* Output gate `ogate` connected (1) or not (0) to a next module
  * (ConnectModules). Until the first call every gate < BG_MAX_GATES counts
  * as connected. EmitPacket to an unconnected gate drops the packet. */
 int bg_module_connect(bg_module *m, uint16_t ogate, int connected);
-/* Device-resident ProcessBatch over a slab. */
-int bg_module_process_device(bg_module *m, void *d_frames, size_t stride,
-                             size_t n, uint16_t *d_ogates, bg_stream_t stream);
+/* Device-resident ProcessBatch over a slab on ctx->device (the slab and
+ * gates must live there). */
+int bg_module_process_device(bg_module *m, const bg_ctx *ctx, void *d_frames,
+                             size_t stride, size_t n, uint16_t *d_ogates,
+                             bg_stream_t stream);
+/* the device of calls whose ctx says -1 (default 0); control path */
 int bg_module_set_device(bg_module *m, int device);
-/* the input gate the next process calls arrive on (ctx->current_igate:
- * ACL emits on it, StaticNAT picks its direction by it); default 0 */
-int bg_module_set_igate(bg_module *m, uint16_t igate);
-/* ctx->current_ns of the process calls that follow (NAT's mapping clock,
- * nat.cc:321-363); until set, CLOCK_MONOTONIC at each call */
-int bg_module_set_now(bg_module *m, uint64_t now_ns);
 /* Metadata layout for attr_name fields (ExactMatch, WildcardMatch): the
  * slot offset of each packet's metadata area and, by attribute name, the
  * offsets the pipeline assigned (Module::attr_offset, core/module.h). */
@@ -454,7 +472,13 @@ int bg_module_desc(const bg_module *m, char *buf, size_t len);
  *           bytes at most, data_len when lens != NULL) into a pinned slot;
  *           a full slot (batch packets) is launched on its own HIP stream:
  *           H2D -> device ProcessBatch -> D2H (gates [+ header lines]).
- *           Blocks only when all `depth` slots are in flight.
+ *           Blocks only when all `depth` slots are in flight. ctx: the
+ *           ProcessBatch's context (NULL as for bg_module_process; its
+ *           device is ignored: the pipe's device is fixed at create). A
+ *           slot holds packets of one context as far as the module reads
+ *           it on the device (ACL, StaticNAT: the input gate; NAT: the
+ *           gate and the clock): a submit whose context differs there
+ *           launches the filling slot first.
  *   flush:  launches the partially filled slot (a RunTask deadline).
  *   poll:   completed packets in submission order: cookie (default: the
  *           head pointer) and the gate EmitPacket would get (BG_GATE_NONE:
@@ -468,8 +492,8 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
                    size_t span, bg_pipe **out);
 void bg_pipe_destroy(bg_pipe *p); /* waits for in-flight slots */
 int bg_pipe_window(const bg_pipe *p, int *lo, int *hi, size_t *stride);
-int bg_pipe_submit(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
-                   void *const *cookies, size_t cnt);
+int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                   const uint16_t *lens, void *const *cookies, size_t cnt);
 int bg_pipe_flush(bg_pipe *p);
 long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
                   size_t cap);
@@ -477,8 +501,8 @@ size_t bg_pipe_pending(const bg_pipe *p);
 /* A worker loop (Source -> module -> Sink): n packets submitted in bursts of
  * `burst`, completions polled after each submit; ogates[i] = packet i's
  * gate. Returns when all n are back. */
-int bg_pipe_run(bg_pipe *p, uint8_t *const *heads, const uint16_t *lens,
-                size_t n, size_t burst, uint16_t *ogates);
+int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                const uint16_t *lens, size_t n, size_t burst, uint16_t *ogates);
 
 /* ---- Persistent classify kernel: a ring of batch descriptors ------------
  * BESS hands a module <= 32 packets per ProcessBatch (core/pktbatch.h:70);

@@ -53,16 +53,26 @@ class GpuModule : public Module {
     return CommandSuccess(*resp);
   }
 
-  // ProcessBatch on the GPU: ctx->current_igate (ACL, StaticNAT, NAT act on
-  // it) and ctx->current_ns (NAT's clock) go first
+  // bessd's per-call Context as the C ABI's bg_ctx: ctx->current_igate
+  // (ACL, StaticNAT, NAT act on it) and ctx->current_ns (NAT's clock) go
+  // with the call, never into the shared module
+  static bg_ctx CallCtx(const Context *ctx) {
+    bg_ctx c;
+    c.now_ns = ctx->current_ns;
+    c.igate = ctx->current_igate;
+    c.device = -1;
+    c.wid = (uint32_t)ctx->wid;
+    return c;
+  }
+
+  // ProcessBatch on the GPU, synchronously
   void Forward(Context *ctx, bess::PacketBatch *batch) {
     const int n = batch->cnt();
-    uint8_t *heads[bess::PacketBatch::kMaxBurst];
+    uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
     uint16_t og[bess::PacketBatch::kMaxBurst];
     for (int i = 0; i < n; i++) heads[i] = batch->pkts()[i]->head_data<uint8_t *>();
-    bg_module_set_igate(m_, ctx->current_igate);
-    bg_module_set_now(m_, ctx->current_ns);
-    if (bg_module_process(m_, heads, (size_t)n, og) < 0) {
+    const bg_ctx c = CallCtx(ctx);
+    if (bg_module_process(m_, &c, heads, (size_t)n, og) < 0) {
       for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
       return;
     }

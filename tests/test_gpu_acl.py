@@ -184,3 +184,46 @@ def test_add_clear_and_pipe():
     m.clear()
     o.clear()
     assert (device_gates(m, f, 64) == 8192).all()
+
+
+def test_concurrent_workers_on_different_input_gates():
+    """8 workers drive ONE ACL module at once, workers 0, 2, ... on input
+    gate 0 and 1, 3, ... on input gate 1 (ctx->current_igate per call,
+    core/module.h:59-75; acl.cc:70 emits a forwarded packet on it): every
+    worker's gates equal the oracle's for its own input gate -- the gate
+    travels with each call (bg_ctx), it is never module state. Then one
+    pipe whose submits alternate input gates: each slot keeps one gate."""
+    import threading
+    rules, f = workload(300, 8192, seed=88)
+    m = ACL(rules=rules)
+    o = OM.OracleACL(rules=rules)
+    want = {g: o.process(f, 64, len(f), igate=g) for g in (0, 1)}
+    assert (want[0] != want[1]).any()
+    heads = f.ctypes.data + 64 * np.arange(len(f), dtype=np.uintp)
+    got, errs = {}, []
+
+    def worker(w):
+        try:
+            outs = [m.run(heads, burst=32, igate=w % 2) for _ in range(6)]
+            got[w] = outs
+        except Exception as e:  # reported below
+            errs.append(e)
+    ths = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    for w in range(8):
+        for g in got[w]:
+            assert (g == want[w % 2]).all(), w
+    # one worker's pipe fed batches from both input gates in turn
+    p = Pipe(m, batch=4096, depth=3)
+    for i in range(0, len(f), 32):
+        p.submit(heads[i:i + 32], cookies=np.arange(i, i + 32, dtype=np.uintp),
+                 igate=(i // 32) % 2)
+    ck, g = p.drain()
+    p.close()
+    exp = np.where((ck // 32) % 2 == 1, want[1][ck], want[0][ck])
+    assert len(ck) == len(f) and (ck == np.arange(len(f))).all()
+    assert (g == exp).all()

@@ -187,10 +187,9 @@ def test_gpu_vs_oracle(stride, ihl_max, igate):
     ref = f.copy()
     want = OM.OracleStaticNAT(pairs=PAIRS).process(ref, stride, n, igate=igate)
     m = StaticNAT(pairs=PAIRS)
-    m.set_igate(igate)
     d = torch.from_numpy(f.reshape(-1)).cuda()
     og = torch.zeros(n, dtype=torch.int16, device="cuda")
-    m.process_device(d, stride, n, og)
+    m.process_device(d, stride, n, og, igate=igate)
     assert (og.cpu().numpy().view(np.uint16) == want).all()
     got = d.cpu().numpy().reshape(n, stride)
     bad = np.nonzero((got != ref).any(1))[0]
@@ -226,12 +225,11 @@ def test_gpu_module_host_path_and_pipe():
     f = nat_frames(n, 128, seed=9)
     ref = f.copy()
     want = OM.OracleStaticNAT(pairs=PAIRS).process(ref, 128, n, igate=1)
-    m.set_igate(1)
     g = f[:500].copy()
-    assert (m.process(g, 128, 500) == want[:500]).all()
+    assert (m.process(g, 128, 500, igate=1) == want[:500]).all()
     assert (g == ref[:500]).all()
     heads = f.ctypes.data + 128 * np.arange(n, dtype=np.uintp)
     p = Pipe(m, batch=4096, depth=3)
-    assert (p.run(heads) == want).all()
+    assert (p.run(heads, igate=1) == want).all()
     p.close()
     assert (f == ref).all()
