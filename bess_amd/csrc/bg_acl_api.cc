@@ -12,31 +12,32 @@
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
+#include <memory>
 #include <vector>
 
 #include "bg_internal.h"
 
 using namespace bg;
 
+// one device's image of one rule-list version: [rules][bit vectors][trees]
+struct AclImage : DevImage {
+  AclArgs a{};  // rules / bv / tree pointers into d and their geometry
+};
+
 struct bg_acl {
   std::vector<bg_acl_rule> rules;
-  bool dirty = true;
-  int device = -1;
-  uint32_t *d_rules = nullptr;
-  size_t d_cap = 0;  // rules
-  uint32_t *d_bv = nullptr;  // the bit-vector form (bv_args), or none
-  size_t bv_cap = 0;         // words
-  AclArgs bv_args{};         // its geometry and offsets (bv = d_bv)
-  uint32_t *d_tree = nullptr;  // the decision tree (tree_words, root), or none
-  size_t tree_cap = 0;         // words
-  uint32_t tree_words = 0, ntrees = 0, roots[4] = {};
+  // list changes bump the version; each device's image is rebuilt fresh at
+  // its next classify (bg_image.h)
+  std::atomic<uint64_t> version{1};
+  std::vector<uint32_t> host_img;  // the image of host_version
+  AclArgs host_a{};                // its launch arguments, offsets in words
+  uint64_t bv_off = 0, tree_off = 0;  // words (0: none)
+  uint64_t host_version = 0;
+  Published<AclImage> dev;
   std::mutex mu;
-  ~bg_acl() {
-    if (d_rules) (void)hipFree(d_rules);
-    if (d_bv) (void)hipFree(d_bv);
-    if (d_tree) (void)hipFree(d_tree);
-  }
 };
+
+static void acl_changed(bg_acl *h) { h->version.fetch_add(1, std::memory_order_acq_rel); }
 
 static uint16_t bswap16(uint16_t v) { return (uint16_t)((v >> 8) | (v << 8)); }
 
@@ -349,10 +350,9 @@ static bool build_tree(const std::vector<bg_acl_rule> &rules, std::vector<uint32
   return true;
 }
 
-static int acl_sync_locked(bg_acl *h, int dev, hipStream_t s) {
-  if (!h->dirty && h->device == dev && (h->d_rules || h->rules.empty())) return 0;
-  int r = set_device(dev);
-  if (r) return r;
+// the host image of the current list: rules, then the bit-vector form and
+// the decision trees when they are built, each 64-byte aligned
+static void acl_build_host(bg_acl *h) {
   const size_t n = h->rules.size();
   const size_t np = (n + 3) / 4 * 4;  // groups of 4; padding never valid
   std::vector<uint32_t> img(std::max<size_t>(np, 4) * 8, 0);
@@ -374,41 +374,58 @@ static int acl_sync_locked(bg_acl *h, int dev, hipStream_t s) {
   // the LDS scan then needs no validity test per rule
   for (size_t i = n; n && i < np; i++)
     memcpy(&img[i * 8], &img[(n - 1) * 8], 32);
-  if (!h->d_rules || h->d_cap < img.size() / 8 || h->device != dev) {
-    if (h->d_rules) (void)hipFree(h->d_rules);
-    h->d_rules = nullptr;
-    h->d_cap = std::max<size_t>(img.size() / 8, 64);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_rules), h->d_cap * 32));
-  }
-  HIP_TRY(hipMemcpyAsync(h->d_rules, img.data(), img.size() * 4,
-                         hipMemcpyHostToDevice, s));
+  AclArgs &a = h->host_a;
+  a = AclArgs{};
   std::vector<uint32_t> bv;
-  h->bv_args = AclArgs{};
-  if (build_bv(h->rules, &bv, &h->bv_args)) {
-    if (!h->d_bv || h->bv_cap < bv.size() || h->device != dev) {
-      if (h->d_bv) (void)hipFree(h->d_bv);
-      h->d_bv = nullptr;
-      h->bv_cap = bv.size();
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_bv), h->bv_cap * 4));
-    }
-    HIP_TRY(hipMemcpyAsync(h->d_bv, bv.data(), bv.size() * 4, hipMemcpyHostToDevice, s));
-    h->bv_args.bv = h->d_bv;
+  h->bv_off = h->tree_off = 0;
+  if (build_bv(h->rules, &bv, &a)) {  // geometry into a, words appended
+    h->bv_off = (img.size() + 15) / 16 * 16;
+    img.resize(h->bv_off, 0);
+    img.insert(img.end(), bv.begin(), bv.end());
   }
   std::vector<uint32_t> tree;
-  h->tree_words = 0;
-  if (build_tree(h->rules, &tree, h->roots, &h->ntrees)) {
-    if (!h->d_tree || h->tree_cap < tree.size() || h->device != dev) {
-      if (h->d_tree) (void)hipFree(h->d_tree);
-      h->d_tree = nullptr;
-      h->tree_cap = tree.size();
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tree), h->tree_cap * 4));
-    }
-    HIP_TRY(hipMemcpyAsync(h->d_tree, tree.data(), tree.size() * 4, hipMemcpyHostToDevice, s));
-    h->tree_words = (uint32_t)tree.size();
+  uint32_t roots[4] = {}, ntrees = 0;
+  if (build_tree(h->rules, &tree, roots, &ntrees)) {
+    h->tree_off = (img.size() + 15) / 16 * 16;
+    img.resize(h->tree_off, 0);
+    img.insert(img.end(), tree.begin(), tree.end());
+    a.tree_words = (uint32_t)tree.size();
+    a.ntrees = ntrees;
+    memcpy(a.roots, roots, sizeof(a.roots));
   }
-  HIP_TRY(hipStreamSynchronize(s));
-  h->device = dev;
-  h->dirty = false;
+  a.nrules = (uint32_t)np;
+  h->host_img.swap(img);
+}
+
+// the device's image of the current list (rebuilt fresh when it changed;
+// the replaced image is retired behind fences)
+static int acl_image(bg_acl *h, int dev, hipStream_t s, AclImage **out) {
+  AclImage *v = h->dev.get(dev);
+  const uint64_t ver = h->version.load(std::memory_order_acquire);
+  if (v && v->version == ver) {
+    *out = v;
+    return 0;
+  }
+  std::lock_guard<std::mutex> lk(h->mu);
+  v = h->dev.get(dev);
+  if (!v || v->version != ver) {
+    if (h->host_version != ver) {
+      acl_build_host(h);
+      h->host_version = ver;
+    }
+    std::unique_ptr<AclImage> img(new AclImage());
+    int r = upload_image(img.get(), dev, h->host_img.data(), h->host_img.size() * 4, s);
+    if (r) return r;
+    img->version = ver;
+    const uint32_t *b = reinterpret_cast<const uint32_t *>(img->d);
+    img->a = h->host_a;
+    img->a.rules = b;
+    img->a.bv = h->bv_off ? b + h->bv_off : nullptr;
+    img->a.tree = h->tree_off ? b + h->tree_off : nullptr;
+    v = img.get();
+    h->dev.publish(dev, img.release());
+  }
+  *out = v;
   return 0;
 }
 
@@ -426,14 +443,14 @@ int bg_acl_add(bg_acl *h, const bg_acl_rule *rules, size_t n) {
   if (n && !rules) return fail(EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(h->mu);
   h->rules.insert(h->rules.end(), rules, rules + n);
-  h->dirty = true;
+  acl_changed(h);
   return 0;
 }
 
 void bg_acl_clear(bg_acl *h) {
   std::lock_guard<std::mutex> lk(h->mu);
   h->rules.clear();
-  h->dirty = true;
+  acl_changed(h);
 }
 
 size_t bg_acl_count(const bg_acl *h) { return h->rules.size(); }
@@ -463,25 +480,10 @@ int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  AclArgs a;
-  memset(&a, 0, sizeof(a));
-  {
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (h->device >= 0) dev = h->device;
-    int r = acl_sync_locked(h, dev, s);
-    if (r) return r;
-    a = h->bv_args;  // the bit-vector form, when it was built
-    a.rules = h->d_rules;
-    if (h->tree_words) {
-      a.tree = h->d_tree;
-      a.tree_words = h->tree_words;
-      a.ntrees = h->ntrees;
-      memcpy(a.roots, h->roots, sizeof(a.roots));
-    }
-    a.nrules = (uint32_t)((h->rules.size() + 3) / 4 * 4);
-  }
-  int r = set_device(dev);
-  if (r) return r;
+  AclImage *img;
+  if (int r = acl_image(h, dev, s, &img)) return r;
+  AclArgs a = img->a;
+  img->used_on(s);
   a.frames = static_cast<const uint8_t *>(d_frames);
   a.stride = stride;
   a.n = n;

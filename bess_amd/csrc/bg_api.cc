@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -232,10 +233,12 @@ void DevTable::release() {
   valid = false;
 }
 
-TableRef DevTable::ref() const {
+TableRef table_ref(const uint8_t *base, uint64_t bytes, const TableLayout &L,
+                   uint64_t filt_off, uint32_t filt_words, bool tags_lds,
+                   uint64_t aux_off) {
   TableRef t;
   memset(&t, 0, sizeof(t));
-  t.base = d_image;
+  t.base = base;
   t.part_bytes = L.part_bytes;
   t.keys_off = L.keys_off;
   t.vals_off = L.vals_off;
@@ -253,6 +256,10 @@ TableRef DevTable::ref() const {
           : filt_words     ? kLdsFilter
                            : kLdsNone;
   return t;
+}
+
+TableRef DevTable::ref() const {
+  return table_ref(d_image, bytes, L, filt_off, filt_words, tags_lds, aux_off);
 }
 
 // Build a full single-device image (all partitions) from flat entries.
@@ -361,6 +368,11 @@ using namespace bg;
 // ============================================================================
 // ExactMatch
 // ============================================================================
+// one device's image of one rule-set version
+struct EmImage : DevImage {
+  TableRef t{};
+};
+
 struct bg_em {
   std::vector<bg_field> fields;
   bool has_attr = false;  // metadata-attribute fields (P15)
@@ -372,14 +384,20 @@ struct bg_em {
   uint32_t raw_size = 0;  // raw_key_size_ (sum of field sizes)
   uint32_t kw = 1;        // device key words (1, 2, 4, 8)
   std::unordered_map<Key, uint16_t, KeyHash> rules;
-  // set by rule changes (THREAD_UNSAFE commands, workers paused); cleared,
-  // after the device image is published, by the sync that rebuilt it
-  std::atomic<bool> dirty{true};
-  DevTable dev;
+  // Rule changes (THREAD_UNSAFE commands, workers paused) bump the version;
+  // a device's image is rebuilt into a fresh allocation at the next launch
+  // there, and the one it replaces is retired behind fences (bg_image.h).
+  std::atomic<uint64_t> version{1};
+  std::vector<uint8_t> host_img;  // the image of host_version (all devices)
+  TableLayout host_L{};
+  uint64_t host_version = 0;
+  Published<EmImage> dev;  // per device
   TableLayout planned;  // sharded build
   bool planned_valid = false;
   std::mutex mu;  // serialises sync (lookups from many workers never lock)
 };
+
+static void em_changed(bg_em *em) { em->version.fetch_add(1, std::memory_order_acq_rel); }
 
 static Key em_key(const bg_em *em, const uint8_t *key) {
   Key k;
@@ -459,7 +477,7 @@ int bg_em_create(const bg_field *fields, int nfields, bg_em **out) {
 
 void bg_em_destroy(bg_em *em) {
   if (!em) return;
-  em->dev.release();
+  em->dev.release();  // retired behind the fences of its launches
   delete em;
 }
 
@@ -468,7 +486,7 @@ size_t bg_em_key_size(const bg_em *em) { return em->key_size; }
 int bg_em_add(bg_em *em, const uint8_t *key, uint16_t gate) {
   if (em->key_size == 0) return fail(EINVAL, "rule has no fields");
   em->rules[em_key(em, key)] = gate;
-  em->dirty = true;
+  em_changed(em);
   return 0;
 }
 
@@ -476,13 +494,13 @@ int bg_em_delete(bg_em *em, const uint8_t *key) {
   if (em->key_size == 0) return fail(EINVAL, "rule has no fields");
   if (em->rules.erase(em_key(em, key)) == 0)
     return fail(ENOENT, "rule doesn't exist");
-  em->dirty = true;
+  em_changed(em);
   return 0;
 }
 
 void bg_em_clear(bg_em *em) {
   em->rules.clear();
-  em->dirty = true;
+  em_changed(em);
 }
 
 size_t bg_em_count(const bg_em *em) { return em->rules.size(); }
@@ -523,31 +541,55 @@ static bool em_vik(const bg_em *em) {
   return knob("BG_EM_VIK", 1) && em->raw_size + 2 <= em->kw * 8;
 }
 
+// the device's image if it is of the current rule-set version
+static EmImage *em_fresh(bg_em *em, int device) {
+  EmImage *v = em->dev.get(device);
+  return v && v->version == em->version.load(std::memory_order_acquire) ? v : nullptr;
+}
+
 static int em_sync_locked(bg_em *em, int device, hipStream_t s) {
-  if (!em->dirty && em->dev.valid && em->dev.device == device) return 0;
-  std::vector<uint64_t> keys, seeds;
-  std::vector<uint8_t> vals, img;
-  em_entries(em, &keys, &vals, &seeds);
-  TableLayout L;
-  int r = build_image(em->kw, 2, 1, keys, vals, seeds, &img, &L, 0.75, em_vik(em));
+  if (em_fresh(em, device)) return 0;
+  const uint64_t ver = em->version.load(std::memory_order_acquire);
+  if (em->host_version != ver) {  // once per version, for every device
+    std::vector<uint64_t> keys, seeds;
+    std::vector<uint8_t> vals;
+    em_entries(em, &keys, &vals, &seeds);
+    TableLayout L;
+    int r = build_image(em->kw, 2, 1, keys, vals, seeds, &em->host_img, &L, 0.75,
+                        em_vik(em));
+    if (r) return r;
+    em->host_L = L;
+    em->host_version = ver;
+  }
+  std::unique_ptr<EmImage> img(new EmImage());
+  int r = upload_image(img.get(), device, em->host_img.data(), em->host_img.size(), s);
   if (r) return r;
-  r = em->dev.upload(device, img, L, s);
-  if (r) return r;
-  em->dirty = false;
+  img->version = ver;
+  img->t = table_ref(img->d, img->bytes, em->host_L, 0, 0, false, 0);
+  em->dev.publish(device, img.release());
+  return 0;
+}
+
+// The image launches on `device` read, rebuilt first if the rules changed
+// (lock-free when it is current: the per-batch calls of many workers).
+static int em_image(bg_em *em, int device, hipStream_t s, EmImage **out) {
+  EmImage *v = em_fresh(em, device);
+  if (!v) {
+    std::lock_guard<std::mutex> lk(em->mu);
+    if (int r = em_sync_locked(em, device, s)) return r;
+    v = em->dev.get(device);
+  }
+  *out = v;
   return 0;
 }
 
 int bg_em_sync(bg_em *em, int device, bg_stream_t stream) {
-  // fast path for the per-batch calls of many workers: no lock
-  if (!em->dirty.load(std::memory_order_acquire) && em->dev.valid &&
-      em->dev.device == device)
-    return 0;
-  std::lock_guard<std::mutex> lk(em->mu);
-  return em_sync_locked(em, device, (hipStream_t)stream);
+  EmImage *img;
+  return em_image(em, device, (hipStream_t)stream, &img);
 }
 
-static int em_launch(bg_em *em, const void *d_frames, size_t stride, size_t n,
-                     uint16_t default_gate, uint16_t *d_gates, int shift,
+static int em_launch(bg_em *em, EmImage *img, const void *d_frames, size_t stride,
+                     size_t n, uint16_t default_gate, uint16_t *d_gates, int shift,
                      hipStream_t s) {
   EmArgs a;
   memset(&a, 0, sizeof(a));
@@ -557,9 +599,17 @@ static int em_launch(bg_em *em, const void *d_frames, size_t stride, size_t n,
   a.gates = d_gates;
   a.default_gate = default_gate;
   a.fp = make_plan(em->dfields, true, shift);
-  a.t = em->dev.ref();
-  HIP_TRY(launch_em(a, num_cus(em->dev.device), s));
+  a.t = img->t;
+  img->used_on(s);
+  HIP_TRY(launch_em(a, num_cus(img->device), s));
   return 0;
+}
+
+// the calling thread's current HIP device (classify calls run there)
+static int current_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
 }
 
 // Every byte a classify kernel reads for packet i lies in its slot, so the
@@ -621,12 +671,10 @@ namespace bg {
 int em_device_plan(bg_em *em, int device, hipStream_t s, FieldPlan *fp,
                    TableRef *t, int *read_end) {
   if (em->has_attr && !em->meta_bound) return no_attr_datapath();
-  {
-    std::lock_guard<std::mutex> lk(em->mu);
-    if (int r = em_sync_locked(em, device, s)) return r;
-  }
+  EmImage *img;
+  if (int r = em_image(em, device, s, &img)) return r;
   *fp = make_plan(em->dfields, true, 0);
-  *t = em->dev.ref();
+  *t = img->t;
   int hi = 0;  // bytes of a slot the kernel reads (check_extent)
   if (!fp->direct) {
     hi = fp->nf ? fp->win_lo + 16 * fp->nch : 0;
@@ -666,17 +714,10 @@ int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   if (int r = check_extent(em->dfields, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
-  // acquire: a clean flag publishes the device image the sync built
-  if (em->dirty.load(std::memory_order_acquire) || !em->dev.valid) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    std::lock_guard<std::mutex> lk(em->mu);
-    int r = em_sync_locked(em, em->dev.valid ? em->dev.device : cur, s);
-    if (r) return r;
-  }
-  int r = set_device(em->dev.device);
-  if (r) return r;
-  return em_launch(em, d_frames, stride, n, default_gate, d_gates, -win_off, s);
+  const int dev = current_device();
+  EmImage *img;
+  if (int r = em_image(em, dev, s, &img)) return r;
+  return em_launch(em, img, d_frames, stride, n, default_gate, d_gates, -win_off, s);
 }
 
 // Stage [lo, hi) of every head (window covering all fields) at a fixed
@@ -710,25 +751,18 @@ int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
                        bg_stream_t stream) {
   if (em->has_attr) return no_attr_datapath();
   if (n == 0) return 0;
-  if (em->dirty.load(std::memory_order_acquire) || !em->dev.valid) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    std::lock_guard<std::mutex> lk(em->mu);
-    int r = em_sync_locked(em, em->dev.valid ? em->dev.device : cur,
-                           thread_stream(cur, (hipStream_t)stream));
-    if (r) return r;
-  }
-  const int dev = em->dev.device;
-  int r = set_device(dev);
-  if (r) return r;
+  const int dev = current_device();
   hipStream_t s = thread_stream(dev, (hipStream_t)stream);
+  EmImage *img;
+  int r = em_image(em, dev, s, &img);
+  if (r) return r;
   Staging &st = thread_staging();
   int shift;
   size_t w;
   r = stage_windows(em->fields, heads, n, st, dev, &shift, &w);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
-  r = em_launch(em, st.d_in, w, n, default_gate,
+  r = em_launch(em, img, st.d_in, w, n, default_gate,
                 reinterpret_cast<uint16_t *>(st.d_out), shift, s);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 2, hipMemcpyDeviceToHost, s));
@@ -776,7 +810,7 @@ int bg_em_add_many(bg_em *em, const uint8_t *keys, size_t n, size_t key_stride,
     if (part >= 0 && key_part(em, k.w, nparts) != (uint32_t)part) continue;
     em->rules[k] = gates[i];
   }
-  em->dirty = true;
+  em_changed(em);
   return 0;
 }
 
@@ -845,24 +879,29 @@ int bg_em_build_part(bg_em *em, int part, void *host_dst) {
   return 0;
 }
 
+// The assembled image becomes the device's image of the current rule set
+// (the caller keeps the memory; a later rule change rebuilds from the rules
+// this handle holds).
 int bg_em_attach(bg_em *em, int device, const void *d_image) {
   if (!em->planned_valid) return fail(EINVAL, "bg_em_plan first");
+  if (device < 0 || device >= kMaxDevices) return fail(ENODEV, "device %d", device);
   std::lock_guard<std::mutex> lk(em->mu);
-  em->dev.release();
-  em->dev.d_image = static_cast<uint8_t *>(const_cast<void *>(d_image));
-  em->dev.owned = false;
-  em->dev.device = device;
-  em->dev.L = em->planned;
-  em->dev.bytes = em->planned.part_bytes * em->planned.nparts;
-  em->dev.valid = true;
-  em->dirty = false;
+  EmImage *img = new EmImage();
+  img->device = device;
+  img->d = static_cast<uint8_t *>(const_cast<void *>(d_image));
+  img->owned = false;
+  img->bytes = em->planned.part_bytes * em->planned.nparts;
+  img->version = em->version.load(std::memory_order_acquire);
+  img->t = table_ref(img->d, img->bytes, em->planned, 0, 0, false, 0);
+  em->dev.publish(device, img);
   return 0;
 }
 
 int bg_em_table_info(const bg_em *em, uint64_t *bytes, int *in_lds) {
-  if (!em->dev.valid) return fail(EINVAL, "no device table yet");
-  *bytes = em->dev.bytes;
-  *in_lds = em->dev.ref().lds ? 1 : 0;
+  const EmImage *img = const_cast<bg_em *>(em)->dev.get(current_device());
+  if (!img) return fail(EINVAL, "no device table yet");
+  *bytes = img->bytes;
+  *in_lds = img->t.lds ? 1 : 0;
   return 0;
 }
 
@@ -876,6 +915,13 @@ struct WmTupleH {
   std::unordered_map<Key, WmVal, KeyHash> ht;
 };
 
+// one device's image of one rule-set version, with the launch arguments
+// that go with it (tuple masks, seeds, direct tuples)
+struct WmImage : DevImage {
+  WmArgs a{};
+  bool no_tags = false;  // BG_PATH_WM_NO_TAGS when it was built
+};
+
 struct bg_wm {
   std::vector<bg_field> fields;
   bool has_attr = false;
@@ -884,15 +930,21 @@ struct bg_wm {
   uint32_t key_size = 0;
   uint32_t kw = 1;
   std::vector<WmTupleH> tuples;
-  std::atomic<bool> dirty{true};  // as bg_em::dirty
-  bool built_no_tags = false;     // BG_PATH_WM_NO_TAGS when the image was built
-  DevTable dev;
-  // direct tuples of the image (WmArgs::ndirect ...), set with it
+  std::atomic<uint64_t> version{1};  // as bg_em::version
+  // the host image of (host_version, host_no_tags) and its launch arguments
+  std::vector<uint8_t> host_img;
+  WmArgs host_a{};
+  uint64_t host_version = 0;
+  bool host_no_tags = false;
+  Published<WmImage> dev;
+  // direct tuples of the image being built (WmArgs::ndirect ...)
   uint32_t ndirect = 0;
   uint32_t dtu[kMaxDirect] = {}, dspec[kMaxDirect] = {};
   uint64_t doff[kMaxDirect] = {};
   std::mutex mu;
 };
+
+static void wm_changed(bg_wm *wm) { wm->version.fetch_add(1, std::memory_order_acq_rel); }
 
 static Key wm_key(const bg_wm *wm, const uint8_t *p) {
   Key k;
@@ -932,7 +984,7 @@ int bg_wm_create(const bg_field *fields, int nfields, bg_wm **out) {
 
 void bg_wm_destroy(bg_wm *wm) {
   if (!wm) return;
-  wm->dev.release();
+  wm->dev.release();  // retired behind the fences of its launches
   delete wm;
 }
 
@@ -950,7 +1002,7 @@ int bg_wm_add(bg_wm *wm, const uint8_t *key, const uint8_t *mask,
     idx = (int)wm->tuples.size() - 1;
   }
   wm->tuples[idx].ht[wm_key(wm, key)] = WmVal{priority, gate};
-  wm->dirty = true;
+  wm_changed(wm);
   return 0;
 }
 
@@ -961,13 +1013,13 @@ int bg_wm_delete(bg_wm *wm, const uint8_t *key, const uint8_t *mask) {
   WmTupleH &t = wm->tuples[idx];
   if (t.ht.erase(wm_key(wm, key)) == 0 && t.ht.empty())
     wm->tuples.erase(wm->tuples.begin() + idx);  // DelEntry quirk (P6)
-  wm->dirty = true;
+  wm_changed(wm);
   return 0;
 }
 
 void bg_wm_clear(bg_wm *wm) {
   for (auto &t : wm->tuples) t.ht.clear();
-  wm->dirty = true;
+  wm_changed(wm);
 }
 
 int bg_wm_num_tuples(const bg_wm *wm) { return (int)wm->tuples.size(); }
@@ -1094,13 +1146,12 @@ static void wm_entries(const bg_wm *wm, std::vector<uint64_t> *keys,
   }
 }
 
-static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
-  const bool no_tags = wm_want_no_tags();
-  if (!wm->dirty && wm->dev.valid && wm->dev.device == device &&
-      wm->built_no_tags == no_tags)
-    return 0;
+// the host image of the current rules and the launch arguments that go with
+// it (wm->host_img / host_a), built once per version for every device
+static int wm_build_host(bg_wm *wm, bool no_tags) {
   std::vector<uint64_t> keys, hashes;
-  std::vector<uint8_t> vals, img;
+  std::vector<uint8_t> vals;
+  std::vector<uint8_t> &img = wm->host_img;
   wm->ndirect = 0;
   wm_entries(wm, &keys, &vals, &hashes);
   TableLayout L;
@@ -1174,38 +1225,11 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
       f[q.word] |= q.bits;
     }
   }
-  r = wm->dev.upload(device, img, L, s);
-  if (r) return r;
-  wm->dev.aux_off = aux_off;
-  wm->dev.filt_off = foff;
-  wm->dev.filt_words = fw;
-  wm->dev.tags_lds = tags_lds;
-  wm->built_no_tags = no_tags;
-  wm->dirty = false;
-  return 0;
-}
-
-int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream) {
-  if (!wm->dirty.load(std::memory_order_acquire) && wm->dev.valid &&
-      wm->dev.device == device && wm->built_no_tags == wm_want_no_tags())
-    return 0;
-  std::lock_guard<std::mutex> lk(wm->mu);
-  return wm_sync_locked(wm, device, (hipStream_t)stream);
-}
-
-static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
-                     uint16_t default_gate, uint16_t *d_gates, int shift,
-                     hipStream_t s) {
-  WmArgs a;
+  // the launch arguments of this image (base pointer filled per device)
+  WmArgs &a = wm->host_a;
   memset(&a, 0, sizeof(a));
-  a.frames = static_cast<const uint8_t *>(d_frames);
-  a.stride = stride;
-  a.n = n;
-  a.gates = d_gates;
-  a.default_gate = default_gate;
+  a.t = table_ref(nullptr, img.size(), L, foff, fw, tags_lds, aux_off);
   a.ntuples = (uint32_t)wm->tuples.size();
-  a.fp = make_plan(wm->dfields, false, shift);
-  a.t = wm->dev.ref();
   for (size_t t = 0; t < wm->tuples.size(); t++) {
     for (uint32_t j = 0; j < wm->kw; j++) a.tmask[t][j] = wm->tuples[t].mask.w[j];
     a.tcover[t] = wm_cover(wm, t);
@@ -1217,8 +1241,68 @@ static int wm_launch(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
     a.dspec[d] = wm->dspec[d];
     a.doff[d] = wm->doff[d];
   }
+  return 0;
+}
+
+// the device's image if it is of the current version and path flags
+static WmImage *wm_fresh(bg_wm *wm, int device) {
+  WmImage *v = wm->dev.get(device);
+  return v && v->version == wm->version.load(std::memory_order_acquire) &&
+                 v->no_tags == wm_want_no_tags()
+             ? v
+             : nullptr;
+}
+
+static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
+  if (wm_fresh(wm, device)) return 0;
+  const uint64_t ver = wm->version.load(std::memory_order_acquire);
+  const bool no_tags = wm_want_no_tags();
+  if (wm->host_version != ver || wm->host_no_tags != no_tags) {
+    if (int r = wm_build_host(wm, no_tags)) return r;
+    wm->host_version = ver;
+    wm->host_no_tags = no_tags;
+  }
+  std::unique_ptr<WmImage> img(new WmImage());
+  int r = upload_image(img.get(), device, wm->host_img.data(), wm->host_img.size(), s);
+  if (r) return r;
+  img->version = ver;
+  img->no_tags = no_tags;
+  img->a = wm->host_a;
+  img->a.t.base = img->d;
+  wm->dev.publish(device, img.release());
+  return 0;
+}
+
+// as em_image
+static int wm_image(bg_wm *wm, int device, hipStream_t s, WmImage **out) {
+  WmImage *v = wm_fresh(wm, device);
+  if (!v) {
+    std::lock_guard<std::mutex> lk(wm->mu);
+    if (int r = wm_sync_locked(wm, device, s)) return r;
+    v = wm->dev.get(device);
+  }
+  *out = v;
+  return 0;
+}
+
+int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream) {
+  WmImage *img;
+  return wm_image(wm, device, (hipStream_t)stream, &img);
+}
+
+static int wm_launch(bg_wm *wm, WmImage *img, const void *d_frames, size_t stride,
+                     size_t n, uint16_t default_gate, uint16_t *d_gates, int shift,
+                     hipStream_t s) {
+  WmArgs a = img->a;
+  a.frames = static_cast<const uint8_t *>(d_frames);
+  a.stride = stride;
+  a.n = n;
+  a.gates = d_gates;
+  a.default_gate = default_gate;
+  a.fp = make_plan(wm->dfields, false, shift);
   a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
-  HIP_TRY(launch_wm(a, num_cus(wm->dev.device), s));
+  img->used_on(s);
+  HIP_TRY(launch_wm(a, num_cus(img->device), s));
   return 0;
 }
 
@@ -1247,17 +1331,9 @@ int bg_wm_classify_window(bg_wm *wm, const void *d_frames, size_t stride,
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
   if (int r = check_extent(wm->dfields, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
-  if (wm->dirty.load(std::memory_order_acquire) || !wm->dev.valid ||
-      wm->built_no_tags != wm_want_no_tags()) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    std::lock_guard<std::mutex> lk(wm->mu);
-    int r = wm_sync_locked(wm, wm->dev.valid ? wm->dev.device : cur, s);
-    if (r) return r;
-  }
-  int r = set_device(wm->dev.device);
-  if (r) return r;
-  return wm_launch(wm, d_frames, stride, n, default_gate, d_gates, -win_off, s);
+  WmImage *img;
+  if (int r = wm_image(wm, current_device(), s, &img)) return r;
+  return wm_launch(wm, img, d_frames, stride, n, default_gate, d_gates, -win_off, s);
 }
 
 int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
@@ -1265,26 +1341,18 @@ int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
                        bg_stream_t stream) {
   if (wm->has_attr) return no_attr_datapath();
   if (n == 0) return 0;
-  if (wm->dirty.load(std::memory_order_acquire) || !wm->dev.valid ||
-      wm->built_no_tags != wm_want_no_tags()) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    std::lock_guard<std::mutex> lk(wm->mu);
-    int r = wm_sync_locked(wm, wm->dev.valid ? wm->dev.device : cur,
-                           thread_stream(cur, (hipStream_t)stream));
-    if (r) return r;
-  }
-  const int dev = wm->dev.device;
-  int r = set_device(dev);
-  if (r) return r;
+  const int dev = current_device();
   hipStream_t s = thread_stream(dev, (hipStream_t)stream);
+  WmImage *img;
+  int r = wm_image(wm, dev, s, &img);
+  if (r) return r;
   Staging &st = thread_staging();
   int shift;
   size_t w;
   r = stage_windows(wm->fields, heads, n, st, dev, &shift, &w);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
-  r = wm_launch(wm, st.d_in, w, n, default_gate,
+  r = wm_launch(wm, img, st.d_in, w, n, default_gate,
                 reinterpret_cast<uint16_t *>(st.d_out), shift, s);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 2, hipMemcpyDeviceToHost, s));
@@ -1298,10 +1366,11 @@ void bg_wm_window(const bg_wm *wm, int *lo, int *hi) {
 }
 
 int bg_wm_table_info(const bg_wm *wm, uint64_t *bytes, int *in_lds) {
-  if (!wm->dev.valid) return fail(EINVAL, "no device table yet");
-  *bytes = wm->dev.bytes;
+  const WmImage *img = const_cast<bg_wm *>(wm)->dev.get(current_device());
+  if (!img) return fail(EINVAL, "no device table yet");
+  *bytes = img->bytes;
   // 2: key filter in LDS, 3: tag words in LDS; bits 8+: direct tuples
-  *in_lds = (int)wm->dev.ref().lds | (int)(wm->ndirect << 8);
+  *in_lds = (int)img->a.t.lds | (int)(img->a.ndirect << 8);
   return 0;
 }
 

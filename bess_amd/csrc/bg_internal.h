@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/bessgpu.h"
+#include "bg_image.h"
 #include "bg_kernels.h"
 #include "bg_table.h"
 
@@ -56,6 +57,15 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
                 TableLayout *out_layout, double max_load = 0.75,
                 bool vik = false, uint32_t probe = 0);
 
+// The TableRef of a table image at `base` (bytes long, layout L; a key
+// filter / direct-tuple tables appended at filt_off / aux_off).
+TableRef table_ref(const uint8_t *base, uint64_t bytes, const TableLayout &L,
+                   uint64_t filt_off, uint32_t filt_words, bool tags_lds,
+                   uint64_t aux_off);
+
+// A single-device table image updated in place in stream order (NAT's
+// lookup copy, bg_dnat_api.cc: its batches run one at a time under the
+// module's lock and are synchronous). Rule tables use bg_image.h instead.
 struct DevTable {
   int device = -1;
   uint8_t *d_image = nullptr;

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -41,40 +42,58 @@ std::vector<uint32_t> position_tables(uint32_t L) {
 
 }  // namespace
 
+// one device's image of one mode + gate-table version: [crc tables][gates]
+struct HlbImage : DevImage {
+  HlbArgs a{};                  // tables into d, mode, geometry
+  std::vector<bg_field> fields;  // fields mode: the key's fields
+};
+
 struct bg_hlb {
   int mode = kHlbL4;
   std::vector<bg_field> fields;
   uint32_t L = 4;  // hash input bytes
   std::vector<uint16_t> gates{0};  // gates_[0 .. max(n, 1))
   uint32_t num_gates = 0;
-  bool dirty = true;
-  int device = -1;
-  uint8_t *d_buf = nullptr;  // [crc tables][gate table]
-  size_t d_cap = 0;
+  // set_mode / set_gates bump the version; each device's image is rebuilt
+  // fresh at its next classify (bg_image.h)
+  std::atomic<uint64_t> version{1};
+  Published<HlbImage> dev;
   std::mutex mu;
-  ~bg_hlb() {
-    if (d_buf) (void)hipFree(d_buf);
-  }
 };
 
-static int hlb_sync_locked(bg_hlb *h, int dev, hipStream_t s) {
-  if (!h->dirty && h->device == dev && h->d_buf) return 0;
-  int r = set_device(dev);
-  if (r) return r;
-  std::vector<uint32_t> T = position_tables(h->L);
-  const size_t tb = T.size() * 4, gb = h->gates.size() * 2;
-  if (!h->d_buf || h->d_cap < tb + gb || h->device != dev) {
-    if (h->d_buf) (void)hipFree(h->d_buf);
-    h->d_buf = nullptr;
-    h->d_cap = std::max<size_t>(tb + gb, 64 * 1024 + 32 * 1024 + 64);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_buf), h->d_cap));
+static void hlb_changed(bg_hlb *h) { h->version.fetch_add(1, std::memory_order_acq_rel); }
+
+static int hlb_image(bg_hlb *h, int dev, hipStream_t s, HlbImage **out) {
+  HlbImage *v = h->dev.get(dev);
+  const uint64_t ver = h->version.load(std::memory_order_acquire);
+  if (v && v->version == ver) {
+    *out = v;
+    return 0;
   }
-  HIP_TRY(hipMemcpyAsync(h->d_buf, T.data(), tb, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(h->d_buf + tb, h->gates.data(), gb,
-                         hipMemcpyHostToDevice, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  h->device = dev;
-  h->dirty = false;
+  std::lock_guard<std::mutex> lk(h->mu);
+  v = h->dev.get(dev);
+  if (!v || v->version != ver) {
+    std::vector<uint32_t> T = position_tables(h->L);
+    const size_t tb = T.size() * 4, gb = h->gates.size() * 2;
+    std::vector<uint8_t> img(tb + gb);
+    memcpy(img.data(), T.data(), tb);
+    memcpy(img.data() + tb, h->gates.data(), gb);
+    std::unique_ptr<HlbImage> p(new HlbImage());
+    int r = upload_image(p.get(), dev, img.data(), img.size(), s);
+    if (r) return r;
+    p->version = ver;
+    p->a.crc_tab = reinterpret_cast<const uint32_t *>(p->d);
+    p->a.gtab = reinterpret_cast<const uint16_t *>(p->d + tb);
+    p->a.mode = (uint32_t)h->mode;
+    p->a.L = h->L;
+    p->a.num_gates = h->num_gates;
+    p->a.ngtab = (uint32_t)h->gates.size();
+    p->fields = h->fields;
+    for (auto &x : p->fields) x.mask = 0;  // AddField(offset, size, 0, i): all bits
+    v = p.get();
+    h->dev.publish(dev, p.release());
+  }
+  *out = v;
   return 0;
 }
 
@@ -121,7 +140,7 @@ int bg_hlb_set_mode(bg_hlb *h, int mode, const bg_field *fields, int nfields,
     h->L = mode == BG_HLB_L2 ? 2 : 4;
   }
   h->mode = mode;
-  h->dirty = true;
+  hlb_changed(h);
   return 0;
 }
 
@@ -132,7 +151,7 @@ int bg_hlb_set_gates(bg_hlb *h, const uint16_t *gates, size_t n,
   std::lock_guard<std::mutex> lk(h->mu);
   h->gates.assign(gates, gates + n);
   h->num_gates = (uint32_t)num_gates;
-  h->dirty = true;
+  hlb_changed(h);
   return 0;
 }
 
@@ -162,29 +181,13 @@ int bg_hlb_classify(bg_hlb *h, const void *d_frames, size_t stride, size_t n,
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  HlbArgs a;
-  memset(&a, 0, sizeof(a));
-  {
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (h->device >= 0) dev = h->device;
-    int r = hlb_sync_locked(h, dev, s);
-    if (r) return r;
-    a.crc_tab = reinterpret_cast<const uint32_t *>(h->d_buf);
-    a.gtab = reinterpret_cast<const uint16_t *>(h->d_buf + (size_t)h->L * 1024);
-    a.mode = (uint32_t)h->mode;
-    a.L = h->L;
-    a.num_gates = h->num_gates;
-    a.ngtab = (uint32_t)h->gates.size();
-    if (h->mode == BG_HLB_FIELDS) {
-      std::vector<bg_field> f = h->fields;
-      for (auto &x : f) x.mask = 0;  // AddField(offset, size, 0, i): all bits
-      a.fp = make_plan(f, false, -win_off);
-    }
-  }
-  if (h->mode != BG_HLB_FIELDS && stride < (size_t)(h->mode == BG_HLB_L2 ? 16 : 64))
+  HlbImage *img;
+  if (int r = hlb_image(h, dev, s, &img)) return r;
+  HlbArgs a = img->a;
+  if (a.mode == (uint32_t)BG_HLB_FIELDS) a.fp = make_plan(img->fields, false, -win_off);
+  if (a.mode != (uint32_t)BG_HLB_FIELDS && stride < (size_t)(a.mode == BG_HLB_L2 ? 16 : 64))
     return fail(EINVAL, "stride %zu too small for the mode", stride);
-  int r = set_device(dev);
-  if (r) return r;
+  img->used_on(s);
   a.frames = static_cast<const uint8_t *>(d_frames);
   a.stride = stride;
   a.n = n;

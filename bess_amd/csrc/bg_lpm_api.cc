@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -25,32 +26,30 @@ uint32_t depth_mask(int depth) {
 }
 }  // namespace
 
+// one device's tables of one route-set version: [tbl24][tbl8][tbl16][tbl2]
+struct LpmImage : DevImage {
+  LpmArgs a{};  // the table pointers into d
+};
+
 struct bg_lpm {
   uint32_t max_rules = 1024, max_tbl8s = 128;
   // (depth, masked ip) -> next hop: map order = ascending depth, the order
   // DIR-24-8 is filled in (longer prefixes overwrite shorter ones)
   std::map<std::pair<int, uint32_t>, uint32_t> rules;
   std::map<uint32_t, int> ext;  // /24 block -> rules deeper than /24 in it
-  bool dirty = true;
-  int device = -1;
-  uint16_t *d_tbl24 = nullptr, *d_tbl8 = nullptr;
-  size_t d_cap8 = 0;  // groups
-  uint16_t *d_tbl16 = nullptr, *d_tbl2 = nullptr;  // DIR-16-8-8 (or none)
-  size_t d_cap2 = 0;  // groups
-  bool has16 = false;
+  // route changes bump the version; each device's tables are rebuilt into a
+  // fresh image at its next lookup (bg_image.h)
+  std::atomic<uint64_t> version{1};
+  std::vector<uint8_t> host_img;  // the tables of host_version
+  uint64_t off8 = 0, off16 = 0, off2 = 0;  // their offsets (off16 0: none)
+  uint64_t host_version = 0;
+  Published<LpmImage> dev;
   std::mutex mu;
-  ~bg_lpm() {
-    if (d_tbl24) (void)hipFree(d_tbl24);
-    if (d_tbl8) (void)hipFree(d_tbl8);
-    if (d_tbl16) (void)hipFree(d_tbl16);
-    if (d_tbl2) (void)hipFree(d_tbl2);
-  }
 };
 
-static int lpm_sync_locked(bg_lpm *h, int dev, hipStream_t s) {
-  if (!h->dirty && h->device == dev && h->d_tbl24) return 0;
-  int r = set_device(dev);
-  if (r) return r;
+static void lpm_changed(bg_lpm *h) { h->version.fetch_add(1, std::memory_order_acq_rel); }
+
+static int lpm_build_host(bg_lpm *h) {
   std::vector<uint16_t> t24(kTbl24, 0);
   std::vector<uint16_t> t8;
   std::map<uint32_t, std::vector<std::pair<int, uint32_t>>> deep;  // block -> rules
@@ -75,25 +74,11 @@ static int lpm_sync_locked(bg_lpm *h, int dev, hipStream_t s) {
     t24[b.first] = (uint16_t)(0x8000u | g);
     g++;
   }
-  if (!h->d_tbl24 || h->device != dev) {
-    if (h->d_tbl24) (void)hipFree(h->d_tbl24);
-    h->d_tbl24 = nullptr;
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl24), (size_t)kTbl24 * 2));
-  }
-  const size_t ng = std::max<size_t>(g, 1);
-  if (!h->d_tbl8 || h->d_cap8 < ng || h->device != dev) {
-    if (h->d_tbl8) (void)hipFree(h->d_tbl8);
-    h->d_tbl8 = nullptr;
-    h->d_cap8 = std::max<size_t>(ng, 64);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl8), h->d_cap8 * 512));
-  }
-  HIP_TRY(hipMemcpyAsync(h->d_tbl24, t24.data(), (size_t)kTbl24 * 2,
-                         hipMemcpyHostToDevice, s));
   // DIR-16-8-8: a /16 block whose 256 tbl24 entries are one plain value
   // keeps it in tbl16; any other block gets a tbl2 group (its entries)
   std::vector<uint16_t> t16(1u << 16), t2;
-  h->has16 = true;
-  for (uint32_t b = 0; b < (1u << 16) && h->has16; b++) {
+  bool has16 = true;
+  for (uint32_t b = 0; b < (1u << 16) && has16; b++) {
     const uint16_t *seg = t24.data() + (size_t)b * 256;
     const bool flat = !(seg[0] & 0x8000u) && std::all_of(seg, seg + 256, [&](uint16_t v) {
       return v == seg[0];
@@ -101,35 +86,58 @@ static int lpm_sync_locked(bg_lpm *h, int dev, hipStream_t s) {
     if (flat) {
       t16[b] = seg[0];
     } else if (t2.size() / 256 >= kMaxGroups) {
-      h->has16 = false;  // past 15-bit group indices: DIR-24-8 only
+      has16 = false;  // past 15-bit group indices: DIR-24-8 only
     } else {
       t16[b] = (uint16_t)(0x8000u | (t2.size() / 256));
       t2.insert(t2.end(), seg, seg + 256);
     }
   }
-  if (h->has16) {
-    if (!h->d_tbl16 || h->device != dev) {
-      if (h->d_tbl16) (void)hipFree(h->d_tbl16);
-      h->d_tbl16 = nullptr;
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl16), t16.size() * 2));
-    }
-    const size_t ng2 = std::max<size_t>(t2.size() / 256, 1);
-    if (!h->d_tbl2 || h->d_cap2 < ng2 || h->device != dev) {
-      if (h->d_tbl2) (void)hipFree(h->d_tbl2);
-      h->d_tbl2 = nullptr;
-      h->d_cap2 = std::max<size_t>(ng2, 64);
-      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tbl2), h->d_cap2 * 512));
-    }
-    HIP_TRY(hipMemcpyAsync(h->d_tbl16, t16.data(), t16.size() * 2, hipMemcpyHostToDevice, s));
-    if (!t2.empty())
-      HIP_TRY(hipMemcpyAsync(h->d_tbl2, t2.data(), t2.size() * 2, hipMemcpyHostToDevice, s));
+  // one image: tbl24, tbl8 (>= 1 group), then tbl16 and tbl2 if built
+  h->off8 = align256((uint64_t)kTbl24 * 2);
+  const uint64_t end8 = h->off8 + std::max<size_t>(g, 1) * 512;
+  h->off16 = has16 ? align256(end8) : 0;
+  h->off2 = has16 ? align256(h->off16 + t16.size() * 2) : 0;
+  const uint64_t total = has16 ? h->off2 + std::max<size_t>(t2.size(), 256) * 2 : end8;
+  std::vector<uint8_t> &img = h->host_img;
+  img.assign(total, 0);
+  memcpy(img.data(), t24.data(), (size_t)kTbl24 * 2);
+  if (g) memcpy(img.data() + h->off8, t8.data(), t8.size() * 2);
+  if (has16) {
+    memcpy(img.data() + h->off16, t16.data(), t16.size() * 2);
+    if (!t2.empty()) memcpy(img.data() + h->off2, t2.data(), t2.size() * 2);
   }
-  if (g)
-    HIP_TRY(hipMemcpyAsync(h->d_tbl8, t8.data(), t8.size() * 2,
-                           hipMemcpyHostToDevice, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  h->device = dev;
-  h->dirty = false;
+  return 0;
+}
+
+// the device's tables of the current routes, rebuilt into a fresh image
+// when they changed (the replaced image is retired behind fences)
+static int lpm_image(bg_lpm *h, int dev, hipStream_t s, LpmImage **out) {
+  LpmImage *v = h->dev.get(dev);
+  const uint64_t ver = h->version.load(std::memory_order_acquire);
+  if (v && v->version == ver) {
+    *out = v;
+    return 0;
+  }
+  std::lock_guard<std::mutex> lk(h->mu);
+  v = h->dev.get(dev);
+  if (!v || v->version != ver) {
+    if (h->host_version != ver) {
+      if (int r = lpm_build_host(h)) return r;
+      h->host_version = ver;
+    }
+    std::unique_ptr<LpmImage> img(new LpmImage());
+    int r = upload_image(img.get(), dev, h->host_img.data(), h->host_img.size(), s);
+    if (r) return r;
+    img->version = ver;
+    uint16_t *b = reinterpret_cast<uint16_t *>(img->d);
+    img->a.tbl24 = b;
+    img->a.tbl8 = b + h->off8 / 2;
+    img->a.tbl16 = h->off16 ? b + h->off16 / 2 : nullptr;
+    img->a.tbl2 = h->off16 ? b + h->off2 / 2 : b + h->off8 / 2;
+    v = img.get();
+    h->dev.publish(dev, img.release());
+  }
+  *out = v;
   return 0;
 }
 
@@ -158,7 +166,7 @@ int bg_lpm_add(bg_lpm *h, uint32_t ip, int depth, uint32_t next_hop) {
   auto it = h->rules.find(key);
   if (it != h->rules.end()) {
     it->second = next_hop;
-    h->dirty = true;
+    lpm_changed(h);
     return 0;
   }
   if (h->rules.size() >= h->max_rules) return fail(ENOSPC, "rule table full");
@@ -173,7 +181,7 @@ int bg_lpm_add(bg_lpm *h, uint32_t ip, int depth, uint32_t next_hop) {
     }
   }
   h->rules[key] = next_hop;
-  h->dirty = true;
+  lpm_changed(h);
   return 0;
 }
 
@@ -188,7 +196,7 @@ int bg_lpm_delete(bg_lpm *h, uint32_t ip, int depth) {
     auto e = h->ext.find(ipm >> 8);
     if (--e->second == 0) h->ext.erase(e);  // tbl8 group recycled
   }
-  h->dirty = true;
+  lpm_changed(h);
   return 0;
 }
 
@@ -196,7 +204,7 @@ void bg_lpm_clear(bg_lpm *h) {
   std::lock_guard<std::mutex> lk(h->mu);
   h->rules.clear();
   h->ext.clear();
-  h->dirty = true;
+  lpm_changed(h);
 }
 
 size_t bg_lpm_count(const bg_lpm *h) { return h->rules.size(); }
@@ -209,20 +217,10 @@ int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  LpmArgs a;
-  memset(&a, 0, sizeof(a));
-  {
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (h->device >= 0) dev = h->device;
-    int r = lpm_sync_locked(h, dev, s);
-    if (r) return r;
-    a.tbl24 = h->d_tbl24;
-    a.tbl8 = h->d_tbl8;
-    a.tbl16 = h->has16 ? h->d_tbl16 : nullptr;
-    a.tbl2 = h->d_tbl2;
-  }
-  int r = set_device(dev);
-  if (r) return r;
+  LpmImage *img;
+  if (int r = lpm_image(h, dev, s, &img)) return r;
+  LpmArgs a = img->a;
+  img->used_on(s);
   a.frames = static_cast<const uint8_t *>(d_frames);
   a.stride = stride;
   a.n = n;

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -12,24 +13,33 @@
 
 using namespace bg;
 
+// one device's pair list of one version: [forward pairs][reverse pairs]
+struct SnatImage : DevImage {
+  size_t np = 0;  // pairs per direction (padded)
+};
+
 struct bg_snat {
   std::vector<uint32_t> int_addr, ext_addr, size;
-  bool dirty = true;
-  int device = -1;
-  uint32_t *d_pairs = nullptr;  // [forward pairs][reverse pairs]
-  size_t d_cap = 0;             // pairs per direction
+  std::atomic<uint64_t> version{1};  // bumped by add; images as bg_image.h
+  Published<SnatImage> dev;
   std::mutex mu;
-  ~bg_snat() {
-    if (d_pairs) (void)hipFree(d_pairs);
-  }
 };
 
 static size_t padded(size_t n) { return std::max<size_t>((n + 3) / 4 * 4, 4); }
 
-static int snat_sync_locked(bg_snat *h, int dev, hipStream_t s) {
-  if (!h->dirty && h->device == dev && h->d_pairs) return 0;
-  int r = set_device(dev);
-  if (r) return r;
+static int snat_image(bg_snat *h, int dev, hipStream_t s, SnatImage **out) {
+  SnatImage *v = h->dev.get(dev);
+  const uint64_t ver = h->version.load(std::memory_order_acquire);
+  if (v && v->version == ver) {
+    *out = v;
+    return 0;
+  }
+  std::lock_guard<std::mutex> lk(h->mu);
+  v = h->dev.get(dev);
+  if (v && v->version == ver) {
+    *out = v;
+    return 0;
+  }
   const size_t n = h->size.size(), np = padded(n);
   std::vector<uint32_t> img(np * 8, 0);  // size 0: never matches
   for (size_t i = 0; i < n; i++) {
@@ -41,17 +51,13 @@ static int snat_sync_locked(bg_snat *h, int dev, hipStream_t s) {
     rv[1] = h->int_addr[i];
     rv[2] = h->size[i];
   }
-  if (!h->d_pairs || h->d_cap < np || h->device != dev) {
-    if (h->d_pairs) (void)hipFree(h->d_pairs);
-    h->d_pairs = nullptr;
-    h->d_cap = std::max<size_t>(np, 64);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_pairs), h->d_cap * 32));
-  }
-  HIP_TRY(hipMemcpyAsync(h->d_pairs, img.data(), img.size() * 4,
-                         hipMemcpyHostToDevice, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  h->device = dev;
-  h->dirty = false;
+  std::unique_ptr<SnatImage> p(new SnatImage());
+  int r = upload_image(p.get(), dev, img.data(), img.size() * 4, s);
+  if (r) return r;
+  p->version = ver;
+  p->np = np;
+  *out = p.get();
+  h->dev.publish(dev, p.release());
   return 0;
 }
 
@@ -70,7 +76,7 @@ int bg_snat_add(bg_snat *h, uint32_t int_addr, uint32_t ext_addr, uint32_t size)
   h->int_addr.push_back(int_addr);
   h->ext_addr.push_back(ext_addr);
   h->size.push_back(size);
-  h->dirty = true;
+  h->version.fetch_add(1, std::memory_order_acq_rel);
   return 0;
 }
 
@@ -85,19 +91,13 @@ int bg_snat_classify(bg_snat *h, void *d_frames, size_t stride, size_t n,
   hipStream_t s = (hipStream_t)stream;
   int dev = 0;
   (void)hipGetDevice(&dev);
+  SnatImage *img;
+  if (int r = snat_image(h, dev, s, &img)) return r;
   NatArgs a;
   memset(&a, 0, sizeof(a));
-  {
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (h->device >= 0) dev = h->device;
-    int r = snat_sync_locked(h, dev, s);
-    if (r) return r;
-    const size_t np = padded(h->size.size());
-    a.pairs = h->d_pairs + (dir ? np * 4 : 0);
-    a.npairs = (uint32_t)np;
-  }
-  int r = set_device(dev);
-  if (r) return r;
+  a.pairs = reinterpret_cast<const uint32_t *>(img->d) + (dir ? img->np * 4 : 0);
+  a.npairs = (uint32_t)img->np;
+  img->used_on(s);
   a.frames = static_cast<uint8_t *>(d_frames);
   a.stride = stride;
   a.n = n;

@@ -172,10 +172,17 @@ int bg_module_command(bg_module *h, const char *cmd, const void *arg,
     if (c.cmd != user_cmd) continue;
     std::shared_lock<std::shared_mutex> shared(h->mu, std::defer_lock);
     std::unique_lock<std::shared_mutex> excl(h->mu, std::defer_lock);
-    if (c.mt_safe == Command::THREAD_SAFE)
+    if (c.mt_safe == Command::THREAD_SAFE) {
       shared.lock();
-    else
+    } else {
       excl.lock();
+      // batches submitted before a rule change keep the rules they were
+      // submitted under: their partly filled pipe slots launch now, and the
+      // device images they read are retired behind fences (bg_image.h)
+      std::lock_guard<std::mutex> pl(h->pipes_mu);
+      for (bg_pipe *p : h->pipes)
+        if (int r = PipeFlushLocked(p)) return r;
+    }
     CommandResponse r = c.func(h->m.get(), arg, arg_len);
     if (r.code() != 0) return respond(r);
     const std::string &d = r.data();

@@ -21,6 +21,8 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <set>
 #include <shared_mutex>
 #include <string>
 #include <vector>
@@ -322,14 +324,25 @@ ModuleBuilder::Factory MakeFactory() {
   static bool __module__##_MOD = ModuleBuilder::RegisterModuleClass(          \
       #_MOD, _NAME_TEMPLATE, _HELP, MakeFactory<_MOD, _ARG>());
 
+struct bg_pipe;
+
 // The C ABI's module handle (include/bessgpu.h bg_module_*).
 struct bg_module {
   std::unique_ptr<Module> m;
   std::string mclass;
-  // ProcessBatch calls and THREAD_SAFE commands share it; THREAD_UNSAFE
-  // commands (which bessd runs only with workers paused,
+  // ProcessBatch calls, pipe launches and THREAD_SAFE commands share it;
+  // THREAD_UNSAFE commands (which bessd runs only with workers paused,
   // core/module.cc:97-101) take it exclusively
   std::shared_mutex mu;
+  // the pipes feeding this module: a THREAD_UNSAFE command first launches
+  // their partly filled slots, so every packet submitted before a rule
+  // change is classified with the rules it was submitted under
+  std::mutex pipes_mu;
+  std::set<bg_pipe *> pipes;
 };
+
+// pipe.cc: launch a pipe's partly filled slot (its module's lock is held
+// by the caller)
+int PipeFlushLocked(bg_pipe *p);
 
 #endif  // BESS_AMD_HOST_MODULE_H_

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <mutex>
 #include <vector>
 
 #include "../../include/bessgpu.h"
@@ -72,11 +73,18 @@ struct bg_pipe {
   std::deque<std::pair<void *, uint16_t>> ready;  // completed, not returned
   size_t pending = 0;    // submitted, not yet returned by poll
   int err = 0;           // sticky launch error
+  // One worker owns a pipe; the lock is for the module's control path
+  // (PipeFlushLocked) and a RunTask on another worker (never contended on
+  // the datapath).
+  std::mutex mu;
 };
 
 static void pipe_release(bg_pipe *p) {
   for (Slot &s : p->slots) {
-    if (s.st) (void)hipStreamSynchronize(s.st);
+    if (s.st) {
+      (void)hipStreamSynchronize(s.st);
+      bg::stream_gone(s.st);  // no table image fences on it any more
+    }
     if (s.h_in) (void)hipHostFree(s.h_in);
     if (s.h_wb) (void)hipHostFree(s.h_wb);
     if (s.h_g) (void)hipHostFree(s.h_g);
@@ -88,7 +96,10 @@ static void pipe_release(bg_pipe *p) {
   p->slots.clear();
 }
 
-// Launch the fill slot (n > 0): H2D, module kernel, D2H, event.
+// Launch the fill slot (n > 0): H2D, module kernel, D2H, event. (No
+// module lock: like bessd's datapath, a pipe relies on THREAD_UNSAFE
+// commands running only while its worker is paused, core/module.cc:97-101;
+// such a command flushes the pipe first, PipeFlushLocked.)
 static int launch_slot(bg_pipe *p) {
   Slot &s = p->slots[p->fill];
   const size_t n = s.n;
@@ -179,13 +190,24 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
       s.wblen.resize(batch);
     }
   }
+  {
+    std::lock_guard<std::mutex> lk(m->pipes_mu);
+    m->pipes.insert(p);
+  }
   *out = p;
   return 0;
 }
 
 void bg_pipe_destroy(bg_pipe *p) {
   if (!p) return;
-  pipe_release(p);
+  {
+    std::lock_guard<std::mutex> lk(p->mod->pipes_mu);
+    p->mod->pipes.erase(p);
+  }
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    pipe_release(p);
+  }
   delete p;
 }
 
@@ -205,6 +227,7 @@ static bool same_ctx(unsigned use, const bg_ctx &a, const bg_ctx &b) {
 
 int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                    const uint16_t *lens, void *const *cookies, size_t cnt) {
+  std::lock_guard<std::mutex> lk(p->mu);
   if (p->err) return p->err;
   int r = bg::set_device(p->device);
   if (r) return r;
@@ -258,7 +281,7 @@ int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
   return 0;
 }
 
-int bg_pipe_flush(bg_pipe *p) {
+static int flush(bg_pipe *p) {
   if (p->err) return p->err;
   Slot &s = p->slots[p->fill];
   if (s.inflight || s.n == 0) return 0;
@@ -269,8 +292,14 @@ int bg_pipe_flush(bg_pipe *p) {
   return 0;
 }
 
+int bg_pipe_flush(bg_pipe *p) {
+  std::lock_guard<std::mutex> lk(p->mu);
+  return flush(p);
+}
+
 long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
                   size_t cap) {
+  std::lock_guard<std::mutex> lk(p->mu);
   if (p->err) return p->err;
   for (;;) {
     int r = retire_oldest(p, wait && p->ready.empty());
@@ -290,6 +319,25 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
 }
 
 size_t bg_pipe_pending(const bg_pipe *p) { return p->pending; }
+
+}  // extern "C"
+
+// A THREAD_UNSAFE command is about to change the module's rules (its lock
+// held exclusively, workers paused): the packets this pipe holds in its
+// filling slot were submitted under the old rules, so they launch now.
+int PipeFlushLocked(bg_pipe *p) {
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  int r;
+  {
+    std::lock_guard<std::mutex> lk(p->mu);
+    r = flush(p);
+  }
+  if (cur >= 0) (void)hipSetDevice(cur);
+  return r;
+}
+
+extern "C" {
 
 // A BESS worker's loop over this module (Source -> module -> Sink, SURVEY
 // §3A): ProcessBatch-sized submits of `burst` packets, completions polled
