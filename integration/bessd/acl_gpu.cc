@@ -8,7 +8,7 @@ class ACL final : public GpuModule {
  public:
   static const Commands cmds;
 
-  CommandResponse Init(const bess::pb::ACLArg &arg) { return Create("ACL", arg); }
+  CommandResponse Init(const bess::pb::ACLArg &arg) { return CreateDeferred("ACL", arg); }
   CommandResponse CommandAdd(const bess::pb::ACLArg &arg) { return Run("add", arg); }
   CommandResponse CommandClear(const bess::pb::EmptyArg &arg) { return Run("clear", arg); }
 

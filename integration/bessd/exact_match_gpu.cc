@@ -9,7 +9,7 @@ class ExactMatch final : public GpuModule {
   static const Commands cmds;
 
   CommandResponse Init(const bess::pb::ExactMatchArg &arg) {
-    return Create("ExactMatch", arg);
+    return CreateDeferred("ExactMatch", arg);
   }
   CommandResponse GetInitialArg(const bess::pb::EmptyArg &arg) {
     bess::pb::ExactMatchArg r;

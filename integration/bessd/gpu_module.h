@@ -5,16 +5,30 @@
 // plugin with -lbessgpu. Each *_gpu.cc declares the same class name,
 // gates, commands table and Init argument as the module it replaces, and
 // forwards everything to the C ABI (include/bessgpu.h):
-//   Init                  -> bg_module_create(<class>, <Class>Arg bytes)
-//   a command             -> bg_module_command(name, arg bytes) (+ response)
-//   ProcessBatch          -> bg_module_process (heads in, a gate per packet)
-//   GetDesc               -> bg_module_desc
-// and maps the gates back onto bessd's EmitPacket / DropPacket, whose own
-// check drops a packet sent to an out-of-range or unconnected gate
+//   Init          -> bg_module_create(<class>, <Class>Arg bytes)
+//   a command     -> bg_module_command(name, arg bytes) (+ response)
+//   GetDesc       -> bg_module_desc
+//   ProcessBatch  -> one of two datapaths:
+//     deferred (CreateDeferred, the classifiers and checksum modules): the
+//       Queue module's split (core/modules/queue.cc:173 ProcessBatch
+//       enqueues, :190 RunTask emits; Init registers the task, :99-102).
+//       Each worker (ctx->wid) has its own bg_pipe; ProcessBatch submits
+//       the batch with its Packet* as cookies and the call's bg_ctx, then
+//       emits what earlier batches have finished; the module's task
+//       flushes a pipe whose worker went quiet and emits the rest. Packets
+//       stay owned by the module until emitted or dropped (core/module.h:
+//       224-226) and leave in submission order, so the per-gate order
+//       within a batch is kept (module.h:268-272). Checksum modules' new
+//       header lines are in the packet before it is emitted.
+//     synchronous (Create): bg_module_process per batch (NAT, whose mapping
+//       state is sequential and which allows one worker, nat.h).
+// Gates map back onto bessd's EmitPacket / DropPacket, whose own check
+// drops a packet sent to an out-of-range or unconnected gate
 // (core/module.h:546-549).
 #ifndef BESS_MODULES_GPU_MODULE_H_
 #define BESS_MODULES_GPU_MODULE_H_
 
+#include <atomic>
 #include <string>
 
 #include "../module.h"
@@ -23,20 +37,75 @@
 
 class GpuModule : public Module {
  public:
+  // the deferred datapath's pipes: packets per device launch, launches in
+  // flight per worker
+  static const size_t kPipeBatch = 16384;
+  static const int kPipeDepth = 4;
+
   void DeInit() override {
+    for (Lane &l : lanes_) {
+      bg_pipe *p = l.pipe.exchange(nullptr);
+      if (!p) continue;
+      // what is still queued is freed unemitted, as Queue::DeInit does
+      (void)bg_pipe_flush(p);
+      void *ck[256];
+      long k;
+      while ((k = bg_pipe_poll(p, 1, ck, nullptr, 256)) > 0)
+        for (long i = 0; i < k; i++) bess::Packet::Free(static_cast<bess::Packet *>(ck[i]));
+      bg_pipe_destroy(p);
+    }
     bg_module_destroy(m_);
     m_ = nullptr;
   }
 
+  // The module's task (deferred datapath): a worker's pipe that received
+  // nothing since the last visit is flushed (its partly filled slot is
+  // launched), then every pipe's finished packets leave (`packets`: those
+  // it handed on, emitted, dropped or not emitted).
+  struct task_result RunTask(Context *ctx, bess::PacketBatch *, void *) override {
+    uint32_t done = 0;
+    for (Lane &l : lanes_) {
+      bg_pipe *p = l.pipe.load(std::memory_order_acquire);
+      if (!p || bg_pipe_pending(p) == 0) continue;
+      const uint64_t sub = l.submits.load(std::memory_order_relaxed);
+      if (sub == l.seen) (void)bg_pipe_flush(p);
+      l.seen = sub;
+      done += Drain(ctx, p);
+    }
+    return {.block = done == 0, .packets = done, .bits = 0};
+  }
+
+  // packets this module holds (submitted, not yet handed on)
+  size_t Pending() const {
+    size_t n = 0;
+    for (const Lane &l : lanes_)
+      if (bg_pipe *p = l.pipe.load(std::memory_order_acquire)) n += bg_pipe_pending(p);
+    return n;
+  }
+
  protected:
+  GpuModule() { max_allowed_workers_ = Worker::kMaxWorkers; }
+
   CommandResponse Create(const char *mclass, const google::protobuf::Message &arg) {
     const std::string b = arg.SerializeAsString();
     const int rc = bg_module_create(mclass, b.data(), b.size(), &m_);
     return rc < 0 ? CommandFailure(-rc, "%s", bg_last_error()) : CommandSuccess();
   }
 
+  // Create, with the deferred datapath: ProcessBatch enqueues, a task emits
+  CommandResponse CreateDeferred(const char *mclass, const google::protobuf::Message &arg) {
+    CommandResponse r = Create(mclass, arg);
+    if (r.code() != 0) return r;
+    if (RegisterTask(nullptr) == INVALID_TASK_ID)
+      return CommandFailure(ENOMEM, "Task creation failed");
+    deferred_ = true;
+    return CommandSuccess();
+  }
+
   // `cmd` with its argument; the C side checks it and answers with the
   // reference's errno and message. resp: the command's response message.
+  // (A THREAD_UNSAFE command launches the pipes' partly filled slots
+  // first, so queued packets keep the rules they were submitted under.)
   CommandResponse Run(const char *cmd, const google::protobuf::Message &arg,
                       google::protobuf::Message *resp = nullptr) {
     const std::string in = arg.SerializeAsString();
@@ -65,8 +134,16 @@ class GpuModule : public Module {
     return c;
   }
 
-  // ProcessBatch on the GPU, synchronously
+  // ProcessBatch: the datapath the module was created with
   void Forward(Context *ctx, bess::PacketBatch *batch) {
+    if (deferred_)
+      Enqueue(ctx, batch);
+    else
+      ProcessSync(ctx, batch);
+  }
+
+  // ProcessBatch on the GPU, synchronously
+  void ProcessSync(Context *ctx, bess::PacketBatch *batch) {
     const int n = batch->cnt();
     uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
     uint16_t og[bess::PacketBatch::kMaxBurst];
@@ -76,20 +153,44 @@ class GpuModule : public Module {
       for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
       return;
     }
-    Emit(ctx, batch, og);
+    for (int i = 0; i < n; i++) Emit(ctx, batch->pkts()[i], og[i]);
+  }
+
+  // ProcessBatch, deferred: the batch joins this worker's pipe, then what
+  // has finished there leaves
+  void Enqueue(Context *ctx, bess::PacketBatch *batch) {
+    const int n = batch->cnt();
+    Lane &l = lanes_[ctx->wid];
+    bg_pipe *p = l.pipe.load(std::memory_order_acquire);
+    if (!p && !(p = OpenLane(ctx->wid))) {
+      for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
+      return;
+    }
+    uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
+    uint16_t lens[bess::PacketBatch::kMaxBurst] = {};
+    for (int i = 0; i < n; i++) {
+      bess::Packet *pkt = batch->pkts()[i];
+      heads[i] = pkt->head_data<uint8_t *>();
+      lens[i] = pkt->data_len();
+    }
+    const bg_ctx c = CallCtx(ctx);
+    if (bg_pipe_submit(p, &c, heads, lens, reinterpret_cast<void *const *>(batch->pkts()),
+                       (size_t)n) < 0) {
+      for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
+      return;
+    }
+    l.submits.fetch_add(1, std::memory_order_relaxed);
+    Drain(ctx, p);
   }
 
   // a gate per packet: BG_GATE_NONE leaves the packet alone (the module did
   // not emit it), BG_DROP_GATE drops it, any other gate goes to EmitPacket
-  void Emit(Context *ctx, bess::PacketBatch *batch, const uint16_t *og) {
-    for (int i = 0; i < batch->cnt(); i++) {
-      bess::Packet *pkt = batch->pkts()[i];
-      if (og[i] == BG_GATE_NONE) continue;
-      if (og[i] >= BG_MAX_GATES)
-        DropPacket(ctx, pkt);
-      else
-        EmitPacket(ctx, pkt, og[i]);
-    }
+  void Emit(Context *ctx, bess::Packet *pkt, uint16_t g) {
+    if (g == BG_GATE_NONE) return;
+    if (g >= BG_MAX_GATES)
+      DropPacket(ctx, pkt);
+    else
+      EmitPacket(ctx, pkt, g);
   }
 
   std::string Desc() const {
@@ -99,6 +200,41 @@ class GpuModule : public Module {
   }
 
   bg_module *m_ = nullptr;
+
+ private:
+  struct Lane {
+    std::atomic<bg_pipe *> pipe{nullptr};
+    std::atomic<uint64_t> submits{0};  // ProcessBatch calls so far
+    uint64_t seen = 0;                 // submits at the task's last visit
+  };
+
+  // the worker's pipe, on device wid % (visible devices): the workers of one
+  // process spread over its GPUs, each using the module's table replica there
+  bg_pipe *OpenLane(int wid) {
+    const int nd = bg_device_count();
+    bg_pipe *p = nullptr;
+    if (nd <= 0 || bg_pipe_create(m_, wid % nd, kPipeBatch, kPipeDepth, 0, &p) < 0)
+      return nullptr;
+    lanes_[wid].pipe.store(p, std::memory_order_release);
+    return p;
+  }
+
+  // emit the pipe's finished packets (in submission order)
+  uint32_t Drain(Context *ctx, bg_pipe *p) {
+    void *ck[512];
+    uint16_t g[512];
+    uint32_t total = 0;
+    long k;
+    while ((k = bg_pipe_poll(p, 0, ck, g, 512)) > 0) {
+      for (long i = 0; i < k; i++) Emit(ctx, static_cast<bess::Packet *>(ck[i]), g[i]);
+      total += (uint32_t)k;
+      if (k < 512) break;
+    }
+    return total;
+  }
+
+  bool deferred_ = false;
+  Lane lanes_[Worker::kMaxWorkers];
 };
 
 #endif  // BESS_MODULES_GPU_MODULE_H_

@@ -8,7 +8,9 @@ class HashLB final : public GpuModule {
   static const gate_idx_t kNumOGates = MAX_GATES;  // hash_lb.h:45
   static const Commands cmds;
 
-  CommandResponse Init(const bess::pb::HashLBArg &arg) { return Create("HashLB", arg); }
+  CommandResponse Init(const bess::pb::HashLBArg &arg) {
+    return CreateDeferred("HashLB", arg);
+  }
   CommandResponse CommandSetMode(const bess::pb::HashLBCommandSetModeArg &arg) {
     return Run("set_mode", arg);
   }

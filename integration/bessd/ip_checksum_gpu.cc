@@ -10,7 +10,7 @@ class IPChecksum final : public GpuModule {
   static const gate_idx_t kNumOGates = 2;  // ip_checksum.h:43
 
   CommandResponse Init(const bess::pb::IPChecksumArg &arg) {
-    return Create("IPChecksum", arg);
+    return CreateDeferred("IPChecksum", arg);
   }
   void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override { Forward(ctx, batch); }
 };

@@ -8,7 +8,9 @@ class IPLookup final : public GpuModule {
   static const gate_idx_t kNumOGates = MAX_GATES;  // ip_lookup.h:43
   static const Commands cmds;
 
-  CommandResponse Init(const bess::pb::IPLookupArg &arg) { return Create("IPLookup", arg); }
+  CommandResponse Init(const bess::pb::IPLookupArg &arg) {
+    return CreateDeferred("IPLookup", arg);
+  }
   CommandResponse CommandAdd(const bess::pb::IPLookupCommandAddArg &arg) {
     return Run("add", arg);
   }

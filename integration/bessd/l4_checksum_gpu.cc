@@ -9,7 +9,7 @@ class L4Checksum final : public GpuModule {
   static const gate_idx_t kNumIGates = MAX_GATES;  // l4_checksum.h:43
 
   CommandResponse Init(const bess::pb::L4ChecksumArg &arg) {
-    return Create("L4Checksum", arg);
+    return CreateDeferred("L4Checksum", arg);
   }
   void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override { Forward(ctx, batch); }
 };

@@ -8,6 +8,8 @@
 // clock is ctx->current_ns (nat.cc:321-363); both go over with each batch.
 class NAT final : public GpuModule {
  public:
+  NAT() { max_allowed_workers_ = 1; }  // Module's default (nat.h sets none)
+
   static const gate_idx_t kNumIGates = 2;  // nat.h:141-142
   static const gate_idx_t kNumOGates = 2;
   static const Commands cmds;

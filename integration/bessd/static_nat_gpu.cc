@@ -7,12 +7,14 @@
 // destinations and emits on 0 (static_nat.cc:179-187).
 class StaticNAT final : public GpuModule {
  public:
+  StaticNAT() { max_allowed_workers_ = 1; }  // Module's default (static_nat.h)
+
   static const gate_idx_t kNumIGates = 2;  // static_nat.h:51-52
   static const gate_idx_t kNumOGates = 2;
   static const Commands cmds;
 
   CommandResponse Init(const bess::pb::StaticNATArg &arg) {
-    return Create("StaticNAT", arg);
+    return CreateDeferred("StaticNAT", arg);
   }
   CommandResponse GetInitialArg(const bess::pb::EmptyArg &arg) {
     bess::pb::StaticNATArg r;

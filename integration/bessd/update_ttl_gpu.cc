@@ -5,7 +5,9 @@
 
 class UpdateTTL final : public GpuModule {
  public:
-  CommandResponse Init(const bess::pb::EmptyArg &arg) { return Create("UpdateTTL", arg); }
+  CommandResponse Init(const bess::pb::EmptyArg &arg) {
+    return CreateDeferred("UpdateTTL", arg);
+  }
   void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override { Forward(ctx, batch); }
 };
 

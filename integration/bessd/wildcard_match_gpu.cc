@@ -9,7 +9,7 @@ class WildcardMatch final : public GpuModule {
   static const Commands cmds;
 
   CommandResponse Init(const bess::pb::WildcardMatchArg &arg) {
-    return Create("WildcardMatch", arg);
+    return CreateDeferred("WildcardMatch", arg);
   }
   CommandResponse GetInitialArg(const bess::pb::EmptyArg &arg) {
     bess::pb::WildcardMatchArg r;

@@ -9,6 +9,10 @@
 //   EmitPacket / DropPacket                           core/module.h:534-594
 //   ADD_MODULE -> ModuleBuilder::RegisterModuleClass  core/module.h:719-733
 //   gate_idx_t, MAX_GATES, DROP_GATE, SNBUF_*         core/gate.h, snbuf_layout.h
+//   RegisterTask / RunTask / task_result, is_task_,    core/module.h:198-311,
+//   max_allowed_workers_, propagate_workers_           core/task.h:40-44
+//   Worker::kMaxWorkers                               core/worker.h:77
+//   bess::Packet::Free                                core/packet.h:194-203
 //
 // EmitPacket keeps bessd's rule (module.h:546-549): an out-of-range or
 // unconnected output gate drops the packet.
@@ -19,6 +23,7 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <atomic>
 #include <functional>
 #include <map>
 #include <string>
@@ -40,7 +45,28 @@ typedef uint16_t gate_idx_t;
 #define SNBUF_HEADROOM_OFF (SNBUF_METADATA_OFF + SNBUF_METADATA + SNBUF_SCRATCHPAD)
 #define SNBUF_SIZE (SNBUF_HEADROOM_OFF + SNBUF_HEADROOM + SNBUF_DATA)
 
+class Worker {
+ public:
+  static const int kMaxWorkers = 64;  // core/worker.h:77
+};
+
+typedef uint16_t task_id_t;
+#define INVALID_TASK_ID ((task_id_t)-1)
+
+// core/task.h:40-44
+struct task_result {
+  bool block;
+  uint32_t packets;
+  uint64_t bits;
+};
+
 namespace bess {
+
+// packets handed back to the pool (Packet::Free), counted by the shell
+inline std::atomic<uint64_t> &freed_packets() {
+  static std::atomic<uint64_t> n{0};
+  return n;
+}
 
 // an snbuf: the packet object at the start of its slot, its data at
 // SNBUF_HEADROOM_OFF + data_off
@@ -57,6 +83,7 @@ class Packet {
   void set_total_len(uint32_t v) { total_len_ = v; }
   uint16_t data_len() const { return data_len_; }
   void set_data_len(uint16_t v) { data_len_ = v; }
+  static void Free(Packet *) { freed_packets()++; }
 
  private:
   uint16_t data_off_ = SNBUF_HEADROOM;
@@ -159,7 +186,20 @@ class Module {
   CommandResponse Init(const bess::pb::EmptyArg &) { return CommandSuccess(); }
   virtual void DeInit() {}
   virtual void ProcessBatch(Context *, bess::PacketBatch *) {}
+  virtual struct task_result RunTask(Context *, bess::PacketBatch *, void *) {
+    return {.block = true, .packets = 0, .bits = 0};
+  }
   virtual std::string GetDesc() const { return ""; }
+
+  // Module::RegisterTask (core/module.cc:156-167): the shell's scheduler
+  // runs each registered task from the worker it is given to
+  task_id_t RegisterTask(void *arg) {
+    tasks_.push_back(arg);
+    return (task_id_t)(tasks_.size() - 1);
+  }
+  size_t num_tasks() const { return tasks_.size(); }
+  bool is_task() const { return is_task_ || !tasks_.empty(); }
+  int max_allowed_workers() const { return max_allowed_workers_; }
 
   // ConnectModules: the output gates with a next module
   void ConnectOGate(gate_idx_t g) {
@@ -190,7 +230,13 @@ class Module {
   int32_t attr_offset(int attr_id) const { return 4 * attr_id; }
   size_t num_attrs() const { return attrs_.size(); }
 
+ protected:
+  bool is_task_ = false;            // core/module.h:464
+  int max_allowed_workers_ = 1;     // core/module.h:485 (default 1)
+  bool propagate_workers_ = true;   // core/module.h:491
+
  private:
+  std::vector<void *> tasks_;
   std::vector<bool> ogates_;
   std::vector<std::string> attrs_;
 };

@@ -12,22 +12,50 @@
 //     swap                        turn each IPv4 TCP/UDP frame into its reply
 //                                 (addresses and ports exchanged; checksums
 //                                 unchanged, the sums being symmetric)
-//     process <igate> <now_ns>    ProcessBatch over the frames, 32 at a time
-//                                 -> "out" + per packet: gate, D (dropped)
-//                                    or - (not emitted); "data <hex>" per
-//                                    packet's first 64 bytes afterwards
+//     process <igate> <now_ns>    ProcessBatch over the frames, 32 at a time,
+//                                 then the module's task until it holds no
+//                                 packet -> "out" + per packet: gate, D
+//                                 (dropped) or - (not emitted); "data <hex>"
+//                                 per packet's first 64 bytes afterwards
+//     pipeline <workers> <reps> <igate> <now_ns> <verify>
+//                                 Source -> module -> Sink on `workers`
+//                                 threads (pinned), each over its own slice
+//                                 of the frames `reps` times in 32-packet
+//                                 batches (wid = worker); worker 0 also runs
+//                                 the module's task (every 8 batches, then
+//                                 until the module holds no packet)
+//                                 -> "pipeline <Mpps> <seconds> <packets>",
+//                                 "out" as above for the last pass, and with
+//                                 verify "order ok|bad": each worker's
+//                                 packets left in the order they came in
+#include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
+#include <atomic>
 #include <fstream>
 #include <iostream>
 #include <map>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "core/module.h"
+#include "core/modules/gpu_module.h"
+
+// mempool object stride: the snbuf plus the mempool's object header, so
+// head_data() sits at +512 of a 2624-byte object (core/snbuf_layout.h)
+static const size_t kObj = SNBUF_SIZE + 64;
+
+static double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
 
 static std::string json_str(const std::string &s) {
   std::string o = "\"";
@@ -81,9 +109,54 @@ static void print_rc(const CommandResponse &r, bool data) {
   printf("\n");
 }
 
+// The module's task until it holds no packet (deferred plugins), or once.
+static void run_task(Module *m, Context *ctx) {
+  GpuModule *g = dynamic_cast<GpuModule *>(m);
+  if (!m->is_task()) return;
+  do {
+    m->RunTask(ctx, nullptr, nullptr);
+  } while (g && g->Pending() > 0);
+}
+
+struct Sink {  // where a worker's emitted and dropped packets go
+  std::vector<std::string> *gate = nullptr;  // per packet (verify)
+  std::vector<uint16_t> *fast = nullptr;     // per packet (timing)
+  std::vector<uint64_t> *seq = nullptr;      // emission order (verify)
+  std::atomic<uint64_t> *counter = nullptr;
+  uint8_t *pool = nullptr;
+  uint64_t n = 0;
+  void take(Context &ctx) {
+    for (auto &e : ctx.emitted) put(e.first, e.second);
+    for (auto *p : ctx.dropped) put(p, 0xFFFF);
+    n += ctx.emitted.size() + ctx.dropped.size();
+    ctx.emitted.clear();
+    ctx.dropped.clear();
+  }
+  void put(bess::Packet *p, uint32_t g) {
+    const size_t i = (size_t)(reinterpret_cast<uint8_t *>(p) - pool) / kObj;
+    if (fast) (*fast)[i] = (uint16_t)g;
+    if (gate) (*gate)[i] = g == 0xFFFF ? "D" : std::to_string(g);
+    if (seq) (*seq)[i] = (*counter)++;
+  }
+};
+
+static void pin(int w) {
+  cpu_set_t set;
+  std::vector<int> cpus;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0)
+    for (int c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &set)) cpus.push_back(c);
+  if (cpus.empty()) return;
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(cpus[(size_t)w % cpus.size()], &one);
+  pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+}
+
 static int run() {
   Module *m = nullptr;
   const ModuleClass *cls = nullptr;
+  uint8_t *pool = nullptr;
   std::vector<uint8_t *> bufs;
   std::string line;
   while (std::getline(std::cin, line)) {
@@ -127,10 +200,13 @@ static int run() {
       in >> path >> stride >> n;
       std::ifstream f(path, std::ios::binary);
       std::vector<char> fr(stride);
+      free(pool);
+      bufs.clear();
+      pool = static_cast<uint8_t *>(aligned_alloc(64, n * kObj));
+      memset(pool, 0, n * kObj);
       for (size_t i = 0; i < n; i++) {
         f.read(fr.data(), (std::streamsize)stride);
-        uint8_t *b = static_cast<uint8_t *>(aligned_alloc(64, SNBUF_SIZE));
-        memset(b, 0, SNBUF_SIZE);
+        uint8_t *b = pool + i * kObj;
         bess::Packet *p = new (b) bess::Packet();
         memcpy(p->head_data<uint8_t *>(), fr.data(), stride);
         p->set_total_len((uint32_t)stride);
@@ -148,28 +224,120 @@ static int run() {
       int ig;
       unsigned long long now;
       in >> ig >> now;
-      std::map<bess::Packet *, std::string> out;
+      std::vector<std::string> out(bufs.size(), "-");
+      Sink sink;
+      sink.gate = &out;
+      sink.pool = pool;
+      Context ctx;
+      ctx.current_igate = (gate_idx_t)ig;
+      ctx.current_ns = now;
       for (size_t b0 = 0; b0 < bufs.size(); b0 += bess::PacketBatch::kMaxBurst) {
         bess::PacketBatch batch;
         for (size_t i = b0; i < bufs.size() && i < b0 + bess::PacketBatch::kMaxBurst; i++)
           batch.add(reinterpret_cast<bess::Packet *>(bufs[i]));
-        Context ctx;
-        ctx.current_igate = (gate_idx_t)ig;
-        ctx.current_ns = now;
         m->ProcessBatch(&ctx, &batch);
-        for (auto &e : ctx.emitted) out[e.first] = std::to_string(e.second);
-        for (auto *p : ctx.dropped) out[p] = "D";
+        sink.take(ctx);
       }
+      run_task(m, &ctx);
+      sink.take(ctx);
       printf("out");
-      for (uint8_t *b : bufs) {
-        auto it = out.find(reinterpret_cast<bess::Packet *>(b));
-        printf(" %s", it == out.end() ? "-" : it->second.c_str());
-      }
+      for (auto &g : out) printf(" %s", g.c_str());
       printf("\n");
       for (uint8_t *b : bufs) {
         bess::Packet *p = reinterpret_cast<bess::Packet *>(b);
         printf("data %u %s\n", p->total_len(),
                hex(std::string(p->head_data<const char *>(), 64)).c_str());
+      }
+    } else if (op == "pipeline") {
+      int nw, reps, ig, verify;
+      unsigned long long now;
+      in >> nw >> reps >> ig >> now >> verify;
+      const size_t n = bufs.size();
+      std::vector<std::string> out(n, "-");
+      std::vector<uint16_t> fast(n, 0xFFFE);
+      std::vector<uint64_t> seq(n, ~0ull);
+      std::atomic<uint64_t> counter{0};
+      std::atomic<int> started{0}, finished{0};
+      std::atomic<bool> go{false};
+      std::vector<uint64_t> sunk(nw, 0);
+      double t0 = 0, t1 = 0;
+      auto worker = [&](int w) {
+        pin(w);
+        Sink sink;
+        sink.pool = pool;
+        if (verify) {
+          sink.gate = &out;
+          sink.seq = &seq;
+          sink.counter = &counter;
+        } else {
+          sink.fast = &fast;
+        }
+        Context ctx;
+        ctx.wid = w;
+        ctx.current_igate = (gate_idx_t)ig;
+        ctx.current_ns = now;
+        ctx.emitted.reserve(1 << 16);
+        const size_t lo = n * w / nw, hi = n * (w + 1) / nw;
+        started++;
+        while (!go.load()) {
+        }
+        uint64_t nb = 0;
+        for (int r = 0; r < reps; r++)
+          for (size_t b0 = lo; b0 < hi; b0 += bess::PacketBatch::kMaxBurst) {
+            bess::PacketBatch batch;  // the Source's batch
+            for (size_t i = b0; i < hi && i < b0 + bess::PacketBatch::kMaxBurst; i++)
+              batch.add(reinterpret_cast<bess::Packet *>(pool + i * kObj));
+            m->ProcessBatch(&ctx, &batch);
+            sink.take(ctx);
+            if (w == 0 && (++nb & 7) == 0 && m->is_task()) {
+              m->RunTask(&ctx, nullptr, nullptr);
+              sink.take(ctx);
+            }
+          }
+        finished++;
+        if (w == 0) {  // the task's worker: until every worker is done
+          while (finished.load() < nw) {
+            if (m->is_task()) m->RunTask(&ctx, nullptr, nullptr);
+            sink.take(ctx);
+          }
+          run_task(m, &ctx);
+          sink.take(ctx);
+          t1 = now_s();
+        }
+        sunk[w] = sink.n;
+      };
+      std::vector<std::thread> th;
+      for (int w = 0; w < nw; w++) th.emplace_back(worker, w);
+      while (started.load() < nw) {
+      }
+      t0 = now_s();
+      go = true;
+      for (auto &t : th) t.join();
+      const double dt = t1 - t0;
+      const double pk = (double)n * reps;
+      printf("pipeline %.3f %.6f %.0f\n", pk / dt / 1e6, dt, pk);
+      printf("out");
+      for (size_t i = 0; i < n; i++) {
+        if (verify)
+          printf(" %s", out[i].c_str());
+        else
+          printf(" %s", fast[i] == 0xFFFE ? "-" : fast[i] == 0xFFFF ? "D"
+                                                 : std::to_string(fast[i]).c_str());
+      }
+      printf("\n");
+      if (verify) {
+        bool ok = true;
+        for (int w = 0; w < nw && ok; w++) {
+          uint64_t last = 0;
+          bool first = true;
+          for (size_t i = n * w / nw; i < n * (w + 1) / nw; i++) {
+            if (seq[i] == ~0ull) continue;
+            if (!first && seq[i] <= last) ok = false;
+            last = seq[i];
+            first = false;
+          }
+        }
+        printf("order %s\n", ok ? "ok" : "bad");
       }
     }
     fflush(stdout);
@@ -178,7 +346,7 @@ static int run() {
     m->DeInit();
     delete m;
   }
-  for (uint8_t *b : bufs) free(b);
+  free(pool);
   return 0;
 }
 

@@ -307,3 +307,88 @@ def test_rewrite_wrapper_rewrites(drive, tmp_path):
         t = ts[i % 3]
         assert int(ln) == len(t)
         assert bytes.fromhex(h)[:min(64, len(t))] == t[:64]
+
+
+def _em_script(keys, gates):
+    arg = pb.dict_to_protobuf(pb.ExactMatchArg, {"fields": FIELDS})
+    script = ["create ExactMatch " + hx(arg)]
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    for k, g in zip(keys, gates):
+        kb = k.tobytes()
+        add = pb.dict_to_protobuf(pb.ExactMatchCommandAddArg, {
+            "gate": int(g), "fields": [{"value_bin": kb[a:c]} for a, c in cut]})
+        script.append("cmd add " + hx(add))
+    return script
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workers", [1, 4])
+def test_deferred_pipeline_em_vs_oracle(drive, tmp_path, workers):
+    """Source -> ExactMatch plugin -> Sink on `workers` pinned worker
+    threads, 32-packet batches, 3 passes: the plugin's ProcessBatch enqueues
+    into its worker's pipe and its task emits (queue.cc:173/190); every
+    packet's gate equals the oracle's, unconnected gates drop, and each
+    worker's packets leave in the order they came in (per-gate order
+    within a batch, core/module.h:268-272)."""
+    from oracle import oracle as O
+    keys, gates, frames = P.em_workload(1000, 40000, seed=33)
+    conn = list(range(0, 64, 2))
+    script = _em_script(keys, gates) + ["connect %d" % g for g in conn]
+    path = tmp_path / "frames.bin"
+    frames.tofile(path)
+    script += ["frames %s 64 %d" % (path, len(frames)),
+               "pipeline %d 3 0 0 1" % workers]
+    out = run(drive, script)
+    stats = [x for x in out if x.startswith("pipeline")][0].split()
+    assert float(stats[3]) == 3 * len(frames)
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    om = O.OracleExactMatch(fields=FIELDS)
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    for k, g in zip(keys, gates):
+        kb = k.tobytes()
+        om.add(fields=[{"value_bin": kb[a:c]} for a, c in cut], gate=int(g))
+    want = om.process(frames, 64, len(frames))
+    exp = [str(int(w)) if int(w) in conn else "D" for w in want]
+    assert got == exp
+    assert "order ok" in out
+
+
+@pytest.mark.gpu
+def test_deferred_pipeline_l4_checksum_and_acl(drive, tmp_path):
+    """The deferred datapath for a writing module (L4Checksum: the header
+    line is back in the packet before it leaves; TCP is not emitted, P8)
+    and for ACL fed on input gate 1 by 4 workers (acl.cc:70 emits on it)."""
+    from oracle import oracle as O
+    from oracle import oracle_more as OM
+    n = 6000
+    cf = P.cksum_workload(n, frame_len=1496)
+    ref = cf.copy()
+    _, l4w = O.cksum_process(ref, 2048, n, 2, False)
+    path = tmp_path / "ck.bin"
+    cf.tofile(path)
+    out = run(drive, ["create L4Checksum -", "connect 0", "connect 1",
+                      "frames %s 2048 %d" % (path, n), "pipeline 2 1 0 0 1"])
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == ["-" if int(w) == 0xFFFF else str(int(w)) for w in l4w]
+    assert "order ok" in out
+    # the recomputed checksum words are in the packets (ProcessBatch + task)
+    out = run(drive, ["create L4Checksum -", "connect 0", "connect 1",
+                      "frames %s 2048 %d" % (path, n), "process 0 0"])
+    data = np.stack([np.frombuffer(bytes.fromhex(x.split()[2]), np.uint8)
+                     for x in out if x.startswith("data")])
+    assert (data == ref[:, :64]).all()
+    # ACL on input gate 1
+    rng = np.random.default_rng(4)
+    t = P.random_tuples(20000, rng)
+    fr = P.build_frames(t, 60, 64)
+    rules = [{"src_ip": "%d.0.0.0/8" % a, "drop": a % 2 == 0} for a in range(0, 256, 5)]
+    rules.append({"dst_ip": "0.0.0.0/1", "drop": False})
+    want = OM.OracleACL(rules=rules).process(fr, 64, len(fr), igate=1)
+    arg = pb.dict_to_protobuf(pb.ACLArg, {"rules": rules})
+    path = tmp_path / "acl.bin"
+    fr.tofile(path)
+    out = run(drive, ["create ACL " + hx(arg), "connect 1",
+                      "frames %s 64 %d" % (path, len(fr)), "pipeline 4 2 1 0 1"])
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == ["1" if int(w) == 1 else "D" for w in want]
+    assert "order ok" in out
