@@ -78,7 +78,7 @@ def parse():
                     help="NAT: skip the new-flow batch stream (PMC passes)")
     ap.add_argument("--lib", default="",
                     help="time another build of libbessgpu.so (same-box A/B)")
-    ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|rewrite|pipe (profiling runs)")
+    ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|rewrite|pipe|plugin|sweep (profiling runs)")
     return ap.parse_args()
 
 
@@ -634,6 +634,70 @@ def run_e2e_pipe(args, torch):
     ck["bytes_per_pkt_pcie"] = {"h2d": 1504, "d2h": 130}
     out["L4Checksum_1500B"] = ck
     return out
+
+
+def run_plugin_pipeline(args):
+    """The bessd drop-in as a BESS user gets it: the ExactMatch plugin
+    (integration/bessd/exact_match_gpu.cc, deferred datapath: ProcessBatch
+    enqueues into its worker's pipe, the module's task emits, as Queue does)
+    compiled against the header shell, driven by the shell's worker loop
+    (tests/bessd_shell/drive.cc `pipeline`): Source -> ExactMatch -> Sink,
+    32-packet batches, T pinned workers, each over its own slice of the
+    pool, EmitPacket to connected gates. The same pool and slicing as the
+    C2 cpu_baseline (2^18 64 B packets in 2624 B snbuf objects, 1000
+    rules), so the two rates compare on the same cores."""
+    import subprocess
+    import tempfile
+    from bess_amd import packets as P
+    from bess_amd import pb
+    from oracle import oracle as O
+    drive = os.path.join(ROOT, "tests", "bessd_shell", "build", "drive")
+    if not os.path.exists(drive):
+        return "skipped: %s not built" % drive
+    n = 1 << 18
+    keys, gates, frames = P.em_workload(args.rules, n, seed=0x5EED, pkt_seed=77)
+    fields = [{"offset": o, "num_bytes": sz} for o, sz in P.FIVE_TUPLE]
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    om = O.OracleExactMatch(fields=fields)
+    script = ["create ExactMatch " +
+              pb.dict_to_protobuf(pb.ExactMatchArg, {"fields": fields})
+              .SerializeToString().hex()]
+    for k, g in zip(keys, gates):
+        kb = k.tobytes()
+        v = [{"value_bin": kb[a:c]} for a, c in cut]
+        om.add(fields=v, gate=int(g))
+        script.append("cmd add " + pb.dict_to_protobuf(
+            pb.ExactMatchCommandAddArg, {"gate": int(g), "fields": v})
+            .SerializeToString().hex())
+    want = om.process(frames, 64, n)
+    script += ["connect %d" % g for g in range(65)]
+    threads = [int(x) for x in args.pipe_threads.split(",")]
+    res, parity = {}, {}
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "frames.bin")
+        frames.tofile(path)
+        script.append("frames %s 64 %d" % (path, n))
+        for t in threads:
+            reps = 64 if t == 1 else 256
+            sc = script + ["pipeline %d 2 0 0 0" % t,  # warm: lanes, tables
+                           "pipeline %d %d 0 0 0" % (t, reps)]
+            r = subprocess.run([drive, "run"], input="\n".join(sc) + "\n",
+                               capture_output=True, text=True, timeout=600)
+            lines = r.stdout.splitlines()
+            stats = [x for x in lines if x.startswith("pipeline")]
+            outs = [x for x in lines if x.startswith("out")]
+            if r.returncode or len(stats) < 2 or len(outs) < 2:
+                res[str(t)] = "failed: rc %d %s" % (r.returncode, r.stderr[-300:])
+                continue
+            res[str(t)] = round(float(stats[-1].split()[1]), 1)
+            got = np.array([int(x) for x in outs[-1].split()[1:]], np.int64)
+            parity[str(t)] = bool((got == want).all())
+    return {"what": "Source -> ExactMatch plugin (deferred: per-worker bg_pipe, "
+                    "task emits) -> Sink, 32-pkt batches, 1000 rules, %d 64B "
+                    "pkts in 2624 B snbufs split over the workers as the "
+                    "cpu_baseline splits them" % n,
+            "Mpps_by_workers": res, "pipe": {"batch": 16384, "depth": 4},
+            "parity": parity}
 
 
 def _time_steps(step, args, torch):
@@ -1504,6 +1568,7 @@ def main():
             "acl": lambda: run_acl(args, dev, torch),
             "hashlb": lambda: run_hashlb(args, dev, torch),
             "pipe": lambda: run_e2e_pipe(args, torch),
+            "plugin": lambda: run_plugin_pipeline(args),
             "c1": lambda: run_c1(args),
             "sweep": lambda: em_sweep(run_em(args, rank, world, dev, torch,
                                              dist), torch)}
@@ -1572,6 +1637,10 @@ def main():
                 out["e2e_pipe"] = run_e2e_pipe(args, torch)
             except Exception as e:
                 out["e2e_pipe"] = "failed: %r" % (e,)
+            try:
+                out["e2e_plugin"] = run_plugin_pipeline(args)
+            except Exception as e:
+                out["e2e_plugin"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
                          ("HashLB", run_hashlb), ("ACL", run_acl),
                          ("IPLookup", run_iplookup),

@@ -85,6 +85,13 @@ _SIGS = {
     "bg_em_build_part": (_int, [_vp, _int, _vp]),
     "bg_em_attach": (_int, [_vp, _int, _vp]),
     "bg_em_table_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
+    "bg_comm_unique_id": (_int, [_vp]),
+    "bg_comm_init_rank": (_int, [_vp, _int, _int, _int, C.POINTER(_vp)]),
+    "bg_comm_init_all": (_int, [_vp, _int, _vp]),
+    "bg_comm_destroy": (None, [_vp]),
+    "bg_comm_info": (_int, [_vp, C.POINTER(_int), C.POINTER(_int), C.POINTER(_int)]),
+    "bg_em_allgather": (_int, [_vp, _vp, _vp]),
+    "bg_em_allgather_all": (_int, [_vp, _vp, _int]),
     "bg_wm_create": (_int, [C.POINTER(bg_field), _int, C.POINTER(_vp)]),
     "bg_wm_destroy": (None, [_vp]),
     "bg_wm_key_size": (_sz, [_vp]),

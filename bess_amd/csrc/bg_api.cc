@@ -897,6 +897,31 @@ int bg_em_attach(bg_em *em, int device, const void *d_image) {
   return 0;
 }
 
+}  // extern "C"
+
+namespace bg {
+int em_publish_owned(bg_em *em, int device, uint8_t *d_img, uint64_t bytes) {
+  if (!em->planned_valid || device < 0 || device >= kMaxDevices) {
+    DevImage tmp;  // frees d_img
+    tmp.device = device;
+    tmp.d = d_img;
+    return fail(EINVAL, "no planned layout / bad device %d", device);
+  }
+  std::lock_guard<std::mutex> lk(em->mu);
+  EmImage *img = new EmImage();
+  img->device = device;
+  img->d = d_img;
+  img->owned = true;
+  img->bytes = bytes;
+  img->version = em->version.load(std::memory_order_acquire);
+  img->t = table_ref(img->d, img->bytes, em->planned, 0, 0, false, 0);
+  em->dev.publish(device, img);
+  return 0;
+}
+}  // namespace bg
+
+extern "C" {
+
 int bg_em_table_info(const bg_em *em, uint64_t *bytes, int *in_lds) {
   const EmImage *img = const_cast<bg_em *>(em)->dev.get(current_device());
   if (!img) return fail(EINVAL, "no device table yet");

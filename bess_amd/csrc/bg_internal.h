@@ -102,6 +102,10 @@ Staging &thread_staging();
 int em_device_plan(bg_em *em, int device, hipStream_t s, FieldPlan *fp,
                    TableRef *t, int *read_end);
 hipStream_t thread_stream(int device, hipStream_t given);
+// bg_comm.cc: an assembled image (d_img, bytes; hipMalloc'ed on `device`,
+// laid out as bg_em_plan*) becomes the device's table image of the current
+// rules, owned (and freed, behind fences) by the table
+int em_publish_owned(bg_em *em, int device, uint8_t *d_img, uint64_t bytes);
 
 }  // namespace bg
 

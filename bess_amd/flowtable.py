@@ -11,7 +11,7 @@ import numpy as np
 from . import _lib
 from ._lib import BessGpuError, bg_field, check, lib
 
-__all__ = ["EmTable", "Ring", "WmTable", "cksum", "cksum_host", "resolve_em_fields",
+__all__ = ["Comm", "EmTable", "Ring", "WmTable", "cksum", "cksum_host", "resolve_em_fields",
            "resolve_wm_fields", "BessGpuError"]
 
 
@@ -132,6 +132,56 @@ class EmTable:
         b, l = C.c_uint64(), C.c_int()
         check(lib().bg_em_table_info(self.h, C.byref(b), C.byref(l)))
         return b.value, bool(l.value)
+
+    def allgather(self, comm, stream=None):
+        """bg_em_allgather: this rank's share of the sharded build over RCCL;
+        the assembled image becomes the table's image on comm's device"""
+        check(lib().bg_em_allgather(self.h, comm.h, _stream_ptr(stream)))
+
+    def allgather_all(self, comms):
+        """bg_em_allgather_all: every rank of an init_all set, one thread"""
+        arr = (C.c_void_p * len(comms))(*[c.h.value for c in comms])
+        check(lib().bg_em_allgather_all(self.h, arr, len(comms)))
+
+
+class Comm:
+    """bg_comm: one rank of an RCCL communicator over the GPUs that share a
+    rule set (the C ABI's own, no torch.distributed)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * 128)()
+        check(lib().bg_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def init_rank(cls, uid, nranks, rank, device):
+        h = C.c_void_p()
+        buf = (C.c_uint8 * 128)(*uid)
+        check(lib().bg_comm_init_rank(buf, nranks, rank, device, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def init_all(cls, devices):
+        devs = (C.c_int * len(devices))(*devices)
+        hs = (C.c_void_p * len(devices))()
+        check(lib().bg_comm_init_all(devs, len(devices), hs))
+        return [cls(C.c_void_p(h)) for h in hs]
+
+    def info(self):
+        r, n, d = C.c_int(), C.c_int(), C.c_int()
+        check(lib().bg_comm_info(self.h, C.byref(r), C.byref(n), C.byref(d)))
+        return r.value, n.value, d.value
+
+    def close(self):
+        if getattr(self, "h", None) is not None and _lib._lib is not None:
+            lib().bg_comm_destroy(self.h)
+            self.h = None
+
+    __del__ = close
 
 
 class Ring:

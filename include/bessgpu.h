@@ -130,6 +130,7 @@ int bg_em_plan_count(bg_em *em, int nparts, uint64_t max_part_entries,
                      uint64_t *part_bytes);
 int bg_em_build_part(bg_em *em, int part, void *host_dst);
 int bg_em_attach(bg_em *em, int device, const void *d_image);
+/* The sharded build over RCCL (xGMI), with no torch: see bg_comm below. */
 /* bytes of the current device table image and whether it lives in LDS */
 int bg_em_table_info(const bg_em *em, uint64_t *bytes, int *in_lds);
 /* Classify staged windows: byte 0 of window i (at d_win + i*stride) is frame
@@ -139,6 +140,32 @@ int bg_em_classify_window(bg_em *em, const void *d_win, size_t stride,
                           uint16_t *d_gates, bg_stream_t stream);
 /* [lo, hi): the frame bytes the fields cover (MakeKeys reads) */
 void bg_em_window(const bg_em *em, int *lo, int *hi);
+
+/* ---- Rule-table collective (RCCL over xGMI) -----------------
+ * The only exchange of the multi-GPU path: the ExactMatch image of a rule
+ * set too large to build on every GPU (C5). A communicator spans the GPUs
+ * that share one rule set, one rank per GPU:
+ *   bg_comm_init_all   every listed GPU of this process at once (a bessd
+ *                      with workers on several GPUs; ncclCommInitAll);
+ *   bg_comm_unique_id + bg_comm_init_rank   one rank per process (the id
+ *                      travels by the caller's own means).
+ * bg_em_allgather (one rank; collective: every rank calls it): the ranks
+ * agree on the layout with one all-reduce MAX of their partition sizes,
+ * build their own partition (the table may hold only partition `rank`'s
+ * rules: bg_em_add_many part = rank) and one all-gather assembles the image,
+ * which becomes the table's image on the rank's device. nranks: 1, 2, 4 or
+ * 8. bg_em_allgather_all: the same for all ranks of an init_all set from
+ * one thread (grouped calls), the table holding all rules. */
+#define BG_COMM_ID_BYTES 128
+typedef struct bg_comm bg_comm;
+int bg_comm_unique_id(uint8_t *id /* BG_COMM_ID_BYTES */);
+int bg_comm_init_rank(const uint8_t *id, int nranks, int rank, int device,
+                      bg_comm **out);
+int bg_comm_init_all(const int *devices, int ndev, bg_comm **comms);
+void bg_comm_destroy(bg_comm *c);
+int bg_comm_info(const bg_comm *c, int *rank, int *nranks, int *device);
+int bg_em_allgather(bg_em *em, bg_comm *comm, bg_stream_t stream);
+int bg_em_allgather_all(bg_em *em, bg_comm *const *comms, int ncomm);
 
 /* ---- WildcardMatch ----------------------------------------------------- */
 typedef struct bg_wm bg_wm;
