@@ -307,10 +307,11 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
               sees);
       graph:  the 512 launches captured in a HIP graph and replayed (no
               host cost; the runtime may overlap independent launches);
-      persistent: ONE running kernel (bg_ring) drains the batches as a host
-              thread submits their descriptors (bg_ring_run: 1M packets in
-              B-packet batches, wall time from the first submit to the last
-              batch's completion; no HIP graph)."""
+      persistent: ONE running kernel (bg_ring) drains the batches as host
+              threads submit their descriptors, each on its own submission
+              lane (bg_ring_run: 1M packets in B-packet batches split over
+              1, 4 or 16 submitter threads, wall time from the first submit
+              to the last batch's completion; no HIP graph)."""
     from bess_amd import flowtable as F
     t, d_frames, d_gates = r["t"], r["d_frames"], r["d_gates"]
     out = {"stream": {}, "graph": {}, "persistent": {}}
@@ -355,22 +356,21 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
         torch.cuda.synchronize()
         ms = timed(g.replay)
         out["graph"][str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
-    ring = F.Ring(t, slots=4096)
+    ring = F.Ring(t, slots=4096, lanes=16)
     npk = 1 << 20
-    launches0 = 0
-    for B in batches:
-        ring.run(d_frames, 64, npk, B, 8192, d_gates)  # warm
-        best = None
-        for _ in range(3):
-            t0 = time.perf_counter()
-            ring.run(d_frames, 64, npk, B, 8192, d_gates)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        out["persistent"][str(B)] = round(npk / best / 1e6, 1)
+    for T in (1, 4, 16):
+        key = "persistent" if T == 1 else "persistent_%dsub" % T
+        out[key] = {}
+        for B in batches:
+            ring.run_lanes(d_frames, 64, npk, B, 8192, d_gates, T)  # warm
+            best = min(ring.run_lanes(d_frames, 64, npk, B, 8192, d_gates, T)
+                       for _ in range(3))
+            out[key][str(B)] = round(npk / best / 1e6, 1)
     launches0, blocks = ring.info()
     ring.close()
     out["persistent_info"] = {"packets_per_point": npk, "kernel_launches": launches0,
-                              "workgroups": blocks, "slots": 4096,
+                              "workgroups": blocks, "slots_per_lane": 4096,
+                              "lanes": 16, "submitters": [1, 4, 16],
                               "timing": "host wall, best of 3"}
     return out
 

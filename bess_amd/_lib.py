@@ -142,12 +142,13 @@ _SIGS = {
     "bg_pipe_poll": (C.c_long, [_vp, _int, _vp, _vp, _sz]),
     "bg_pipe_pending": (_sz, [_vp]),
     "bg_pipe_run": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
-    "bg_em_ring_create": (_int, [_vp, _int, _int, _int, C.c_uint32, C.POINTER(_vp)]),
+    "bg_em_ring_create": (_int, [_vp, _int, _int, _int, _int, C.c_uint32,
+                                 C.POINTER(_vp)]),
     "bg_ring_destroy": (None, [_vp]),
-    "bg_ring_submit": (C.c_int64, [_vp, _vp, _sz, _sz, _u16, _vp]),
-    "bg_ring_wait": (_int, [_vp, C.c_int64]),
-    "bg_ring_completed": (C.c_int64, [_vp]),
-    "bg_ring_run": (_int, [_vp, _vp, _sz, _sz, _sz, _u16, _vp]),
+    "bg_ring_submit": (C.c_int64, [_vp, _int, _vp, _sz, _sz, _u16, _vp]),
+    "bg_ring_wait": (_int, [_vp, _int, C.c_int64]),
+    "bg_ring_completed": (C.c_int64, [_vp, _int]),
+    "bg_ring_run": (_int, [_vp, _int, _vp, _sz, _sz, _sz, _u16, _vp]),
     "bg_ring_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
     "bg_hlb_create": (_int, [_int, C.POINTER(bg_field), _int, C.POINTER(_vp)]),
     "bg_hlb_destroy": (None, [_vp]),

@@ -307,19 +307,26 @@ struct DnatArgs {
 // worker re-checks dev[1] once and exits if its ticket is still
 // unpublished, and the grid ends. The host relaunches from its oldest
 // unfinished ticket (re-classifying a finished batch is harmless).
+// Submission lanes (one per worker thread), each its own ring of nslots
+// descriptors, done words and published count; lane l's words at
+// l * kRingLaneWords (64 bytes apart).
 struct RingArgs {
-  const uint64_t *desc;   // host memory (mapped)
-  uint32_t *done;         // host memory (mapped)
-  const uint64_t *pub;    // host memory: tickets published
+  const uint64_t *desc;   // host memory (mapped): nlanes x nslots x 4 words
+  uint32_t *done;         // host memory (mapped): nlanes x nslots
+  const uint64_t *pub;    // host memory: tickets published, per lane
   const uint32_t *stop;   // host memory: the owner stops the grid
-  unsigned long long *dev;  // device memory: [0] next ticket to claim,
-                            // [1] published (mirror), [2] stop
-  uint32_t nslots, pad;
+  uint32_t *ended;        // host memory: launch_id of the grid that ended
+  unsigned long long *dev;  // device memory, per lane: [0] next ticket to
+                            // claim, [1] published (mirror); then the stop word
+  uint32_t nslots, nlanes;
+  uint32_t launch_id, pad;
   uint64_t idle_ticks;
   FieldPlan fp;
   TableRef t;
 };
 constexpr int kRingBlock = 256;
+constexpr int kRingLaneWords = 8;
+constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
 
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.

@@ -383,22 +383,34 @@ __device__ __forceinline__ void st_agent(unsigned long long *p, uint64_t v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// workgroup 0, one lane: *pub (PCIe) -> dev[1] (L2) until idle or stopped
+// Workgroup 0, its first wave (one wave lane per submission lane): lane l
+// reads the host's published count of submission lane l (PCIe) and mirrors
+// it in device memory (L2), where that lane's workgroups wait, until the
+// grid has been idle for idle_ticks or the owner stops it. On its way out it
+// raises the device stop word and tells the host which launch ended.
 __device__ __forceinline__ void ring_dispatch(const RingArgs &a) {
-  uint64_t last = ld_agent(a.dev + 1);
+  const uint32_t l = threadIdx.x;
+  const bool mine = l < a.nlanes;
+  unsigned long long *dl = a.dev + (size_t)l * kRingLaneWords;
+  uint64_t last = mine ? ld_agent(dl + 1) : 0;
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    const uint64_t p = ld_sys(a.pub);
+    const uint64_t p = mine ? ld_sys(a.pub + (size_t)l * kRingLaneWords) : last;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (p != last) {
-      st_agent(a.dev + 1, p);
+    const bool moved = p != last;
+    if (moved) {
+      st_agent(dl + 1, p);
       last = p;
-      t0 = now;
     }
+    if (__ballot(moved)) t0 = now;
     const uint32_t st = __hip_atomic_load(a.stop, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_SYSTEM);
     if (st || now - t0 > a.idle_ticks) {
-      st_agent(a.dev + 2, 1);
+      if (l == 0) {
+        st_agent(a.dev + (size_t)a.nlanes * kRingLaneWords, 1);
+        __hip_atomic_store(a.ended, a.launch_id, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       return;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -446,6 +458,10 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
   }
 }
 
+// Workgroup b >= 1 serves submission lane (b - 1) % nlanes: it claims that
+// lane's tickets in order, waits until the ticket is published, reads the
+// descriptor (every word tagged with the ticket), classifies the batch and
+// marks the ticket done in host memory.
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
@@ -454,23 +470,28 @@ void em_ring_kernel(RingArgs a) {
   __shared__ uint64_t sh_t;
   __shared__ uint32_t sh_go;
   if (blockIdx.x == 0) {
-    if (threadIdx.x == 0) ring_dispatch(a);
+    if (threadIdx.x < 64) ring_dispatch(a);
     return;
   }
+  const uint32_t lane = (blockIdx.x - 1) % a.nlanes;
+  unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
+  const unsigned long long *dstop = a.dev + (size_t)a.nlanes * kRingLaneWords;
+  const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * 4;
+  uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   copy_table_to_lds(lds, a.t);  // (ends with a barrier)
   const uint64_t mask48 = (1ull << 48) - 1;
   constexpr int kPpl = 4;  // packets per lane per round, loads in flight
   for (;;) {
     if (threadIdx.x == 0) {
-      const uint64_t t = atomicAdd(a.dev, 1ull);
+      const uint64_t t = atomicAdd(dl, 1ull);
       uint32_t go = 0;
       for (;;) {
-        if (ld_agent(a.dev + 1) > t) {
+        if (ld_agent(dl + 1) > t) {
           go = 1;
           break;
         }
-        if (ld_agent(a.dev + 2)) {  // stopping: published meanwhile?
-          go = ld_agent(a.dev + 1) > t ? 1u : 0u;
+        if (ld_agent(dstop)) {  // stopping: published meanwhile?
+          go = ld_agent(dl + 1) > t ? 1u : 0u;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -478,7 +499,7 @@ void em_ring_kernel(RingArgs a) {
       uint64_t w[4] = {0, 0, 0, 0};
       if (go) {
         const uint64_t tag = (t + 1) & 0xFFFF;
-        const uint64_t *d = a.desc + (t % a.nslots) * 4;
+        const uint64_t *d = ldesc + (t % a.nslots) * 4;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
@@ -518,7 +539,7 @@ void em_ring_kernel(RingArgs a) {
       // the batch's gates leave the L2 before the host can see `done`
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.done + (t % a.nslots), (uint32_t)(t + 1),
+      __hip_atomic_store(ldone + (t % a.nslots), (uint32_t)(t + 1),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();  // sh_* are rewritten for the next ticket

@@ -34,26 +34,36 @@
 
 using namespace bg;
 
+// One submission lane: a worker thread's own ring of descriptors.
+struct RingLane {
+  uint64_t *h_desc = nullptr;  // nslots x 4 words (host, coherent, mapped)
+  uint32_t *h_done = nullptr;  // nslots
+  uint64_t *h_pub = nullptr;   // tickets published (its own 64-byte line)
+  uint64_t next = 0;           // next ticket to publish
+  std::atomic<uint64_t> done_upto{0};  // every ticket below has completed
+  std::mutex mu;  // one worker per lane; the lock only guards misuse
+};
+
 struct bg_ring {
   int device = 0;
-  uint32_t nslots = 0;
+  uint32_t nslots = 0, nlanes = 0;
   int blocks = 0;
   int read_end = 0;         // bytes of a slot the kernel reads
   hipStream_t st = nullptr;  // the kernel's own stream
   hipEvent_t ev = nullptr;   // recorded after each launch: has it ended?
-  uint64_t *h_desc = nullptr;  // nslots x 4 words, host (coherent, mapped)
-  uint32_t *h_done = nullptr;  // nslots, host
+  uint64_t *h_desc = nullptr;  // nlanes x nslots x 4 words
+  uint32_t *h_done = nullptr;  // nlanes x nslots
+  uint64_t *h_pub = nullptr;   // nlanes x kRingLaneWords
   uint32_t *h_stop = nullptr;  // 1 word, host
-  uint64_t *h_pub = nullptr;   // tickets published, host
+  uint32_t *h_ended = nullptr;  // launch id of the grid that ended, host
   uint64_t *h_reset = nullptr;  // pinned source of the device words' reset
-  unsigned long long *d_dev = nullptr;  // next ticket, published, stop
+  unsigned long long *d_dev = nullptr;  // per lane: next ticket, published; stop
   uint8_t *d_table = nullptr;  // the ring's own copy of the table image
   RingArgs a{};
-  uint64_t next = 0;      // next ticket to publish
-  uint64_t done_upto = 0;  // every ticket < done_upto has completed
-  bool running = false;
+  std::atomic<uint32_t> launch_id{0};  // of the grid launched last (0: none)
   uint64_t launches = 0;
-  std::mutex mu;  // one ring per worker; the lock only guards misuse
+  std::mutex run_mu;  // (re)launches
+  RingLane lanes[kRingMaxLanes];
 };
 
 namespace {
@@ -66,38 +76,60 @@ double now_s() {
   return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
-bool done_at(const bg_ring *r, uint64_t t) {
-  const uint32_t v = __atomic_load_n(r->h_done + (t % r->nslots), __ATOMIC_ACQUIRE);
+bool done_at(const bg_ring *r, const RingLane &l, uint64_t t) {
+  const uint32_t v = __atomic_load_n(l.h_done + (t % r->nslots), __ATOMIC_ACQUIRE);
   return v == (uint32_t)(t + 1);
 }
 
-// Advance done_upto over completed tickets (in order).
-void retire(bg_ring *r) {
-  while (r->done_upto < r->next && done_at(r, r->done_upto)) r->done_upto++;
+// Advance the lane's done_upto over completed tickets (in order); the
+// lane's owner only.
+void retire(bg_ring *r, RingLane &l) {
+  uint64_t d = l.done_upto.load(std::memory_order_relaxed);
+  while (d < l.next && done_at(r, l, d)) d++;
+  l.done_upto.store(d, std::memory_order_release);
 }
 
-// (Re)launch the kernel from the oldest unfinished ticket if it is not
-// running. A grid that stopped itself (idle) has ended once its event has.
+// Is the last launched grid still serving? Its dispatcher writes its launch
+// id to h_ended on the way out, so the submit path reads one host word and
+// makes no HIP call.
+bool grid_live(const bg_ring *r) {
+  const uint32_t id = r->launch_id.load(std::memory_order_acquire);
+  return id != 0 && __atomic_load_n(r->h_ended, __ATOMIC_ACQUIRE) != id;
+}
+
+// (Re)launch the grid if it has ended and a lane has unfinished tickets;
+// every lane's claims restart at its oldest unfinished ticket (later ones
+// that already finished are classified again: same gates).
 int ensure_running(bg_ring *r) {
-  if (r->running) {
-    const hipError_t q = hipEventQuery(r->ev);
-    if (q == hipErrorNotReady) return 0;
-    if (q != hipSuccess)
-      return fail(EIO, "ring kernel: %s", hipGetErrorString(q));
-    r->running = false;
-  }
-  retire(r);
-  if (r->done_upto == r->next) return 0;  // nothing outstanding
+  if (grid_live(r)) return 0;
+  std::lock_guard<std::mutex> lk(r->run_mu);
+  if (grid_live(r)) return 0;
   int rc = set_device(r->device);
   if (rc) return rc;
+  if (r->launch_id.load() != 0) HIP_TRY(hipEventSynchronize(r->ev));  // all exited
+  bool work = false;
+  for (uint32_t i = 0; i < r->nlanes; i++) {
+    RingLane &l = r->lanes[i];
+    // the lane's published count and its oldest unfinished ticket (read
+    // without its owner's lock: done_upto only grows, pub is atomic)
+    const uint64_t pub = __atomic_load_n(l.h_pub, __ATOMIC_ACQUIRE);
+    uint64_t d = l.done_upto.load(std::memory_order_acquire);
+    while (d < pub && done_at(r, l, d)) d++;
+    work |= d < pub;
+    r->h_reset[i * kRingLaneWords + 0] = d;  // claims restart here
+    r->h_reset[i * kRingLaneWords + 1] = d;  // the dispatcher picks up pub
+  }
+  if (!work) return 0;
+  r->h_reset[(size_t)r->nlanes * kRingLaneWords] = 0;  // stop word
   __atomic_store_n(r->h_stop, 0u, __ATOMIC_RELEASE);
-  r->h_reset[0] = r->done_upto;  // claims restart at the oldest unfinished
-  r->h_reset[1] = r->done_upto;  // the dispatcher picks up *pub at once
-  r->h_reset[2] = 0;
-  HIP_TRY(hipMemcpyAsync(r->d_dev, r->h_reset, 24, hipMemcpyHostToDevice, r->st));
+  HIP_TRY(hipMemcpyAsync(r->d_dev, r->h_reset,
+                         ((size_t)r->nlanes * kRingLaneWords + 1) * 8,
+                         hipMemcpyHostToDevice, r->st));
+  const uint32_t id = r->launch_id.load() + 1;
+  r->a.launch_id = id;
   HIP_TRY(launch_em_ring(r->a, r->blocks, r->st));
   HIP_TRY(hipEventRecord(r->ev, r->st));
-  r->running = true;
+  r->launch_id.store(id, std::memory_order_release);
   r->launches++;
   return 0;
 }
@@ -107,8 +139,9 @@ void ring_release(bg_ring *r) {
   if (r->st) (void)hipStreamSynchronize(r->st);  // every workgroup exits
   if (r->h_desc) (void)hipHostFree(r->h_desc);
   if (r->h_done) (void)hipHostFree(r->h_done);
-  if (r->h_stop) (void)hipHostFree(r->h_stop);
   if (r->h_pub) (void)hipHostFree(r->h_pub);
+  if (r->h_stop) (void)hipHostFree(r->h_stop);
+  if (r->h_ended) (void)hipHostFree(r->h_ended);
   if (r->h_reset) (void)hipHostFree(r->h_reset);
   if (r->d_dev) (void)hipFree(r->d_dev);
   if (r->d_table) (void)hipFree(r->d_table);
@@ -128,13 +161,19 @@ T *dev_alias(T *h) {
   return hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? static_cast<T *>(d) : nullptr;
 }
 
+int bad_lane(const bg_ring *r, int lane) {
+  return fail(EINVAL, "lane %d not in [0,%u)", lane, r->nlanes);
+}
+
 }  // namespace
 
 extern "C" {
 
-int bg_em_ring_create(bg_em *em, int device, int slots, int blocks,
+int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
                       uint32_t idle_us, bg_ring **out) {
   if (!em || !out) return fail(EINVAL, "bad arguments");
+  if (lanes < 1 || lanes > kRingMaxLanes)
+    return fail(EINVAL, "lanes %d not in [1,%d]", lanes, kRingMaxLanes);
   if (slots < 2 || slots > 32768 || (slots & (slots - 1)))
     return fail(EINVAL, "slots %d: a power of two in [2, 32768]", slots);
   if (idle_us < 100 || idle_us > 60000000)
@@ -144,34 +183,50 @@ int bg_em_ring_create(bg_em *em, int device, int slots, int blocks,
   bg_ring *r = new bg_ring();
   r->device = device;
   r->nslots = (uint32_t)slots;
-  // workers + the dispatcher
-  r->blocks = (blocks > 0 ? blocks : 2 * num_cus(device)) + 1;
+  r->nlanes = (uint32_t)lanes;
+  // workers (at least one per lane) + the dispatcher
+  int wk = blocks > 0 ? blocks : 2 * num_cus(device);
+  wk = std::max(wk, lanes);
+  r->blocks = wk + 1;
+  const size_t nl = (size_t)lanes, ns = (size_t)slots;
   hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = host_alloc(&r->h_desc, (size_t)slots * 32);
-  if (e == hipSuccess) e = host_alloc(&r->h_done, (size_t)slots * 4);
+  if (e == hipSuccess) e = host_alloc(&r->h_desc, nl * ns * 32);
+  if (e == hipSuccess) e = host_alloc(&r->h_done, nl * ns * 4);
+  if (e == hipSuccess) e = host_alloc(&r->h_pub, nl * kRingLaneWords * 8);
   if (e == hipSuccess) e = host_alloc(&r->h_stop, 64);
-  if (e == hipSuccess) e = host_alloc(&r->h_pub, 64);
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&r->h_reset), 64);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->d_dev), 64);
+  if (e == hipSuccess) e = host_alloc(&r->h_ended, 64);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void **>(&r->h_reset), (nl * kRingLaneWords + 8) * 8);
+  if (e == hipSuccess)
+    e = hipMalloc(reinterpret_cast<void **>(&r->d_dev), (nl * kRingLaneWords + 8) * 8);
   if (e != hipSuccess) {
     ring_release(r);
     delete r;
     return fail(EIO, "ring allocation: %s", hipGetErrorString(e));
   }
-  memset(r->h_desc, 0, (size_t)slots * 32);  // tag 0: no ticket's
-  memset(r->h_done, 0, (size_t)slots * 4);
+  memset(r->h_desc, 0, nl * ns * 32);  // tag 0: no ticket's
+  memset(r->h_done, 0, nl * ns * 4);
+  memset(r->h_pub, 0, nl * kRingLaneWords * 8);
   *r->h_stop = 0;
-  *r->h_pub = 0;
+  *r->h_ended = 0;
+  for (size_t i = 0; i < nl; i++) {
+    RingLane &l = r->lanes[i];
+    l.h_desc = r->h_desc + i * ns * 4;
+    l.h_done = r->h_done + i * ns;
+    l.h_pub = r->h_pub + i * kRingLaneWords;
+  }
   RingArgs &a = r->a;
   a.desc = dev_alias(r->h_desc);
   a.done = dev_alias(r->h_done);
   a.stop = dev_alias(r->h_stop);
   a.pub = dev_alias(r->h_pub);
+  a.ended = dev_alias(r->h_ended);
   a.dev = r->d_dev;
   a.nslots = (uint32_t)slots;
+  a.nlanes = (uint32_t)lanes;
   a.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
-  if (!a.desc || !a.done || !a.stop || !a.pub) {
+  if (!a.desc || !a.done || !a.stop || !a.pub || !a.ended) {
     ring_release(r);
     delete r;
     return fail(EIO, "no device address for the ring's host memory");
@@ -205,8 +260,9 @@ void bg_ring_destroy(bg_ring *r) {
   delete r;
 }
 
-int64_t bg_ring_submit(bg_ring *r, const void *frames, size_t stride, size_t n,
-                       uint16_t default_gate, uint16_t *gates) {
+int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
+                       size_t n, uint16_t default_gate, uint16_t *gates) {
+  if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
   if (n > 0xFFFFFFFFu || stride == 0 || stride > 0xFFFF)
     return fail(EINVAL, "n %zu / stride %zu out of range", n, stride);
   if ((int)stride < r->read_end)
@@ -215,60 +271,67 @@ int64_t bg_ring_submit(bg_ring *r, const void *frames, size_t stride, size_t n,
   if ((((uintptr_t)frames | (uintptr_t)gates) & ~kMaskAddr) ||
       ((uintptr_t)frames & 15) || (stride & 15))
     return fail(EINVAL, "frames 16-byte aligned with stride %% 16 == 0 below 2^48");
-  std::lock_guard<std::mutex> lk(r->mu);
-  // ring full: the oldest ticket must finish before its slot is reused
-  const double t0 = now_s();
-  while (r->next - r->done_upto >= r->nslots) {
-    retire(r);
-    if (r->next - r->done_upto < r->nslots) break;
-    if (int rc = ensure_running(r)) return rc;
-    if (now_s() - t0 > 10.0) return fail(ETIMEDOUT, "ring full for 10 s");
-    _mm_pause();
+  RingLane &l = r->lanes[lane];
+  std::lock_guard<std::mutex> lk(l.mu);
+  // lane full: its oldest ticket must finish before its slot is reused
+  if (l.next - l.done_upto.load(std::memory_order_relaxed) >= r->nslots) {
+    const double t0 = now_s();
+    for (;;) {
+      retire(r, l);
+      if (l.next - l.done_upto.load(std::memory_order_relaxed) < r->nslots) break;
+      if (int rc = ensure_running(r)) return rc;
+      if (now_s() - t0 > 10.0) return fail(ETIMEDOUT, "ring lane full for 10 s");
+      _mm_pause();
+    }
   }
-  const uint64_t t = r->next;
+  const uint64_t t = l.next;
   const uint64_t tag = ((t + 1) & 0xFFFF) << 48;
-  uint64_t *d = r->h_desc + (t % r->nslots) * 4;
+  uint64_t *d = l.h_desc + (t % r->nslots) * 4;
   __atomic_store_n(d + 0, ((uint64_t)(uintptr_t)frames & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 1, ((uint64_t)(uintptr_t)gates & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 2, (uint64_t)n | ((uint64_t)stride << 32) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 3, (uint64_t)default_gate | tag, __ATOMIC_RELAXED);
-  __atomic_store_n(r->h_pub, t + 1, __ATOMIC_RELEASE);
-  r->next = t + 1;
+  __atomic_store_n(l.h_pub, t + 1, __ATOMIC_RELEASE);
+  l.next = t + 1;
   if (int rc = ensure_running(r)) return rc;
   return (int64_t)t;
 }
 
-int bg_ring_wait(bg_ring *r, int64_t ticket) {
-  std::lock_guard<std::mutex> lk(r->mu);
-  if (ticket < 0 || (uint64_t)ticket >= r->next)
+int bg_ring_wait(bg_ring *r, int lane, int64_t ticket) {
+  if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
+  RingLane &l = r->lanes[lane];
+  std::lock_guard<std::mutex> lk(l.mu);
+  if (ticket < 0 || (uint64_t)ticket >= l.next)
     return fail(EINVAL, "ticket %lld not submitted", (long long)ticket);
   const double t0 = now_s();
   for (;;) {
-    retire(r);
-    if ((uint64_t)ticket < r->done_upto) return 0;
+    retire(r, l);
+    if ((uint64_t)ticket < l.done_upto.load(std::memory_order_relaxed)) return 0;
     if (int rc = ensure_running(r)) return rc;
     if (now_s() - t0 > 10.0) return fail(ETIMEDOUT, "ticket %lld: 10 s", (long long)ticket);
     _mm_pause();
   }
 }
 
-int64_t bg_ring_completed(bg_ring *r) {
-  std::lock_guard<std::mutex> lk(r->mu);
-  retire(r);
+int64_t bg_ring_completed(bg_ring *r, int lane) {
+  if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
+  RingLane &l = r->lanes[lane];
+  std::lock_guard<std::mutex> lk(l.mu);
+  retire(r, l);
   if (int rc = ensure_running(r)) return rc;
-  return (int64_t)r->done_upto;
+  return (int64_t)l.done_upto.load(std::memory_order_relaxed);
 }
 
-int bg_ring_run(bg_ring *r, const void *frames, size_t stride, size_t n,
+int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride, size_t n,
                 size_t burst, uint16_t default_gate, uint16_t *gates) {
   if (burst < 1) return fail(EINVAL, "burst must be >= 1");
   int64_t last = -1;
   for (size_t i = 0; i < n; i += burst) {
-    last = bg_ring_submit(r, static_cast<const uint8_t *>(frames) + i * stride, stride,
-                          std::min(burst, n - i), default_gate, gates + i);
+    last = bg_ring_submit(r, lane, static_cast<const uint8_t *>(frames) + i * stride,
+                          stride, std::min(burst, n - i), default_gate, gates + i);
     if (last < 0) return (int)last;
   }
-  return last < 0 ? 0 : bg_ring_wait(r, last);
+  return last < 0 ? 0 : bg_ring_wait(r, lane, last);
 }
 
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks) {

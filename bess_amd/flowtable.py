@@ -186,14 +186,17 @@ class Comm:
 
 class Ring:
     """bg_ring: one persistent ExactMatch kernel draining batch descriptors
-    (the table as of creation, in LDS for the kernel's whole run)."""
+    from `lanes` submission lanes, one per worker thread (the table as of
+    creation, in LDS for the kernel's whole run)."""
 
-    def __init__(self, table, device=0, slots=1024, blocks=0, idle_us=200000):
+    def __init__(self, table, device=0, slots=1024, blocks=0, idle_us=200000,
+                 lanes=1):
         h = C.c_void_p()
-        check(lib().bg_em_ring_create(table.h, device, slots, blocks, idle_us,
-                                      C.byref(h)))
+        check(lib().bg_em_ring_create(table.h, device, lanes, slots, blocks,
+                                      idle_us, C.byref(h)))
         self.h = h
         self.table = table
+        self.lanes = lanes
 
     def close(self):
         if getattr(self, "h", None) is not None and _lib._lib is not None:
@@ -202,22 +205,51 @@ class Ring:
 
     __del__ = close
 
-    def submit(self, frames, stride, n, default_gate, gates, offset=0):
+    def submit(self, frames, stride, n, default_gate, gates, offset=0, lane=0):
         """frames / gates: device tensors; batch = packets [offset, offset+n)"""
-        t = lib().bg_ring_submit(self.h, C.c_void_p(frames.data_ptr() + offset * stride),
+        t = lib().bg_ring_submit(self.h, lane,
+                                 C.c_void_p(frames.data_ptr() + offset * stride),
                                  stride, n, default_gate,
                                  C.c_void_p(gates.data_ptr() + 2 * offset))
         return check(t)
 
-    def wait(self, ticket):
-        check(lib().bg_ring_wait(self.h, ticket))
+    def wait(self, ticket, lane=0):
+        check(lib().bg_ring_wait(self.h, lane, ticket))
 
-    def completed(self):
-        return check(lib().bg_ring_completed(self.h))
+    def completed(self, lane=0):
+        return check(lib().bg_ring_completed(self.h, lane))
 
-    def run(self, frames, stride, n, burst, default_gate, gates):
-        check(lib().bg_ring_run(self.h, _dev_ptr(frames), stride, n, burst,
-                                default_gate, _dev_ptr(gates)))
+    def run(self, frames, stride, n, burst, default_gate, gates, lane=0, offset=0):
+        """packets [offset, offset + n) in batches of `burst` on one lane"""
+        check(lib().bg_ring_run(self.h, lane,
+                                C.c_void_p(frames.data_ptr() + offset * stride),
+                                stride, n, burst, default_gate,
+                                C.c_void_p(gates.data_ptr() + 2 * offset)))
+
+    def run_lanes(self, frames, stride, n, burst, default_gate, gates, threads):
+        """`threads` submitters at once (threads <= lanes), thread i on lane
+        i over packets [i*n/threads, (i+1)*n/threads); -> wall seconds"""
+        import threading
+        import time
+        errs = []
+
+        def work(i):
+            lo, hi = n * i // threads, n * (i + 1) // threads
+            try:
+                self.run(frames, stride, hi - lo, burst, default_gate, gates, lane=i,
+                         offset=lo)
+            except Exception as e:  # reported below
+                errs.append(e)
+        ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        return dt
 
     def info(self):
         launches, blocks = C.c_uint64(), C.c_int()

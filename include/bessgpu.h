@@ -531,34 +531,38 @@ size_t bg_pipe_pending(const bg_pipe *p);
 int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                 const uint16_t *lens, size_t n, size_t burst, uint16_t *ogates);
 
-/* ---- Persistent classify kernel: a ring of batch descriptors ------------
+/* ---- Persistent classify kernel: rings of batch descriptors -------------
  * BESS hands a module <= 32 packets per ProcessBatch (core/pktbatch.h:70);
  * a kernel launch per batch costs more than the batch. A ring is ONE
- * running ExactMatch kernel that drains batch descriptors a worker writes
- * into pinned host memory (the Queue split, core/modules/queue.cc:173,190):
- * submit enqueues a batch (frames at `frames` + i*stride, device or mapped
- * host memory; gates written to `gates`) and returns its ticket; wait
- * blocks until that ticket's gates are written; completed returns the
- * number of tickets finished in order. The kernel keeps the table in LDS
- * for its whole run and classifies with the rule set as of
- * bg_em_ring_create (it holds its own copy of the table image: re-create
- * the ring after rule changes, which bessd makes with workers paused).
- * slots: ring size, a power of two <= 32768 (submit blocks while `slots`
- * tickets are unfinished); blocks: workgroups (0: 2 per CU); idle_us: the
- * kernel exits after this long without work and is relaunched by the next
- * submit (so it never outlives its work). One ring per worker thread. */
+ * running ExactMatch kernel that drains batch descriptors the workers write
+ * into pinned host memory (the Queue split, core/modules/queue.cc:173,190).
+ * Each worker thread submits on its own lane (0 .. lanes-1: its own ring of
+ * `slots` descriptors, done words and published count, so workers never
+ * share a cache line or a lock): submit enqueues a batch (frames at
+ * `frames` + i*stride, device or mapped host memory; gates written to
+ * `gates`) and returns the lane's ticket; wait blocks until that ticket's
+ * gates are written; completed returns the number of the lane's tickets
+ * finished in order. The grid's workgroups are spread over the lanes; the
+ * kernel keeps the table in LDS for its whole run and classifies with the
+ * rule set as of bg_em_ring_create (it holds its own copy of the table
+ * image: re-create the ring after rule changes, which bessd makes with
+ * workers paused). slots: a power of two <= 32768 (submit blocks while
+ * `slots` of the lane's tickets are unfinished); blocks: workgroups (0: 2 per
+ * CU); idle_us: the kernel exits after this long without work and is
+ * relaunched by the next submit or wait (so it never outlives its work); a
+ * submit makes no HIP call while the kernel runs. */
 typedef struct bg_ring bg_ring;
-int bg_em_ring_create(bg_em *em, int device, int slots, int blocks,
+int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
                       uint32_t idle_us, bg_ring **out);
 void bg_ring_destroy(bg_ring *r); /* stops the kernel and waits for it */
-int64_t bg_ring_submit(bg_ring *r, const void *frames, size_t stride, size_t n,
-                       uint16_t default_gate, uint16_t *gates);
-int bg_ring_wait(bg_ring *r, int64_t ticket);
-int64_t bg_ring_completed(bg_ring *r);
-/* A worker loop: n packets in batches of `burst` submitted back to back,
- * then waits for the last (the persistent series of the C2 sweep). */
-int bg_ring_run(bg_ring *r, const void *frames, size_t stride, size_t n,
-                size_t burst, uint16_t default_gate, uint16_t *gates);
+int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
+                       size_t n, uint16_t default_gate, uint16_t *gates);
+int bg_ring_wait(bg_ring *r, int lane, int64_t ticket);
+int64_t bg_ring_completed(bg_ring *r, int lane);
+/* A worker loop on one lane: n packets in batches of `burst` submitted back
+ * to back, then waits for the last (the persistent series of the C2 sweep). */
+int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride,
+                size_t n, size_t burst, uint16_t default_gate, uint16_t *gates);
 /* kernel launches so far (1 + relaunches after idle exits), workgroups */
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks);
 

@@ -27,7 +27,8 @@
 //                                 -> "pipeline <Mpps> <seconds> <packets>",
 //                                 "out" as above for the last pass, and with
 //                                 verify "order ok|bad": each worker's
-//                                 packets left in the order they came in
+//                                 emitted packets left in the order they
+//                                 came in (hence per gate, module.h:268-272)
 #include <pthread.h>
 #include <sched.h>
 #include <stdio.h>
@@ -126,6 +127,8 @@ struct Sink {  // where a worker's emitted and dropped packets go
   uint8_t *pool = nullptr;
   uint64_t n = 0;
   void take(Context &ctx) {
+    // (emitted packets in emission order; drops go to the dead batch, so
+    // only emitted packets carry an emission sequence number)
     for (auto &e : ctx.emitted) put(e.first, e.second);
     for (auto *p : ctx.dropped) put(p, 0xFFFF);
     n += ctx.emitted.size() + ctx.dropped.size();
@@ -136,7 +139,7 @@ struct Sink {  // where a worker's emitted and dropped packets go
     const size_t i = (size_t)(reinterpret_cast<uint8_t *>(p) - pool) / kObj;
     if (fast) (*fast)[i] = (uint16_t)g;
     if (gate) (*gate)[i] = g == 0xFFFF ? "D" : std::to_string(g);
-    if (seq) (*seq)[i] = (*counter)++;
+    if (seq && g != 0xFFFF) (*seq)[i] = (*counter)++;
   }
 };
 

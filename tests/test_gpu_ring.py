@@ -84,3 +84,31 @@ def test_ring_idle_exit_relaunch_and_snapshot():
     ring.run(d, 64, n, 512, 8192, dg)
     assert (dg.cpu().numpy().view(np.uint16) == 8192).all()
     ring.close()
+
+
+@pytest.mark.parametrize("lanes,threads", [(4, 4), (16, 16), (16, 3)])
+def test_ring_submission_lanes_vs_oracle(lanes, threads):
+    """several worker threads, each on its own submission lane of one
+    running kernel, 32-packet batches (and ragged 100-packet ones): every
+    gate as the oracle's; an idle exit in between relaunches for all lanes"""
+    n = 1 << 18
+    keys, gates, frames = P.em_workload(1000, n, seed=lanes, pkt_seed=9)
+    want = oracle_gates(keys, gates, frames)
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    d = torch.from_numpy(frames.reshape(-1)).cuda()
+    ring = F.Ring(t, slots=512, lanes=lanes, idle_us=3000)
+    for burst in (32, 100):
+        dg = torch.full((n,), -1, dtype=torch.int16, device="cuda")
+        ring.run_lanes(d, 64, n, burst, 8192, dg, threads)
+        torch.cuda.synchronize()
+        assert (dg.cpu().numpy().view(np.uint16) == want).all(), burst
+        time.sleep(0.02)  # idle: the grid stops; the next run relaunches it
+    launches, _ = ring.info()
+    assert launches >= 2
+    # tickets count per lane
+    for lane in range(min(lanes, 3)):
+        tk = ring.submit(d, 64, 32, 8192, dg, offset=32 * lane, lane=lane)
+        ring.wait(tk, lane=lane)
+        assert ring.completed(lane=lane) == tk + 1
+    ring.close()
