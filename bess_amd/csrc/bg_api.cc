@@ -1266,6 +1266,9 @@ static int wm_build_host(bg_wm *wm, bool no_tags) {
     a.dspec[d] = wm->dspec[d];
     a.doff[d] = wm->doff[d];
   }
+  a.hmask = 0;
+  for (size_t t = 0; t < wm->tuples.size(); t++)
+    if (!wm_is_direct(wm, t)) a.hmask |= 1u << t;
   return 0;
 }
 

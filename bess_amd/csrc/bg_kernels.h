@@ -123,6 +123,7 @@ struct WmArgs {
   // hashed table's format, empty = all ones), one read per packet, no hash,
   // no fingerprint, no key compare.
   uint32_t ndirect;
+  uint32_t hmask;  // bit tu: tuple tu is probed by hash (tu < ntuples, not direct)
   uint32_t dtu[kMaxDirect];    // tuple index
   uint32_t dspec[kMaxDirect];  // key byte a | byte b << 8 | mask a << 16 | mask b << 24
   uint64_t doff[kMaxDirect];   // the table's byte offset in the image

@@ -125,18 +125,25 @@ BG_HD uint32_t wm_hash(const uint32_t *kd, uint32_t cover, int ndw, uint32_t see
   return h;
 }
 
+// The second bucket's offset from the first: an odd number from the
+// fingerprint alone (partial-key cuckoo hashing), so a (first bucket,
+// fingerprint) pair names both buckets -- the tag-word kernel queues one
+// entry per (packet, tuple) and its check derives the other bucket.
+BG_HD uint32_t wm_alt(uint32_t tag, uint32_t lg) {
+  return lg ? (((tag * 0x5BD1E995u) >> (32 - lg)) | 1u) : 0u;
+}
 // first bucket from the low bits, fingerprint from the top byte, second
-// bucket the first XOR an odd number from the top bits of one more product
+// bucket the first XOR the fingerprint's odd offset (wm_alt)
 // (nbp = 2^lg, lg >= 1)
 BG_HD Probe wm_probe(uint32_t h, uint32_t lg) {
   Probe p;
   const uint32_t m = (1u << lg) - 1;
   p.part = 0;
   p.b1 = h & m;
-  // b1 XOR an odd offset: never b1, no compare-and-fix
-  p.b2 = p.b1 ^ (((h * 0xC2B2AE35u) >> (32 - lg)) | 1u);
   const uint32_t t = h >> 24;
   p.tag = t ? t : 1u;
+  // b1 XOR an odd offset: never b1 (lg > 0), no compare-and-fix
+  p.b2 = p.b1 ^ wm_alt(p.tag, lg);
   return p;
 }
 

@@ -11,13 +11,12 @@
 //      P4), the next tile's window in flight;
 //   2. per tuple (wave-uniform): key & mask, hash, both tag words from
 //      LDS (all tuples' reads issued before any is used);
-//   3. every fingerprint match goes into a per-wave LDS queue as (slot,
-//      lane, tuple): each lane counts its matches, a bit-sliced wave prefix
-//      sum (one ballot + mbcnt per count bit) gives each lane its first
-//      queue position, and each lane writes its own entries -- so the key
-//      checks run on dense lanes instead of on whichever lanes matched
-//      (measured: the per-tuple ballot loop this replaces took a third of
-//      the kernel);
+//   3. every (packet, tuple) whose buckets hold the packet's fingerprint
+//      goes into a per-wave LDS queue as (first bucket, lane, tuple,
+//      fingerprint) -- the second bucket follows from the first and the
+//      fingerprint (wm_alt) -- at a scalar base + mbcnt of the tuple's
+//      match mask, so the key checks run on dense lanes instead of on
+//      whichever lanes matched;
 //   4. the queue (<= 256 entries; more go in further rounds) is checked
 //      with up to four entries per lane, all their loads in flight at
 //      once: a lane loads each entry's slot key and value from L2 and the
@@ -87,34 +86,41 @@ __device__ __forceinline__ bool wm_hit(const uint64_t *mlds, uint32_t e,
   return hit;
 }
 
-// fingerprint matches of entry e's tag in its bucket: bit 7 of each byte
-__device__ __forceinline__ uint32_t entry_matches(const uint32_t *tags, uint32_t e) {
-  return zero_bytes(tags[e & 0x7FFFu] ^ __builtin_amdgcn_perm(0u, e >> 24, 0u));
+// fingerprint matches of entry e's tag in bucket b: bit 7 of each byte
+__device__ __forceinline__ uint32_t bucket_matches(const uint32_t *tags, uint32_t b,
+                                                   uint32_t e) {
+  return zero_bytes(tags[b] ^ __builtin_amdgcn_perm(0u, e >> 24, 0u));
 }
 
-__device__ __forceinline__ uint32_t match_slot(uint32_t e, uint32_t z) {
-  return (e & 0x7FFFu) * kSlots + (__builtin_ctz(z) >> 3);
+// Entry e = (packet, tuple, first bucket b1, fingerprint); its second bucket
+// is b1 ^ wm_alt(fingerprint). Candidate slots: the matches of b1 (z1),
+// then those of b2 (z2); the next candidate's slot index.
+__device__ __forceinline__ uint32_t next_slot(uint32_t e, uint32_t lg, uint32_t z1,
+                                              uint32_t z2) {
+  const uint32_t b1 = e & 0x7FFFu;
+  const uint32_t b = z1 ? b1 : b1 ^ wm_alt(e >> 24, lg);
+  return b * kSlots + (__builtin_ctz(z1 ? z1 : z2) >> 3);
 }
 
 // Check queue entries [0, m), m <= kQueue: lane l takes entries l, l + 64,
-// ... Each entry is a (packet, tuple, bucket) whose tag word holds the
-// packet's fingerprint: the lane re-reads the tag word, and the first
-// matching slot's key and value loads of every entry are issued before any
-// is compared (one L2 round trip). An entry whose first match is not the
-// key (a fingerprint collision) tries its further matches (rare).
+// ... Each entry is a (packet, tuple) whose tag words hold the packet's
+// fingerprint in one of its two buckets: the lane re-reads both tag words,
+// and the first candidate slot's key and value loads of every entry are
+// issued before any is compared (one L2 round trip). An entry whose first
+// candidate is not the key (a fingerprint collision) tries the rest (rare).
 template <int KW>
 __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
                                          const uint64_t *mlds, uint64_t *best,
                                          const uint32_t *q, uint32_t m, int lane,
-                                         const uint64_t (&k)[KW]) {
+                                         uint32_t lg, const uint64_t (&k)[KW]) {
   const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
-  uint32_t e[kPerLane], z[kPerLane];
+  uint32_t e[kPerLane], z1[kPerLane], z2[kPerLane];
   uint64_t v[kPerLane], sk[kPerLane][KW], kk[kPerLane][KW];
 #pragma unroll
   for (int r = 0; r < kPerLane; r++) {
     const uint32_t i = (uint32_t)lane + 64u * r;
-    e[r] = z[r] = 0;
+    e[r] = z1[r] = z2[r] = 0;
     v[r] = 0;
 #pragma unroll
     for (int j = 0; j < KW; j++) sk[r][j] = kk[r][j] = 0;
@@ -122,8 +128,10 @@ __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
       e[r] = q[i];
       owner_key<KW>(e[r], k, kk[r]);
       if (i < m) {
-        z[r] = entry_matches(tags, e[r]);
-        const uint32_t slot = match_slot(e[r], z[r]);
+        const uint32_t b1 = e[r] & 0x7FFFu;
+        z1[r] = bucket_matches(tags, b1, e[r]);
+        z2[r] = bucket_matches(tags, b1 ^ wm_alt(e[r] >> 24, lg), e[r]);
+        const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
 #ifdef BG_AB  // phase timing: checks without their L2 loads
         if (a.ab_phase == 3) continue;
 #endif
@@ -140,37 +148,43 @@ __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
     if (i < m) {
       if (wm_hit<KW>(mlds, e[r], v[r], sk[r], kk[r])) {
         wm_fold(best, e[r], v[r]);
-        z[r] = 0;
+        z1[r] = z2[r] = 0;
+      } else if (z1[r]) {  // the candidates not tried yet
+        z1[r] &= z1[r] - 1;
       } else {
-        z[r] &= z[r] - 1;  // the matches not tried yet
+        z2[r] &= z2[r] - 1;
       }
     } else {
-      z[r] = 0;
+      z1[r] = z2[r] = 0;
     }
-    more |= z[r] != 0;
+    more |= (z1[r] | z2[r]) != 0;
   }
   if (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform, rare
 #pragma unroll
     for (int r = 0; r < kPerLane; r++) {
-      while (z[r]) {
-        const uint32_t slot = match_slot(e[r], z[r]);
-        z[r] &= z[r] - 1;
+      while (z1[r] | z2[r]) {
+        const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
+        if (z1[r])
+          z1[r] &= z1[r] - 1;
+        else
+          z2[r] &= z2[r] - 1;
         const uint64_t vv = vals[slot];
         uint64_t s2[KW];
 #pragma unroll
         for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * KW + j];
         if (wm_hit<KW>(mlds, e[r], vv, s2, kk[r])) {
           wm_fold(best, e[r], vv);
-          z[r] = 0;
+          z1[r] = z2[r] = 0;
         }
       }
     }
   }
 }
 
-// any byte of x zero (the SWAR test of zero_bytes, as a predicate)
-__device__ __forceinline__ bool has_zero_byte(uint32_t x) {
-  return ((x - 0x01010101u) & ~x & 0x80808080u) != 0;
+// bit 7 of each byte of x that is zero, OR-ed over two words (the SWAR
+// test of zero_bytes; only the any-match result is exact)
+__device__ __forceinline__ uint32_t zero_bytes2(uint32_t x, uint32_t y) {
+  return (((x - 0x01010101u) & ~x) | ((y - 0x01010101u) & ~y)) & 0x80808080u;
 }
 
 // Dense 64 B header slab (PAIR): the two 16-byte window chunks of a slot
@@ -285,58 +299,57 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
     }
 #endif
     const kconst_u64 tm = tuple_masks(a);  // laundered per tile: no hoisting
-    const int ntu = (int)tuple_words(a, offsetof(WmArgs, ntuples))[0];
+    const uint32_t hmask = tuple_words(a, offsetof(WmArgs, hmask))[0];
 
-    // A. every tuple's hash and both tag words (16 LDS reads in flight)
-    uint32_t b[2 * kMaxTuples], c[2 * kMaxTuples], et[kMaxTuples];
+    // A. every hashed tuple's probe: both tag words from LDS (all reads in
+    // flight before any is used); zz[tu] != 0 iff a bucket holds the
+    // packet's fingerprint, ent[tu] its queue entry
+    uint32_t zz[kMaxTuples], ent[kMaxTuples];
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
-      b[2 * tu] = b[2 * tu + 1] = 0;
-      c[2 * tu] = c[2 * tu + 1] = 0xFFFFFFFFu;  // no zero byte: no match
-      et[tu] = 0;
-      bool direct = false;
-#pragma unroll
-      for (int d = 0; d < kMaxDirect; d++) direct |= (uint32_t)d < ndir && dtu[d] == (uint32_t)tu;
-      if (tu < ntu && !direct) {
+      zz[tu] = 0;
+      ent[tu] = 0;
+      if ((hmask >> tu) & 1u) {  // wave-uniform (a scalar test)
         const Probe p = wm_probe(wm_tuple_hash<KW>(k, tm, tu, a), lg);
-        b[2 * tu] = p.b1;
-        b[2 * tu + 1] = p.b2;
         const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
-        c[2 * tu] = tags[p.b1] ^ tb;  // zero bytes = fingerprint matches
-        c[2 * tu + 1] = tags[p.b2] ^ tb;
-        et[tu] = ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24);
+        zz[tu] = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
+        ent[tu] = p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24);
       }
     }
-    // B/C. queue entries, one per (packet, tuple, bucket) with a
-    // fingerprint match, bucket-major: for each bucket word the wave's
-    // mask of matching lanes gives each lane its position (a scalar base +
-    // mbcnt) and the base advances by the mask's popcount. The entries
-    // that fall into [r0, r0 + kQueue) are written, then checked; the
-    // first round's base ends as the tile's total (more rounds are rare:
-    // over four candidate buckets per packet).
+    // B/C. one queue entry per (packet, tuple) with a fingerprint match,
+    // tuple-major: the wave's mask of matching lanes gives each lane its
+    // position (a scalar base + mbcnt) and the base advances by the mask's
+    // popcount. Usually the tile's entries fit one queue; more go in
+    // further rounds of kQueue.
     const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
+    uint64_t mk[kMaxTuples];
     uint32_t total = 0;
-    for (uint32_t r0 = 0;; r0 += kQueue) {
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      mk[tu] = __builtin_amdgcn_ballot_w64(zz[tu] != 0) & livemask;
+      total += (uint32_t)__popcll(mk[tu]);
+    }
+    for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
       uint32_t base = 0;
 #pragma unroll
-      for (int x = 0; x < 2 * kMaxTuples; x++) {
-        const bool hz = live && has_zero_byte(c[x]);
-        const uint64_t mk = __builtin_amdgcn_ballot_w64(hz) & livemask;
+      for (int tu = 0; tu < kMaxTuples; tu++) {
         const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, base));
-        if (hz && pos - r0 < kQueue) q[pos - r0] = b[x] | et[x / 2];
-        base += (uint32_t)__popcll(mk);
+            (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
+        const bool mine = live && zz[tu] != 0;
+        if (total <= kQueue) {  // wave-uniform: one round, no window test
+          if (mine) q[pos] = ent[tu];
+        } else if (mine && pos - r0 < kQueue) {
+          q[pos - r0] = ent[tu];
+        }
+        base += (uint32_t)__popcll(mk[tu]);
       }
-      total = base;
 #ifdef BG_AB  // phase timing: + hashes, tag reads and the queue writes
       if (a.ab_phase == 2) break;
 #endif
-      if (total <= r0) break;
       lds_fence();
       const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
-      wm_check<KW>(a, tags, mlds, best, q, m, lane, k);
+      wm_check<KW>(a, tags, mlds, best, q, m, lane, lg, k);
       lds_fence();  // the queue is rewritten by the next round
-      if (total <= r0 + kQueue) break;
     }
     lds_fence();
     uint64_t bb = best[lane];

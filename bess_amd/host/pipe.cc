@@ -47,7 +47,9 @@ struct Slot {
   uint8_t *h_wb = nullptr;                    // header lines back (writeback)
   uint16_t *h_g = nullptr, *d_g = nullptr;    // gates
   hipStream_t st = nullptr;
-  hipEvent_t ev = nullptr;
+  uint64_t *h_done = nullptr;  // pinned, mapped: = seq once the slot's D2H is done
+  uint64_t *d_done = nullptr;  // its device address (hipStreamWriteValue64)
+  uint64_t seq = 0;            // this launch's number
   std::vector<uint8_t *> heads;  // writeback targets
   std::vector<uint16_t> wblen;   // bytes of the header line to write back
   std::vector<void *> cookies;
@@ -73,6 +75,7 @@ struct bg_pipe {
   std::deque<std::pair<void *, uint16_t>> ready;  // completed, not returned
   size_t pending = 0;    // submitted, not yet returned by poll
   int err = 0;           // sticky launch error
+  uint64_t launched = 0;  // slot launches so far (Slot::seq)
   // One worker owns a pipe; the lock is for the module's control path
   // (PipeFlushLocked) and a RunTask on another worker (never contended on
   // the datapath).
@@ -88,9 +91,9 @@ static void pipe_release(bg_pipe *p) {
     if (s.h_in) (void)hipHostFree(s.h_in);
     if (s.h_wb) (void)hipHostFree(s.h_wb);
     if (s.h_g) (void)hipHostFree(s.h_g);
+    if (s.h_done) (void)hipHostFree(s.h_done);
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_g) (void)hipFree(s.d_g);
-    if (s.ev) (void)hipEventDestroy(s.ev);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   p->slots.clear();
@@ -103,6 +106,8 @@ static void pipe_release(bg_pipe *p) {
 static int launch_slot(bg_pipe *p) {
   Slot &s = p->slots[p->fill];
   const size_t n = s.n;
+  int rc = bg::set_device(p->device);
+  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
   bg_ctx c = s.ctx;
   c.device = (int16_t)p->device;
@@ -114,7 +119,10 @@ static int launch_slot(bg_pipe *p) {
     HIP_TRY(hipMemcpy2DAsync(s.h_wb, line, s.d_in, p->w, line, n,
                              hipMemcpyDeviceToHost, s.st));
   }
-  HIP_TRY(hipEventRecord(s.ev, s.st));
+  // completion lands in host memory after the D2H copies: poll reads one
+  // word and makes no HIP call
+  s.seq = ++p->launched;
+  HIP_TRY(hipStreamWriteValue64(s.st, s.d_done, s.seq, 0));
   s.inflight = true;
   p->inflight++;
   p->fill = (p->fill + 1) % p->slots.size();
@@ -126,13 +134,14 @@ static int launch_slot(bg_pipe *p) {
 static int retire_oldest(bg_pipe *p, bool wait) {
   if (p->inflight == 0) return 0;
   Slot &s = p->slots[p->oldest];
-  if (wait) {
-    HIP_TRY(hipEventSynchronize(s.ev));
-  } else {
-    hipError_t q = hipEventQuery(s.ev);
-    if (q == hipErrorNotReady) return 0;
-    if (q != hipSuccess)
-      return fail(EIO, "HIP error %d: %s", (int)q, hipGetErrorString(q));
+  if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq) {
+    if (!wait) return 0;
+    int rc = bg::set_device(p->device);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s.st));
+    if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq)
+      return fail(EIO, "pipe slot %llu: completion word not written",
+                  (unsigned long long)s.seq);
   }
   if (p->writeback) {
     const size_t line = std::min(p->w, kWriteback);
@@ -178,7 +187,13 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
       e = hipHostMalloc(reinterpret_cast<void **>(&s.h_wb),
                         batch * std::min(p->w, kWriteback), hipHostMallocDefault);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
+    if (e == hipSuccess)
+      e = hipHostMalloc(reinterpret_cast<void **>(&s.h_done), 64,
+                        hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+      *s.h_done = 0;
+      e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.d_done), s.h_done, 0);
+    }
     if (e != hipSuccess) {
       pipe_release(p);
       delete p;
@@ -229,8 +244,7 @@ int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                    const uint16_t *lens, void *const *cookies, size_t cnt) {
   std::lock_guard<std::mutex> lk(p->mu);
   if (p->err) return p->err;
-  int r = bg::set_device(p->device);
-  if (r) return r;
+  int r;
   const bg_ctx c = ResolveCtx(ctx, p->device);
   const size_t span = (size_t)(p->hi - p->lo);
   size_t i = 0;
@@ -285,9 +299,7 @@ static int flush(bg_pipe *p) {
   if (p->err) return p->err;
   Slot &s = p->slots[p->fill];
   if (s.inflight || s.n == 0) return 0;
-  int r = bg::set_device(p->device);
-  if (r) return r;
-  r = launch_slot(p);
+  int r = launch_slot(p);
   if (r < 0) return p->err = r;
   return 0;
 }
