@@ -356,9 +356,10 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
         torch.cuda.synchronize()
         ms = timed(g.replay)
         out["graph"][str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
-    ring = F.Ring(t, slots=4096, lanes=16)
     npk = 1 << 20
-    for T in (1, 4, 16):
+    launches0 = 0
+    for T in (1, 4, 16):  # a ring with one submission lane per submitter
+        ring = F.Ring(t, slots=4096, lanes=T)
         key = "persistent" if T == 1 else "persistent_%dsub" % T
         out[key] = {}
         for B in batches:
@@ -366,11 +367,12 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
             best = min(ring.run_lanes(d_frames, 64, npk, B, 8192, d_gates, T)
                        for _ in range(3))
             out[key][str(B)] = round(npk / best / 1e6, 1)
-    launches0, blocks = ring.info()
-    ring.close()
+        launches, blocks = ring.info()
+        launches0 += launches
+        ring.close()
     out["persistent_info"] = {"packets_per_point": npk, "kernel_launches": launches0,
                               "workgroups": blocks, "slots_per_lane": 4096,
-                              "lanes": 16, "submitters": [1, 4, 16],
+                              "lanes": "one per submitter", "submitters": [1, 4, 16],
                               "timing": "host wall, best of 3"}
     return out
 
@@ -672,7 +674,7 @@ def run_plugin_pipeline(args):
     want = om.process(frames, 64, n)
     script += ["connect %d" % g for g in range(65)]
     threads = [int(x) for x in args.pipe_threads.split(",")]
-    res, parity = {}, {}
+    res, parity, pipe_stats = {}, {}, {}
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "frames.bin")
         frames.tofile(path)
@@ -690,6 +692,9 @@ def run_plugin_pipeline(args):
                 res[str(t)] = "failed: rc %d %s" % (r.returncode, r.stderr[-300:])
                 continue
             res[str(t)] = round(float(stats[-1].split()[1]), 1)
+            pst = [x for x in lines if x.startswith("stats")]
+            if pst:
+                pipe_stats[str(t)] = pst[-1][6:]
             # EmitPacket to DROP_GATE (the default gate) drops: "D"
             exp = ["D" if int(w) >= 8192 else str(int(w)) for w in want]
             parity[str(t)] = outs[-1].split()[1:] == exp
@@ -698,7 +703,7 @@ def run_plugin_pipeline(args):
                     "pkts in 2624 B snbufs split over the workers as the "
                     "cpu_baseline splits them" % n,
             "Mpps_by_workers": res, "pipe": {"batch": 16384, "depth": 4},
-            "parity": parity}
+            "worker0_pipe_stats": pipe_stats, "parity": parity}
 
 
 def _time_steps(step, args, torch):

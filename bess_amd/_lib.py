@@ -141,6 +141,7 @@ _SIGS = {
     "bg_pipe_flush": (_int, [_vp]),
     "bg_pipe_poll": (C.c_long, [_vp, _int, _vp, _vp, _sz]),
     "bg_pipe_pending": (_sz, [_vp]),
+    "bg_pipe_stats": (_int, [_vp, _vp, _int]),
     "bg_pipe_run": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
     "bg_em_ring_create": (_int, [_vp, _int, _int, _int, _int, C.c_uint32,
                                  C.POINTER(_vp)]),

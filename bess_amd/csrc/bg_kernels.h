@@ -325,7 +325,7 @@ struct RingArgs {
   FieldPlan fp;
   TableRef t;
 };
-constexpr int kRingBlock = 256;
+constexpr int kRingBlock = 64;  // one wave: a 32-packet batch fills half of it
 constexpr int kRingLaneWords = 8;
 constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
 

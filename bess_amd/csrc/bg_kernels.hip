@@ -460,34 +460,13 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
   }
 }
 
-// A workgroup (b >= 1) takes the next published ticket of any lane, its
-// home lane (b - 1) % nlanes first: it claims a ticket only once the
-// lane's mirror shows it published (check, then a CAS on the lane's claim
-// counter), so an idle lane never holds a workgroup. It reads the
-// descriptor (every word tagged with the ticket), classifies the batch,
-// writes the gates through to memory (sc0 sc1 stores: no L2 write-back
-// needed) and marks the ticket done in host memory.
-__device__ __forceinline__ bool ring_claim(const RingArgs &a, uint32_t home,
-                                           uint32_t *lane, uint64_t *t) {
-  for (uint32_t j = 0; j < a.nlanes; j++) {
-    uint32_t l = home + j;
-    if (l >= a.nlanes) l -= a.nlanes;
-    unsigned long long *dl = a.dev + (size_t)l * kRingLaneWords;
-    uint64_t c = ld_agent(dl);
-    while (c < ld_agent(dl + 1)) {
-      const unsigned long long got = atomicCAS(dl, (unsigned long long)c,
-                                               (unsigned long long)(c + 1));
-      if (got == c) {
-        *lane = l;
-        *t = c;
-        return true;
-      }
-      c = got;
-    }
-  }
-  return false;
-}
-
+// Workgroup b >= 1 serves submission lane (b - 1) % nlanes: it claims the
+// lane's next ticket (one atomic; claims run ahead of publication, so the
+// lane's workgroups queue up on its coming tickets), waits until it is
+// published, reads the descriptor (every word tagged with the ticket),
+// classifies the batch, writes the gates through to memory (sc0 sc1
+// stores: no L2 write-back per ticket) and marks the ticket done in host
+// memory. Create a ring with as many lanes as workers submit on.
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
@@ -499,25 +478,27 @@ void em_ring_kernel(RingArgs a) {
     if (threadIdx.x < 64) ring_dispatch(a);
     return;
   }
-  const uint32_t home = (blockIdx.x - 1) % a.nlanes;
+  const uint32_t lane = (blockIdx.x - 1) % a.nlanes;
+  unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
   const unsigned long long *dstop = a.dev + (size_t)a.nlanes * kRingLaneWords;
-  __shared__ uint32_t sh_lane;
+  const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * 4;
+  uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   copy_table_to_lds(lds, a.t);  // (ends with a barrier)
   const uint64_t mask48 = (1ull << 48) - 1;
   constexpr int kPpl = 4;  // packets per lane per round, loads in flight
   for (;;) {
     if (threadIdx.x == 0) {
-      uint64_t t = 0;
-      uint32_t lane = 0, go = 0;
+      const uint64_t t = atomicAdd(dl, 1ull);
+      uint32_t go = 0;
       for (;;) {
-        if (ring_claim(a, home, &lane, &t)) {
+        if (ld_agent(dl + 1) > t) {
           go = 1;
           break;
         }
-        // stopping (the dispatcher's mirrors precede its stop word): one
-        // more look at every lane, then out
+        // stopping (the dispatcher's mirrors precede its stop word):
+        // published meanwhile?
         if (__hip_atomic_load(dstop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
-          go = ring_claim(a, home, &lane, &t) ? 1u : 0u;
+          go = ld_agent(dl + 1) > t ? 1u : 0u;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -525,13 +506,12 @@ void em_ring_kernel(RingArgs a) {
       uint64_t w[4] = {0, 0, 0, 0};
       if (go) {
         const uint64_t tag = (t + 1) & 0xFFFF;
-        const uint64_t *d = a.desc + ((size_t)lane * a.nslots + t % a.nslots) * 4;
+        const uint64_t *d = ldesc + (t % a.nslots) * 4;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
       for (int i = 0; i < 4; i++) sh_w[i] = w[i];
       sh_t = t;
-      sh_lane = lane;
       sh_go = go;
     }
     __syncthreads();
@@ -567,8 +547,8 @@ void em_ring_kernel(RingArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
-      __hip_atomic_store(a.done + (size_t)sh_lane * a.nslots + t % a.nslots,
-                         (uint32_t)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();  // sh_* are rewritten for the next ticket
   }
 }

@@ -184,8 +184,9 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
   r->device = device;
   r->nslots = (uint32_t)slots;
   r->nlanes = (uint32_t)lanes;
-  // workers (at least one per lane) + the dispatcher
-  int wk = blocks > 0 ? blocks : 2 * num_cus(device);
+  // workers (at least one per lane; one-wave workgroups, 4 per CU beside a
+  // 38 KB LDS table) + the dispatcher
+  int wk = blocks > 0 ? blocks : 4 * num_cus(device);
   wk = std::max(wk, lanes);
   r->blocks = wk + 1;
   const size_t nl = (size_t)lanes, ns = (size_t)slots;

@@ -26,6 +26,7 @@
 // device only ever sees copies of their bytes, core/module.h:224-226).
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <deque>
@@ -55,6 +56,8 @@ struct Slot {
   std::vector<void *> cookies;
   size_t n = 0;
   bool inflight = false;
+  bool draining = false;  // completed; poll hands out [cursor, n)
+  size_t cursor = 0;
   bg_ctx ctx{};  // the context of the slot's packets (Module::CtxUse fields)
 };
 
@@ -72,10 +75,16 @@ struct bg_pipe {
   size_t fill = 0;       // slot being filled
   size_t oldest = 0;     // oldest in-flight slot
   size_t inflight = 0;   // slots in flight
-  std::deque<std::pair<void *, uint16_t>> ready;  // completed, not returned
+  // completed packets of a slot that had to be reused before poll took
+  // them (they leave first); normally poll reads the slots themselves
+  std::deque<std::pair<void *, uint16_t>> ready;
   size_t pending = 0;    // submitted, not yet returned by poll
   int err = 0;           // sticky launch error
   uint64_t launched = 0;  // slot launches so far (Slot::seq)
+  // bg_pipe_stats: submits, packets, ns in launches (HIP calls), ns a
+  // submit waited for a free slot, ns a poll waited
+  uint64_t st_submits = 0, st_pkts = 0, st_launch_ns = 0, st_full_ns = 0,
+           st_wait_ns = 0;
   // One worker owns a pipe; the lock is for the module's control path
   // (PipeFlushLocked) and a RunTask on another worker (never contended on
   // the datapath).
@@ -99,6 +108,33 @@ static void pipe_release(bg_pipe *p) {
   p->slots.clear();
 }
 
+// dst <- src, w bytes (a multiple of 16): fixed-size 16-byte moves, no
+// libc call per packet
+static inline uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+static inline void copy16(uint8_t *dst, const uint8_t *src, size_t w) {
+  switch (w) {
+    case 16:
+      __builtin_memcpy(dst, src, 16);
+      return;
+    case 32:
+      __builtin_memcpy(dst, src, 32);
+      return;
+    case 48:
+      __builtin_memcpy(dst, src, 48);
+      return;
+    case 64:
+      __builtin_memcpy(dst, src, 64);
+      return;
+    default:
+      memcpy(dst, src, w);
+  }
+}
+
 // Launch the fill slot (n > 0): H2D, module kernel, D2H, event. (No
 // module lock: like bessd's datapath, a pipe relies on THREAD_UNSAFE
 // commands running only while its worker is paused, core/module.cc:97-101;
@@ -106,6 +142,7 @@ static void pipe_release(bg_pipe *p) {
 static int launch_slot(bg_pipe *p) {
   Slot &s = p->slots[p->fill];
   const size_t n = s.n;
+  const uint64_t t0 = mono_ns();
   int rc = bg::set_device(p->device);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
@@ -123,22 +160,26 @@ static int launch_slot(bg_pipe *p) {
   // word and makes no HIP call
   s.seq = ++p->launched;
   HIP_TRY(hipStreamWriteValue64(s.st, s.d_done, s.seq, 0));
+  p->st_launch_ns += mono_ns() - t0;
   s.inflight = true;
   p->inflight++;
   p->fill = (p->fill + 1) % p->slots.size();
   return 0;
 }
 
-// Retire the oldest in-flight slot (blocking when `wait`). Returns 1 if a
-// slot was retired, 0 if not (nothing in flight / not done), or -errno.
+// Retire the oldest slot if it is in flight and done (blocking when
+// `wait`): header lines written back, the slot's packets ready for poll.
+// Returns 1 if it was retired, 0 if not (not in flight / not done), -errno.
 static int retire_oldest(bg_pipe *p, bool wait) {
-  if (p->inflight == 0) return 0;
   Slot &s = p->slots[p->oldest];
+  if (!s.inflight) return 0;
   if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq) {
     if (!wait) return 0;
+    const uint64_t t0 = mono_ns();
     int rc = bg::set_device(p->device);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s.st));
+    p->st_wait_ns += mono_ns() - t0;
     if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq)
       return fail(EIO, "pipe slot %llu: completion word not written",
                   (unsigned long long)s.seq);
@@ -148,12 +189,50 @@ static int retire_oldest(bg_pipe *p, bool wait) {
     for (size_t i = 0; i < s.n; i++)
       memcpy(s.heads[i], s.h_wb + i * line, s.wblen[i]);
   }
-  for (size_t i = 0; i < s.n; i++) p->ready.emplace_back(s.cookies[i], s.h_g[i]);
-  s.n = 0;
   s.inflight = false;
+  s.draining = true;
+  s.cursor = 0;
   p->inflight--;
-  p->oldest = (p->oldest + 1) % p->slots.size();
   return 1;
+}
+
+// The oldest slot, drained: the next one becomes the oldest.
+static void release_oldest(bg_pipe *p) {
+  Slot &s = p->slots[p->oldest];
+  s.draining = false;
+  s.n = 0;
+  p->oldest = (p->oldest + 1) % p->slots.size();
+}
+
+// Completed packets in submission order into cookies / gates (cap): the
+// spilled ones first, then the oldest slots in place.
+static long take_done(bg_pipe *p, bool wait, void **cookies, uint16_t *gates,
+                      size_t cap) {
+  size_t k = 0;
+  while (k < cap && !p->ready.empty()) {
+    const auto &e = p->ready.front();
+    if (cookies) cookies[k] = e.first;
+    if (gates) gates[k] = e.second;
+    p->ready.pop_front();
+    k++;
+  }
+  while (k < cap) {
+    Slot &s = p->slots[p->oldest];
+    if (s.draining) {
+      const size_t m = std::min(cap - k, s.n - s.cursor);
+      if (cookies) memcpy(cookies + k, s.cookies.data() + s.cursor, m * sizeof(void *));
+      if (gates) memcpy(gates + k, s.h_g + s.cursor, m * 2);
+      s.cursor += m;
+      k += m;
+      if (s.cursor == s.n) release_oldest(p);
+      continue;
+    }
+    const int r = retire_oldest(p, wait && k == 0);
+    if (r < 0) return r;
+    if (r == 0) break;
+  }
+  p->pending -= k;
+  return (long)k;
 }
 
 extern "C" {
@@ -246,13 +325,23 @@ int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
   if (p->err) return p->err;
   int r;
   const bg_ctx c = ResolveCtx(ctx, p->device);
+  p->st_submits++;
+  p->st_pkts += cnt;
   const size_t span = (size_t)(p->hi - p->lo);
   size_t i = 0;
   while (i < cnt) {
     Slot &s = p->slots[p->fill];
     if (s.inflight) {  // ring full: backpressure until the oldest retires
+      const uint64_t t0 = mono_ns(), w0 = p->st_wait_ns;
       r = retire_oldest(p, true);
       if (r < 0) return p->err = r;
+      p->st_full_ns += mono_ns() - t0;
+      p->st_wait_ns = w0;  // counted as a full ring, not as a poll wait
+      continue;
+    }
+    if (s.draining) {  // completed but not polled: its rest waits aside
+      for (size_t j = s.cursor; j < s.n; j++) p->ready.emplace_back(s.cookies[j], s.h_g[j]);
+      release_oldest(p);
       continue;
     }
     if (s.n == 0) {
@@ -270,7 +359,9 @@ int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
       if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
       const uint8_t *src = heads[k] + p->lo;
       if (!p->writeback) {
-        memcpy(dst, src, span);
+        // the window rounded up to 16 bytes (the bytes past it are not
+        // read by the kernel; the packet buffer holds them, SNBUF_DATA)
+        copy16(dst, src, p->w);
       } else {
         // the frame (data_len bytes when given, at least its header line),
         // zero-padded to the slot
@@ -298,7 +389,7 @@ int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
 static int flush(bg_pipe *p) {
   if (p->err) return p->err;
   Slot &s = p->slots[p->fill];
-  if (s.inflight || s.n == 0) return 0;
+  if (s.inflight || s.draining || s.n == 0) return 0;
   int r = launch_slot(p);
   if (r < 0) return p->err = r;
   return 0;
@@ -313,24 +404,19 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
                   size_t cap) {
   std::lock_guard<std::mutex> lk(p->mu);
   if (p->err) return p->err;
-  for (;;) {
-    int r = retire_oldest(p, wait && p->ready.empty());
-    if (r < 0) return p->err = r;
-    if (r == 0) break;
-  }
-  size_t k = 0;
-  while (k < cap && !p->ready.empty()) {
-    const auto &e = p->ready.front();
-    if (cookies) cookies[k] = e.first;
-    if (gates) gates[k] = e.second;
-    p->ready.pop_front();
-    k++;
-  }
-  p->pending -= k;
-  return (long)k;
+  const long k = take_done(p, wait != 0, cookies, gates, cap);
+  if (k < 0) return p->err = (int)k;
+  return k;
 }
 
 size_t bg_pipe_pending(const bg_pipe *p) { return p->pending; }
+
+int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n) {
+  const uint64_t v[7] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
+                         p->st_full_ns, p->st_wait_ns, (uint64_t)p->batch};
+  for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+  return 0;
+}
 
 }  // extern "C"
 

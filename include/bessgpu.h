@@ -525,6 +525,10 @@ int bg_pipe_flush(bg_pipe *p);
 long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
                   size_t cap);
 size_t bg_pipe_pending(const bg_pipe *p);
+/* counters (first n of): submits, packets, slot launches, ns spent in
+ * launches (HIP calls), ns submits waited for a free slot, ns polls
+ * waited, the slot size */
+int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n);
 /* A worker loop (Source -> module -> Sink): n packets submitted in bursts of
  * `burst`, completions polled after each submit; ogates[i] = packet i's
  * gate. Returns when all n are back. */
@@ -542,13 +546,13 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
  * `frames` + i*stride, device or mapped host memory; gates written to
  * `gates`) and returns the lane's ticket; wait blocks until that ticket's
  * gates are written; completed returns the number of the lane's tickets
- * finished in order. The grid's workgroups are spread over the lanes; the
+ * finished in order. Create it with as many lanes as workers submit on. The
  * kernel keeps the table in LDS for its whole run and classifies with the
  * rule set as of bg_em_ring_create (it holds its own copy of the table
  * image: re-create the ring after rule changes, which bessd makes with
  * workers paused). slots: a power of two <= 32768 (submit blocks while
- * `slots` of the lane's tickets are unfinished); blocks: workgroups (0: 2 per
- * CU); idle_us: the kernel exits after this long without work and is
+ * `slots` of the lane's tickets are unfinished); blocks: one-wave workgroups
+ * (0: 4 per CU), spread evenly over the lanes; idle_us: the kernel exits after this long without work and is
  * relaunched by the next submit or wait (so it never outlives its work); a
  * submit makes no HIP call while the kernel runs. */
 typedef struct bg_ring bg_ring;

@@ -75,6 +75,12 @@ class GpuModule : public Module {
     return {.block = done == 0, .packets = done, .bits = 0};
   }
 
+  // a worker's pipe counters (bg_pipe_stats); 0 if it has none
+  int PipeStats(int wid, uint64_t *out, int n) const {
+    bg_pipe *p = lanes_[wid].pipe.load(std::memory_order_acquire);
+    return p ? bg_pipe_stats(p, out, n) : -1;
+  }
+
   // packets this module holds (submitted, not yet handed on)
   size_t Pending() const {
     size_t n = 0;
@@ -202,7 +208,8 @@ class GpuModule : public Module {
   bg_module *m_ = nullptr;
 
  private:
-  struct Lane {
+  // one cache line per worker: its ProcessBatch calls count submits here
+  struct alignas(64) Lane {
     std::atomic<bg_pipe *> pipe{nullptr};
     std::atomic<uint64_t> submits{0};  // ProcessBatch calls so far
     uint64_t seen = 0;                 // submits at the task's last visit

@@ -84,11 +84,15 @@ class Packet {
   uint16_t data_len() const { return data_len_; }
   void set_data_len(uint16_t v) { data_len_ = v; }
   static void Free(Packet *) { freed_packets()++; }
+  // the shell's pool position of the packet (its Sink's bookkeeping)
+  uint32_t pool_index() const { return pool_index_; }
+  void set_pool_index(uint32_t i) { pool_index_ = i; }
 
  private:
   uint16_t data_off_ = SNBUF_HEADROOM;
   uint16_t data_len_ = 0;
   uint32_t total_len_ = 0;
+  uint32_t pool_index_ = 0;
 };
 
 class PacketBatch {

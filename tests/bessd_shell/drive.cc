@@ -136,7 +136,7 @@ struct Sink {  // where a worker's emitted and dropped packets go
     ctx.dropped.clear();
   }
   void put(bess::Packet *p, uint32_t g) {
-    const size_t i = (size_t)(reinterpret_cast<uint8_t *>(p) - pool) / kObj;
+    const size_t i = p->pool_index();
     if (fast) (*fast)[i] = (uint16_t)g;
     if (gate) (*gate)[i] = g == 0xFFFF ? "D" : std::to_string(g);
     if (seq && g != 0xFFFF) (*seq)[i] = (*counter)++;
@@ -211,6 +211,7 @@ static int run() {
         f.read(fr.data(), (std::streamsize)stride);
         uint8_t *b = pool + i * kObj;
         bess::Packet *p = new (b) bess::Packet();
+        p->set_pool_index((uint32_t)i);
         memcpy(p->head_data<uint8_t *>(), fr.data(), stride);
         p->set_total_len((uint32_t)stride);
         p->set_data_len((uint16_t)stride);
@@ -328,6 +329,15 @@ static int run() {
                                                  : std::to_string(fast[i]).c_str());
       }
       printf("\n");
+      if (GpuModule *g = dynamic_cast<GpuModule *>(m)) {
+        uint64_t st[7];
+        if (g->PipeStats(0, st, 7) == 0)
+          printf("stats submits %llu pkts %llu launches %llu launch_ms %.3f full_ms %.3f "
+                 "wait_ms %.3f batch %llu\n",
+                 (unsigned long long)st[0], (unsigned long long)st[1],
+                 (unsigned long long)st[2], st[3] * 1e-6, st[4] * 1e-6, st[5] * 1e-6,
+                 (unsigned long long)st[6]);
+      }
       if (verify) {
         bool ok = true;
         for (int w = 0; w < nw && ok; w++) {
