@@ -356,7 +356,7 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
         torch.cuda.synchronize()
         ms = timed(g.replay)
         out["graph"][str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
-    npk = 1 << 20
+    npk = min(16 << 20, r["n"])  # the C2 slab: enough tickets at any batch size
     launches0 = 0
     for T in (1, 4, 16):  # a ring with one submission lane per submitter
         ring = F.Ring(t, slots=4096, lanes=T)
@@ -674,36 +674,51 @@ def run_plugin_pipeline(args):
     want = om.process(frames, 64, n)
     script += ["connect %d" % g for g in range(65)]
     threads = [int(x) for x in args.pipe_threads.split(",")]
-    res, parity, pipe_stats = {}, {}, {}
+    res, parity, pipe_stats, cpu_res, cpu_parity = {}, {}, {}, {}, {}
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "frames.bin")
         frames.tofile(path)
+        kpath, gpath = os.path.join(td, "keys.bin"), os.path.join(td, "gates.bin")
+        np.ascontiguousarray(keys, dtype=np.uint8).tofile(kpath)
+        np.ascontiguousarray(gates, dtype=np.uint16).tofile(gpath)
         script.append("frames %s 64 %d" % (path, n))
+        script.append("cpu_em %s %s %d" % (kpath, gpath, len(keys)))
         for t in threads:
             reps = 64 if t == 1 else 256
             sc = script + ["pipeline %d 2 0 0 0" % t,  # warm: lanes, tables
-                           "pipeline %d %d 0 0 0" % (t, reps)]
+                           "pipeline %d %d 0 0 0" % (t, reps),
+                           # the CPU baseline in the same harness: the
+                           # restated reference ProcessBatch on the workers
+                           "pipeline_cpu %d 2" % t, "pipeline_cpu %d %d" % (t, reps)]
             r = subprocess.run([drive, "run"], input="\n".join(sc) + "\n",
                                capture_output=True, text=True, timeout=600)
             lines = r.stdout.splitlines()
             stats = [x for x in lines if x.startswith("pipeline")]
             outs = [x for x in lines if x.startswith("out")]
-            if r.returncode or len(stats) < 2 or len(outs) < 2:
+            if r.returncode or len(stats) < 4 or len(outs) < 4:
                 res[str(t)] = "failed: rc %d %s" % (r.returncode, r.stderr[-300:])
                 continue
-            res[str(t)] = round(float(stats[-1].split()[1]), 1)
+            res[str(t)] = round(float(stats[1].split()[1]), 1)
+            cpu_res[str(t)] = round(float(stats[3].split()[1]), 1)
             pst = [x for x in lines if x.startswith("stats")]
             if pst:
                 pipe_stats[str(t)] = pst[-1][6:]
             # EmitPacket to DROP_GATE (the default gate) drops: "D"
             exp = ["D" if int(w) >= 8192 else str(int(w)) for w in want]
-            parity[str(t)] = outs[-1].split()[1:] == exp
+            parity[str(t)] = outs[1].split()[1:] == exp
+            cpu_parity[str(t)] = outs[3].split()[1:] == exp
     return {"what": "Source -> ExactMatch plugin (deferred: per-worker bg_pipe, "
                     "task emits) -> Sink, 32-pkt batches, 1000 rules, %d 64B "
                     "pkts in 2624 B snbufs split over the workers as the "
                     "cpu_baseline splits them" % n,
-            "Mpps_by_workers": res, "pipe": {"batch": 16384, "depth": 4},
-            "worker0_pipe_stats": pipe_stats, "parity": parity}
+            "Mpps_by_workers": res, "pipe": {"batch": 65536, "depth": 4},
+            "worker0_pipe_stats": pipe_stats, "parity": parity,
+            "cpu_same_harness": {
+                "what": "the same Source -> Sink workers with the restated "
+                        "reference ExactMatch::ProcessBatch (oracle: head_data() "
+                        "per packet, MakeKeys, CuckooMap/CRC32C Find, EmitPacket) "
+                        "in place of the plugin",
+                "Mpps_by_workers": cpu_res, "parity": cpu_parity}}
 
 
 def _time_steps(step, args, torch):

@@ -100,10 +100,10 @@ struct SlotHit {
   uint32_t slot, entry;
   uint64_t ep;
 };
-__device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
-  const uint32_t *tags = reinterpret_cast<const uint32_t *>(a.t.base);
-  const u32x4 *kv = reinterpret_cast<const u32x4 *>(a.t.base + a.t.keys_off);
-  const Probe p = split_hash(hash_words(&key, 1, a.t.seed), 1, a.t.nbp);
+__device__ __forceinline__ SlotHit lookup_in(const TableRef &t, uint64_t key) {
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(t.base);
+  const u32x4 *kv = reinterpret_cast<const u32x4 *>(t.base + t.keys_off);
+  const Probe p = split_hash(hash_words(&key, 1, t.seed), 1, t.nbp);
   uint32_t c = tag_match(tags[p.b1], p.tag) | (tag_match(tags[p.b2], p.tag) << 4);
   SlotHit h;
   h.slot = ~0u;
@@ -122,6 +122,9 @@ __device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
     }
   }
   return h;
+}
+__device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
+  return lookup_in(a.t, key);
 }
 // endpoint -> entry index, or kDnatMiss
 __device__ __forceinline__ uint32_t lookup(const DnatArgs &a, uint64_t key) {
@@ -213,13 +216,22 @@ __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
     } else
 #endif
     if (key != ~0ull) h = lookup_hit(a, key);
+    // a reverse miss: the forward entries are in the same map (nat.cc Find)
+    if (h.slot == ~0u && key != ~0ull && a.dir == 1 && a.t2.base) h = lookup_in(a.t2, key);
     if (h.slot != ~0u && a.dir == 0) ts = a.ts[h.entry];
 #ifdef BG_AB
     if (a.ab_phase >= 1) ts = a.now;  // timing: the timestamp round trip
 #endif
   }
   // only a forward entry's timestamp decides expiry (nat.cc:222-226)
-  const bool expired = h.slot != ~0u && a.dir == 0 && a.now - ts > a.timeout;
+  bool expired = h.slot != ~0u && a.dir == 0 && a.now - ts > a.timeout;
+  // a forward packet from an external address: an earlier packet of the
+  // batch may create an entry under its endpoint -- the host decides
+  if (a.dir == 0 && h.slot != ~0u) {
+    bool ext = a.list_fwd != 0;
+    for (uint32_t j = 0; j < a.next; j++) ext |= (uint32_t)key == a.ext[j];
+    expired |= ext;
+  }
   const bool fmiss =
       live && key != ~0ull && a.dir == 0 && (h.slot == ~0u || expired);
   const uint64_t m = __ballot(fmiss);

@@ -278,14 +278,17 @@ struct bg_dnat {
   // now - last_refresh > kTimeOutNs (nat.cc:217, u64 arithmetic) with the
   // entry's current timestamp: a host value that says "expired" may be
   // stale, so it is re-read from the device first
+  // (a timestamp that cannot be read counts as live: a mapping is never
+  // evicted on a guess)
   bool expired(uint32_t e, uint64_t now) {
     if (now - ent_ts[e] <= kTimeOutNs) return false;
     if (exact_walk[e] != walk && d_ts && e < d_cap) {
       uint64_t t = 0;
-      if (hipMemcpyAsync(&t, d_ts + e, 8, hipMemcpyDeviceToHost, walk_stream) ==
-              hipSuccess &&
-          hipStreamSynchronize(walk_stream) == hipSuccess)
-        ent_ts[e] = std::max(ent_ts[e], t);
+      if (hipMemcpyAsync(&t, d_ts + e, 8, hipMemcpyDeviceToHost, walk_stream) !=
+              hipSuccess ||
+          hipStreamSynchronize(walk_stream) != hipSuccess)
+        return false;
+      ent_ts[e] = std::max(ent_ts[e], t);
       exact_walk[e] = walk;
     }
     return now - ent_ts[e] > kTimeOutNs;
@@ -531,6 +534,10 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.now = now;
   a.timeout = kTimeOutNs;
   a.t = h->tab[dir].ref();
+  if (dir == 1) a.t2 = h->tab[0].ref();  // reverse misses: the forward entries
+  a.next = (uint32_t)std::min<size_t>(h->ext.size(), kDnatMaxExt);
+  a.list_fwd = h->ext.size() > (size_t)kDnatMaxExt ? 1u : 0u;
+  for (uint32_t j = 0; j < a.next; j++) a.ext[j] = h->ext[j];
   a.keys = h->d_keys;
   a.res = h->d_res;
   a.nmiss = h->d_nmiss;

@@ -288,7 +288,19 @@ struct DnatArgs {
   uint32_t ab_phase;  // A/B build only (timing): 1 = no timestamp read/refresh
   uint64_t nlist;
   const uint32_t *mres;
+  // The reference's map holds both directions' entries (nat.h: one
+  // HashTable): a reverse packet whose destination is an internal endpoint
+  // finds that forward entry (t2 = the forward image, probed on a reverse
+  // miss), and a forward packet whose source address is one of the NAT's
+  // external addresses may meet an entry an earlier packet of the batch
+  // creates (CreateNewEntry inserts ext_addr:port keys): such forward
+  // packets are listed for the host's in-order walk (next addresses, raw
+  // be32; list_fwd: more than kDnatMaxExt, list every forward packet).
+  TableRef t2;
+  uint32_t next, list_fwd;
+  uint32_t ext[16];
 };
+constexpr int kDnatMaxExt = 16;
 
 // Persistent ExactMatch kernel fed by a ring of batch descriptors
 // (bg_ring.cc). Descriptor of ticket t at desc + (t % nslots) * 4: four

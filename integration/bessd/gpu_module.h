@@ -39,7 +39,7 @@ class GpuModule : public Module {
  public:
   // the deferred datapath's pipes: packets per device launch, launches in
   // flight per worker
-  static const size_t kPipeBatch = 16384;
+  static const size_t kPipeBatch = 65536;
   static const int kPipeDepth = 4;
 
   void DeInit() override {
@@ -174,6 +174,8 @@ class GpuModule : public Module {
     }
     uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
     uint16_t lens[bess::PacketBatch::kMaxBurst] = {};
+    // the packets' mbuf lines in flight together (head_data() reads them)
+    for (int i = 0; i < n; i++) __builtin_prefetch(batch->pkts()[i]);
     for (int i = 0; i < n; i++) {
       bess::Packet *pkt = batch->pkts()[i];
       heads[i] = pkt->head_data<uint8_t *>();

@@ -29,6 +29,15 @@
 //                                 verify "order ok|bad": each worker's
 //                                 emitted packets left in the order they
 //                                 came in (hence per gate, module.h:268-272)
+//     cpu_em <keys> <gates> <n>   the CPU baseline's table: the oracle's
+//                                 restatement of ExactMatch (5-tuple fields)
+//                                 with n rules (13-byte keys, u16 gates)
+//     pipeline_cpu <workers> <reps>  the same Source -> Sink loop with the
+//                                 restated reference ProcessBatch on the CPU
+//                                 in the middle (head_data() per packet,
+//                                 MakeKeys + CuckooMap Find, EmitPacket with
+//                                 the created module's connected gates) --
+//                                 the cpu_baseline in the same harness
 #include <pthread.h>
 #include <sched.h>
 #include <stdio.h>
@@ -47,6 +56,7 @@
 
 #include "core/module.h"
 #include "core/modules/gpu_module.h"
+#include "oracle.h"  // test infrastructure: the CPU baseline (pipeline_cpu)
 
 // mempool object stride: the snbuf plus the mempool's object header, so
 // head_data() sits at +512 of a 2624-byte object (core/snbuf_layout.h)
@@ -160,6 +170,7 @@ static int run() {
   Module *m = nullptr;
   const ModuleClass *cls = nullptr;
   uint8_t *pool = nullptr;
+  or_em *cpu_em = nullptr;
   std::vector<uint8_t *> bufs;
   std::string line;
   while (std::getline(std::cin, line)) {
@@ -252,10 +263,30 @@ static int run() {
         printf("data %u %s\n", p->total_len(),
                hex(std::string(p->head_data<const char *>(), 64)).c_str());
       }
-    } else if (op == "pipeline") {
-      int nw, reps, ig, verify;
-      unsigned long long now;
-      in >> nw >> reps >> ig >> now >> verify;
+    } else if (op == "cpu_em") {
+      std::string kp, gp;
+      size_t nr;
+      in >> kp >> gp >> nr;
+      std::vector<uint8_t> keys(nr * 13);
+      std::vector<uint16_t> gates(nr);
+      std::ifstream fk(kp, std::ios::binary), fg(gp, std::ios::binary);
+      fk.read(reinterpret_cast<char *>(keys.data()), (std::streamsize)keys.size());
+      fg.read(reinterpret_cast<char *>(gates.data()), (std::streamsize)(nr * 2));
+      if (cpu_em) or_em_free(cpu_em);
+      cpu_em = or_em_new();
+      const int fo[5] = {23, 26, 30, 34, 36}, fs[5] = {1, 4, 4, 2, 2};
+      for (int i = 0; i < 5; i++) or_em_add_field(cpu_em, fo[i], fs[i], 0, i, nullptr, 0);
+      printf("cpu_em %d\n", or_em_add_rules(cpu_em, keys.data(), nr, 13, gates.data()));
+    } else if (op == "pipeline" || op == "pipeline_cpu") {
+      const bool cpu = op == "pipeline_cpu";
+      int nw, reps, ig = 0, verify = 0;
+      unsigned long long now = 0;
+      in >> nw >> reps;
+      if (!cpu) in >> ig >> now >> verify;
+      if (cpu && !cpu_em) {
+        printf("rc 22 cpu_em first\n");
+        continue;
+      }
       const size_t n = bufs.size();
       std::vector<std::string> out(n, "-");
       std::vector<uint16_t> fast(n, 0xFFFE);
@@ -291,9 +322,18 @@ static int run() {
             bess::PacketBatch batch;  // the Source's batch
             for (size_t i = b0; i < hi && i < b0 + bess::PacketBatch::kMaxBurst; i++)
               batch.add(reinterpret_cast<bess::Packet *>(pool + i * kObj));
-            m->ProcessBatch(&ctx, &batch);
+            if (cpu) {  // ExactMatch::ProcessBatch restated (exact_match.cc:224-244)
+              const uint8_t *heads[bess::PacketBatch::kMaxBurst];
+              uint16_t g[bess::PacketBatch::kMaxBurst];
+              for (int i = 0; i < batch.cnt(); i++)
+                heads[i] = batch.pkts()[i]->head_data<const uint8_t *>();
+              or_em_process_batch(cpu_em, heads, batch.cnt(), DROP_GATE, g);
+              for (int i = 0; i < batch.cnt(); i++) m->EmitPacket(&ctx, batch.pkts()[i], g[i]);
+            } else {
+              m->ProcessBatch(&ctx, &batch);
+            }
             sink.take(ctx);
-            if (w == 0 && (++nb & 7) == 0 && m->is_task()) {
+            if (!cpu && w == 0 && (++nb & 63) == 0 && m->is_task()) {
               m->RunTask(&ctx, nullptr, nullptr);
               sink.take(ctx);
             }
@@ -301,10 +341,10 @@ static int run() {
         finished++;
         if (w == 0) {  // the task's worker: until every worker is done
           while (finished.load() < nw) {
-            if (m->is_task()) m->RunTask(&ctx, nullptr, nullptr);
+            if (!cpu && m->is_task()) m->RunTask(&ctx, nullptr, nullptr);
             sink.take(ctx);
           }
-          run_task(m, &ctx);
+          if (!cpu) run_task(m, &ctx);
           sink.take(ctx);
           t1 = now_s();
         }
@@ -360,6 +400,7 @@ static int run() {
     delete m;
   }
   free(pool);
+  if (cpu_em) or_em_free(cpu_em);
   return 0;
 }
 

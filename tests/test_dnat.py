@@ -303,3 +303,55 @@ def test_gpu_expired_hits_in_order(order):
                  "interleaved": [C, D, B, A, D, C]}[order]
         run(np.concatenate(batch), now)
         run(np.concatenate([A, B, C, D]), now + 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [STRIDE, 64])
+def test_gpu_overlapping_internal_and_external_endpoints(stride):
+    """The reference keeps both directions' entries in ONE map (nat.h), so
+    when internal and external endpoints overlap: a reverse packet whose
+    destination is an internal endpoint finds that forward entry and is
+    translated with it; a forward packet whose source is an external
+    endpoint finds its reverse entry; and a forward packet whose source
+    endpoint an earlier packet of the same batch installs as an external
+    endpoint meets the new entry. Sources here come from the NAT's own
+    external addresses (10.9.0.1, 10.9.0.2, 8.8.8.8) as well as internal
+    ones, batch after batch, every byte and gate as the oracle's."""
+    import torch
+    from bess_amd.modules import NAT
+    rng = np.random.default_rng(23)
+    ext = [{"ext_addr": "10.9.0.1", "port_ranges": [{"begin": 2000, "end": 2040}]},
+           {"ext_addr": "10.9.0.2", "port_ranges": [{"begin": 2000, "end": 2040}]}]
+    m, o = NAT(ext_addrs=ext, seed=0x77), OM.OracleNAT(ext_addrs=ext, seed=0x77)
+
+    def run(f, igate, now):
+        ref = f.copy()
+        want = o.process(ref, stride, len(f), igate, now)
+        d = torch.from_numpy(f.reshape(-1).copy()).cuda()
+        og = torch.zeros(len(f), dtype=torch.int16, device="cuda")
+        m.process_device(d, stride, len(f), og, now, igate=igate)
+        got = d.cpu().numpy().reshape(len(f), stride)
+        assert (og.cpu().numpy().view(np.uint16) == want).all()
+        bad = np.nonzero((got != ref).any(1))[0]
+        assert len(bad) == 0, bad[:5]
+        return ref, want
+
+    exts = np.array([0x0A090001, 0x0A090002], np.uint64)
+    for b in range(4):
+        n = 400
+        internal = (0xC0A80000 | rng.integers(0, 64, n)).astype(np.uint64)
+        use_ext = rng.random(n) < 0.4  # sources on the external side
+        src = np.where(use_ext, exts[rng.integers(0, 2, n)], internal)
+        sport = np.where(use_ext, rng.integers(2000, 2040, n), rng.integers(2000, 2040, n))
+        proto = np.where(rng.random(n) < 0.5, 6, 17)
+        dst = np.where(rng.random(n) < 0.5, exts[rng.integers(0, 2, n)],
+                       (0xC0A80000 | rng.integers(0, 64, n)).astype(np.uint64))
+        dport = rng.integers(2000, 2040, n)
+        f = frames(src, sport, dst, dport, proto, np.zeros(n, int), rng,
+                   ihl=np.full(n, 5), stride=stride)
+        run(f, 0, T0 + b * 1000)
+        # the same endpoints arriving on the external side: destinations
+        # that are internal endpoints hit forward entries
+        r = frames(dst, dport, src, sport, proto, np.zeros(n, int), rng,
+                   ihl=np.full(n, 5), stride=stride)
+        run(r, 1, T0 + b * 1000 + 500)
