@@ -15,12 +15,25 @@
 //   w64s192 : 64 B at +128 of every 192 B slot, 4 lanes per slot (the
 //             Rewrite bench's shape: a 60 B template in 32 B blocks)
 //   w64s128 : 64 B at +64 of every 128 B slot (one half line per slot)
+// Scattered read shapes (`./hbm_probe GiB s`; TB/s of the 66 B/packet
+// algorithmic basis, and Gpkts/s):
+//   s2k32   : bytes 16..47 of every 2048 B slot (two 16 B loads per lane,
+//             lane = slot) + a 2-byte store -- C4's header window in 2 KB
+//             IMIX slots
+//   s2k64   : bytes 0..63 of every 2048 B slot (four 16 B loads)
+//   rnd36   : the em32 stream over 64 B slots + per packet one random 4 B
+//             read from a 4 MiB tag region and, for half the packets, one
+//             random 16 B read from a 32 MiB key region -- C5's 1 M-rule
+//             ExactMatch probe shape (36 MB table)
+// `./hbm_probe GiB only SHAPE BLOCKS_PER_CU LAUNCHES` runs one shape (for
+// rocprofv3 --pmc passes: FETCH_SIZE per launch against a known shape).
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
 // bytes read (median of 5 rounds of 20 back-to-back launches).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <vector>
@@ -79,6 +92,50 @@ __global__ __launch_bounds__(512) void half32(const u32x4 *src, size_t nslots,
   }
 }
 
+// bytes [off, off + 16 * nch) of every 2048 B slot, lane = slot
+template <int NCH, int OFF>
+__global__ __launch_bounds__(512) void s2k(const u32x4 *src, size_t nslots,
+                                           uint16_t *gates) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
+       i += step) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const u32x4 a = ldnt(src + 128 * i + OFF / 16 + c);
+      x ^= a.x ^ a.w;
+    }
+    gates[i] = (uint16_t)x;
+  }
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
+// em32 + a random tag word (4 MiB) + for half the packets a random 16 B key
+// (32 MiB): the C5 probe shape. tab: 36 MiB.
+__global__ __launch_bounds__(512) void rnd36(const u32x4 *src, size_t nslots,
+                                             const uint32_t *tab, uint16_t *gates) {
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  const u32x4 *keys = reinterpret_cast<const u32x4 *>(tab + (1u << 20));
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nslots;
+       i += step) {
+    const u32x4 a = ldnt(src + 4 * i + 1), b = ldnt(src + 4 * i + 2);
+    const uint32_t h = mix32((uint32_t)i ^ a.x ^ b.z);
+    uint32_t x = tab[h & ((1u << 20) - 1)];
+    if (h >> 31) {
+      const u32x4 k = keys[(h >> 8) & ((1u << 21) - 1)];
+      x ^= k.x ^ k.w;
+    }
+    gates[i] = (uint16_t)x;
+  }
+}
+
 __global__ __launch_bounds__(512) void wfull16(u32x4 *dst, size_t n16) {
   const size_t step = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += step)
@@ -121,14 +178,31 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const bool wr = argc > 2 && argv[2][0] == 'w';
-  const char *names[7] = {"full16", "em32", "slot64", "half32",
-                          "wfull16", "w64s192", "w64s128"};
-  for (int shape = wr ? 4 : 0; shape < (wr ? 7 : 4); shape++) {
+  const bool sc = argc > 2 && argv[2][0] == 's';
+  const bool only = argc > 5 && !strcmp(argv[2], "only");
+  const char *names[10] = {"full16", "em32", "slot64", "half32",
+                           "wfull16", "w64s192", "w64s128", "s2k32", "s2k64", "rnd36"};
+  uint32_t *tab = nullptr;
+  CK(hipMalloc(&tab, 36u << 20));
+  CK(hipMemset(tab, 0x33, 36u << 20));
+  int s0 = wr ? 4 : sc ? 7 : 0, s1 = wr ? 7 : sc ? 10 : 4;
+  int only_bpc = 0, only_launches = 0;
+  if (only) {
+    for (int k = 0; k < 10; k++)
+      if (!strcmp(argv[3], names[k])) s0 = k, s1 = k + 1;
+    only_bpc = atoi(argv[4]);
+    only_launches = atoi(argv[5]);
+  }
+  for (int shape = s0; shape < s1; shape++) {
     for (int bpc : {1, 2, 4, 8}) {
+      if (only && bpc != only_bpc) continue;
       const int blocks = cus * bpc;
       double moved = (double)bytes;  // bytes read or written per launch
+      double pkts = (double)nslots;
       if (shape == 5) moved = (double)(bytes / 192) * 64;
       if (shape == 6) moved = (double)(bytes / 128) * 64;
+      if (shape == 7 || shape == 8) pkts = (double)(bytes / 2048);
+      if (shape >= 7) moved = pkts * 66;  // the algorithmic basis
       auto launch = [&]() {
         if (shape == 0)
           hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
@@ -147,10 +221,26 @@ int main(int argc, char **argv) {
         else if (shape == 5)
           hipLaunchKernelGGL(w64, dim3(blocks), dim3(512), 0, 0, src, bytes / 192,
                              192u, 128u);
-        else
+        else if (shape == 6)
           hipLaunchKernelGGL(w64, dim3(blocks), dim3(512), 0, 0, src, bytes / 128,
                              128u, 64u);
+        else if (shape == 7)
+          hipLaunchKernelGGL((s2k<2, 16>), dim3(blocks), dim3(512), 0, 0, src,
+                             bytes / 2048, gates);
+        else if (shape == 8)
+          hipLaunchKernelGGL((s2k<4, 0>), dim3(blocks), dim3(512), 0, 0, src,
+                             bytes / 2048, gates);
+        else
+          hipLaunchKernelGGL(rnd36, dim3(blocks), dim3(512), 0, 0, src, nslots, tab,
+                             gates);
       };
+      if (only) {  // a fixed number of launches, no timing (rocprofv3 passes)
+        for (int w = 0; w < only_launches; w++) launch();
+        CK(hipDeviceSynchronize());
+        printf("{\"shape\": \"%s\", \"launches\": %d, \"pkts\": %.0f}\n", names[shape],
+               only_launches, pkts);
+        continue;
+      }
       for (int w = 0; w < 20; w++) launch();
       CK(hipDeviceSynchronize());
       std::vector<float> ms;
@@ -166,8 +256,8 @@ int main(int argc, char **argv) {
       std::sort(ms.begin(), ms.end());
       const double t = ms[2] * 1e-3;
       printf("{\"shape\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, "
-             "\"TBps\": %.3f}\n",
-             names[shape], bpc, ms[2], moved / t / 1e12);
+             "\"TBps\": %.3f, \"Gpkts\": %.2f}\n",
+             names[shape], bpc, ms[2], moved / t / 1e12, pkts / t / 1e9);
       fflush(stdout);
     }
   }
