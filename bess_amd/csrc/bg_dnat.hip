@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_apply_kernel(DnatArgs a) {
       continue;
     }
     if (a.refresh) a.ts[e] = a.now;  // forward packets only (rfc4787 REQ-6)
-    stamp(frame_of(a, i), a.keys[k], a.ent[e], a.dir);
+    stamp(frame_of(a, i), a.keys[k], a.list ? a.meps[k] : a.ent[e], a.dir);
     a.out[i] = a.dir == 0 ? 1 : 0;
   }
 }

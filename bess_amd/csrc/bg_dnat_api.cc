@@ -224,13 +224,14 @@ struct bg_dnat {
   size_t d_cap = 0;  // entries the device arrays hold
   uint64_t *d_keys = nullptr;
   uint32_t *d_res = nullptr, *d_nmiss = nullptr, *d_mres = nullptr;
+  uint64_t *d_meps = nullptr;
   size_t d_n = 0;
   uint64_t *d_up = nullptr;  // update lists (ensure_up)
   size_t d_upcap = 0;
   std::mutex mu;
   ~bg_dnat() {
     for (void *p : {(void *)d_ent, (void *)d_ts, (void *)d_keys, (void *)d_res,
-                    (void *)d_nmiss, (void *)d_mres, (void *)d_up})
+                    (void *)d_nmiss, (void *)d_mres, (void *)d_up, (void *)d_meps})
       if (p) (void)hipFree(p);
   }
 
@@ -370,12 +371,13 @@ struct bg_dnat {
 
   int ensure_batch(size_t n) {
     if (n <= d_n) return 0;
-    for (void *p : {(void *)d_keys, (void *)d_res, (void *)d_mres})
+    for (void *p : {(void *)d_keys, (void *)d_res, (void *)d_mres, (void *)d_meps})
       if (p) (void)hipFree(p);
     d_n = std::max<size_t>(n, 4096);
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_keys), d_n * 8));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_res), d_n * 4));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_mres), d_n * 4));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_meps), d_n * 8));
     if (!d_nmiss) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_nmiss), 4));
     return 0;
   }
@@ -558,6 +560,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   if (nlist == 0) return 0;
   // the listed packets in packet order on the host (DoProcessBatch 321-363)
   std::vector<uint32_t> idx(nlist), ent(nlist);
+  std::vector<uint64_t> eps(nlist);
   std::vector<uint64_t> key(nlist);
   HIP_TRY(hipMemcpyAsync(idx.data(), h->d_res, nlist * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(key.data(), h->d_keys, nlist * 8, hipMemcpyDeviceToHost, s));
@@ -580,12 +583,14 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
       h->changed.push_back((uint32_t)e);
     }
     ent[k] = e < 0 ? kDnatMiss : (uint32_t)e;
+    eps[k] = e < 0 ? 0 : h->ent_ep[e];  // Stamp's `after` at this packet's turn
   }
   r = h->sync(dev, s);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(h->d_res, sidx.data(), nlist * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->d_keys, skey.data(), nlist * 8, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->d_mres, ent.data(), nlist * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(h->d_meps, eps.data(), nlist * 8, hipMemcpyHostToDevice, s));
   a.t = h->tab[dir].ref();
   a.ent = h->d_ent;
   a.ts = h->d_ts;
@@ -593,6 +598,7 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.list = 1;
   a.nlist = nlist;
   a.mres = h->d_mres;
+  a.meps = h->d_meps;
   HIP_TRY(launch_dnat_apply(a, ncu, s));
   HIP_TRY(hipStreamSynchronize(s));  // the host vectors outlive the copies
   return 0;

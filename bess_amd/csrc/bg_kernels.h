@@ -288,6 +288,10 @@ struct DnatArgs {
   uint32_t ab_phase;  // A/B build only (timing): 1 = no timestamp read/refresh
   uint64_t nlist;
   const uint32_t *mres;
+  // per listed packet: the translated endpoint as the walk found it when it
+  // reached the packet (a later packet of the batch may overwrite the
+  // entry: Stamp uses the value of its own moment, nat.cc:353-360)
+  const uint64_t *meps;
   // The reference's map holds both directions' entries (nat.h: one
   // HashTable): a reverse packet whose destination is an internal endpoint
   // finds that forward entry (t2 = the forward image, probed on a reverse
