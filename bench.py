@@ -682,7 +682,7 @@ def run_plugin_pipeline(args):
         np.ascontiguousarray(keys, dtype=np.uint8).tofile(kpath)
         np.ascontiguousarray(gates, dtype=np.uint16).tofile(gpath)
         script.append("frames %s 64 %d" % (path, n))
-        script.append("cpu_em %s %s %d" % (kpath, gpath, len(keys)))
+        script.append("cpu_em %s %s %d %d" % (kpath, gpath, len(keys), keys.shape[1]))
         for t in threads:
             reps = 64 if t == 1 else 256
             sc = script + ["pipeline %d 2 0 0 0" % t,  # warm: lanes, tables
@@ -701,8 +701,12 @@ def run_plugin_pipeline(args):
             res[str(t)] = round(float(stats[1].split()[1]), 1)
             cpu_res[str(t)] = round(float(stats[3].split()[1]), 1)
             pst = [x for x in lines if x.startswith("stats")]
+            cyc = [x for x in lines if x.startswith("cycles")]
             if pst:
                 pipe_stats[str(t)] = pst[-1][6:]
+            if len(cyc) >= 4:
+                pipe_stats[str(t) + "_cycles_gpu"] = cyc[1][7:]
+                pipe_stats[str(t) + "_cycles_cpu"] = cyc[3][7:]
             # EmitPacket to DROP_GATE (the default gate) drops: "D"
             exp = ["D" if int(w) >= 8192 else str(int(w)) for w in want]
             parity[str(t)] = outs[1].split()[1:] == exp
@@ -843,7 +847,8 @@ def run_acl(args, dev, torch):
 def run_iplookup(args, dev, torch):
     """IPLookup (core/modules/ip_lookup.cc) on the C2 slab: 16M 64 B packets,
     10K routes (/8../24, 5 % /25../32, nested), half the destinations inside
-    a route; DIR-24-8 tables (32 MB tbl24) in HBM/MALL"""
+    a route; the default DIR-16-8-8 tables (tbl16 staged in LDS, tbl2 groups
+    in L2; DIR-24-8 only past 32 K groups)"""
     import sys as _s
     _s.path.insert(0, os.path.join(ROOT, "tests"))
     from test_gpu_iplookup import build, dsts_inside, frames_to, routes
@@ -865,7 +870,8 @@ def run_iplookup(args, dev, torch):
                    o.process(frames, 64, k)).all())
     ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
     out = {"workload": "IPLookup: 64B pkts (64B slots), %d resident pkts, 10K "
-                       "routes, DIR-24-8" % n, "pkts": n, "routes": len(o.rules),
+                       "routes, DIR-16-8-8 (tbl16 in LDS)" % n, "pkts": n,
+           "routes": len(o.rules),
            "ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
            "roofline": _roof(EM_BYTES_PER_PKT, n, ms, "iplookup"),
            "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}

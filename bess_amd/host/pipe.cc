@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <time.h>
+#include <x86intrin.h>
 
 #include <algorithm>
 #include <deque>
@@ -85,6 +86,7 @@ struct bg_pipe {
   // submit waited for a free slot, ns a poll waited
   uint64_t st_submits = 0, st_pkts = 0, st_launch_ns = 0, st_full_ns = 0,
            st_wait_ns = 0;
+  uint64_t st_submit_tsc = 0, st_poll_tsc = 0;  // cycles inside submit / poll
   // One worker owns a pipe; the lock is for the module's control path
   // (PipeFlushLocked) and a RunTask on another worker (never contended on
   // the datapath).
@@ -319,9 +321,20 @@ static bool same_ctx(unsigned use, const bg_ctx &a, const bg_ctx &b) {
   return true;
 }
 
+static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                  const uint16_t *lens, void *const *cookies, size_t cnt);
+
 int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                    const uint16_t *lens, void *const *cookies, size_t cnt) {
   std::lock_guard<std::mutex> lk(p->mu);
+  const uint64_t t0 = __rdtsc();
+  const int r = submit(p, ctx, heads, lens, cookies, cnt);
+  p->st_submit_tsc += __rdtsc() - t0;
+  return r;
+}
+
+static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                  const uint16_t *lens, void *const *cookies, size_t cnt) {
   if (p->err) return p->err;
   int r;
   const bg_ctx c = ResolveCtx(ctx, p->device);
@@ -404,7 +417,9 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
                   size_t cap) {
   std::lock_guard<std::mutex> lk(p->mu);
   if (p->err) return p->err;
+  const uint64_t t0 = __rdtsc();
   const long k = take_done(p, wait != 0, cookies, gates, cap);
+  p->st_poll_tsc += __rdtsc() - t0;
   if (k < 0) return p->err = (int)k;
   return k;
 }
@@ -412,9 +427,10 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
 size_t bg_pipe_pending(const bg_pipe *p) { return p->pending; }
 
 int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n) {
-  const uint64_t v[7] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
-                         p->st_full_ns, p->st_wait_ns, (uint64_t)p->batch};
-  for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+  const uint64_t v[9] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
+                         p->st_full_ns, p->st_wait_ns, (uint64_t)p->batch,
+                         p->st_submit_tsc, p->st_poll_tsc};
+  for (int i = 0; i < n && i < 9; i++) out[i] = v[i];
   return 0;
 }
 

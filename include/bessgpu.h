@@ -527,7 +527,7 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
 size_t bg_pipe_pending(const bg_pipe *p);
 /* counters (first n of): submits, packets, slot launches, ns spent in
  * launches (HIP calls), ns submits waited for a free slot, ns polls
- * waited, the slot size */
+ * waited, the slot size, TSC cycles inside submit, inside poll */
 int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n);
 /* A worker loop (Source -> module -> Sink): n packets submitted in bursts of
  * `burst`, completions polled after each submit; ogates[i] = packet i's

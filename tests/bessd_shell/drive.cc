@@ -29,9 +29,10 @@
 //                                 verify "order ok|bad": each worker's
 //                                 emitted packets left in the order they
 //                                 came in (hence per gate, module.h:268-272)
-//     cpu_em <keys> <gates> <n>   the CPU baseline's table: the oracle's
-//                                 restatement of ExactMatch (5-tuple fields)
-//                                 with n rules (13-byte keys, u16 gates)
+//     cpu_em <keys> <gates> <n> <stride>  the CPU baseline's table: the
+//                                 oracle's restatement of ExactMatch (5-tuple
+//                                 fields), n rules (keys `stride` bytes
+//                                 apart in gather_key layout, u16 gates)
 //     pipeline_cpu <workers> <reps>  the same Source -> Sink loop with the
 //                                 restated reference ProcessBatch on the CPU
 //                                 in the middle (head_data() per packet,
@@ -39,6 +40,7 @@
 //                                 the created module's connected gates) --
 //                                 the cpu_baseline in the same harness
 #include <pthread.h>
+#include <x86intrin.h>
 #include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -265,9 +267,9 @@ static int run() {
       }
     } else if (op == "cpu_em") {
       std::string kp, gp;
-      size_t nr;
-      in >> kp >> gp >> nr;
-      std::vector<uint8_t> keys(nr * 13);
+      size_t nr, ks = 16;
+      in >> kp >> gp >> nr >> ks;
+      std::vector<uint8_t> keys(nr * ks);
       std::vector<uint16_t> gates(nr);
       std::ifstream fk(kp, std::ios::binary), fg(gp, std::ios::binary);
       fk.read(reinterpret_cast<char *>(keys.data()), (std::streamsize)keys.size());
@@ -276,7 +278,7 @@ static int run() {
       cpu_em = or_em_new();
       const int fo[5] = {23, 26, 30, 34, 36}, fs[5] = {1, 4, 4, 2, 2};
       for (int i = 0; i < 5; i++) or_em_add_field(cpu_em, fo[i], fs[i], 0, i, nullptr, 0);
-      printf("cpu_em %d\n", or_em_add_rules(cpu_em, keys.data(), nr, 13, gates.data()));
+      printf("cpu_em %d\n", or_em_add_rules(cpu_em, keys.data(), nr, ks, gates.data()));
     } else if (op == "pipeline" || op == "pipeline_cpu") {
       const bool cpu = op == "pipeline_cpu";
       int nw, reps, ig = 0, verify = 0;
@@ -295,7 +297,9 @@ static int run() {
       std::atomic<int> started{0}, finished{0};
       std::atomic<bool> go{false};
       std::vector<uint64_t> sunk(nw, 0);
+      uint64_t tsc[3] = {0, 0, 0};
       double t0 = 0, t1 = 0;
+      const uint64_t tsc0 = __rdtsc();
       auto worker = [&](int w) {
         pin(w);
         Sink sink;
@@ -317,11 +321,13 @@ static int run() {
         while (!go.load()) {
         }
         uint64_t nb = 0;
+        uint64_t c_proc = 0, c_sink = 0, c_task = 0;  // TSC cycles per phase
         for (int r = 0; r < reps; r++)
           for (size_t b0 = lo; b0 < hi; b0 += bess::PacketBatch::kMaxBurst) {
             bess::PacketBatch batch;  // the Source's batch
             for (size_t i = b0; i < hi && i < b0 + bess::PacketBatch::kMaxBurst; i++)
               batch.add(reinterpret_cast<bess::Packet *>(pool + i * kObj));
+            const uint64_t c0 = __rdtsc();
             if (cpu) {  // ExactMatch::ProcessBatch restated (exact_match.cc:224-244)
               const uint8_t *heads[bess::PacketBatch::kMaxBurst];
               uint16_t g[bess::PacketBatch::kMaxBurst];
@@ -332,10 +338,15 @@ static int run() {
             } else {
               m->ProcessBatch(&ctx, &batch);
             }
+            const uint64_t c1 = __rdtsc();
             sink.take(ctx);
+            const uint64_t c2 = __rdtsc();
+            c_proc += c1 - c0;
+            c_sink += c2 - c1;
             if (!cpu && w == 0 && (++nb & 63) == 0 && m->is_task()) {
               m->RunTask(&ctx, nullptr, nullptr);
               sink.take(ctx);
+              c_task += __rdtsc() - c2;
             }
           }
         finished++;
@@ -349,6 +360,11 @@ static int run() {
           t1 = now_s();
         }
         sunk[w] = sink.n;
+        if (w == 0) {
+          tsc[0] = c_proc;
+          tsc[1] = c_sink;
+          tsc[2] = c_task;
+        }
       };
       std::vector<std::thread> th;
       for (int w = 0; w < nw; w++) th.emplace_back(worker, w);
@@ -360,6 +376,11 @@ static int run() {
       const double dt = t1 - t0;
       const double pk = (double)n * reps;
       printf("pipeline %.3f %.6f %.0f\n", pk / dt / 1e6, dt, pk);
+      // worker 0's cycles per packet of its own: ProcessBatch, Sink, task
+      const double ghz = (double)(__rdtsc() - tsc0) / (now_s() - t0 + 1e-12) / 1e9;
+      const double p0 = pk / nw;
+      printf("cycles w0 proc %.1f sink %.1f task %.1f per_pkt tsc_ghz %.2f\n",
+             tsc[0] / p0, tsc[1] / p0, tsc[2] / p0, ghz);
       printf("out");
       for (size_t i = 0; i < n; i++) {
         if (verify)
@@ -370,13 +391,14 @@ static int run() {
       }
       printf("\n");
       if (GpuModule *g = dynamic_cast<GpuModule *>(m)) {
-        uint64_t st[7];
-        if (g->PipeStats(0, st, 7) == 0)
+        uint64_t st[9];
+        if (g->PipeStats(0, st, 9) == 0)
           printf("stats submits %llu pkts %llu launches %llu launch_ms %.3f full_ms %.3f "
-                 "wait_ms %.3f batch %llu\n",
+                 "wait_ms %.3f batch %llu submit_cyc_per_pkt %.1f poll_cyc_per_pkt %.1f\n",
                  (unsigned long long)st[0], (unsigned long long)st[1],
                  (unsigned long long)st[2], st[3] * 1e-6, st[4] * 1e-6, st[5] * 1e-6,
-                 (unsigned long long)st[6]);
+                 (unsigned long long)st[6], st[7] / (double)(st[1] ? st[1] : 1),
+                 st[8] / (double)(st[1] ? st[1] : 1));
       }
       if (verify) {
         bool ok = true;
