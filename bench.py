@@ -569,17 +569,23 @@ def run_e2e_pipe(args, torch):
     heads = snb.ctypes.data + 512 + 2624 * np.arange(n, dtype=np.uintp)
     want = om.process(frames, 64, n)
     del frames
+    from bess_amd._lib import kernel_paths, BG_PATH_PIPE_NO_RING
     em = {}
-    for batch in (4096, 65536):
-        p = Pipe(m, batch=batch, depth=4)
-        em["parity_batch%d" % batch] = bool((p.run(heads) == want).all())
-        p.close()
-        rates = {}
-        for th in [int(x) for x in args.pipe_threads.split(",")]:
-            rates[str(th)] = _pipe_rate(
-                lambda: Pipe(m, batch=batch, depth=4), heads, None, th,
-                reps=2 if th == 1 else 4)
-        em["Mpps_by_threads_batch%d" % batch] = rates
+    # ring: slots go to the module's persistent kernel (the plugin's shape,
+    # 8 x 1024 in flight per worker); launch: H2D/kernel/D2H per slot
+    for mode, batch, depth in (("ring", 1024, 8), ("launch", 4096, 4),
+                               ("launch", 65536, 4)):
+        key = "%s_batch%d_depth%d" % (mode, batch, depth)
+        with kernel_paths(BG_PATH_PIPE_NO_RING if mode == "launch" else 0):
+            p = Pipe(m, batch=batch, depth=depth)
+            em["parity_" + key] = bool((p.run(heads) == want).all())
+            p.close()
+            rates = {}
+            for th in [int(x) for x in args.pipe_threads.split(",")]:
+                rates[str(th)] = _pipe_rate(
+                    lambda: Pipe(m, batch=batch, depth=depth), heads, None, th,
+                    reps=2 if th == 1 else 4)
+        em["Mpps_by_threads_" + key] = rates
     out["ExactMatch_64B"] = em
     del snb
     # WildcardMatch, C4 rules (100 K over 8 masks), IMIX frames: the heavier
@@ -715,7 +721,9 @@ def run_plugin_pipeline(args):
                     "task emits) -> Sink, 32-pkt batches, 1000 rules, %d 64B "
                     "pkts in 2624 B snbufs split over the workers as the "
                     "cpu_baseline splits them" % n,
-            "Mpps_by_workers": res, "pipe": {"batch": 65536, "depth": 4},
+            "Mpps_by_workers": res,
+            "pipe": {"mode": "ring (bg_em_ring, one lane per worker)",
+                     "batch": 1024, "depth": 8},
             "worker0_pipe_stats": pipe_stats, "parity": parity,
             "cpu_same_harness": {
                 "what": "the same Source -> Sink workers with the restated "

@@ -22,6 +22,7 @@ BG_PATH_ACL_SCAN = 16
 BG_PATH_ACL_BV = 32
 BG_PATH_ACL_LDS = 64
 BG_PATH_LPM_DIR24 = 128
+BG_PATH_PIPE_NO_RING = 256
 KEY_BYTES = 64
 
 
@@ -143,7 +144,7 @@ _SIGS = {
     "bg_pipe_pending": (_sz, [_vp]),
     "bg_pipe_stats": (_int, [_vp, _vp, _int]),
     "bg_pipe_run": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
-    "bg_em_ring_create": (_int, [_vp, _int, _int, _int, _int, C.c_uint32,
+    "bg_em_ring_create": (_int, [_vp, _int, _int, _int, _int, C.c_uint32, _int,
                                  C.POINTER(_vp)]),
     "bg_ring_destroy": (None, [_vp]),
     "bg_ring_submit": (C.c_int64, [_vp, _int, _vp, _sz, _sz, _u16, _vp]),

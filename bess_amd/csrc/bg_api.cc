@@ -668,12 +668,17 @@ static int bind_meta(const std::vector<bg_field> &fields, int meta_off,
 namespace bg {
 // The device plan of a table for launches outside this file (the persistent
 // ring, bg_ring.cc): table synced to `device`, field plan of the slot layout.
-int em_device_plan(bg_em *em, int device, hipStream_t s, FieldPlan *fp,
-                   TableRef *t, int *read_end) {
+uint64_t em_version(const bg_em *em) { return em->version.load(std::memory_order_acquire); }
+
+int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off,
+                   FieldPlan *fp, TableRef *t, int *read_end, uint64_t *version) {
   if (em->has_attr && !em->meta_bound) return no_attr_datapath();
+  if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
+  if (int r = check_extent(em->dfields, -win_off, 0xFFFF)) return r;
   EmImage *img;
   if (int r = em_image(em, device, s, &img)) return r;
-  *fp = make_plan(em->dfields, true, 0);
+  *version = img->version;
+  *fp = make_plan(em->dfields, true, -win_off);
   *t = img->t;
   int hi = 0;  // bytes of a slot the kernel reads (check_extent)
   if (!fp->direct) {

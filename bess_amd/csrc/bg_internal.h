@@ -98,9 +98,15 @@ struct Staging {
 // when the caller passes no stream, runs on its own non-blocking stream per
 // device (never the legacy stream, which would serialise the workers).
 Staging &thread_staging();
-// bg_api.cc: a table's field plan (slot layout) and synced device table
-int em_device_plan(bg_em *em, int device, hipStream_t s, FieldPlan *fp,
-                   TableRef *t, int *read_end);
+// bg_api.cc: a table's field plan for slots that start at frame byte
+// win_off, its synced device table, and the rule version that image holds
+int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off,
+                   FieldPlan *fp, TableRef *t, int *read_end, uint64_t *version);
+uint64_t em_version(const bg_em *em);  // bumped by every rule change
+// bg_ring.cc: the rule version a ring classifies with; whether a lane's
+// ticket has finished (one host word, no lock)
+uint64_t ring_version(const bg_ring *r);
+bool ring_done(const bg_ring *r, int lane, int64_t ticket);
 hipStream_t thread_stream(int device, hipStream_t given);
 // bg_comm.cc: an assembled image (d_img, bytes; hipMalloc'ed on `device`,
 // laid out as bg_em_plan*) becomes the device's table image of the current

@@ -326,7 +326,8 @@ constexpr int kDnatMaxExt = 16;
 // unfinished ticket (re-classifying a finished batch is harmless).
 // Submission lanes (one per worker thread), each its own ring of nslots
 // descriptors, done words and published count; lane l's words at
-// l * kRingLaneWords (64 bytes apart).
+// l * kRingLaneWords (128 bytes apart: an L2 line and a host line pair of
+// their own, so lanes' claim atomics and submitters never share a line).
 struct RingArgs {
   const uint64_t *desc;   // host memory (mapped): nlanes x nslots x 4 words
   uint32_t *done;         // host memory (mapped): nlanes x nslots
@@ -341,8 +342,11 @@ struct RingArgs {
   FieldPlan fp;
   TableRef t;
 };
-constexpr int kRingBlock = 64;  // one wave: a 32-packet batch fills half of it
-constexpr int kRingLaneWords = 8;
+// four waves: a ticket's packets are spread over 256 lanes (4 per lane per
+// round), so a 1024-packet batch takes one round of loads and lookups
+// rather than four on one wave (a ticket's latency is its rounds')
+constexpr int kRingBlock = 256;
+constexpr int kRingLaneWords = 16;
 constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
 
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or

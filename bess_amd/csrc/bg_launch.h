@@ -32,7 +32,8 @@ constexpr uint32_t kPathAclScan = 16;   // ACL: the rule scan with scalar rule l
 constexpr uint32_t kPathAclBv = 32;     // ACL: per-dimension bit vectors
 constexpr uint32_t kPathAclLds = 64;    // ACL: the rule scan from LDS (not the tree)
 constexpr uint32_t kPathLpmDir24 = 128;  // IPLookup: DIR-24-8 (not DIR-16-8-8)
-constexpr uint32_t kPathAll = 255;
+constexpr uint32_t kPathPipeNoRing = 256;  // pipes launch per slot (no ring)
+constexpr uint32_t kPathAll = 511;
 
 uint32_t path_flags();
 

@@ -34,8 +34,10 @@
 
 using namespace bg;
 
-// One submission lane: a worker thread's own ring of descriptors.
-struct RingLane {
+// One submission lane: a worker thread's own ring of descriptors. Lanes sit
+// on lines of their own (128 B: the adjacent-line prefetcher pairs 64 B
+// lines), as each is written by its own submitter.
+struct alignas(128) RingLane {
   uint64_t *h_desc = nullptr;  // nslots x 4 words (host, coherent, mapped)
   uint32_t *h_done = nullptr;  // nslots
   uint64_t *h_pub = nullptr;   // tickets published (its own 64-byte line)
@@ -49,6 +51,7 @@ struct bg_ring {
   uint32_t nslots = 0, nlanes = 0;
   int blocks = 0;
   int read_end = 0;         // bytes of a slot the kernel reads
+  uint64_t version = 0;     // the rule version of its table copy
   hipStream_t st = nullptr;  // the kernel's own stream
   hipEvent_t ev = nullptr;   // recorded after each launch: has it ended?
   uint64_t *h_desc = nullptr;  // nlanes x nslots x 4 words
@@ -167,10 +170,22 @@ int bad_lane(const bg_ring *r, int lane) {
 
 }  // namespace
 
+namespace bg {
+
+uint64_t ring_version(const bg_ring *r) { return r->version; }
+
+bool ring_done(const bg_ring *r, int lane, int64_t ticket) {
+  const RingLane &l = r->lanes[lane];
+  if ((uint64_t)ticket < l.done_upto.load(std::memory_order_acquire)) return true;
+  return done_at(r, l, (uint64_t)ticket);
+}
+
+}  // namespace bg
+
 extern "C" {
 
 int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
-                      uint32_t idle_us, bg_ring **out) {
+                      uint32_t idle_us, int win_off, bg_ring **out) {
   if (!em || !out) return fail(EINVAL, "bad arguments");
   if (lanes < 1 || lanes > kRingMaxLanes)
     return fail(EINVAL, "lanes %d not in [1,%d]", lanes, kRingMaxLanes);
@@ -184,7 +199,7 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
   r->device = device;
   r->nslots = (uint32_t)slots;
   r->nlanes = (uint32_t)lanes;
-  // workers (at least one per lane; one-wave workgroups, 4 per CU beside a
+  // workers (at least one per lane; four-wave workgroups, 4 per CU beside a
   // 38 KB LDS table) + the dispatcher
   int wk = blocks > 0 ? blocks : 4 * num_cus(device);
   wk = std::max(wk, lanes);
@@ -232,7 +247,7 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
     delete r;
     return fail(EIO, "no device address for the ring's host memory");
   }
-  rc = em_device_plan(em, device, r->st, &a.fp, &a.t, &r->read_end);
+  rc = em_device_plan(em, device, r->st, win_off, &a.fp, &a.t, &r->read_end, &r->version);
   if (rc == 0) {
     // The ring classifies with the rule set as of its creation: it keeps
     // its own copy of the table image, so a later rule change (bessd makes

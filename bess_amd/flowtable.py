@@ -190,10 +190,10 @@ class Ring:
     creation, in LDS for the kernel's whole run)."""
 
     def __init__(self, table, device=0, slots=1024, blocks=0, idle_us=200000,
-                 lanes=1):
+                 lanes=1, win_off=0):
         h = C.c_void_p()
         check(lib().bg_em_ring_create(table.h, device, lanes, slots, blocks,
-                                      idle_us, C.byref(h)))
+                                      idle_us, win_off, C.byref(h)))
         self.h = h
         self.table = table
         self.lanes = lanes

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/bessgpu.h"
+#include "../csrc/bg_internal.h"
 #include "module.h"
 
 namespace {
@@ -56,7 +57,10 @@ class ExactMatch final : public Module {
   static const gate_idx_t kNumOGates = MAX_GATES;
   static const Commands kCmds;
 
-  ~ExactMatch() override { bg_em_destroy(table_); }
+  ~ExactMatch() override {
+    rings_.clear();
+    bg_em_destroy(table_);
+  }
 
   const Commands &cmds() const override { return kCmds; }
 
@@ -119,6 +123,36 @@ class ExactMatch final : public Module {
     if (rc < 0) return rc;
     return bg_em_classify_window(table_, d_win, wstride, n, win_off,
                                  default_gate_, d_ogates, stream);
+  }
+
+  // A pipe's slots go to one persistent classify kernel per device (bg_ring:
+  // no HIP call per slot; the kernel reads the staged windows from pinned
+  // host memory and writes the gates back there), re-created after a rule
+  // change. Its workgroups take 2 per CU (half of each CU's LDS), leaving
+  // room for other modules' kernels on the device.
+  static const int kPipeRingLanes = 16;
+  int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) override {
+    out->reset();
+    if (!all_attrs().empty() || (bg_get_path_flags() & BG_PATH_PIPE_NO_RING)) return 0;
+    std::lock_guard<std::mutex> lk(ring_mu_);
+    std::shared_ptr<PipeRing> &cur = rings_[device];
+    if (!cur || cur->version != bg::em_version(table_)) {
+      int lo = 0, hi = 0;
+      bg_em_window(table_, &lo, &hi);
+      bg_ring *r = nullptr;
+      const int rc = bg_em_ring_create(table_, device, kPipeRingLanes, 64,
+                                       2 * bg::num_cus(device), 10000, lo, &r);
+      if (rc < 0) return rc;
+      auto pr = std::make_shared<PipeRing>();
+      pr->r = r;
+      pr->device = device;
+      pr->lanes = kPipeRingLanes;
+      pr->version = bg::ring_version(r);
+      cur = std::move(pr);
+    }
+    *out = cur;
+    *dflt = default_gate_;
+    return 0;
   }
 
   // exact_match.cc:122-147
@@ -330,6 +364,8 @@ class ExactMatch final : public Module {
   gate_idx_t default_gate_ = DROP_GATE;
   bool empty_masks_ = true;
   bg_em *table_ = nullptr;
+  std::mutex ring_mu_;
+  std::map<int, std::shared_ptr<PipeRing>> rings_;  // per device
 };
 
 // exact_match.cc:45-60

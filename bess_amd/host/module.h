@@ -18,6 +18,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <functional>
 #include <map>
 #include <memory>
@@ -127,6 +128,20 @@ CommandResponse CommandFailure(int code, const char *fmt = nullptr, ...)
 
 class Module;
 
+// A persistent ring (bg_ring) serving a module's staged windows on one
+// device, shared by the module's pipes (each on a lane of its own while
+// there are lanes) and by their in-flight slots: it is destroyed -- its
+// grid stopped -- when the last of them lets go, so a rule change retires
+// it only once every slot submitted under the old rules has finished.
+struct PipeRing {
+  bg_ring *r = nullptr;
+  int device = 0;
+  int lanes = 0;
+  uint64_t version = 0;  // the rules it classifies with
+  std::atomic<int> next_lane{0};
+  ~PipeRing() { bg_ring_destroy(r); }
+};
+
 struct Command {
   enum ThreadSafety { THREAD_UNSAFE = 0, THREAD_SAFE = 1 };
   std::string cmd;
@@ -193,6 +208,16 @@ class Module {
                                   void *stream) {
     if (win_off != 0) return -EINVAL;
     return ProcessDevice(c, d_win, wstride, n, d_ogates, stream);
+  }
+  // The ring a pipe submits its slots to on `device` (their windows start at
+  // DeviceWindow's lo), with the gate of packets no rule matches; null when
+  // the module has none (the pipe launches H2D/kernel/D2H per slot). A
+  // module returns a new ring once its rules changed (<0: -errno).
+  virtual int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) {
+    (void)device;
+    (void)dflt;
+    out->reset();
+    return 0;
   }
   // attr_name fields: metadata area at slot offset meta_off, attribute
   // offsets by name (bg_module_bind_meta). Modules without attr fields on

@@ -24,6 +24,13 @@
 // i+1, the H2D of slot i, the kernel of slot i-1 and the D2H of slot i-2
 // overlap. Packets stay owned by the caller until poll returns them (the
 // device only ever sees copies of their bytes, core/module.h:224-226).
+//
+// Ring mode (a module with a persistent kernel, Module::PipeRingFor:
+// ExactMatch): a slot's staging and gates live in pinned host memory the
+// device maps; launch writes one descriptor on the pipe's lane of the
+// module's bg_ring and poll reads the lane's done word -- no HIP call per
+// slot, so slots can be small (little in flight per worker, as bessd's
+// packet pool is shared by all workers) at no launch cost.
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <time.h>
@@ -60,6 +67,13 @@ struct Slot {
   bool draining = false;  // completed; poll hands out [cursor, n)
   size_t cursor = 0;
   bg_ctx ctx{};  // the context of the slot's packets (Module::CtxUse fields)
+  // ring mode: the device addresses of h_in / h_g, and the ticket in flight
+  uint8_t *dv_in = nullptr;
+  uint16_t *dv_g = nullptr;
+  std::shared_ptr<PipeRing> ring;  // the ring (rules) it was submitted to
+  int lane = 0;
+  int64_t ticket = -1;
+  uint64_t t_launch = 0;  // TSC at launch (bg_pipe_stats: launch -> done)
 };
 
 }  // namespace
@@ -72,6 +86,9 @@ struct bg_pipe {
   size_t w = 0;          // staged stride (16-byte multiple)
   bool writeback = false;
   unsigned ctx_use = 0;  // Module::CtxUse(): the context fields a slot fixes
+  bool ring_mode = false;          // slots go to the module's ring
+  std::shared_ptr<PipeRing> ring;  // the ring this pipe has a lane on
+  int lane = 0;
   std::vector<Slot> slots;
   size_t fill = 0;       // slot being filled
   size_t oldest = 0;     // oldest in-flight slot
@@ -87,6 +104,7 @@ struct bg_pipe {
   uint64_t st_submits = 0, st_pkts = 0, st_launch_ns = 0, st_full_ns = 0,
            st_wait_ns = 0;
   uint64_t st_submit_tsc = 0, st_poll_tsc = 0;  // cycles inside submit / poll
+  uint64_t st_lat_tsc = 0, st_lat_max = 0;      // slot launch -> seen done
   // One worker owns a pipe; the lock is for the module's control path
   // (PipeFlushLocked) and a RunTask on another worker (never contended on
   // the datapath).
@@ -95,6 +113,10 @@ struct bg_pipe {
 
 static void pipe_release(bg_pipe *p) {
   for (Slot &s : p->slots) {
+    if (s.ring) {  // the kernel may still read the staging: let it finish
+      if (s.inflight) (void)bg_ring_wait(s.ring->r, s.lane, s.ticket);
+      s.ring.reset();
+    }
     if (s.st) {
       (void)hipStreamSynchronize(s.st);
       bg::stream_gone(s.st);  // no table image fences on it any more
@@ -145,6 +167,31 @@ static int launch_slot(bg_pipe *p) {
   Slot &s = p->slots[p->fill];
   const size_t n = s.n;
   const uint64_t t0 = mono_ns();
+  s.t_launch = __rdtsc();
+  if (p->ring_mode) {
+    // one descriptor on the pipe's lane of the module's current ring (a new
+    // ring after a rule change: a lane there)
+    std::shared_ptr<PipeRing> ring;
+    uint16_t dflt = 0;
+    int rc = p->mod->m->PipeRingFor(p->device, &ring, &dflt);
+    if (rc < 0) return rc;
+    if (!ring) return fail(ENOTSUP, "the module no longer serves pipes through a ring");
+    if (ring != p->ring) {
+      p->ring = ring;
+      p->lane = ring->next_lane.fetch_add(1) % ring->lanes;
+    }
+    const int64_t t = bg_ring_submit(ring->r, p->lane, s.dv_in, p->w, n, dflt, s.dv_g);
+    if (t < 0) return (int)t;
+    s.ring = std::move(ring);
+    s.lane = p->lane;
+    s.ticket = t;
+    s.seq = ++p->launched;
+    p->st_launch_ns += mono_ns() - t0;
+    s.inflight = true;
+    p->inflight++;
+    p->fill = (p->fill + 1) % p->slots.size();
+    return 0;
+  }
   int rc = bg::set_device(p->device);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
@@ -175,7 +222,23 @@ static int launch_slot(bg_pipe *p) {
 static int retire_oldest(bg_pipe *p, bool wait) {
   Slot &s = p->slots[p->oldest];
   if (!s.inflight) return 0;
-  if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq) {
+  if (s.ring) {
+    if (!bg::ring_done(s.ring->r, s.lane, s.ticket)) {
+      // (through the ring's own check, which relaunches a grid that ended)
+      const int64_t c = bg_ring_completed(s.ring->r, s.lane);
+      if (c < 0) return (int)c;
+      if (c <= s.ticket) {
+        if (!wait) return 0;
+        const uint64_t t0 = mono_ns();
+        if (int rc = bg_ring_wait(s.ring->r, s.lane, s.ticket)) return rc;
+        p->st_wait_ns += mono_ns() - t0;
+      }
+    }
+    s.ring.reset();  // the last slot on a replaced ring retires it
+    const uint64_t lat = __rdtsc() - s.t_launch;
+    p->st_lat_tsc += lat;
+    p->st_lat_max = std::max(p->st_lat_max, lat);
+  } else if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq) {
     if (!wait) return 0;
     const uint64_t t0 = mono_ns();
     int rc = bg::set_device(p->device);
@@ -185,6 +248,11 @@ static int retire_oldest(bg_pipe *p, bool wait) {
     if (__atomic_load_n(s.h_done, __ATOMIC_ACQUIRE) != s.seq)
       return fail(EIO, "pipe slot %llu: completion word not written",
                   (unsigned long long)s.seq);
+  }
+  if (!s.ring) {
+    const uint64_t lat = __rdtsc() - s.t_launch;
+    p->st_lat_tsc += lat;
+    p->st_lat_max = std::max(p->st_lat_max, lat);
   }
   if (p->writeback) {
     const size_t line = std::min(p->w, kWriteback);
@@ -255,8 +323,36 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
   if (p->hi <= p->lo) p->hi = p->lo + 1;
   p->w = ((size_t)(p->hi - p->lo) + 15) / 16 * 16;
   p->ctx_use = m->m->CtxUse();
+  if (!p->writeback) {
+    uint16_t dflt = 0;
+    r = m->m->PipeRingFor(device, &p->ring, &dflt);
+    if (r < 0) {
+      delete p;
+      return r;
+    }
+    p->ring_mode = p->ring != nullptr;
+    if (p->ring_mode) p->lane = p->ring->next_lane.fetch_add(1) % p->ring->lanes;
+  }
   p->slots.resize((size_t)depth);
   for (Slot &s : p->slots) {
+    if (p->ring_mode) {
+      // the kernel reads the windows and writes the gates in place (mapped,
+      // coherent: never cached on the device, so a refilled slot is seen)
+      const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+      hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.h_in), batch * p->w + 64, fl);
+      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_g), batch * 2 + 64, fl);
+      if (e == hipSuccess)
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dv_in), s.h_in, 0);
+      if (e == hipSuccess)
+        e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dv_g), s.h_g, 0);
+      if (e != hipSuccess) {
+        pipe_release(p);
+        delete p;
+        return fail(EIO, "HIP error %d: %s", (int)e, hipGetErrorString(e));
+      }
+      s.cookies.resize(batch);
+      continue;
+    }
     // +64 B: window loads of the last packet may run past its slot
     hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.h_in), batch * p->w + 64,
                                  hipHostMallocDefault);
@@ -303,6 +399,7 @@ void bg_pipe_destroy(bg_pipe *p) {
   {
     std::lock_guard<std::mutex> lk(p->mu);
     pipe_release(p);
+    p->ring.reset();
   }
   delete p;
 }
@@ -427,10 +524,11 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
 size_t bg_pipe_pending(const bg_pipe *p) { return p->pending; }
 
 int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n) {
-  const uint64_t v[9] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
-                         p->st_full_ns, p->st_wait_ns, (uint64_t)p->batch,
-                         p->st_submit_tsc, p->st_poll_tsc};
-  for (int i = 0; i < n && i < 9; i++) out[i] = v[i];
+  const uint64_t v[11] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
+                          p->st_full_ns, p->st_wait_ns, (uint64_t)p->batch,
+                          p->st_submit_tsc, p->st_poll_tsc, p->st_lat_tsc,
+                          p->st_lat_max};
+  for (int i = 0; i < n && i < 11; i++) out[i] = v[i];
   return 0;
 }
 

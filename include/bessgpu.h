@@ -235,6 +235,7 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_ACL_BV 32   /* ACL: per-dimension bit vectors */
 #define BG_PATH_ACL_LDS 64  /* ACL: rule scan from LDS (not the decision tree) */
 #define BG_PATH_LPM_DIR24 128 /* IPLookup: DIR-24-8 tables (not DIR-16-8-8) */
+#define BG_PATH_PIPE_NO_RING 256 /* pipes launch per slot (not via a ring) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */
@@ -527,7 +528,8 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
 size_t bg_pipe_pending(const bg_pipe *p);
 /* counters (first n of): submits, packets, slot launches, ns spent in
  * launches (HIP calls), ns submits waited for a free slot, ns polls
- * waited, the slot size, TSC cycles inside submit, inside poll */
+ * waited, the slot size, TSC cycles inside submit, inside poll, TSC cycles
+ * from slot launches to their completion being seen (sum, max) */
 int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n);
 /* A worker loop (Source -> module -> Sink): n packets submitted in bursts of
  * `burst`, completions polled after each submit; ogates[i] = packet i's
@@ -536,6 +538,8 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                 const uint16_t *lens, size_t n, size_t burst, uint16_t *ogates);
 
 /* ---- Persistent classify kernel: rings of batch descriptors -------------
+ * (A pipe on an ExactMatch module submits its slots to such a ring: see
+ * bg_pipe_create.) 
  * BESS hands a module <= 32 packets per ProcessBatch (core/pktbatch.h:70);
  * a kernel launch per batch costs more than the batch. A ring is ONE
  * running ExactMatch kernel that drains batch descriptors the workers write
@@ -543,21 +547,22 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
  * Each worker thread submits on its own lane (0 .. lanes-1: its own ring of
  * `slots` descriptors, done words and published count, so workers never
  * share a cache line or a lock): submit enqueues a batch (frames at
- * `frames` + i*stride, device or mapped host memory; gates written to
- * `gates`) and returns the lane's ticket; wait blocks until that ticket's
+ * `frames` + i*stride, device or mapped host memory, each slot holding the
+ * frame from byte win_off on -- 0: whole frames, the field window's start:
+ * staged windows; gates written to `gates`) and returns the lane's ticket; wait blocks until that ticket's
  * gates are written; completed returns the number of the lane's tickets
  * finished in order. Create it with as many lanes as workers submit on. The
  * kernel keeps the table in LDS for its whole run and classifies with the
  * rule set as of bg_em_ring_create (it holds its own copy of the table
  * image: re-create the ring after rule changes, which bessd makes with
  * workers paused). slots: a power of two <= 32768 (submit blocks while
- * `slots` of the lane's tickets are unfinished); blocks: one-wave workgroups
+ * `slots` of the lane's tickets are unfinished); blocks: 256-thread workgroups
  * (0: 4 per CU), spread evenly over the lanes; idle_us: the kernel exits after this long without work and is
  * relaunched by the next submit or wait (so it never outlives its work); a
  * submit makes no HIP call while the kernel runs. */
 typedef struct bg_ring bg_ring;
 int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
-                      uint32_t idle_us, bg_ring **out);
+                      uint32_t idle_us, int win_off, bg_ring **out);
 void bg_ring_destroy(bg_ring *r); /* stops the kernel and waits for it */
 int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
                        size_t n, uint16_t default_gate, uint16_t *gates);

@@ -9,7 +9,8 @@ class ExactMatch final : public GpuModule {
   static const Commands cmds;
 
   CommandResponse Init(const bess::pb::ExactMatchArg &arg) {
-    return CreateDeferred("ExactMatch", arg);
+    // served by a persistent ring on each device: small pipe slots
+    return CreateDeferred("ExactMatch", arg, kRingPipeBatch, kRingPipeDepth);
   }
   CommandResponse GetInitialArg(const bess::pb::EmptyArg &arg) {
     bess::pb::ExactMatchArg r;

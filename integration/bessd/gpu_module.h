@@ -36,11 +36,27 @@
 #include "bessgpu.h"
 
 class GpuModule : public Module {
+ private:
+  // one cache line per worker: its ProcessBatch calls count submits here
+  struct alignas(64) Lane {
+    std::atomic<bg_pipe *> pipe{nullptr};
+    std::atomic<uint64_t> submits{0};  // ProcessBatch calls so far
+    uint64_t seen = 0;                 // submits at the task's last visit
+    std::atomic<bool> in_call{false};   // the owner is in ProcessBatch
+    std::atomic<bool> draining{false};  // the task is emitting this pipe
+  };
+
  public:
   // the deferred datapath's pipes: packets per device launch, launches in
-  // flight per worker
+  // flight per worker. A module served by a persistent ring (ExactMatch)
+  // submits small slots at no launch cost: 8 x 1024 packets in flight per
+  // worker (bessd's default pool is 256 K buffers for all workers,
+  // core/opts.cc:127); the others launch H2D/kernel/D2H per slot and
+  // amortise that over 64 K packets.
   static const size_t kPipeBatch = 65536;
   static const int kPipeDepth = 4;
+  static const size_t kRingPipeBatch = 1024;
+  static const int kRingPipeDepth = 8;
 
   void DeInit() override {
     for (Lane &l : lanes_) {
@@ -60,17 +76,28 @@ class GpuModule : public Module {
 
   // The module's task (deferred datapath): a worker's pipe that received
   // nothing since the last visit is flushed (its partly filled slot is
-  // launched), then every pipe's finished packets leave (`packets`: those
-  // it handed on, emitted, dropped or not emitted).
+  // launched) and its finished packets leave (`packets`: those it handed
+  // on, emitted, dropped or not emitted). A worker that keeps calling
+  // ProcessBatch drains its own pipe there, so the task's worker never
+  // carries the others' emissions; and a pipe's packets are emitted by one
+  // thread at a time (the owner waits while the task empties its pipe), so
+  // they leave in submission order.
   struct task_result RunTask(Context *ctx, bess::PacketBatch *, void *) override {
     uint32_t done = 0;
     for (Lane &l : lanes_) {
       bg_pipe *p = l.pipe.load(std::memory_order_acquire);
       if (!p || bg_pipe_pending(p) == 0) continue;
       const uint64_t sub = l.submits.load(std::memory_order_relaxed);
-      if (sub == l.seen) (void)bg_pipe_flush(p);
-      l.seen = sub;
-      done += Drain(ctx, p);
+      if (sub != l.seen) {
+        l.seen = sub;
+        continue;
+      }
+      if (l.draining.exchange(true)) continue;
+      if (!l.in_call.load()) {  // (seq_cst: pairs with Enqueue's entry)
+        (void)bg_pipe_flush(p);
+        done += Drain(ctx, p);
+      }
+      l.draining.store(false, std::memory_order_release);
     }
     return {.block = done == 0, .packets = done, .bits = 0};
   }
@@ -99,9 +126,13 @@ class GpuModule : public Module {
   }
 
   // Create, with the deferred datapath: ProcessBatch enqueues, a task emits
-  CommandResponse CreateDeferred(const char *mclass, const google::protobuf::Message &arg) {
+  CommandResponse CreateDeferred(const char *mclass, const google::protobuf::Message &arg,
+                                 size_t pipe_batch = kPipeBatch,
+                                 int pipe_depth = kPipeDepth) {
     CommandResponse r = Create(mclass, arg);
     if (r.code() != 0) return r;
+    pipe_batch_ = pipe_batch;
+    pipe_depth_ = pipe_depth;
     if (RegisterTask(nullptr) == INVALID_TASK_ID)
       return CommandFailure(ENOMEM, "Task creation failed");
     deferred_ = true;
@@ -165,8 +196,16 @@ class GpuModule : public Module {
   // ProcessBatch, deferred: the batch joins this worker's pipe, then what
   // has finished there leaves
   void Enqueue(Context *ctx, bess::PacketBatch *batch) {
-    const int n = batch->cnt();
     Lane &l = lanes_[ctx->wid];
+    l.in_call.store(true);  // (seq_cst: pairs with RunTask's claim)
+    while (l.draining.load(std::memory_order_acquire)) {
+    }
+    EnqueueOwned(ctx, batch, l);
+    l.in_call.store(false, std::memory_order_release);
+  }
+
+  void EnqueueOwned(Context *ctx, bess::PacketBatch *batch, Lane &l) {
+    const int n = batch->cnt();
     bg_pipe *p = l.pipe.load(std::memory_order_acquire);
     if (!p && !(p = OpenLane(ctx->wid))) {
       for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
@@ -210,32 +249,30 @@ class GpuModule : public Module {
   bg_module *m_ = nullptr;
 
  private:
-  // one cache line per worker: its ProcessBatch calls count submits here
-  struct alignas(64) Lane {
-    std::atomic<bg_pipe *> pipe{nullptr};
-    std::atomic<uint64_t> submits{0};  // ProcessBatch calls so far
-    uint64_t seen = 0;                 // submits at the task's last visit
-  };
-
   // the worker's pipe, on device wid % (visible devices): the workers of one
   // process spread over its GPUs, each using the module's table replica there
   bg_pipe *OpenLane(int wid) {
     const int nd = bg_device_count();
     bg_pipe *p = nullptr;
-    if (nd <= 0 || bg_pipe_create(m_, wid % nd, kPipeBatch, kPipeDepth, 0, &p) < 0)
+    if (nd <= 0 || bg_pipe_create(m_, wid % nd, pipe_batch_, pipe_depth_, 0, &p) < 0)
       return nullptr;
     lanes_[wid].pipe.store(p, std::memory_order_release);
     return p;
   }
 
-  // emit the pipe's finished packets (in submission order)
+  // emit the pipe's finished packets (in submission order); each packet's
+  // mbuf line is fetched a few packets ahead for the module downstream
   uint32_t Drain(Context *ctx, bg_pipe *p) {
     void *ck[512];
     uint16_t g[512];
     uint32_t total = 0;
     long k;
     while ((k = bg_pipe_poll(p, 0, ck, g, 512)) > 0) {
-      for (long i = 0; i < k; i++) Emit(ctx, static_cast<bess::Packet *>(ck[i]), g[i]);
+      for (long i = 0; i < k && i < 8; i++) __builtin_prefetch(ck[i]);
+      for (long i = 0; i < k; i++) {
+        if (i + 8 < k) __builtin_prefetch(ck[i + 8]);
+        Emit(ctx, static_cast<bess::Packet *>(ck[i]), g[i]);
+      }
       total += (uint32_t)k;
       if (k < 512) break;
     }
@@ -243,6 +280,8 @@ class GpuModule : public Module {
   }
 
   bool deferred_ = false;
+  size_t pipe_batch_ = kPipeBatch;
+  int pipe_depth_ = kPipeDepth;
   Lane lanes_[Worker::kMaxWorkers];
 };
 

@@ -7,7 +7,7 @@ OUT=gpurun_out; mkdir -p $OUT
 nproc > $OUT/nproc.txt; lscpu > $OUT/lscpu.txt 2>&1
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 \
-      --timeout-method thread $PYTEST_ARGS > $OUT/tests.log 2>&1
+      --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/tests.log 2>&1
   rc=$?; tail -3 $OUT/tests.log; [ $rc -ne 0 ] && exit $rc
 fi
 for leg in "$@"; do

@@ -118,6 +118,10 @@ struct Context {
   // where each packet went (the shell's stand-in for the task's batches)
   std::vector<std::pair<bess::Packet *, gate_idx_t>> emitted;
   std::vector<bess::Packet *> dropped;
+  // (verify) emission order: a number from one counter shared by all
+  // workers, per packet (Packet::pool_index), taken when EmitPacket runs
+  std::atomic<uint64_t> *emit_counter = nullptr;
+  std::vector<uint64_t> *emit_seq = nullptr;
 };
 
 class CommandResponse {
@@ -216,6 +220,7 @@ class Module {
       return;
     }
     ctx->emitted.push_back({pkt, ogate});
+    if (ctx->emit_seq) (*ctx->emit_seq)[pkt->pool_index()] = (*ctx->emit_counter)++;
   }
   void DropPacket(Context *ctx, bess::Packet *pkt) { ctx->dropped.push_back(pkt); }
   // core/module.h:530-532: the whole batch to output gate 0

@@ -134,13 +134,10 @@ static void run_task(Module *m, Context *ctx) {
 struct Sink {  // where a worker's emitted and dropped packets go
   std::vector<std::string> *gate = nullptr;  // per packet (verify)
   std::vector<uint16_t> *fast = nullptr;     // per packet (timing)
-  std::vector<uint64_t> *seq = nullptr;      // emission order (verify)
-  std::atomic<uint64_t> *counter = nullptr;
+
   uint8_t *pool = nullptr;
   uint64_t n = 0;
   void take(Context &ctx) {
-    // (emitted packets in emission order; drops go to the dead batch, so
-    // only emitted packets carry an emission sequence number)
     for (auto &e : ctx.emitted) put(e.first, e.second);
     for (auto *p : ctx.dropped) put(p, 0xFFFF);
     n += ctx.emitted.size() + ctx.dropped.size();
@@ -151,7 +148,6 @@ struct Sink {  // where a worker's emitted and dropped packets go
     const size_t i = p->pool_index();
     if (fast) (*fast)[i] = (uint16_t)g;
     if (gate) (*gate)[i] = g == 0xFFFF ? "D" : std::to_string(g);
-    if (seq && g != 0xFFFF) (*seq)[i] = (*counter)++;
   }
 };
 
@@ -304,14 +300,16 @@ static int run() {
         pin(w);
         Sink sink;
         sink.pool = pool;
+        Context ctx;
         if (verify) {
           sink.gate = &out;
-          sink.seq = &seq;
-          sink.counter = &counter;
+          // (only emitted packets carry an emission number: drops go to
+          // the dead batch)
+          ctx.emit_seq = &seq;
+          ctx.emit_counter = &counter;
         } else {
           sink.fast = &fast;
         }
-        Context ctx;
         ctx.wid = w;
         ctx.current_igate = (gate_idx_t)ig;
         ctx.current_ns = now;
@@ -391,14 +389,16 @@ static int run() {
       }
       printf("\n");
       if (GpuModule *g = dynamic_cast<GpuModule *>(m)) {
-        uint64_t st[9];
-        if (g->PipeStats(0, st, 9) == 0)
+        uint64_t st[11];
+        if (g->PipeStats(0, st, 11) == 0)
           printf("stats submits %llu pkts %llu launches %llu launch_ms %.3f full_ms %.3f "
-                 "wait_ms %.3f batch %llu submit_cyc_per_pkt %.1f poll_cyc_per_pkt %.1f\n",
+                 "wait_ms %.3f batch %llu submit_cyc_per_pkt %.1f poll_cyc_per_pkt %.1f "
+                 "slot_latency_us avg %.1f max %.1f\n",
                  (unsigned long long)st[0], (unsigned long long)st[1],
                  (unsigned long long)st[2], st[3] * 1e-6, st[4] * 1e-6, st[5] * 1e-6,
                  (unsigned long long)st[6], st[7] / (double)(st[1] ? st[1] : 1),
-                 st[8] / (double)(st[1] ? st[1] : 1));
+                 st[8] / (double)(st[1] ? st[1] : 1),
+                 st[9] / (double)(st[2] ? st[2] : 1) / 3300.0, st[10] / 3300.0);
       }
       if (verify) {
         bool ok = true;

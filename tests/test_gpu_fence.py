@@ -51,7 +51,17 @@ def pipe_across_update(m, frames, stride, update, batch=4096, depth=4):
     return g, split
 
 
-def test_exact_match_pipe_across_rule_change():
+@pytest.mark.parametrize("mode", ["ring", "launch"])
+def test_exact_match_pipe_across_rule_change(mode):
+    """ring: slots in flight on the module's persistent kernel keep the ring
+    (and its table copy) of their submission; the next slot goes to a new
+    ring with the new rules"""
+    from bess_amd._lib import kernel_paths, BG_PATH_PIPE_NO_RING
+    with kernel_paths(BG_PATH_PIPE_NO_RING if mode == "launch" else 0):
+        _exact_match_pipe_across_rule_change(1024 if mode == "ring" else 4096)
+
+
+def _exact_match_pipe_across_rule_change(batch):
     keys, gates, frames = P.em_workload(1000, 40000, seed=5)
     m = ExactMatch(fields=FIELDS)
     o_old, o_new = O.OracleExactMatch(fields=FIELDS), O.OracleExactMatch(fields=FIELDS)
@@ -66,7 +76,8 @@ def test_exact_match_pipe_across_rule_change():
     def update():  # every rule's gate changes (overwrite, P7)
         for k, g in zip(keys, gates):
             m.add(**em_rule(k, (int(g) + 7) % 64))
-    got, split = pipe_across_update(m, frames, 64, update)
+    got, split = pipe_across_update(m, frames, 64, update, batch=batch,
+                                    depth=8 if batch == 1024 else 4)
     assert (got[:split] == want_old[:split]).all()
     assert (got[split:] == want_new[split:]).all()
 

@@ -73,9 +73,19 @@ def em_pair(keys, gates):
     return m, om
 
 
+@pytest.mark.parametrize("mode", ["ring", "launch"])
 @pytest.mark.parametrize("batch,depth,burst", [(4096, 4, 32), (1000, 2, 32),
-                                               (1, 1, 3), (65536, 3, 32)])
-def test_em_pipe_vs_oracle(batch, depth, burst):
+                                               (1, 1, 3), (65536, 3, 32),
+                                               (1024, 8, 32)])
+def test_em_pipe_vs_oracle(batch, depth, burst, mode):
+    """ring: the slots go to the module's persistent kernel (the default
+    for ExactMatch); launch: H2D / kernel / D2H per slot"""
+    from bess_amd._lib import kernel_paths, BG_PATH_PIPE_NO_RING
+    with kernel_paths(BG_PATH_PIPE_NO_RING if mode == "launch" else 0):
+        _em_pipe_vs_oracle(batch, depth, burst)
+
+
+def _em_pipe_vs_oracle(batch, depth, burst):
     n = 20000 if batch > 1 else 500
     keys, gates, frames = P.em_workload(1000, n, seed=11)
     m, om = em_pair(keys, gates)
@@ -93,6 +103,36 @@ def test_em_pipe_vs_oracle(batch, depth, burst):
     got = run_pipe(pipe, heads[:k], burst=burst)
     assert (got == om.process(frames[:k], 64, k)).all()
     pipe.close()
+
+
+def test_em_pipes_share_ring_lanes():
+    """18 pipes on one module, each run by its own thread (as bessd workers
+    submit): more pipes than the module's ring has lanes (16), so two pairs
+    share a lane; every packet's gate is bit-exact"""
+    import threading
+    n = 16384
+    keys, gates, frames = P.em_workload(1000, n, seed=12)
+    m, om = em_pair(keys, gates)
+    want = om.process(frames, 64, n)
+    buf, heads = snbufs(frames)
+    pipes = [Pipe(m, batch=1024, depth=8) for _ in range(18)]
+    outs, errs = [None] * len(pipes), []
+
+    def work(i):
+        try:
+            outs[i] = pipes[i].run(heads)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(pipes))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for p in pipes:
+        p.close()
+    assert not errs, errs
+    for o in outs:
+        assert (o == want).all()
 
 
 def test_wm_pipe_vs_oracle():
