@@ -1210,15 +1210,31 @@ def run_wm(args, dev, torch):
     want = np.zeros(ns, np.uint16)
     L.or_wm_process(ow, sample.ctypes.data, 2048, ns, 8192, want.ctypes.data)
 
-    def timed(slab, stride, gates):
-        for _ in range(args.warmup):
+    # the run-time compiled kernel of this rule set (bg_wm_jit.cc): the
+    # product's launch once ready; compiled on a background thread
+    from bess_amd import _lib as LB
+    tj = time.time()
+    t.jit_wait()
+    jit_s = time.time() - tj
+
+    def timed(slab, stride, gates, flags=0):
+        with LB.kernel_paths(flags):
+            for _ in range(args.warmup):
+                t.classify(slab, stride, n, 8192, gates)
+            torch.cuda.synchronize()
+            timer = Timer(torch)
+            timer.start()
+            for _ in range(args.steps):
+                t.classify(slab, stride, n, 8192, gates)
+            return timer.stop_ms() / args.steps
+
+    def aot_check(slab, stride, gates, g_jit):
+        """the ahead-of-time kernel: same gates, its time"""
+        with LB.kernel_paths(LB.BG_PATH_WM_NO_JIT):
             t.classify(slab, stride, n, 8192, gates)
-        torch.cuda.synchronize()
-        timer = Timer(torch)
-        timer.start()
-        for _ in range(args.steps):
-            t.classify(slab, stride, n, 8192, gates)
-        return timer.stop_ms() / args.steps
+            torch.cuda.synchronize()
+        same = bool((gates.cpu().numpy().view(np.uint16)[:n0] == g_jit).all())
+        return same, timed(slab, stride, gates, LB.BG_PATH_WM_NO_JIT)
 
     def check(gates_t):
         got = gates_t.cpu().numpy().view(np.uint16)
@@ -1226,7 +1242,7 @@ def run_wm(args, dev, torch):
                     (got.reshape(rep, n0) == got[:n0]).all()), got[:n0]
 
     nan = float("nan")
-    parity, ms2k, g2k = True, nan, None
+    parity, ms2k, g2k, aot2k, aot_h = True, nan, None, nan, nan
     if args.wm_layout != "slab":  # the frames in 2 KB slots
         d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
         d = d0.repeat(rep)
@@ -1236,6 +1252,8 @@ def run_wm(args, dev, torch):
         torch.cuda.synchronize()
         parity, g2k = check(dg)
         ms2k = timed(d, 2048, dg)
+        same2k, aot2k = aot_check(d, 2048, dg, g2k)
+        parity = parity and same2k
         del d, dg
     gbs2k = EM_BYTES_PER_PKT * n / (ms2k * 1e-3) / 1e9
     # The same packets' header lines in a dense 64 B slab: the layout the
@@ -1253,6 +1271,8 @@ def run_wm(args, dev, torch):
         if g2k is not None:
             parity_h = parity_h and bool((gh == g2k).all())
         ms = timed(hs, 64, dgh)
+        same_h, aot_h = aot_check(hs, 64, dgh, gh)
+        parity_h = parity_h and same_h
         del hs, dgh
     mpps = n / (ms * 1e-3) / 1e6
     gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
@@ -1266,6 +1286,12 @@ def run_wm(args, dev, torch):
                             2: "key filter (table in L2/MALL)",
                             3: "tag words (keys/values in L2/MALL)"}[int(in_lds)],
            "direct_tuples": t.direct_tuples(),
+           "kernel": "run-time compiled for this rule set's shape (bg_wm_jit.cc, "
+                     "hiprtc, %.2f s on a background thread); ahead-of-time "
+                     "kernel beside" % jit_s,
+           "ahead_of_time": {"ms_per_step": round(aot_h, 4),
+                             "slots_2k_ms_per_step": round(aot2k, 4),
+                             "same_gates": bool(parity and parity_h)},
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),

@@ -23,6 +23,7 @@ BG_PATH_ACL_BV = 32
 BG_PATH_ACL_LDS = 64
 BG_PATH_LPM_DIR24 = 128
 BG_PATH_PIPE_NO_RING = 256
+BG_PATH_WM_NO_JIT = 512
 KEY_BYTES = 64
 
 
@@ -108,6 +109,9 @@ _SIGS = {
     "bg_wm_classify": (_int, [_vp, _vp, _sz, _sz, _u16, _vp, _vp]),
     "bg_wm_process_host": (_int, [_vp, _vp, _sz, _u16, _vp, _vp]),
     "bg_wm_table_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
+    "bg_wm_jit_wait": (_int, [_vp, _int, _int]),
+    "bg_wm_jit_source": (_int, [_vp, _int, _vp, _sz, C.POINTER(_sz)]),
+    "bg_wm_jit_check": (_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "bg_cksum": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp, _vp, _vp]),
     "bg_cksum_process_host": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp,
                                      _vp, _vp]),

@@ -16,6 +16,7 @@
 
 #include "../../include/bessgpu.h"
 #include "bg_internal.h"
+#include "bg_wm_jit.h"
 #include "bg_kernels.h"
 #include "bg_launch.h"
 #include "bg_table.h"
@@ -950,6 +951,9 @@ struct WmTupleH {
 struct WmImage : DevImage {
   WmArgs a{};
   bool no_tags = false;  // BG_PATH_WM_NO_TAGS when it was built
+  // the kernels compiled at run time for this image's shape (bg_wm_jit.cc;
+  // shared with every image of the same shape), or null
+  std::shared_ptr<WmJit> jit;
 };
 
 struct bg_wm {
@@ -1302,6 +1306,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   img->no_tags = no_tags;
   img->a = wm->host_a;
   img->a.t.base = img->d;
+  img->jit = wm_jit_request(img->a, make_plan(wm->dfields, false, 0), wm->kw);
   wm->dev.publish(device, img.release());
   return 0;
 }
@@ -1335,7 +1340,70 @@ static int wm_launch(bg_wm *wm, WmImage *img, const void *d_frames, size_t strid
   a.fp = make_plan(wm->dfields, false, shift);
   a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
   img->used_on(s);
+  hipError_t e;
+  if (!a.ab_phase && wm_jit_launch(img->jit.get(), a, img->device, num_cus(img->device), s, &e)) {
+    HIP_TRY(e);
+    return 0;
+  }
   HIP_TRY(launch_wm(a, num_cus(img->device), s));
+  return 0;
+}
+
+int bg_wm_jit_wait(bg_wm *wm, int device, int timeout_ms) {
+  int r = set_device(device);
+  if (r) return r;
+  WmImage *img;
+  r = wm_image(wm, device, nullptr, &img);
+  if (r) return r;
+  return wm_jit_wait(img->jit.get(), timeout_ms);
+}
+
+int bg_wm_jit_check(bg_wm *wm, char *log, size_t len, size_t *code_bytes) {
+  std::lock_guard<std::mutex> lk(wm->mu);
+  const uint64_t ver = wm->version.load(std::memory_order_acquire);
+  if (wm->host_version != ver || wm->host_no_tags) {
+    if (int r = wm_build_host(wm, false)) return r;
+    wm->host_version = ver;
+    wm->host_no_tags = false;
+  }
+  std::string lg;
+  size_t cb = 0;
+  const int r = wm_jit_compile_now(wm->host_a, make_plan(wm->dfields, false, 0), wm->kw, &lg, &cb);
+  if (code_bytes) *code_bytes = cb;
+  if (log && len) {
+    const size_t n = std::min(len - 1, lg.size());
+    memcpy(log, lg.data(), n);
+    log[n] = 0;
+  }
+  return r;
+}
+
+int bg_wm_jit_source(bg_wm *wm, int device, char *buf, size_t len, size_t *need) {
+  std::string src;
+  if (device < 0) {  // the host image's: no device
+    std::lock_guard<std::mutex> lk(wm->mu);
+    const uint64_t ver = wm->version.load(std::memory_order_acquire);
+    if (wm->host_version != ver || wm->host_no_tags) {
+      if (int r = wm_build_host(wm, false)) return r;
+      wm->host_version = ver;
+      wm->host_no_tags = false;
+    }
+    src = wm_jit_gen(wm->host_a, make_plan(wm->dfields, false, 0), wm->kw);
+  } else {
+    int r = set_device(device);
+    if (r) return r;
+    WmImage *img;
+    r = wm_image(wm, device, nullptr, &img);
+    if (r) return r;
+    src = wm_jit_source(img->jit.get());
+  }
+  if (need) *need = src.size() + 1;
+  if (src.empty()) return fail(ENOENT, "this table has no run-time compiled kernel");
+  if (buf && len) {
+    const size_t n = std::min(len - 1, src.size());
+    memcpy(buf, src.data(), n);
+    buf[n] = 0;
+  }
   return 0;
 }
 

@@ -2,8 +2,10 @@
 #ifndef BESS_AMD_BG_KERNELS_H_
 #define BESS_AMD_BG_KERNELS_H_
 
+#ifndef __HIPCC_RTC__  // hiprtc (bg_wm_jit.cc) has its own
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "bg_table.h"
 
@@ -129,6 +131,18 @@ struct WmArgs {
   uint64_t doff[kMaxDirect];   // the table's byte offset in the image
   uint32_t ab_phase, pad2;  // A/B build only: stop after a phase (timing)
 };
+
+// WildcardMatch tag-word kernels (bg_wm_body.h): one 1024-thread workgroup
+// per CU; LDS = the tag words, the tuple masks, and per wave best[64] plus
+// a queue of kWmQueue entries
+constexpr int kWmBlock = 1024;
+constexpr int kWmWaves = kWmBlock / 64;
+constexpr uint32_t kWmQueue = 256;
+constexpr uint32_t kWmWaveLds = 64 * 8 + kWmQueue * 4;
+BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
+  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 +
+         (uint64_t)kWmWaves * kWmWaveLds;
+}
 
 struct CkArgs {
   uint8_t *frames;
@@ -349,6 +363,7 @@ constexpr int kRingBlock = 256;
 constexpr int kRingLaneWords = 16;
 constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
 
+#ifndef __HIPCC_RTC__  // host launchers: not part of a run-time compile
 // Launchers (grid sizing from the device's CU count). Return hipSuccess or
 // the launch error.
 hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s);
@@ -375,6 +390,7 @@ hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword
+#endif
 bool fits_nch2(const FieldPlan &fp);
 
 }  // namespace bg

@@ -5,7 +5,9 @@
 #ifndef BESS_AMD_BG_KEYS_DEV_H_
 #define BESS_AMD_BG_KEYS_DEV_H_
 
+#ifndef __HIPCC_RTC__  // hiprtc (bg_wm_jit.cc) has its own
 #include <hip/hip_runtime.h>
+#endif
 
 #include "bg_kernels.h"
 

@@ -33,7 +33,8 @@ constexpr uint32_t kPathAclBv = 32;     // ACL: per-dimension bit vectors
 constexpr uint32_t kPathAclLds = 64;    // ACL: the rule scan from LDS (not the tree)
 constexpr uint32_t kPathLpmDir24 = 128;  // IPLookup: DIR-24-8 (not DIR-16-8-8)
 constexpr uint32_t kPathPipeNoRing = 256;  // pipes launch per slot (no ring)
-constexpr uint32_t kPathAll = 511;
+constexpr uint32_t kPathWmNoJit = 512;   // WildcardMatch: never the run-time compiled kernel
+constexpr uint32_t kPathAll = 1023;
 
 uint32_t path_flags();
 

@@ -20,8 +20,20 @@
 #ifndef BESS_AMD_BG_TABLE_H_
 #define BESS_AMD_BG_TABLE_H_
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#else  // hiprtc (bg_wm_jit.cc): its runtime header declares these in a namespace
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint16_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+using __hip_internal::uint8_t;
+#ifndef offsetof
+#define offsetof(t, m) __builtin_offsetof(t, m)
+#endif
+#endif
 
 #ifdef __HIPCC__
 #define BG_HD __host__ __device__ __forceinline__

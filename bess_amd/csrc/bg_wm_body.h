@@ -1,0 +1,423 @@
+// bg_wm_body.h -- the WildcardMatch tag-word kernel body (WildcardMatch::
+// ProcessBatch, core/modules/wildcard_match.cc:159-203, LookupEntry
+// 136-157) for tables whose tag words fit in LDS, written over a `Spec`
+// that supplies the table's tuple data:
+//
+//   * WmRuntimeSpec (below): read per tile from the kernel arguments --
+//     the kernel bg_wm.hip compiles ahead of time for any table;
+//   * a generated spec (bg_wm_jit.cc): the same data as compile-time
+//     constants -- hashed-tuple set, per-tuple covered dwords, mask dwords
+//     and seeds, the direct tuples' byte specs and the key's byte-permute
+//     plan -- compiled at run time (hiprtc) for one rule-set shape, so the
+//     per-tuple branches, scalar loads and window-index moves fold away.
+//
+// Spec interface (static __device__ members):
+//   uint32_t hashed(a)               bit tu: tuple tu is probed by hash
+//   uint32_t hash<KW>(k, tu, a)      tuple tu's wm_hash of key k (bg_table.h)
+//   uint32_t ndirect(a)              direct tuples (<= kMaxDirect)
+//   uint32_t dtu(a, d), dspec(a, d)  direct tuple d's tuple index, byte spec
+//   void key<KW, NCH>(w, a, k)       the packet key from its header window
+//
+// This header is compiled by hipcc (bg_wm.hip) and by hiprtc (the text is
+// embedded in libbessgpu.so, bg_wm_jit.cc), so it includes nothing beyond
+// the kernel headers. Lane = packet, 64 packets per wave tile:
+//
+//   1. header window -> raw key (WildcardMatch's unmasked 8-byte loads,
+//      P4), the next tile's window in flight;
+//   2. per tuple (wave-uniform): key & mask, hash, both tag words from
+//      LDS (all tuples' reads issued before any is used);
+//   3. every (packet, tuple) whose buckets hold the packet's fingerprint
+//      goes into a per-wave LDS queue as (first bucket, lane, tuple,
+//      fingerprint) -- the second bucket follows from the first and the
+//      fingerprint (wm_alt) -- at a scalar base + mbcnt of the tuple's
+//      match mask, so the key checks run on dense lanes instead of on
+//      whichever lanes matched;
+//   4. the queue (<= 256 entries; more go in further rounds) is checked
+//      with up to four entries per lane, all their loads in flight at
+//      once: a lane loads each entry's slot key and value from L2 and the
+//      owning lane's key comes over with ds_bpermute; a hit is folded into
+//      the packet's best with a 64-bit LDS atomic max over (priority,
+//      tuple, gate) -- the highest priority wins and an equal priority
+//      goes to the later tuple, LookupEntry's '>=' (P5);
+//   5. gate = the best's gate, or the default gate when nothing matched.
+//
+// One 1024-thread workgroup per CU (tags <= 128 KB + 1.5 KB per wave).
+#ifndef BESS_AMD_BG_WM_BODY_H_
+#define BESS_AMD_BG_WM_BODY_H_
+
+#include "bg_kernels.h"
+#include "bg_keys_dev.h"
+
+namespace bg {
+namespace {
+
+constexpr int kWaves = kWmWaves;
+constexpr uint32_t kQueue = kWmQueue;   // entries per wave per round
+constexpr int kPerLane = kQueue / 64;   // entries a lane checks per round
+constexpr uint32_t kWaveLds = kWmWaveLds;
+
+// The table data from the kernel arguments, read per tile through the
+// laundered kernarg pointer (hoisted, the per-tuple data of 8 tuples would
+// take more scalar registers than the kernel has)
+struct WmRuntimeSpec {
+  __device__ static uint32_t hashed(const WmArgs &a) {
+    return tuple_words(a, offsetof(WmArgs, hmask))[0];
+  }
+  template <int KW>
+  __device__ static uint32_t hash(const uint64_t (&k)[KW], int tu, const WmArgs &a) {
+    return wm_tuple_hash<KW>(k, tuple_masks(a), tu, a);
+  }
+  __device__ static uint32_t ndirect(const WmArgs &a) {
+    return tuple_words(a, offsetof(WmArgs, ndirect))[0];
+  }
+  __device__ static uint32_t dtu(const WmArgs &a, int d) {
+    return tuple_words(a, offsetof(WmArgs, dtu))[d];
+  }
+  __device__ static uint32_t dspec(const WmArgs &a, int d) {
+    return tuple_words(a, offsetof(WmArgs, dspec))[d];
+  }
+  template <int KW, int NCH>
+  __device__ static void key(const uint32_t (&w)[NCH * 4 + 2], const WmArgs &a,
+                             uint64_t (&k)[KW]) {
+    extract_key<KW, NCH>(w, a.fp, k);
+  }
+};
+
+// one step of wm_hash (bg_table.h) over masked key dword x
+__device__ __forceinline__ uint32_t wm_step(uint32_t h, uint32_t x) {
+  h = (h ^ x) * 0x9E3779B1u;
+  return h ^ (h >> 15);
+}
+__device__ __forceinline__ uint32_t wm_final(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  return h ^ (h >> 13);
+}
+
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
+// Queue entry: bucket (bits 0-14; tags <= 128 KB, so < 2^15 buckets) |
+// lane << 15 | tuple << 21 | fingerprint << 24.
+__device__ __forceinline__ uint32_t entry_lane(uint32_t e) { return (e >> 15) & 63u; }
+__device__ __forceinline__ uint32_t entry_tuple(uint32_t e) { return (e >> 21) & 7u; }
+
+// The owning lane's key for queue entry e (every lane takes part in the
+// permutes)
+template <int KW>
+__device__ __forceinline__ void owner_key(uint32_t e, const uint64_t (&k)[KW],
+                                          uint64_t (&kk)[KW]) {
+  const int pl = (int)entry_lane(e);
+#pragma unroll
+  for (int j = 0; j < KW; j++) {
+    const uint32_t lo = shfl32((uint32_t)k[j], pl);
+    const uint32_t hi = shfl32((uint32_t)(k[j] >> 32), pl);
+    kk[j] = (uint64_t)hi << 32 | lo;
+  }
+}
+
+// fold a hit of entry e (slot value v) into its packet's best
+__device__ __forceinline__ void wm_fold(uint64_t *best, uint32_t e, uint64_t v) {
+  // (priority as unsigned order, valid bit, tuple, gate)
+  const uint64_t comb = ((uint64_t)((uint32_t)v ^ 0x80000000u) << 32) |
+                        (1u << 19) | (entry_tuple(e) << 16) |
+                        ((uint32_t)(v >> 32) & 0xFFFFu);
+  atomicMax(reinterpret_cast<unsigned long long *>(best + entry_lane(e)),
+            (unsigned long long)comb);
+}
+
+template <int KW>
+__device__ __forceinline__ bool wm_hit(const uint64_t *mlds, uint32_t e,
+                                       uint64_t v, const uint64_t (&sk)[KW],
+                                       const uint64_t (&kk)[KW]) {
+  const uint32_t tu = entry_tuple(e);
+  bool hit = (uint32_t)(v >> 48) == tu;
+#pragma unroll
+  for (int j = 0; j < KW; j++) hit &= sk[j] == (kk[j] & mlds[tu * KW + j]);
+  return hit;
+}
+
+// fingerprint matches of entry e's tag in bucket b: bit 7 of each byte
+__device__ __forceinline__ uint32_t bucket_matches(const uint32_t *tags, uint32_t b,
+                                                   uint32_t e) {
+  return zero_bytes(tags[b] ^ __builtin_amdgcn_perm(0u, e >> 24, 0u));
+}
+
+// Entry e = (packet, tuple, first bucket b1, fingerprint); its second bucket
+// is b1 ^ wm_alt(fingerprint). Candidate slots: the matches of b1 (z1),
+// then those of b2 (z2); the next candidate's slot index.
+__device__ __forceinline__ uint32_t next_slot(uint32_t e, uint32_t lg, uint32_t z1,
+                                              uint32_t z2) {
+  const uint32_t b1 = e & 0x7FFFu;
+  const uint32_t b = z1 ? b1 : b1 ^ wm_alt(e >> 24, lg);
+  return b * kSlots + (__builtin_ctz(z1 ? z1 : z2) >> 3);
+}
+
+// Check queue entries [0, m), m <= kQueue: lane l takes entries l, l + 64,
+// ... Each entry is a (packet, tuple) whose tag words hold the packet's
+// fingerprint in one of its two buckets: the lane re-reads both tag words,
+// and the first candidate slot's key and value loads of every entry are
+// issued before any is compared (one L2 round trip). An entry whose first
+// candidate is not the key (a fingerprint collision) tries the rest (rare).
+template <int KW>
+__device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
+                                         const uint64_t *mlds, uint64_t *best,
+                                         const uint32_t *q, uint32_t m, int lane,
+                                         uint32_t lg, const uint64_t (&k)[KW]) {
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
+  uint32_t e[kPerLane], z1[kPerLane], z2[kPerLane];
+  uint64_t v[kPerLane], sk[kPerLane][KW], kk[kPerLane][KW];
+#pragma unroll
+  for (int r = 0; r < kPerLane; r++) {
+    const uint32_t i = (uint32_t)lane + 64u * r;
+    e[r] = z1[r] = z2[r] = 0;
+    v[r] = 0;
+#pragma unroll
+    for (int j = 0; j < KW; j++) sk[r][j] = kk[r][j] = 0;
+    if (64u * r < m) {  // wave-uniform: the permutes need every lane
+      e[r] = q[i];
+      owner_key<KW>(e[r], k, kk[r]);
+      if (i < m) {
+        const uint32_t b1 = e[r] & 0x7FFFu;
+        z1[r] = bucket_matches(tags, b1, e[r]);
+        z2[r] = bucket_matches(tags, b1 ^ wm_alt(e[r] >> 24, lg), e[r]);
+        const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
+#ifdef BG_AB  // phase timing: checks without their L2 loads
+        if (a.ab_phase == 3) continue;
+#endif
+        v[r] = vals[slot];
+#pragma unroll
+        for (int j = 0; j < KW; j++) sk[r][j] = keys[(uint64_t)slot * KW + j];
+      }
+    }
+  }
+  bool more = false;
+#pragma unroll
+  for (int r = 0; r < kPerLane; r++) {
+    const uint32_t i = (uint32_t)lane + 64u * r;
+    if (i < m) {
+      if (wm_hit<KW>(mlds, e[r], v[r], sk[r], kk[r])) {
+        wm_fold(best, e[r], v[r]);
+        z1[r] = z2[r] = 0;
+      } else if (z1[r]) {  // the candidates not tried yet
+        z1[r] &= z1[r] - 1;
+      } else {
+        z2[r] &= z2[r] - 1;
+      }
+    } else {
+      z1[r] = z2[r] = 0;
+    }
+    more |= (z1[r] | z2[r]) != 0;
+  }
+  if (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform, rare
+#pragma unroll
+    for (int r = 0; r < kPerLane; r++) {
+      while (z1[r] | z2[r]) {
+        const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
+        if (z1[r])
+          z1[r] &= z1[r] - 1;
+        else
+          z2[r] &= z2[r] - 1;
+        const uint64_t vv = vals[slot];
+        uint64_t s2[KW];
+#pragma unroll
+        for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * KW + j];
+        if (wm_hit<KW>(mlds, e[r], vv, s2, kk[r])) {
+          wm_fold(best, e[r], vv);
+          z1[r] = z2[r] = 0;
+        }
+      }
+    }
+  }
+}
+
+// bit 7 of each byte of x that is zero, OR-ed over two words (the SWAR
+// test of zero_bytes; only the any-match result is exact)
+__device__ __forceinline__ uint32_t zero_bytes2(uint32_t x, uint32_t y) {
+  return (((x - 0x01010101u) & ~x) | ((y - 0x01010101u) & ~y)) & 0x80808080u;
+}
+
+// Dense 64 B header slab (PAIR): the two 16-byte window chunks of a slot
+// are loaded by a lane pair -- load 0 of lanes 2m, 2m+1 holds chunks q0,
+// q0+1 of slot m, load 1 those of slot 32+m -- so each load instruction
+// covers 32 B of each of 32 adjacent slots (half the cache lines per
+// instruction of one 16 B chunk per lane at a 64 B stride). One DPP swap
+// per dword completes the windows: lane 2m takes slot m, lane 2m+1 slot
+// 32+m.
+__device__ __forceinline__ uint64_t pair_slot(int lane) {
+  return (lane & 1) ? 32u + (lane >> 1) : (uint32_t)(lane >> 1);
+}
+
+__device__ __forceinline__ void load_pair(const uint8_t *__restrict__ frames,
+                                          uint64_t n, uint64_t p0, int lane,
+                                          uint32_t win_lo, uint32_t (&r)[8]) {
+  const uint64_t s0 = p0 + (lane >> 1), s1 = s0 + 32;
+  const uint32_t off = win_lo + (lane & 1) * 16;
+  uint4 x = make_uint4(0, 0, 0, 0), y = x;
+  if (s0 < n) x = ld_stream(reinterpret_cast<const uint4 *>(frames + s0 * 64 + off));
+  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(frames + s1 * 64 + off));
+  r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+  r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
+}
+
+template <int NCH>
+__device__ __forceinline__ void pair_window(const uint32_t (&r)[8], int lane,
+                                            uint32_t (&w)[NCH * 4 + 2]) {
+  static_assert(NCH == 2, "pair loads carry two chunks");
+  const bool odd = lane & 1;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    const uint32_t src = odd ? r[d] : r[4 + d];
+    // quad_perm [1,0,3,2]: swap with the neighbouring lane
+    const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)src, 0xB1, 0xF, 0xF, false);
+    w[d] = odd ? recv : r[d];
+    w[4 + d] = odd ? r[4 + d] : recv;
+  }
+  w[8] = 0;
+  w[9] = 0;
+}
+
+template <class Spec, int KW, int NCH, int PAIR>
+__device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
+  {  // stage the tag words
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.t.base);
+    uint4 *dst = reinterpret_cast<uint4 *>(lds);
+    for (uint32_t i = threadIdx.x; i < tag_bytes / 16; i += kWmBlock) dst[i] = src[i];
+  }
+  uint64_t *mlds = reinterpret_cast<uint64_t *>(lds + tag_bytes);
+  {
+    const kconst_u64 tm = tuple_masks(a);
+    if (threadIdx.x < kMaxTuples * KW)
+      mlds[threadIdx.x] = tm[(threadIdx.x / KW) * kMaxKeyWords + threadIdx.x % KW];
+  }
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + wid * kWaveLds;
+  uint64_t *best = reinterpret_cast<uint64_t *>(wl);
+  uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
+  best[lane] = 0;
+  __syncthreads();
+
+  const uint32_t lg = 31 - __builtin_clz(a.t.nbp);
+  const uint64_t ntiles = (a.n + 63) / 64;
+  const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  uint32_t wn[PAIR ? 8 : NCH * 4 + 2];
+  if constexpr (PAIR) {
+    if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, wn);
+  } else {
+    if (t < ntiles && t * 64 + lane < a.n)
+      load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
+  }
+  for (; t < ntiles; t += nw) {
+    const uint64_t idx = t * 64 + (PAIR ? pair_slot(lane) : (uint64_t)lane);
+    const bool live = idx < a.n;
+    uint32_t w[NCH * 4 + 2];
+    if constexpr (PAIR) {
+      pair_window<NCH>(wn, lane, w);
+      if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, wn);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
+      const uint64_t nidx = (t + nw) * 64 + lane;
+      if (t + nw < ntiles && nidx < a.n)
+        load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
+    }
+    uint64_t k[KW];
+    Spec::template key<KW, NCH>(w, a, k);
+    // direct tuples: one value read each, issued now, folded at the end
+    const uint32_t ndir = Spec::ndirect(a);
+    uint64_t dv[kMaxDirect];
+#pragma unroll
+    for (int d = 0; d < kMaxDirect; d++) {
+      dv[d] = ~0ull;
+      if ((uint32_t)d < ndir && live) {
+        const uint64_t off =
+            reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
+                tuple_words(a, offsetof(WmArgs, doff)))[d];
+        dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)
+            [direct_index_k<KW>(k, Spec::dspec(a, d))];
+      }
+    }
+#ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
+    if (a.ab_phase == 1) {
+      if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
+      continue;
+    }
+#endif
+    const uint32_t hmask = Spec::hashed(a);
+
+    // A. every hashed tuple's probe: both tag words from LDS (all reads in
+    // flight before any is used); zz[tu] != 0 iff a bucket holds the
+    // packet's fingerprint, ent[tu] its queue entry
+    uint32_t zz[kMaxTuples], ent[kMaxTuples];
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      zz[tu] = 0;
+      ent[tu] = 0;
+      if ((hmask >> tu) & 1u) {  // wave-uniform (a scalar test, or a constant)
+        const Probe p = wm_probe(Spec::template hash<KW>(k, tu, a), lg);
+        const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
+        zz[tu] = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
+        ent[tu] = p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24);
+      }
+    }
+    // B/C. one queue entry per (packet, tuple) with a fingerprint match,
+    // tuple-major: the wave's mask of matching lanes gives each lane its
+    // position (a scalar base + mbcnt) and the base advances by the mask's
+    // popcount. Usually the tile's entries fit one queue; more go in
+    // further rounds of kQueue.
+    const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
+    uint64_t mk[kMaxTuples];
+    uint32_t total = 0;
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      mk[tu] = __builtin_amdgcn_ballot_w64(zz[tu] != 0) & livemask;
+      total += (uint32_t)__popcll(mk[tu]);
+    }
+    for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
+      uint32_t base = 0;
+#pragma unroll
+      for (int tu = 0; tu < kMaxTuples; tu++) {
+        const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
+        const bool mine = live && zz[tu] != 0;
+        if (total <= kQueue) {  // wave-uniform: one round, no window test
+          if (mine) q[pos] = ent[tu];
+        } else if (mine && pos - r0 < kQueue) {
+          q[pos - r0] = ent[tu];
+        }
+        base += (uint32_t)__popcll(mk[tu]);
+      }
+#ifdef BG_AB  // phase timing: + hashes, tag reads and the queue writes
+      if (a.ab_phase == 2) break;
+#endif
+      lds_fence();
+      const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
+      wm_check<KW>(a, tags, mlds, best, q, m, lane, lg, k);
+      lds_fence();  // the queue is rewritten by the next round
+    }
+    lds_fence();
+    uint64_t bb = best[lane];
+    best[lane] = 0;
+#pragma unroll
+    for (int d = 0; d < kMaxDirect; d++) {
+      const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFu;
+      if ((uint32_t)(dv[d] >> 48) == tu) {  // same order as wm_fold
+        const uint64_t comb = ((uint64_t)((uint32_t)dv[d] ^ 0x80000000u) << 32) |
+                              (1u << 19) | (tu << 16) | ((uint32_t)(dv[d] >> 32) & 0xFFFFu);
+        bb = comb > bb ? comb : bb;
+      }
+    }
+    if (live) a.gates[idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
+  }
+}
+
+}  // namespace
+}  // namespace bg
+
+#endif  // BESS_AMD_BG_WM_BODY_H_

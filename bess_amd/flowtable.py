@@ -309,6 +309,26 @@ class WmTable:
         # 0 L2/MALL, 1 table in LDS, 2 key filter in LDS, 3 tag words in LDS
         return b.value, l.value & 0xFF
 
+    def jit_wait(self, device=0, timeout_ms=120000):
+        """Block until the run-time compiled kernel of the current rules is
+        ready on `device` (bg_wm_jit_wait)."""
+        check(lib().bg_wm_jit_wait(self.h, device, timeout_ms))
+
+    def jit_source(self, device=0):
+        need = C.c_size_t()
+        check(lib().bg_wm_jit_source(self.h, device, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        check(lib().bg_wm_jit_source(self.h, device, buf, need.value, C.byref(need)))
+        return buf.value.decode()
+
+    def jit_check(self):
+        """Compile the specialised kernel of the current rules on this thread
+        (no device): (rc, code bytes, compiler log)."""
+        log = C.create_string_buffer(1 << 16)
+        cb = C.c_size_t()
+        rc = lib().bg_wm_jit_check(self.h, log, len(log), C.byref(cb))
+        return rc, cb.value, log.value.decode(errors="replace")
+
     def direct_tuples(self):
         """tuples of the device image read by index (one- or two-byte masks)"""
         b, l = C.c_uint64(), C.c_int()

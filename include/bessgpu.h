@@ -204,6 +204,21 @@ int bg_wm_classify_window(bg_wm *wm, const void *d_win, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,
                           uint16_t *d_gates, bg_stream_t stream);
 void bg_wm_window(const bg_wm *wm, int *lo, int *hi);
+/* Run-time compiled kernels (bess_amd/csrc/bg_wm_jit.cc). A tag-word image's
+ * tuple data (masks, seeds, direct tuples) and its key plan are compiled
+ * into a specialised kernel with hiprtc on a background thread; launches use
+ * it once ready and the ahead-of-time kernel until then (same results).
+ * bg_wm_jit_wait syncs the table on `device` and blocks until that kernel
+ * is ready: 0, -ETIMEDOUT, -ENOEXEC (compile failed; the ahead-of-time kernel
+ * stays in use) or -ENOENT (the image has no tag words: nothing to compile).
+ * bg_wm_jit_source copies the generated source (*need: bytes incl. NUL;
+ * device < 0: the source for the current rules' host image, no device). */
+int bg_wm_jit_wait(bg_wm *wm, int device, int timeout_ms);
+int bg_wm_jit_source(bg_wm *wm, int device, char *buf, size_t len, size_t *need);
+/* Build the host image of the current rules and compile its specialised
+ * kernel on the calling thread; no device needed (0, -ENOENT: no tag-word
+ * image, -ENOEXEC: compile failed, log in `log`). */
+int bg_wm_jit_check(bg_wm *wm, char *log, size_t len, size_t *code_bytes);
 
 /* ---- IPChecksum / L4Checksum ------------------------------------------ */
 /* mode: BG_CK_IP, BG_CK_L4 or both (= IPChecksum -> L4Checksum pipeline:
@@ -236,6 +251,8 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_ACL_LDS 64  /* ACL: rule scan from LDS (not the decision tree) */
 #define BG_PATH_LPM_DIR24 128 /* IPLookup: DIR-24-8 tables (not DIR-16-8-8) */
 #define BG_PATH_PIPE_NO_RING 256 /* pipes launch per slot (not via a ring) */
+#define BG_PATH_WM_NO_JIT 512 /* WildcardMatch: the ahead-of-time kernel, never the
+                                run-time compiled one (bg_wm_jit_wait) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */

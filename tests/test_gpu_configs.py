@@ -133,8 +133,10 @@ def test_c5_8_partitions_attached(c5):
 
 
 # ------------------------------------------------------------------- C4
-@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_TAGS])
+@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_TAGS])
 def test_c4_imix_2k_slots(flags):
+    """flags 0: the run-time compiled kernel (bg_wm_jit.cc) once ready;
+    BG_PATH_WM_NO_JIT the ahead-of-time one; BG_PATH_WM_NO_TAGS the key filter"""
     n = 1 << 18
     rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n, stride=2048)
     assert set(np.unique(flen)) == {60, 590, 1514}
@@ -142,12 +144,14 @@ def test_c4_imix_2k_slots(flags):
     for k, m, p, g in zip(rk, rm, prio, gates):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
     assert t.num_tuples() == 8
+    if flags == 0:
+        t.jit_wait()
     d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
     with LB.kernel_paths(flags):
         t.classify(to_dev(frames), 2048, n, 8192, d_g)
         torch.cuda.synchronize()
         in_lds = t.table_info()[1]
-    assert in_lds == (2 if flags else 3)  # key filter / tag words in LDS
+    assert in_lds == (2 if flags & LB.BG_PATH_WM_NO_TAGS else 3)  # key filter / tag words
     L = O.lib()
     ow = L.or_wm_new()
     for off, size in P.FIVE_TUPLE:
@@ -191,10 +195,14 @@ def test_c4_header_slab_full_size():
     h = to_dev(np.ascontiguousarray(frames[:, :64])).repeat(rep)
     del frames
     d_g = torch.zeros(n0 * rep, dtype=torch.int16, device="cuda")
-    t.classify(h, 64, n0 * rep, 8192, d_g)
-    torch.cuda.synchronize()
-    assert t.table_info()[1] == 3 and t.direct_tuples() == 2
-    assert (d_g.cpu().numpy().view(np.uint16).reshape(rep, n0) == want).all()
+    t.jit_wait()
+    for flags in (0, LB.BG_PATH_WM_NO_JIT):  # run-time compiled, ahead-of-time
+        d_g.zero_()
+        with LB.kernel_paths(flags):
+            t.classify(h, 64, n0 * rep, 8192, d_g)
+            torch.cuda.synchronize()
+        assert t.table_info()[1] == 3 and t.direct_tuples() == 2
+        assert (d_g.cpu().numpy().view(np.uint16).reshape(rep, n0) == want).all(), flags
 
 
 # ------------------------------------------- concurrent workers, one module

@@ -3,6 +3,7 @@
 Marked gpu: runs on a real MI355X. Every comparison is bit-exact (gates,
 checksum words, whole frames after in-place checksum writes).
 """
+import errno
 import ctypes as C
 
 import numpy as np
@@ -202,16 +203,31 @@ def test_em_sharded_build_matches_single(dev):
 def classify_all_paths_wm(t, d_frames, stride, n, default_gate, dev, tags):
     """classify_all_paths with BG_PATH_WM_NO_TAGS kept on (tags == 0)"""
     keep = 0 if tags else LB.BG_PATH_WM_NO_TAGS
+    paths = TABLE_PATHS
+    if tags and wm_jit_ready(t):  # the run-time compiled kernel, then without it
+        paths = TABLE_PATHS + (LB.BG_PATH_WM_NO_JIT,)
     outs = []
-    for flags in TABLE_PATHS:
+    for flags in paths:
         with LB.kernel_paths(flags | keep):
             d_g = torch.zeros(n, dtype=torch.int16, device=dev)
             t.classify(d_frames, stride, n, default_gate, d_g)
             torch.cuda.synchronize()
         outs.append(d_g.cpu().numpy().view(np.uint16))
-    for o, flags in zip(outs[1:], TABLE_PATHS[1:]):
+    for o, flags in zip(outs[1:], paths[1:]):
         assert (o == outs[0]).all(), flags
     return outs[0]
+
+
+def wm_jit_ready(t, dev=0):
+    """Wait for the table's run-time compiled kernel (bg_wm_jit_wait): True
+    once it serves launches, False for an image without tag words."""
+    try:
+        t.jit_wait(dev)
+    except LB.BessGpuError as e:
+        if e.code == errno.ENOENT:
+            return False
+        raise
+    return True
 
 
 def oracle_wm(fields, rkeys, rmasks, prio, gates):
