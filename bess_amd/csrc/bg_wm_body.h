@@ -160,17 +160,19 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t e, uint32_t lg, uint32_t 
 // and the first candidate slot's key and value loads of every entry are
 // issued before any is compared (one L2 round trip). An entry whose first
 // candidate is not the key (a fingerprint collision) tries the rest (rare).
-template <int KW>
-__device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
-                                         const uint64_t *mlds, uint64_t *best,
-                                         const uint32_t *q, uint32_t m, int lane,
-                                         uint32_t lg, const uint64_t (&k)[KW]) {
+// R entries per lane (m <= 64 R); the usual tile has fewer than 64
+// entries and takes R = 1
+template <int KW, int R>
+__device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags,
+                                           const uint64_t *mlds, uint64_t *best,
+                                           const uint32_t *q, uint32_t m, int lane,
+                                           uint32_t lg, const uint64_t (&k)[KW]) {
   const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
-  uint32_t e[kPerLane], z1[kPerLane], z2[kPerLane];
-  uint64_t v[kPerLane], sk[kPerLane][KW], kk[kPerLane][KW];
+  uint32_t e[R], z1[R], z2[R];
+  uint64_t v[R], sk[R][KW], kk[R][KW];
 #pragma unroll
-  for (int r = 0; r < kPerLane; r++) {
+  for (int r = 0; r < R; r++) {
     const uint32_t i = (uint32_t)lane + 64u * r;
     e[r] = z1[r] = z2[r] = 0;
     v[r] = 0;
@@ -195,7 +197,7 @@ __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
   }
   bool more = false;
 #pragma unroll
-  for (int r = 0; r < kPerLane; r++) {
+  for (int r = 0; r < R; r++) {
     const uint32_t i = (uint32_t)lane + 64u * r;
     if (i < m) {
       if (wm_hit<KW>(mlds, e[r], v[r], sk[r], kk[r])) {
@@ -213,7 +215,7 @@ __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
   }
   if (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform, rare
 #pragma unroll
-    for (int r = 0; r < kPerLane; r++) {
+    for (int r = 0; r < R; r++) {
       while (z1[r] | z2[r]) {
         const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
         if (z1[r])
@@ -231,6 +233,17 @@ __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
       }
     }
   }
+}
+
+template <int KW>
+__device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
+                                         const uint64_t *mlds, uint64_t *best,
+                                         const uint32_t *q, uint32_t m, int lane,
+                                         uint32_t lg, const uint64_t (&k)[KW]) {
+  if (m <= 64)  // wave-uniform
+    wm_check_r<KW, 1>(a, tags, mlds, best, q, m, lane, lg, k);
+  else
+    wm_check_r<KW, kPerLane>(a, tags, mlds, best, q, m, lane, lg, k);
 }
 
 // bit 7 of each byte of x that is zero, OR-ed over two words (the SWAR

@@ -44,6 +44,7 @@ class GpuModule : public Module {
     uint64_t seen = 0;                 // submits at the task's last visit
     std::atomic<bool> in_call{false};   // the owner is in ProcessBatch
     std::atomic<bool> draining{false};  // the task is emitting this pipe
+    int win_lo = 0;                     // first data byte the pipe gathers
   };
 
  public:
@@ -213,12 +214,14 @@ class GpuModule : public Module {
     }
     uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
     uint16_t lens[bess::PacketBatch::kMaxBurst] = {};
-    // the packets' mbuf lines in flight together (head_data() reads them)
+    // the packets' mbuf lines in flight together (head_data() reads them),
+    // then, as each arrives, the line of its data the pipe gathers from
     for (int i = 0; i < n; i++) __builtin_prefetch(batch->pkts()[i]);
     for (int i = 0; i < n; i++) {
       bess::Packet *pkt = batch->pkts()[i];
       heads[i] = pkt->head_data<uint8_t *>();
       lens[i] = pkt->data_len();
+      __builtin_prefetch(heads[i] + l.win_lo);
     }
     const bg_ctx c = CallCtx(ctx);
     if (bg_pipe_submit(p, &c, heads, lens, reinterpret_cast<void *const *>(batch->pkts()),
@@ -256,6 +259,9 @@ class GpuModule : public Module {
     bg_pipe *p = nullptr;
     if (nd <= 0 || bg_pipe_create(m_, wid % nd, pipe_batch_, pipe_depth_, 0, &p) < 0)
       return nullptr;
+    int lo = 0, hi = 0;
+    size_t stride = 0;
+    if (bg_pipe_window(p, &lo, &hi, &stride) == 0 && lo > 0) lanes_[wid].win_lo = lo;
     lanes_[wid].pipe.store(p, std::memory_order_release);
     return p;
   }
