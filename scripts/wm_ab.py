@@ -29,6 +29,11 @@ def main():
     for k, m, p, g in zip(rk, rm, prio, gates):
         t.add(k.tobytes(), m.tobytes(), int(p), int(g))
     out = {"lib": os.path.basename(_lib.LIB_PATH)}
+    try:  # the run-time compiled kernel, when the build has one
+        t.jit_wait()
+        out["jit"] = True
+    except (_lib.BessGpuError, AttributeError):
+        out["jit"] = False
 
     def timed(slab, stride, g):
         t.classify(slab, stride, n, 8192, g)
