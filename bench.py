@@ -117,6 +117,26 @@ def load_traffic(key):
     return None if e is None else e.get("traffic_bytes")
 
 
+def shape_ceiling(shape, pkts, ms):
+    """The measured ceiling of an access shape (scripts/hbm_probe.hip, the
+    latest profiles/r*_calibration.json): the probe's packet rate, the time
+    it would take for `pkts`, and this kernel's fraction of it."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_calibration.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            e = json.load(f)["shapes"][shape]["ceiling"]
+    except (OSError, ValueError, KeyError):
+        return None
+    floor_ms = pkts / (e["Gpkts_per_s"] * 1e9) * 1e3
+    return {"shape": shape, "probe_Gpkts_per_s": e["Gpkts_per_s"],
+            "probe_ms_for_these_pkts": round(floor_ms, 4),
+            "frac_of_ceiling": round(floor_ms / ms, 4),
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 def traffic_gbs(key, kernel_ms):
     """PMC bytes per launch / measured launch duration, in GB/s (same basis
     as roofline.achieved); None until profiles/ holds a PMC measurement."""
@@ -1306,7 +1326,8 @@ def run_wm(args, dev, torch):
                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": round(gbs2k / HBM_PEAK_GBS, 4),
                                      "traffic": traffic_gbs("wm2k", ms2k),
-                                     "traffic_bytes_per_launch": load_traffic("wm2k")}}}
+                                     "traffic_bytes_per_launch": load_traffic("wm2k")},
+                        "measured_ceiling": shape_ceiling("s2k32", n, ms2k)}}
     if not args.no_cpu:
         cn = 1 << 16
         g = np.zeros(cn, np.uint16)
@@ -1400,7 +1421,10 @@ def run_c5(args, dev, torch):
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),
                         "traffic": traffic_gbs("c5", ms),
-                        "traffic_bytes_per_launch": load_traffic("c5")},
+                        "traffic_bytes_per_launch": load_traffic("c5"),
+                        "traffic_note": "counts the table's random reads the "
+                                        "Infinity Cache serves (r03 calibration)"},
+           "measured_ceiling": shape_ceiling("rnd36", n, ms),
            "parity": "bit-exact vs oracle on 256K-pkt sample" if parity
                      else "MISMATCH"}
     if not args.no_cpu:

@@ -3,6 +3,7 @@
 The HIP library is the product: if it is missing this module raises instead of
 falling back to anything else.
 """
+import atexit
 import ctypes as C
 import os
 
@@ -112,6 +113,7 @@ _SIGS = {
     "bg_wm_jit_wait": (_int, [_vp, _int, _int]),
     "bg_wm_jit_source": (_int, [_vp, _int, _vp, _sz, C.POINTER(_sz)]),
     "bg_wm_jit_check": (_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
+    "bg_shutdown": (None, []),
     "bg_cksum": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp, _vp, _vp]),
     "bg_cksum_process_host": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp,
                                      _vp, _vp]),
@@ -227,6 +229,11 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         _lib = L
+        # the run-time compiler thread must be idle before the C-level exit
+        # handlers run (bg_shutdown, include/bessgpu.h); Python's atexit
+        # hooks run first
+        if getattr(L, "bg_shutdown", None) is not None:  # (older builds: none)
+            atexit.register(L.bg_shutdown)
     return _lib
 
 

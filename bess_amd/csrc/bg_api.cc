@@ -1349,6 +1349,8 @@ static int wm_launch(bg_wm *wm, WmImage *img, const void *d_frames, size_t strid
   return 0;
 }
 
+void bg_shutdown(void) { jit_shutdown(); }
+
 int bg_wm_jit_wait(bg_wm *wm, int device, int timeout_ms) {
   int r = set_device(device);
   if (r) return r;

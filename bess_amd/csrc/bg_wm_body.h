@@ -267,10 +267,16 @@ __device__ __forceinline__ void load_pair(const uint8_t *__restrict__ frames,
                                           uint64_t n, uint64_t p0, int lane,
                                           uint32_t win_lo, uint32_t (&r)[8]) {
   const uint64_t s0 = p0 + (lane >> 1), s1 = s0 + 32;
-  const uint32_t off = win_lo + (lane & 1) * 16;
+  // a uniform base plus a 32-bit lane offset recomputed here (hoisted out
+  // of the tile loop, the per-lane 64-bit addresses were spilled, and the
+  // reload's wait retired every load issued before it)
+  uint32_t ln = (uint32_t)lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t off = (ln >> 1) * 64 + win_lo + (ln & 1) * 16;
+  const uint8_t *base = frames + p0 * 64;
   uint4 x = make_uint4(0, 0, 0, 0), y = x;
-  if (s0 < n) x = ld_stream(reinterpret_cast<const uint4 *>(frames + s0 * 64 + off));
-  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(frames + s1 * 64 + off));
+  if (s0 < n) x = ld_stream(reinterpret_cast<const uint4 *>(base + off));
+  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(base + off + 32 * 64));
   r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
   r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
 }
@@ -332,13 +338,9 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
     uint32_t w[NCH * 4 + 2];
     if constexpr (PAIR) {
       pair_window<NCH>(wn, lane, w);
-      if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, wn);
     } else {
 #pragma unroll
       for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
-      const uint64_t nidx = (t + nw) * 64 + lane;
-      if (t + nw < ntiles && nidx < a.n)
-        load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
     }
     uint64_t k[KW];
     Spec::template key<KW, NCH>(w, a, k);
@@ -356,6 +358,17 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
             [direct_index_k<KW>(k, Spec::dspec(a, d))];
       }
     }
+    // the next tile's header window, issued AFTER the direct reads: vector
+    // loads retire in order (vmcnt), so waiting for a load also waits for
+    // every older one -- the direct values, consumed in this tile, must not
+    // be younger than the prefetch the next tile consumes
+    if constexpr (PAIR) {
+      if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, wn);
+    } else {
+      const uint64_t nidx = (t + nw) * 64 + lane;
+      if (t + nw < ntiles && nidx < a.n)
+        load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
+    }
 #ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
     if (a.ab_phase == 1) {
       if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
@@ -365,18 +378,19 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
     const uint32_t hmask = Spec::hashed(a);
 
     // A. every hashed tuple's probe: both tag words from LDS (all reads in
-    // flight before any is used); zz[tu] != 0 iff a bucket holds the
-    // packet's fingerprint, ent[tu] its queue entry
-    uint32_t zz[kMaxTuples], ent[kMaxTuples];
+    // flight before any is used); ent[tu] is the packet's queue entry when
+    // a bucket holds its fingerprint, else 0 (an entry is never 0: its
+    // fingerprint is not)
+    uint32_t ent[kMaxTuples];
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
-      zz[tu] = 0;
       ent[tu] = 0;
       if ((hmask >> tu) & 1u) {  // wave-uniform (a scalar test, or a constant)
         const Probe p = wm_probe(Spec::template hash<KW>(k, tu, a), lg);
         const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
-        zz[tu] = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
-        ent[tu] = p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24);
+        const uint32_t zz = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
+        ent[tu] = zz ? p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24)
+                     : 0u;
       }
     }
     // B/C. one queue entry per (packet, tuple) with a fingerprint match,
@@ -389,7 +403,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
     uint32_t total = 0;
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
-      mk[tu] = __builtin_amdgcn_ballot_w64(zz[tu] != 0) & livemask;
+      mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
       total += (uint32_t)__popcll(mk[tu]);
     }
     for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
@@ -398,7 +412,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
       for (int tu = 0; tu < kMaxTuples; tu++) {
         const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
             (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
-        const bool mine = live && zz[tu] != 0;
+        const bool mine = live && ent[tu] != 0;
         if (total <= kQueue) {  // wave-uniform: one round, no window test
           if (mine) q[pos] = ent[tu];
         } else if (mine && pos - r0 < kQueue) {

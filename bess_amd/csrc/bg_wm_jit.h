@@ -26,6 +26,8 @@ int wm_jit_wait(WmJit *j, int timeout_ms);
 bool wm_jit_launch(WmJit *j, const WmArgs &a, int device, int num_cus, hipStream_t s,
                    hipError_t *err);
 std::string wm_jit_source(const WmJit *j);
+// stop the compiler thread after the compile in progress (bg_shutdown)
+void jit_shutdown();
 // the generated source for a / plan (empty: no tag-word image)
 std::string wm_jit_gen(const WmArgs &a, const FieldPlan &plan, uint32_t kw);
 // compile a's source synchronously on the calling thread (no device needed):

@@ -269,7 +269,7 @@ class WmTable:
         self.key_size = lib().bg_wm_key_size(h)
 
     def __del__(self):
-        if getattr(self, "h", None) is not None and _lib._lib is not None:
+        if getattr(self, "h", None) is not None and _lib is not None and _lib._lib is not None:
             lib().bg_wm_destroy(self.h)
             self.h = None
 

@@ -219,6 +219,12 @@ int bg_wm_jit_source(bg_wm *wm, int device, char *buf, size_t len, size_t *need)
  * kernel on the calling thread; no device needed (0, -ENOENT: no tag-word
  * image, -ENOEXEC: compile failed, log in `log`). */
 int bg_wm_jit_check(bg_wm *wm, char *log, size_t len, size_t *code_bytes);
+/* Before a process exits: stop the background compiler after the compile in
+ * progress (at most a few seconds). A process that exits while it compiles
+ * may crash in the compiler library's static destructors. Idempotent; later
+ * tables keep the ahead-of-time kernels. (bess_amd/_lib.py registers it with
+ * Python's atexit.) */
+void bg_shutdown(void);
 
 /* ---- IPChecksum / L4Checksum ------------------------------------------ */
 /* mode: BG_CK_IP, BG_CK_L4 or both (= IPChecksum -> L4Checksum pipeline:

@@ -5,11 +5,14 @@
 
 Reads every counter_collection.csv under gpurun_out/pmc_<workload>_<i>/,
 averages each counter over the dispatches of the workload's kernel and
-applies MI355X_MICROARCH.md's gfx950 corrections:
-  * FETCH_SIZE (KB) reports 1/2 of the bytes of wide streaming reads
-    (FETCH_SIZE = TCC_EA0_RDREQ x 64 B for 128 B requests) -> doubled;
+applies MI355X_MICROARCH.md's gfx950 corrections, calibrated per access
+shape on known byte counts (profiles/r03_calibration.json):
+  * FETCH_SIZE (KB) = TCC_EA0_RDREQ x 64 B. Wide streaming reads and dense
+    slots make 128 B requests: x2 (the guide's correction). A 32 B window
+    per 2 KB slot (C4 on 2 KB slots) makes one 64 B request: x1 (FETCH).
   * WRITE_SIZE (KB) is exact for 16 B/lane stores.
-traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 bytes per launch.
+traffic = FETCH[wl] * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 bytes per launch.
+Random table reads that hit the Infinity Cache are counted too (C5).
 """
 import csv
 import glob
@@ -20,7 +23,7 @@ from collections import defaultdict
 
 # bench workload -> substring of its timed kernel's name
 KERNELS = {"em": "em_slab_kernel", "cksum": "cksum_kernel",
-           "wm": "wm_tags_kernel", "wm2k": "wm_tags_kernel",
+           "wm": ("bg_wm_jit", "wm_tags_kernel"), "wm2k": ("bg_wm_jit", "wm_tags_kernel"),
            "c5": "em_slab_kernel",
            "hashlb": "HlbOp<2>", "acl": "AclTreeOp", "iplookup": "Lpm16LdsOp",
            "ttl": "TtlOp<4>", "nat": "NatOp", "dnat": "dnat_fused_slab_kernel",
@@ -32,6 +35,8 @@ ALGO = {"em": 66 * (16 << 20), "cksum": 1502 * (1 << 20),
         "iplookup": 66 * (16 << 20), "ttl": 130 * (16 << 20),
         "nat": 130 * (16 << 20), "dnat": 130 * (16 << 20),
         "rewrite": 70 * (16 << 20)}
+# FETCH_SIZE -> bytes factor by access shape (r03_calibration.json)
+FETCH = {"wm2k": 1}
 
 
 def collect(root, wl):
@@ -41,7 +46,8 @@ def collect(root, wl):
         per = defaultdict(float)  # (dispatch, counter) -> value
         with open(p) as f:
             for r in csv.DictReader(f):
-                if KERNELS[wl] not in r["Kernel_Name"]:
+                names = KERNELS[wl] if isinstance(KERNELS[wl], tuple) else (KERNELS[wl],)
+                if not any(k in r["Kernel_Name"] for k in names):
                     continue
                 per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         for (d, c), v in per.items():
@@ -56,12 +62,13 @@ def main():
         c = collect(root, wl)
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             continue
-        fetch = 2 * c["FETCH_SIZE"] * 1024
+        fetch = FETCH.get(wl, 2) * c["FETCH_SIZE"] * 1024
         write = c["WRITE_SIZE"] * 1024
         e = {"traffic_bytes": round(fetch + write),
              "fetch_bytes_corrected": round(fetch),
              "write_bytes": round(write),
              "algorithmic_bytes": ALGO[wl],
+             "fetch_factor": FETCH.get(wl, 2),
              "traffic_over_algorithmic": round((fetch + write) / ALGO[wl], 4),
              "raw": {k: round(v, 1) for k, v in c.items()}}
         if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
