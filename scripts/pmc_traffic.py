@@ -23,7 +23,7 @@ from collections import defaultdict
 
 # bench workload -> substring of its timed kernel's name
 KERNELS = {"em": "em_slab_kernel", "cksum": "cksum_kernel",
-           "wm": ("bg_wm_jit", "wm_tags_kernel"), "wm2k": ("bg_wm_jit", "wm_tags_kernel"),
+           "wm": "bg_wm_jit", "wm2k": "bg_wm_jit",  # the run-time compiled kernel
            "c5": "em_slab_kernel",
            "hashlb": "HlbOp<2>", "acl": "AclTreeOp", "iplookup": "Lpm16LdsOp",
            "ttl": "TtlOp<4>", "nat": "NatOp", "dnat": "dnat_fused_slab_kernel",
@@ -46,8 +46,7 @@ def collect(root, wl):
         per = defaultdict(float)  # (dispatch, counter) -> value
         with open(p) as f:
             for r in csv.DictReader(f):
-                names = KERNELS[wl] if isinstance(KERNELS[wl], tuple) else (KERNELS[wl],)
-                if not any(k in r["Kernel_Name"] for k in names):
+                if KERNELS[wl] not in r["Kernel_Name"]:
                     continue
                 per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         for (d, c), v in per.items():

@@ -206,3 +206,22 @@ def test_jit_follows_rule_changes():
     L.or_wm_free(wm)
     assert (first == want).all() and (second == want).all()
     del rng
+
+
+@pytest.mark.gpu
+def test_exit_while_compiling():
+    """a process that syncs a tag-word table (starting its background compile)
+    and exits at once ends cleanly: bg_shutdown, registered with Python's
+    atexit, waits for the compile before LLVM's static destructors run"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from bess_amd import flowtable as F, packets as P\n"
+            "rk, rm, pr, g, _, _ = P.wm_workload(20000, 64, stride=64, sizes=((60, 1),))\n"
+            "t = F.WmTable(P.FIVE_TUPLE)\n"
+            "[t.add(k.tobytes(), m.tobytes(), int(p), int(x)) for k, m, p, x in zip(rk, rm, pr, g)]\n"
+            "t.sync(0)\n" % root)
+    r = subprocess.run([sys.executable, "-c", code], timeout=120, capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
