@@ -355,6 +355,11 @@ struct RingArgs {
   uint64_t idle_ticks;
   FieldPlan fp;
   TableRef t;
+  // A/B build only (BG_RING_TRACE): per (lane, ticket < trace_n) five
+  // s_memrealtime stamps -- claimed, seen published, descriptor read, gates
+  // stored, done written; null in the product
+  uint64_t *trace;
+  uint64_t trace_n;
 };
 // four waves: a ticket's packets are spread over 256 lanes (4 per lane per
 // round), so a 1024-packet batch takes one round of loads and lookups

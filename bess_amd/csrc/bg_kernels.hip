@@ -489,6 +489,11 @@ void em_ring_kernel(RingArgs a) {
   for (;;) {
     if (threadIdx.x == 0) {
       const uint64_t t = atomicAdd(dl, 1ull);
+#ifdef BG_AB
+      uint64_t *tr = a.trace && t < a.trace_n ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5
+                                              : nullptr;
+      if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
+#endif
       uint32_t go = 0;
       for (;;) {
         if (ld_agent(dl + 1) > t) {
@@ -504,11 +509,17 @@ void em_ring_kernel(RingArgs a) {
         __builtin_amdgcn_s_sleep(2);
       }
       uint64_t w[4] = {0, 0, 0, 0};
+#ifdef BG_AB
+      if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
+#endif
       if (go) {
         const uint64_t tag = (t + 1) & 0xFFFF;
         const uint64_t *d = ldesc + (t % a.nslots) * 4;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
+#ifdef BG_AB
+      if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
+#endif
 #pragma unroll
       for (int i = 0; i < 4; i++) sh_w[i] = w[i];
       sh_t = t;
@@ -546,9 +557,21 @@ void em_ring_kernel(RingArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
+#ifdef BG_AB
+      uint64_t *tr = a.trace && t < a.trace_n ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5
+                                              : nullptr;
+      if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+#endif
       __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef BG_AB
+      if (tr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tr[4] = __builtin_amdgcn_s_memrealtime();
+      }
+#endif
+    }
     __syncthreads();  // sh_* are rewritten for the next ticket
   }
 }

@@ -31,6 +31,7 @@
 #include "../../include/bessgpu.h"
 #include "bg_internal.h"
 #include "bg_kernels.h"
+#include "bg_launch.h"
 
 using namespace bg;
 
@@ -148,6 +149,7 @@ void ring_release(bg_ring *r) {
   if (r->h_reset) (void)hipHostFree(r->h_reset);
   if (r->d_dev) (void)hipFree(r->d_dev);
   if (r->d_table) (void)hipFree(r->d_table);
+  if (r->a.trace) (void)hipFree(r->a.trace);
   if (r->ev) (void)hipEventDestroy(r->ev);
   if (r->st) (void)hipStreamDestroy(r->st);
 }
@@ -242,6 +244,18 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
   a.nslots = (uint32_t)slots;
   a.nlanes = (uint32_t)lanes;
   a.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
+  a.trace = nullptr;
+  a.trace_n = 0;
+#ifdef BG_AB  // per-ticket stamps (scripts/ring_probe.py trace)
+  if (const int tn = knob("BG_RING_TRACE", 0)) {
+    const size_t bytes = nl * (size_t)tn * 5 * 8;
+    if (hipMalloc(reinterpret_cast<void **>(&a.trace), bytes) == hipSuccess &&
+        hipMemset(a.trace, 0, bytes) == hipSuccess)
+      a.trace_n = (uint64_t)tn;
+    else
+      a.trace = nullptr;
+  }
+#endif
   if (!a.desc || !a.done || !a.stop || !a.pub || !a.ended) {
     ring_release(r);
     delete r;
@@ -349,6 +363,19 @@ int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride, size_t 
   }
   return last < 0 ? 0 : bg_ring_wait(r, lane, last);
 }
+
+#ifdef BG_AB
+// the A/B build's per-ticket stamps (lanes x trace_n x 5 u64); returns
+// trace_n, 0 without a trace
+int bg_ring_trace(bg_ring *r, uint64_t *out, size_t cap_words) {
+  if (!r->a.trace) return 0;
+  const size_t w = (size_t)r->nlanes * r->a.trace_n * 5;
+  if (cap_words < w) return fail(ENOBUFS, "trace needs %zu words", w);
+  HIP_TRY(hipStreamSynchronize(r->st));
+  HIP_TRY(hipMemcpy(out, r->a.trace, w * 8, hipMemcpyDeviceToHost));
+  return (int)r->a.trace_n;
+}
+#endif
 
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks) {
   if (launches) *launches = r->launches;
