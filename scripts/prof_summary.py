@@ -19,8 +19,8 @@ def main():
     with open(sys.argv[1]) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"]
-            if "bg::" not in name:
-                continue
+            if "bg::" not in name and not name.startswith("bg_wm_jit"):
+                continue  # (bg_wm_jit_*: the run-time compiled WM kernels)
             m = re.search(r"(\w+)(<[^>]*>)?\(bg::", name)
             short = (m.group(1) + (m.group(2) or "")) if m else name
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
