@@ -343,7 +343,7 @@ constexpr int kDnatMaxExt = 16;
 // l * kRingLaneWords (128 bytes apart: an L2 line and a host line pair of
 // their own, so lanes' claim atomics and submitters never share a line).
 struct RingArgs {
-  const uint64_t *desc;   // host memory (mapped): nlanes x nslots x 4 words
+  const uint64_t *desc;   // nlanes x nslots x kRingDescWords (4 used)
   uint32_t *done;         // host memory (mapped): nlanes x nslots
   const uint64_t *pub;    // host memory: tickets published, per lane
   const uint32_t *stop;   // host memory: the owner stops the grid
@@ -366,6 +366,11 @@ struct RingArgs {
 // rather than four on one wave (a ticket's latency is its rounds')
 constexpr int kRingBlock = 256;
 constexpr int kRingLaneWords = 16;
+// a descriptor slot: 4 tagged words + 4 of padding, one 64-byte line, so a
+// host writing it through write-combining buffers fills a whole buffer,
+// which leaves for the device at once (a half-written line can wait in the
+// buffer until the next descriptor's stores)
+constexpr int kRingDescWords = 8;
 constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
 
 #ifndef __HIPCC_RTC__  // host launchers: not part of a run-time compile

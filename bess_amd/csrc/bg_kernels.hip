@@ -481,7 +481,7 @@ void em_ring_kernel(RingArgs a) {
   const uint32_t lane = (blockIdx.x - 1) % a.nlanes;
   unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
   const unsigned long long *dstop = a.dev + (size_t)a.nlanes * kRingLaneWords;
-  const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * 4;
+  const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * kRingDescWords;
   uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   copy_table_to_lds(lds, a.t);  // (ends with a barrier)
   const uint64_t mask48 = (1ull << 48) - 1;
@@ -514,7 +514,7 @@ void em_ring_kernel(RingArgs a) {
 #endif
       if (go) {
         const uint64_t tag = (t + 1) & 0xFFFF;
-        const uint64_t *d = ldesc + (t % a.nslots) * 4;
+        const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
 #ifdef BG_AB

@@ -4,10 +4,18 @@
 // BESS hands a module <= 32 packets per ProcessBatch (core/pktbatch.h:70);
 // a kernel launch per batch is launch-bound (~5 us each). Like the Queue
 // module (core/modules/queue.cc:173 enqueues in ProcessBatch, 190 emits
-// from RunTask), a submit here only writes one 32-byte descriptor into a
+// from RunTask), a submit here only writes one descriptor (a 64-byte line) into a
 // ring in pinned host memory; em_ring_kernel (bg_kernels.hip), launched
 // once, claims tickets in order, classifies each batch and publishes
 // done[t % slots] = t + 1 in host memory, which wait/poll read.
+//
+// Where the descriptors live: in device memory when the host can write it
+// (the PCIe BAR maps all of it on MI355X; scripts/bar_probe.hip measured a
+// 32-byte descriptor write at 1.5 ns, posted), uncached on the device, so
+// a worker reads its descriptor from HBM (~1 us) instead of over PCIe (a
+// round trip that queued to 8-23 us per ticket under 16 submitters,
+// profiles/r03_ring_trace.jsonl). Otherwise (no CPU mapping of device
+// memory, or BG_RING_HOST_DESC=1) in pinned host memory, read over PCIe.
 //
 // One lane of the grid (the dispatcher) polls the host's published count
 // over PCIe and mirrors it in device memory, where the other workgroups
@@ -20,7 +28,10 @@
 // descriptor is read whole without fences.
 #include <errno.h>
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
 #include <time.h>
 #include <x86intrin.h>
 
@@ -39,12 +50,17 @@ using namespace bg;
 // on lines of their own (128 B: the adjacent-line prefetcher pairs 64 B
 // lines), as each is written by its own submitter.
 struct alignas(128) RingLane {
-  uint64_t *h_desc = nullptr;  // nslots x 4 words (host, coherent, mapped)
+  uint64_t *h_desc = nullptr;  // nslots x kRingDescWords (the host's view)
   uint32_t *h_done = nullptr;  // nslots
   uint64_t *h_pub = nullptr;   // tickets published (its own 64-byte line)
   uint64_t next = 0;           // next ticket to publish
   std::atomic<uint64_t> done_upto{0};  // every ticket below has completed
-  std::mutex mu;  // one worker per lane; the lock only guards misuse
+  // One worker per lane: a second thread inside the lane's calls at the
+  // same time gets EBUSY. A flag with plain loads and stores, not a lock:
+  // a locked instruction drains the CPU's write-combining buffers, which
+  // hold the descriptors bound for device memory (~300 ns per ticket,
+  // scripts/bar_probe.hip), so a mutex here cost every submit a flush.
+  std::atomic<uint32_t> busy{0};
 };
 
 struct bg_ring {
@@ -55,7 +71,8 @@ struct bg_ring {
   uint64_t version = 0;     // the rule version of its table copy
   hipStream_t st = nullptr;  // the kernel's own stream
   hipEvent_t ev = nullptr;   // recorded after each launch: has it ended?
-  uint64_t *h_desc = nullptr;  // nlanes x nslots x 4 words
+  uint64_t *h_desc = nullptr;  // nlanes x nslots x kRingDescWords (pinned host) ...
+  uint64_t *d_desc = nullptr;  // ... or in device memory, written by the host
   uint32_t *h_done = nullptr;  // nlanes x nslots
   uint64_t *h_pub = nullptr;   // nlanes x kRingLaneWords
   uint32_t *h_stop = nullptr;  // 1 word, host
@@ -142,6 +159,7 @@ void ring_release(bg_ring *r) {
   if (r->h_stop) __atomic_store_n(r->h_stop, 1u, __ATOMIC_RELEASE);
   if (r->st) (void)hipStreamSynchronize(r->st);  // every workgroup exits
   if (r->h_desc) (void)hipHostFree(r->h_desc);
+  if (r->d_desc) (void)hipFree(r->d_desc);
   if (r->h_done) (void)hipHostFree(r->h_done);
   if (r->h_pub) (void)hipHostFree(r->h_pub);
   if (r->h_stop) (void)hipHostFree(r->h_stop);
@@ -164,6 +182,42 @@ template <typename T>
 T *dev_alias(T *h) {
   void *d = nullptr;
   return hipHostGetDevicePointer(&d, h, 0) == hipSuccess ? static_cast<T *>(d) : nullptr;
+}
+
+// device memory for the descriptors that this process can also write from
+// the host (the allocation's addresses are mapped on the CPU side: mincore
+// fails with ENOMEM on an unmapped range); nullptr when it cannot
+uint64_t *host_writable_device_alloc(size_t bytes) {
+  const char *env = getenv("BG_RING_HOST_DESC");
+  if (env && env[0] == '1') return nullptr;
+  void *d = nullptr;
+  if (hipExtMallocWithFlags(&d, bytes, hipDeviceMallocUncached) != hipSuccess) return nullptr;
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  const uintptr_t lo = (uintptr_t)d & ~(pg - 1);
+  const size_t len = (((uintptr_t)d + bytes + pg - 1) & ~(pg - 1)) - lo;
+  unsigned char vec[64];
+  if (mincore(reinterpret_cast<void *>(lo), pg, vec) != 0 ||
+      mincore(reinterpret_cast<void *>(lo + len - pg), pg, vec) != 0) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  return static_cast<uint64_t *>(d);
+}
+
+// the lane for this call (see RingLane::busy); ok false: in use elsewhere
+struct LaneUse {
+  RingLane &l;
+  const bool ok;
+  explicit LaneUse(RingLane &x) : l(x), ok(x.busy.load(std::memory_order_acquire) == 0) {
+    if (ok) l.busy.store(1, std::memory_order_relaxed);
+  }
+  ~LaneUse() {
+    if (ok) l.busy.store(0, std::memory_order_release);
+  }
+};
+
+int lane_busy(int lane) {
+  return fail(EBUSY, "lane %d in use by another thread (one worker per lane)", lane);
 }
 
 int bad_lane(const bg_ring *r, int lane) {
@@ -209,7 +263,8 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
   const size_t nl = (size_t)lanes, ns = (size_t)slots;
   hipError_t e = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = host_alloc(&r->h_desc, nl * ns * 32);
+  if (e == hipSuccess && !(r->d_desc = host_writable_device_alloc(nl * ns * kRingDescWords * 8)))
+    e = host_alloc(&r->h_desc, nl * ns * kRingDescWords * 8);
   if (e == hipSuccess) e = host_alloc(&r->h_done, nl * ns * 4);
   if (e == hipSuccess) e = host_alloc(&r->h_pub, nl * kRingLaneWords * 8);
   if (e == hipSuccess) e = host_alloc(&r->h_stop, 64);
@@ -218,24 +273,26 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
     e = hipHostMalloc(reinterpret_cast<void **>(&r->h_reset), (nl * kRingLaneWords + 8) * 8);
   if (e == hipSuccess)
     e = hipMalloc(reinterpret_cast<void **>(&r->d_dev), (nl * kRingLaneWords + 8) * 8);
+  if (e == hipSuccess && r->d_desc) e = hipMemset(r->d_desc, 0, nl * ns * kRingDescWords * 8);  // tag 0
   if (e != hipSuccess) {
     ring_release(r);
     delete r;
     return fail(EIO, "ring allocation: %s", hipGetErrorString(e));
   }
-  memset(r->h_desc, 0, nl * ns * 32);  // tag 0: no ticket's
+  if (r->h_desc) memset(r->h_desc, 0, nl * ns * kRingDescWords * 8);  // tag 0: no ticket's
+  uint64_t *desc = r->d_desc ? r->d_desc : r->h_desc;  // the host's view
   memset(r->h_done, 0, nl * ns * 4);
   memset(r->h_pub, 0, nl * kRingLaneWords * 8);
   *r->h_stop = 0;
   *r->h_ended = 0;
   for (size_t i = 0; i < nl; i++) {
     RingLane &l = r->lanes[i];
-    l.h_desc = r->h_desc + i * ns * 4;
+    l.h_desc = desc + i * ns * kRingDescWords;
     l.h_done = r->h_done + i * ns;
     l.h_pub = r->h_pub + i * kRingLaneWords;
   }
   RingArgs &a = r->a;
-  a.desc = dev_alias(r->h_desc);
+  a.desc = r->d_desc ? r->d_desc : dev_alias(r->h_desc);
   a.done = dev_alias(r->h_done);
   a.stop = dev_alias(r->h_stop);
   a.pub = dev_alias(r->h_pub);
@@ -302,9 +359,11 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
       ((uintptr_t)frames & 15) || (stride & 15))
     return fail(EINVAL, "frames 16-byte aligned with stride %% 16 == 0 below 2^48");
   RingLane &l = r->lanes[lane];
-  std::lock_guard<std::mutex> lk(l.mu);
+  LaneUse use(l);
+  if (!use.ok) return lane_busy(lane);
   // lane full: its oldest ticket must finish before its slot is reused
   if (l.next - l.done_upto.load(std::memory_order_relaxed) >= r->nslots) {
+    if (r->d_desc) _mm_sfence();  // (the last descriptor out before we wait)
     const double t0 = now_s();
     for (;;) {
       retire(r, l);
@@ -316,11 +375,19 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
   }
   const uint64_t t = l.next;
   const uint64_t tag = ((t + 1) & 0xFFFF) << 48;
-  uint64_t *d = l.h_desc + (t % r->nslots) * 4;
+  uint64_t *d = l.h_desc + (t % r->nslots) * kRingDescWords;
   __atomic_store_n(d + 0, ((uint64_t)(uintptr_t)frames & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 1, ((uint64_t)(uintptr_t)gates & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 2, (uint64_t)n | ((uint64_t)stride << 32) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 3, (uint64_t)default_gate | tag, __ATOMIC_RELAXED);
+  for (int i = 4; i < kRingDescWords; i++)  // the rest of the line (see kRingDescWords)
+    __atomic_store_n(d + i, tag, __ATOMIC_RELAXED);
+  // A descriptor in device memory goes through the CPU's write-combining
+  // buffers and may reach the device after the count below: the tags make
+  // a worker read it again until it has. Its stores fill one 64-byte
+  // buffer, which leaves at once. (An sfence per ticket here,
+  // BG_RING_SFENCE=1 in the A/B build, costs a PCIe flush, ~300 ns.)
+  if (r->d_desc && knob("BG_RING_SFENCE", 0)) _mm_sfence();
   __atomic_store_n(l.h_pub, t + 1, __ATOMIC_RELEASE);
   l.next = t + 1;
   if (int rc = ensure_running(r)) return rc;
@@ -330,9 +397,11 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
 int bg_ring_wait(bg_ring *r, int lane, int64_t ticket) {
   if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
   RingLane &l = r->lanes[lane];
-  std::lock_guard<std::mutex> lk(l.mu);
+  LaneUse use(l);
+  if (!use.ok) return lane_busy(lane);
   if (ticket < 0 || (uint64_t)ticket >= l.next)
     return fail(EINVAL, "ticket %lld not submitted", (long long)ticket);
+  if (r->d_desc) _mm_sfence();  // this submitter's last descriptor out to the device
   const double t0 = now_s();
   for (;;) {
     retire(r, l);
@@ -346,7 +415,9 @@ int bg_ring_wait(bg_ring *r, int lane, int64_t ticket) {
 int64_t bg_ring_completed(bg_ring *r, int lane) {
   if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
   RingLane &l = r->lanes[lane];
-  std::lock_guard<std::mutex> lk(l.mu);
+  LaneUse use(l);
+  if (!use.ok) return lane_busy(lane);
+  if (r->d_desc) _mm_sfence();  // (as in bg_ring_wait)
   retire(r, l);
   if (int rc = ensure_running(r)) return rc;
   return (int64_t)l.done_upto.load(std::memory_order_relaxed);
@@ -376,6 +447,8 @@ int bg_ring_trace(bg_ring *r, uint64_t *out, size_t cap_words) {
   return (int)r->a.trace_n;
 }
 #endif
+
+int bg_ring_desc_in_device(const bg_ring *r) { return r && r->d_desc ? 1 : 0; }
 
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks) {
   if (launches) *launches = r->launches;

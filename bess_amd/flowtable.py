@@ -197,6 +197,7 @@ class Ring:
         self.h = h
         self.table = table
         self.lanes = lanes
+        self.device = device
 
     def close(self):
         if getattr(self, "h", None) is not None and _lib._lib is not None:
@@ -255,6 +256,10 @@ class Ring:
         launches, blocks = C.c_uint64(), C.c_int()
         lib().bg_ring_info(self.h, C.byref(launches), C.byref(blocks))
         return launches.value, blocks.value
+
+    def desc_in_device(self):
+        """True: descriptors in device memory the host writes (BAR)."""
+        return bool(lib().bg_ring_desc_in_device(self.h))
 
 
 class WmTable:

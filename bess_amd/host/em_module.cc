@@ -147,6 +147,7 @@ class ExactMatch final : public Module {
       pr->r = r;
       pr->device = device;
       pr->lanes = kPipeRingLanes;
+      pr->lane_mu.reset(new std::mutex[kPipeRingLanes]);
       pr->version = bg::ring_version(r);
       cur = std::move(pr);
     }

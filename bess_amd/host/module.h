@@ -139,6 +139,9 @@ struct PipeRing {
   int lanes = 0;
   uint64_t version = 0;  // the rules it classifies with
   std::atomic<int> next_lane{0};
+  // pipes past `lanes` share a lane; bg_ring's lanes take one thread at a
+  // time (EBUSY otherwise), so a pipe holds its lane's lock around each call
+  std::unique_ptr<std::mutex[]> lane_mu;
   ~PipeRing() { bg_ring_destroy(r); }
 };
 

@@ -114,7 +114,10 @@ struct bg_pipe {
 static void pipe_release(bg_pipe *p) {
   for (Slot &s : p->slots) {
     if (s.ring) {  // the kernel may still read the staging: let it finish
-      if (s.inflight) (void)bg_ring_wait(s.ring->r, s.lane, s.ticket);
+      if (s.inflight) {
+        std::lock_guard<std::mutex> lk(s.ring->lane_mu[s.lane]);
+        (void)bg_ring_wait(s.ring->r, s.lane, s.ticket);
+      }
       s.ring.reset();
     }
     if (s.st) {
@@ -180,7 +183,11 @@ static int launch_slot(bg_pipe *p) {
       p->ring = ring;
       p->lane = ring->next_lane.fetch_add(1) % ring->lanes;
     }
-    const int64_t t = bg_ring_submit(ring->r, p->lane, s.dv_in, p->w, n, dflt, s.dv_g);
+    int64_t t;
+    {
+      std::lock_guard<std::mutex> lk(ring->lane_mu[p->lane]);
+      t = bg_ring_submit(ring->r, p->lane, s.dv_in, p->w, n, dflt, s.dv_g);
+    }
     if (t < 0) return (int)t;
     s.ring = std::move(ring);
     s.lane = p->lane;
@@ -225,6 +232,7 @@ static int retire_oldest(bg_pipe *p, bool wait) {
   if (s.ring) {
     if (!bg::ring_done(s.ring->r, s.lane, s.ticket)) {
       // (through the ring's own check, which relaunches a grid that ended)
+      std::lock_guard<std::mutex> lk(s.ring->lane_mu[s.lane]);
       const int64_t c = bg_ring_completed(s.ring->r, s.lane);
       if (c < 0) return (int)c;
       if (c <= s.ticket) {

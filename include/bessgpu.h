@@ -597,6 +597,10 @@ int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride,
                 size_t n, size_t burst, uint16_t default_gate, uint16_t *gates);
 /* kernel launches so far (1 + relaunches after idle exits), workgroups */
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks);
+/* 1: the descriptors live in device memory the host writes through the
+ * PCIe BAR (workers read them from HBM); 0: in pinned host memory (read
+ * over PCIe; no CPU mapping of device memory, or BG_RING_HOST_DESC=1). */
+int bg_ring_desc_in_device(const bg_ring *r);
 
 #ifdef __cplusplus
 }

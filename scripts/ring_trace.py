@@ -41,6 +41,7 @@ def main():
         os.environ.pop("BG_RING_TRACE")
         ring.run_lanes(d_frames, 64, n, B, 8192, d_g, T)  # warm (stamps overwritten)
         dt = ring.run_lanes(d_frames, 64, n, B, 8192, d_g, T)
+        dev = ring.desc_in_device()
         buf = np.zeros(T * per_lane * 5, np.uint64)
         tn = L.bg_ring_trace(ring.h, buf.ctypes.data, buf.size)
         ring.close()
@@ -49,7 +50,7 @@ def main():
         s = st[ok]
         iv = {"claim_to_seen_us": s[:, 1] - s[:, 0], "seen_to_desc_us": s[:, 2] - s[:, 1],
               "desc_to_stored_us": s[:, 3] - s[:, 2], "stored_to_done_us": s[:, 4] - s[:, 3]}
-        out = {"submitters": T, "tickets": int(ok.sum()), "batch": B,
+        out = {"submitters": T, "desc_in_device": dev, "tickets": int(ok.sum()), "batch": B,
                "Mpps": round(n / dt / 1e6, 1)}
         for k, v in iv.items():
             out[k] = {"p50": round(float(np.median(v)) / 1e3, 2),

@@ -86,11 +86,18 @@ def test_ring_idle_exit_relaunch_and_snapshot():
     ring.close()
 
 
+@pytest.mark.parametrize("host_desc", [False, True])
 @pytest.mark.parametrize("lanes,threads", [(4, 4), (16, 16), (16, 3)])
-def test_ring_submission_lanes_vs_oracle(lanes, threads):
+def test_ring_submission_lanes_vs_oracle(lanes, threads, host_desc, monkeypatch):
     """several worker threads, each on its own submission lane of one
     running kernel, 32-packet batches (and ragged 100-packet ones): every
-    gate as the oracle's; an idle exit in between relaunches for all lanes"""
+    gate as the oracle's; an idle exit in between relaunches for all lanes.
+    Both descriptor homes: device memory written by the host (the default
+    where the BAR maps it) and pinned host memory (BG_RING_HOST_DESC=1)"""
+    if host_desc:
+        monkeypatch.setenv("BG_RING_HOST_DESC", "1")
+    else:
+        monkeypatch.delenv("BG_RING_HOST_DESC", raising=False)
     n = 1 << 18
     keys, gates, frames = P.em_workload(1000, n, seed=lanes, pkt_seed=9)
     want = oracle_gates(keys, gates, frames)
@@ -98,6 +105,8 @@ def test_ring_submission_lanes_vs_oracle(lanes, threads):
     t.add_many(keys, gates)
     d = torch.from_numpy(frames.reshape(-1)).cuda()
     ring = F.Ring(t, slots=512, lanes=lanes, idle_us=3000)
+    if host_desc:
+        assert not ring.desc_in_device()
     for burst in (32, 100):
         dg = torch.full((n,), -1, dtype=torch.int16, device="cuda")
         ring.run_lanes(d, 64, n, burst, 8192, dg, threads)
