@@ -417,7 +417,6 @@ int64_t bg_ring_completed(bg_ring *r, int lane) {
   RingLane &l = r->lanes[lane];
   LaneUse use(l);
   if (!use.ok) return lane_busy(lane);
-  if (r->d_desc) _mm_sfence();  // (as in bg_ring_wait)
   retire(r, l);
   if (int rc = ensure_running(r)) return rc;
   return (int64_t)l.done_upto.load(std::memory_order_relaxed);

@@ -59,7 +59,8 @@ struct Slot {
   uint64_t *h_done = nullptr;  // pinned, mapped: = seq once the slot's D2H is done
   uint64_t *d_done = nullptr;  // its device address (hipStreamWriteValue64)
   uint64_t seq = 0;            // this launch's number
-  std::vector<uint8_t *> heads;  // writeback targets
+  std::vector<uint8_t *> heads;  // writeback targets; the lagging gather's sources
+  size_t gathered = 0;           // packets [0, gathered) are in h_in
   std::vector<uint16_t> wblen;   // bytes of the header line to write back
   std::vector<void *> cookies;
   size_t n = 0;
@@ -166,8 +167,21 @@ static inline void copy16(uint8_t *dst, const uint8_t *src, size_t w) {
 // module lock: like bessd's datapath, a pipe relies on THREAD_UNSAFE
 // commands running only while its worker is paused, core/module.cc:97-101;
 // such a command flushes the pipe first, PipeFlushLocked.)
+// The lagging gather (field windows, no writeback): a submit records its
+// packets' heads and copies the windows of the packets the PREVIOUS call
+// recorded, whose data lines the caller's prefetch has brought in since
+// (copying them at once stalled on the line misses the prefetch had just
+// started: about a miss latency per 32-packet batch). A slot is gathered
+// whole before it launches.
+static void gather(bg_pipe *p, Slot &s) {
+  uint8_t *dst = s.h_in + s.gathered * p->w;
+  for (size_t j = s.gathered; j < s.n; j++, dst += p->w) copy16(dst, s.heads[j] + p->lo, p->w);
+  s.gathered = s.n;
+}
+
 static int launch_slot(bg_pipe *p) {
   Slot &s = p->slots[p->fill];
+  if (!p->writeback) gather(p, s);
   const size_t n = s.n;
   const uint64_t t0 = mono_ns();
   s.t_launch = __rdtsc();
@@ -279,6 +293,7 @@ static void release_oldest(bg_pipe *p) {
   Slot &s = p->slots[p->oldest];
   s.draining = false;
   s.n = 0;
+  s.gathered = 0;
   p->oldest = (p->oldest + 1) % p->slots.size();
 }
 
@@ -359,6 +374,7 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
         return fail(EIO, "HIP error %d: %s", (int)e, hipGetErrorString(e));
       }
       s.cookies.resize(batch);
+      s.heads.resize(batch);
       continue;
     }
     // +64 B: window loads of the last packet may run past its slot
@@ -385,10 +401,8 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
       return fail(EIO, "HIP error %d: %s", (int)e, hipGetErrorString(e));
     }
     s.cookies.resize(batch);
-    if (p->writeback) {
-      s.heads.resize(batch);
-      s.wblen.resize(batch);
-    }
+    s.heads.resize(batch);
+    if (p->writeback) s.wblen.resize(batch);
   }
   {
     std::lock_guard<std::mutex> lk(m->pipes_mu);
@@ -442,6 +456,7 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                   const uint16_t *lens, void *const *cookies, size_t cnt) {
   if (p->err) return p->err;
   int r;
+  if (!p->writeback) gather(p, p->slots[p->fill]);  // the previous call's packets
   const bg_ctx c = ResolveCtx(ctx, p->device);
   p->st_submits++;
   p->st_pkts += cnt;
@@ -474,13 +489,15 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
     uint8_t *dst = s.h_in + s.n * p->w;
     for (size_t j = 0; j < take; j++, dst += p->w) {
       const size_t k = i + j;
-      if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
       const uint8_t *src = heads[k] + p->lo;
       if (!p->writeback) {
-        // the window rounded up to 16 bytes (the bytes past it are not
-        // read by the kernel; the packet buffer holds them, SNBUF_DATA)
-        copy16(dst, src, p->w);
+        // the window (rounded up to 16 bytes: the bytes past it are not
+        // read by the kernel; the packet buffer holds them, SNBUF_DATA) is
+        // copied by the next call's gather
+        __builtin_prefetch(src);
+        s.heads[s.n + j] = heads[k];
       } else {
+        if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
         // the frame (data_len bytes when given, at least its header line),
         // zero-padded to the slot
         size_t len = lens ? std::min<size_t>(lens[k], span) : span;

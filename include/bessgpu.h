@@ -536,8 +536,10 @@ int bg_module_desc(const bg_module *m, char *buf, size_t len);
  *           not emitted); checksum modules' recomputed header lines are
  *           written back into the packet buffers first. wait != 0 blocks
  *           until a launched slot completes (returns 0 if none in flight).
- * Packets stay owned by the caller until poll returns them. One pipe per
- * worker thread; pipes may share a module. */
+ * Packets stay owned by the caller until poll returns them, their bytes
+ * unchanged: a submit's windows are copied by the pipe's next call (by then
+ * the caller's prefetch of their lines has landed) or when their slot
+ * launches. One pipe per worker thread; pipes may share a module. */
 typedef struct bg_pipe bg_pipe;
 int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
                    size_t span, bg_pipe **out);
