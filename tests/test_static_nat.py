@@ -59,7 +59,13 @@ def nat_frames(n, stride, seed, valid=True, ihl_max=15):
     f[:, 23] = np.where(r < 0.8, f[:, 23], np.where(
         r < 0.9, 1, rng.integers(0, 256, n))).astype(np.uint8)
     if valid:
-        O.cksum_process(f, stride, n, 3, False)
+        # (on a copy with a spare zero slot after the last frame: a frame
+        # whose IHL was raised above has its L4 bytes run past the slot, and
+        # the oracle's read of the last one must stay inside the array)
+        g = np.zeros((n + 1, stride), np.uint8)
+        g[:n] = f.reshape(n, stride)
+        O.cksum_process(g, stride, n, 3, False)
+        f.reshape(n, stride)[:] = g[:n]
     # UDP with checksum 0 (not set): stays 0
     l4 = 14 + 4 * ihl
     z = np.nonzero((f[:, 23] == 17) & (rng.random(n) < 0.2))[0]
