@@ -132,6 +132,7 @@ _SIGS = {
     "bg_em_bind_meta": (_int, [_vp, _int, _vp, _int]),
     "bg_wm_bind_meta": (_int, [_vp, _int, _vp, _int]),
     "bg_module_desc": (_int, [_vp, C.c_char_p, _sz]),
+    "bg_module_attr": (_int, [_vp, _int, C.c_char_p, _sz, C.POINTER(C.c_uint32)]),
     "bg_set_path_flags": (_int, [C.c_uint32]),
     "bg_get_path_flags": (C.c_uint32, []),
     "bg_is_ab_build": (_int, []),
@@ -145,6 +146,12 @@ _SIGS = {
     "bg_pipe_window": (_int, [_vp, C.POINTER(_int), C.POINTER(_int),
                               C.POINTER(_sz)]),
     "bg_pipe_submit": (_int, [_vp, _vp, _vp, _vp, _vp, _sz]),
+    "bg_pipe_submit_meta": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _sz]),
+    "bg_module_process_meta": (_int, [_vp, _vp, _vp, _vp, _sz, _vp]),
+    "bg_em_classify_staged": (_int, [_vp, _vp, _sz, _sz, _int, _int, _u16, _vp, _vp]),
+    "bg_wm_classify_staged": (_int, [_vp, _vp, _sz, _sz, _int, _int, _u16, _vp, _vp]),
+    "bg_em_meta_window": (_int, [_vp, C.POINTER(_int), C.POINTER(_int)]),
+    "bg_wm_meta_window": (_int, [_vp, C.POINTER(_int), C.POINTER(_int)]),
     "bg_pipe_flush": (_int, [_vp]),
     "bg_pipe_poll": (C.c_long, [_vp, _int, _vp, _vp, _sz]),
     "bg_pipe_pending": (_sz, [_vp]),

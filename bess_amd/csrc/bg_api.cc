@@ -381,6 +381,10 @@ struct bg_em {
   // by bg_em_bind_meta (meta_bound), otherwise = fields
   std::vector<bg_field> dfields;
   bool meta_bound = false;
+  // attr_offset() of each attribute (bind_meta): where staged rows (pipes,
+  // host paths) take each packet's attr field bytes from
+  std::vector<int32_t> attr_offs;
+  bool attrs_known = false;
   uint32_t key_size = 0;  // total_key_size_
   uint32_t raw_size = 0;  // raw_key_size_ (sum of field sizes)
   uint32_t kw = 1;        // device key words (1, 2, 4, 8)
@@ -589,7 +593,8 @@ int bg_em_sync(bg_em *em, int device, bg_stream_t stream) {
   return em_image(em, device, (hipStream_t)stream, &img);
 }
 
-static int em_launch(bg_em *em, EmImage *img, const void *d_frames, size_t stride,
+static int em_launch(const std::vector<bg_field> &df, EmImage *img, const void *d_frames,
+                     size_t stride,
                      size_t n, uint16_t default_gate, uint16_t *d_gates, int shift,
                      hipStream_t s) {
   EmArgs a;
@@ -599,7 +604,7 @@ static int em_launch(bg_em *em, EmImage *img, const void *d_frames, size_t strid
   a.n = n;
   a.gates = d_gates;
   a.default_gate = default_gate;
-  a.fp = make_plan(em->dfields, true, shift);
+  a.fp = make_plan(df, true, shift);
   a.t = img->t;
   img->used_on(s);
   HIP_TRY(launch_em(a, num_cus(img->device), s));
@@ -645,41 +650,104 @@ static int no_attr_datapath() {
 // 177-195 mt_offset_to_databuf_offset). The device slot carries the
 // metadata area at meta_off, so an attr field becomes an offset field at
 // meta_off + attr_offsets[attr_id].
-static int bind_meta(const std::vector<bg_field> &fields, int meta_off,
-                     const int32_t *attr_offsets, int nattrs,
-                     std::vector<bg_field> *out) {
-  if (meta_off < 0 || meta_off > 2048)
-    return fail(EINVAL, "meta_off %d not in [0,2048]", meta_off);
+static int resolve_attrs(const std::vector<bg_field> &fields, int meta_off,
+                         const std::vector<int32_t> &offs, std::vector<bg_field> *out) {
   std::vector<bg_field> d = fields;
   for (auto &f : d) {
     if (f.attr_id < 0) continue;
-    if (f.attr_id >= nattrs || !attr_offsets || attr_offsets[f.attr_id] < 0)
-      return fail(EINVAL, "attribute %d has no metadata offset", f.attr_id);
-    f.offset = meta_off + attr_offsets[f.attr_id];
+    f.offset = meta_off + offs[f.attr_id];
     f.attr_id = -1;
-    if (f.offset + 8 > 2048)  // raw 8-byte loads stay inside 2 KB
-      return fail(EINVAL, "metadata field at slot offset %d: past 2040", f.offset);
   }
   out->swap(d);
   return 0;
 }
 
+// bg_*_bind_meta: the attribute offsets (kept for staged rows) and, with
+// meta_off >= 0, the device slab's fields; meta_off -1: offsets only
+static int bind_meta(const std::vector<bg_field> &fields, int meta_off,
+                     const int32_t *attr_offsets, int nattrs,
+                     std::vector<int32_t> *offs, std::vector<bg_field> *out,
+                     bool *slab_bound) {
+  if (meta_off < -1 || meta_off > 2048)
+    return fail(EINVAL, "meta_off %d not in [-1,2048]", meta_off);
+  if (nattrs < 0 || nattrs > 64) return fail(EINVAL, "nattrs %d", nattrs);
+  std::vector<int32_t> o(attr_offsets ? attr_offsets : nullptr,
+                         attr_offsets ? attr_offsets + nattrs : nullptr);
+  for (auto &f : fields) {
+    if (f.attr_id < 0) continue;
+    if (f.attr_id >= nattrs || o[f.attr_id] < 0)
+      return fail(EINVAL, "attribute %d has no metadata offset", f.attr_id);
+    // (SNBUF_METADATA: a 128-byte area the attribute lies in)
+    if (o[f.attr_id] + f.size > 128)
+      return fail(EINVAL, "attribute %d at metadata offset %d: past the 128-byte area",
+                  f.attr_id, o[f.attr_id]);
+    if (meta_off >= 0 && meta_off + o[f.attr_id] + 8 > 2048)  // inside 2 KB
+      return fail(EINVAL, "metadata field at slot offset %d: past 2040",
+                  meta_off + o[f.attr_id]);
+  }
+  if (meta_off >= 0) {
+    resolve_attrs(fields, meta_off, o, out);
+    *slab_bound = true;
+  }
+  offs->swap(o);
+  return 0;
+}
+
+// The metadata bytes [lo, hi) the attr fields read (hi == lo: none)
+static int meta_window(const std::vector<bg_field> &fields, bool has_attr, bool known,
+                       const std::vector<int32_t> &offs, int *lo, int *hi) {
+  *lo = *hi = 0;
+  if (!has_attr) return 0;
+  if (!known)
+    return fail(ENOTSUP, "metadata-attribute (attr_name) fields: the attribute "
+                "offsets are not bound yet (bg_module_bind_meta)");
+  int l = 1 << 30, h = 0;
+  for (auto &f : fields) {
+    if (f.attr_id < 0) continue;
+    l = std::min(l, offs[f.attr_id]);
+    h = std::max(h, offs[f.attr_id] + f.size);
+  }
+  *lo = l;
+  *hi = h;
+  return 0;
+}
+
 }  // extern "C"
+
+// The fields a launch reads, in frame coordinates: the device slab's
+// (meta_row == kSlabMeta: attr fields at the bound meta_off) or a staged
+// row's (byte 0 = frame byte win_off; metadata byte 0 at row offset
+// meta_row, i.e. frame coordinate win_off + meta_row)
+static int em_fields_for(const bg_em *em, int win_off, int meta_row,
+                         std::vector<bg_field> *out) {
+  if (!em->has_attr) {
+    *out = em->fields;
+    return 0;
+  }
+  if (meta_row == bg::kSlabMeta) {
+    if (!em->meta_bound) return no_attr_datapath();
+    *out = em->dfields;
+    return 0;
+  }
+  if (!em->attrs_known) return no_attr_datapath();
+  return resolve_attrs(em->fields, win_off + meta_row, em->attr_offs, out);
+}
 
 namespace bg {
 // The device plan of a table for launches outside this file (the persistent
 // ring, bg_ring.cc): table synced to `device`, field plan of the slot layout.
 uint64_t em_version(const bg_em *em) { return em->version.load(std::memory_order_acquire); }
 
-int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off,
+int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off, int meta_row,
                    FieldPlan *fp, TableRef *t, int *read_end, uint64_t *version) {
-  if (em->has_attr && !em->meta_bound) return no_attr_datapath();
+  std::vector<bg_field> df;
+  if (int r = em_fields_for(em, win_off, meta_row, &df)) return r;
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
-  if (int r = check_extent(em->dfields, -win_off, 0xFFFF)) return r;
+  if (int r = check_extent(df, -win_off, 0xFFFF)) return r;
   EmImage *img;
   if (int r = em_image(em, device, s, &img)) return r;
   *version = img->version;
-  *fp = make_plan(em->dfields, true, -win_off);
+  *fp = make_plan(df, true, -win_off);
   *t = img->t;
   int hi = 0;  // bytes of a slot the kernel reads (check_extent)
   if (!fp->direct) {
@@ -691,6 +759,10 @@ int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off,
   *read_end = hi;
   return 0;
 }
+
+int em_meta_window(const bg_em *em, int *lo, int *hi) {
+  return meta_window(em->fields, em->has_attr, em->attrs_known, em->attr_offs, lo, hi);
+}
 }  // namespace bg
 
 extern "C" {
@@ -698,9 +770,10 @@ extern "C" {
 int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
                     int nattrs) {
   std::lock_guard<std::mutex> lk(em->mu);
-  int r = bind_meta(em->fields, meta_off, attr_offsets, nattrs, &em->dfields);
+  int r = bind_meta(em->fields, meta_off, attr_offsets, nattrs, &em->attr_offs,
+                    &em->dfields, &em->meta_bound);
   if (r) return r;
-  em->meta_bound = true;
+  em->attrs_known = true;
   return 0;
 }
 
@@ -714,16 +787,28 @@ int bg_em_classify(bg_em *em, const void *d_frames, size_t stride, size_t n,
 int bg_em_classify_window(bg_em *em, const void *d_frames, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,
                           uint16_t *d_gates, bg_stream_t stream) {
-  if (em->has_attr && !em->meta_bound) return no_attr_datapath();
+  return bg_em_classify_staged(em, d_frames, stride, n, win_off, bg::kSlabMeta,
+                               default_gate, d_gates, stream);
+}
+
+int bg_em_classify_staged(bg_em *em, const void *d_win, size_t stride, size_t n,
+                          int win_off, int meta_row, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream) {
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
-  if (stride % 16 || ((uintptr_t)d_frames & 15))
+  if (stride % 16 || ((uintptr_t)d_win & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
-  if (int r = check_extent(em->dfields, -win_off, stride)) return r;
+  std::vector<bg_field> df;
+  if (int r = em_fields_for(em, win_off, meta_row, &df)) return r;
+  if (int r = check_extent(df, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
   const int dev = current_device();
   EmImage *img;
   if (int r = em_image(em, dev, s, &img)) return r;
-  return em_launch(em, img, d_frames, stride, n, default_gate, d_gates, -win_off, s);
+  return em_launch(df, img, d_win, stride, n, default_gate, d_gates, -win_off, s);
+}
+
+int bg_em_meta_window(const bg_em *em, int *lo, int *hi) {
+  return bg::em_meta_window(em, lo, hi);
 }
 
 // Stage [lo, hi) of every head (window covering all fields) at a fixed
@@ -768,7 +853,7 @@ int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
   r = stage_windows(em->fields, heads, n, st, dev, &shift, &w);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
-  r = em_launch(em, img, st.d_in, w, n, default_gate,
+  r = em_launch(em->fields, img, st.d_in, w, n, default_gate,
                 reinterpret_cast<uint16_t *>(st.d_out), shift, s);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 2, hipMemcpyDeviceToHost, s));
@@ -777,14 +862,17 @@ int bg_em_process_host(bg_em *em, const uint8_t *const *heads, size_t n,
   return 0;
 }
 
+// the frame bytes the offset fields cover (attr fields read the metadata
+// area instead: bg_em_meta_window)
 static void fields_window(const std::vector<bg_field> &fields, int *lo,
                           int *hi) {
   int l = 1 << 30, h = 0;
   for (auto &f : fields) {
+    if (f.attr_id >= 0) continue;
     l = std::min(l, f.offset);
     h = std::max(h, f.offset + f.size);
   }
-  if (fields.empty()) l = h = 0;
+  if (h == 0) l = h = 0;
   *lo = l;
   *hi = h;
 }
@@ -961,6 +1049,8 @@ struct bg_wm {
   bool has_attr = false;
   std::vector<bg_field> dfields;  // as in bg_em
   bool meta_bound = false;
+  std::vector<int32_t> attr_offs;  // as in bg_em
+  bool attrs_known = false;
   uint32_t key_size = 0;
   uint32_t kw = 1;
   std::vector<WmTupleH> tuples;
@@ -985,6 +1075,21 @@ static Key wm_key(const bg_wm *wm, const uint8_t *p) {
   memset(&k, 0, sizeof(k));
   memcpy(k.w, p, wm->key_size);
   return k;
+}
+
+static int wm_fields_for(const bg_wm *wm, int win_off, int meta_row,
+                         std::vector<bg_field> *out) {  // as em_fields_for
+  if (!wm->has_attr) {
+    *out = wm->fields;
+    return 0;
+  }
+  if (meta_row == bg::kSlabMeta) {
+    if (!wm->meta_bound) return no_attr_datapath();
+    *out = wm->dfields;
+    return 0;
+  }
+  if (!wm->attrs_known) return no_attr_datapath();
+  return resolve_attrs(wm->fields, win_off + meta_row, wm->attr_offs, out);
 }
 
 static int wm_find_tuple(const bg_wm *wm, const Key &mask) {
@@ -1328,7 +1433,8 @@ int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream) {
   return wm_image(wm, device, (hipStream_t)stream, &img);
 }
 
-static int wm_launch(bg_wm *wm, WmImage *img, const void *d_frames, size_t stride,
+static int wm_launch(const std::vector<bg_field> &df, WmImage *img, const void *d_frames,
+                     size_t stride,
                      size_t n, uint16_t default_gate, uint16_t *d_gates, int shift,
                      hipStream_t s) {
   WmArgs a = img->a;
@@ -1337,7 +1443,7 @@ static int wm_launch(bg_wm *wm, WmImage *img, const void *d_frames, size_t strid
   a.n = n;
   a.gates = d_gates;
   a.default_gate = default_gate;
-  a.fp = make_plan(wm->dfields, false, shift);
+  a.fp = make_plan(df, false, shift);
   a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
   img->used_on(s);
   hipError_t e;
@@ -1412,9 +1518,10 @@ int bg_wm_jit_source(bg_wm *wm, int device, char *buf, size_t len, size_t *need)
 int bg_wm_bind_meta(bg_wm *wm, int meta_off, const int32_t *attr_offsets,
                     int nattrs) {
   std::lock_guard<std::mutex> lk(wm->mu);
-  int r = bind_meta(wm->fields, meta_off, attr_offsets, nattrs, &wm->dfields);
+  int r = bind_meta(wm->fields, meta_off, attr_offsets, nattrs, &wm->attr_offs,
+                    &wm->dfields, &wm->meta_bound);
   if (r) return r;
-  wm->meta_bound = true;
+  wm->attrs_known = true;
   return 0;
 }
 
@@ -1428,15 +1535,27 @@ int bg_wm_classify(bg_wm *wm, const void *d_frames, size_t stride, size_t n,
 int bg_wm_classify_window(bg_wm *wm, const void *d_frames, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,
                           uint16_t *d_gates, bg_stream_t stream) {
-  if (wm->has_attr && !wm->meta_bound) return no_attr_datapath();
+  return bg_wm_classify_staged(wm, d_frames, stride, n, win_off, bg::kSlabMeta,
+                               default_gate, d_gates, stream);
+}
+
+int bg_wm_classify_staged(bg_wm *wm, const void *d_win, size_t stride, size_t n,
+                          int win_off, int meta_row, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream) {
   if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
-  if (stride % 16 || ((uintptr_t)d_frames & 15))
+  if (stride % 16 || ((uintptr_t)d_win & 15))
     return fail(EINVAL, "frame slab must be 16-byte aligned with stride %% 16 == 0");
-  if (int r = check_extent(wm->dfields, -win_off, stride)) return r;
+  std::vector<bg_field> df;
+  if (int r = wm_fields_for(wm, win_off, meta_row, &df)) return r;
+  if (int r = check_extent(df, -win_off, stride)) return r;
   hipStream_t s = (hipStream_t)stream;
   WmImage *img;
   if (int r = wm_image(wm, current_device(), s, &img)) return r;
-  return wm_launch(wm, img, d_frames, stride, n, default_gate, d_gates, -win_off, s);
+  return wm_launch(df, img, d_win, stride, n, default_gate, d_gates, -win_off, s);
+}
+
+int bg_wm_meta_window(const bg_wm *wm, int *lo, int *hi) {
+  return meta_window(wm->fields, wm->has_attr, wm->attrs_known, wm->attr_offs, lo, hi);
 }
 
 int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
@@ -1455,7 +1574,7 @@ int bg_wm_process_host(bg_wm *wm, const uint8_t *const *heads, size_t n,
   r = stage_windows(wm->fields, heads, n, st, dev, &shift, &w);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.d_in, st.h_in, n * w, hipMemcpyHostToDevice, s));
-  r = wm_launch(wm, img, st.d_in, w, n, default_gate,
+  r = wm_launch(wm->fields, img, st.d_in, w, n, default_gate,
                 reinterpret_cast<uint16_t *>(st.d_out), shift, s);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(st.h_out, st.d_out, n * 2, hipMemcpyDeviceToHost, s));

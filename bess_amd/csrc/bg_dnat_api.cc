@@ -522,7 +522,10 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (h->device >= 0) dev = h->device;
-  hipStream_t s = thread_stream(dev, (hipStream_t)stream);
+  // the caller's stream as given (NULL: the legacy default stream): the
+  // kernels read and rewrite the caller's slab and gates, so they must run
+  // after the caller's earlier work on them
+  hipStream_t s = (hipStream_t)stream;
   int r = h->sync(dev, s);
   if (r) return r;
   r = h->ensure_batch(n);

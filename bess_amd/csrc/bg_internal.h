@@ -100,8 +100,17 @@ struct Staging {
 Staging &thread_staging();
 // bg_api.cc: a table's field plan for slots that start at frame byte
 // win_off, its synced device table, and the rule version that image holds
-int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off,
+// meta_row: where a staged row carries the packet's metadata area (row
+// offset of its byte 0; attr fields only), or kSlabMeta for a device slab
+// laid out by bg_em_bind_meta
+constexpr int kSlabMeta = -(1 << 30);
+int em_device_plan(bg_em *em, int device, hipStream_t s, int win_off, int meta_row,
                    FieldPlan *fp, TableRef *t, int *read_end, uint64_t *version);
+// the metadata bytes [lo, hi) the attr fields read (none: lo == hi == 0)
+int em_meta_window(const bg_em *em, int *lo, int *hi);
+// bg_ring.cc: bg_em_ring_create over staged rows with metadata at meta_row
+int em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
+                   uint32_t idle_us, int win_off, int meta_row, bg_ring **out);
 uint64_t em_version(const bg_em *em);  // bumped by every rule change
 // bg_ring.cc: the rule version a ring classifies with; whether a lane's
 // ticket has finished (one host word, no lock)

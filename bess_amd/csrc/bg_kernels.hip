@@ -464,9 +464,10 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
 // lane's next ticket (one atomic; claims run ahead of publication, so the
 // lane's workgroups queue up on its coming tickets), waits until it is
 // published, reads the descriptor (every word tagged with the ticket),
+// acquires (system scope: no line of an earlier batch survives in L1/L2),
 // classifies the batch, writes the gates through to memory (sc0 sc1
-// stores: no L2 write-back per ticket) and marks the ticket done in host
-// memory. Create a ring with as many lanes as workers submit on.
+// stores) and marks the ticket done in host memory with a system-scope
+// release. Create a ring with as many lanes as workers submit on.
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
@@ -516,6 +517,13 @@ void em_ring_kernel(RingArgs a) {
         const uint64_t tag = (t + 1) & 0xFFFF;
         const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
+        // acquire at system scope: the batch's frames were written (by the
+        // host or a copy) before the descriptor was published, and this
+        // grid outlives many batches, so lines of an earlier batch in the
+        // same buffer may still sit in this CU's L1 or the XCD's L2 (mapped
+        // host memory is cached there as non-coherent lines): invalidate
+        // them before any wave reads the frames (after the barrier below)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       }
 #ifdef BG_AB
       if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
@@ -563,7 +571,9 @@ void em_ring_kernel(RingArgs a) {
                                               : nullptr;
       if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-      __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
+      // release at system scope: every wave's gate stores (drained above,
+      // before the barrier) are visible to the host before the done word
+      __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef BG_AB
       if (tr) {

@@ -164,7 +164,10 @@ int bg_rewrite_process(bg_rewrite *h, int device, void *d_slots, size_t stride,
     return fail(EINVAL, "slots and headroom must be 16-byte aligned");
   int r = set_device(device);
   if (r) return r;
-  hipStream_t s = thread_stream(device, (hipStream_t)stream);
+  // the caller's stream as given (NULL: the legacy default stream), so the
+  // kernel is ordered after the caller's earlier work on the slots and the
+  // head / len arrays (a private non-blocking stream would not be)
+  hipStream_t s = (hipStream_t)stream;
   r = sync_templates(h, device, s);
   if (r) return r;
   RewriteArgs a;
@@ -185,7 +188,6 @@ int bg_rewrite_process(bg_rewrite *h, int device, void *d_slots, size_t stride,
   a.len = d_len;
   HIP_TRY(launch_rewrite(a, num_cus(device), s));
   if (nt > 1) h->next = (h->next + n) % nt;  // consecutive batches' turns
-  if (!stream) HIP_TRY(hipStreamSynchronize(s));
   return 0;
 }
 

@@ -204,17 +204,34 @@ uint64_t *host_writable_device_alloc(size_t bytes) {
   return static_cast<uint64_t *>(d);
 }
 
-// the lane for this call (see RingLane::busy); ok false: in use elsewhere
+// the lane for this call (see RingLane::busy); ok false: in use elsewhere.
+// `claim`: take the flag with an exchange (wait / completed, which are not
+// per-ticket paths); submit checks it with plain loads and stores (no
+// locked instruction per ticket), so there EBUSY is best-effort detection
+// of a second thread on the lane, not a guarantee (include/bessgpu.h)
 struct LaneUse {
   RingLane &l;
   const bool ok;
-  explicit LaneUse(RingLane &x) : l(x), ok(x.busy.load(std::memory_order_acquire) == 0) {
-    if (ok) l.busy.store(1, std::memory_order_relaxed);
+  LaneUse(RingLane &x, bool claim)
+      : l(x),
+        ok(claim ? x.busy.exchange(1, std::memory_order_acquire) == 0
+                 : x.busy.load(std::memory_order_acquire) == 0) {
+    if (ok && !claim) l.busy.store(1, std::memory_order_relaxed);
   }
   ~LaneUse() {
     if (ok) l.busy.store(0, std::memory_order_release);
   }
 };
+
+// The grid faulted or was aborted (its dispatcher never wrote h_ended):
+// -EIO with the HIP error. Called on the slow paths only (lane full,
+// waiting), never per ticket.
+int grid_failed(bg_ring *r) {
+  if (r->launch_id.load(std::memory_order_acquire) == 0) return 0;
+  const hipError_t e = hipEventQuery(r->ev);
+  if (e == hipSuccess || e == hipErrorNotReady) return 0;
+  return fail(EIO, "ring kernel: HIP error %d: %s", (int)e, hipGetErrorString(e));
+}
 
 int lane_busy(int lane) {
   return fail(EBUSY, "lane %d in use by another thread (one worker per lane)", lane);
@@ -242,6 +259,14 @@ extern "C" {
 
 int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
                       uint32_t idle_us, int win_off, bg_ring **out) {
+  return bg::em_ring_create(em, device, lanes, slots, blocks, idle_us, win_off,
+                            bg::kSlabMeta, out);
+}
+
+}  // extern "C"
+
+int bg::em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
+                       uint32_t idle_us, int win_off, int meta_row, bg_ring **out) {
   if (!em || !out) return fail(EINVAL, "bad arguments");
   if (lanes < 1 || lanes > kRingMaxLanes)
     return fail(EINVAL, "lanes %d not in [1,%d]", lanes, kRingMaxLanes);
@@ -318,7 +343,8 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
     delete r;
     return fail(EIO, "no device address for the ring's host memory");
   }
-  rc = em_device_plan(em, device, r->st, win_off, &a.fp, &a.t, &r->read_end, &r->version);
+  rc = em_device_plan(em, device, r->st, win_off, meta_row, &a.fp, &a.t, &r->read_end,
+                      &r->version);
   if (rc == 0) {
     // The ring classifies with the rule set as of its creation: it keeps
     // its own copy of the table image, so a later rule change (bessd makes
@@ -341,6 +367,8 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
   return 0;
 }
 
+extern "C" {
+
 void bg_ring_destroy(bg_ring *r) {
   if (!r) return;
   ring_release(r);
@@ -359,17 +387,22 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
       ((uintptr_t)frames & 15) || (stride & 15))
     return fail(EINVAL, "frames 16-byte aligned with stride %% 16 == 0 below 2^48");
   RingLane &l = r->lanes[lane];
-  LaneUse use(l);
+  LaneUse use(l, false);
   if (!use.ok) return lane_busy(lane);
   // lane full: its oldest ticket must finish before its slot is reused
   if (l.next - l.done_upto.load(std::memory_order_relaxed) >= r->nslots) {
     if (r->d_desc) _mm_sfence();  // (the last descriptor out before we wait)
     const double t0 = now_s();
-    for (;;) {
+    for (uint64_t spin = 0;; spin++) {
       retire(r, l);
       if (l.next - l.done_upto.load(std::memory_order_relaxed) < r->nslots) break;
       if (int rc = ensure_running(r)) return rc;
-      if (now_s() - t0 > 10.0) return fail(ETIMEDOUT, "ring lane full for 10 s");
+      if ((spin & 1023) == 1023)
+        if (int rc = grid_failed(r)) return rc;
+      if (now_s() - t0 > 10.0) {
+        if (int rc = grid_failed(r)) return rc;
+        return fail(ETIMEDOUT, "ring lane full for 10 s");
+      }
       _mm_pause();
     }
   }
@@ -397,17 +430,22 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
 int bg_ring_wait(bg_ring *r, int lane, int64_t ticket) {
   if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
   RingLane &l = r->lanes[lane];
-  LaneUse use(l);
+  LaneUse use(l, true);
   if (!use.ok) return lane_busy(lane);
   if (ticket < 0 || (uint64_t)ticket >= l.next)
     return fail(EINVAL, "ticket %lld not submitted", (long long)ticket);
   if (r->d_desc) _mm_sfence();  // this submitter's last descriptor out to the device
   const double t0 = now_s();
-  for (;;) {
+  for (uint64_t spin = 0;; spin++) {
     retire(r, l);
     if ((uint64_t)ticket < l.done_upto.load(std::memory_order_relaxed)) return 0;
     if (int rc = ensure_running(r)) return rc;
-    if (now_s() - t0 > 10.0) return fail(ETIMEDOUT, "ticket %lld: 10 s", (long long)ticket);
+    if ((spin & 1023) == 1023)
+      if (int rc = grid_failed(r)) return rc;
+    if (now_s() - t0 > 10.0) {
+      if (int rc = grid_failed(r)) return rc;
+      return fail(ETIMEDOUT, "ticket %lld: 10 s", (long long)ticket);
+    }
     _mm_pause();
   }
 }
@@ -415,7 +453,7 @@ int bg_ring_wait(bg_ring *r, int lane, int64_t ticket) {
 int64_t bg_ring_completed(bg_ring *r, int lane) {
   if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
   RingLane &l = r->lanes[lane];
-  LaneUse use(l);
+  LaneUse use(l, true);
   if (!use.ok) return lane_busy(lane);
   retire(r, l);
   if (int rc = ensure_running(r)) return rc;

@@ -118,11 +118,22 @@ class ExactMatch final : public Module {
 
   int ProcessDeviceWindow(const bg_ctx &c, void *d_win, size_t wstride, size_t n,
                           int win_off, uint16_t *d_ogates, void *stream) override {
-    if (!all_attrs().empty()) return -ENOTSUP;  // staged windows: no metadata
     int rc = bg_em_sync(table_, c.device, stream);
     if (rc < 0) return rc;
-    return bg_em_classify_window(table_, d_win, wstride, n, win_off,
+    return bg_em_classify_staged(table_, d_win, wstride, n, win_off, StagedMetaRow(),
                                  default_gate_, d_ogates, stream);
+  }
+
+  int MetaWindow(int *mlo, int *mhi) const override {
+    return bg_em_meta_window(table_, mlo, mhi);
+  }
+
+  // the row offset of metadata byte 0 in a staged row (module.h StagedMetaAt)
+  int StagedMetaRow() const {
+    int lo, hi, mlo, mhi;
+    bg_em_window(table_, &lo, &hi);
+    if (bg_em_meta_window(table_, &mlo, &mhi) < 0 || mlo == mhi) return 0;
+    return StagedMetaAt(lo, hi) - mlo;
   }
 
   // A pipe's slots go to one persistent classify kernel per device (bg_ring:
@@ -133,18 +144,23 @@ class ExactMatch final : public Module {
   static const int kPipeRingLanes = 16;
   int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) override {
     out->reset();
-    if (!all_attrs().empty() || (bg_get_path_flags() & BG_PATH_PIPE_NO_RING)) return 0;
+    if (bg_get_path_flags() & BG_PATH_PIPE_NO_RING) return 0;
+    int mlo, mhi;
+    if (int rc = MetaWindow(&mlo, &mhi)) return rc;
+    const int meta_row = StagedMetaRow();  // (attr fields: rows carry metadata)
     std::lock_guard<std::mutex> lk(ring_mu_);
     std::shared_ptr<PipeRing> &cur = rings_[device];
-    if (!cur || cur->version != bg::em_version(table_)) {
+    if (!cur || cur->version != bg::em_version(table_) || cur->meta_row != meta_row) {
       int lo = 0, hi = 0;
       bg_em_window(table_, &lo, &hi);
       bg_ring *r = nullptr;
-      const int rc = bg_em_ring_create(table_, device, kPipeRingLanes, 64,
-                                       2 * bg::num_cus(device), 10000, lo, &r);
+      const int rc = bg::em_ring_create(table_, device, kPipeRingLanes, 64,
+                                        2 * bg::num_cus(device), 10000, lo,
+                                        mlo == mhi ? bg::kSlabMeta : meta_row, &r);
       if (rc < 0) return rc;
       auto pr = std::make_shared<PipeRing>();
       pr->r = r;
+      pr->meta_row = meta_row;
       pr->device = device;
       pr->lanes = kPipeRingLanes;
       pr->lane_mu.reset(new std::mutex[kPipeRingLanes]);

@@ -89,22 +89,31 @@ bg_ctx ResolveCtx(const bg_ctx *c, int module_device) {
 // The synchronous host datapath shared by every module (see module.h).
 int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) {
   if (cnt == 0) return 0;
-  int lo, hi;
+  int lo, hi, mlo, mhi;
   bool wb;
   DeviceWindow(&lo, &hi, &wb);
-  uint32_t span = 0xFFFFFFFFu;
-  for (size_t i = 0; i < cnt; i++) span = std::min(span, pkts[i]->span());
-  if (hi > (int)span) hi = (int)span;
-  if (hi <= lo) hi = lo + 1;
-  const size_t len = (size_t)(hi - lo);
-  const size_t w = (len + 15) / 16 * 16;
-  const size_t line = std::min<size_t>(w, 128);  // header line written back
-  const bg_ctx &c = ctx->call;
-  int r = bg::set_device(c.device);
   auto drop_all = [&](int rc) {
     for (size_t i = 0; i < cnt; i++) DropPacket(ctx, pkts[i]);
     return rc;
   };
+  int r = MetaWindow(&mlo, &mhi);
+  if (r) return drop_all(r);
+  const bool meta = mhi > mlo;  // attr fields: the row carries metadata too
+  if (meta)
+    for (size_t i = 0; i < cnt; i++)
+      if (!pkts[i]->metadata<uint8_t *>())
+        return drop_all(fail(EINVAL, "the module reads metadata attributes: "
+                             "pass each packet's metadata area"));
+  uint32_t span = 0xFFFFFFFFu;
+  for (size_t i = 0; i < cnt; i++) span = std::min(span, pkts[i]->span());
+  if (!meta && hi > (int)span) hi = (int)span;
+  if (hi <= lo) hi = lo + 1;
+  const size_t len = (size_t)(hi - lo);
+  const size_t w = meta ? StagedStride(lo, hi, mlo, mhi) : (len + 15) / 16 * 16;
+  const size_t mat = (size_t)StagedMetaAt(lo, hi), mlen = (size_t)(mhi - mlo);
+  const size_t line = std::min<size_t>(w, 128);  // header line written back
+  const bg_ctx &c = ctx->call;
+  r = bg::set_device(c.device);
   if (r) return drop_all(r);
   bg::Staging &st = bg::thread_staging();
   // +64 B: the last window's 16-byte loads may run past its slot
@@ -115,6 +124,7 @@ int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) 
     uint8_t *dst = st.h_in + i * w;
     memcpy(dst, pkts[i]->head_data<uint8_t *>() + lo, len);
     if (w > len) memset(dst + len, 0, w - len);
+    if (meta) memcpy(dst + mat, pkts[i]->metadata<uint8_t *>() + mlo, mlen);
   }
   uint16_t *d_g = reinterpret_cast<uint16_t *>(st.d_out);
   hipError_t e = hipMemcpyAsync(st.d_in, st.h_in, cnt * w, hipMemcpyHostToDevice, s);
@@ -140,6 +150,10 @@ int Module::ProcessPackets(Context *ctx, bess::Packet *const *pkts, size_t cnt) 
   return 0;
 }
 
+void ModuleUnref(bg_module *m) {
+  if (m->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete m;
+}
+
 static int respond(const CommandResponse &r) {
   if (r.code() != 0) return fail(r.code(), "%s", r.errmsg().c_str());
   bg::g_err.clear();
@@ -162,7 +176,9 @@ int bg_module_create(const char *mclass, const void *arg, size_t arg_len,
   return 0;
 }
 
-void bg_module_destroy(bg_module *m) { delete m; }
+void bg_module_destroy(bg_module *m) {
+  if (m) ModuleUnref(m);
+}
 
 // ModuleBuilder::RunCommand (core/module.cc:92-116)
 int bg_module_command(bg_module *h, const char *cmd, const void *arg,
@@ -201,13 +217,14 @@ int bg_module_command(bg_module *h, const char *cmd, const void *arg,
 }
 
 static int process(bg_module *h, const bg_ctx *call, uint8_t *const *heads,
-                   size_t cnt, uint16_t *ogates, EmitLog *log) {
+                   uint8_t *const *metas, size_t cnt, uint16_t *ogates, EmitLog *log) {
   std::shared_lock<std::shared_mutex> lk(h->mu);  // many workers at once
   for (size_t i = 0; i < cnt; i++) ogates[i] = BG_GATE_NONE;
   std::vector<bess::Packet> pkts(cnt);
   std::vector<bess::Packet *> ptrs(cnt);
   for (size_t i = 0; i < cnt; i++) {
-    pkts[i] = bess::Packet(heads[i], 2048, (uint32_t)i);  // SNBUF_DATA span
+    pkts[i] = bess::Packet(heads[i], 2048, (uint32_t)i,  // SNBUF_DATA span
+                           metas ? metas[i] : nullptr);
     ptrs[i] = &pkts[i];
   }
   Context ctx;
@@ -220,7 +237,12 @@ static int process(bg_module *h, const bg_ctx *call, uint8_t *const *heads,
 
 int bg_module_process(bg_module *h, const bg_ctx *ctx, uint8_t *const *heads,
                       size_t cnt, uint16_t *ogates) {
-  return process(h, ctx, heads, cnt, ogates, nullptr);
+  return process(h, ctx, heads, nullptr, cnt, ogates, nullptr);
+}
+
+int bg_module_process_meta(bg_module *h, const bg_ctx *ctx, uint8_t *const *heads,
+                           uint8_t *const *metas, size_t cnt, uint16_t *ogates) {
+  return process(h, ctx, heads, metas, cnt, ogates, nullptr);
 }
 
 int bg_module_process_batches(bg_module *h, const bg_ctx *ctx,
@@ -229,7 +251,7 @@ int bg_module_process_batches(bg_module *h, const bg_ctx *ctx,
                               uint32_t *batch_len, uint32_t *pkt_idx,
                               size_t *nbatches, size_t *ndead) {
   EmitLog log;
-  int r = process(h, ctx, heads, cnt, ogates, &log);
+  int r = process(h, ctx, heads, nullptr, cnt, ogates, &log);
   if (r < 0) return r;
   size_t k = 0;
   for (size_t b = 0; b < log.batches.size(); b++) {
@@ -249,7 +271,7 @@ int bg_module_run(bg_module *h, const bg_ctx *ctx, uint8_t *const *heads,
                   size_t n, size_t burst, uint16_t *ogates) {
   if (burst < 1) return fail(EINVAL, "burst must be >= 1");
   for (size_t i = 0; i < n; i += burst) {
-    int r = process(h, ctx, heads + i, std::min(burst, n - i), ogates + i, nullptr);
+    int r = process(h, ctx, heads + i, nullptr, std::min(burst, n - i), ogates + i, nullptr);
     if (r < 0) return r;
   }
   return 0;
@@ -296,6 +318,14 @@ int bg_module_bind_meta(bg_module *h, int meta_off, const char *const *names,
     return fail(ENOTSUP, "'%s' has no metadata fields on its datapath",
                 h->mclass.c_str());
   return r;
+}
+
+int bg_module_attr(const bg_module *h, int i, char *name, size_t cap, uint32_t *size) {
+  const auto &a = h->m->all_attrs();
+  if (i < 0 || (size_t)i >= a.size()) return 0;
+  if (name && cap) snprintf(name, cap, "%s", a[(size_t)i].name.c_str());
+  if (size) *size = (uint32_t)a[(size_t)i].size;
+  return 1;
 }
 
 int bg_module_desc(const bg_module *h, char *buf, size_t len) {

@@ -43,17 +43,24 @@ namespace bess {
 class Packet {
  public:
   Packet() = default;
-  Packet(uint8_t *head, uint32_t span, uint32_t index)
-      : head_(head), span_(span), index_(index) {}
+  Packet(uint8_t *head, uint32_t span, uint32_t index, uint8_t *meta = nullptr)
+      : head_(head), meta_(meta), span_(span), index_(index) {}
   template <typename T = void *>
   T head_data() const {
     return reinterpret_cast<T>(head_);
+  }
+  // the packet's metadata area (Packet::metadata(), core/packet.h; the
+  // snbuf's SNBUF_METADATA bytes), when the caller passed it
+  template <typename T = void *>
+  T metadata() const {
+    return reinterpret_cast<T>(meta_);
   }
   uint32_t span() const { return span_; }
   uint32_t index() const { return index_; }
 
  private:
   uint8_t *head_ = nullptr;
+  uint8_t *meta_ = nullptr;
   uint32_t span_ = 0;
   uint32_t index_ = 0;
 };
@@ -128,6 +135,17 @@ CommandResponse CommandFailure(int code, const char *fmt = nullptr, ...)
 
 class Module;
 
+// The staged row of one packet (bg_pipe slots, Module::ProcessPackets):
+// frame bytes [lo, hi) at row offset 0, then, for a module whose attr_name
+// fields read the metadata area (Module::MetaWindow [mlo, mhi)), those
+// metadata bytes at row offset StagedMetaAt(lo, hi) -- so metadata byte 0
+// sits at row offset StagedMetaAt(lo, hi) - mlo (bg_em_classify_staged's
+// meta_row). Row stride: StagedStride.
+inline int StagedMetaAt(int lo, int hi) { return (hi - lo + 15) / 16 * 16; }
+inline size_t StagedStride(int lo, int hi, int mlo, int mhi) {
+  return (size_t)StagedMetaAt(lo, hi) + (size_t)((mhi - mlo + 15) / 16 * 16);
+}
+
 // A persistent ring (bg_ring) serving a module's staged windows on one
 // device, shared by the module's pipes (each on a lane of its own while
 // there are lanes) and by their in-flight slots: it is destroyed -- its
@@ -138,6 +156,7 @@ struct PipeRing {
   int device = 0;
   int lanes = 0;
   uint64_t version = 0;  // the rules it classifies with
+  int meta_row = 0;      // where its rows carry the metadata (StagedMetaAt)
   std::atomic<int> next_lane{0};
   // pipes past `lanes` share a lane; bg_ring's lanes take one thread at a
   // time (EBUSY otherwise), so a pipe holds its lane's lock around each call
@@ -204,8 +223,16 @@ class Module {
     *hi = 2048;  // SNBUF_DATA (core/snbuf_layout.h:34-68)
     *writeback = false;
   }
-  // ProcessDevice over staged windows: byte 0 of window i is frame offset
-  // `win_off` of packet i.
+  // The metadata bytes [*mlo, *mhi) the device datapath reads (attr_name
+  // fields), staged after the frame window (StagedMetaAt);
+  // none: *mlo == *mhi. -errno while the attribute offsets are unbound.
+  virtual int MetaWindow(int *mlo, int *mhi) const {
+    *mlo = *mhi = 0;
+    return 0;
+  }
+  // ProcessDevice over staged rows: byte 0 of row i is frame offset
+  // `win_off` of packet i (= DeviceWindow's lo), followed by the packet's
+  // metadata bytes as StagedMetaAt lays them out when MetaWindow has any.
   virtual int ProcessDeviceWindow(const bg_ctx &c, void *d_win, size_t wstride,
                                   size_t n, int win_off, uint16_t *d_ogates,
                                   void *stream) {
@@ -222,9 +249,10 @@ class Module {
     out->reset();
     return 0;
   }
-  // attr_name fields: metadata area at slot offset meta_off, attribute
-  // offsets by name (bg_module_bind_meta). Modules without attr fields on
-  // their datapath: ENOTSUP.
+  // attr_name fields: metadata area at slot offset meta_off (-1: none, the
+  // attribute offsets only -- staged rows carry the metadata bytes),
+  // attribute offsets by name (bg_module_bind_meta). Modules without attr
+  // fields on their datapath: ENOTSUP.
   virtual int BindMeta(int meta_off, const std::vector<std::string> &names,
                        const std::vector<int32_t> &offsets) {
     (void)meta_off;
@@ -367,7 +395,14 @@ struct bg_module {
   // change is classified with the rules it was submitted under
   std::mutex pipes_mu;
   std::set<bg_pipe *> pipes;
+  // the owner's handle (bg_module_destroy) and every open pipe hold one
+  // reference: a module destroyed under open pipes lives until the last
+  // pipe goes (a host may tear its graph down in any order)
+  std::atomic<int> refs{1};
 };
+
+// drop one reference (the owner's or a pipe's); the last one frees it
+void ModuleUnref(bg_module *m);
 
 // pipe.cc: launch a pipe's partly filled slot (its module's lock is held
 // by the caller)

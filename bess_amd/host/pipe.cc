@@ -60,6 +60,7 @@ struct Slot {
   uint64_t *d_done = nullptr;  // its device address (hipStreamWriteValue64)
   uint64_t seq = 0;            // this launch's number
   std::vector<uint8_t *> heads;  // writeback targets; the lagging gather's sources
+  std::vector<uint8_t *> metas;  // metadata areas (modules with attr fields)
   size_t gathered = 0;           // packets [0, gathered) are in h_in
   std::vector<uint16_t> wblen;   // bytes of the header line to write back
   std::vector<void *> cookies;
@@ -85,6 +86,11 @@ struct bg_pipe {
   size_t batch = 0;
   int lo = 0, hi = 0;    // staged frame bytes [lo, hi)
   size_t w = 0;          // staged stride (16-byte multiple)
+  // attr fields (Module::MetaWindow): metadata bytes [mlo, mhi) of each
+  // packet staged at row offset mat (module.h StagedMetaAt)
+  bool meta = false;
+  int mlo = 0, mhi = 0;
+  size_t mat = 0;
   bool writeback = false;
   unsigned ctx_use = 0;  // Module::CtxUse(): the context fields a slot fixes
   bool ring_mode = false;          // slots go to the module's ring
@@ -175,7 +181,15 @@ static inline void copy16(uint8_t *dst, const uint8_t *src, size_t w) {
 // whole before it launches.
 static void gather(bg_pipe *p, Slot &s) {
   uint8_t *dst = s.h_in + s.gathered * p->w;
-  for (size_t j = s.gathered; j < s.n; j++, dst += p->w) copy16(dst, s.heads[j] + p->lo, p->w);
+  if (p->meta) {
+    const size_t ml = (size_t)(p->mhi - p->mlo);
+    for (size_t j = s.gathered; j < s.n; j++, dst += p->w) {
+      copy16(dst, s.heads[j] + p->lo, p->mat);
+      memcpy(dst + p->mat, s.metas[j] + p->mlo, ml);
+    }
+  } else {
+    for (size_t j = s.gathered; j < s.n; j++, dst += p->w) copy16(dst, s.heads[j] + p->lo, p->w);
+  }
   s.gathered = s.n;
 }
 
@@ -197,6 +211,11 @@ static int launch_slot(bg_pipe *p) {
       p->ring = ring;
       p->lane = ring->next_lane.fetch_add(1) % ring->lanes;
     }
+    // the gathered windows reach memory before the descriptor that points
+    // at them (the descriptor goes out through write-combining buffers,
+    // which x86 does not order after earlier write-back stores): one
+    // fence per slot
+    _mm_sfence();
     int64_t t;
     {
       std::lock_guard<std::mutex> lk(ring->lane_mu[p->lane]);
@@ -328,6 +347,16 @@ static long take_done(bg_pipe *p, bool wait, void **cookies, uint16_t *gates,
   return (long)k;
 }
 
+// mapped pinned memory the device reads uncached (see bg_pipe_create)
+static hipError_t host_alloc_uc(void **p, size_t bytes) {
+  hipError_t e = hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocUncached);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    e = hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  }
+  return e;
+}
+
 extern "C" {
 
 int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
@@ -342,9 +371,19 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
   p->device = device;
   p->batch = batch;
   m->m->DeviceWindow(&p->lo, &p->hi, &p->writeback);
-  if (span && p->lo == 0 && (int)span < p->hi) p->hi = (int)span;
+  r = m->m->MetaWindow(&p->mlo, &p->mhi);
+  if (r < 0) {
+    delete p;
+    return r;
+  }
+  p->meta = p->mhi > p->mlo;
+  if (span && !p->meta && p->lo == 0 && (int)span < p->hi) p->hi = (int)span;
   if (p->hi <= p->lo) p->hi = p->lo + 1;
   p->w = ((size_t)(p->hi - p->lo) + 15) / 16 * 16;
+  if (p->meta) {
+    p->mat = (size_t)StagedMetaAt(p->lo, p->hi);
+    p->w = StagedStride(p->lo, p->hi, p->mlo, p->mhi);
+  }
   p->ctx_use = m->m->CtxUse();
   if (!p->writeback) {
     uint16_t dflt = 0;
@@ -359,11 +398,14 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
   p->slots.resize((size_t)depth);
   for (Slot &s : p->slots) {
     if (p->ring_mode) {
-      // the kernel reads the windows and writes the gates in place (mapped,
-      // coherent: never cached on the device, so a refilled slot is seen)
-      const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-      hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.h_in), batch * p->w + 64, fl);
-      if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&s.h_g), batch * 2 + 64, fl);
+      // the kernel reads the windows and writes the gates in place. Mapped
+      // uncached (MTYPE UC): a refilled slot's windows are never served
+      // from a line an earlier batch left in the device's L1/L2 (coherent
+      // host memory alone is cached there as non-coherent lines, and the
+      // ring's grid outlives many batches; the kernel also acquires at
+      // system scope per ticket). Coherent when UC is not available.
+      hipError_t e = host_alloc_uc(reinterpret_cast<void **>(&s.h_in), batch * p->w + 64);
+      if (e == hipSuccess) e = host_alloc_uc(reinterpret_cast<void **>(&s.h_g), batch * 2 + 64);
       if (e == hipSuccess)
         e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dv_in), s.h_in, 0);
       if (e == hipSuccess)
@@ -375,6 +417,7 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
       }
       s.cookies.resize(batch);
       s.heads.resize(batch);
+      if (p->meta) s.metas.resize(batch);
       continue;
     }
     // +64 B: window loads of the last packet may run past its slot
@@ -402,12 +445,14 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
     }
     s.cookies.resize(batch);
     s.heads.resize(batch);
+    if (p->meta) s.metas.resize(batch);
     if (p->writeback) s.wblen.resize(batch);
   }
   {
     std::lock_guard<std::mutex> lk(m->pipes_mu);
     m->pipes.insert(p);
   }
+  m->refs.fetch_add(1, std::memory_order_relaxed);  // released by bg_pipe_destroy
   *out = p;
   return 0;
 }
@@ -423,7 +468,9 @@ void bg_pipe_destroy(bg_pipe *p) {
     pipe_release(p);
     p->ring.reset();
   }
+  bg_module *m = p->mod;
   delete p;
+  ModuleUnref(m);  // the module's last reference may be this pipe's
 }
 
 int bg_pipe_window(const bg_pipe *p, int *lo, int *hi, size_t *stride) {
@@ -441,20 +488,31 @@ static bool same_ctx(unsigned use, const bg_ctx &a, const bg_ctx &b) {
 }
 
 static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
-                  const uint16_t *lens, void *const *cookies, size_t cnt);
+                  uint8_t *const *metas, const uint16_t *lens, void *const *cookies,
+                  size_t cnt);
 
 int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                    const uint16_t *lens, void *const *cookies, size_t cnt) {
+  return bg_pipe_submit_meta(p, ctx, heads, nullptr, lens, cookies, cnt);
+}
+
+int bg_pipe_submit_meta(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                        uint8_t *const *metas, const uint16_t *lens,
+                        void *const *cookies, size_t cnt) {
   std::lock_guard<std::mutex> lk(p->mu);
   const uint64_t t0 = __rdtsc();
-  const int r = submit(p, ctx, heads, lens, cookies, cnt);
+  const int r = submit(p, ctx, heads, metas, lens, cookies, cnt);
   p->st_submit_tsc += __rdtsc() - t0;
   return r;
 }
 
 static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
-                  const uint16_t *lens, void *const *cookies, size_t cnt) {
+                  uint8_t *const *metas, const uint16_t *lens, void *const *cookies,
+                  size_t cnt) {
   if (p->err) return p->err;
+  if (p->meta && !metas && cnt)  // (not sticky: nothing was taken)
+    return fail(EINVAL, "the module reads metadata attributes: submit each "
+                "packet's metadata area (bg_pipe_submit_meta)");
   int r;
   if (!p->writeback) gather(p, p->slots[p->fill]);  // the previous call's packets
   const bg_ctx c = ResolveCtx(ctx, p->device);
@@ -496,6 +554,10 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
         // copied by the next call's gather
         __builtin_prefetch(src);
         s.heads[s.n + j] = heads[k];
+        if (p->meta) {
+          __builtin_prefetch(metas[k] + p->mlo);
+          s.metas[s.n + j] = metas[k];
+        }
       } else {
         if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
         // the frame (data_len bytes when given, at least its header line),

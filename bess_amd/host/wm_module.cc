@@ -104,11 +104,22 @@ class WildcardMatch final : public Module {
 
   int ProcessDeviceWindow(const bg_ctx &c, void *d_win, size_t wstride, size_t n,
                           int win_off, uint16_t *d_ogates, void *stream) override {
-    if (!all_attrs().empty()) return -ENOTSUP;  // staged windows: no metadata
     int rc = bg_wm_sync(table_, c.device, stream);
     if (rc < 0) return rc;
-    return bg_wm_classify_window(table_, d_win, wstride, n, win_off,
+    return bg_wm_classify_staged(table_, d_win, wstride, n, win_off, StagedMetaRow(),
                                  default_gate_, d_ogates, stream);
+  }
+
+  int MetaWindow(int *mlo, int *mhi) const override {
+    return bg_wm_meta_window(table_, mlo, mhi);
+  }
+
+  // the row offset of metadata byte 0 in a staged row (module.h StagedMetaAt)
+  int StagedMetaRow() const {
+    int lo, hi, mlo, mhi;
+    bg_wm_window(table_, &lo, &hi);
+    if (bg_wm_meta_window(table_, &mlo, &mhi) < 0 || mlo == mhi) return 0;
+    return StagedMetaAt(lo, hi) - mlo;
   }
 
   // wildcard_match.cc:317-354

@@ -107,6 +107,18 @@ class Module:
         offs = (C.c_int32 * max(len(names), 1))(*[int(attr_offsets[n]) for n in names])
         _check(lib().bg_module_bind_meta(self.h, meta_off, arr, offs, len(names)))
 
+    def process_meta(self, heads, metas, igate=0, now=None, device=-1):
+        """ProcessBatch over host packets given by head_data() and metadata
+        area addresses (numpy uintp arrays; bg_module_process_meta)"""
+        heads = np.ascontiguousarray(heads, dtype=np.uintp)
+        metas = np.ascontiguousarray(metas, dtype=np.uintp)
+        n = len(heads)
+        og = np.full(n, BG_GATE_NONE, np.uint16)
+        _check(lib().bg_module_process_meta(self.h, make_ctx(igate, now, device),
+                                            heads.ctypes.data, metas.ctypes.data, n,
+                                            og.ctypes.data))
+        return og
+
     def process(self, frames, stride, n, igate=0, now=None, device=-1):
         """ProcessBatch over host frames (numpy uint8 slab, frame i at
         i*stride, each with >= 2048 accessible bytes for the checksum
@@ -413,11 +425,14 @@ class Pipe:
         lib().bg_pipe_window(self.h, C.byref(lo), C.byref(hi), C.byref(st))
         return lo.value, hi.value, st.value
 
-    def submit(self, heads, lens=None, cookies=None, igate=0, now=None):
+    def submit(self, heads, lens=None, cookies=None, igate=0, now=None, metas=None):
         """heads: numpy uintp array of head_data() addresses; igate / now:
-        the ProcessBatch's context."""
+        the ProcessBatch's context; metas: the packets' metadata areas
+        (modules with attr_name fields)."""
         heads = np.ascontiguousarray(heads, dtype=np.uintp)
         n = len(heads)
+        if metas is not None:
+            metas = np.ascontiguousarray(metas, dtype=np.uintp)
         lp = None
         if lens is not None:
             lens = np.ascontiguousarray(lens, dtype=np.uint16)
@@ -426,8 +441,12 @@ class Pipe:
         if cookies is not None:
             cookies = np.ascontiguousarray(cookies, dtype=np.uintp)
             cp = cookies.ctypes.data
-        _check(lib().bg_pipe_submit(self.h, make_ctx(igate, now), heads.ctypes.data,
-                                    lp, cp, n))
+        if metas is None:
+            _check(lib().bg_pipe_submit(self.h, make_ctx(igate, now), heads.ctypes.data,
+                                        lp, cp, n))
+        else:
+            _check(lib().bg_pipe_submit_meta(self.h, make_ctx(igate, now), heads.ctypes.data,
+                                             metas.ctypes.data, lp, cp, n))
 
     def flush(self):
         _check(lib().bg_pipe_flush(self.h))

@@ -97,9 +97,11 @@ int bg_em_sync(bg_em *em, int device, bg_stream_t stream);
  * core/module.h:679-684). On the device each slot carries that metadata
  * area at byte meta_off; attr_offsets[attr_id] is attr_offset(attr_id)
  * (nattrs entries, < 0: none -> EINVAL, where the reference would
- * dereference a null attribute pointer). Until bound, classify returns
- * ENOTSUP for tables with attr fields; host staging paths never carry
- * metadata and keep returning ENOTSUP. */
+ * dereference a null attribute pointer). meta_off -1: the attribute offsets
+ * only (staged rows, bg_em_classify_staged; the device-slab calls stay
+ * unbound). Until bound, classify returns ENOTSUP for tables with attr
+ * fields; bg_em_process_host (head pointers only) never carries metadata
+ * and keeps returning ENOTSUP. */
 int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
                     int nattrs);
 /* Device-resident classify: d_gates[i] = gate for frame i (default_gate on
@@ -140,6 +142,17 @@ int bg_em_classify_window(bg_em *em, const void *d_win, size_t stride,
                           uint16_t *d_gates, bg_stream_t stream);
 /* [lo, hi): the frame bytes the fields cover (MakeKeys reads) */
 void bg_em_window(const bg_em *em, int *lo, int *hi);
+/* Staged rows with metadata (the aggregation queue, host packets): byte 0
+ * of row i (d_win + i*stride) is frame byte win_off of packet i, and row
+ * offset meta_row + a is byte a of packet i's metadata area, so an attr
+ * field reads the row at meta_row + attr_offset (offsets as bound by
+ * bg_em_bind_meta, whose meta_off may then be -1: offsets only). */
+int bg_em_classify_staged(bg_em *em, const void *d_win, size_t stride, size_t n,
+                          int win_off, int meta_row, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream);
+/* [lo, hi): the metadata bytes the attr fields read (lo == hi: none);
+ * -ENOTSUP while attr offsets are unbound */
+int bg_em_meta_window(const bg_em *em, int *lo, int *hi);
 
 /* ---- Rule-table collective (RCCL over xGMI) -----------------
  * The only exchange of the multi-GPU path: the ExactMatch image of a rule
@@ -204,6 +217,11 @@ int bg_wm_classify_window(bg_wm *wm, const void *d_win, size_t stride,
                           size_t n, int win_off, uint16_t default_gate,
                           uint16_t *d_gates, bg_stream_t stream);
 void bg_wm_window(const bg_wm *wm, int *lo, int *hi);
+/* as bg_em_classify_staged / bg_em_meta_window */
+int bg_wm_classify_staged(bg_wm *wm, const void *d_win, size_t stride, size_t n,
+                          int win_off, int meta_row, uint16_t default_gate,
+                          uint16_t *d_gates, bg_stream_t stream);
+int bg_wm_meta_window(const bg_wm *wm, int *lo, int *hi);
 /* Run-time compiled kernels (bess_amd/csrc/bg_wm_jit.cc). A tag-word image's
  * tuple data (masks, seeds, direct tuples) and its key plan are compiled
  * into a specialised kernel with hiprtc on a background thread; launches use
@@ -382,7 +400,8 @@ size_t bg_dnat_count(const bg_dnat *h);
  * gate 1; dir 1 maps external destinations and emits on 0; unknown
  * endpoints and other protocols: DROP_GATE. now: ctx->current_ns. A batch
  * with new forward flows is decided on the host in packet order (the port
- * search is sequential); synchronous. */
+ * search is sequential); synchronous, on `stream` as given (NULL: the legacy
+ * default stream). */
 int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
                     int dir, uint64_t now, uint16_t *d_out, bg_stream_t stream);
 
@@ -402,12 +421,14 @@ size_t bg_rewrite_count(const bg_rewrite *h);
  * as a bessd plugin receives its Init / add argument */
 int bg_rewrite_add_pb(bg_rewrite *h, const void *arg, size_t len);
 /* ProcessBatch (72-113) over n packets in one call, as consecutive batches:
+ * asynchronous on `stream` as given (NULL: the legacy default stream, so
+ * the kernel runs after the caller's earlier work there):
  * packet i (slot d_slots + i*stride) gets template (turn + i) % count at
  * slot + headroom, d_head[i] = headroom (data_off), d_len[i] = its size;
  * the turn advances by n. Whole 32-byte blocks are written, as the
  * reference's sloppy copy does (bytes past the size are the template's
  * zero padding), so headroom + the largest size rounded up to 32 must fit
- * the slot. No template: packets untouched. stream NULL: synchronous. */
+ * the slot. No template: packets untouched. */
 int bg_rewrite_process(bg_rewrite *h, int device, void *d_slots, size_t stride,
                        size_t n, uint32_t headroom, uint16_t *d_head, uint32_t *d_len,
                        bg_stream_t stream);
@@ -463,6 +484,8 @@ typedef struct bg_ctx {
  * reference's message via bg_last_error(). */
 int bg_module_create(const char *mclass, const void *arg, size_t arg_len,
                      bg_module **out);
+/* Releases the caller's handle. Pipes still open on the module keep it
+ * alive: it is freed when the last of them is destroyed. */
 void bg_module_destroy(bg_module *m);
 /* cmd by name with its serialized argument (arg type per the module's cmds
  * table). The serialized response message (e.g. ExactMatchConfig for
@@ -479,6 +502,11 @@ int bg_module_command(bg_module *m, const char *cmd, const void *arg,
  * each with its own ctx. */
 int bg_module_process(bg_module *m, const bg_ctx *ctx, uint8_t *const *heads,
                       size_t cnt, uint16_t *ogates);
+/* bg_module_process with each packet's metadata area (metas[i], as
+ * bg_pipe_submit_meta): the synchronous path of a module with attr_name
+ * fields (bg_module_process on one: every packet dropped, -EINVAL). */
+int bg_module_process_meta(bg_module *m, const bg_ctx *ctx, uint8_t *const *heads,
+                           uint8_t *const *metas, size_t cnt, uint16_t *ogates);
 /* bg_module_process plus the batches the Task would run next
  * (core/module.h:543-618): per output gate, packets in emission order cut
  * into batches of <= 32 (PacketBatch::kMaxBurst), in the order the batches
@@ -506,10 +534,17 @@ int bg_module_process_device(bg_module *m, const bg_ctx *ctx, void *d_frames,
 /* the device of calls whose ctx says -1 (default 0); control path */
 int bg_module_set_device(bg_module *m, int device);
 /* Metadata layout for attr_name fields (ExactMatch, WildcardMatch): the
- * slot offset of each packet's metadata area and, by attribute name, the
- * offsets the pipeline assigned (Module::attr_offset, core/module.h). */
+ * slot offset of each packet's metadata area in a device slab (-1: no
+ * device-slab layout; the host paths stage each packet's metadata bytes
+ * themselves) and, by attribute name, the offsets the pipeline assigned
+ * (Module::attr_offset, core/module.h). */
 int bg_module_bind_meta(bg_module *m, int meta_off, const char *const *names,
                         const int32_t *offsets, int n);
+/* The module's i-th metadata attribute (the attr_name fields of ExactMatch
+ * and WildcardMatch, in field order: AddMetadataAttr, core/module.h:294) --
+ * what a bessd wrapper registers with bessd so its pipeline assigns the
+ * offset. Returns 1 (name, size filled) or 0 past the last. */
+int bg_module_attr(const bg_module *m, int i, char *name, size_t cap, uint32_t *size);
 /* GetDesc() (exact_match.cc:246-249, wildcard_match.cc:205-213) */
 int bg_module_desc(const bg_module *m, char *buf, size_t len);
 
@@ -547,6 +582,15 @@ void bg_pipe_destroy(bg_pipe *p); /* waits for in-flight slots */
 int bg_pipe_window(const bg_pipe *p, int *lo, int *hi, size_t *stride);
 int bg_pipe_submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                    const uint16_t *lens, void *const *cookies, size_t cnt);
+/* submit for a module with attr_name fields (ExactMatch / WildcardMatch,
+ * exact_match.cc:230-236, wildcard_match.cc:177-195): metas[i] = packet i's
+ * metadata area (Packet::metadata(): the snbuf's SNBUF_METADATA bytes); the
+ * bytes the fields read (bg_em_meta_window, attribute offsets bound with
+ * bg_module_bind_meta, meta_off -1 will do) travel in the packet's staged
+ * row after its field window. bg_pipe_submit on such a module: -EINVAL. */
+int bg_pipe_submit_meta(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
+                        uint8_t *const *metas, const uint16_t *lens,
+                        void *const *cookies, size_t cnt);
 int bg_pipe_flush(bg_pipe *p);
 long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
                   size_t cap);
@@ -576,7 +620,9 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
  * frame from byte win_off on -- 0: whole frames, the field window's start:
  * staged windows; gates written to `gates`) and returns the lane's ticket; wait blocks until that ticket's
  * gates are written; completed returns the number of the lane's tickets
- * finished in order. Create it with as many lanes as workers submit on. The
+ * finished in order. Create it with as many lanes as workers submit on (one
+ * thread per lane: wait / completed claim the lane and return -EBUSY to a
+ * second thread; submit only detects one on a best-effort basis). The
  * kernel keeps the table in LDS for its whole run and classifies with the
  * rule set as of bg_em_ring_create (it holds its own copy of the table
  * image: re-create the ring after rule changes, which bessd makes with

@@ -29,7 +29,10 @@
 #define BESS_MODULES_GPU_MODULE_H_
 
 #include <atomic>
+#include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <vector>
 
 #include "../module.h"
 #include "../pb/module_msg.pb.h"
@@ -85,6 +88,9 @@ class GpuModule : public Module {
   // they leave in submission order.
   struct task_result RunTask(Context *ctx, bess::PacketBatch *, void *) override {
     uint32_t done = 0;
+    std::shared_lock<std::shared_mutex> meta(meta_mu_, std::defer_lock);
+    if (has_attrs_ && !meta.try_lock())  // a worker is re-binding the attributes
+      return {.block = true, .packets = 0, .bits = 0};
     for (Lane &l : lanes_) {
       bg_pipe *p = l.pipe.load(std::memory_order_acquire);
       if (!p || bg_pipe_pending(p) == 0) continue;
@@ -123,7 +129,24 @@ class GpuModule : public Module {
   CommandResponse Create(const char *mclass, const google::protobuf::Message &arg) {
     const std::string b = arg.SerializeAsString();
     const int rc = bg_module_create(mclass, b.data(), b.size(), &m_);
-    return rc < 0 ? CommandFailure(-rc, "%s", bg_last_error()) : CommandSuccess();
+    if (rc < 0) return CommandFailure(-rc, "%s", bg_last_error());
+    return RegisterAttrs();
+  }
+
+  // The metadata attributes the module reads (the attr_name fields of
+  // ExactMatch / WildcardMatch: AddFieldOne's AddMetadataAttr,
+  // exact_match.cc:78-86, wildcard_match.cc:89-95) registered with bessd,
+  // whose pipeline assigns their offsets (Module::attr_offset)
+  CommandResponse RegisterAttrs() {
+    char name[128];
+    uint32_t size = 0;
+    int i = 0;
+    for (; bg_module_attr(m_, i, name, sizeof(name), &size) > 0; i++) {
+      const int r = AddMetadataAttr(name, size, bess::metadata::Attribute::AccessMode::kRead);
+      if (r < 0) return CommandFailure(-r, "idx %d: add_metadata_attr() failed", i);
+    }
+    has_attrs_ = i > 0;
+    return CommandSuccess();
   }
 
   // Create, with the deferred datapath: ProcessBatch enqueues, a task emits
@@ -184,10 +207,23 @@ class GpuModule : public Module {
   void ProcessSync(Context *ctx, bess::PacketBatch *batch) {
     const int n = batch->cnt();
     uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
+    uint8_t *metas[bess::PacketBatch::kMaxBurst] = {};
     uint16_t og[bess::PacketBatch::kMaxBurst];
-    for (int i = 0; i < n; i++) heads[i] = batch->pkts()[i]->head_data<uint8_t *>();
+    for (int i = 0; i < n; i++) {
+      heads[i] = batch->pkts()[i]->head_data<uint8_t *>();
+      metas[i] = batch->pkts()[i]->metadata<uint8_t *>();
+    }
     const bg_ctx c = CallCtx(ctx);
-    if (bg_module_process(m_, &c, heads, (size_t)n, og) < 0) {
+    std::shared_lock<std::shared_mutex> meta(meta_mu_, std::defer_lock);
+    if (has_attrs_) {
+      if (!AttrsBound() && !Rebind(ctx)) {
+        for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
+        return;
+      }
+      meta.lock();
+    }
+    if ((has_attrs_ ? bg_module_process_meta(m_, &c, heads, metas, (size_t)n, og)
+                    : bg_module_process(m_, &c, heads, (size_t)n, og)) < 0) {
       for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
       return;
     }
@@ -197,12 +233,63 @@ class GpuModule : public Module {
   // ProcessBatch, deferred: the batch joins this worker's pipe, then what
   // has finished there leaves
   void Enqueue(Context *ctx, bess::PacketBatch *batch) {
+    std::shared_lock<std::shared_mutex> meta(meta_mu_, std::defer_lock);
+    if (has_attrs_) {  // the metadata layout the pipes stage with is current
+      if (!AttrsBound() && !Rebind(ctx)) {
+        for (int i = 0; i < batch->cnt(); i++) DropPacket(ctx, batch->pkts()[i]);
+        return;
+      }
+      meta.lock();
+    }
     Lane &l = lanes_[ctx->wid];
     l.in_call.store(true);  // (seq_cst: pairs with RunTask's claim)
     while (l.draining.load(std::memory_order_acquire)) {
     }
     EnqueueOwned(ctx, batch, l);
     l.in_call.store(false, std::memory_order_release);
+  }
+
+  // Whether the attribute offsets bessd assigned are the ones bound into the
+  // library (bessd recomputes them when the pipeline changes, workers paused)
+  bool AttrsBound() const {
+    const size_t n = all_attrs().size();
+    if (nbound_.load(std::memory_order_acquire) != (int)n) return false;
+    for (size_t i = 0; i < n; i++)
+      if (bound_[i].load(std::memory_order_relaxed) != (int32_t)attr_offset(i)) return false;
+    return true;
+  }
+
+  // Bind the current offsets (first batch, or after a pipeline change): every
+  // worker's pipe -- staged with the old layout -- is drained (its packets
+  // leave here, in order) and closed; workers open new ones. false: the
+  // library refused the layout (an attribute no upstream module writes,
+  // where the reference would dereference a null attribute pointer).
+  bool Rebind(Context *ctx) {
+    std::unique_lock<std::shared_mutex> lk(meta_mu_);
+    if (AttrsBound()) return true;
+    for (Lane &l : lanes_) {
+      bg_pipe *p = l.pipe.exchange(nullptr);
+      if (!p) continue;
+      (void)bg_pipe_flush(p);
+      void *ck[256];
+      uint16_t g[256];
+      long k;
+      while ((k = bg_pipe_poll(p, 1, ck, g, 256)) > 0)
+        for (long i = 0; i < k; i++) Emit(ctx, static_cast<bess::Packet *>(ck[i]), g[i]);
+      bg_pipe_destroy(p);
+    }
+    const size_t n = all_attrs().size();
+    std::vector<const char *> names(n);
+    std::vector<int32_t> offs(n);
+    for (size_t i = 0; i < n; i++) {
+      names[i] = all_attrs()[i].name.c_str();
+      offs[i] = attr_offset(i);
+    }
+    nbound_.store(-1, std::memory_order_relaxed);
+    if (bg_module_bind_meta(m_, -1, names.data(), offs.data(), (int)n) < 0) return false;
+    for (size_t i = 0; i < n; i++) bound_[i].store(offs[i], std::memory_order_relaxed);
+    nbound_.store((int)n, std::memory_order_release);
+    return true;
   }
 
   void EnqueueOwned(Context *ctx, bess::PacketBatch *batch, Lane &l) {
@@ -213,6 +300,7 @@ class GpuModule : public Module {
       return;
     }
     uint8_t *heads[bess::PacketBatch::kMaxBurst] = {};
+    uint8_t *metas[bess::PacketBatch::kMaxBurst] = {};
     uint16_t lens[bess::PacketBatch::kMaxBurst] = {};
     // the packets' mbuf lines in flight together (head_data() reads them),
     // then, as each arrives, the line of its data the pipe gathers from
@@ -222,10 +310,12 @@ class GpuModule : public Module {
       heads[i] = pkt->head_data<uint8_t *>();
       lens[i] = pkt->data_len();
       __builtin_prefetch(heads[i] + l.win_lo);
+      if (has_attrs_) metas[i] = pkt->metadata<uint8_t *>();
     }
     const bg_ctx c = CallCtx(ctx);
-    if (bg_pipe_submit(p, &c, heads, lens, reinterpret_cast<void *const *>(batch->pkts()),
-                       (size_t)n) < 0) {
+    void *const *ck = reinterpret_cast<void *const *>(batch->pkts());
+    if ((has_attrs_ ? bg_pipe_submit_meta(p, &c, heads, metas, lens, ck, (size_t)n)
+                    : bg_pipe_submit(p, &c, heads, lens, ck, (size_t)n)) < 0) {
       for (int i = 0; i < n; i++) DropPacket(ctx, batch->pkts()[i]);
       return;
     }
@@ -286,6 +376,12 @@ class GpuModule : public Module {
   }
 
   bool deferred_ = false;
+  // attr_name fields: the offsets bound into the library (AttrsBound); the
+  // datapath holds meta_mu_ shared, a re-bind exclusively
+  bool has_attrs_ = false;
+  std::shared_mutex meta_mu_;
+  std::atomic<int> nbound_{-1};
+  std::atomic<int32_t> bound_[16] = {};
   size_t pipe_batch_ = kPipeBatch;
   int pipe_depth_ = kPipeDepth;
   Lane lanes_[Worker::kMaxWorkers];

@@ -11,6 +11,7 @@
 class IPEncap final : public GpuModule {
  public:
   CommandResponse Init(const bess::pb::IPEncapArg &) {
+    using AccessMode = bess::metadata::Attribute::AccessMode;
     AddMetadataAttr("ip_src", 4, AccessMode::kRead);  // ip_encap.cc:53-57
     AddMetadataAttr("ip_dst", 4, AccessMode::kRead);
     AddMetadataAttr("ip_proto", 1, AccessMode::kRead);

@@ -19,6 +19,7 @@
 #ifndef BESSD_SHELL_MODULE_H_
 #define BESSD_SHELL_MODULE_H_
 
+#include <errno.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -77,6 +78,12 @@ class Packet {
     return reinterpret_cast<T>(reinterpret_cast<uint8_t *>(this) + SNBUF_HEADROOM_OFF +
                                data_off_);
   }
+  // the metadata area (core/packet.h:100-104: Packet::metadata_, at
+  // SNBUF_METADATA_OFF of the snbuf)
+  template <typename T = void *>
+  T metadata() {
+    return reinterpret_cast<T>(reinterpret_cast<uint8_t *>(this) + SNBUF_METADATA_OFF);
+  }
   uint16_t data_off() const { return data_off_; }
   void set_data_off(uint16_t v) { data_off_ = v; }
   uint32_t total_len() const { return total_len_; }
@@ -107,6 +114,19 @@ class PacketBatch {
   int cnt_ = 0;
   Packet *pkts_[kMaxBurst];
 };
+
+namespace metadata {
+// core/metadata.h: an attribute's access mode; the offset of an attribute
+// no upstream module writes (kMetadataOffsetNoRead)
+struct Attribute {
+  enum class AccessMode { kRead = 0, kWrite, kUpdate };
+  std::string name;
+  size_t size;
+  AccessMode mode;
+};
+typedef int16_t mt_offset_t;
+static const mt_offset_t kMetadataOffsetNoRead = -2;
+}  // namespace metadata
 
 }  // namespace bess
 
@@ -228,16 +248,29 @@ class Module {
     for (int i = 0; i < batch->cnt(); i++) EmitPacket(ctx, batch->pkts()[i], 0);
   }
 
-  // Module::AddMetadataAttr / attr_offset (core/module.h:640-700); the
-  // shell's pipeline places attribute i at metadata offset 4 * i
-  enum class AccessMode { kRead = 0, kWrite, kUpdate };
-  int AddMetadataAttr(const std::string &name, size_t size, AccessMode) {
-    attrs_.push_back(name);
-    (void)size;
+  // Module::AddMetadataAttr / attr_offset (core/module.h:294-328): the
+  // shell's pipeline packs the attributes in registration order (bessd's
+  // allocator, core/metadata.cc, places them by its own rules; a script may
+  // place them with set_attr_offset, as Pipeline::ComputeMetadataOffsets
+  // does before the workers resume)
+  int AddMetadataAttr(const std::string &name, size_t size,
+                      bess::metadata::Attribute::AccessMode mode) {
+    for (const auto &a : attrs_)
+      if (a.name == name) return -EEXIST;
+    int32_t off = 0;
+    for (const auto &a : attrs_) off += (int32_t)a.size;
+    attrs_.push_back(bess::metadata::Attribute{name, size, mode});
+    attr_offsets_.push_back(off);
     return (int)attrs_.size() - 1;
   }
-  int32_t attr_offset(int attr_id) const { return 4 * attr_id; }
+  bess::metadata::mt_offset_t attr_offset(size_t attr_id) const {
+    return (bess::metadata::mt_offset_t)attr_offsets_[attr_id];
+  }
+  void set_attr_offset(size_t attr_id, bess::metadata::mt_offset_t off) {
+    if (attr_id < attr_offsets_.size()) attr_offsets_[attr_id] = off;
+  }
   size_t num_attrs() const { return attrs_.size(); }
+  const std::vector<bess::metadata::Attribute> &all_attrs() const { return attrs_; }
 
  protected:
   bool is_task_ = false;            // core/module.h:464
@@ -247,7 +280,8 @@ class Module {
  private:
   std::vector<void *> tasks_;
   std::vector<bool> ogates_;
-  std::vector<std::string> attrs_;
+  std::vector<bess::metadata::Attribute> attrs_;
+  std::vector<int32_t> attr_offsets_;
 };
 inline const Commands Module::cmds = {};
 

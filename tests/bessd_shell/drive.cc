@@ -9,6 +9,11 @@
 //     desc                        GetDesc         -> "desc <text>"
 //     connect <ogate>             ConnectModules for that output gate
 //     frames <path> <stride> <n>  n frames of `stride` bytes into snbufs
+//     meta <path> <bytes>         each packet's metadata area (Packet::metadata,
+//                                 SNBUF_METADATA_OFF) gets `bytes` bytes from
+//                                 the file, packet after packet
+//     attr_offset <id> <off>      place the module's attribute `id` at metadata
+//                                 offset `off` (Pipeline::ComputeMetadataOffsets)
 //     swap                        turn each IPv4 TCP/UDP frame into its reply
 //                                 (addresses and ports exchanged; checksums
 //                                 unchanged, the sums being symmetric)
@@ -226,6 +231,21 @@ static int run() {
         p->set_data_len((uint16_t)stride);
         bufs.push_back(b);
       }
+    } else if (op == "meta") {
+      std::string path;
+      size_t nb;
+      in >> path >> nb;
+      std::ifstream f(path, std::ios::binary);
+      std::vector<char> md(nb);
+      for (uint8_t *b : bufs) {
+        f.read(md.data(), (std::streamsize)nb);
+        memcpy(reinterpret_cast<bess::Packet *>(b)->metadata<uint8_t *>(), md.data(),
+               std::min<size_t>(nb, SNBUF_METADATA));
+      }
+    } else if (op == "attr_offset") {
+      int id, off;
+      in >> id >> off;
+      m->set_attr_offset((size_t)id, (bess::metadata::mt_offset_t)off);
     } else if (op == "swap") {
       for (uint8_t *b : bufs) {
         uint8_t *f = reinterpret_cast<bess::Packet *>(b)->head_data<uint8_t *>();

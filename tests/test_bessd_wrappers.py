@@ -392,3 +392,145 @@ def test_deferred_pipeline_l4_checksum_and_acl(drive, tmp_path):
     got = [x for x in out if x.startswith("out")][0].split()[1:]
     assert got == ["1" if int(w) == 1 else "D" for w in want]
     assert "order ok" in out
+
+
+# ---- attr_name fields through the plugins: bessctl/module_tests
+# exact_match.py:88-123 and wildcard_match.py:104-139 restated (scapy and
+# SetMetadata are absent: the shell writes each packet's metadata area, as
+# SetMetadata upstream would, and places the attribute as bessd's metadata
+# allocator would)
+def _sangjin_script(cls):
+    if cls == "ExactMatch":
+        arg = pb.dict_to_protobuf(pb.ExactMatchArg, {
+            "fields": [{"attr_name": "sangjin", "num_bytes": 2}],
+            "masks": [{"value_bin": b"\xff\xff"}]})
+        adds = [pb.dict_to_protobuf(pb.ExactMatchCommandAddArg, {
+            "fields": [{"value_bin": v}], "gate": g}) for v, g in
+            ((b"\x88\x80", 1), (b"\x77\x70", 2))]
+        dflt = pb.dict_to_protobuf(pb.ExactMatchCommandSetDefaultGateArg, {"gate": 0})
+    else:
+        arg = pb.dict_to_protobuf(pb.WildcardMatchArg, {
+            "fields": [{"attr_name": "sangjin", "num_bytes": 2}]})
+        adds = [pb.dict_to_protobuf(pb.WildcardMatchCommandAddArg, {
+            "gate": g, "priority": 0, "masks": [{"value_bin": b"\xff\xff"}],
+            "values": [{"value_bin": v}]}) for v, g in
+            ((b"\x88\x80", 1), (b"\x77\x70", 2))]
+        dflt = pb.dict_to_protobuf(pb.WildcardMatchCommandSetDefaultGateArg, {"gate": 0})
+    return (["create %s %s" % (cls, hx(arg))] + ["cmd add " + hx(a) for a in adds] +
+            ["cmd set_default_gate " + hx(dflt), "connect 0", "connect 1", "connect 2"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", ["ExactMatch", "WildcardMatch"])
+@pytest.mark.parametrize("offset", [0, 42])
+def test_metadata_field_module_test(drive, tmp_path, cls, offset):
+    """three packets tagged 77 90 / 88 80 / 77 70 in attribute 'sangjin'
+    leave on gates 0 / 1 / 2 (the default, the two rules), with the
+    attribute where the pipeline placed it"""
+    frames = np.zeros((3, 64), np.uint8)
+    frames[:, 12:14] = [0x08, 0x00]
+    meta = np.zeros((3, 128), np.uint8)
+    for i, v in enumerate((b"\x77\x90", b"\x88\x80", b"\x77\x70")):
+        meta[i, offset:offset + 2] = list(v)
+    fp, mp = tmp_path / "f.bin", tmp_path / "m.bin"
+    frames.tofile(fp)
+    meta.tofile(mp)
+    script = _sangjin_script(cls) + ["frames %s 64 3" % fp, "meta %s 128" % mp,
+                                     "attr_offset 0 %d" % offset, "process 0 0"]
+    out = run(drive, script)
+    assert all(rc(x)[0] == 0 for x in out if x.startswith("rc")), out
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == ["0", "1", "2"]
+
+
+def _em_attr_rules_script(o, f, rng):
+    from test_attr_fields import EM_FIELDS, EM_MASKS, em_rules
+    arg = pb.dict_to_protobuf(pb.ExactMatchArg, {"fields": EM_FIELDS, "masks": EM_MASKS})
+    script = ["create ExactMatch " + hx(arg)]
+    for vals, g in em_rules(o, f, 1500, rng):
+        o.add(fields=vals, gate=g)
+        script.append("cmd add " + hx(pb.dict_to_protobuf(
+            pb.ExactMatchCommandAddArg, {"fields": vals, "gate": g})))
+    o.set_default_gate(70)
+    script.append("cmd set_default_gate " + hx(pb.dict_to_protobuf(
+        pb.ExactMatchCommandSetDefaultGateArg, {"gate": 70})))
+    return script
+
+
+@pytest.mark.gpu
+def test_metadata_fields_pipeline_vs_oracle(drive, tmp_path):
+    """ExactMatch with two attribute fields around an offset field (masks
+    in both byte orders, P1) through the plugin on 4 workers, bit-exact
+    against the oracle; then the pipeline moves the attributes (bessd
+    recomputes the offsets, workers paused) and the plugin re-binds: the
+    next pass reads them at their new place"""
+    from oracle import oracle as O
+    from test_attr_fields import EM_FIELDS, EM_MASKS, slots
+    n = 24000
+    f = slots(n, 41)                      # frame [0, 128), metadata [128, 256)
+    o = O.OracleExactMatch(fields=EM_FIELDS, masks=EM_MASKS)
+    script = _em_attr_rules_script(o, f, np.random.default_rng(42))
+    script += ["connect %d" % g for g in range(0, 71)]
+    fp = tmp_path / "f.bin"
+    f[:, :128].copy().tofile(fp)
+    script.append("frames %s 128 %d" % (fp, n))
+    wants = []
+    for k, offs in enumerate(({"foo": 8, "bar": 21}, {"foo": 100, "bar": 40})):
+        meta = np.zeros((n, 128), np.uint8)
+        # the same attribute bytes at the new offsets
+        meta[:, offs["foo"]:offs["foo"] + 2] = f[:, 128 + 8:128 + 10]
+        meta[:, offs["bar"]:offs["bar"] + 4] = f[:, 128 + 21:128 + 25]
+        mp = tmp_path / ("m%d.bin" % k)
+        meta.tofile(mp)
+        slab = np.zeros((n, 256), np.uint8)
+        slab[:, :128] = f[:, :128]
+        slab[:, 128:] = meta
+        wants.append(o.process(slab, 256, n, meta_off=128, attr_offsets=offs))
+        script += ["meta %s 128" % mp, "attr_offset 0 %d" % offs["foo"],
+                   "attr_offset 1 %d" % offs["bar"], "pipeline 4 1 0 0 1"]
+    assert (wants[0] == wants[1]).all() and (wants[0] != 70).mean() > 0.02
+    out = run(drive, script)
+    outs = [x.split()[1:] for x in out if x.startswith("out")]
+    assert len(outs) == 2 and out.count("order ok") == 2
+    for got, want in zip(outs, wants):
+        assert got == [str(int(w)) for w in want]
+
+
+@pytest.mark.gpu
+def test_metadata_fields_wildcard_pipeline_vs_oracle(drive, tmp_path):
+    """WildcardMatch with attribute fields through the plugin, 2 workers"""
+    from oracle import oracle as O
+    from test_attr_fields import slots
+    fields = [{"attr_name": "foo", "num_bytes": 2}, {"offset": 30, "num_bytes": 4},
+              {"attr_name": "bar", "num_bytes": 1}]
+    n = 20000
+    f = slots(n, 43)
+    rng = np.random.default_rng(44)
+    masks = [[b"\xff\xff", b"\x00\x00\x00\x00", b"\x00"],
+             [b"\x00\x00", b"\xff\xff\xff\x00", b"\x03"],
+             [b"\xff\x00", b"\x00\x00\x00\x00", b"\xff"]]
+    o = O.OracleWildcardMatch(fields=fields)
+    script = ["create WildcardMatch " + hx(pb.dict_to_protobuf(pb.WildcardMatchArg,
+                                                               {"fields": fields}))]
+    offs = {"foo": 8, "bar": 21}
+    for i in rng.choice(n, 500, replace=False):
+        mk = masks[int(rng.integers(0, 3))]
+        src = [f[i, 128 + offs["foo"]:128 + offs["foo"] + 2].tobytes(),
+               f[i, 30:34].tobytes(), f[i, 128 + offs["bar"]:128 + offs["bar"] + 1].tobytes()]
+        vals = [bytes(x & y for x, y in zip(s, mb)) for s, mb in zip(src, mk)]
+        arg = dict(gate=int(rng.integers(0, 64)), priority=int(rng.integers(0, 5)),
+                   values=[{"value_bin": v} for v in vals],
+                   masks=[{"value_bin": mb} for mb in mk])
+        o.add(**arg)
+        script.append("cmd add " + hx(pb.dict_to_protobuf(pb.WildcardMatchCommandAddArg, arg)))
+    want = o.process(f, 256, n, meta_off=128, attr_offsets=offs)
+    fp, mp = tmp_path / "f.bin", tmp_path / "m.bin"
+    f[:, :128].copy().tofile(fp)
+    f[:, 128:].copy().tofile(mp)
+    script += ["connect %d" % g for g in range(64)]
+    script += ["frames %s 128 %d" % (fp, n), "meta %s 128" % mp,
+               "attr_offset 0 8", "attr_offset 1 21", "pipeline 2 1 0 0 1"]
+    out = run(drive, script)
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == [str(int(w)) if int(w) < 64 else "D" for w in want]
+    assert "order ok" in out

@@ -187,6 +187,32 @@ def test_gpu_batches_vs_oracle(stride):
     run(rev[:2000], 1, T0 + 302 * 10**9)                  # some mappings now gone
 
 
+@pytest.mark.gpu
+def test_gpu_ordered_after_default_stream_work(default_stream_backlog):
+    """stream NULL is the caller's legacy default stream: the slab is
+    written there behind a ~20 ms backlog right before the call, and NAT
+    must translate those bytes, not the ones under them"""
+    import torch
+    from bess_amd.modules import NAT
+    rng = np.random.default_rng(21)
+    m, o = NAT(ext_addrs=EXT, seed=0x77), OM.OracleNAT(ext_addrs=EXT, seed=0x77)
+    s, p, pr, it = flows(2000, rng)
+    f = frames(s, p, rng.integers(1, 1 << 32, 2000), rng.integers(1, 65536, 2000), pr, it, rng)
+    ref = f.copy()
+    want = o.process(ref, STRIDE, len(f), 0, T0)
+    d = torch.zeros(f.size, dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(f.reshape(-1).copy()).cuda()
+    og = torch.empty(len(f), dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    default_stream_backlog()
+    d.copy_(src)
+    og.fill_(0x1234)
+    m.process_device(d, STRIDE, len(f), og, T0, igate=0)
+    torch.cuda.synchronize()
+    assert (og.cpu().numpy().view(np.uint16) == want).all()
+    assert (d.cpu().numpy().reshape(len(f), STRIDE) == ref).all()
+
+
 # ---- bessctl/module_tests/nat.py, restated (scapy is absent: packets are
 # built field by field with scapy's defaults and fresh checksums)
 def scapy_pkt(src, dst, kind, sport=0, dport=0, udp_ck0=False, icmp_id=0):

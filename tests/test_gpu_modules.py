@@ -106,9 +106,38 @@ def test_em_module_random_traffic_vs_oracle():
     assert (want != 77).mean() > 0.2
 
 
-def test_attr_fields_host_path_carries_no_metadata():
+def test_attr_fields_host_path_needs_metadata():
+    """the synchronous host path of a module with attr_name fields: the
+    attribute offsets must be bound (ENOTSUP before), and each packet's
+    metadata area passed (bg_module_process_meta; EINVAL without)"""
     m = ExactMatch(fields=[{"attr_name": "foo", "num_bytes": 2}])
     m.add(fields=[{"value_bin": b"\x01\x02"}], gate=1)
     with pytest.raises(ModuleError) as e:
         m.process(np.zeros((2, 64), np.uint8), 64, 2)
     assert e.value.code == 95
+    m.bind_meta(-1, {"foo": 6})
+    with pytest.raises(ModuleError) as e:
+        m.process(np.zeros((2, 64), np.uint8), 64, 2)
+    assert e.value.code == 22
+
+
+@pytest.mark.gpu
+def test_attr_fields_host_path_vs_oracle():
+    """bg_module_process_meta: frames and metadata areas in separate host
+    buffers, bit-exact against the oracle's slot layout"""
+    from test_attr_fields import ATTR_OFF, EM_FIELDS, EM_MASKS, META_OFF, STRIDE, em_rules, slots
+    n = 5000
+    f = slots(n, 51)
+    o = O.OracleExactMatch(fields=EM_FIELDS, masks=EM_MASKS)
+    m = ExactMatch(fields=EM_FIELDS, masks=EM_MASKS)
+    for vals, g in em_rules(o, f, 400, np.random.default_rng(52)):
+        o.add(fields=vals, gate=g)
+        m.add(fields=vals, gate=g)
+    want = o.process(f, STRIDE, n, meta_off=META_OFF, attr_offsets=ATTR_OFF)
+    frames = np.ascontiguousarray(f[:, :META_OFF])
+    meta = np.ascontiguousarray(f[:, META_OFF:])
+    heads = frames.ctypes.data + META_OFF * np.arange(n, dtype=np.uintp)
+    metas = meta.ctypes.data + (STRIDE - META_OFF) * np.arange(n, dtype=np.uintp)
+    m.bind_meta(-1, ATTR_OFF)
+    got = m.process_meta(heads, metas)
+    assert (got == want).all() and (want != O.DROP_GATE).mean() > 0.02

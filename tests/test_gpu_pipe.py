@@ -105,6 +105,107 @@ def _em_pipe_vs_oracle(batch, depth, burst):
     pipe.close()
 
 
+@pytest.mark.parametrize("mode", ["ring", "launch"])
+def test_module_destroyed_before_its_pipe(mode):
+    """bg_module_destroy with a pipe still open (a host tearing its graph
+    down in any order, or Python's collector freeing a cycle): the module
+    stays alive until the pipe goes, and the pipe keeps classifying"""
+    import ctypes as C
+    from bess_amd._lib import kernel_paths, lib, BG_PATH_PIPE_NO_RING
+    with kernel_paths(BG_PATH_PIPE_NO_RING if mode == "launch" else 0):
+        n = 5000
+        keys, gates, frames = P.em_workload(200, n, seed=13)
+        m, om = em_pair(keys, gates)
+        want = om.process(frames, 64, n)
+        buf, heads = snbufs(frames)
+        pipe = Pipe(m, batch=1024, depth=2)
+        got1 = run_pipe(pipe, heads[:2000])
+        lib().bg_module_destroy(m.h)  # the owner lets go first
+        m.h = None
+        got2 = run_pipe(pipe, heads[2000:])
+        pipe.close()
+        assert (np.concatenate([got1, got2]) == want).all()
+
+
+def test_ring_pipe_refilled_slots():
+    """ring mode with slots refilled many times: each refill's windows must
+    be read fresh by the persistent kernel (no line of an earlier batch
+    served from the device's caches), over several rounds of the same slots"""
+    n = 60000
+    keys, gates, frames = P.em_workload(1000, n, seed=14)
+    m, om = em_pair(keys, gates)
+    want = om.process(frames, 64, n)
+    buf, heads = snbufs(frames)
+    pipe = Pipe(m, batch=512, depth=2)
+    for rnd in range(3):
+        got = run_pipe(pipe, heads, shuffle_seed=100 + rnd)
+        assert (got == want).all(), rnd
+    pipe.close()
+
+
+@pytest.mark.parametrize("mode", ["ring", "launch"])
+@pytest.mark.parametrize("cls", ["em", "wm"])
+def test_pipe_metadata_fields_vs_oracle(mode, cls):
+    """attr_name fields on the aggregation queue: each packet's metadata
+    bytes travel in its staged row after the field window (frames and
+    metadata areas in separate host buffers), bit-exact against the oracle;
+    submitting without metadata is refused"""
+    from bess_amd._lib import kernel_paths, BG_PATH_PIPE_NO_RING
+    from bess_amd.modules import ModuleError
+    from test_attr_fields import (ATTR_OFF, EM_FIELDS, EM_MASKS, META_OFF, STRIDE,
+                                  em_rules, slots)
+    n = 30000
+    f = slots(n, 61)
+    if cls == "em":
+        o = O.OracleExactMatch(fields=EM_FIELDS, masks=EM_MASKS)
+        m = ExactMatch(fields=EM_FIELDS, masks=EM_MASKS)
+        for vals, g in em_rules(o, f, 2000, np.random.default_rng(62)):
+            o.add(fields=vals, gate=g)
+            m.add(fields=vals, gate=g)
+    else:
+        fields = [{"attr_name": "foo", "num_bytes": 2}, {"offset": 30, "num_bytes": 4},
+                  {"attr_name": "bar", "num_bytes": 1}]
+        o = O.OracleWildcardMatch(fields=fields)
+        m = WildcardMatch(fields=fields)
+        rng = np.random.default_rng(63)
+        for i in rng.choice(n, 500, replace=False):
+            src = [f[i, META_OFF + 8:META_OFF + 10].tobytes(), f[i, 30:34].tobytes(),
+                   f[i, META_OFF + 21:META_OFF + 22].tobytes()]
+            mk = [b"\xff\xff", b"\xff\xff\x00\x00", b"\x03"]
+            arg = dict(gate=int(rng.integers(0, 64)), priority=int(rng.integers(0, 5)),
+                       values=[{"value_bin": bytes(x & y for x, y in zip(s_, mb))}
+                               for s_, mb in zip(src, mk)],
+                       masks=[{"value_bin": mb} for mb in mk])
+            o.add(**arg)
+            m.add(**arg)
+    want = o.process(f, STRIDE, n, meta_off=META_OFF, attr_offsets=ATTR_OFF)
+    frames = np.ascontiguousarray(f[:, :META_OFF])
+    meta = np.ascontiguousarray(f[:, META_OFF:])
+    heads = frames.ctypes.data + META_OFF * np.arange(n, dtype=np.uintp)
+    metas = meta.ctypes.data + (STRIDE - META_OFF) * np.arange(n, dtype=np.uintp)
+    m.bind_meta(-1, ATTR_OFF)
+    with kernel_paths(BG_PATH_PIPE_NO_RING if mode == "launch" else 0):
+        pipe = Pipe(m, batch=1024, depth=4)
+        with pytest.raises(ModuleError):
+            pipe.submit(heads[:8])
+        order = np.random.default_rng(64).permutation(n).astype(np.uintp)
+        cs, gs = [], []
+        for i in range(0, n, 32):
+            idx = order[i:i + 32]
+            pipe.submit(heads[idx], cookies=idx, metas=metas[idx])
+            c, g = pipe.poll()
+            cs.append(c)
+            gs.append(g)
+        c, g = pipe.drain()
+        pipe.close()
+    c = np.concatenate(cs + [c])
+    g = np.concatenate(gs + [g])
+    assert (c == order).all()
+    got = np.empty(n, np.uint16)
+    got[c.astype(np.int64)] = g
+    assert (got == want).all() and (want != O.DROP_GATE).mean() > 0.02
+
+
 def test_em_pipes_share_ring_lanes():
     """18 pipes on one module, each run by its own thread (as bessd workers
     submit): more pipes than the module's ring has lanes (16), so two pairs

@@ -74,6 +74,34 @@ def test_gpu_vs_oracle(k, lo, hi):
 
 
 @pytest.mark.gpu
+def test_gpu_ordered_after_default_stream_work(default_stream_backlog):
+    """stream NULL is the caller's legacy default stream: the output arrays
+    are filled there behind a ~20 ms backlog right before the call, and the
+    kernel must run after that fill (on a private non-blocking stream it
+    ran first and the fill then overwrote every length)"""
+    import torch
+    ts = templates(3, 77, 0, 200)
+    m, o = Rewrite(templates=ts), OM.OracleRewrite(ts)
+    n, stride = 4096, 512
+    s = slab(n, stride, 5)
+    d = torch.from_numpy(s.reshape(-1).copy()).cuda()
+    dh = torch.empty(n, dtype=torch.int16, device="cuda")
+    dl = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    default_stream_backlog()
+    dh.fill_(0x5A5A)
+    dl.fill_(-1)
+    m.process_device(d, stride, n, dh, dl)
+    torch.cuda.synchronize()
+    head = np.zeros(n, np.uint16)
+    ln = np.zeros(n, np.uint32)
+    o.process(s, stride, n, head, ln)
+    assert (dl.cpu().numpy().view(np.uint32) == ln).all()
+    assert (dh.cpu().numpy().view(np.uint16) == head).all()
+    assert (d.cpu().numpy().reshape(n, stride) == s).all()
+
+
+@pytest.mark.gpu
 def test_gpu_host_packets_and_clear():
     """host buffers through the staging path; clear, then fewer and smaller
     templates (compared on each packet's data: the reference's sloppy copy
