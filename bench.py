@@ -157,22 +157,12 @@ def em_setup(args, rank, world, dev, torch, dist):
     d_gates = torch.empty(args.pkts, dtype=torch.int16, device=dev)
     t = F.EmTable(P.em_fields_5tuple())
     t0 = time.time()
-    if world > 1:  # this rank's partition only
-        t.add_many(keys, gates, part=rank, nparts=world)
-    else:
-        t.add_many(keys, gates)
+    # C2's 1K rules: every rank builds the whole (38 KB) table itself; the
+    # all-gather is C5's (run_c5_multi)
+    t.add_many(keys, gates)
     log("[rank %d] %d rules inserted in %.1fs" % (rank, len(t), time.time() - t0))
-    table = {"rules": len(keys)}
-    if world > 1:
-        # sharded build + RCCL all-gather of the partition images
-        from bess_amd import dist as D
-        dist.barrier()
-        _, st = D.sharded_em_table(t, rank, world, device=dev)
-        table["allgather_ms"] = round(st["allgather_ms"], 3)
-        table["allgather_bytes"] = st["bytes"]
-        table["part_build_ms"] = round(st["build_ms"], 2)
-    else:
-        t.sync(dev.index)
+    table = {"rules": len(keys), "build": "replicated (each GPU builds the rule set)"}
+    t.sync(dev.index)
     nbytes, in_lds = t.table_info()
     table.update({"bytes": nbytes, "in_lds": in_lds})
     return t, d_frames, d_gates, keys, gates, table
@@ -1450,8 +1440,10 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
     only partition r's rules; all-reduce MAX of the partition sizes fixes
     the layout; each rank builds its partition; one all-gather of the
     partition images over RCCL/xGMI assembles the replicated table), then
-    every rank classifies its own 16M packets through the 1M-rule table."""
-    from bess_amd import dist as D
+    every rank classifies its own 16M packets through the 1M-rule table.
+    The collective is the C ABI's own (bg_comm_init_rank + bg_em_allgather,
+    what a bessd calls): torch.distributed carries only the communicator's
+    128-byte id and the timing reductions, never the table."""
     from bess_amd import flowtable as F
     from bess_amd import packets as P
     n, nr = args.pkts, args.c5_rules
@@ -1467,7 +1459,12 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
     t.add_many(keys, gates, part=rank, nparts=world)
     insert_s = time.perf_counter() - t0
     held = len(t)
-    _, st = D.sharded_em_table(t, rank, world, device=dev)
+    comm = F.Comm.over_process_group(rank, world, dev.index, dist)
+    dist.barrier()
+    t0 = time.perf_counter()
+    t.allgather(comm)
+    st = comm.last_stats()
+    st["call_ms"] = (time.perf_counter() - t0) * 1e3
     t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
     ns = sample.shape[0]
@@ -1487,7 +1484,8 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
     dist.barrier()
     wall = time.perf_counter() - w0
     per = torch.tensor([wall, kern_ms, insert_s * 1e3, st["build_ms"],
-                        st["allgather_ms"], held, 1.0 if parity else 0.0],
+                        st["allgather_ms"], held, 1.0 if parity else 0.0,
+                        st["allreduce_ms"], st["call_ms"]],
                        dtype=torch.float64, device=dev)
     allr = [torch.zeros_like(per) for _ in range(world)]
     dist.all_gather(allr, per)
@@ -1505,15 +1503,19 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
             "per_rank_Mpps": [round(n / (x[1] * 1e-3) / 1e6, 1) for x in allr],
             "rules_inserted_per_rank": [int(x[5]) for x in allr],
             "insert_ms_per_rank": [round(x[2], 1) for x in allr],
+            "collective": "bg_em_allgather (C ABI, RCCL)",
             "part_build_ms": round(max(x[3] for x in allr), 2),
+            "size_allreduce_ms": round(max(x[7] for x in allr), 3),
             "allgather_ms": round(max(x[4] for x in allr), 3),
+            "allgather_call_ms": round(max(x[8] for x in allr), 3),
             "allgather_bytes": st["bytes"], "table_bytes": nbytes,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gbs / HBM_PEAK_GBS, 4),
                          "per": "GPU (slowest rank's kernel)"},
             "parity": "bit-exact vs oracle on 256K pkts per rank"
-                      if all(x[6] for x in allr) else "MISMATCH"}
+                      if all(x[6] for x in allr) else "MISMATCH",
+            "_comm": comm}
 
 
 def run_c1(args):
@@ -1695,11 +1697,13 @@ def main():
                   else "MISMATCH",
         "cpu_baseline": None,
     }
+    comm = None  # C5's communicator (N > 1), closed before the process group
     if world > 1:
         del r
         torch.cuda.empty_cache()
         try:
             out["C5"] = run_c5_multi(args, rank, world, dev, torch, dist)
+            comm = out["C5"].pop("_comm")
         except Exception as e:  # report, do not hide
             out["C5"] = "failed: %r" % (e,)
     if rank == 0 and world == 1 and not args.no_extra:
@@ -1744,6 +1748,9 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        if comm is not None:
+            torch.cuda.synchronize()
+            comm.close()
         dist.destroy_process_group()
 
 

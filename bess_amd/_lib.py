@@ -94,6 +94,7 @@ _SIGS = {
     "bg_comm_destroy": (None, [_vp]),
     "bg_comm_info": (_int, [_vp, C.POINTER(_int), C.POINTER(_int), C.POINTER(_int)]),
     "bg_em_allgather": (_int, [_vp, _vp, _vp]),
+    "bg_comm_last_stats": (_int, [_vp, _vp, C.POINTER(C.c_uint64)]),
     "bg_em_allgather_all": (_int, [_vp, _vp, _int]),
     "bg_wm_create": (_int, [C.POINTER(bg_field), _int, C.POINTER(_vp)]),
     "bg_wm_destroy": (None, [_vp]),

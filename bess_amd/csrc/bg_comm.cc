@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
+#include <time.h>
 
 #include <memory>
 #include <vector>
@@ -28,7 +29,17 @@ struct bg_comm {
   ncclComm_t c = nullptr;
   int device = -1;
   int rank = 0, nranks = 1;
+  // the last bg_em_allgather on this rank: ns in the size all-reduce, the
+  // partition build (host), the upload + all-gather; image bytes
+  uint64_t last_ns[3] = {0, 0, 0};
+  uint64_t last_bytes = 0;
 };
+
+static uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 
 #define NCCL_TRY(expr)                                                        \
   do {                                                                        \
@@ -101,6 +112,7 @@ int bg_em_allgather(bg_em *em, bg_comm *comm, bg_stream_t stream) {
   int r = set_device(comm->device);
   if (r) return r;
   hipStream_t s = (hipStream_t)stream;
+  const uint64_t t0 = mono_ns();
   // the layout: the largest partition over all ranks (all-reduce MAX)
   uint64_t cnt = 0;
   if ((r = bg_em_part_count(em, rank, nr, &cnt))) return r;
@@ -112,11 +124,13 @@ int bg_em_allgather(bg_em *em, bg_comm *comm, bg_stream_t stream) {
   NCCL_TRY(ncclAllReduce(d_cnt, d_cnt, 1, ncclUint64, ncclMax, comm->c, s));
   HIP_TRY(hipMemcpyAsync(&cnt, d_cnt, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  const uint64_t t1 = mono_ns();
   uint64_t part_bytes = 0;
   if ((r = bg_em_plan_count(em, nr, cnt, &part_bytes))) return r;
   // this rank's partition, in place in the gathered image
   std::vector<uint8_t> part(part_bytes);
   if ((r = bg_em_build_part(em, rank, part.data()))) return r;
+  const uint64_t t2 = mono_ns();
   uint8_t *d_img = nullptr;
   HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_img), part_bytes * nr));
   uint8_t *mine = d_img + part_bytes * rank;
@@ -129,7 +143,19 @@ int bg_em_allgather(bg_em *em, bg_comm *comm, bg_stream_t stream) {
     return q != ncclSuccess ? fail(EIO, "ncclAllGather: %s", ncclGetErrorString(q))
                             : fail(EIO, "HIP: %s", hipGetErrorString(e));
   }
+  const uint64_t t3 = mono_ns();
+  comm->last_ns[0] = t1 - t0;
+  comm->last_ns[1] = t2 - t1;
+  comm->last_ns[2] = t3 - t2;
+  comm->last_bytes = part_bytes * nr;
   return em_publish_owned(em, comm->device, d_img, part_bytes * nr);
+}
+
+int bg_comm_last_stats(const bg_comm *c, uint64_t *ns3, uint64_t *bytes) {
+  if (!c) return fail(EINVAL, "bad arguments");
+  if (ns3) memcpy(ns3, c->last_ns, sizeof(c->last_ns));
+  if (bytes) *bytes = c->last_bytes;
+  return 0;
 }
 
 // Every GPU of this process at once: the host holds all the rules, so each

@@ -176,6 +176,24 @@ class Comm:
         check(lib().bg_comm_info(self.h, C.byref(r), C.byref(n), C.byref(d)))
         return r.value, n.value, d.value
 
+    def last_stats(self):
+        """the rank's last EmTable.allgather: {"allreduce_ms", "build_ms",
+        "allgather_ms", "bytes"} (bg_comm_last_stats)"""
+        ns = (C.c_uint64 * 3)()
+        b = C.c_uint64()
+        check(lib().bg_comm_last_stats(self.h, ns, C.byref(b)))
+        return {"allreduce_ms": ns[0] / 1e6, "build_ms": ns[1] / 1e6,
+                "allgather_ms": ns[2] / 1e6, "bytes": b.value}
+
+    @classmethod
+    def over_process_group(cls, rank, world, device, dist, group=None):
+        """one rank of a communicator for `world` processes: rank 0's unique
+        id travels over the caller's existing torch.distributed group (128
+        control bytes; the table itself never goes through torch)"""
+        uid = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0, group=group)
+        return cls.init_rank(uid[0], world, rank, device)
+
     def close(self):
         if getattr(self, "h", None) is not None and _lib._lib is not None:
             lib().bg_comm_destroy(self.h)

@@ -141,7 +141,9 @@ class Module;
 // metadata bytes at row offset StagedMetaAt(lo, hi) -- so metadata byte 0
 // sits at row offset StagedMetaAt(lo, hi) - mlo (bg_em_classify_staged's
 // meta_row). Row stride: StagedStride.
-inline int StagedMetaAt(int lo, int hi) { return (hi - lo + 15) / 16 * 16; }
+// (at least 16: a module whose fields are all attributes stages one chunk
+// of frame bytes, as the pipe and the host path stage [lo, max(hi, lo + 1)))
+inline int StagedMetaAt(int lo, int hi) { return hi > lo ? (hi - lo + 15) / 16 * 16 : 16; }
 inline size_t StagedStride(int lo, int hi, int mlo, int mhi) {
   return (size_t)StagedMetaAt(lo, hi) + (size_t)((mhi - mlo + 15) / 16 * 16);
 }

@@ -178,6 +178,9 @@ int bg_comm_init_all(const int *devices, int ndev, bg_comm **comms);
 void bg_comm_destroy(bg_comm *c);
 int bg_comm_info(const bg_comm *c, int *rank, int *nranks, int *device);
 int bg_em_allgather(bg_em *em, bg_comm *comm, bg_stream_t stream);
+/* the rank's last bg_em_allgather: ns3 = {size all-reduce, partition build
+ * on the host, upload + all-gather} in ns; bytes = the gathered image */
+int bg_comm_last_stats(const bg_comm *c, uint64_t *ns3, uint64_t *bytes);
 int bg_em_allgather_all(bg_em *em, bg_comm *const *comms, int ncomm);
 
 /* ---- WildcardMatch ----------------------------------------------------- */
