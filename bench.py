@@ -370,6 +370,7 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
     launches0 = 0
     for T in (1, 4, 16):  # a ring with one submission lane per submitter
         ring = F.Ring(t, slots=4096, lanes=T)
+        ring.set_coherence(1, 0)  # as the pipes use it (ExactMatch module)
         key = "persistent" if T == 1 else "persistent_%dsub" % T
         out[key] = {}
         for B in batches:

@@ -167,6 +167,7 @@ _SIGS = {
     "bg_ring_run": (_int, [_vp, _int, _vp, _sz, _sz, _sz, _u16, _vp]),
     "bg_ring_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
     "bg_ring_desc_in_device": (_int, [_vp]),
+    "bg_ring_set_coherence": (_int, [_vp, _int, _int]),
     "bg_hlb_create": (_int, [_int, C.POINTER(bg_field), _int, C.POINTER(_vp)]),
     "bg_hlb_destroy": (None, [_vp]),
     "bg_hlb_set_mode": (_int, [_vp, _int, C.POINTER(bg_field), _int, _int]),

@@ -371,6 +371,16 @@ constexpr int kRingLaneWords = 16;
 // which leaves for the device at once (a half-written line can wait in the
 // buffer until the next descriptor's stores)
 constexpr int kRingDescWords = 8;
+// descriptor word 3, bits 16..: how the ticket's frames and gates meet the
+// host (bg_ring_set_coherence). kRingSysAcquire: the frames may sit in
+// memory the device caches non-coherently (mapped host memory that is not
+// uncached, or device memory a copy engine wrote): acquire at system scope
+// (invalidates L2's non-coherent lines) instead of agent scope (the CU's
+// L1 only). kRingRelease: the done word is a system-scope release (writes
+// L2 back) instead of a relaxed store after every wave's gate stores have
+// completed (the gates are system-scope write-through stores).
+constexpr uint64_t kRingSysAcquire = 1ull << 16;
+constexpr uint64_t kRingRelease = 1ull << 17;
 constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
 
 #ifndef __HIPCC_RTC__  // host launchers: not part of a run-time compile

@@ -464,10 +464,11 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
 // lane's next ticket (one atomic; claims run ahead of publication, so the
 // lane's workgroups queue up on its coming tickets), waits until it is
 // published, reads the descriptor (every word tagged with the ticket),
-// acquires (system scope: no line of an earlier batch survives in L1/L2),
-// classifies the batch, writes the gates through to memory (sc0 sc1
-// stores) and marks the ticket done in host memory with a system-scope
-// release. Create a ring with as many lanes as workers submit on.
+// acquires (no line of an earlier batch survives in L1, or in L2 for
+// non-coherently cached memory: kRingSysAcquire), classifies the batch,
+// writes the gates through to memory (sc0 sc1 stores) and marks the ticket
+// done in host memory after them (kRingRelease: as a system-scope release).
+// Create a ring with as many lanes as workers submit on.
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
@@ -517,13 +518,16 @@ void em_ring_kernel(RingArgs a) {
         const uint64_t tag = (t + 1) & 0xFFFF;
         const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
-        // acquire at system scope: the batch's frames were written (by the
-        // host or a copy) before the descriptor was published, and this
-        // grid outlives many batches, so lines of an earlier batch in the
-        // same buffer may still sit in this CU's L1 or the XCD's L2 (mapped
-        // host memory is cached there as non-coherent lines): invalidate
-        // them before any wave reads the frames (after the barrier below)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // acquire: the batch's frames were written (by the host or a copy)
+        // before the descriptor was published, and this grid outlives many
+        // batches, so lines of an earlier batch in the same buffer may
+        // still sit in this CU's L1 (and, for memory the device caches
+        // non-coherently, in the XCD's L2): invalidate them before any wave
+        // reads the frames (after the barrier below)
+        if (w[3] & kRingSysAcquire)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        else
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
 #ifdef BG_AB
       if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
@@ -540,6 +544,7 @@ void em_ring_kernel(RingArgs a) {
     const uint32_t n = (uint32_t)sh_w[2];
     const uint64_t stride = (sh_w[2] >> 32) & 0xFFFF;
     const uint32_t dflt = (uint32_t)(sh_w[3] & 0xFFFF);
+    const bool release = (sh_w[3] & kRingRelease) != 0;
     const uint64_t t = sh_t;
     for (uint32_t base = threadIdx.x; base < n; base += kRingBlock * kPpl) {
       // kPpl packets per lane, their header windows loaded before any key
@@ -571,10 +576,16 @@ void em_ring_kernel(RingArgs a) {
                                               : nullptr;
       if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-      // release at system scope: every wave's gate stores (drained above,
-      // before the barrier) are visible to the host before the done word
-      __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      // every wave's gate stores (system-scope write-through stores,
+      // completed by each wave's vmcnt(0) before the barrier) reach the
+      // host before the done word; with kRingRelease the done store is a
+      // system-scope release as well (L2 written back first)
+      if (release)
+        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef BG_AB
       if (tr) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

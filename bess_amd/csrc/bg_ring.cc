@@ -69,6 +69,7 @@ struct bg_ring {
   int blocks = 0;
   int read_end = 0;         // bytes of a slot the kernel reads
   uint64_t version = 0;     // the rule version of its table copy
+  uint64_t coherence = kRingSysAcquire | kRingRelease;  // descriptor word 3 flags
   hipStream_t st = nullptr;  // the kernel's own stream
   hipEvent_t ev = nullptr;   // recorded after each launch: has it ended?
   uint64_t *h_desc = nullptr;  // nlanes x nslots x kRingDescWords (pinned host) ...
@@ -412,7 +413,7 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
   __atomic_store_n(d + 0, ((uint64_t)(uintptr_t)frames & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 1, ((uint64_t)(uintptr_t)gates & kMaskAddr) | tag, __ATOMIC_RELAXED);
   __atomic_store_n(d + 2, (uint64_t)n | ((uint64_t)stride << 32) | tag, __ATOMIC_RELAXED);
-  __atomic_store_n(d + 3, (uint64_t)default_gate | tag, __ATOMIC_RELAXED);
+  __atomic_store_n(d + 3, (uint64_t)default_gate | r->coherence | tag, __ATOMIC_RELAXED);
   for (int i = 4; i < kRingDescWords; i++)  // the rest of the line (see kRingDescWords)
     __atomic_store_n(d + i, tag, __ATOMIC_RELAXED);
   // A descriptor in device memory goes through the CPU's write-combining
@@ -486,6 +487,18 @@ int bg_ring_trace(bg_ring *r, uint64_t *out, size_t cap_words) {
 #endif
 
 int bg_ring_desc_in_device(const bg_ring *r) { return r && r->d_desc ? 1 : 0; }
+
+int bg_ring_set_coherence(bg_ring *r, int frames, int done) {
+  if (!r || frames < 0 || frames > 1 || done < 0 || done > 1)
+    return fail(EINVAL, "bad arguments");
+  uint64_t c = (frames ? kRingSysAcquire : 0) | (done ? kRingRelease : 0);
+#ifdef BG_AB  // A/B: BG_RING_COHERENCE=1+bit0 sys acquire, +bit1 release
+  if (const int k = knob("BG_RING_COHERENCE", 0))
+    c = ((k - 1) & 1 ? kRingSysAcquire : 0) | ((k - 1) & 2 ? kRingRelease : 0);
+#endif
+  r->coherence = c;
+  return 0;
+}
 
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks) {
   if (launches) *launches = r->launches;

@@ -270,6 +270,12 @@ class Ring:
             raise errs[0]
         return dt
 
+    def set_coherence(self, frames, done):
+        """bg_ring_set_coherence: frames 0 for device memory written by
+        kernels or uncached host memory (1: any memory); done 1 for a
+        system-scope release on the done word"""
+        check(lib().bg_ring_set_coherence(self.h, int(frames), int(done)))
+
     def info(self):
         launches, blocks = C.c_uint64(), C.c_int()
         lib().bg_ring_info(self.h, C.byref(launches), C.byref(blocks))

@@ -142,6 +142,7 @@ class ExactMatch final : public Module {
   // change. Its workgroups take 2 per CU (half of each CU's LDS), leaving
   // room for other modules' kernels on the device.
   static const int kPipeRingLanes = 16;
+  static const int kPipeRingRelease = 0;  // the done word: see PipeRingFor
   int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) override {
     out->reset();
     if (bg_get_path_flags() & BG_PATH_PIPE_NO_RING) return 0;
@@ -158,6 +159,12 @@ class ExactMatch final : public Module {
                                         2 * bg::num_cus(device), 10000, lo,
                                         mlo == mhi ? bg::kSlabMeta : meta_row, &r);
       if (rc < 0) return rc;
+      // per ticket: a system-scope acquire (measured as cheap as the CU's
+      // L1 alone) and the done word stored once the gate stores -- system-
+      // scope write-through stores into the pipe's uncached slots -- have
+      // completed; a release there (an L2 write-back per ticket) halved the
+      // 32-packet ticket rate (scripts/ring_coherence_ab.py)
+      (void)bg_ring_set_coherence(r, 1, kPipeRingRelease);
       auto pr = std::make_shared<PipeRing>();
       pr->r = r;
       pr->meta_row = meta_row;

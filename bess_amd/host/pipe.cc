@@ -349,12 +349,7 @@ static long take_done(bg_pipe *p, bool wait, void **cookies, uint16_t *gates,
 
 // mapped pinned memory the device reads uncached (see bg_pipe_create)
 static hipError_t host_alloc_uc(void **p, size_t bytes) {
-  hipError_t e = hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocUncached);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    e = hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent);
-  }
-  return e;
+  return hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocUncached);
 }
 
 extern "C" {
@@ -400,10 +395,10 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
     if (p->ring_mode) {
       // the kernel reads the windows and writes the gates in place. Mapped
       // uncached (MTYPE UC): a refilled slot's windows are never served
-      // from a line an earlier batch left in the device's L1/L2 (coherent
-      // host memory alone is cached there as non-coherent lines, and the
-      // ring's grid outlives many batches; the kernel also acquires at
-      // system scope per ticket). Coherent when UC is not available.
+      // from a line an earlier batch left in the device's L2 (coherent host
+      // memory alone is cached there as non-coherent lines, and the ring's
+      // grid outlives many batches), so the ring's tickets acquire at agent
+      // scope only (their CU's L1; bg_ring_set_coherence in the EM module).
       hipError_t e = host_alloc_uc(reinterpret_cast<void **>(&s.h_in), batch * p->w + 64);
       if (e == hipSuccess) e = host_alloc_uc(reinterpret_cast<void **>(&s.h_g), batch * 2 + 64);
       if (e == hipSuccess)

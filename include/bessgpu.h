@@ -652,6 +652,17 @@ int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks);
  * PCIe BAR (workers read them from HBM); 0: in pinned host memory (read
  * over PCIe; no CPU mapping of device memory, or BG_RING_HOST_DESC=1). */
 int bg_ring_desc_in_device(const bg_ring *r);
+/* How the kernel meets the memory of later submits (one thread, before or
+ * between submits). frames 1 (default): the frames may be memory the
+ * device caches non-coherently -- mapped host memory that is not uncached
+ * (hipHostMallocUncached), or device memory rewritten by a copy between
+ * tickets -- so each ticket acquires at system scope (invalidating L2's
+ * non-coherent lines); 0: frames in device memory written by kernels, or in
+ * uncached host memory (each ticket invalidates its CU's L1 only). done 1
+ * (default): the done word is a system-scope release; 0: a system-scope
+ * store after the ticket's gate stores (themselves system-scope
+ * write-through stores) have completed. */
+int bg_ring_set_coherence(bg_ring *r, int frames, int done);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@ for step in ${STEPS:-tests ab phase calib pmc}; do
     ab)    for rep in 1 2; do
              { [ ! -f bess_amd/libbessgpu_prev.so ] || timeout -k 10 180 python scripts/wm_ab.py bess_amd/libbessgpu_prev.so >> $OUT/ab.jsonl 2>> $OUT/ab.err; } &&
              timeout -k 10 180 python scripts/wm_ab.py >> $OUT/ab.jsonl 2>> $OUT/ab.err &&
-             WM_AB_FLAGS=${WM_AB_FLAGS:-512} timeout -k 10 180 python scripts/wm_ab.py bess_amd/libbessgpu_ab.so >> $OUT/ab.jsonl 2>> $OUT/ab.err || break
+             WM_AB_FLAGS=${WM_AB_FLAGS:-512} timeout -k 10 180 python scripts/wm_ab.py scripts/bin/libbessgpu_ab.so >> $OUT/ab.jsonl 2>> $OUT/ab.err || break
            done ;;
     calib) timeout -k 10 600 bash scripts/gpu_calib.sh > $OUT/calib.log 2>&1 ;;
     pmc)   timeout -k 10 500 bash scripts/wm_pmc.sh > $OUT/wm_pmc.log 2>&1 ;;

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bess_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "bess_amd", "libbessgpu_ab.so")
+_lib.LIB_PATH = os.path.join(ROOT, "scripts", "bin", "libbessgpu_ab.so")
 from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 

@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 
 from bess_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "bess_amd", "libbessgpu_ab.so")
+_lib.LIB_PATH = os.path.join(ROOT, "scripts", "bin", "libbessgpu_ab.so")
 assert _lib.lib().bg_is_ab_build() == 1, "variants.py needs libbessgpu_ab.so"
 
 from bess_amd import flowtable as F  # noqa: E402
