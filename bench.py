@@ -744,6 +744,75 @@ def run_plugin_pipeline(args):
                 "Mpps_by_workers": cpu_res, "parity": cpu_parity}}
 
 
+def run_plugin_pool(args):
+    """bessd plugins on a bounded packet pool (tests/bessd_shell `pool`):
+    16 workers' Sources allocate every 32-packet batch from 262,144 snbufs
+    (bessd's --buffers default, core/opts.cc:127) and copy the frame in, as
+    Source copies its template; Sinks free the packets back. WildcardMatch
+    (C4-style rules, IMIX frames in 2 KB slots) and L4Checksum (1496 B frames)
+    plugins on the deferred datapath, each worker's pipe held to its share
+    of the pool (GpuModule::PipeBudget). Mpps over the packets the Sinks
+    took; parity of the last pass against the oracle."""
+    import subprocess
+    import tempfile
+    from bess_amd import packets as P
+    from bess_amd import pb
+    from oracle import oracle as O
+    drive = os.path.join(ROOT, "tests", "bessd_shell", "build", "drive")
+    if not os.path.exists(drive):
+        return "skipped: %s not built" % drive
+    n = 1 << 17
+    fields = [{"offset": o, "num_bytes": sz} for o, sz in P.FIVE_TUPLE]
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    out = {"pool": 262144, "workers": 16, "pkts_per_pass": n}
+    with tempfile.TemporaryDirectory() as td:
+        for name in ("WildcardMatch", "L4Checksum"):
+            if name == "WildcardMatch":
+                nr = 100000
+                rk, rm, prio, wg, frames, _ = P.wm_workload(nr, n, stride=2048)
+                ow = O.OracleWildcardMatch(fields=fields)
+                script = ["create WildcardMatch " + pb.dict_to_protobuf(
+                    pb.WildcardMatchArg, {"fields": fields}).SerializeToString().hex()]
+                for k, mk, p, g in zip(rk, rm, prio, wg):
+                    kb, mb = k.tobytes(), mk.tobytes()
+                    a = dict(gate=int(g), priority=int(p),
+                             values=[{"value_bin": kb[x:y]} for x, y in cut],
+                             masks=[{"value_bin": mb[x:y]} for x, y in cut])
+                    ow.add(**a)
+                    script.append("cmd add " + pb.dict_to_protobuf(
+                        pb.WildcardMatchCommandAddArg, a).SerializeToString().hex())
+                script += ["connect %d" % g for g in range(64)]
+                want = ow.process(frames, 2048, n)
+                exp = [str(int(w)) if int(w) < 64 else "D" for w in want]
+            else:
+                frames = P.cksum_workload(n, frame_len=1496)
+                ref = frames.copy()
+                _, l4w = O.cksum_process(ref, 2048, n, 2, False)
+                script = ["create L4Checksum -", "connect 0", "connect 1"]
+                exp = ["-" if int(w) == 0xFFFF else str(int(w)) for w in l4w]
+            path = os.path.join(td, "f.bin")
+            frames.tofile(path)
+            reps = 6 if name == "WildcardMatch" else 3
+            script += ["frames %s 2048 %d" % (path, n), "pool 262144",
+                       "pipeline 16 1 0 0 0", "pipeline 16 %d 0 0 0" % reps]
+            r = subprocess.run([drive, "run"], input="\n".join(script) + "\n",
+                               capture_output=True, text=True, timeout=600)
+            lines = r.stdout.splitlines()
+            stats = [x for x in lines if x.startswith("pipeline")]
+            outs = [x for x in lines if x.startswith("out")]
+            pools = [x.split() for x in lines if x.startswith("pool")]
+            if r.returncode or len(stats) < 2 or len(outs) < 2:
+                out[name] = "failed: rc %d %s" % (r.returncode, r.stderr[-300:])
+                continue
+            out[name] = {"Mpps": round(float(stats[1].split()[1]), 1),
+                         "parity": outs[1].split()[1:] == exp,
+                         "pool_after": "%s of %s back" % (pools[-1][1], pools[-1][2]),
+                         "source_waits": int(pools[-1][3])}
+            if name == "WildcardMatch":
+                out[name]["rules"] = nr
+    return out
+
+
 def _time_steps(step, args, torch):
     """warmup, then ms per launch over args.steps launches (HIP events on
     the launching stream)"""
@@ -1657,6 +1726,7 @@ def main():
             "hashlb": lambda: run_hashlb(args, dev, torch),
             "pipe": lambda: run_e2e_pipe(args, torch),
             "plugin": lambda: run_plugin_pipeline(args),
+            "plugin_pool": lambda: run_plugin_pool(args),
             "c1": lambda: run_c1(args),
             "sweep": lambda: em_sweep(run_em(args, rank, world, dev, torch,
                                              dist), torch)}
@@ -1731,6 +1801,10 @@ def main():
                 out["e2e_plugin"] = run_plugin_pipeline(args)
             except Exception as e:
                 out["e2e_plugin"] = "failed: %r" % (e,)
+            try:
+                out["e2e_plugin_pool"] = run_plugin_pool(args)
+            except Exception as e:
+                out["e2e_plugin_pool"] = "failed: %r" % (e,)
         for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
                          ("HashLB", run_hashlb), ("ACL", run_acl),
                          ("IPLookup", run_iplookup),

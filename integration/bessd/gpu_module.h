@@ -28,6 +28,7 @@
 #ifndef BESS_MODULES_GPU_MODULE_H_
 #define BESS_MODULES_GPU_MODULE_H_
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <shared_mutex>
@@ -52,15 +53,28 @@ class GpuModule : public Module {
 
  public:
   // the deferred datapath's pipes: packets per device launch, launches in
-  // flight per worker. A module served by a persistent ring (ExactMatch)
-  // submits small slots at no launch cost: 8 x 1024 packets in flight per
-  // worker (bessd's default pool is 256 K buffers for all workers,
-  // core/opts.cc:127); the others launch H2D/kernel/D2H per slot and
-  // amortise that over 64 K packets.
+  // flight per worker, at most. A module served by a persistent ring
+  // (ExactMatch) submits small slots at no launch cost (8 x 1024); the
+  // others launch H2D/kernel/D2H per slot and amortise that over up to 64 K
+  // packets. Either way a worker's pipe holds no more than PipeBudget().
   static const size_t kPipeBatch = 65536;
   static const int kPipeDepth = 4;
   static const size_t kRingPipeBatch = 1024;
   static const int kRingPipeDepth = 8;
+
+  // The packets one worker's pipe of a module may hold: a quarter of that
+  // worker's share of its socket's packet pool (bessd allocates --buffers,
+  // 262,144 per socket, core/opts.cc:127, for every port, module and worker
+  // there), so deferred modules never starve the Sources. A full pipe
+  // blocks the worker's submit until its oldest slot completes -- the
+  // Queue module's backpressure (queue.cc:173-190), never a drop.
+  static size_t PipeBudget() {
+    size_t cap = 262144;
+    if (bess::PacketPool *pool = bess::PacketPool::GetDefaultPool(current_worker.socket()))
+      cap = pool->Capacity();
+    const size_t w = num_workers > 0 ? (size_t)num_workers : 1;
+    return std::max<size_t>(cap / (4 * w), 256);
+  }
 
   void DeInit() override {
     for (Lane &l : lanes_) {
@@ -347,7 +361,9 @@ class GpuModule : public Module {
   bg_pipe *OpenLane(int wid) {
     const int nd = bg_device_count();
     bg_pipe *p = nullptr;
-    if (nd <= 0 || bg_pipe_create(m_, wid % nd, pipe_batch_, pipe_depth_, 0, &p) < 0)
+    const size_t batch =
+        std::min(pipe_batch_, std::max<size_t>(32, PipeBudget() / (size_t)pipe_depth_));
+    if (nd <= 0 || bg_pipe_create(m_, wid % nd, batch, pipe_depth_, 0, &p) < 0)
       return nullptr;
     int lo = 0, hi = 0;
     size_t stride = 0;

@@ -11,8 +11,10 @@
 //   gate_idx_t, MAX_GATES, DROP_GATE, SNBUF_*         core/gate.h, snbuf_layout.h
 //   RegisterTask / RunTask / task_result, is_task_,    core/module.h:198-311,
 //   max_allowed_workers_, propagate_workers_           core/task.h:40-44
-//   Worker::kMaxWorkers                               core/worker.h:77
-//   bess::Packet::Free                                core/packet.h:194-203
+//   Worker::kMaxWorkers, current_worker.socket(),     core/worker.h:77,101,143,155
+//   num_workers
+//   bess::PacketPool (GetDefaultPool, Capacity, Size, core/packet_pool.h:32-64
+//   AllocBulk), bess::Packet::Free                    core/packet.h:194-203
 //
 // EmitPacket keeps bessd's rule (module.h:546-549): an out-of-range or
 // unconnected output gate drops the packet.
@@ -24,9 +26,14 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <atomic>
 #include <functional>
 #include <map>
+#include <mutex>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -49,7 +56,11 @@ typedef uint16_t gate_idx_t;
 class Worker {
  public:
   static const int kMaxWorkers = 64;  // core/worker.h:77
+  int socket() const { return 0; }    // the shell: one socket
 };
+// core/worker.h:143,155: the calling worker; workers launched
+inline thread_local Worker current_worker;
+inline int num_workers = 1;
 
 typedef uint16_t task_id_t;
 #define INVALID_TASK_ID ((task_id_t)-1)
@@ -68,6 +79,8 @@ inline std::atomic<uint64_t> &freed_packets() {
   static std::atomic<uint64_t> n{0};
   return n;
 }
+
+class PacketPool;
 
 // an snbuf: the packet object at the start of its slot, its data at
 // SNBUF_HEADROOM_OFF + data_off
@@ -90,7 +103,14 @@ class Packet {
   void set_total_len(uint32_t v) { total_len_ = v; }
   uint16_t data_len() const { return data_len_; }
   void set_data_len(uint16_t v) { data_len_ = v; }
-  static void Free(Packet *) { freed_packets()++; }
+  // back to the packet's pool (a pool-less packet: the shell's static
+  // buffers of the `frames` command) -- core/packet.h:194-203
+  static inline void Free(Packet *p);
+  static inline void Free(Packet **pkts, size_t cnt) {
+    for (size_t i = 0; i < cnt; i++) Free(pkts[i]);
+  }
+  PacketPool *pool() const { return pool_; }
+  void set_pool(PacketPool *p) { pool_ = p; }
   // the shell's pool position of the packet (its Sink's bookkeeping)
   uint32_t pool_index() const { return pool_index_; }
   void set_pool_index(uint32_t i) { pool_index_ = i; }
@@ -100,7 +120,113 @@ class Packet {
   uint16_t data_len_ = 0;
   uint32_t total_len_ = 0;
   uint32_t pool_index_ = 0;
+  PacketPool *pool_ = nullptr;
 };
+
+// core/packet_pool.h: a fixed set of snbufs (mempool objects of SNBUF_SIZE +
+// 64 bytes, the frame at +512), handed out and taken back by every worker;
+// each thread keeps a cache of up to 512 (rte_mempool's per-lcore cache)
+class PacketPool {
+ public:
+  static const size_t kObj = SNBUF_SIZE + 64;
+  static PacketPool *GetDefaultPool(int) { return default_pool(); }
+  static PacketPool *&default_pool() {
+    static PacketPool *p = nullptr;
+    return p;
+  }
+  explicit PacketPool(size_t capacity) : capacity_(capacity) {
+    mem_ = static_cast<uint8_t *>(aligned_alloc(64, capacity * kObj));
+    memset(mem_, 0, capacity * kObj);
+    free_.reserve(capacity);
+    for (size_t i = capacity; i-- > 0;) {
+      Packet *p = new (mem_ + i * kObj) Packet();
+      p->set_pool(this);
+      free_.push_back(p);
+    }
+    gen_ = ++generation();
+  }
+  ~PacketPool() {
+    ++generation();  // thread caches of this pool are stale now
+    free(mem_);
+  }
+  size_t Capacity() const { return capacity_; }
+  size_t Size() const {  // available: the shared list (thread caches not counted)
+    std::lock_guard<std::mutex> lk(mu_);
+    return free_.size();
+  }
+  // all or nothing (packet_pool.h:56-58)
+  bool AllocBulk(Packet **pkts, size_t count, size_t len = 0) {
+    Cache &c = cache();
+    if (c.v.size() < count) {
+      std::lock_guard<std::mutex> lk(mu_);
+      size_t want = std::min(free_.size(), kCache / 2 + count - c.v.size());
+      for (size_t i = 0; i < want; i++) {
+        c.v.push_back(free_.back());
+        free_.pop_back();
+      }
+    }
+    if (c.v.size() < count) return false;
+    for (size_t i = 0; i < count; i++) {
+      pkts[i] = c.v.back();
+      c.v.pop_back();
+      pkts[i]->set_data_off(SNBUF_HEADROOM);
+      pkts[i]->set_data_len((uint16_t)len);
+      pkts[i]->set_total_len((uint32_t)len);
+    }
+    return true;
+  }
+  void Put(Packet *p) {
+    Cache &c = cache();
+    c.v.push_back(p);
+    if (c.v.size() >= kCache) Spill(c, kCache / 2);
+  }
+  // a worker thread's cache back into the shared list (thread exit)
+  void FlushThreadCache() {
+    Cache &c = cache();
+    Spill(c, c.v.size());
+  }
+
+ private:
+  static const size_t kCache = 512;
+  struct Cache {
+    uint64_t gen = 0;
+    PacketPool *owner = nullptr;
+    std::vector<Packet *> v;
+    ~Cache() {
+      if (owner && gen == generation()) owner->Spill(*this, v.size());
+    }
+  };
+  static std::atomic<uint64_t> &generation() {
+    static std::atomic<uint64_t> g{0};
+    return g;
+  }
+  Cache &cache() {
+    thread_local Cache c;
+    if (c.owner != this || c.gen != gen_) {
+      c.owner = this;
+      c.gen = gen_;
+      c.v.clear();
+    }
+    return c;
+  }
+  void Spill(Cache &c, size_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < n && !c.v.empty(); i++) {
+      free_.push_back(c.v.back());
+      c.v.pop_back();
+    }
+  }
+  size_t capacity_;
+  uint8_t *mem_ = nullptr;
+  uint64_t gen_ = 0;
+  mutable std::mutex mu_;
+  std::vector<Packet *> free_;
+};
+
+inline void Packet::Free(Packet *p) {
+  freed_packets()++;
+  if (p->pool_) p->pool_->Put(p);
+}
 
 class PacketBatch {
  public:

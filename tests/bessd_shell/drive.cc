@@ -22,13 +22,22 @@
 //                                 packet -> "out" + per packet: gate, D
 //                                 (dropped) or - (not emitted); "data <hex>"
 //                                 per packet's first 64 bytes afterwards
+//     pool <capacity>             a packet pool of `capacity` snbufs (bessd's
+//                                 --buffers, core/opts.cc:127): `pipeline`
+//                                 then allocates every Source batch from it
+//                                 (AllocBulk; a Source finding it empty
+//                                 waits) and copies the frame in, as Source
+//                                 does with its template, and the Sink frees
+//                                 each packet back (Packet::Free)
 //     pipeline <workers> <reps> <igate> <now_ns> <verify>
 //                                 Source -> module -> Sink on `workers`
 //                                 threads (pinned), each over its own slice
 //                                 of the frames `reps` times in 32-packet
 //                                 batches (wid = worker); worker 0 also runs
-//                                 the module's task (every 8 batches, then
-//                                 until the module holds no packet)
+//                                 the module's task (every 64 batches, then
+//                                 until the module holds no packet); with a
+//                                 pool: "pool <available> <capacity>
+//                                 <source_waits>" afterwards
 //                                 -> "pipeline <Mpps> <seconds> <packets>",
 //                                 "out" as above for the last pass, and with
 //                                 verify "order ok|bad": each worker's
@@ -141,11 +150,16 @@ struct Sink {  // where a worker's emitted and dropped packets go
   std::vector<uint16_t> *fast = nullptr;     // per packet (timing)
 
   uint8_t *pool = nullptr;
+  bool free_packets = false;  // pool mode: each packet goes back (Packet::Free)
   uint64_t n = 0;
   void take(Context &ctx) {
     for (auto &e : ctx.emitted) put(e.first, e.second);
     for (auto *p : ctx.dropped) put(p, 0xFFFF);
     n += ctx.emitted.size() + ctx.dropped.size();
+    if (free_packets) {
+      for (auto &e : ctx.emitted) bess::Packet::Free(e.first);
+      for (auto *p : ctx.dropped) bess::Packet::Free(p);
+    }
     ctx.emitted.clear();
     ctx.dropped.clear();
   }
@@ -175,6 +189,9 @@ static int run() {
   uint8_t *pool = nullptr;
   or_em *cpu_em = nullptr;
   std::vector<uint8_t *> bufs;
+  std::vector<char> fdata;  // the frames file (pool mode: the Sources' frames)
+  size_t fstride = 0;
+  bess::PacketPool *ppool = nullptr;
   std::string line;
   while (std::getline(std::cin, line)) {
     std::istringstream in(line);
@@ -216,21 +233,29 @@ static int run() {
       size_t stride, n;
       in >> path >> stride >> n;
       std::ifstream f(path, std::ios::binary);
-      std::vector<char> fr(stride);
+      fdata.assign(n * stride, 0);
+      f.read(fdata.data(), (std::streamsize)(n * stride));
+      fstride = stride;
       free(pool);
       bufs.clear();
       pool = static_cast<uint8_t *>(aligned_alloc(64, n * kObj));
       memset(pool, 0, n * kObj);
       for (size_t i = 0; i < n; i++) {
-        f.read(fr.data(), (std::streamsize)stride);
+        const char *fr = fdata.data() + i * stride;
         uint8_t *b = pool + i * kObj;
         bess::Packet *p = new (b) bess::Packet();
         p->set_pool_index((uint32_t)i);
-        memcpy(p->head_data<uint8_t *>(), fr.data(), stride);
+        memcpy(p->head_data<uint8_t *>(), fr, stride);
         p->set_total_len((uint32_t)stride);
         p->set_data_len((uint16_t)stride);
         bufs.push_back(b);
       }
+    } else if (op == "pool") {
+      size_t cap;
+      in >> cap;
+      delete ppool;
+      ppool = new bess::PacketPool(cap);
+      bess::PacketPool::default_pool() = ppool;
     } else if (op == "meta") {
       std::string path;
       size_t nb;
@@ -306,6 +331,8 @@ static int run() {
         continue;
       }
       const size_t n = bufs.size();
+      num_workers = nw;
+      std::atomic<uint64_t> source_waits{0};
       std::vector<std::string> out(n, "-");
       std::vector<uint16_t> fast(n, 0xFFFE);
       std::vector<uint64_t> seq(n, ~0ull);
@@ -320,6 +347,7 @@ static int run() {
         pin(w);
         Sink sink;
         sink.pool = pool;
+        sink.free_packets = ppool != nullptr;
         Context ctx;
         if (verify) {
           sink.gate = &out;
@@ -343,8 +371,30 @@ static int run() {
         for (int r = 0; r < reps; r++)
           for (size_t b0 = lo; b0 < hi; b0 += bess::PacketBatch::kMaxBurst) {
             bess::PacketBatch batch;  // the Source's batch
-            for (size_t i = b0; i < hi && i < b0 + bess::PacketBatch::kMaxBurst; i++)
-              batch.add(reinterpret_cast<bess::Packet *>(pool + i * kObj));
+            const size_t cnt = std::min(hi - b0, (size_t)bess::PacketBatch::kMaxBurst);
+            if (ppool) {
+              // packets from the pool, each filled with its frame (Source
+              // copies its template the same way); an empty pool: wait
+              // for the Sinks (worker 0 keeps running the module's task)
+              bess::Packet *pk[bess::PacketBatch::kMaxBurst];
+              while (!ppool->AllocBulk(pk, cnt, fstride)) {
+                source_waits++;
+                if (!cpu && w == 0 && m->is_task()) {
+                  m->RunTask(&ctx, nullptr, nullptr);
+                  sink.take(ctx);
+                }
+                std::this_thread::yield();
+              }
+              for (size_t j = 0; j < cnt; j++) {
+                memcpy(pk[j]->head_data<uint8_t *>(), fdata.data() + (b0 + j) * fstride,
+                       fstride);
+                pk[j]->set_pool_index((uint32_t)(b0 + j));
+                batch.add(pk[j]);
+              }
+            } else {
+              for (size_t i = b0; i < b0 + cnt; i++)
+                batch.add(reinterpret_cast<bess::Packet *>(pool + i * kObj));
+            }
             const uint64_t c0 = __rdtsc();
             if (cpu) {  // ExactMatch::ProcessBatch restated (exact_match.cc:224-244)
               const uint8_t *heads[bess::PacketBatch::kMaxBurst];
@@ -378,6 +428,7 @@ static int run() {
           t1 = now_s();
         }
         sunk[w] = sink.n;
+        if (ppool) ppool->FlushThreadCache();
         if (w == 0) {
           tsc[0] = c_proc;
           tsc[1] = c_sink;
@@ -408,6 +459,9 @@ static int run() {
                                                  : std::to_string(fast[i]).c_str());
       }
       printf("\n");
+      if (ppool)
+        printf("pool %zu %zu %llu\n", ppool->Size(), ppool->Capacity(),
+               (unsigned long long)source_waits.load());
       if (GpuModule *g = dynamic_cast<GpuModule *>(m)) {
         uint64_t st[11];
         if (g->PipeStats(0, st, 11) == 0)
@@ -442,6 +496,8 @@ static int run() {
     delete m;
   }
   free(pool);
+  bess::PacketPool::default_pool() = nullptr;
+  delete ppool;
   if (cpu_em) or_em_free(cpu_em);
   return 0;
 }

@@ -534,3 +534,54 @@ def test_metadata_fields_wildcard_pipeline_vs_oracle(drive, tmp_path):
     got = [x for x in out if x.startswith("out")][0].split()[1:]
     assert got == [str(int(w)) if int(w) < 64 else "D" for w in want]
     assert "order ok" in out
+
+
+def _wm_plugin_script(n_rules, n, seed=0x5EED):
+    """WildcardMatch plugin with C4-style rules over IMIX frames in 2 KB
+    slots; -> (script, frames, want) with want the oracle's gates"""
+    from oracle import oracle as O
+    rk, rm, prio, wg, wf, flen = P.wm_workload(n_rules, n, stride=2048, seed=seed)
+    script = ["create WildcardMatch " + hx(pb.dict_to_protobuf(
+        pb.WildcardMatchArg, {"fields": FIELDS}))]
+    ow = O.OracleWildcardMatch(fields=FIELDS)
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    for k, mk, p, g in zip(rk, rm, prio, wg):
+        kb, mb = k.tobytes(), mk.tobytes()
+        arg = dict(gate=int(g), priority=int(p),
+                   values=[{"value_bin": kb[a:c]} for a, c in cut],
+                   masks=[{"value_bin": mb[a:c]} for a, c in cut])
+        ow.add(**arg)
+        script.append("cmd add " + hx(pb.dict_to_protobuf(pb.WildcardMatchCommandAddArg, arg)))
+    script += ["connect %d" % g for g in range(64)]
+    return script, wf, ow.process(wf, 2048, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", ["WildcardMatch", "L4Checksum"])
+def test_pool_bounded_pipeline_16_workers(drive, tmp_path, cls):
+    """bessd's packet pool (262,144 snbufs, core/opts.cc:127): 16 workers'
+    Sources allocate every batch from it and the Sink frees each packet
+    back; the deferred plugin holds at most its pool share per worker
+    (GpuModule::PipeBudget), so the run completes, every packet's gate is
+    the oracle's, each worker's packets leave in order and every buffer is
+    back in the pool at the end"""
+    from oracle import oracle as O
+    n = 1 << 16
+    if cls == "WildcardMatch":
+        script, frames, want = _wm_plugin_script(20000, n)
+        exp = [str(int(w)) if int(w) < 64 else "D" for w in want]
+    else:
+        frames = P.cksum_workload(n, frame_len=1496)
+        ref = frames.copy()
+        _, l4w = O.cksum_process(ref, 2048, n, 2, False)
+        script = ["create L4Checksum -", "connect 0", "connect 1"]
+        exp = ["-" if int(w) == 0xFFFF else str(int(w)) for w in l4w]
+    fp = tmp_path / "f.bin"
+    frames.tofile(fp)
+    script += ["frames %s 2048 %d" % (fp, n), "pool 262144", "pipeline 16 3 0 0 1"]
+    out = run(drive, script)
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == exp
+    assert "order ok" in out
+    pool = [x.split() for x in out if x.startswith("pool")][0]
+    assert pool[1] == pool[2] == "262144", pool  # every buffer back, once
