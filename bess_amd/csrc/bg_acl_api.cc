@@ -490,6 +490,7 @@ int bg_acl_classify(bg_acl *h, const void *d_frames, size_t stride, size_t n,
   a.out = d_out;
   a.igate = igate;
   HIP_TRY(launch_acl(a, num_cus(dev), s));
+  img->launched_on(s);
   return 0;
 }
 

@@ -348,8 +348,12 @@ hipStream_t thread_stream(int device, hipStream_t given) {
   if (given) return given;
   if (device < 0 || device >= 16) return nullptr;
   hipStream_t &s = t_stage.streams[device];
-  if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
-    s = nullptr;  // fall back to the legacy stream
+  if (!s) {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+      s = nullptr;  // fall back to the legacy stream
+    else
+      own_stream(s);  // (lives as long as the thread; never destroyed)
+  }
   return s;
 }
 
@@ -608,6 +612,7 @@ static int em_launch(const std::vector<bg_field> &df, EmImage *img, const void *
   a.t = img->t;
   img->used_on(s);
   HIP_TRY(launch_em(a, num_cus(img->device), s));
+  img->launched_on(s);
   return 0;
 }
 
@@ -1411,7 +1416,7 @@ static int wm_sync_locked(bg_wm *wm, int device, hipStream_t s) {
   img->no_tags = no_tags;
   img->a = wm->host_a;
   img->a.t.base = img->d;
-  img->jit = wm_jit_request(img->a, make_plan(wm->dfields, false, 0), wm->kw);
+  img->jit = wm_jit_request(img->a, make_plan(wm->dfields, false, 0), wm->kw, device);
   wm->dev.publish(device, img.release());
   return 0;
 }
@@ -1449,9 +1454,11 @@ static int wm_launch(const std::vector<bg_field> &df, WmImage *img, const void *
   hipError_t e;
   if (!a.ab_phase && wm_jit_launch(img->jit.get(), a, img->device, num_cus(img->device), s, &e)) {
     HIP_TRY(e);
+    img->launched_on(s);
     return 0;
   }
   HIP_TRY(launch_wm(a, num_cus(img->device), s));
+  img->launched_on(s);
   return 0;
 }
 

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <shared_mutex>
 #include <unordered_set>
 #include <vector>
 
@@ -29,6 +30,8 @@ struct Registry {
   std::mutex mu;
   std::unordered_set<DevImage *> live;  // for stream_gone
   std::vector<Dead> dead;
+  std::shared_mutex own_mu;
+  std::unordered_set<uintptr_t> own;  // the library's streams (own_stream)
 };
 
 Registry &reg() {
@@ -61,10 +64,24 @@ bool done(Dead &x, bool wait) {
   return true;
 }
 
+// the null stream or one the library created: fenced by recording on it
+bool library_stream(hipStream_t s) {
+  if (!s) return true;
+  std::shared_lock<std::shared_mutex> lk(reg().own_mu);
+  return reg().own.count(reinterpret_cast<uintptr_t>(s)) != 0;
+}
+
 }  // namespace
+
+void own_stream(hipStream_t s) {
+  if (!s) return;
+  std::unique_lock<std::shared_mutex> lk(reg().own_mu);
+  reg().own.insert(reinterpret_cast<uintptr_t>(s));
+}
 
 DevImage::DevImage() {
   for (auto &u : users) u.store(0, std::memory_order_relaxed);
+  for (auto &u : ext) u.store(0, std::memory_order_relaxed);
   std::lock_guard<std::mutex> lk(reg().mu);
   reg().live.insert(this);
 }
@@ -80,9 +97,12 @@ DevImage::~DevImage() {
     (void)hipFree(d);
   }
   d = nullptr;
+  for (hipEvent_t &e : ext_ev)
+    if (e) (void)hipEventDestroy(e);  // (retire handed the recorded ones on)
 }
 
 void DevImage::used_on(hipStream_t s) {
+  if (!library_stream(s)) return;  // launched_on fences it
   const uintptr_t e = enc(s);
   for (auto &u : users) {
     uintptr_t v = u.load(std::memory_order_acquire);
@@ -93,6 +113,32 @@ void DevImage::used_on(hipStream_t s) {
     }
   }
   overflow.store(true, std::memory_order_release);
+}
+
+void DevImage::launched_on(hipStream_t s) {
+  if (library_stream(s)) return;
+  const uintptr_t e = enc(s);
+  int z = 0;
+  while (!ext_lock.compare_exchange_weak(z, 1, std::memory_order_acquire)) z = 0;
+  int slot = -1;
+  for (int i = 0; i < kMaxImageExtUsers && slot < 0; i++) {
+    const uintptr_t v = ext[i].load(std::memory_order_relaxed);
+    if (v == e) slot = i;
+  }
+  for (int i = 0; i < kMaxImageExtUsers && slot < 0; i++)
+    if (ext[i].load(std::memory_order_relaxed) == 0) {
+      ext[i].store(e, std::memory_order_relaxed);
+      slot = i;
+    }
+  bool ok = slot >= 0;
+  if (ok && !ext_ev[slot] &&
+      hipEventCreateWithFlags(&ext_ev[slot], hipEventDisableTiming) != hipSuccess) {
+    ext_ev[slot] = nullptr;
+    ok = false;
+  }
+  if (ok && hipEventRecord(ext_ev[slot], s) != hipSuccess) ok = false;
+  ext_lock.store(0, std::memory_order_release);
+  if (!ok) overflow.store(true, std::memory_order_release);
 }
 
 int upload_image(DevImage *img, int dev, const void *host, uint64_t bytes,
@@ -132,6 +178,12 @@ void retire_image(DevImage *img) {
         }
         x.evs.push_back(ev);
       }
+      // callers' streams: the events their launches recorded
+      for (int i = 0; i < kMaxImageExtUsers; i++)
+        if (img->ext[i].load(std::memory_order_acquire) && img->ext_ev[i]) {
+          x.evs.push_back(img->ext_ev[i]);
+          img->ext_ev[i] = nullptr;
+        }
     }
   }
   {
@@ -162,6 +214,10 @@ void reap_images(bool wait) {
 
 void stream_gone(hipStream_t s) {
   const uintptr_t e = enc(s);
+  {
+    std::unique_lock<std::shared_mutex> lk(reg().own_mu);
+    reg().own.erase(reinterpret_cast<uintptr_t>(s));
+  }
   std::lock_guard<std::mutex> lk(reg().mu);
   for (DevImage *img : reg().live)
     for (auto &u : img->users) {

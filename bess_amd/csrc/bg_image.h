@@ -11,7 +11,10 @@
 //   * the next launch on a device whose image is older builds a NEW image
 //     (fresh allocation), uploads it and publishes it for that device;
 //   * the image it replaces is retired: an event is recorded on every stream
-//     that launched against it (DevImage::used_on), and it is freed only
+//     of the library's own that launched against it (DevImage::used_on),
+//     and a caller's stream -- whose handle the library must not keep, as
+//     the caller may destroy it -- is fenced by an event the launch itself
+//     recorded after it (DevImage::launched_on); the image is freed only
 //     when all those events have completed (reap_images).
 // Each device has its own published image (a replica), so one module can be
 // driven from workers on several GPUs of one process (core/worker.h:77).
@@ -27,6 +30,7 @@ namespace bg {
 
 constexpr int kMaxDevices = 16;
 constexpr int kMaxImageUsers = 256;
+constexpr int kMaxImageExtUsers = 64;
 
 // One device copy of one table version (subclassed by each table for the
 // launch arguments that go with the image).
@@ -39,13 +43,27 @@ struct DevImage {
 
   DevImage();
   virtual ~DevImage();
-  // A launch against this image was queued on `s` (lock-free; the null
-  // stream included). Retirement fences every such stream.
+  // A launch against this image is about to be queued on `s` (lock-free
+  // for the library's own streams and the null stream, which retirement
+  // fences by recording on them).
   void used_on(hipStream_t s);
+  // ... and was queued: a stream the library does not own gets an event
+  // recorded behind the launch (the image's event for that stream).
+  void launched_on(hipStream_t s);
 
   std::atomic<uintptr_t> users[kMaxImageUsers];
   std::atomic<bool> overflow{false};  // more streams than slots: device sync
+  // callers' streams: the handle (identity only, never recorded on at
+  // retirement) and the event its launches re-record
+  std::atomic<uintptr_t> ext[kMaxImageExtUsers];
+  hipEvent_t ext_ev[kMaxImageExtUsers] = {};
+  std::atomic<int> ext_lock{0};
 };
+
+// The library created `s` (pipe slots, worker threads' streams): images
+// fence it by recording on it at retirement; stream_gone() before it is
+// destroyed.
+void own_stream(hipStream_t s);
 
 // Allocate img->d (bytes, at least 256) on `dev` and copy `host` into it on
 // stream s, synchronously (control path). Returns 0 or -errno.

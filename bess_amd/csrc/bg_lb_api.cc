@@ -193,6 +193,7 @@ int bg_hlb_classify(bg_hlb *h, const void *d_frames, size_t stride, size_t n,
   a.n = n;
   a.out = d_gates;
   HIP_TRY(launch_hlb(a, num_cus(dev), s));
+  img->launched_on(s);
   return 0;
 }
 

@@ -227,6 +227,7 @@ int bg_lpm_classify(bg_lpm *h, const void *d_frames, size_t stride, size_t n,
   a.out = d_out;
   a.default_gate = default_gate;
   HIP_TRY(launch_lpm(a, num_cus(dev), s));
+  img->launched_on(s);
   return 0;
 }
 

@@ -104,6 +104,7 @@ int bg_snat_classify(bg_snat *h, void *d_frames, size_t stride, size_t n,
   a.out = d_out;
   a.dir = (uint32_t)dir;
   HIP_TRY(launch_nat(a, num_cus(dev), s));
+  img->launched_on(s);
   return 0;
 }
 

@@ -14,8 +14,10 @@ namespace bg {
 struct WmJit;
 // The run-time compiled kernels for an image's tuple data (a) and the key
 // plan of its fields at frame offset 0; shared by every image of the same
-// shape, compiled on a background thread. nullptr: no tag-word image.
-std::shared_ptr<WmJit> wm_jit_request(const WmArgs &a, const FieldPlan &plan, uint32_t kw);
+// shape, compiled on a background thread for `device`'s architecture.
+// nullptr: no tag-word image.
+std::shared_ptr<WmJit> wm_jit_request(const WmArgs &a, const FieldPlan &plan, uint32_t kw,
+                                      int device);
 // 1 ready, 0 compiling, -1 failed or none
 int wm_jit_state(const WmJit *j);
 // block until compiled (0), failed (-ENOEXEC) or timeout_ms passed (-ETIMEDOUT)

@@ -426,6 +426,7 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
       e = hipHostMalloc(reinterpret_cast<void **>(&s.h_wb),
                         batch * std::min(p->w, kWriteback), hipHostMallocDefault);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
+    if (e == hipSuccess) bg::own_stream(s.st);
     if (e == hipSuccess)
       e = hipHostMalloc(reinterpret_cast<void **>(&s.h_done), 64,
                         hipHostMallocMapped | hipHostMallocCoherent);
