@@ -409,9 +409,6 @@ hipError_t launch_dnat_scatter(const uint64_t *d_up, size_t k, uint64_t *ent,
 hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
-// dense 64 B header slabs read with whole-line loads (bg_wm_body.h QUAD);
-// the A/B build's BG_WM_QUAD=0 keeps the pair loads
-bool wm_quad_loads();
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword
 #endif
 bool fits_nch2(const FieldPlan &fp);

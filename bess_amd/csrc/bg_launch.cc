@@ -31,8 +31,6 @@ int knob(const char *name, int dflt) {
 }
 #endif
 
-bool wm_quad_loads() { return knob("BG_WM_QUAD", 1) != 0; }
-
 uint32_t path_flags() {
   uint32_t f = g_path.load(std::memory_order_relaxed);
 #ifdef BG_AB  // scripts/variants.py selects paths through the environment

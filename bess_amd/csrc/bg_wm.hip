@@ -32,15 +32,11 @@ hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   const bool n2 = fits_nch2(a.fp);
   if (a.fp.direct || a.fp.nch > 4 || a.t.nbp > (1u << 15)) return hipErrorInvalidValue;
-  // dense 64 B slots whose window is two chunks inside the slot: whole-line
-  // loads gathered by quad broadcasts (or, A/B build BG_WM_QUAD=0, the pair
-  // loads)
+  // the pair loads: dense 64 B slots whose window is two chunks inside the slot
   const bool pair = n2 && a.stride == 64 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64;
-  const bool quad = pair && wm_quad_loads();
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
-    return quad ? launch_tags<KW, 2, 2>(a, num_cus, s)                     \
-                : pair ? launch_tags<KW, 2, 1>(a, num_cus, s)              \
+    return pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                     \
                 : n2 ? launch_tags<KW, 2, 0>(a, num_cus, s)                \
                      : launch_tags<KW, 4, 0>(a, num_cus, s);
   BG_WT(1) BG_WT(2) BG_WT(4) BG_WT(8)

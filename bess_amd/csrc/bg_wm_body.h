@@ -298,77 +298,6 @@ __device__ __forceinline__ void pair_window(const uint32_t (&r)[8], int lane,
   w[9] = 0;
 }
 
-// Dense 64 B header slab (QUAD, PAIR == 2): a wave's 64 slots are 4 KB
-// contiguous, read whole by four lane-contiguous 16 B loads -- lane l's load
-// c is unit 64c + l: chunk l & 3 of slot 16c + (l >> 2) -- so every load
-// instruction asks for whole 128 B lines (the pair loads above ask for 32 B
-// of each of 32 lines: 64 B requests, which stream at ~4.2 TB/s where whole
-// lines reach ~5.8, em_slab_kernel). Lane l takes slot 16 (l & 3) + (l >> 2):
-// that slot's chunks sit in register l & 3 of the lanes of l's own quad, so
-// DPP quad broadcasts and a select gather the window (no LDS).
-__device__ __forceinline__ uint64_t quad_slot(int lane) {
-  return 16u * (uint32_t)(lane & 3) + (uint32_t)(lane >> 2);
-}
-
-__device__ __forceinline__ void load_quad(const uint8_t *__restrict__ frames, uint64_t n,
-                                          uint64_t p0, int lane, uint32_t (&r)[16]) {
-  const uint64_t units = (n - p0 < 64 ? n - p0 : 64) * 4;
-  const uint4 *g = reinterpret_cast<const uint4 *>(frames) + p0 * 4;
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const uint32_t u = (uint32_t)(c * 64 + lane);
-    const uint4 x = u < units ? ld_stream(g + u) : make_uint4(0, 0, 0, 0);
-    r[4 * c] = x.x;
-    r[4 * c + 1] = x.y;
-    r[4 * c + 2] = x.z;
-    r[4 * c + 3] = x.w;
-  }
-}
-
-// lane q of every quad, broadcast to the quad (DPP quad_perm [q, q, q, q])
-template <int Q>
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, Q | Q << 2 | Q << 4 | Q << 6, 0xF, 0xF,
-                                            false);
-}
-
-// chunk Q of this lane's slot into w[at .. at + 4): register (lane & 3) of
-// quad lane Q
-template <int Q>
-__device__ __forceinline__ void quad_chunk(const uint32_t (&r)[16], int lane, uint32_t (&w)[10],
-                                           int at) {
-  const bool c1 = lane & 1, c2 = lane & 2;
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    const uint32_t x0 = quad_bcast<Q>(r[d]);
-    const uint32_t x1 = quad_bcast<Q>(r[4 + d]);
-    const uint32_t x2 = quad_bcast<Q>(r[8 + d]);
-    const uint32_t x3 = quad_bcast<Q>(r[12 + d]);
-    w[at + d] = c2 ? (c1 ? x3 : x2) : (c1 ? x1 : x0);
-  }
-}
-
-template <int Q0>
-__device__ __forceinline__ void quad_window_q(const uint32_t (&r)[16], int lane,
-                                              uint32_t (&w)[10]) {
-  quad_chunk<Q0>(r, lane, w, 0);
-  quad_chunk<Q0 + 1>(r, lane, w, 4);
-  w[8] = 0;
-  w[9] = 0;
-}
-
-template <int NCH>
-__device__ __forceinline__ void quad_window(const uint32_t (&r)[16], int lane, uint32_t q0,
-                                            uint32_t (&w)[NCH * 4 + 2]) {
-  static_assert(NCH == 2, "quad windows carry two chunks");
-  if (q0 == 0)  // wave-uniform: the DPP patterns are immediates
-    quad_window_q<0>(r, lane, w);
-  else if (q0 == 1)
-    quad_window_q<1>(r, lane, w);
-  else
-    quad_window_q<2>(r, lane, w);
-}
-
 template <class Spec, int KW, int NCH, int PAIR>
 __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -396,24 +325,18 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
-  uint32_t wn[PAIR == 2 ? 16 : PAIR ? 8 : NCH * 4 + 2];
-  const uint32_t q0 = (uint32_t)a.fp.win_lo >> 4;
-  if constexpr (PAIR == 2) {
-    if (t < ntiles) load_quad(a.frames, a.n, t * 64, lane, wn);
-  } else if constexpr (PAIR) {
+  uint32_t wn[PAIR ? 8 : NCH * 4 + 2];
+  if constexpr (PAIR) {
     if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, wn);
   } else {
     if (t < ntiles && t * 64 + lane < a.n)
       load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
   }
   for (; t < ntiles; t += nw) {
-    const uint64_t idx = t * 64 + (PAIR == 2 ? quad_slot(lane)
-                                   : PAIR ? pair_slot(lane) : (uint64_t)lane);
+    const uint64_t idx = t * 64 + (PAIR ? pair_slot(lane) : (uint64_t)lane);
     const bool live = idx < a.n;
     uint32_t w[NCH * 4 + 2];
-    if constexpr (PAIR == 2) {
-      quad_window<NCH>(wn, lane, q0, w);
-    } else if constexpr (PAIR) {
+    if constexpr (PAIR) {
       pair_window<NCH>(wn, lane, w);
     } else {
 #pragma unroll
@@ -439,9 +362,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
     // loads retire in order (vmcnt), so waiting for a load also waits for
     // every older one -- the direct values, consumed in this tile, must not
     // be younger than the prefetch the next tile consumes
-    if constexpr (PAIR == 2) {
-      if (t + nw < ntiles) load_quad(a.frames, a.n, (t + nw) * 64, lane, wn);
-    } else if constexpr (PAIR) {
+    if constexpr (PAIR) {
       if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, wn);
     } else {
       const uint64_t nidx = (t + nw) * 64 + lane;
