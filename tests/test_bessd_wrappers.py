@@ -564,9 +564,12 @@ def test_pool_bounded_pipeline_16_workers(drive, tmp_path, cls):
     back; the deferred plugin holds at most its pool share per worker
     (GpuModule::PipeBudget), so the run completes, every packet's gate is
     the oracle's, each worker's packets leave in order and every buffer is
-    back in the pool at the end"""
+    back in the pool at the end -- except those the reference never frees:
+    L4Checksum does not emit TCP packets when not verifying (P8,
+    l4_checksum.cc:72-80), so each pass keeps its TCP packets out of the
+    pool, exactly as many as the oracle leaves unemitted"""
     from oracle import oracle as O
-    n = 1 << 16
+    n, reps = 1 << 16, 3
     if cls == "WildcardMatch":
         script, frames, want = _wm_plugin_script(20000, n)
         exp = [str(int(w)) if int(w) < 64 else "D" for w in want]
@@ -578,10 +581,11 @@ def test_pool_bounded_pipeline_16_workers(drive, tmp_path, cls):
         exp = ["-" if int(w) == 0xFFFF else str(int(w)) for w in l4w]
     fp = tmp_path / "f.bin"
     frames.tofile(fp)
-    script += ["frames %s 2048 %d" % (fp, n), "pool 262144", "pipeline 16 3 0 0 1"]
+    script += ["frames %s 2048 %d" % (fp, n), "pool 262144", "pipeline 16 %d 0 0 1" % reps]
     out = run(drive, script)
     got = [x for x in out if x.startswith("out")][0].split()[1:]
     assert got == exp
     assert "order ok" in out
     pool = [x.split() for x in out if x.startswith("pool")][0]
-    assert pool[1] == pool[2] == "262144", pool  # every buffer back, once
+    kept = reps * exp.count("-")  # never emitted, never freed (the reference's leak)
+    assert int(pool[2]) == 262144 and int(pool[1]) == 262144 - kept, (pool, kept)
