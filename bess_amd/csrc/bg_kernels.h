@@ -365,12 +365,19 @@ struct RingArgs {
 // round), so a 1024-packet batch takes one round of loads and lookups
 // rather than four on one wave (a ticket's latency is its rounds')
 constexpr int kRingBlock = 256;
+// + one wave that only writes the done words: a store's completion is
+// waited for by the next load or atomic of the wave that issued it (vector
+// memory operations retire in order), and a done word bound for host memory
+// takes microseconds to complete under load, so the wave that claims the
+// next ticket must not be the one that wrote the last done word
+constexpr int kRingThreads = kRingBlock + 64;
 constexpr int kRingLaneWords = 16;
 // a descriptor slot: 4 tagged words + 4 of padding, one 64-byte line, so a
 // host writing it through write-combining buffers fills a whole buffer,
 // which leaves for the device at once (a half-written line can wait in the
 // buffer until the next descriptor's stores)
 constexpr int kRingDescWords = 8;
+
 // descriptor word 3, bits 16..: how the ticket's frames and gates meet the
 // host (bg_ring_set_coherence). kRingSysAcquire: the frames may sit in
 // memory the device caches non-coherently (mapped host memory that is not

@@ -460,6 +460,59 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
   }
 }
 
+// The ticket loop's two barriers without __syncthreads' fences:
+// __syncthreads' workgroup acquire waits for every outstanding vector memory
+// operation of each wave (vmcnt(0)), which for the done wave is the done
+// word still in flight to the host -- the stall the done wave exists to
+// avoid. Each wave's LDS writes before it are complete (lgkmcnt).
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// The done wave (threads kRingBlock.. of a worker workgroup): per ticket,
+// after the first barrier it takes the ticket's number, after the second
+// (every wave's gate stores complete) its lane 0 writes the done word --
+// and never waits for that store, so no claim or frame load of the next
+// ticket waits behind the write's trip to the host. Its barriers pair one
+// to one with em_ring_kernel's.
+__device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldone,
+                                            const uint64_t *sh_w, const uint64_t *sh_t,
+                                            const uint32_t *sh_go, uint32_t lane) {
+  (void)lane;
+  for (;;) {
+    ring_barrier();  // B1: the ticket is in sh_*
+    if (!*sh_go) return;
+    const uint64_t t = *sh_t;
+    const bool release = (sh_w[3] & kRingRelease) != 0;
+    ring_barrier();  // B2: the gates are stored (sh_* free for the next ticket)
+    if ((threadIdx.x & 63) == 0) {
+#ifdef BG_AB
+      uint64_t *tr = a.trace && t < a.trace_n ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5
+                                              : nullptr;
+      if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+      // every wave's gate stores (system-scope write-through stores,
+      // completed by each wave's vmcnt(0) before B2) reach the host before
+      // the done word; with kRingRelease the done store is a system-scope
+      // release as well (L2 written back first)
+      if (release)
+        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef BG_AB
+      if (tr) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tr[4] = __builtin_amdgcn_s_memrealtime();
+      }
+#endif
+    }
+  }
+}
+
 // Workgroup b >= 1 serves submission lane (b - 1) % nlanes: it claims the
 // lane's next ticket (one atomic; claims run ahead of publication, so the
 // lane's workgroups queue up on its coming tickets), waits until it is
@@ -470,7 +523,7 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
 // done in host memory after them (kRingRelease: as a system-scope release).
 // Create a ring with as many lanes as workers submit on.
 template <int KW, int NCH>
-__global__ __launch_bounds__(kRingBlock) __attribute__((amdgpu_num_sgpr(80)))
+__global__ __launch_bounds__(kRingThreads) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ uint64_t sh_w[4];
@@ -486,6 +539,10 @@ void em_ring_kernel(RingArgs a) {
   const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * kRingDescWords;
   uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   copy_table_to_lds(lds, a.t);  // (ends with a barrier)
+  if (threadIdx.x >= kRingBlock) {  // wave-uniform
+    ring_done_wave(a, ldone, sh_w, &sh_t, &sh_go, lane);
+    return;
+  }
   const uint64_t mask48 = (1ull << 48) - 1;
   constexpr int kPpl = 4;  // packets per lane per round, loads in flight
   for (;;) {
@@ -537,15 +594,16 @@ void em_ring_kernel(RingArgs a) {
       sh_t = t;
       sh_go = go;
     }
-    __syncthreads();
+    // B1 (ring_barrier): the frames' freshness for every wave is the
+    // system-scope acquire above (its invalidations are the CU's L1 and the
+    // XCD's L2)
+    ring_barrier();
     if (!sh_go) return;
     const uint8_t *frames = reinterpret_cast<const uint8_t *>(sh_w[0] & mask48);
     uint16_t *gates = reinterpret_cast<uint16_t *>(sh_w[1] & mask48);
     const uint32_t n = (uint32_t)sh_w[2];
     const uint64_t stride = (sh_w[2] >> 32) & 0xFFFF;
     const uint32_t dflt = (uint32_t)(sh_w[3] & 0xFFFF);
-    const bool release = (sh_w[3] & kRingRelease) != 0;
-    const uint64_t t = sh_t;
     for (uint32_t base = threadIdx.x; base < n; base += kRingBlock * kPpl) {
       // kPpl packets per lane, their header windows loaded before any key
       // is built; one named window array per packet (a 2-D array indexed
@@ -568,32 +626,8 @@ void em_ring_kernel(RingArgs a) {
                              __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-#ifdef BG_AB
-      uint64_t *tr = a.trace && t < a.trace_n ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5
-                                              : nullptr;
-      if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
-#endif
-      // every wave's gate stores (system-scope write-through stores,
-      // completed by each wave's vmcnt(0) before the barrier) reach the
-      // host before the done word; with kRingRelease the done store is a
-      // system-scope release as well (L2 written back first)
-      if (release)
-        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      else
-        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-#ifdef BG_AB
-      if (tr) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        tr[4] = __builtin_amdgcn_s_memrealtime();
-      }
-#endif
-    }
-    __syncthreads();  // sh_* are rewritten for the next ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gates complete
+    ring_barrier();  // B2 (then sh_* may be rewritten for the next ticket)
   }
 }
 
@@ -1513,7 +1547,7 @@ hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s) {
 #define BG_RING(KW, NCH)                                                     \
   if (a.t.kw == KW && nch == NCH) {                                          \
     hipLaunchKernelGGL((em_ring_kernel<KW, NCH>), dim3((unsigned)blocks),     \
-                       dim3(kRingBlock), lds, s, a);                         \
+                       dim3(kRingThreads), lds, s, a);                       \
     return hipGetLastError();                                                \
   }
 #define BG_RINGS(KW) BG_RING(KW, 0) BG_RING(KW, 2) BG_RING(KW, 4)

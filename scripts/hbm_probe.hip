@@ -25,6 +25,10 @@
 //             read from a 4 MiB tag region and, for half the packets, one
 //             random 16 B read from a 32 MiB key region -- C5's 1 M-rule
 //             ExactMatch probe shape (36 MB table)
+//   rnd36s  : the same random reads behind the C5 kernel's own stream: a
+//             wave reads its 64 slots (4 KB) with four lane-contiguous 16 B
+//             loads (em_slab_kernel's shape), lane l then makes slot l's
+//             random reads with a hash of the data it loaded
 // `./hbm_probe GiB only SHAPE BLOCKS_PER_CU LAUNCHES` runs one shape (for
 // rocprofv3 --pmc passes: FETCH_SIZE per launch against a known shape).
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
@@ -136,6 +140,27 @@ __global__ __launch_bounds__(512) void rnd36(const u32x4 *src, size_t nslots,
   }
 }
 
+// rnd36 with em_slab_kernel's load shape (nslots: a multiple of 64)
+__global__ __launch_bounds__(512) void rnd36s(const u32x4 *src, size_t nslots,
+                                              const uint32_t *tab, uint16_t *gates) {
+  const u32x4 *keys = reinterpret_cast<const u32x4 *>(tab + (1u << 20));
+  const int lane = threadIdx.x & 63;
+  const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t * 64 < nslots;
+       t += nwaves) {
+    const u32x4 *g = src + t * 256;
+    const u32x4 a = ldnt(g + lane), b = ldnt(g + 64 + lane), c = ldnt(g + 128 + lane),
+                d = ldnt(g + 192 + lane);
+    const uint32_t h = mix32((uint32_t)(t * 64 + lane) ^ a.x ^ b.y ^ c.z ^ d.w);
+    uint32_t x = tab[h & ((1u << 20) - 1)];
+    if (h >> 31) {
+      const u32x4 k = keys[(h >> 8) & ((1u << 21) - 1)];
+      x ^= k.x ^ k.w;
+    }
+    gates[t * 64 + lane] = (uint16_t)x;
+  }
+}
+
 __global__ __launch_bounds__(512) void wfull16(u32x4 *dst, size_t n16) {
   const size_t step = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += step)
@@ -180,15 +205,15 @@ int main(int argc, char **argv) {
   const bool wr = argc > 2 && argv[2][0] == 'w';
   const bool sc = argc > 2 && argv[2][0] == 's';
   const bool only = argc > 5 && !strcmp(argv[2], "only");
-  const char *names[10] = {"full16", "em32", "slot64", "half32",
-                           "wfull16", "w64s192", "w64s128", "s2k32", "s2k64", "rnd36"};
+  const char *names[11] = {"full16", "em32",  "slot64", "half32", "wfull16", "w64s192",
+                           "w64s128", "s2k32", "s2k64", "rnd36", "rnd36s"};
   uint32_t *tab = nullptr;
   CK(hipMalloc(&tab, 36u << 20));
   CK(hipMemset(tab, 0x33, 36u << 20));
-  int s0 = wr ? 4 : sc ? 7 : 0, s1 = wr ? 7 : sc ? 10 : 4;
+  int s0 = wr ? 4 : sc ? 7 : 0, s1 = wr ? 7 : sc ? 11 : 4;
   int only_bpc = 0, only_launches = 0;
   if (only) {
-    for (int k = 0; k < 10; k++)
+    for (int k = 0; k < 11; k++)
       if (!strcmp(argv[3], names[k])) s0 = k, s1 = k + 1;
     only_bpc = atoi(argv[4]);
     only_launches = atoi(argv[5]);
@@ -230,8 +255,11 @@ int main(int argc, char **argv) {
         else if (shape == 8)
           hipLaunchKernelGGL((s2k<4, 0>), dim3(blocks), dim3(512), 0, 0, src,
                              bytes / 2048, gates);
-        else
+        else if (shape == 9)
           hipLaunchKernelGGL(rnd36, dim3(blocks), dim3(512), 0, 0, src, nslots, tab,
+                             gates);
+        else
+          hipLaunchKernelGGL(rnd36s, dim3(blocks), dim3(512), 0, 0, src, nslots, tab,
                              gates);
       };
       if (only) {  // a fixed number of launches, no timing (rocprofv3 passes)

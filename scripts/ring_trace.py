@@ -38,6 +38,7 @@ def main():
         per_lane = n // T // B
         os.environ["BG_RING_TRACE"] = str(per_lane)
         ring = F.Ring(t, slots=4096, lanes=T)
+        ring.set_coherence(1, 0)  # as the pipes and the bench sweep use it
         os.environ.pop("BG_RING_TRACE")
         ring.run_lanes(d_frames, 64, n, B, 8192, d_g, T)  # warm (stamps overwritten)
         dt = ring.run_lanes(d_frames, 64, n, B, 8192, d_g, T)

@@ -53,7 +53,10 @@
 //                                 MakeKeys + CuckooMap Find, EmitPacket with
 //                                 the created module's connected gates) --
 //                                 the cpu_baseline in the same harness
+#include <execinfo.h>
 #include <pthread.h>
+#include <signal.h>
+#include <unistd.h>
 #include <x86intrin.h>
 #include <sched.h>
 #include <stdio.h>
@@ -502,7 +505,18 @@ static int run() {
   return 0;
 }
 
+// a fatal signal prints the faulting thread's stack (test diagnostics)
+static void on_fatal(int sig) {
+  void *frames[64];
+  const int n = backtrace(frames, 64);
+  fprintf(stderr, "drive: signal %d\n", sig);
+  backtrace_symbols_fd(frames, n, 2);
+  _exit(128 + sig);
+}
+
 int main(int argc, char **argv) {
+  signal(SIGSEGV, on_fatal);
+  signal(SIGBUS, on_fatal);
   if (argc > 1 && !strcmp(argv[1], "dump")) return dump();
   if (argc > 1 && !strcmp(argv[1], "run")) return run();
   fprintf(stderr, "usage: drive dump | run < script\n");
