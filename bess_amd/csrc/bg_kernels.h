@@ -372,6 +372,11 @@ constexpr int kRingBlock = 256;
 // next ticket must not be the one that wrote the last done word
 constexpr int kRingThreads = kRingBlock + 64;
 constexpr int kRingLaneWords = 16;
+// A worker workgroup takes up to kRingRunMax published tickets of its lane
+// as one run, and claims about kRingRunPackets packets' worth of tickets at
+// a time (one round of its 256 lanes x 4 packets)
+constexpr uint32_t kRingRunMax = 16;
+constexpr uint32_t kRingRunPackets = kRingBlock * 4;
 // a descriptor slot: 4 tagged words + 4 of padding, one 64-byte line, so a
 // host writing it through write-combining buffers fills a whole buffer,
 // which leaves for the device at once (a half-written line can wait in the

@@ -419,28 +419,25 @@ __device__ __forceinline__ void ring_dispatch(const RingArgs &a) {
   }
 }
 
+// kPpl packets' keys of one round: packet j's frame at f[j] (null: none)
 template <int KW, int NCH>
-__device__ __forceinline__ void ring_key1(const uint8_t *frames, uint64_t stride,
-                                          uint32_t n, uint32_t i,
-                                          const FieldPlan &fp,
+__device__ __forceinline__ void ring_key1(const uint8_t *f, const FieldPlan &fp,
                                           uint32_t (&w)[NCH * 4 + 2]) {
 #pragma unroll
   for (int q = 0; q < NCH * 4 + 2; q++) w[q] = 0;
-  if (i < n) load_window<NCH>(frames + (uint64_t)i * stride, fp, w);
+  if (f) load_window<NCH>(f, fp, w);
 }
 
 template <int KW, int NCH>
-__device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride,
-                                          uint32_t n, uint32_t base,
-                                          const FieldPlan &fp, uint64_t (&k0)[KW],
-                                          uint64_t (&k1)[KW], uint64_t (&k2)[KW],
-                                          uint64_t (&k3)[KW]) {
+__device__ __forceinline__ void ring_keys(const uint8_t *const (&f)[4], const FieldPlan &fp,
+                                          uint64_t (&k0)[KW], uint64_t (&k1)[KW],
+                                          uint64_t (&k2)[KW], uint64_t (&k3)[KW]) {
   if constexpr (NCH > 0) {
     uint32_t w0[NCH * 4 + 2], w1[NCH * 4 + 2], w2[NCH * 4 + 2], w3[NCH * 4 + 2];
-    ring_key1<KW, NCH>(frames, stride, n, base, fp, w0);
-    ring_key1<KW, NCH>(frames, stride, n, base + kRingBlock, fp, w1);
-    ring_key1<KW, NCH>(frames, stride, n, base + 2 * kRingBlock, fp, w2);
-    ring_key1<KW, NCH>(frames, stride, n, base + 3 * kRingBlock, fp, w3);
+    ring_key1<KW, NCH>(f[0], fp, w0);
+    ring_key1<KW, NCH>(f[1], fp, w1);
+    ring_key1<KW, NCH>(f[2], fp, w2);
+    ring_key1<KW, NCH>(f[3], fp, w3);
     extract_key<KW, NCH>(w0, fp, k0);
     extract_key<KW, NCH>(w1, fp, k1);
     extract_key<KW, NCH>(w2, fp, k2);
@@ -449,9 +446,8 @@ __device__ __forceinline__ void ring_keys(const uint8_t *frames, uint64_t stride
     uint64_t (*ks[4])[KW] = {&k0, &k1, &k2, &k3};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint32_t i = base + j * kRingBlock;
-      if (i < n) {
-        direct_key<KW>(frames + (uint64_t)i * stride, fp, *ks[j]);
+      if (f[j]) {
+        direct_key<KW>(f[j], fp, *ks[j]);
       } else {
 #pragma unroll
         for (int q = 0; q < KW; q++) (*ks[j])[q] = 0;
@@ -471,64 +467,69 @@ __device__ __forceinline__ void ring_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// The done wave (threads kRingBlock.. of a worker workgroup): per ticket,
-// after the first barrier it takes the ticket's number, after the second
-// (every wave's gate stores complete) its lane 0 writes the done word --
-// and never waits for that store, so no claim or frame load of the next
-// ticket waits behind the write's trip to the host. Its barriers pair one
-// to one with em_ring_kernel's.
+// The done wave (threads kRingBlock.. of a worker workgroup): per run of
+// tickets, after the first barrier it takes the run's first ticket and
+// length, after the second (every wave's gate stores complete) its lanes
+// 0..k-1 write the k done words (adjacent words: one or two lines) -- and
+// never wait for those stores, so no claim or frame load of the next run
+// waits behind the writes' trip to the host. Its barriers pair one to one
+// with em_ring_kernel's.
 __device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldone,
-                                            const uint64_t *sh_w, const uint64_t *sh_t,
-                                            const uint32_t *sh_go, uint32_t lane) {
+                                            const uint64_t *sh_t, const uint32_t *sh_k,
+                                            const uint32_t *sh_rel, uint32_t lane) {
   (void)lane;
+  const uint32_t wl = threadIdx.x & 63;
   for (;;) {
-    ring_barrier();  // B1: the ticket is in sh_*
-    if (!*sh_go) return;
-    const uint64_t t = *sh_t;
-    const bool release = (sh_w[3] & kRingRelease) != 0;
-    ring_barrier();  // B2: the gates are stored (sh_* free for the next ticket)
-    if ((threadIdx.x & 63) == 0) {
+    ring_barrier();  // B1: the run is in sh_*
+    const uint32_t k = *sh_k;
+    if (!k) return;
+    const uint64_t t = *sh_t + wl;
+    const bool release = *sh_rel != 0;
+    ring_barrier();  // B2: the gates are stored (sh_* free for the next run)
 #ifdef BG_AB
-      uint64_t *tr = a.trace && t < a.trace_n ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5
-                                              : nullptr;
-      if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
+    uint64_t *tr = a.trace && wl < k && t < a.trace_n
+                       ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5 : nullptr;
+    if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
 #endif
-      // every wave's gate stores (system-scope write-through stores,
-      // completed by each wave's vmcnt(0) before B2) reach the host before
-      // the done word; with kRingRelease the done store is a system-scope
-      // release as well (L2 written back first)
-      if (release)
-        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      else
-        __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    // every wave's gate stores (system-scope write-through stores,
+    // completed by each wave's vmcnt(0) before B2) reach the host before
+    // the done words; with kRingRelease the L2 is written back first
+    // (one system-scope release fence for the run)
+    if (release) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (wl < k)
+      __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef BG_AB
-      if (tr) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        tr[4] = __builtin_amdgcn_s_memrealtime();
-      }
-#endif
+    if (tr) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tr[4] = __builtin_amdgcn_s_memrealtime();
     }
+#endif
   }
 }
 
-// Workgroup b >= 1 serves submission lane (b - 1) % nlanes: it claims the
-// lane's next ticket (one atomic; claims run ahead of publication, so the
-// lane's workgroups queue up on its coming tickets), waits until it is
-// published, reads the descriptor (every word tagged with the ticket),
-// acquires (no line of an earlier batch survives in L1, or in L2 for
-// non-coherently cached memory: kRingSysAcquire), classifies the batch,
-// writes the gates through to memory (sc0 sc1 stores) and marks the ticket
-// done in host memory after them (kRingRelease: as a system-scope release).
+// Workgroup b >= 1 serves submission lane (b - 1) % nlanes. Its first wave
+// claims a range of the lane's next tickets (one atomic; claims run ahead of
+// publication, so the lane's workgroups queue up on its coming tickets),
+// waits until the range's next ticket is published and takes every ticket
+// of the range published by then as one run (<= kRingRunMax tickets: a
+// 32-packet batch alone would leave 7/8 of the workgroup's lanes idle),
+// reads the run's descriptors (one per lane, every word tagged with its
+// ticket), acquires (no line of an earlier batch survives in L1, or in L2
+// for non-coherently cached memory: kRingSysAcquire), and the workgroup
+// classifies the run's packets, writes the gates through to memory (sc0 sc1
+// stores) and marks the tickets done in host memory after them
+// (kRingRelease: behind a system-scope release). The range length adapts to
+// the batch size the lane sees: about kRingRunPackets packets per claim.
 // Create a ring with as many lanes as workers submit on.
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingThreads) __attribute__((amdgpu_num_sgpr(80)))
 void em_ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ uint64_t sh_w[4];
+  __shared__ uint64_t sh_w[kRingRunMax][4];
+  __shared__ uint32_t sh_pre[kRingRunMax + 1];  // the run's packet prefix sums
   __shared__ uint64_t sh_t;
-  __shared__ uint32_t sh_go;
+  __shared__ uint32_t sh_k, sh_rel;
   if (blockIdx.x == 0) {
     if (threadIdx.x < 64) ring_dispatch(a);
     return;
@@ -540,94 +541,150 @@ void em_ring_kernel(RingArgs a) {
   uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   copy_table_to_lds(lds, a.t);  // (ends with a barrier)
   if (threadIdx.x >= kRingBlock) {  // wave-uniform
-    ring_done_wave(a, ldone, sh_w, &sh_t, &sh_go, lane);
+    ring_done_wave(a, ldone, &sh_t, &sh_k, &sh_rel, lane);
     return;
   }
   const uint64_t mask48 = (1ull << 48) - 1;
   constexpr int kPpl = 4;  // packets per lane per round, loads in flight
-  for (;;) {
-    if (threadIdx.x == 0) {
-      const uint64_t t = atomicAdd(dl, 1ull);
+  const uint32_t wl = threadIdx.x & 63;
+  // wave 0's claim state (uniform): the claimed range [next, end)
+  uint64_t next = 0, end = 0;
+  uint32_t claim = 1;  // tickets per claim
 #ifdef BG_AB
-      uint64_t *tr = a.trace && t < a.trace_n ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5
-                                              : nullptr;
-      if (tr) tr[0] = __builtin_amdgcn_s_memrealtime();
+  uint64_t tclaim = 0;
 #endif
-      uint32_t go = 0;
-      for (;;) {
-        if (ld_agent(dl + 1) > t) {
-          go = 1;
-          break;
-        }
-        // stopping (the dispatcher's mirrors precede its stop word):
-        // published meanwhile?
-        if (__hip_atomic_load(dstop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
-          go = ld_agent(dl + 1) > t ? 1u : 0u;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
+  for (;;) {
+    if (threadIdx.x < 64) {  // wave 0
+      if (next == end) {
+        uint64_t t = 0;
+        if (wl == 0) t = atomicAdd(dl, (unsigned long long)claim);
+        next = __shfl(t, 0);
+        end = next + claim;
+#ifdef BG_AB
+        tclaim = __builtin_amdgcn_s_memrealtime();
+#endif
       }
+      uint64_t p = 0;
+      if (wl == 0) {
+        for (;;) {
+          p = ld_agent(dl + 1);
+          if (p > next) break;
+          // stopping (the dispatcher's mirrors precede its stop word):
+          // published meanwhile?
+          if (__hip_atomic_load(dstop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+            p = ld_agent(dl + 1);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      p = __shfl(p, 0);
+      const uint32_t k = p > next ? (uint32_t)((p < end ? p : end) - next) : 0u;
+      const uint64_t t = next + wl;
       uint64_t w[4] = {0, 0, 0, 0};
 #ifdef BG_AB
-      if (tr) tr[1] = __builtin_amdgcn_s_memrealtime();
+      uint64_t *tr = a.trace && wl < k && t < a.trace_n
+                         ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5 : nullptr;
+      if (tr) {
+        tr[0] = tclaim;
+        tr[1] = __builtin_amdgcn_s_memrealtime();
+      }
 #endif
-      if (go) {
+      if (wl < k) {
         const uint64_t tag = (t + 1) & 0xFFFF;
         const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
-        // acquire: the batch's frames were written (by the host or a copy)
-        // before the descriptor was published, and this grid outlives many
-        // batches, so lines of an earlier batch in the same buffer may
-        // still sit in this CU's L1 (and, for memory the device caches
-        // non-coherently, in the XCD's L2): invalidate them before any wave
-        // reads the frames (after the barrier below)
-        if (w[3] & kRingSysAcquire)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        else
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
+      // acquire: the batches' frames were written (by the host or a copy)
+      // before their descriptors were published, and this grid outlives
+      // many batches, so lines of an earlier batch in the same buffer may
+      // still sit in this CU's L1 (and, for memory the device caches
+      // non-coherently, in the XCD's L2): invalidate them before any wave
+      // reads the frames (after the barrier below)
+      if (__ballot(wl < k && (w[3] & kRingSysAcquire)))
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      else if (k)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #ifdef BG_AB
       if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
 #endif
+      // the run's packet prefix sums (inclusive scan over the wave)
+      uint32_t c = wl < k ? (uint32_t)w[2] : 0u;
 #pragma unroll
-      for (int i = 0; i < 4; i++) sh_w[i] = w[i];
-      sh_t = t;
-      sh_go = go;
+      for (int o = 1; o < kRingRunMax; o <<= 1) {
+        const uint32_t v = __shfl_up(c, o);
+        if (wl >= (uint32_t)o) c += v;
+      }
+      if (wl < k) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) sh_w[wl][i] = w[i];
+        sh_pre[wl + 1] = c;
+      }
+      const uint32_t total = __shfl(c, (int)(k ? k - 1 : 0));
+      const bool rel = __ballot(wl < k && (w[3] & kRingRelease)) != 0;
+      if (wl == 0) {
+        sh_pre[0] = 0;
+        sh_t = next;
+        sh_k = k;
+        sh_rel = rel ? 1u : 0u;
+      }
+      next += k;
+      // the next claim: about kRingRunPackets packets of this lane's batches
+      if (k && next == end) {
+        const uint32_t per = max(total / k, 1u);
+        claim = min(max(kRingRunPackets / per, 1u), (uint32_t)kRingRunMax);
+      }
     }
     // B1 (ring_barrier): the frames' freshness for every wave is the
     // system-scope acquire above (its invalidations are the CU's L1 and the
     // XCD's L2)
     ring_barrier();
-    if (!sh_go) return;
-    const uint8_t *frames = reinterpret_cast<const uint8_t *>(sh_w[0] & mask48);
-    uint16_t *gates = reinterpret_cast<uint16_t *>(sh_w[1] & mask48);
-    const uint32_t n = (uint32_t)sh_w[2];
-    const uint64_t stride = (sh_w[2] >> 32) & 0xFFFF;
-    const uint32_t dflt = (uint32_t)(sh_w[3] & 0xFFFF);
-    for (uint32_t base = threadIdx.x; base < n; base += kRingBlock * kPpl) {
+    const uint32_t k = sh_k;
+    if (!k) return;
+    const uint32_t total = sh_pre[k];
+    for (uint32_t base = threadIdx.x; base < total; base += kRingBlock * kPpl) {
       // kPpl packets per lane, their header windows loaded before any key
       // is built; one named window array per packet (a 2-D array indexed
       // by the plan's runtime dword index would live in scratch)
-      uint64_t k0[KW], k1[KW], k2[KW], k3[KW];
-      ring_keys<KW, NCH>(frames, stride, n, base, a.fp, k0, k1, k2, k3);
-      const uint64_t *kk[kPpl] = {k0, k1, k2, k3};
+      const uint8_t *f[kPpl];
+      uint16_t *g[kPpl];
+      uint32_t dflt[kPpl];
 #pragma unroll
       for (int j = 0; j < kPpl; j++) {
         const uint32_t i = base + j * kRingBlock;
-        uint64_t k[KW];
+        uint32_t q = 0;  // the run's ticket holding packet i
+        if (k > 1) {
 #pragma unroll
-        for (int q = 0; q < KW; q++) k[q] = kk[j][q];
-        const uint32_t g = a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, k, dflt)
-                                                : em_lookup<KW>(a.t.base, a.t, k, dflt);
+          for (uint32_t st = kRingRunMax / 2; st; st >>= 1)
+            if (q + st < k && sh_pre[q + st] <= i) q += st;
+        }
+        const uint32_t x = i - sh_pre[q];
+        const uint64_t w2 = sh_w[q][2];
+        const bool in = i < total;
+        f[j] = in ? reinterpret_cast<const uint8_t *>(sh_w[q][0] & mask48) +
+                        (uint64_t)x * ((w2 >> 32) & 0xFFFF)
+                  : nullptr;
+        g[j] = reinterpret_cast<uint16_t *>(sh_w[q][1] & mask48) + x;
+        dflt[j] = (uint32_t)(sh_w[q][3] & 0xFFFF);
+      }
+      uint64_t k0[KW], k1[KW], k2[KW], k3[KW];
+      ring_keys<KW, NCH>(f, a.fp, k0, k1, k2, k3);
+      const uint64_t *kk[kPpl] = {k0, k1, k2, k3};
+#pragma unroll
+      for (int j = 0; j < kPpl; j++) {
+        uint64_t key[KW];
+#pragma unroll
+        for (int q = 0; q < KW; q++) key[q] = kk[j][q];
+        const uint32_t gt = a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, key, dflt[j])
+                                                 : em_lookup<KW>(a.t.base, a.t, key, dflt[j]);
         // written through to memory (sc0 sc1): seen by any reader once
         // this wave's stores have drained
-        if (i < n)
-          __hip_atomic_store(gates + i, (uint16_t)g, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+        if (f[j])
+          __hip_atomic_store(g[j], (uint16_t)gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gates complete
-    ring_barrier();  // B2 (then sh_* may be rewritten for the next ticket)
+    ring_barrier();  // B2 (then sh_* may be rewritten for the next run)
   }
 }
 

@@ -245,9 +245,11 @@ class Ring:
                                 stride, n, burst, default_gate,
                                 C.c_void_p(gates.data_ptr() + 2 * offset)))
 
-    def run_lanes(self, frames, stride, n, burst, default_gate, gates, threads):
+    def run_lanes(self, frames, stride, n, burst, default_gate, gates, threads, reps=1):
         """`threads` submitters at once (threads <= lanes), thread i on lane
-        i over packets [i*n/threads, (i+1)*n/threads); -> wall seconds"""
+        i over packets [i*n/threads, (i+1)*n/threads), `reps` times in a
+        row (so that starting the threads is not what gets timed); -> wall
+        seconds per rep"""
         import threading
         import time
         errs = []
@@ -255,8 +257,9 @@ class Ring:
         def work(i):
             lo, hi = n * i // threads, n * (i + 1) // threads
             try:
-                self.run(frames, stride, hi - lo, burst, default_gate, gates, lane=i,
-                         offset=lo)
+                for _ in range(reps):
+                    self.run(frames, stride, hi - lo, burst, default_gate, gates, lane=i,
+                             offset=lo)
             except Exception as e:  # reported below
                 errs.append(e)
         ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
@@ -268,7 +271,7 @@ class Ring:
         dt = time.perf_counter() - t0
         if errs:
             raise errs[0]
-        return dt
+        return dt / reps
 
     def set_coherence(self, frames, done):
         """bg_ring_set_coherence: frames 0 for device memory written by

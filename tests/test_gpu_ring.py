@@ -121,3 +121,45 @@ def test_ring_submission_lanes_vs_oracle(lanes, threads, host_desc, monkeypatch)
         ring.wait(tk, lane=lane)
         assert ring.completed(lane=lane) == tk + 1
     ring.close()
+
+
+def test_ring_mixed_runs_vs_oracle():
+    """a workgroup takes the published tickets of its claimed range as one
+    run (em_ring_kernel): consecutive tickets of ragged sizes (0 to 300
+    packets) alternating between two slabs with different strides, default
+    gates and gate arrays -- every gate as the oracle's, nothing written
+    past a ticket's packets"""
+    n = 1 << 16
+    keys, gates, frames = P.em_workload(1000, n, seed=21, pkt_seed=22)
+    want_a = oracle_gates(keys, gates, frames, default_gate=8192)
+    want_b = oracle_gates(keys, gates, frames, default_gate=77)
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    f128 = np.zeros((n, 128), np.uint8)
+    f128[:, :64] = frames.reshape(n, 64)
+    da = torch.from_numpy(frames.reshape(-1)).cuda()
+    db = torch.from_numpy(f128.reshape(-1)).cuda()
+    ga = torch.full((n + 64,), -1, dtype=torch.int16, device="cuda")
+    gb = torch.full((n + 64,), -1, dtype=torch.int16, device="cuda")
+    rng = np.random.default_rng(23)
+    ring = F.Ring(t, slots=1024)
+    ca = cb = 0
+    last = None
+    while True:
+        m = int(rng.integers(0, 301)) if rng.random() > 0.1 else 0
+        if rng.random() < 0.5:
+            m = min(m, n - ca)
+            last = ring.submit(da, 64, m, 8192, ga, offset=ca)
+            ca += m
+        else:
+            m = min(m, n - cb)
+            last = ring.submit(db, 128, m, 77, gb, offset=cb)
+            cb += m
+        if ca == n and cb == n:
+            break
+    ring.wait(last)
+    got_a = ga.cpu().numpy().view(np.uint16)
+    got_b = gb.cpu().numpy().view(np.uint16)
+    assert (got_a[:n] == want_a).all() and (got_b[:n] == want_b).all()
+    assert (got_a[n:] == 0xFFFF).all() and (got_b[n:] == 0xFFFF).all()
+    ring.close()
