@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <functional>
 #include <map>
@@ -73,12 +74,6 @@ struct task_result {
 };
 
 namespace bess {
-
-// packets handed back to the pool (Packet::Free), counted by the shell
-inline std::atomic<uint64_t> &freed_packets() {
-  static std::atomic<uint64_t> n{0};
-  return n;
-}
 
 class PacketPool;
 
@@ -125,7 +120,9 @@ class Packet {
 
 // core/packet_pool.h: a fixed set of snbufs (mempool objects of SNBUF_SIZE +
 // 64 bytes, the frame at +512), handed out and taken back by every worker;
-// each thread keeps a cache of up to 512 (rte_mempool's per-lcore cache)
+// each thread keeps a cache of up to 512 (rte_mempool's per-lcore cache) and
+// trades whole magazines of 256 with the shared list, so the lock is held for
+// a pointer move, not while 256 pointers another core wrote are copied
 class PacketPool {
  public:
   static const size_t kObj = SNBUF_SIZE + 64;
@@ -137,11 +134,16 @@ class PacketPool {
   explicit PacketPool(size_t capacity) : capacity_(capacity) {
     mem_ = static_cast<uint8_t *>(aligned_alloc(64, capacity * kObj));
     memset(mem_, 0, capacity * kObj);
-    free_.reserve(capacity);
+    std::vector<Packet *> m;
     for (size_t i = capacity; i-- > 0;) {
       Packet *p = new (mem_ + i * kObj) Packet();
       p->set_pool(this);
-      free_.push_back(p);
+      m.push_back(p);
+      if (m.size() == kMag || i == 0) {
+        avail_ += m.size();
+        mags_.push_back(std::move(m));
+        m.clear();
+      }
     }
     gen_ = ++generation();
   }
@@ -152,18 +154,21 @@ class PacketPool {
   size_t Capacity() const { return capacity_; }
   size_t Size() const {  // available: the shared list (thread caches not counted)
     std::lock_guard<std::mutex> lk(mu_);
-    return free_.size();
+    return avail_;
   }
   // all or nothing (packet_pool.h:56-58)
   bool AllocBulk(Packet **pkts, size_t count, size_t len = 0) {
     Cache &c = cache();
-    if (c.v.size() < count) {
-      std::lock_guard<std::mutex> lk(mu_);
-      size_t want = std::min(free_.size(), kCache / 2 + count - c.v.size());
-      for (size_t i = 0; i < want; i++) {
-        c.v.push_back(free_.back());
-        free_.pop_back();
+    while (c.v.size() < count) {
+      std::vector<Packet *> m;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (mags_.empty()) break;
+        m = std::move(mags_.back());
+        mags_.pop_back();
+        avail_ -= m.size();
       }
+      c.v.insert(c.v.end(), m.begin(), m.end());
     }
     if (c.v.size() < count) return false;
     for (size_t i = 0; i < count; i++) {
@@ -178,7 +183,7 @@ class PacketPool {
   void Put(Packet *p) {
     Cache &c = cache();
     c.v.push_back(p);
-    if (c.v.size() >= kCache) Spill(c, kCache / 2);
+    if (c.v.size() >= kCache) Spill(c, kMag);
   }
   // a worker thread's cache back into the shared list (thread exit)
   void FlushThreadCache() {
@@ -188,6 +193,7 @@ class PacketPool {
 
  private:
   static const size_t kCache = 512;
+  static const size_t kMag = 256;
   struct Cache {
     uint64_t gen = 0;
     PacketPool *owner = nullptr;
@@ -210,21 +216,23 @@ class PacketPool {
     return c;
   }
   void Spill(Cache &c, size_t n) {
+    n = std::min(n, c.v.size());
+    if (!n) return;
+    std::vector<Packet *> m(c.v.end() - (std::ptrdiff_t)n, c.v.end());
+    c.v.resize(c.v.size() - n);
     std::lock_guard<std::mutex> lk(mu_);
-    for (size_t i = 0; i < n && !c.v.empty(); i++) {
-      free_.push_back(c.v.back());
-      c.v.pop_back();
-    }
+    avail_ += m.size();
+    mags_.push_back(std::move(m));
   }
   size_t capacity_;
   uint8_t *mem_ = nullptr;
   uint64_t gen_ = 0;
   mutable std::mutex mu_;
-  std::vector<Packet *> free_;
+  std::vector<std::vector<Packet *>> mags_;  // magazines of <= kMag
+  size_t avail_ = 0;
 };
 
 inline void Packet::Free(Packet *p) {
-  freed_packets()++;
   if (p->pool_) p->pool_->Put(p);
 }
 

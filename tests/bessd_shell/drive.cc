@@ -194,6 +194,10 @@ static int run() {
   std::vector<uint8_t *> bufs;
   std::vector<char> fdata;  // the frames file (pool mode: the Sources' frames)
   size_t fstride = 0;
+  // each frame's length (Ethernet + the IPv4 total length, within the
+  // slot): what pool mode's Source copies per packet, as the reference's
+  // Source copies its pkt_size-byte template
+  std::vector<uint16_t> flen;
   bess::PacketPool *ppool = nullptr;
   std::string line;
   while (std::getline(std::cin, line)) {
@@ -239,6 +243,14 @@ static int run() {
       fdata.assign(n * stride, 0);
       f.read(fdata.data(), (std::streamsize)(n * stride));
       fstride = stride;
+      flen.assign(n, (uint16_t)std::min<size_t>(stride, 0xFFFF));
+      for (size_t i = 0; i < n; i++) {
+        const uint8_t *fr = reinterpret_cast<const uint8_t *>(fdata.data() + i * stride);
+        if (stride >= 18 && fr[12] == 0x08 && fr[13] == 0x00) {
+          const size_t l = 14 + ((size_t)fr[16] << 8 | fr[17]);
+          flen[i] = (uint16_t)std::max<size_t>(60, std::min(l, stride));
+        }
+      }
       free(pool);
       bufs.clear();
       pool = static_cast<uint8_t *>(aligned_alloc(64, n * kObj));
@@ -389,8 +401,10 @@ static int run() {
                 std::this_thread::yield();
               }
               for (size_t j = 0; j < cnt; j++) {
-                memcpy(pk[j]->head_data<uint8_t *>(), fdata.data() + (b0 + j) * fstride,
-                       fstride);
+                const uint16_t fl = flen[b0 + j];
+                memcpy(pk[j]->head_data<uint8_t *>(), fdata.data() + (b0 + j) * fstride, fl);
+                pk[j]->set_total_len(fl);
+                pk[j]->set_data_len(fl);
                 pk[j]->set_pool_index((uint32_t)(b0 + j));
                 batch.add(pk[j]);
               }
