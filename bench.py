@@ -78,6 +78,8 @@ def parse():
                     help="NAT: skip the new-flow batch stream (PMC passes)")
     ap.add_argument("--lib", default="",
                     help="time another build of libbessgpu.so (same-box A/B)")
+    ap.add_argument("--drive", default="",
+                    help="another build of tests/bessd_shell's driver (same-box A/B)")
     ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|rewrite|pipe|plugin|sweep (profiling runs)")
     return ap.parse_args()
 
@@ -671,7 +673,7 @@ def run_plugin_pipeline(args):
     from bess_amd import packets as P
     from bess_amd import pb
     from oracle import oracle as O
-    drive = os.path.join(ROOT, "tests", "bessd_shell", "build", "drive")
+    drive = args.drive or os.path.join(ROOT, "tests", "bessd_shell", "build", "drive")
     if not os.path.exists(drive):
         return "skipped: %s not built" % drive
     n = 1 << 18
@@ -760,7 +762,7 @@ def run_plugin_pool(args):
     from bess_amd import packets as P
     from bess_amd import pb
     from oracle import oracle as O
-    drive = os.path.join(ROOT, "tests", "bessd_shell", "build", "drive")
+    drive = args.drive or os.path.join(ROOT, "tests", "bessd_shell", "build", "drive")
     if not os.path.exists(drive):
         return "skipped: %s not built" % drive
     n = 1 << 17
@@ -786,6 +788,13 @@ def run_plugin_pool(args):
                 script += ["connect %d" % g for g in range(64)]
                 want = ow.process(frames, 2048, n)
                 exp = [str(int(w)) if int(w) < 64 else "D" for w in want]
+                # the CPU baseline in the same harness: the restated
+                # reference WildcardMatch::ProcessBatch on the same workers
+                wpaths = [os.path.join(td, x) for x in ("k", "m", "p", "g")]
+                for arr, pth, dt in zip((rk, rm, prio, wg), wpaths,
+                                        (np.uint8, np.uint8, np.int32, np.uint16)):
+                    np.ascontiguousarray(arr, dtype=dt).tofile(pth)
+                script.append("cpu_wm %s %s %s %s %d" % (*wpaths, nr))
             else:
                 # UDP only: the reference's L4Checksum never emits (nor
                 # frees) a TCP packet in calculate mode (P8), so a TCP share
@@ -803,6 +812,8 @@ def run_plugin_pool(args):
             reps = 40 if name == "WildcardMatch" else 20
             script += ["frames %s 2048 %d" % (path, n), "pool 262144",
                        "pipeline 16 1 0 0 0", "pipeline 16 %d 0 0 0" % reps]
+            if name == "WildcardMatch":
+                script += ["pipeline_cpu 16 1", "pipeline_cpu 16 %d" % reps]
             r = subprocess.run([drive, "run"], input="\n".join(script) + "\n",
                                capture_output=True, text=True, timeout=600)
             lines = r.stdout.splitlines()
@@ -819,6 +830,13 @@ def run_plugin_pool(args):
                          "source_waits": int(pools[-1][3])}
             if name == "WildcardMatch":
                 out[name]["rules"] = nr
+                if len(stats) >= 4 and len(outs) >= 4:
+                    out[name]["cpu_same_harness"] = {
+                        "what": "the same pool, Sources and Sinks with the restated "
+                                "reference WildcardMatch::ProcessBatch (oracle tuple-"
+                                "space search) in place of the plugin",
+                        "Mpps": round(float(stats[3].split()[1]), 1),
+                        "parity": outs[3].split()[1:] == exp}
     return out
 
 

@@ -361,9 +361,14 @@ class GpuModule : public Module {
   bg_pipe *OpenLane(int wid) {
     const int nd = bg_device_count();
     bg_pipe *p = nullptr;
-    const size_t batch =
-        std::min(pipe_batch_, std::max<size_t>(32, PipeBudget() / (size_t)pipe_depth_));
-    if (nd <= 0 || bg_pipe_create(m_, wid % nd, batch, pipe_depth_, 0, &p) < 0)
+    // within the budget, full-size slots first (each slot costs a submit or
+    // a launch), then as many in flight as fit, at least two
+    const size_t budget = PipeBudget();
+    int depth = pipe_depth_;
+    if (budget / (size_t)depth < pipe_batch_)
+      depth = (int)std::max<size_t>(2, std::min<size_t>((size_t)depth, budget / pipe_batch_));
+    const size_t batch = std::min(pipe_batch_, std::max<size_t>(32, budget / (size_t)depth));
+    if (nd <= 0 || bg_pipe_create(m_, wid % nd, batch, depth, 0, &p) < 0)
       return nullptr;
     int lo = 0, hi = 0;
     size_t stride = 0;

@@ -47,6 +47,8 @@
 //                                 oracle's restatement of ExactMatch (5-tuple
 //                                 fields), n rules (keys `stride` bytes
 //                                 apart in gather_key layout, u16 gates)
+//     cpu_wm <keys> <masks> <prios> <gates> <n>  the same for WildcardMatch
+//                                 (16-byte keys and masks, i32 priorities)
 //     pipeline_cpu <workers> <reps>  the same Source -> Sink loop with the
 //                                 restated reference ProcessBatch on the CPU
 //                                 in the middle (head_data() per packet,
@@ -191,6 +193,7 @@ static int run() {
   const ModuleClass *cls = nullptr;
   uint8_t *pool = nullptr;
   or_em *cpu_em = nullptr;
+  or_wm *cpu_wm = nullptr;
   std::vector<uint8_t *> bufs;
   std::vector<char> fdata;  // the frames file (pool mode: the Sources' frames)
   size_t fstride = 0;
@@ -331,18 +334,47 @@ static int run() {
       fk.read(reinterpret_cast<char *>(keys.data()), (std::streamsize)keys.size());
       fg.read(reinterpret_cast<char *>(gates.data()), (std::streamsize)(nr * 2));
       if (cpu_em) or_em_free(cpu_em);
+  if (cpu_wm) or_wm_free(cpu_wm);
       cpu_em = or_em_new();
       const int fo[5] = {23, 26, 30, 34, 36}, fs[5] = {1, 4, 4, 2, 2};
       for (int i = 0; i < 5; i++) or_em_add_field(cpu_em, fo[i], fs[i], 0, i, nullptr, 0);
       printf("cpu_em %d\n", or_em_add_rules(cpu_em, keys.data(), nr, ks, gates.data()));
+    } else if (op == "cpu_wm") {
+      // keys / masks: n x 16 bytes (the 13-byte 5-tuple key, zero padded),
+      // priorities n x int32, gates n x u16
+      std::string kp, mp, pp, gp;
+      size_t nr;
+      in >> kp >> mp >> pp >> gp >> nr;
+      std::vector<uint8_t> keys(nr * 16), masks(nr * 16);
+      std::vector<int32_t> prio(nr);
+      std::vector<uint16_t> gates(nr);
+      std::ifstream fk(kp, std::ios::binary), fm(mp, std::ios::binary),
+          fp(pp, std::ios::binary), fg(gp, std::ios::binary);
+      fk.read(reinterpret_cast<char *>(keys.data()), (std::streamsize)keys.size());
+      fm.read(reinterpret_cast<char *>(masks.data()), (std::streamsize)masks.size());
+      fp.read(reinterpret_cast<char *>(prio.data()), (std::streamsize)(nr * 4));
+      fg.read(reinterpret_cast<char *>(gates.data()), (std::streamsize)(nr * 2));
+      if (cpu_wm) or_wm_free(cpu_wm);
+      cpu_wm = or_wm_new();
+      const int fo[5] = {23, 26, 30, 34, 36}, fs[5] = {1, 4, 4, 2, 2};
+      for (int i = 0; i < 5; i++) or_wm_add_field(cpu_wm, fo[i], fs[i], nullptr, 0);
+      or_wm_init_done(cpu_wm);
+      int rc = 0;
+      for (size_t i = 0; i < nr && !rc; i++) {
+        uint8_t k[OR_KEY_BYTES] = {}, m[OR_KEY_BYTES] = {};
+        memcpy(k, &keys[i * 16], 16);
+        memcpy(m, &masks[i * 16], 16);
+        rc = or_wm_add(cpu_wm, k, m, prio[i], gates[i]);
+      }
+      printf("cpu_wm %d\n", rc);
     } else if (op == "pipeline" || op == "pipeline_cpu") {
       const bool cpu = op == "pipeline_cpu";
       int nw, reps, ig = 0, verify = 0;
       unsigned long long now = 0;
       in >> nw >> reps;
       if (!cpu) in >> ig >> now >> verify;
-      if (cpu && !cpu_em) {
-        printf("rc 22 cpu_em first\n");
+      if (cpu && !cpu_em && !cpu_wm) {
+        printf("rc 22 cpu_em / cpu_wm first\n");
         continue;
       }
       const size_t n = bufs.size();
@@ -414,11 +446,15 @@ static int run() {
             }
             const uint64_t c0 = __rdtsc();
             if (cpu) {  // ExactMatch::ProcessBatch restated (exact_match.cc:224-244)
+                        // or WildcardMatch's (cpu_wm)
               const uint8_t *heads[bess::PacketBatch::kMaxBurst];
               uint16_t g[bess::PacketBatch::kMaxBurst];
               for (int i = 0; i < batch.cnt(); i++)
                 heads[i] = batch.pkts()[i]->head_data<const uint8_t *>();
-              or_em_process_batch(cpu_em, heads, batch.cnt(), DROP_GATE, g);
+              if (cpu_wm)  // WildcardMatch::ProcessBatch (wildcard_match.cc:159-203)
+                or_wm_process_batch(cpu_wm, heads, batch.cnt(), DROP_GATE, g);
+              else
+                or_em_process_batch(cpu_em, heads, batch.cnt(), DROP_GATE, g);
               for (int i = 0; i < batch.cnt(); i++) m->EmitPacket(&ctx, batch.pkts()[i], g[i]);
             } else {
               m->ProcessBatch(&ctx, &batch);
@@ -516,6 +552,7 @@ static int run() {
   bess::PacketPool::default_pool() = nullptr;
   delete ppool;
   if (cpu_em) or_em_free(cpu_em);
+  if (cpu_wm) or_wm_free(cpu_wm);
   return 0;
 }
 
