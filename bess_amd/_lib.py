@@ -160,6 +160,8 @@ _SIGS = {
     "bg_pipe_run": (_int, [_vp, _vp, _vp, _vp, _sz, _sz, _vp]),
     "bg_em_ring_create": (_int, [_vp, _int, _int, _int, _int, C.c_uint32, _int,
                                  C.POINTER(_vp)]),
+    "bg_wm_ring_create": (_int, [_vp, _int, _int, _int, _int, C.c_uint32, _int,
+                                 C.POINTER(_vp)]),
     "bg_ring_destroy": (None, [_vp]),
     "bg_ring_submit": (C.c_int64, [_vp, _int, _vp, _sz, _sz, _u16, _vp]),
     "bg_ring_wait": (_int, [_vp, _int, C.c_int64]),

@@ -1433,6 +1433,41 @@ static int wm_image(bg_wm *wm, int device, hipStream_t s, WmImage **out) {
   return 0;
 }
 
+}  // extern "C"
+
+namespace bg {
+uint64_t wm_version(const bg_wm *wm) { return wm->version.load(std::memory_order_acquire); }
+
+// A WildcardMatch ring's plan (bg::wm_ring_create): the device image's
+// arguments with the key plan of windows staged from win_off, the image's
+// bytes and version, and the bytes of a slot the kernel reads
+int wm_device_plan(bg_wm *wm, int device, hipStream_t s, int win_off, int meta_row,
+                   WmArgs *a, uint64_t *bytes, int *read_end, uint64_t *version) {
+  if (win_off < 0 || win_off > 1024) return fail(EINVAL, "win_off %d", win_off);
+  std::vector<bg_field> df;
+  if (int r = wm_fields_for(wm, win_off, meta_row, &df)) return r;
+  if (int r = check_extent(df, -win_off, 0xFFFF)) return r;
+  WmImage *img;
+  if (int r = wm_image(wm, device, s, &img)) return r;
+  *version = img->version;
+  *a = img->a;
+  a->fp = make_plan(df, false, -win_off);
+  *bytes = img->bytes;
+  const FieldPlan &fp = a->fp;
+  int hi = 0;
+  if (!fp.direct) {
+    hi = fp.nf ? fp.win_lo + 16 * fp.nch : 0;
+  } else {
+    for (int i = 0; i < fp.nf; i++)
+      hi = std::max(hi, (fspec_d(fp.fspec[i]) + fspec_nd(fp.fspec[i])) * 4);
+  }
+  *read_end = hi;
+  return 0;
+}
+}  // namespace bg
+
+extern "C" {
+
 int bg_wm_sync(bg_wm *wm, int device, bg_stream_t stream) {
   WmImage *img;
   return wm_image(wm, device, (hipStream_t)stream, &img);

@@ -112,6 +112,12 @@ int em_meta_window(const bg_em *em, int *lo, int *hi);
 int em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
                    uint32_t idle_us, int win_off, int meta_row, bg_ring **out);
 uint64_t em_version(const bg_em *em);  // bumped by every rule change
+uint64_t wm_version(const bg_wm *wm);
+int wm_device_plan(bg_wm *wm, int device, hipStream_t s, int win_off, int meta_row,
+                   WmArgs *a, uint64_t *bytes, int *read_end, uint64_t *version);
+// a persistent ring over a WildcardMatch table (bg_ring.cc; as em_ring_create)
+int wm_ring_create(bg_wm *wm, int device, int lanes, int slots, int blocks,
+                   uint32_t idle_us, int win_off, int meta_row, bg_ring **out);
 // bg_ring.cc: the rule version a ring classifies with; whether a lane's
 // ticket has finished (one host word, no lock)
 uint64_t ring_version(const bg_ring *r);

@@ -391,6 +391,9 @@ constexpr int kRingDescWords = 8;
 // L1 only). kRingRelease: the done word is a system-scope release (writes
 // L2 back) instead of a relaxed store after every wave's gate stores have
 // completed (the gates are system-scope write-through stores).
+// a WildcardMatch ring's table default gate: "no rule matched" (each
+// ticket's own default gate applies)
+constexpr uint32_t kRingNoGate = 0x10000;
 constexpr uint64_t kRingSysAcquire = 1ull << 16;
 constexpr uint64_t kRingRelease = 1ull << 17;
 constexpr int kRingMaxLanes = 64;  // one dispatcher wave lane each
@@ -419,6 +422,7 @@ hipError_t launch_dnat_scatter(const uint64_t *d_up, size_t k, uint64_t *ent,
                                uint64_t *ts, hipStream_t s);
 // the persistent ring kernel: `blocks` workgroups
 hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s);
+hipError_t launch_wm_ring(const RingArgs &a, const WmArgs &w, int blocks, hipStream_t s);
 // WildcardMatch with the tag words in LDS (t.lds == kLdsTags)
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s);
 // all key fields within two 16-byte chunks, <= 2 byte-permutes per key dword

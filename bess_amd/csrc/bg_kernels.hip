@@ -522,30 +522,28 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldon
 // (kRingRelease: behind a system-scope release). The range length adapts to
 // the batch size the lane sees: about kRingRunPackets packets per claim.
 // Create a ring with as many lanes as workers submit on.
-template <int KW, int NCH>
-__global__ __launch_bounds__(kRingThreads) __attribute__((amdgpu_num_sgpr(80)))
-void em_ring_kernel(RingArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+//
+// The serving loop is shared by the table kinds: `look(key, default_gate)`
+// is the classifier (em_ring_kernel: ExactMatch, wm_ring_kernel:
+// WildcardMatch); the workgroup's table copy in LDS is made before.
+template <int KW, int NCH, int PPL, class Look>
+__device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
+  static_assert(PPL == 1 || PPL == 4, "packets per lane per round: 1 or 4");
   __shared__ uint64_t sh_w[kRingRunMax][4];
   __shared__ uint32_t sh_pre[kRingRunMax + 1];  // the run's packet prefix sums
   __shared__ uint64_t sh_t;
   __shared__ uint32_t sh_k, sh_rel;
-  if (blockIdx.x == 0) {
-    if (threadIdx.x < 64) ring_dispatch(a);
-    return;
-  }
   const uint32_t lane = (blockIdx.x - 1) % a.nlanes;
   unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
   const unsigned long long *dstop = a.dev + (size_t)a.nlanes * kRingLaneWords;
   const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * kRingDescWords;
   uint32_t *ldone = a.done + (size_t)lane * a.nslots;
-  copy_table_to_lds(lds, a.t);  // (ends with a barrier)
   if (threadIdx.x >= kRingBlock) {  // wave-uniform
     ring_done_wave(a, ldone, &sh_t, &sh_k, &sh_rel, lane);
     return;
   }
   const uint64_t mask48 = (1ull << 48) - 1;
-  constexpr int kPpl = 4;  // packets per lane per round, loads in flight
+  constexpr int kPpl = PPL;  // packets per lane per round, loads in flight
   const uint32_t wl = threadIdx.x & 63;
   // wave 0's claim state (uniform): the claimed range [next, end)
   uint64_t next = 0, end = 0;
@@ -668,15 +666,25 @@ void em_ring_kernel(RingArgs a) {
         dflt[j] = (uint32_t)(sh_w[q][3] & 0xFFFF);
       }
       uint64_t k0[KW], k1[KW], k2[KW], k3[KW];
-      ring_keys<KW, NCH>(f, a.fp, k0, k1, k2, k3);
-      const uint64_t *kk[kPpl] = {k0, k1, k2, k3};
+      if constexpr (PPL == 4) {
+        ring_keys<KW, NCH>(f, a.fp, k0, k1, k2, k3);
+      } else if constexpr (NCH > 0) {
+        uint32_t w0[NCH * 4 + 2];
+        ring_key1<KW, NCH>(f[0], a.fp, w0);
+        extract_key<KW, NCH>(w0, a.fp, k0);
+      } else if (f[0]) {
+        direct_key<KW>(f[0], a.fp, k0);
+      } else {
+#pragma unroll
+        for (int q = 0; q < KW; q++) k0[q] = 0;
+      }
+      const uint64_t *kk[4] = {k0, k1, k2, k3};
 #pragma unroll
       for (int j = 0; j < kPpl; j++) {
         uint64_t key[KW];
 #pragma unroll
         for (int q = 0; q < KW; q++) key[q] = kk[j][q];
-        const uint32_t gt = a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, key, dflt[j])
-                                                 : em_lookup<KW>(a.t.base, a.t, key, dflt[j]);
+        const uint32_t gt = look(key, dflt[j]);
         // written through to memory (sc0 sc1): seen by any reader once
         // this wave's stores have drained
         if (f[j])
@@ -686,6 +694,21 @@ void em_ring_kernel(RingArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gates complete
     ring_barrier();  // B2 (then sh_* may be rewritten for the next run)
   }
+}
+
+template <int KW, int NCH>
+__global__ __launch_bounds__(kRingThreads) __attribute__((amdgpu_num_sgpr(80)))
+void em_ring_kernel(RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 64) ring_dispatch(a);
+    return;
+  }
+  copy_table_to_lds(lds, a.t);  // (ends with a barrier)
+  ring_serve<KW, NCH, 4>(a, [&](const uint64_t(&key)[KW], uint32_t dflt) -> uint32_t {
+    return a.t.lds == kLdsTable ? em_lookup<KW>(lds, a.t, key, dflt)
+                                : em_lookup<KW>(a.t.base, a.t, key, dflt);
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -854,6 +877,32 @@ void wm_classify_kernel(WmArgs a) {
   // beats the batched-rounds lookup, which hashes every tuple twice; the
   // next packet's header is prefetched (PPL = 1)
   wm_body<KW, NCH, PPL, 1, 8, true>(a, lds);
+}
+
+// The persistent ring over a WildcardMatch table (bg::wm_ring_create): the
+// ring's own copy of the image, probed in L2/MALL (wm_lookup_seq) or, for a
+// table of <= 40 KB, from LDS; w.default_gate is kRingNoGate, so a miss
+// takes each ticket's own default gate. One packet per lane per round (the
+// lookup's dependent L2 reads are the latency; four packets' lookups inlined
+// in a row spilled). WmArgs is the FIRST argument: the
+// lookup reads the tuple data at the kernarg segment's start (tuple_masks).
+#ifndef BG_WM_RING_PPL
+#define BG_WM_RING_PPL 1
+#endif
+constexpr int kWmRingPpl = BG_WM_RING_PPL;
+template <int KW, int NCH>
+__global__ __launch_bounds__(kRingThreads) __attribute__((amdgpu_num_sgpr(80)))
+void wm_ring_kernel(WmArgs w, RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 64) ring_dispatch(a);
+    return;
+  }
+  copy_table_to_lds(lds, w.t);  // (ends with a barrier)
+  ring_serve<KW, NCH, kWmRingPpl>(a, [&](const uint64_t(&key)[KW], uint32_t dflt) -> uint32_t {
+    const uint32_t g = wm_lookup_any<KW, true, 1, 8>(w, key, lds);
+    return g == kRingNoGate ? dflt : g;
+  });
 }
 
 #ifdef BG_AB
@@ -1611,6 +1660,24 @@ hipError_t launch_em_ring(const RingArgs &a, int blocks, hipStream_t s) {
   BG_RINGS(1) BG_RINGS(2) BG_RINGS(4) BG_RINGS(8)
 #undef BG_RINGS
 #undef BG_RING
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_wm_ring(const RingArgs &a, const WmArgs &w, int blocks, hipStream_t s) {
+  int maxops = 0;
+  for (int q = 0; q < a.fp.nkd; q++) maxops = std::max(maxops, kd_nops_of(a.fp, q));
+  const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 && maxops <= 2 ? 2 : 4);
+  const size_t lds = w.t.lds == kLdsTable ? (w.t.bytes_total + 15) & ~(size_t)15 : 0;
+#define BG_WRING(KW, NCH)                                                    \
+  if (w.t.kw == KW && nch == NCH) {                                          \
+    hipLaunchKernelGGL((wm_ring_kernel<KW, NCH>), dim3((unsigned)blocks),     \
+                       dim3(kRingThreads), lds, s, w, a);                    \
+    return hipGetLastError();                                                \
+  }
+#define BG_WRINGS(KW) BG_WRING(KW, 0) BG_WRING(KW, 2) BG_WRING(KW, 4)
+  BG_WRINGS(1) BG_WRINGS(2) BG_WRINGS(4) BG_WRINGS(8)
+#undef BG_WRINGS
+#undef BG_WRING
   return hipErrorInvalidValue;
 }
 

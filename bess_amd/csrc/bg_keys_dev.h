@@ -38,9 +38,9 @@ __device__ __forceinline__ uint32_t tag_match(uint32_t tags, uint32_t tag) {
 // The WildcardMatch tuple masks (up to 64 words) would otherwise be hoisted
 // into scalar registers for the whole kernel and spilled; laundering the
 // kernarg pointer per packet makes them cheap scalar-cache loads instead.
-// (The WmArgs block is the kernel's only argument, so it starts at the
-// kernarg segment; taking the parameter's address instead would copy the
-// whole block to scratch.)
+// (The WmArgs block is every WildcardMatch kernel's first argument, so it
+// starts at the kernarg segment; taking the parameter's address instead
+// would copy the whole block to scratch.)
 typedef const uint64_t __attribute__((address_space(4))) *kconst_u64;
 __device__ __forceinline__ kconst_u64 tuple_masks(const WmArgs &) {
   const __attribute__((address_space(4))) uint8_t *ka =

@@ -82,6 +82,8 @@ struct bg_ring {
   unsigned long long *d_dev = nullptr;  // per lane: next ticket, published; stop
   uint8_t *d_table = nullptr;  // the ring's own copy of the table image
   RingArgs a{};
+  bool wm = false;  // a WildcardMatch ring: wa is its table's arguments
+  WmArgs wa{};
   std::atomic<uint32_t> launch_id{0};  // of the grid launched last (0: none)
   uint64_t launches = 0;
   std::mutex run_mu;  // (re)launches
@@ -149,7 +151,8 @@ int ensure_running(bg_ring *r) {
                          hipMemcpyHostToDevice, r->st));
   const uint32_t id = r->launch_id.load() + 1;
   r->a.launch_id = id;
-  HIP_TRY(launch_em_ring(r->a, r->blocks, r->st));
+  HIP_TRY(r->wm ? launch_wm_ring(r->a, r->wa, r->blocks, r->st)
+                : launch_em_ring(r->a, r->blocks, r->st));
   HIP_TRY(hipEventRecord(r->ev, r->st));
   r->launch_id.store(id, std::memory_order_release);
   r->launches++;
@@ -264,11 +267,17 @@ int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
                             bg::kSlabMeta, out);
 }
 
+int bg_wm_ring_create(bg_wm *wm, int device, int lanes, int slots, int blocks,
+                      uint32_t idle_us, int win_off, bg_ring **out) {
+  return bg::wm_ring_create(wm, device, lanes, slots, blocks, idle_us, win_off,
+                            bg::kSlabMeta, out);
+}
+
 }  // extern "C"
 
-int bg::em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
-                       uint32_t idle_us, int win_off, int meta_row, bg_ring **out) {
-  if (!em || !out) return fail(EINVAL, "bad arguments");
+// The ring's memory and host state (both table kinds)
+static int ring_alloc(int device, int lanes, int slots, int blocks, uint32_t idle_us,
+                      bg_ring **out) {
   if (lanes < 1 || lanes > kRingMaxLanes)
     return fail(EINVAL, "lanes %d not in [1,%d]", lanes, kRingMaxLanes);
   if (slots < 2 || slots > 32768 || (slots & (slots - 1)))
@@ -344,26 +353,68 @@ int bg::em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
     delete r;
     return fail(EIO, "no device address for the ring's host memory");
   }
-  rc = em_device_plan(em, device, r->st, win_off, meta_row, &a.fp, &a.t, &r->read_end,
-                      &r->version);
-  if (rc == 0) {
-    // The ring classifies with the rule set as of its creation: it keeps
-    // its own copy of the table image, so a later rule change (bessd makes
-    // them with the workers paused) never frees memory the running kernel
-    // reads; a worker re-creates its ring after one.
-    const size_t bytes = (size_t)a.t.part_bytes * a.t.nparts;
-    e = hipMalloc(reinterpret_cast<void **>(&r->d_table), std::max<size_t>(bytes, 256));
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(r->d_table, a.t.base, bytes, hipMemcpyDeviceToDevice, r->st);
-    if (e == hipSuccess) e = hipStreamSynchronize(r->st);
-    if (e != hipSuccess) rc = fail(EIO, "ring table copy: %s", hipGetErrorString(e));
-    a.t.base = r->d_table;
-  }
+  *out = r;
+  return 0;
+}
+
+// The ring classifies with the rule set as of its creation: it keeps its own
+// copy of the table image, so a later rule change (bessd makes them with the
+// workers paused) never frees memory the running kernel reads; a worker
+// re-creates its ring after one.
+static int ring_copy_table(bg_ring *r, const uint8_t *src, size_t bytes) {
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&r->d_table), std::max<size_t>(bytes, 256));
+  if (e == hipSuccess) e = hipMemcpyAsync(r->d_table, src, bytes, hipMemcpyDeviceToDevice, r->st);
+  if (e == hipSuccess) e = hipStreamSynchronize(r->st);
+  if (e != hipSuccess) return fail(EIO, "ring table copy: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int bg::em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
+                       uint32_t idle_us, int win_off, int meta_row, bg_ring **out) {
+  if (!em || !out) return fail(EINVAL, "bad arguments");
+  bg_ring *r = nullptr;
+  if (int rc = ring_alloc(device, lanes, slots, blocks, idle_us, &r)) return rc;
+  RingArgs &a = r->a;
+  int rc = em_device_plan(em, device, r->st, win_off, meta_row, &a.fp, &a.t, &r->read_end,
+                          &r->version);
+  if (rc == 0) rc = ring_copy_table(r, a.t.base, (size_t)a.t.part_bytes * a.t.nparts);
   if (rc) {
     ring_release(r);
     delete r;
     return rc;
   }
+  a.t.base = r->d_table;
+  *out = r;
+  return 0;
+}
+
+int bg::wm_ring_create(bg_wm *wm, int device, int lanes, int slots, int blocks,
+                       uint32_t idle_us, int win_off, int meta_row, bg_ring **out) {
+  if (!wm || !out) return fail(EINVAL, "bad arguments");
+  bg_ring *r = nullptr;
+  if (int rc = ring_alloc(device, lanes, slots, blocks, idle_us, &r)) return rc;
+  WmArgs &w = r->wa;
+  uint64_t bytes = 0;
+  int rc = wm_device_plan(wm, device, r->st, win_off, meta_row, &w, &bytes, &r->read_end,
+                          &r->version);
+  if (rc == 0) rc = ring_copy_table(r, w.t.base, (size_t)bytes);
+  if (rc) {
+    ring_release(r);
+    delete r;
+    return rc;
+  }
+  r->wm = true;
+  w.t.base = r->d_table;
+  // the workgroups' LDS holds a table of <= 40 KB whole; anything larger
+  // (tag words, a key filter) is probed in L2/MALL, leaving the CUs' LDS to
+  // the modules' other kernels
+  if (w.t.lds != kLdsTable) w.t.lds = kLdsNone;
+  w.default_gate = kRingNoGate;
+  w.frames = nullptr;
+  w.gates = nullptr;
+  w.n = 0;
+  r->a.fp = w.fp;  // the serving loop builds the keys
+  r->a.t = w.t;
   *out = r;
   return 0;
 }

@@ -203,15 +203,17 @@ class Comm:
 
 
 class Ring:
-    """bg_ring: one persistent ExactMatch kernel draining batch descriptors
+    """bg_ring: one persistent ExactMatch (or WildcardMatch: bg_wm_ring_create)
+    kernel draining batch descriptors
     from `lanes` submission lanes, one per worker thread (the table as of
     creation, in LDS for the kernel's whole run)."""
 
     def __init__(self, table, device=0, slots=1024, blocks=0, idle_us=200000,
                  lanes=1, win_off=0):
         h = C.c_void_p()
-        check(lib().bg_em_ring_create(table.h, device, lanes, slots, blocks,
-                                      idle_us, win_off, C.byref(h)))
+        create = (lib().bg_wm_ring_create if isinstance(table, WmTable)
+                  else lib().bg_em_ring_create)
+        check(create(table.h, device, lanes, slots, blocks, idle_us, win_off, C.byref(h)))
         self.h = h
         self.table = table
         self.lanes = lanes

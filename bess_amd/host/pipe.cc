@@ -348,6 +348,8 @@ static long take_done(bg_pipe *p, bool wait, void **cookies, uint16_t *gates,
 }
 
 // mapped pinned memory the device reads uncached (see bg_pipe_create)
+constexpr size_t kPipeRingMaxBatch = 8192;  // ring-mode slots (bg_pipe_create)
+
 static hipError_t host_alloc_uc(void **p, size_t bytes) {
   return hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocUncached);
 }
@@ -380,7 +382,9 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
     p->w = StagedStride(p->lo, p->hi, p->mlo, p->mhi);
   }
   p->ctx_use = m->m->CtxUse();
-  if (!p->writeback) {
+  // a ring ticket is served by one workgroup: past a few thousand packets
+  // a launch per slot spreads them over the whole device instead
+  if (!p->writeback && batch <= kPipeRingMaxBatch) {
     uint16_t dflt = 0;
     r = m->m->PipeRingFor(device, &p->ring, &dflt);
     if (r < 0) {

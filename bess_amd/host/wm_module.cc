@@ -5,10 +5,14 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/bessgpu.h"
+#include "../csrc/bg_internal.h"
 #include "module.h"
 
 namespace {
@@ -33,7 +37,10 @@ class WildcardMatch final : public Module {
   static const gate_idx_t kNumOGates = MAX_GATES;
   static const Commands kCmds;
 
-  ~WildcardMatch() override { bg_wm_destroy(table_); }
+  ~WildcardMatch() override {
+    rings_.clear();
+    bg_wm_destroy(table_);
+  }
 
   const Commands &cmds() const override { return kCmds; }
 
@@ -112,6 +119,43 @@ class WildcardMatch final : public Module {
 
   int MetaWindow(int *mlo, int *mhi) const override {
     return bg_wm_meta_window(table_, mlo, mhi);
+  }
+
+  // As ExactMatch's: a pipe's slots go to one persistent classify kernel per
+  // device (bg::wm_ring_create; the table probed in L2, no per-slot H2D /
+  // launch / D2H), re-created after a rule change
+  static const int kPipeRingLanes = 16;
+  int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) override {
+    out->reset();
+    if (bg_get_path_flags() & BG_PATH_PIPE_NO_RING) return 0;
+    int mlo, mhi;
+    if (int rc = MetaWindow(&mlo, &mhi)) return rc;
+    const int meta_row = StagedMetaRow();
+    std::lock_guard<std::mutex> lk(ring_mu_);
+    std::shared_ptr<PipeRing> &cur = rings_[device];
+    if (!cur || cur->version != bg::wm_version(table_) || cur->meta_row != meta_row) {
+      int lo = 0, hi = 0;
+      bg_wm_window(table_, &lo, &hi);
+      bg_ring *r = nullptr;
+      const int rc = bg::wm_ring_create(table_, device, kPipeRingLanes, 64,
+                                        2 * bg::num_cus(device), 10000, lo,
+                                        mlo == mhi ? bg::kSlabMeta : meta_row, &r);
+      if (rc < 0) return rc;
+      // per ticket a system-scope acquire, the done word relaxed (see
+      // ExactMatch::PipeRingFor)
+      (void)bg_ring_set_coherence(r, 1, 0);
+      auto pr = std::make_shared<PipeRing>();
+      pr->r = r;
+      pr->meta_row = meta_row;
+      pr->device = device;
+      pr->lanes = kPipeRingLanes;
+      pr->lane_mu.reset(new std::mutex[kPipeRingLanes]);
+      pr->version = bg::ring_version(r);
+      cur = std::move(pr);
+    }
+    *out = cur;
+    *dflt = default_gate_;
+    return 0;
   }
 
   // the row offset of metadata byte 0 in a staged row (module.h StagedMetaAt)
@@ -290,6 +334,8 @@ class WildcardMatch final : public Module {
   size_t total_key_size_ = 0;
   std::vector<WmField> fields_;
   bg_wm *table_ = nullptr;
+  std::mutex ring_mu_;
+  std::map<int, std::shared_ptr<PipeRing>> rings_;  // per device
 };
 
 // wildcard_match.cc:58-73

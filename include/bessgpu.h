@@ -560,7 +560,10 @@ int bg_module_desc(const bg_module *m, char *buf, size_t len);
  *           ExactMatch/WildcardMatch; the frame for IP/L4Checksum, span
  *           bytes at most, data_len when lens != NULL) into a pinned slot;
  *           a full slot (batch packets) is launched on its own HIP stream:
- *           H2D -> device ProcessBatch -> D2H (gates [+ header lines]).
+ *           H2D -> device ProcessBatch -> D2H (gates [+ header lines]);
+ *           on an ExactMatch / WildcardMatch module a slot of <= 8192
+ *           packets is instead one ticket of the module's persistent ring
+ *           (no HIP call; BG_PATH_PIPE_NO_RING: launches).
  *           Blocks only when all `depth` slots are in flight. ctx: the
  *           ProcessBatch's context (NULL as for bg_module_process; its
  *           device is ignored: the pipe's device is fixed at create). A
@@ -610,8 +613,8 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
                 const uint16_t *lens, size_t n, size_t burst, uint16_t *ogates);
 
 /* ---- Persistent classify kernel: rings of batch descriptors -------------
- * (A pipe on an ExactMatch module submits its slots to such a ring: see
- * bg_pipe_create.) 
+ * (A pipe on an ExactMatch / WildcardMatch module submits its slots to
+ * such a ring: see bg_pipe_create.)
  * BESS hands a module <= 32 packets per ProcessBatch (core/pktbatch.h:70);
  * a kernel launch per batch costs more than the batch. A ring is ONE
  * running ExactMatch kernel that drains batch descriptors the workers write
@@ -636,6 +639,12 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
  * submit makes no HIP call while the kernel runs. */
 typedef struct bg_ring bg_ring;
 int bg_em_ring_create(bg_em *em, int device, int lanes, int slots, int blocks,
+                      uint32_t idle_us, int win_off, bg_ring **out);
+/* The same ring over a WildcardMatch table (WildcardMatch::ProcessBatch,
+ * wildcard_match.cc:159-203, per ticket): the kernel probes its own copy of
+ * the table image in L2 (in LDS when the image is <= 40 KB); a ticket's
+ * default gate applies where no rule matches. */
+int bg_wm_ring_create(bg_wm *wm, int device, int lanes, int slots, int blocks,
                       uint32_t idle_us, int win_off, bg_ring **out);
 void bg_ring_destroy(bg_ring *r); /* stops the kernel and waits for it */
 int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,

@@ -3,13 +3,24 @@
 // argument, forwarding to libbessgpu.so (gpu_module.h).
 #include "gpu_module.h"
 
+// A WildcardMatch ticket takes a ring workgroup ~20 us per 256 packets (its
+// lookups' dependent L2 reads), so 512-packet slots, 8 in flight: the
+// bounded-pool leg measured 512 x 8 against 1024 x 4 and 256 x 8 / x 16 on
+// one box (profiles/r04_wm_plugin_slots.jsonl). (Compile-time: the
+// harness's A/B builds set them.)
+#ifndef BG_WM_PIPE_BATCH
+#define BG_WM_PIPE_BATCH 512
+#define BG_WM_PIPE_DEPTH 8
+#endif
+
 class WildcardMatch final : public GpuModule {
  public:
   static const gate_idx_t kNumOGates = MAX_GATES;  // wildcard_match.h:133
   static const Commands cmds;
 
   CommandResponse Init(const bess::pb::WildcardMatchArg &arg) {
-    return CreateDeferred("WildcardMatch", arg);
+    // served by a persistent ring on each device: small pipe slots
+    return CreateDeferred("WildcardMatch", arg, BG_WM_PIPE_BATCH, BG_WM_PIPE_DEPTH);
   }
   CommandResponse GetInitialArg(const bess::pb::EmptyArg &arg) {
     bess::pb::WildcardMatchArg r;

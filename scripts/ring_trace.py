@@ -5,7 +5,7 @@ T lanes; the kernel stamps each ticket (s_memrealtime, 100 MHz) when a
 workgroup claims it, sees it published, has read its descriptor, has its
 gates stored, and has written its done word. Prints one JSON line per T
 with the medians of each interval and the ticket rate.
-Usage: python scripts/ring_trace.py [T ...]"""
+Usage: python scripts/ring_trace.py [--wm] [--batch=B] [T ...]"""
 import ctypes as C
 import json
 import os
@@ -24,11 +24,26 @@ from bess_amd import packets as P  # noqa: E402
 
 
 def main():
-    ts = [int(x) for x in sys.argv[1:]] or [1, 4, 16]
-    n, B = 1 << 20, 32
-    keys, gates, frames = P.em_workload(1000, n, seed=0x5EED, pkt_seed=77)
-    t = F.EmTable(P.em_fields_5tuple())
-    t.add_many(keys, gates)
+    args = sys.argv[1:]
+    wm = "--wm" in args  # C4's WildcardMatch table (bg_wm_ring_create)
+    args = [a for a in args if a != "--wm"]
+    B = 32
+    for a in list(args):
+        if a.startswith("--batch="):
+            B = int(a.split("=")[1])
+            args.remove(a)
+    ts = [int(x) for x in args] or [1, 4, 16]
+    n = 1 << 20
+    if wm:
+        rk, rm, prio, wg, wf, _ = P.wm_workload(100000, n, stride=2048)
+        t = F.WmTable(P.FIVE_TUPLE)
+        for k, m, p, g in zip(rk, rm, prio, wg):
+            t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+        frames = np.ascontiguousarray(wf[:, :64])
+    else:
+        keys, gates, frames = P.em_workload(1000, n, seed=0x5EED, pkt_seed=77)
+        t = F.EmTable(P.em_fields_5tuple())
+        t.add_many(keys, gates)
     d_frames = torch.from_numpy(frames.reshape(-1)).cuda()
     d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
     L = _lib.lib()
@@ -51,7 +66,7 @@ def main():
         s = st[ok]
         iv = {"claim_to_seen_us": s[:, 1] - s[:, 0], "seen_to_desc_us": s[:, 2] - s[:, 1],
               "desc_to_stored_us": s[:, 3] - s[:, 2], "stored_to_done_us": s[:, 4] - s[:, 3]}
-        out = {"submitters": T, "desc_in_device": dev, "tickets": int(ok.sum()), "batch": B,
+        out = {"table": "wm" if wm else "em", "submitters": T, "desc_in_device": dev, "tickets": int(ok.sum()), "batch": B,
                "Mpps": round(n / dt / 1e6, 1)}
         for k, v in iv.items():
             out[k] = {"p50": round(float(np.median(v)) / 1e3, 2),

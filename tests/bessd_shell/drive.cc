@@ -47,6 +47,8 @@
 //                                 oracle's restatement of ExactMatch (5-tuple
 //                                 fields), n rules (keys `stride` bytes
 //                                 apart in gather_key layout, u16 gates)
+//     sleep <ms>                  pause (after a warm pass: the module's
+//                                 run-time compile finishes untimed)
 //     cpu_wm <keys> <masks> <prios> <gates> <n>  the same for WildcardMatch
 //                                 (16-byte keys and masks, i32 priorities)
 //     pipeline_cpu <workers> <reps>  the same Source -> Sink loop with the
@@ -56,6 +58,8 @@
 //                                 the created module's connected gates) --
 //                                 the cpu_baseline in the same harness
 #include <execinfo.h>
+
+#include <chrono>
 #include <pthread.h>
 #include <signal.h>
 #include <unistd.h>
@@ -234,6 +238,11 @@ static int run() {
       if (!found) printf("rc 95 no such command\n");
     } else if (op == "desc") {
       printf("desc %s\n", m->GetDesc().c_str());
+    } else if (op == "sleep") {  // ms: lets a module's background work
+                                  // (a run-time compile) finish untimed
+      int ms;
+      in >> ms;
+      std::this_thread::sleep_for(std::chrono::milliseconds(ms));
     } else if (op == "connect") {
       int g;
       in >> g;

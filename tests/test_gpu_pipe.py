@@ -236,23 +236,43 @@ def test_em_pipes_share_ring_lanes():
         assert (o == want).all()
 
 
-def test_wm_pipe_vs_oracle():
-    rk, rm, prio, wg, wf, flen = P.wm_workload(2000, 12000, stride=2048)
+@pytest.mark.parametrize("mode", ["ring", "launch"])
+@pytest.mark.parametrize("n_rules,batch,depth", [(2000, 2048, 3), (100000, 1024, 8),
+                                                 (300, 512, 2)])
+def test_wm_pipe_vs_oracle(n_rules, batch, depth, mode):
+    """ring: the slots go to the module's persistent WildcardMatch kernel
+    (its own image copy probed in L2, or in LDS for a small table: 300
+    rules); launch: H2D / kernel / D2H per slot. A rule change and a new
+    default gate between batches are seen by the next slots (a new ring)"""
+    from bess_amd._lib import kernel_paths, BG_PATH_PIPE_NO_RING
+    rk, rm, prio, wg, wf, flen = P.wm_workload(n_rules, 12000, stride=2048)
     m = WildcardMatch(fields=FIELDS)
     ow = O.OracleWildcardMatch(fields=FIELDS)
     cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
-    for k, mk, p, g in zip(rk, rm, prio, wg):
+
+    def add(k, mk, p, g):
         kb, mb = k.tobytes(), mk.tobytes()
         kw = dict(gate=int(g), priority=int(p),
                   values=[{"value_bin": kb[a:c]} for a, c in cut],
                   masks=[{"value_bin": mb[a:c]} for a, c in cut])
         m.add(**kw)
         ow.add(**kw)
-    want = ow.process(wf, 2048, len(wf))
+    half = len(rk) // 2
+    for r in zip(rk[:half], rm[:half], prio[:half], wg[:half]):
+        add(*r)
     _, heads = snbufs(wf)
-    pipe = Pipe(m, batch=2048, depth=3)
-    got = run_pipe(pipe, heads)
-    assert (got == want).all()
+    with kernel_paths(BG_PATH_PIPE_NO_RING if mode == "launch" else 0):
+        pipe = Pipe(m, batch=batch, depth=depth)
+        got = run_pipe(pipe, heads, shuffle_seed=n_rules)
+        assert (got == ow.process(wf, 2048, len(wf))).all()
+        for r in zip(rk[half:], rm[half:], prio[half:], wg[half:]):
+            add(*r)
+        m.set_default_gate(gate=7)
+        ow.set_default_gate(7)
+        got = run_pipe(pipe, heads)
+        want = ow.process(wf, 2048, len(wf))
+        assert (got == want).all() and (want == 7).any()
+        pipe.close()
 
 
 @pytest.mark.parametrize("cls,mode", [(IPChecksum, 1), (L4Checksum, 2)])

@@ -163,3 +163,41 @@ def test_ring_mixed_runs_vs_oracle():
     assert (got_a[:n] == want_a).all() and (got_b[:n] == want_b).all()
     assert (got_a[n:] == 0xFFFF).all() and (got_b[n:] == 0xFFFF).all()
     ring.close()
+
+
+@pytest.mark.parametrize("n_rules", [300, 100000])
+def test_wm_ring_vs_oracle(n_rules):
+    """the ring over a WildcardMatch table (bg_wm_ring_create): its image
+    probed in L2 (100 K rules: tag words, direct tuples) or held in LDS (300
+    rules); batches of 32 / 100 / 4096 and per-ticket default gates, every
+    gate as the oracle's WildcardMatch::ProcessBatch"""
+    n = 1 << 16
+    rk, rm, prio, wg, wf, _ = P.wm_workload(n_rules, n, stride=2048)
+    frames = np.ascontiguousarray(wf[:, :64])
+    fields = [{"offset": o, "num_bytes": s} for o, s in P.FIVE_TUPLE]
+    ow = O.OracleWildcardMatch(fields=fields)
+    t = F.WmTable(P.FIVE_TUPLE)
+    cut = [(0, 1), (1, 5), (5, 9), (9, 11), (11, 13)]
+    for k, m, p, g in zip(rk, rm, prio, wg):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+        kb, mb = k.tobytes(), m.tobytes()
+        ow.add(gate=int(g), priority=int(p), values=[{"value_bin": kb[a:c]} for a, c in cut],
+               masks=[{"value_bin": mb[a:c]} for a, c in cut])
+    want = ow.process(frames, 64, n)  # default gate: DROP_GATE (8192)
+    hit = want != O.DROP_GATE
+    d = torch.from_numpy(frames.reshape(-1)).cuda()
+    ring = F.Ring(t, slots=512)
+    for burst in (32, 100, 4096):
+        dg = torch.full((n,), -1, dtype=torch.int16, device="cuda")
+        ring.run(d, 64, n, burst, 8192, dg)
+        assert (dg.cpu().numpy().view(np.uint16) == want).all(), burst
+    dg = torch.full((n,), -1, dtype=torch.int16, device="cuda")
+    last = None
+    for i, off in enumerate(range(0, n, 1000)):
+        m = min(1000, n - off)
+        last = ring.submit(d, 64, m, 77 if i % 2 else 8192, dg, offset=off)
+    ring.wait(last)
+    got = dg.cpu().numpy().view(np.uint16)
+    dflt = np.where((np.arange(n) // 1000) % 2 == 1, 77, 8192)
+    assert (got == np.where(hit, want, dflt)).all()
+    ring.close()
