@@ -811,7 +811,8 @@ def run_plugin_pool(args):
             # workers' pipes; a pass of 2^17 packets is ~10 ms)
             reps = 40 if name == "WildcardMatch" else 20
             script += ["frames %s 2048 %d" % (path, n), "pool 262144",
-                       "pipeline 16 1 0 0 0", "pipeline 16 %d 0 0 0" % reps]
+                       "pipeline 16 1 0 0 0", "sleep 3000",  # (the run-time compile)
+                       "pipeline 16 %d 0 0 0" % reps]
             if name == "WildcardMatch":
                 script += ["pipeline_cpu 16 1", "pipeline_cpu 16 %d" % reps]
             r = subprocess.run([drive, "run"], input="\n".join(script) + "\n",
