@@ -316,7 +316,7 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
     of B packets is one kernel launch, 512 batches per measurement.
       stream: back-to-back bg_em_classify calls on one stream (host launch
               cost included: what one BESS worker issuing B-packet batches
-              sees);
+              sees; the stream attached with bg_stream_attach);
       graph:  the 512 launches captured in a HIP graph and replayed (no
               host cost; the runtime may overlap independent launches);
       persistent: ONE running kernel (bg_ring) drains the batches as host
@@ -335,6 +335,10 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
     from bess_amd import lib
     classify = lib().bg_em_classify
     fp, gp, sp = d_frames.data_ptr(), d_gates.data_ptr(), C.c_void_p(s.cuda_stream)
+    # the worker's stream attached (bg_stream_attach): a rule change fences it
+    # once, instead of an event recorded per launch; detached below
+    if lib().bg_stream_attach(sp):
+        raise RuntimeError("bg_stream_attach failed")
 
     def launches(B):  # straight C-ABI calls: no per-launch tensor slicing
         for j in range(nl):
@@ -369,6 +373,7 @@ def em_sweep(r, torch, batches=(32, 64, 128, 256, 512, 1024, 2048, 4096)):
         torch.cuda.synchronize()
         ms = timed(g.replay)
         out["graph"][str(B)] = round(nl * B / (ms * 1e-3) / 1e6, 1)
+    lib().bg_stream_detach(sp)
     npk = min(16 << 20, r["n"])  # the C2 slab: enough tickets at any batch size
     launches0 = 0
     for T in (1, 4, 16):  # a ring with one submission lane per submitter

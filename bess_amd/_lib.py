@@ -115,6 +115,8 @@ _SIGS = {
     "bg_wm_jit_source": (_int, [_vp, _int, _vp, _sz, C.POINTER(_sz)]),
     "bg_wm_jit_check": (_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "bg_shutdown": (None, []),
+    "bg_stream_attach": (_int, [_vp]),
+    "bg_stream_detach": (_int, [_vp]),
     "bg_cksum": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp, _vp, _vp]),
     "bg_cksum_process_host": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp,
                                      _vp, _vp]),

@@ -227,3 +227,23 @@ void stream_gone(hipStream_t s) {
 }
 
 }  // namespace bg
+
+extern "C" {
+
+int bg_stream_attach(bg_stream_t stream) {
+  if (!stream) return 0;  // the null stream is always fenced lazily
+  bg::own_stream(reinterpret_cast<hipStream_t>(stream));
+  return 0;
+}
+
+int bg_stream_detach(bg_stream_t stream) {
+  if (!stream) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // its launches done, it drops out of the images' lazily fenced streams
+  const hipError_t e = hipStreamSynchronize(s);
+  bg::stream_gone(s);
+  if (e != hipSuccess) return bg::fail(EIO, "hipStreamSynchronize: %s", hipGetErrorString(e));
+  return 0;
+}
+
+}  // extern "C"

@@ -240,12 +240,21 @@ int bg_wm_jit_source(bg_wm *wm, int device, char *buf, size_t len, size_t *need)
  * kernel on the calling thread; no device needed (0, -ENOENT: no tag-word
  * image, -ENOEXEC: compile failed, log in `log`). */
 int bg_wm_jit_check(bg_wm *wm, char *log, size_t len, size_t *code_bytes);
-/* Before a process exits: stop the background compiler after the compile in
- * progress (at most a few seconds). A process that exits while it compiles
- * may crash in the compiler library's static destructors. Idempotent; later
+/* Before a process exits: stop the background compiler (a compile in
+ * progress in the bg_rtc helper process is killed). Idempotent; later
  * tables keep the ahead-of-time kernels. (bess_amd/_lib.py registers it with
- * Python's atexit.) */
+ * Python's atexit; a C process gets it registered at its first compile.) */
 void bg_shutdown(void);
+
+/* A caller's stream the library may fence lazily. A table image replaced by
+ * a rule change is freed only after every launch that reads it has
+ * finished; on a stream the library does not know, each launch records an
+ * event to prove that (a few microseconds per launch: the HIP runtime
+ * cannot be asked about a stream handle that may have been destroyed). An
+ * attached stream is fenced once, when an image retires, instead. Detach
+ * before destroying the stream: detach synchronizes it. 0 or -errno. */
+int bg_stream_attach(bg_stream_t stream);
+int bg_stream_detach(bg_stream_t stream);
 
 /* ---- IPChecksum / L4Checksum ------------------------------------------ */
 /* mode: BG_CK_IP, BG_CK_L4 or both (= IPChecksum -> L4Checksum pipeline:
