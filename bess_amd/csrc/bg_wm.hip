@@ -32,8 +32,14 @@ hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
 hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   const bool n2 = fits_nch2(a.fp);
   if (a.fp.direct || a.fp.nch > 4 || a.t.nbp > (1u << 15)) return hipErrorInvalidValue;
-  // the pair loads: dense 64 B slots whose window is two chunks inside the slot
-  const bool pair = n2 && a.stride == 64 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64;
+  // the pair loads: a window of two chunks inside the slot's first line,
+  // lanes 2m / 2m+1 loading slot m's two (one 32 B request per slot per
+  // load instead of two 16 B ones): on the dense 64 B slab and, since round
+  // 4, on any stride (C4's 2 KB slots 0.319 -> 0.262 ms, same gates,
+  // profiles/r04_wm_pair_2k_ab.jsonl)
+  // (both chunks inside the slot: no read past a staged row or the slab)
+  const bool pair = n2 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
+                    a.fp.win_lo + 32 <= a.stride && a.stride <= 65536;
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
     return pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                     \

@@ -265,18 +265,19 @@ __device__ __forceinline__ uint64_t pair_slot(int lane) {
 
 __device__ __forceinline__ void load_pair(const uint8_t *__restrict__ frames,
                                           uint64_t n, uint64_t p0, int lane,
-                                          uint32_t win_lo, uint32_t (&r)[8]) {
+                                          uint32_t win_lo, uint32_t stride,
+                                          uint32_t (&r)[8]) {
   const uint64_t s0 = p0 + (lane >> 1), s1 = s0 + 32;
   // a uniform base plus a 32-bit lane offset recomputed here (hoisted out
   // of the tile loop, the per-lane 64-bit addresses were spilled, and the
   // reload's wait retired every load issued before it)
   uint32_t ln = (uint32_t)lane;
   asm volatile("" : "+v"(ln));
-  const uint32_t off = (ln >> 1) * 64 + win_lo + (ln & 1) * 16;
-  const uint8_t *base = frames + p0 * 64;
+  const uint32_t off = (ln >> 1) * stride + win_lo + (ln & 1) * 16;
+  const uint8_t *base = frames + p0 * stride;
   uint4 x = make_uint4(0, 0, 0, 0), y = x;
   if (s0 < n) x = ld_stream(reinterpret_cast<const uint4 *>(base + off));
-  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(base + off + 32 * 64));
+  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(base + off + 32 * stride));
   r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
   r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
 }
@@ -327,7 +328,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
   uint32_t wn[PAIR ? 8 : NCH * 4 + 2];
   if constexpr (PAIR) {
-    if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, wn);
+    if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);
   } else {
     if (t < ntiles && t * 64 + lane < a.n)
       load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
@@ -363,7 +364,8 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
     // every older one -- the direct values, consumed in this tile, must not
     // be younger than the prefetch the next tile consumes
     if constexpr (PAIR) {
-      if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, wn);
+      if (t + nw < ntiles)
+        load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);
     } else {
       const uint64_t nidx = (t + nw) * 64 + lane;
       if (t + nw < ntiles && nidx < a.n)

@@ -119,7 +119,8 @@ def test_random_layouts_compile(seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed,stride,n", [(11, 64, 65536), (12, 64, 65536 + 37),
                                            (13, 128, 40000), (14, 2048, 20000),
-                                           (15, 64, 45), (16, 96, 30001)])
+                                           (15, 64, 45), (16, 96, 30001),
+                                           (17, 32, 5001), (18, 48, 7000)])
 def test_jit_vs_oracle_random_layouts(seed, stride, n):
     torch = pytest.importorskip("torch")
     rng = np.random.default_rng(seed)
