@@ -29,6 +29,7 @@ checksum, C4 wildcard, the §8f modules, batch-size sweeps, host legs) are
 measured at N = 1 only, as extra keys.
 """
 import argparse
+import datetime
 import json
 import os
 import socket
@@ -1543,6 +1544,14 @@ def run_c5(args, dev, torch):
     return out
 
 
+def _agree(ok, dist, torch, dev):
+    """True when the step succeeded on every rank: a rank that failed says
+    so before the others enter a collective it would never join"""
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
 def run_c5_multi(args, rank, world, dev, torch, dist):
     """C5 at N = world GPUs: 1M rules sharded over the ranks (rank r inserts
     only partition r's rules; all-reduce MAX of the partition sizes fixes
@@ -1564,13 +1573,25 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
     t = F.EmTable(P.em_fields_5tuple())
     dist.barrier()
     t0 = time.perf_counter()
-    t.add_many(keys, gates, part=rank, nparts=world)
+    err = None
+    try:
+        t.add_many(keys, gates, part=rank, nparts=world)
+    except Exception as e:
+        err = e
+    if not _agree(err is None, dist, torch, dev):
+        raise RuntimeError("C5 partition insert failed on a rank: %r" % (err,))
     insert_s = time.perf_counter() - t0
     held = len(t)
     comm = F.Comm.over_process_group(rank, world, dev.index, dist)
     dist.barrier()
     t0 = time.perf_counter()
-    t.allgather(comm)
+    try:
+        t.allgather(comm)
+    except Exception as e:
+        err = e
+    if not _agree(err is None, dist, torch, dev):
+        comm.close()
+        raise RuntimeError("C5 all-gather failed on a rank: %r" % (err,))
     st = comm.last_stats()
     st["call_ms"] = (time.perf_counter() - t0) * 1e3
     t.classify(d, 64, n, 8192, dg)
@@ -1746,7 +1767,9 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # a bounded wait: a rank that died must not hold the others forever
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(minutes=5))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     import bess_amd

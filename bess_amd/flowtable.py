@@ -190,8 +190,15 @@ class Comm:
         """one rank of a communicator for `world` processes: rank 0's unique
         id travels over the caller's existing torch.distributed group (128
         control bytes; the table itself never goes through torch)"""
-        uid = [cls.unique_id() if rank == 0 else None]
+        uid = [None]
+        if rank == 0:
+            try:
+                uid[0] = cls.unique_id()
+            except Exception as e:  # every rank learns it (none waits in init)
+                uid[0] = "bg_comm_unique_id failed: %r" % (e,)
         dist.broadcast_object_list(uid, src=0, group=group)
+        if not isinstance(uid[0], (bytes, bytearray)):
+            raise RuntimeError(str(uid[0]))
         return cls.init_rank(uid[0], world, rank, device)
 
     def close(self):
