@@ -226,3 +226,35 @@ def test_exit_while_compiling():
             "t.sync(0)\n" % root)
     r = subprocess.run([sys.executable, "-c", code], timeout=120, capture_output=True)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
+
+
+@pytest.mark.parametrize("helper", ["missing", "fails"])
+def test_compile_without_a_working_helper(tmp_path, helper):
+    """the run-time compile runs in bg_rtc next to the library; with no
+    helper there, or one that dies, the compile fails with its reason and
+    the process carries on (the tables keep the ahead-of-time kernel)"""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    shutil.copy(os.path.join(root, "bess_amd", "libbessgpu.so"), tmp_path / "libbessgpu.so")
+    if helper == "fails":
+        fake = tmp_path / "bg_rtc"
+        fake.write_text("#!/bin/sh\nexec 0<&-\necho dying >&2\nexit 3\n")
+        fake.chmod(0o755)
+    code = ("import sys, errno; sys.path.insert(0, %r)\n"
+            "from bess_amd import _lib\n"
+            "_lib.LIB_PATH = %r\n"
+            "from bess_amd import flowtable as F, packets as P\n"
+            "rk, rm, pr, g, _, _ = P.wm_workload(20000, 64, stride=64, sizes=((60, 1),))\n"
+            "t = F.WmTable(P.FIVE_TUPLE)\n"
+            "[t.add(k.tobytes(), m.tobytes(), int(p), int(x)) for k, m, p, x in zip(rk, rm, pr, g)]\n"
+            "rc, code, log = t.jit_check()\n"
+            "print(rc, code, log.replace(chr(10), ' ')[:300])\n"
+            % (root, str(tmp_path / "libbessgpu.so")))
+    r = subprocess.run([sys.executable, "-c", code], timeout=120, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rc, nbytes, log = r.stdout.split(" ", 2)
+    assert int(rc) == -errno.ENOEXEC and int(nbytes) == 0
+    assert ("not found" in log) if helper == "missing" else ("exit status 3" in log and "dying" in log)
