@@ -54,7 +54,8 @@ class GpuModule : public Module {
  public:
   // the deferred datapath's pipes: packets per device launch, launches in
   // flight per worker, at most. A module served by a persistent ring
-  // (ExactMatch, WildcardMatch) submits small slots at no launch cost (8 x 1024); the
+  // (ExactMatch, WildcardMatch) submits small slots at no launch cost
+  // (8 x 1024; WildcardMatch 8 x 512, wildcard_match_gpu.cc); the
   // others launch H2D/kernel/D2H per slot and amortise that over up to 64 K
   // packets. Either way a worker's pipe holds no more than PipeBudget().
   static const size_t kPipeBatch = 65536;
