@@ -143,6 +143,11 @@ class ExactMatch final : public Module {
   // room for other modules' kernels on the device.
   static const int kPipeRingLanes = 16;
   static const int kPipeRingRelease = 0;  // the done word: see PipeRingFor
+  bool PipeRingCurrent(const PipeRing &ring, uint16_t *dflt) const override {
+    if (ring.version != bg::em_version(table_) || ring.meta_row != StagedMetaRow()) return false;
+    *dflt = default_gate_;
+    return true;
+  }
   int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) override {
     out->reset();
     if (bg_get_path_flags() & BG_PATH_PIPE_NO_RING) return 0;

@@ -251,6 +251,14 @@ class Module {
     out->reset();
     return 0;
   }
+  // Whether `ring` (from PipeRingFor) is still the one PipeRingFor would
+  // return -- same rules, same row layout -- with the current default gate:
+  // the per-slot check without PipeRingFor's lock (workers share it).
+  virtual bool PipeRingCurrent(const PipeRing &ring, uint16_t *dflt) const {
+    (void)ring;
+    (void)dflt;
+    return false;
+  }
   // attr_name fields: metadata area at slot offset meta_off (-1: none, the
   // attribute offsets only -- staged rows carry the metadata bytes),
   // attribute offsets by name (bg_module_bind_meta). Modules without attr

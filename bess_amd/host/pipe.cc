@@ -204,8 +204,12 @@ static int launch_slot(bg_pipe *p) {
     // ring after a rule change: a lane there)
     std::shared_ptr<PipeRing> ring;
     uint16_t dflt = 0;
-    int rc = p->mod->m->PipeRingFor(p->device, &ring, &dflt);
-    if (rc < 0) return rc;
+    if (p->ring && p->mod->m->PipeRingCurrent(*p->ring, &dflt)) {
+      ring = p->ring;  // (no module lock per slot: workers share the module)
+    } else {
+      int rc = p->mod->m->PipeRingFor(p->device, &ring, &dflt);
+      if (rc < 0) return rc;
+    }
     if (!ring) return fail(ENOTSUP, "the module no longer serves pipes through a ring");
     if (ring != p->ring) {
       p->ring = ring;

@@ -125,6 +125,11 @@ class WildcardMatch final : public Module {
   // device (bg::wm_ring_create; the table probed in L2, no per-slot H2D /
   // launch / D2H), re-created after a rule change
   static const int kPipeRingLanes = 16;
+  bool PipeRingCurrent(const PipeRing &ring, uint16_t *dflt) const override {
+    if (ring.version != bg::wm_version(table_) || ring.meta_row != StagedMetaRow()) return false;
+    *dflt = default_gate_;
+    return true;
+  }
   int PipeRingFor(int device, std::shared_ptr<PipeRing> *out, uint16_t *dflt) override {
     out->reset();
     if (bg_get_path_flags() & BG_PATH_PIPE_NO_RING) return 0;
