@@ -122,6 +122,8 @@ int wm_ring_create(bg_wm *wm, int device, int lanes, int slots, int blocks,
 // ticket has finished (one host word, no lock)
 uint64_t ring_version(const bg_ring *r);
 bool ring_done(const bg_ring *r, int lane, int64_t ticket);
+// the ring's grid is running (one host word read; no lock, no HIP call)
+bool ring_live(const bg_ring *r);
 hipStream_t thread_stream(int device, hipStream_t given);
 // bg_comm.cc: an assembled image (d_img, bytes; hipMalloc'ed on `device`,
 // laid out as bg_em_plan*) becomes the device's table image of the current

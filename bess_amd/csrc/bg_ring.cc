@@ -251,6 +251,8 @@ namespace bg {
 
 uint64_t ring_version(const bg_ring *r) { return r->version; }
 
+bool ring_live(const bg_ring *r) { return grid_live(r); }
+
 bool ring_done(const bg_ring *r, int lane, int64_t ticket) {
   const RingLane &l = r->lanes[lane];
   if ((uint64_t)ticket < l.done_upto.load(std::memory_order_acquire)) return true;

@@ -268,6 +268,9 @@ static int retire_oldest(bg_pipe *p, bool wait) {
   if (!s.inflight) return 0;
   if (s.ring) {
     if (!bg::ring_done(s.ring->r, s.lane, s.ticket)) {
+      // not yet, and the grid that will finish it is running: no lane lock
+      // per poll (the lane is shared with the pipe's own submits)
+      if (!wait && bg::ring_live(s.ring->r)) return 0;
       // (through the ring's own check, which relaunches a grid that ended)
       std::lock_guard<std::mutex> lk(s.ring->lane_mu[s.lane]);
       const int64_t c = bg_ring_completed(s.ring->r, s.lane);
