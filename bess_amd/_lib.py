@@ -25,6 +25,7 @@ BG_PATH_ACL_LDS = 64
 BG_PATH_LPM_DIR24 = 128
 BG_PATH_PIPE_NO_RING = 256
 BG_PATH_WM_NO_JIT = 512
+BG_PATH_RING_HOST_DESC = 1024
 KEY_BYTES = 64
 
 

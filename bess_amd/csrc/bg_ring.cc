@@ -15,7 +15,8 @@
 // a worker reads its descriptor from HBM (~1 us) instead of over PCIe (a
 // round trip that queued to 8-23 us per ticket under 16 submitters,
 // profiles/r03_ring_trace.jsonl). Otherwise (no CPU mapping of device
-// memory, or BG_RING_HOST_DESC=1) in pinned host memory, read over PCIe.
+// memory, or the path flag BG_PATH_RING_HOST_DESC) in pinned host memory,
+// read over PCIe.
 //
 // One lane of the grid (the dispatcher) polls the host's published count
 // over PCIe and mirrors it in device memory, where the other workgroups
@@ -192,8 +193,7 @@ T *dev_alias(T *h) {
 // the host (the allocation's addresses are mapped on the CPU side: mincore
 // fails with ENOMEM on an unmapped range); nullptr when it cannot
 uint64_t *host_writable_device_alloc(size_t bytes) {
-  const char *env = getenv("BG_RING_HOST_DESC");
-  if (env && env[0] == '1') return nullptr;
+  if (path_flags() & kPathRingHostDesc) return nullptr;
   void *d = nullptr;
   if (hipExtMallocWithFlags(&d, bytes, hipDeviceMallocUncached) != hipSuccess) return nullptr;
   const size_t pg = (size_t)sysconf(_SC_PAGESIZE);

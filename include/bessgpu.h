@@ -289,6 +289,9 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_PIPE_NO_RING 256 /* pipes launch per slot (not via a ring) */
 #define BG_PATH_WM_NO_JIT 512 /* WildcardMatch: the ahead-of-time kernel, never the
                                 run-time compiled one (bg_wm_jit_wait) */
+#define BG_PATH_RING_HOST_DESC 1024 /* rings created now keep their descriptors in
+                                       pinned host memory (not device memory
+                                       through the BAR) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */
@@ -668,7 +671,7 @@ int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride,
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks);
 /* 1: the descriptors live in device memory the host writes through the
  * PCIe BAR (workers read them from HBM); 0: in pinned host memory (read
- * over PCIe; no CPU mapping of device memory, or BG_RING_HOST_DESC=1). */
+ * over PCIe; no CPU mapping of device memory, or BG_PATH_RING_HOST_DESC). */
 int bg_ring_desc_in_device(const bg_ring *r);
 /* How the kernel meets the memory of later submits (one thread, before or
  * between submits). frames 1 (default): the frames may be memory the

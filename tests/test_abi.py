@@ -32,6 +32,19 @@ def test_library_exports_only_the_c_abi():
     assert set(_lib.declared_symbols()) <= set(names)
 
 
+def test_product_reads_no_environment():
+    """the product library selects no path through the environment (A/B
+    knobs live in the separate measurement build; tests pick kernel paths
+    with bg_set_path_flags): it does not even import getenv"""
+    import os
+    import subprocess
+    so = os.path.join(_lib.HERE, "libbessgpu.so")
+    out = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True,
+                         text=True, check=True).stdout
+    assert not any(ln.split()[-1].startswith(("getenv", "secure_getenv"))
+                   for ln in out.splitlines() if ln.strip())
+
+
 def test_header_is_plain_c():
     import os
     hdr = open(os.path.join(os.path.dirname(_lib.HERE), "include",

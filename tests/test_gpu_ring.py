@@ -88,16 +88,18 @@ def test_ring_idle_exit_relaunch_and_snapshot():
 
 @pytest.mark.parametrize("host_desc", [False, True])
 @pytest.mark.parametrize("lanes,threads", [(4, 4), (16, 16), (16, 3)])
-def test_ring_submission_lanes_vs_oracle(lanes, threads, host_desc, monkeypatch):
+def test_ring_submission_lanes_vs_oracle(lanes, threads, host_desc):
     """several worker threads, each on its own submission lane of one
     running kernel, 32-packet batches (and ragged 100-packet ones): every
     gate as the oracle's; an idle exit in between relaunches for all lanes.
     Both descriptor homes: device memory written by the host (the default
-    where the BAR maps it) and pinned host memory (BG_RING_HOST_DESC=1)"""
-    if host_desc:
-        monkeypatch.setenv("BG_RING_HOST_DESC", "1")
-    else:
-        monkeypatch.delenv("BG_RING_HOST_DESC", raising=False)
+    where the BAR maps it) and pinned host memory (BG_PATH_RING_HOST_DESC)"""
+    from bess_amd._lib import kernel_paths, BG_PATH_RING_HOST_DESC
+    with kernel_paths(BG_PATH_RING_HOST_DESC if host_desc else 0):
+        _ring_submission_lanes(lanes, threads, host_desc)
+
+
+def _ring_submission_lanes(lanes, threads, host_desc):
     n = 1 << 18
     keys, gates, frames = P.em_workload(1000, n, seed=lanes, pkt_seed=9)
     want = oracle_gates(keys, gates, frames)
