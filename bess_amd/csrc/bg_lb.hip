@@ -79,6 +79,48 @@ struct HlbOp {
   }
 };
 
+// fields mode as a header-line op (the fields inside the frame's first 64
+// bytes): the line arrives through the slab kernel's lane-contiguous loads,
+// the key window is cut from it at the plan's (16-byte aligned) start --
+// a uniform branch per possible start, so every register index is a
+// constant -- then MakeKeys and the byte-table CRC as below
+template <int KW, int NCH>
+struct HlbFieldsOp {
+  using Args = HlbArgs;
+  static constexpr bool kWrites = false;
+  static constexpr int c0 = 0, c1 = 4;
+  static size_t lds_bytes(const HlbArgs &x) { return HlbOp<kHlbL4>::lds_bytes(x); }
+  __device__ static void stage(uint32_t *lds, const HlbArgs &x) { hlb_stage_lds(lds, x); }
+  __device__ static uint32_t decide(const HlbArgs &x, const uint32_t *T,
+                                    uint32_t (&d)[16], uint8_t *) {
+    uint32_t w[NCH * 4 + 2];
+    const uint32_t c = (uint32_t)x.fp.win_lo >> 4;  // wave-uniform
+#pragma unroll
+    for (int cc = 0; cc < 4; cc++) {
+      if (c == (uint32_t)cc) {
+#pragma unroll
+        for (int i = 0; i < NCH * 4; i++) w[i] = 4 * cc + i < 16 ? d[4 * cc + i] : 0u;
+      }
+    }
+    w[NCH * 4] = 0;
+    w[NCH * 4 + 1] = 0;
+    uint64_t k[KW];
+    extract_key<KW, NCH>(w, x.fp, k);
+    const uint32_t nw = x.L / 8;
+    uint32_t crc = 0;
+#pragma unroll
+    for (int j = 0; j < KW; j++) {
+      if ((uint32_t)j < nw) {
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+          crc ^= T[(8 * j + b) * 256 + (uint32_t)((k[j] >> (8 * b)) & 0xFF)];
+      }
+    }
+    const uint16_t *g = reinterpret_cast<const uint16_t *>(T + x.L * 256);
+    return g[(uint32_t)(((uint64_t)crc * x.num_gates) >> 32)];
+  }
+};
+
 // fields mode: MakeKeys key, CRC over its first L bytes
 template <int KW, int NCH>
 __global__ __launch_bounds__(kHlbBlock) void hlb_fields_kernel(HlbArgs a) {
@@ -132,8 +174,16 @@ hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s) {
   const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 && maxops <= 2 ? 2 : 4);
   const int w8 = (int)(a.L + 7) / 8;
   const int kw = w8 <= 1 ? 1 : w8 <= 2 ? 2 : w8 <= 4 ? 4 : 8;
-#define BG_HLB(KW, NCH) \
-  if (kw == KW && nch == NCH) return launch_hlb_fields<KW, NCH>(a, num_cus, s);
+  // the fields inside the first 64 bytes of dense 64 B slots: a line op on
+  // the slab kernel's lane-contiguous loads (wider strides keep the
+  // lane-per-packet kernel, which loads only the window's chunks)
+  const bool line = nch > 0 && a.fp.win_lo + 16 * nch <= 64 && a.stride == 64 &&
+                    ((uintptr_t)a.frames & 15) == 0 && !(path_flags() & kPathNoSlab) &&
+                    !knob("BG_HLB_FIELDS_LANE", 0);
+#define BG_HLB(KW, NCH)                                                       \
+  if (kw == KW && nch == NCH)                                                 \
+    return line && NCH > 0 ? launch_line<HlbFieldsOp<KW, (NCH > 0 ? NCH : 2)>>(a, num_cus, s) \
+                           : launch_hlb_fields<KW, NCH>(a, num_cus, s);
 #define BG_HLB_K(KW) BG_HLB(KW, 0) BG_HLB(KW, 2) BG_HLB(KW, 4)
   BG_HLB_K(1) BG_HLB_K(2) BG_HLB_K(4) BG_HLB_K(8)
 #undef BG_HLB_K
