@@ -82,14 +82,30 @@ FIELDSETS = [
                                        for fi in range(len(FIELDSETS))] +
                          [(0, 64), (1, 64), (2, 64), (4, 64)])
 def test_fields_vs_oracle(fi, stride):
-    """hlb_fields_kernel at slot strides 64 (a ragged last tile), 128 and
-    1040 (fields too far apart for one window)"""
+    """fields mode at slot strides 64 (the header-line op, a ragged last
+    tile), 128 and 1040 (hlb_fields_kernel; fields too far apart for one
+    window)"""
     fl = FIELDSETS[fi]
     f = frames(8001, stride, seed=10 + fi)
     g = list(range(37))
     m = HashLB(gates=g, fields=fl)
     o = OM.OracleHashLB(gates=g, fields=fl)
     assert (device_gates(m, f, stride) == o.process(f, stride, len(f))).all()
+
+
+@pytest.mark.parametrize("fi", [0, 1, 2, 4])
+def test_fields_lane_kernel_on_dense_slots(fi):
+    """BG_PATH_NO_SLAB: dense 64 B slots through hlb_fields_kernel (one
+    packet per lane) instead of the header-line op -- same gates"""
+    from bess_amd._lib import kernel_paths, BG_PATH_NO_SLAB
+    fl = FIELDSETS[fi]
+    f = frames(8001, 64, seed=40 + fi)
+    g = list(range(29))
+    m = HashLB(gates=g, fields=fl)
+    o = OM.OracleHashLB(gates=g, fields=fl)
+    with kernel_paths(BG_PATH_NO_SLAB):
+        got = device_gates(m, f, 64)
+    assert (got == o.process(f, 64, len(f))).all()
 
 
 def test_partial_updates_match_reference():
