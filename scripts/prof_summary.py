@@ -9,9 +9,25 @@ and at batch sizes 32..4096 (the sweep), so this splits the average by
 grid size -- the full-size row is the one bench.py's kernel_ms must match.
 """
 import csv
-import re
 import sys
 from collections import defaultdict
+
+
+def short_name(name):
+    """the kernel's name with its template arguments, without the return
+    type, the argument list and the namespaces"""
+    name = name.replace("bg::(anonymous namespace)::", "").replace("bg::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    depth = 0
+    for i, c in enumerate(name):
+        if c == "<":
+            depth += 1
+        elif c == ">":
+            depth -= 1
+        elif c == "(" and depth == 0:
+            return name[:i].replace("> >", ">>")
+    return name
 
 
 def main():
@@ -21,8 +37,7 @@ def main():
             name = r["Kernel_Name"]
             if "bg::" not in name and not name.startswith("bg_wm_jit"):
                 continue  # (bg_wm_jit_*: the run-time compiled WM kernels)
-            m = re.search(r"(\w+)(<[^>]*>)?\(bg::", name)
-            short = (m.group(1) + (m.group(2) or "")) if m else name
+            short = short_name(name)
             d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
             rows[(short, int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]),
                   int(r["VGPR_Count"]), int(r["SGPR_Count"]))].append(d)
