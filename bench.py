@@ -1827,6 +1827,8 @@ def main():
                      "bytes_per_pkt": EM_BYTES_PER_PKT},
         "parity": "bit-exact vs oracle on 1M-pkt sample" if r["parity"]
                   else "MISMATCH",
+        # the same memory traffic without the lookup (hbm_probe slab66)
+        "measured_ceiling": shape_ceiling("slab66", r["n"], kern_ms),
         "cpu_baseline": None,
     }
     comm = None  # C5's communicator (N > 1), closed before the process group

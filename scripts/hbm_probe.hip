@@ -29,6 +29,11 @@
 //             wave reads its 64 slots (4 KB) with four lane-contiguous 16 B
 //             loads (em_slab_kernel's shape), lane l then makes slot l's
 //             random reads with a hash of the data it loaded
+// Line-op shape (`./hbm_probe GiB c`; TB/s of the 66 B/packet basis):
+//   slab66  : em_slab_kernel's / line_slab_kernel's memory traffic alone --
+//             a wave reads its 64 slots (4 KB) with four lane-contiguous
+//             16 B loads and lane l stores slot l's 2-byte gate (no LDS, no
+//             lookup): the ceiling of C2 and the header-line ops
 // `./hbm_probe GiB only SHAPE BLOCKS_PER_CU LAUNCHES` runs one shape (for
 // rocprofv3 --pmc passes: FETCH_SIZE per launch against a known shape).
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
@@ -177,6 +182,20 @@ __global__ __launch_bounds__(512) void w64(u32x4 *dst, size_t nslots, uint32_t s
     dst[((u >> 2) * slot + off) / 16 + (u & 3)] = u32x4{(uint32_t)u, 1u, 2u, 3u};
 }
 
+// rnd36s's stream without the random reads (nslots: a multiple of 64)
+__global__ __launch_bounds__(512) void slab66(const u32x4 *src, size_t nslots,
+                                              uint16_t *gates) {
+  const int lane = threadIdx.x & 63;
+  const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t * 64 < nslots;
+       t += nwaves) {
+    const u32x4 *g = src + t * 256;
+    const u32x4 a = ldnt(g + lane), b = ldnt(g + 64 + lane), c = ldnt(g + 128 + lane),
+                d = ldnt(g + 192 + lane);
+    gates[t * 64 + lane] = (uint16_t)(a.x ^ b.y ^ c.z ^ d.w);
+  }
+}
+
 #define CK(x)                                                            \
   do {                                                                   \
     hipError_t e = (x);                                                  \
@@ -205,15 +224,16 @@ int main(int argc, char **argv) {
   const bool wr = argc > 2 && argv[2][0] == 'w';
   const bool sc = argc > 2 && argv[2][0] == 's';
   const bool only = argc > 5 && !strcmp(argv[2], "only");
-  const char *names[11] = {"full16", "em32",  "slot64", "half32", "wfull16", "w64s192",
-                           "w64s128", "s2k32", "s2k64", "rnd36", "rnd36s"};
+  const bool cs = argc > 2 && argv[2][0] == 'c';
+  const char *names[12] = {"full16",  "em32",  "slot64", "half32", "wfull16", "w64s192",
+                           "w64s128", "s2k32", "s2k64",  "rnd36",  "rnd36s",  "slab66"};
   uint32_t *tab = nullptr;
   CK(hipMalloc(&tab, 36u << 20));
   CK(hipMemset(tab, 0x33, 36u << 20));
-  int s0 = wr ? 4 : sc ? 7 : 0, s1 = wr ? 7 : sc ? 11 : 4;
+  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 12 : 4;
   int only_bpc = 0, only_launches = 0;
   if (only) {
-    for (int k = 0; k < 11; k++)
+    for (int k = 0; k < 12; k++)
       if (!strcmp(argv[3], names[k])) s0 = k, s1 = k + 1;
     only_bpc = atoi(argv[4]);
     only_launches = atoi(argv[5]);
@@ -227,7 +247,7 @@ int main(int argc, char **argv) {
       if (shape == 5) moved = (double)(bytes / 192) * 64;
       if (shape == 6) moved = (double)(bytes / 128) * 64;
       if (shape == 7 || shape == 8) pkts = (double)(bytes / 2048);
-      if (shape >= 7) moved = pkts * 66;  // the algorithmic basis
+      if (shape >= 7) moved = pkts * 66;  // the algorithmic basis (slab66 too)
       auto launch = [&]() {
         if (shape == 0)
           hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
@@ -258,9 +278,11 @@ int main(int argc, char **argv) {
         else if (shape == 9)
           hipLaunchKernelGGL(rnd36, dim3(blocks), dim3(512), 0, 0, src, nslots, tab,
                              gates);
-        else
+        else if (shape == 10)
           hipLaunchKernelGGL(rnd36s, dim3(blocks), dim3(512), 0, 0, src, nslots, tab,
                              gates);
+        else
+          hipLaunchKernelGGL(slab66, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
       };
       if (only) {  // a fixed number of launches, no timing (rocprofv3 passes)
         for (int w = 0; w < only_launches; w++) launch();
