@@ -29,11 +29,14 @@
 //             wave reads its 64 slots (4 KB) with four lane-contiguous 16 B
 //             loads (em_slab_kernel's shape), lane l then makes slot l's
 //             random reads with a hash of the data it loaded
-// Line-op shape (`./hbm_probe GiB c`; TB/s of the 66 B/packet basis):
+// Line-op shapes (`./hbm_probe GiB c`; TB/s of the 66 / 130 B/packet basis):
 //   slab66  : em_slab_kernel's / line_slab_kernel's memory traffic alone --
 //             a wave reads its 64 slots (4 KB) with four lane-contiguous
 //             16 B loads and lane l stores slot l's 2-byte gate (no LDS, no
 //             lookup): the ceiling of C2 and the header-line ops
+//   slab130 : the same tile read, every line stored back in place (lane-
+//             contiguous 16 B stores) and the gates: UpdateTTL's / StaticNAT's
+//             traffic (130 B/packet basis)
 // `./hbm_probe GiB only SHAPE BLOCKS_PER_CU LAUNCHES` runs one shape (for
 // rocprofv3 --pmc passes: FETCH_SIZE per launch against a known shape).
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
@@ -196,6 +199,24 @@ __global__ __launch_bounds__(512) void slab66(const u32x4 *src, size_t nslots,
   }
 }
 
+// slab66 with every line written back (in place)
+__global__ __launch_bounds__(512) void slab130(u32x4 *src, size_t nslots, uint16_t *gates) {
+  const int lane = threadIdx.x & 63;
+  const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t * 64 < nslots;
+       t += nwaves) {
+    u32x4 *g = src + t * 256;
+    u32x4 a = ldnt(g + lane), b = ldnt(g + 64 + lane), c = ldnt(g + 128 + lane),
+          d = ldnt(g + 192 + lane);
+    a.x ^= 1u; b.y ^= 1u; c.z ^= 1u; d.w ^= 1u;
+    g[lane] = a;
+    g[64 + lane] = b;
+    g[128 + lane] = c;
+    g[192 + lane] = d;
+    gates[t * 64 + lane] = (uint16_t)(a.y ^ b.x);
+  }
+}
+
 #define CK(x)                                                            \
   do {                                                                   \
     hipError_t e = (x);                                                  \
@@ -225,15 +246,15 @@ int main(int argc, char **argv) {
   const bool sc = argc > 2 && argv[2][0] == 's';
   const bool only = argc > 5 && !strcmp(argv[2], "only");
   const bool cs = argc > 2 && argv[2][0] == 'c';
-  const char *names[12] = {"full16",  "em32",  "slot64", "half32", "wfull16", "w64s192",
-                           "w64s128", "s2k32", "s2k64",  "rnd36",  "rnd36s",  "slab66"};
+  const char *names[13] = {"full16",  "em32",  "slot64", "half32", "wfull16", "w64s192", "w64s128",
+                           "s2k32",   "s2k64", "rnd36",  "rnd36s", "slab66",  "slab130"};
   uint32_t *tab = nullptr;
   CK(hipMalloc(&tab, 36u << 20));
   CK(hipMemset(tab, 0x33, 36u << 20));
-  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 12 : 4;
+  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 13 : 4;
   int only_bpc = 0, only_launches = 0;
   if (only) {
-    for (int k = 0; k < 12; k++)
+    for (int k = 0; k < 13; k++)
       if (!strcmp(argv[3], names[k])) s0 = k, s1 = k + 1;
     only_bpc = atoi(argv[4]);
     only_launches = atoi(argv[5]);
@@ -247,7 +268,7 @@ int main(int argc, char **argv) {
       if (shape == 5) moved = (double)(bytes / 192) * 64;
       if (shape == 6) moved = (double)(bytes / 128) * 64;
       if (shape == 7 || shape == 8) pkts = (double)(bytes / 2048);
-      if (shape >= 7) moved = pkts * 66;  // the algorithmic basis (slab66 too)
+      if (shape >= 7) moved = pkts * (shape == 12 ? 130 : 66);  // the algorithmic basis
       auto launch = [&]() {
         if (shape == 0)
           hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
@@ -281,8 +302,10 @@ int main(int argc, char **argv) {
         else if (shape == 10)
           hipLaunchKernelGGL(rnd36s, dim3(blocks), dim3(512), 0, 0, src, nslots, tab,
                              gates);
-        else
+        else if (shape == 11)
           hipLaunchKernelGGL(slab66, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
+        else
+          hipLaunchKernelGGL(slab130, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
       };
       if (only) {  // a fixed number of launches, no timing (rocprofv3 passes)
         for (int w = 0; w < only_launches; w++) launch();
