@@ -73,6 +73,8 @@ def parse():
                     help="worker threads of the bg_pipe legs")
     ap.add_argument("--wm-layout", default="both", choices=("both", "slab", "2k"),
                     help="C4 layouts to time (PMC passes time one at a time)")
+    ap.add_argument("--em1500-pkts", type=int, default=1 << 22,
+                    help="resident 1500 B packets of the EM 1500 B leg (2 KB slots)")
     ap.add_argument("--c5-rules", type=int, default=1 << 20,
                     help="rules of the sharded C5 table in the N > 1 line")
     ap.add_argument("--no-churn", action="store_true",
@@ -81,7 +83,7 @@ def parse():
                     help="time another build of libbessgpu.so (same-box A/B)")
     ap.add_argument("--drive", default="",
                     help="another build of tests/bessd_shell's driver (same-box A/B)")
-    ap.add_argument("--only", default="", help="c1|cksum|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|rewrite|pipe|plugin|sweep (profiling runs)")
+    ap.add_argument("--only", default="", help="c1|cksum|em1500|wm|c5|hashlb|acl|iplookup|ttl|nat|dnat|rewrite|pipe|plugin|sweep (profiling runs)")
     return ap.parse_args()
 
 
@@ -449,6 +451,64 @@ def run_cksum(args, dev, torch):
     return out
 
 
+def run_em1500(args, dev, torch):
+    """The north star's 1500 B match point: C2's 1K-rule 5-tuple
+    ExactMatch (exact_match.cc:224-244) over 1500 B packets (1496 B frames,
+    SURVEY §8d) resident in 2 KB slots, the snbuf data area's size. The
+    classifier reads each frame's field window only (66 B/pkt, as C2)."""
+    from bess_amd import flowtable as F
+    from bess_amd import packets as P
+    from oracle import oracle as O
+    n = args.em1500_pkts
+    # the frames' first 64 bytes (Ethernet / IPv4 with ip.length 1482 /
+    # UDP or TCP), then the slab: zero payload past them
+    keys, gates, hdr = P.em_workload(args.rules, n, seed=0x5EED, stride=64,
+                                     frame_len=1496, pkt_seed=0x1500)
+    d = torch.zeros(n * 2048, dtype=torch.uint8, device=dev)
+    d.view(n, 2048)[:, :64] = torch.from_numpy(hdr).to(dev)
+    ns = 1 << 20
+    sample = np.ascontiguousarray(hdr[:ns])
+    del hdr
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    t.sync(dev.index)
+    dg = torch.empty(n, dtype=torch.int16, device=dev)
+    t.classify(d, 2048, n, 8192, dg)
+    torch.cuda.synchronize()
+    em = oracle_em_bulk(keys, gates)
+    L = O.lib()
+    want = np.zeros(ns, np.uint16)
+    L.or_em_process(em, sample.ctypes.data, 64, ns, 8192, want.ctypes.data)
+    parity = bool((dg[:ns].cpu().numpy().view(np.uint16) == want).all())
+    ms = _time_steps(lambda: t.classify(d, 2048, n, 8192, dg), args, torch)
+    out = {"workload": "1500B pkts (1496B frames, 2048B slots), %d-rule 5-tuple "
+                       "ExactMatch, %d resident pkts" % (args.rules, n),
+           "pkts": n, "ms_per_step": round(ms, 4),
+           "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
+           "kernel": "em_classify_kernel (one 32 B field window per 2 KB slot)",
+           "roofline": _roof(EM_BYTES_PER_PKT, n, ms, "em1500"),
+           # a 32 B window per 2 KB slot is one 64 B HBM request: the
+           # shape's own rate (hbm_probe s2k32) bounds this leg
+           "measured_ceiling": shape_ceiling("s2k32", n, ms),
+           "parity": "bit-exact vs oracle on %d pkts" % ns if parity else "MISMATCH"}
+    if not args.no_cpu:
+        cn = 1 << 18
+        snb = np.zeros((cn, 2624), np.uint8)
+        snb[:, 512:512 + 64] = sample[:cn]
+        base = snb.ctypes.data + 512
+        g = np.zeros(cn, np.uint16)
+        threads, res = cpu_rate(
+            lambda nt, reps: L.or_em_bench(em, base, 2624, cn, 8192, g.ctypes.data,
+                                           nt, reps), cn, args.cpu_seconds / 2)
+        out["cpu_baseline"] = cpu_baseline(
+            res, threads, "%d 1500B pkts x reps, 1K-rule 5-tuple ExactMatch, snbuf "
+                          "layout (2624 B stride), 32-pkt batches" % cn)
+    L.or_em_free(em)
+    del d, dg
+    torch.cuda.empty_cache()
+    return out
+
+
 def run_e2e_host(r, args, torch):
     """End-to-end rate from host memory (the reference's path starts and
     ends in mbufs): frames in snbuf-like host buffers (2624 B stride, frame
@@ -811,6 +871,9 @@ def run_plugin_pool(args):
                 _, l4w = O.cksum_process(ref, 2048, n, 2, False)
                 script = ["create L4Checksum -", "connect 0", "connect 1"]
                 exp = ["-" if int(w) == 0xFFFF else str(int(w)) for w in l4w]
+                # the CPU baseline in the same harness: the restated
+                # reference L4Checksum::ProcessBatch (AVX2/adc CalculateSum)
+                script.append("cpu_l4 0")
             path = os.path.join(td, "f.bin")
             frames.tofile(path)
             # enough passes for the steady state (the first pass opens the
@@ -819,8 +882,7 @@ def run_plugin_pool(args):
             script += ["frames %s 2048 %d" % (path, n), "pool 262144",
                        "pipeline 16 1 0 0 0", "sleep 3000",  # (the run-time compile)
                        "pipeline 16 %d 0 0 0" % reps]
-            if name == "WildcardMatch":
-                script += ["pipeline_cpu 16 1", "pipeline_cpu 16 %d" % reps]
+            script += ["pipeline_cpu 16 1", "pipeline_cpu 16 %d" % reps]
             r = subprocess.run([drive, "run"], input="\n".join(script) + "\n",
                                capture_output=True, text=True, timeout=600)
             lines = r.stdout.splitlines()
@@ -835,15 +897,24 @@ def run_plugin_pool(args):
                          "pool_after": "%s of %s back" % (pools[-1][1], pools[-1][2]),
                          "never_emitted_per_pass": exp.count("-"),
                          "source_waits": int(pools[-1][3])}
+            # worker 0's pipe counters and TSC cycles per packet of the timed
+            # GPU pass (where the host side's time goes)
+            st = [x for x in lines if x.startswith("stats")]
+            cyc = [x for x in lines if x.startswith("cycles")]
+            if len(st) >= 2:
+                out[name]["pipe_w0"] = st[1][6:]
+            if len(cyc) >= 2:
+                out[name]["cycles_w0_gpu"] = cyc[1][7:]
+            if len(cyc) >= 4:
+                out[name]["cycles_w0_cpu"] = cyc[3][7:]
             if name == "WildcardMatch":
                 out[name]["rules"] = nr
-                if len(stats) >= 4 and len(outs) >= 4:
-                    out[name]["cpu_same_harness"] = {
-                        "what": "the same pool, Sources and Sinks with the restated "
-                                "reference WildcardMatch::ProcessBatch (oracle tuple-"
-                                "space search) in place of the plugin",
-                        "Mpps": round(float(stats[3].split()[1]), 1),
-                        "parity": outs[3].split()[1:] == exp}
+            if len(stats) >= 4 and len(outs) >= 4:
+                out[name]["cpu_same_harness"] = {
+                    "what": "the same pool, Sources and Sinks with the restated "
+                            "reference %s::ProcessBatch in place of the plugin" % name,
+                    "Mpps": round(float(stats[3].split()[1]), 1),
+                    "parity": outs[3].split()[1:] == exp}
     return out
 
 
@@ -1776,6 +1847,7 @@ def main():
     bess_amd.lib()  # fail loudly if the HIP library is missing
 
     only = {"cksum": lambda: run_cksum(args, dev, torch),
+            "em1500": lambda: run_em1500(args, dev, torch),
             "wm": lambda: run_wm(args, dev, torch),
             "c5": lambda: run_c5(args, dev, torch),
             "ttl": lambda: run_update_ttl(args, dev, torch),
@@ -1868,7 +1940,8 @@ def main():
                 out["e2e_plugin_pool"] = run_plugin_pool(args)
             except Exception as e:
                 out["e2e_plugin_pool"] = "failed: %r" % (e,)
-        for name, fn in (("C3", run_cksum), ("C4", run_wm), ("C5", run_c5),
+        for name, fn in (("C3", run_cksum), ("EM_1500B", run_em1500),
+                         ("C4", run_wm), ("C5", run_c5),
                          ("HashLB", run_hashlb), ("ACL", run_acl),
                          ("IPLookup", run_iplookup),
                          ("UpdateTTL", run_update_ttl),

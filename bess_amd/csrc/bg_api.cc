@@ -693,6 +693,9 @@ static int bind_meta(const std::vector<bg_field> &fields, int meta_off,
   if (meta_off >= 0) {
     resolve_attrs(fields, meta_off, o, out);
     *slab_bound = true;
+  } else {  // offsets only: the device-slab calls stay unbound until bound
+    out->clear();
+    *slab_bound = false;
   }
   offs->swap(o);
   return 0;
@@ -779,6 +782,10 @@ int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
                     &em->dfields, &em->meta_bound);
   if (r) return r;
   em->attrs_known = true;
+  // what was derived from the old offsets (a pipe's ring and its field
+  // plan, PipeRingCurrent) is keyed on the version: a new layout is a new
+  // version, even one whose metadata window [mlo, mhi) did not move
+  em_changed(em);
   return 0;
 }
 
@@ -1564,6 +1571,7 @@ int bg_wm_bind_meta(bg_wm *wm, int meta_off, const int32_t *attr_offsets,
                     &wm->dfields, &wm->meta_bound);
   if (r) return r;
   wm->attrs_known = true;
+  wm_changed(wm);  // as bg_em_bind_meta: rings of the old layout retire
   return 0;
 }
 

@@ -21,6 +21,7 @@ struct bg_rewrite {
   std::vector<uint16_t> size;
   uint64_t next = 0;            // next_turn_
   bool dirty = true;
+  bool uploaded = false;        // d_tmpl holds templates a kernel may read
   int device = -1;
   uint8_t *d_tmpl = nullptr;    // kRwMaxTemplates x kRwMaxSize
   uint16_t *d_size = nullptr;
@@ -41,6 +42,7 @@ int sync_templates(bg_rewrite *h, int device, hipStream_t s) {
     h->d_size = nullptr;
     h->device = device;
     h->dirty = true;
+    h->uploaded = false;
   }
   if (!h->d_tmpl) {
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tmpl),
@@ -48,11 +50,17 @@ int sync_templates(bg_rewrite *h, int device, hipStream_t s) {
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_size), kRwMaxTemplates * 2));
   }
   if (h->dirty && !h->size.empty()) {
+    // a rewrite launched earlier, on any stream, may still read the old
+    // templates: they are overwritten only once the device is idle (template
+    // changes are THREAD_UNSAFE commands, made with the workers paused, so
+    // this waits for queued batches only)
+    if (h->uploaded) HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyAsync(h->d_tmpl, h->tmpl.data(), h->tmpl.size(),
                            hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(h->d_size, h->size.data(), h->size.size() * 2,
                            hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
+    h->uploaded = true;
   }
   h->dirty = false;
   return 0;

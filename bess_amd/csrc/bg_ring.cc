@@ -94,6 +94,7 @@ struct bg_ring {
 namespace {
 
 constexpr uint64_t kMaskAddr = (1ull << 48) - 1;
+constexpr size_t kTicketMaxPkts = (size_t)1 << 27;  // packets per ticket
 
 double now_s() {
   timespec ts;
@@ -432,7 +433,9 @@ void bg_ring_destroy(bg_ring *r) {
 int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
                        size_t n, uint16_t default_gate, uint16_t *gates) {
   if (lane < 0 || (uint32_t)lane >= r->nlanes) return bad_lane(r, lane);
-  if (n > 0xFFFFFFFFu || stride == 0 || stride > 0xFFFF)
+  // a run sums up to 16 tickets' counts in 32 bits (ring_serve's prefix
+  // sums and `base < total` loop): 16 x 2^27 stays below 2^32
+  if (n > kTicketMaxPkts || stride == 0 || stride > 0xFFFF)
     return fail(EINVAL, "n %zu / stride %zu out of range", n, stride);
   if ((int)stride < r->read_end)
     return fail(EINVAL, "fields read %d bytes, past the %zu-byte slot",

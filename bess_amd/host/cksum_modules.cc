@@ -34,6 +34,26 @@ class ChecksumModule : public Module {
     *writeback = true;
   }
 
+  // The bytes the reference reads past data_len (P11): L4Checksum sums
+  // udp.length bytes from the UDP header (checksum.h:398-407) or ip.length
+  // minus the IP header from the TCP header (checksum.h:492-504) of an
+  // untagged IPv4 frame (l4_checksum.cc:53-82), without checking data_len.
+  // IPChecksum reads at most 22 + 60 bytes, inside the header line the pipe
+  // always stages.
+  size_t StageReach(const uint8_t *f, size_t len) const override {
+    if (kMode != BG_CK_L4 || f[12] != 0x08 || f[13] != 0x00) return len;
+    const size_t l4 = 14 + (size_t)(f[14] & 15) * 4;
+    size_t end = 0;
+    if (f[23] == 17) {  // UDP: length at l4 + 4 (l4 + 6 <= 80, in the line)
+      const size_t ulen = (size_t)f[l4 + 4] << 8 | f[l4 + 5];
+      if (ulen >= 8) end = l4 + ulen;
+    } else if (f[23] == 6) {  // TCP: ip.length - IHL*4 bytes from l4
+      const size_t ip_len = (size_t)f[16] << 8 | f[17];
+      if (ip_len >= l4 - 14 + 20) end = 14 + ip_len;
+    }
+    return std::max(len, end);
+  }
+
   int ProcessDevice(const bg_ctx &c, void *d_frames, size_t stride, size_t n,
                     uint16_t *d_ogates, void *stream) override {
     return bg_cksum(c.device, d_frames, stride, n, kMode, verify_ ? 1 : 0,

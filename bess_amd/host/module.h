@@ -225,6 +225,15 @@ class Module {
     *hi = 2048;  // SNBUF_DATA (core/snbuf_layout.h:34-68)
     *writeback = false;
   }
+  // How many bytes from the head a writeback datapath reads of a frame whose
+  // data_len is `len` (the pipe stages that many, capped to the window, and
+  // zero-pads only past them). The reference's checksum modules sum the
+  // byte counts the headers give, whatever data_len is: they
+  // override this.
+  virtual size_t StageReach(const uint8_t *frame, size_t len) const {
+    (void)frame;
+    return len;
+  }
   // The metadata bytes [*mlo, *mhi) the device datapath reads (attr_name
   // fields), staged after the frame window (StagedMetaAt);
   // none: *mlo == *mhi. -errno while the attribute offsets are unbound.

@@ -526,6 +526,7 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
   p->st_submits++;
   p->st_pkts += cnt;
   const size_t span = (size_t)(p->hi - p->lo);
+  const Module *mod = p->mod->m.get();
   size_t i = 0;
   while (i < cnt) {
     Slot &s = p->slots[p->fill];
@@ -567,9 +568,10 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
         }
       } else {
         if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
-        // the frame (data_len bytes when given, at least its header line),
-        // zero-padded to the slot
-        size_t len = lens ? std::min<size_t>(lens[k], span) : span;
+        // the bytes the module reads (data_len when given, or what its
+        // headers reach past it, Module::StageReach; at least the header
+        // line), zero-padded to the slot
+        size_t len = lens ? std::min<size_t>(mod->StageReach(heads[k], lens[k]), span) : span;
         const size_t line = std::min(span, kWriteback);
         len = std::max(len, line);
         memcpy(dst, src, len);

@@ -190,3 +190,29 @@ def cksum_workload(n_pkts, frame_len=1496, stride=2048, udp_frac=0.5,
     f[udp, 40:42] = rng.integers(0, 256, (int(udp.sum()), 2), dtype=np.uint8)
     f[~udp, 50:52] = rng.integers(0, 256, (int((~udp).sum()), 2), dtype=np.uint8)
     return f
+
+
+def cksum_p11_workload(n, seed=11):
+    """Frames whose UDP / TCP length fields run past data_len over non-zero
+    bytes: the reference sums udp.length / ip.length-derived
+    byte counts from the packet buffer whatever data_len is
+    (checksum.h:398-407, 492-504; l4_checksum.cc:61-82). Returns (frames
+    n x 2048 -- the whole data area, every byte past the frame random --,
+    data_len per packet)."""
+    rng = np.random.default_rng(seed)
+    f = cksum_workload(n, frame_len=1496, seed=seed)
+    f[:, 1496:] = rng.integers(1, 256, (n, 2048 - 1496), dtype=np.uint8)
+    lens = rng.integers(60, 1497, n).astype(np.uint16)
+    udp = f[:, 23] == 17
+    # a third of the frames: length fields out to the end of the data area
+    far = rng.random(n) < 1 / 3
+    ln = rng.integers(1500, 2048 - 34, n)
+    u = far & udp
+    f[u, 38] = ln[u] >> 8
+    f[u, 39] = ln[u] & 255
+    t = far & ~udp
+    f[t, 16] = (ln[t] + 20) >> 8
+    f[t, 17] = (ln[t] + 20) & 255
+    # and some with data_len past what the headers give (nothing to add)
+    lens[rng.random(n) < 0.1] = 2048
+    return f, lens

@@ -98,10 +98,11 @@ int bg_em_sync(bg_em *em, int device, bg_stream_t stream);
  * area at byte meta_off; attr_offsets[attr_id] is attr_offset(attr_id)
  * (nattrs entries, < 0: none -> EINVAL, where the reference would
  * dereference a null attribute pointer). meta_off -1: the attribute offsets
- * only (staged rows, bg_em_classify_staged; the device-slab calls stay
- * unbound). Until bound, classify returns ENOTSUP for tables with attr
- * fields; bg_em_process_host (head pointers only) never carries metadata
- * and keeps returning ENOTSUP. */
+ * only (staged rows, bg_em_classify_staged; the device-slab calls are
+ * unbound, including a slab layout an earlier call bound). Until bound,
+ * classify returns ENOTSUP for tables with attr fields; bg_em_process_host
+ * (head pointers only) never carries metadata and keeps returning ENOTSUP.
+ * A bind is a table change: pipes' rings built on the old offsets retire. */
 int bg_em_bind_meta(bg_em *em, int meta_off, const int32_t *attr_offsets,
                     int nattrs);
 /* Device-resident classify: d_gates[i] = gate for frame i (default_gate on
@@ -634,7 +635,7 @@ int bg_pipe_run(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
  * Each worker thread submits on its own lane (0 .. lanes-1: its own ring of
  * `slots` descriptors, done words and published count, so workers never
  * share a cache line or a lock): submit enqueues a batch (frames at
- * `frames` + i*stride, device or mapped host memory, each slot holding the
+ * `frames` + i*stride (n <= 2^27), device or mapped host memory, each slot holding the
  * frame from byte win_off on -- 0: whole frames, the field window's start:
  * staged windows; gates written to `gates`) and returns the lane's ticket; wait blocks until that ticket's
  * gates are written; completed returns the number of the lane's tickets

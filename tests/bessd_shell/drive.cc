@@ -9,6 +9,9 @@
 //     desc                        GetDesc         -> "desc <text>"
 //     connect <ogate>             ConnectModules for that output gate
 //     frames <path> <stride> <n>  n frames of `stride` bytes into snbufs
+//     lens <path>                 each packet's data_len (and total_len): one
+//                                 u16 per packet (the bytes past it keep the
+//                                 frames file's, as a reused buffer would)
 //     meta <path> <bytes>         each packet's metadata area (Packet::metadata,
 //                                 SNBUF_METADATA_OFF) gets `bytes` bytes from
 //                                 the file, packet after packet
@@ -51,6 +54,7 @@
 //                                 run-time compile finishes untimed)
 //     cpu_wm <keys> <masks> <prios> <gates> <n>  the same for WildcardMatch
 //                                 (16-byte keys and masks, i32 priorities)
+//     cpu_l4 <verify>             the same for L4Checksum (in place)
 //     pipeline_cpu <workers> <reps>  the same Source -> Sink loop with the
 //                                 restated reference ProcessBatch on the CPU
 //                                 in the middle (head_data() per packet,
@@ -198,6 +202,7 @@ static int run() {
   uint8_t *pool = nullptr;
   or_em *cpu_em = nullptr;
   or_wm *cpu_wm = nullptr;
+  int cpu_l4 = -1;  // L4Checksum's verify flag (cpu_l4), -1: none
   std::vector<uint8_t *> bufs;
   std::vector<char> fdata;  // the frames file (pool mode: the Sources' frames)
   size_t fstride = 0;
@@ -277,6 +282,20 @@ static int run() {
         p->set_data_len((uint16_t)stride);
         bufs.push_back(b);
       }
+    } else if (op == "lens") {
+      std::string path;
+      in >> path;
+      std::ifstream f(path, std::ios::binary);
+      for (uint8_t *b : bufs) {
+        uint16_t l = 0;
+        f.read(reinterpret_cast<char *>(&l), 2);
+        bess::Packet *p = reinterpret_cast<bess::Packet *>(b);
+        p->set_total_len(l);
+        p->set_data_len(l);
+      }
+    } else if (op == "cpu_l4") {
+      in >> cpu_l4;
+      printf("cpu_l4 %d\n", cpu_l4);
     } else if (op == "pool") {
       size_t cap;
       in >> cap;
@@ -382,8 +401,8 @@ static int run() {
       unsigned long long now = 0;
       in >> nw >> reps;
       if (!cpu) in >> ig >> now >> verify;
-      if (cpu && !cpu_em && !cpu_wm) {
-        printf("rc 22 cpu_em / cpu_wm first\n");
+      if (cpu && !cpu_em && !cpu_wm && cpu_l4 < 0) {
+        printf("rc 22 cpu_em / cpu_wm / cpu_l4 first\n");
         continue;
       }
       const size_t n = bufs.size();
@@ -455,16 +474,19 @@ static int run() {
             }
             const uint64_t c0 = __rdtsc();
             if (cpu) {  // ExactMatch::ProcessBatch restated (exact_match.cc:224-244)
-                        // or WildcardMatch's (cpu_wm)
-              const uint8_t *heads[bess::PacketBatch::kMaxBurst];
+                        // or WildcardMatch's (cpu_wm), L4Checksum's (cpu_l4)
+              uint8_t *heads[bess::PacketBatch::kMaxBurst];
               uint16_t g[bess::PacketBatch::kMaxBurst];
               for (int i = 0; i < batch.cnt(); i++)
-                heads[i] = batch.pkts()[i]->head_data<const uint8_t *>();
-              if (cpu_wm)  // WildcardMatch::ProcessBatch (wildcard_match.cc:159-203)
+                heads[i] = batch.pkts()[i]->head_data<uint8_t *>();
+              if (cpu_l4 >= 0)  // L4Checksum::ProcessBatch (l4_checksum.cc:41-83)
+                or_l4_checksum_batch(heads, batch.cnt(), cpu_l4, g);
+              else if (cpu_wm)  // WildcardMatch::ProcessBatch (wildcard_match.cc:159-203)
                 or_wm_process_batch(cpu_wm, heads, batch.cnt(), DROP_GATE, g);
               else
                 or_em_process_batch(cpu_em, heads, batch.cnt(), DROP_GATE, g);
-              for (int i = 0; i < batch.cnt(); i++) m->EmitPacket(&ctx, batch.pkts()[i], g[i]);
+              for (int i = 0; i < batch.cnt(); i++)
+                if (g[i] != OR_GATE_NONE) m->EmitPacket(&ctx, batch.pkts()[i], g[i]);
             } else {
               m->ProcessBatch(&ctx, &batch);
             }

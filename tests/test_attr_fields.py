@@ -117,6 +117,12 @@ def test_gpu_em_attr_fields_vs_oracle():
     got = og.cpu().numpy().view(np.uint16)
     assert (got == want).all()
     assert (want != 70).mean() > 0.02
+    # offsets only (a host datapath's bind): the slab layout bound before
+    # is gone, so the device-slab call is unbound again
+    m.bind_meta(-1, ATTR_OFF)
+    with pytest.raises(ModuleError) as e:
+        m.process_device(d, STRIDE, n, og)
+    assert e.value.code == errno.ENOTSUP
 
 
 @pytest.mark.gpu

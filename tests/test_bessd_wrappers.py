@@ -394,6 +394,37 @@ def test_deferred_pipeline_l4_checksum_and_acl(drive, tmp_path):
     assert "order ok" in out
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("verify", [False, True])
+def test_l4_checksum_plugin_reads_past_data_len(drive, tmp_path, verify):
+    """The L4Checksum plugin on packets whose UDP / TCP length fields run
+    past data_len over stale non-zero bytes: the reference
+    sums what the buffer holds there (checksum.h:398-407, 492-504), so the
+    plugin's gates and checksum words equal the oracle's over the whole
+    2048 B data areas."""
+    from oracle import oracle as O
+    n = 2000
+    f, lens = P.cksum_p11_workload(n, seed=21)
+    if verify:
+        O.cksum_process(f[:n // 2], 2048, n // 2, 3, False)
+    ref = f.copy()
+    _, l4w = O.cksum_process(ref, 2048, n, 2, verify)
+    path, lpath = tmp_path / "f.bin", tmp_path / "l.bin"
+    f.tofile(path)
+    lens.tofile(lpath)
+    arg = "-" if not verify else hx(pb.dict_to_protobuf(pb.L4ChecksumArg, {"verify": True}))
+    out = run(drive, ["create L4Checksum " + arg, "connect 0", "connect 1",
+                      "frames %s 2048 %d" % (path, n), "lens %s" % lpath,
+                      "process 0 0"])
+    got = [x for x in out if x.startswith("out")][0].split()[1:]
+    assert got == ["-" if int(w) == 0xFFFF else str(int(w)) for w in l4w]
+    data = np.stack([np.frombuffer(bytes.fromhex(x.split()[2]), np.uint8)
+                     for x in out if x.startswith("data")])
+    assert (data == ref[:, :64]).all()
+    if verify:
+        assert "0" in got and "1" in got
+
+
 # ---- attr_name fields through the plugins: bessctl/module_tests
 # exact_match.py:88-123 and wildcard_match.py:104-139 restated (scapy and
 # SetMetadata are absent: the shell writes each packet's metadata area, as

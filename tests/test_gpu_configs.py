@@ -92,6 +92,33 @@ def test_c3_full_size():
     assert (d.cpu().numpy() == cf.reshape(-1)).all()
 
 
+# ---------------------------------------------- ExactMatch on 1500 B packets
+def test_em_1500b_full_size():
+    """the north star's 1500 B match point (bench EM_1500B): C2's 1K rules
+    over the bench's 4 M 1500 B packets (1496 B frames in 2 KB slots, the
+    payload random here), every gate against the oracle run on the whole
+    frames"""
+    n = 1 << 22
+    keys, gates, hdr = P.em_workload(1000, n, seed=0x5EED, stride=64,
+                                     frame_len=1496, pkt_seed=0x1500)
+    d = torch.randint(0, 256, (n, 2048), dtype=torch.uint8, device="cuda")
+    d[:, :64] = torch.from_numpy(hdr).cuda()
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
+    t.classify(d.view(-1), 2048, n, 8192, d_g)
+    got = d_g.cpu().numpy().view(np.uint16)
+    # the oracle over whole 2 KB slots on a sample, over the header lines
+    # (all it reads at these field offsets) for the rest
+    k = 1 << 16
+    full = d[:k].cpu().numpy()
+    assert (full[:, :64] == hdr[:k]).all()
+    assert (got[:k] == oracle_em_gates(keys, gates, full, 2048)).all()
+    want = oracle_em_gates(keys, gates, hdr, 64)
+    assert (got == want).all()
+    assert 0.4 < (want != 8192).mean() < 0.6
+
+
 # ------------------------------------------------------------------- C5
 @pytest.mark.parametrize("flags", [0, LB.BG_PATH_NO_SLAB])
 def test_c5_1m_rules_single_image(c5, flags):
