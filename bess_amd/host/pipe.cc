@@ -112,6 +112,9 @@ struct bg_pipe {
            st_wait_ns = 0;
   uint64_t st_submit_tsc = 0, st_poll_tsc = 0;  // cycles inside submit / poll
   uint64_t st_lat_tsc = 0, st_lat_max = 0;      // slot launch -> seen done
+  // ns of a launch by HIP call: H2D copy, module kernel, gate D2H, header
+  // lines D2H, completion write (launch mode)
+  uint64_t st_call_ns[5] = {0, 0, 0, 0, 0};
   // One worker owns a pipe; the lock is for the module's control path
   // (PipeFlushLocked) and a RunTask on another worker (never contended on
   // the datapath).
@@ -238,21 +241,32 @@ static int launch_slot(bg_pipe *p) {
   }
   int rc = bg::set_device(p->device);
   if (rc) return rc;
+  uint64_t t1 = mono_ns(), t2;
+  auto lap = [&](int k) {
+    t2 = mono_ns();
+    p->st_call_ns[k] += t2 - t1;
+    t1 = t2;
+  };
   HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
+  lap(0);
   bg_ctx c = s.ctx;
   c.device = (int16_t)p->device;
   int r = p->mod->m->ProcessDeviceWindow(c, s.d_in, p->w, n, p->lo, s.d_g, s.st);
   if (r < 0) return r;
+  lap(1);
   HIP_TRY(hipMemcpyAsync(s.h_g, s.d_g, n * 2, hipMemcpyDeviceToHost, s.st));
+  lap(2);
   if (p->writeback) {
     const size_t line = std::min(p->w, kWriteback);
     HIP_TRY(hipMemcpy2DAsync(s.h_wb, line, s.d_in, p->w, line, n,
                              hipMemcpyDeviceToHost, s.st));
   }
+  lap(3);
   // completion lands in host memory after the D2H copies: poll reads one
   // word and makes no HIP call
   s.seq = ++p->launched;
   HIP_TRY(hipStreamWriteValue64(s.st, s.d_done, s.seq, 0));
+  lap(4);
   p->st_launch_ns += mono_ns() - t0;
   s.inflight = true;
   p->inflight++;
@@ -620,11 +634,12 @@ long bg_pipe_poll(bg_pipe *p, int wait, void **cookies, uint16_t *gates,
 size_t bg_pipe_pending(const bg_pipe *p) { return p->pending; }
 
 int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n) {
-  const uint64_t v[11] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
+  const uint64_t v[16] = {p->st_submits, p->st_pkts, p->launched, p->st_launch_ns,
                           p->st_full_ns, p->st_wait_ns, (uint64_t)p->batch,
                           p->st_submit_tsc, p->st_poll_tsc, p->st_lat_tsc,
-                          p->st_lat_max};
-  for (int i = 0; i < n && i < 11; i++) out[i] = v[i];
+                          p->st_lat_max, p->st_call_ns[0], p->st_call_ns[1],
+                          p->st_call_ns[2], p->st_call_ns[3], p->st_call_ns[4]};
+  for (int i = 0; i < n && i < 16; i++) out[i] = v[i];
   return 0;
 }
 

@@ -617,7 +617,9 @@ size_t bg_pipe_pending(const bg_pipe *p);
 /* counters (first n of): submits, packets, slot launches, ns spent in
  * launches (HIP calls), ns submits waited for a free slot, ns polls
  * waited, the slot size, TSC cycles inside submit, inside poll, TSC cycles
- * from slot launches to their completion being seen (sum, max) */
+ * from slot launches to their completion being seen (sum, max), and the
+ * launch ns by HIP call (launch mode): H2D copy, module kernel, gates D2H,
+ * header lines D2H, completion write */
 int bg_pipe_stats(const bg_pipe *p, uint64_t *out, int n);
 /* A worker loop (Source -> module -> Sink): n packets submitted in bursts of
  * `burst`, completions polled after each submit; ogates[i] = packet i's

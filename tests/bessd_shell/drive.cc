@@ -547,16 +547,19 @@ static int run() {
         printf("pool %zu %zu %llu\n", ppool->Size(), ppool->Capacity(),
                (unsigned long long)source_waits.load());
       if (GpuModule *g = dynamic_cast<GpuModule *>(m)) {
-        uint64_t st[11];
-        if (g->PipeStats(0, st, 11) == 0)
+        uint64_t st[16];
+        if (g->PipeStats(0, st, 16) == 0)
           printf("stats submits %llu pkts %llu launches %llu launch_ms %.3f full_ms %.3f "
                  "wait_ms %.3f batch %llu submit_cyc_per_pkt %.1f poll_cyc_per_pkt %.1f "
-                 "slot_latency_us avg %.1f max %.1f\n",
+                 "slot_latency_us avg %.1f max %.1f call_ms h2d %.3f kernel %.3f "
+                 "gates %.3f lines %.3f done %.3f\n",
                  (unsigned long long)st[0], (unsigned long long)st[1],
                  (unsigned long long)st[2], st[3] * 1e-6, st[4] * 1e-6, st[5] * 1e-6,
                  (unsigned long long)st[6], st[7] / (double)(st[1] ? st[1] : 1),
                  st[8] / (double)(st[1] ? st[1] : 1),
-                 st[9] / (double)(st[2] ? st[2] : 1) / 3300.0, st[10] / 3300.0);
+                 st[9] / (double)(st[2] ? st[2] : 1) / 3300.0, st[10] / 3300.0,
+                 st[11] * 1e-6, st[12] * 1e-6, st[13] * 1e-6, st[14] * 1e-6,
+                 st[15] * 1e-6);
       }
       if (verify) {
         bool ok = true;
