@@ -1413,13 +1413,14 @@ def run_wm(args, dev, torch):
                 t.classify(slab, stride, n, 8192, gates)
             return timer.stop_ms() / args.steps
 
-    def aot_check(slab, stride, gates, g_jit):
-        """the ahead-of-time kernel: same gates, its time"""
-        with LB.kernel_paths(LB.BG_PATH_WM_NO_JIT):
+    def aot_check(slab, stride, gates, g_jit, flags=LB.BG_PATH_WM_NO_JIT):
+        """another form of the kernel (default: the ahead-of-time one): same
+        gates, its time"""
+        with LB.kernel_paths(flags):
             t.classify(slab, stride, n, 8192, gates)
             torch.cuda.synchronize()
         same = bool((gates.cpu().numpy().view(np.uint16)[:n0] == g_jit).all())
-        return same, timed(slab, stride, gates, LB.BG_PATH_WM_NO_JIT)
+        return same, timed(slab, stride, gates, flags)
 
     def check(gates_t):
         got = gates_t.cpu().numpy().view(np.uint16)
@@ -1428,6 +1429,8 @@ def run_wm(args, dev, torch):
 
     nan = float("nan")
     parity, ms2k, g2k, aot2k, aot_h = True, nan, None, nan, nan
+    # the form in which every wave loads its own windows (no producer waves)
+    ns2k, ns_h = nan, nan
     if args.wm_layout != "slab":  # the frames in 2 KB slots
         d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
         d = d0.repeat(rep)
@@ -1438,7 +1441,8 @@ def run_wm(args, dev, torch):
         parity, g2k = check(dg)
         ms2k = timed(d, 2048, dg)
         same2k, aot2k = aot_check(d, 2048, dg, g2k)
-        parity = parity and same2k
+        same2s, ns2k = aot_check(d, 2048, dg, g2k, LB.BG_PATH_WM_NO_STREAM)
+        parity = parity and same2k and same2s
         del d, dg
     gbs2k = EM_BYTES_PER_PKT * n / (ms2k * 1e-3) / 1e9
     # The same packets' header lines in a dense 64 B slab: the layout the
@@ -1457,7 +1461,8 @@ def run_wm(args, dev, torch):
             parity_h = parity_h and bool((gh == g2k).all())
         ms = timed(hs, 64, dgh)
         same_h, aot_h = aot_check(hs, 64, dgh, gh)
-        parity_h = parity_h and same_h
+        same_s, ns_h = aot_check(hs, 64, dgh, gh, LB.BG_PATH_WM_NO_STREAM)
+        parity_h = parity_h and same_h and same_s
         del hs, dgh
     mpps = n / (ms * 1e-3) / 1e6
     gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
@@ -1477,6 +1482,9 @@ def run_wm(args, dev, torch):
            "ahead_of_time": {"ms_per_step": round(aot_h, 4),
                              "slots_2k_ms_per_step": round(aot2k, 4),
                              "same_gates": bool(parity and parity_h)},
+           "no_stream": {"what": "every wave loads its own windows (BG_PATH_WM_NO_STREAM)",
+                         "ms_per_step": round(ns_h, 4),
+                         "slots_2k_ms_per_step": round(ns2k, 4)},
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),

@@ -279,6 +279,10 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
   for (auto &m : members) maxc = std::max(maxc, m.size());
   TableLayout L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load, vik);
   L.probe = probe;
+  // WildcardMatch (probe 1): the bucket count the load asks for, not the
+  // next power of two (wm_probe takes any count)
+  if (probe)
+    relayout(L, std::max<uint32_t>(2, (uint32_t)((double)maxc / (kSlots * max_load)) + 1));
   for (int attempt = 0; attempt < 8; attempt++) {
     img->assign((size_t)L.part_bytes * nparts, 0);
     bool ok = true;
@@ -298,7 +302,7 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
       return 0;
     }
     if (L.nbp >= kMaxBucketsPerPart) break;
-    relayout(L, L.nbp * 2);
+    relayout(L, probe ? L.nbp + L.nbp / 8 + 1 : L.nbp * 2);
   }
   return fail(ENOSPC, "flow table build failed (%zu entries)", n);
 }
@@ -1319,7 +1323,10 @@ static int wm_build_host(bg_wm *wm, bool no_tags) {
       wm_pick_direct(wm);
       wm_entries(wm, &keys, &vals, &hashes);
     }
-    for (double load : {0.75, 0.93}) {
+    // the highest load that builds: the fewest tag words, the most LDS left
+    // beside them (each packet checks the same 2 buckets per tuple; a fuller
+    // bucket only adds fingerprint collisions, ~3 % per tuple at 0.95)
+    for (double load : {0.95, 0.9, 0.75}) {
       std::vector<uint8_t> img2;
       TableLayout L2;
       if (build_image(wm->kw, 8, 1, keys, vals, hashes, &img2, &L2, load, false,

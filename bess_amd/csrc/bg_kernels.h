@@ -129,7 +129,8 @@ struct WmArgs {
   uint32_t dtu[kMaxDirect];    // tuple index
   uint32_t dspec[kMaxDirect];  // key byte a | byte b << 8 | mask a << 16 | mask b << 24
   uint64_t doff[kMaxDirect];   // the table's byte offset in the image
-  uint32_t ab_phase, pad2;  // A/B build only: stop after a phase (timing)
+  uint32_t ab_phase;  // A/B build only: stop after a phase (timing)
+  uint32_t ring_slots;  // the streamed form's LDS ring (wm_stream_slots)
 };
 
 // WildcardMatch tag-word kernels (bg_wm_body.h): one 1024-thread workgroup
@@ -142,6 +143,30 @@ constexpr uint32_t kWmWaveLds = 64 * 8 + kWmQueue * 4;
 BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
   return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 +
          (uint64_t)kWmWaves * kWmWaveLds;
+}
+// the streamed form (bg_wm_body.h wm_tags_stream_body): producer waves load
+// the pair-shaped windows (32 B per packet) into an LDS ring of tiles that
+// the consumer waves look up; ring slots: 64 x 32 B + two flag words
+constexpr int kStreamProducers = 1;
+constexpr int kStreamDepth = 16;  // tiles in flight per producer (vmcnt <= 63)
+constexpr uint32_t kStreamTileBytes = 64 * 32;
+constexpr uint32_t kStreamMaxSlots = 64;
+constexpr uint32_t kLdsMax = 160 * 1024;  // gfx950 LDS per workgroup
+BG_HD uint64_t wm_stream_fixed_lds(uint32_t nbp, uint32_t kw) {
+  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 +
+         (uint64_t)(kWmWaves - kStreamProducers) * kWmWaveLds;
+}
+// ring slots that fit beside the tag words (0: too few for the producers'
+// depth, the streamed form does not apply)
+BG_HD uint32_t wm_stream_slots(uint32_t nbp, uint32_t kw) {
+  const uint64_t fixed = wm_stream_fixed_lds(nbp, kw);
+  if (fixed >= kLdsMax) return 0;
+  uint64_t r = (kLdsMax - fixed) / (kStreamTileBytes + 8);
+  if (r > kStreamMaxSlots) r = kStreamMaxSlots;
+  return r > (uint64_t)(kStreamProducers * kStreamDepth + 4) ? (uint32_t)r : 0u;
+}
+BG_HD uint64_t wm_stream_lds_bytes(uint32_t nbp, uint32_t kw, uint32_t slots) {
+  return wm_stream_fixed_lds(nbp, kw) + (uint64_t)slots * (kStreamTileBytes + 8);
 }
 
 struct CkArgs {

@@ -735,8 +735,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
                                                   const uint64_t (&k)[KW],
                                                   const uint32_t *filt) {
   const kconst_u64 tm = tuple_masks(a);
-  const uint32_t lg = 31 - __builtin_clz(a.t.nbp);
-  uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples];
+    uint32_t b1[kMaxTuples], b2[kMaxTuples], tg[kMaxTuples];
   uint32_t w1[kMaxTuples], w2[kMaxTuples];
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(tab);
   uint64_t dv[kMaxDirect];  // direct tuples' values (global, issued first)
@@ -759,7 +758,7 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
         pass = (filt[q.word] & q.bits) == q.bits;
       }
       if (pass) {
-        const Probe p = wm_probe(h, lg);
+        const Probe p = wm_probe(h, a.t.nbp);
         b1[tu] = p.b1;
         b2[tu] = p.b2;
         tg[tu] = p.tag;

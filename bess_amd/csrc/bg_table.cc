@@ -50,9 +50,8 @@ bool build_partition(const TableLayout &L, uint32_t part, size_t n,
   if (n > nslots) return false;
   std::vector<int32_t> occ(nslots, -1);
   std::vector<Probe> pr(n);
-  const uint32_t lg = log2_pow2(L.nbp);
   for (size_t i = 0; i < n; i++) {
-    pr[i] = L.probe ? wm_probe((uint32_t)hashes[i], lg)
+    pr[i] = L.probe ? wm_probe((uint32_t)hashes[i], L.nbp)
                     : split_hash(hashes[i], L.nparts, L.nbp);
     if (pr[i].part != part) return false;  // caller filtered wrongly
   }

@@ -51,7 +51,7 @@ struct TableLayout {
   uint32_t kw;         // key words (total_key_size / 8), 1..8
   uint32_t val_bytes;  // 2 (EM gate) or 8 (WM {prio, gate, tuple})
   uint32_t nparts;     // power of 2, <= 8
-  uint32_t nbp;        // buckets per partition, power of 2
+  uint32_t nbp;        // buckets per partition, power of 2 (probe 0)
   uint64_t part_bytes; // bytes per partition image
   uint64_t keys_off;   // byte offset of keys within a partition
   uint64_t vals_off;   // byte offset of values within a partition
@@ -61,7 +61,8 @@ struct TableLayout {
   // P4), so one key read also yields the value; no value array
   uint32_t vik;
   // 0: split_hash of a 64-bit hash_words value (ExactMatch, NAT);
-  // 1: wm_probe of a 32-bit wm_hash value (WildcardMatch, one partition)
+  // 1: wm_probe of a 32-bit wm_hash value (WildcardMatch, one partition;
+  // nbp any number >= 2)
   uint32_t probe;
 };
 
@@ -137,25 +138,31 @@ BG_HD uint32_t wm_hash(const uint32_t *kd, uint32_t cover, int ndw, uint32_t see
   return h;
 }
 
-// The second bucket's offset from the first: an odd number from the
-// fingerprint alone (partial-key cuckoo hashing), so a (first bucket,
-// fingerprint) pair names both buckets -- the tag-word kernel queues one
-// entry per (packet, tuple) and its check derives the other bucket.
-BG_HD uint32_t wm_alt(uint32_t tag, uint32_t lg) {
-  return lg ? (((tag * 0x5BD1E995u) >> (32 - lg)) | 1u) : 0u;
+// WildcardMatch tables take any bucket count nbp >= 2 (not only powers of
+// two: a table whose tag words live in LDS is sized to its entries, C4's
+// 75 K hashed entries take 79 KB of tag words at load 0.95 where the next
+// power of two took 128 KB). x in [0, 2^32) scaled to [0, n): the high half
+// of a 32 x 32 product (one v_mul_hi_u32).
+BG_HD uint32_t wm_range(uint32_t x, uint32_t n) { return (uint32_t)(((uint64_t)x * n) >> 32); }
+
+// The second bucket from the first and the fingerprint alone (partial-key
+// cuckoo hashing), so a (first bucket, fingerprint) pair names both buckets
+// -- the tag-word kernel queues one entry per (packet, tuple) and its check
+// derives the other bucket: b1 plus an offset in [1, nbp) drawn from the
+// fingerprint, modulo nbp (never b1).
+BG_HD uint32_t wm_b2(uint32_t b1, uint32_t tag, uint32_t nbp) {
+  const uint32_t b = b1 + 1u + wm_range(tag * 0x5BD1E995u, nbp - 1u);
+  return b >= nbp ? b - nbp : b;
 }
-// first bucket from the low bits, fingerprint from the top byte, second
-// bucket the first XOR the fingerprint's odd offset (wm_alt)
-// (nbp = 2^lg, lg >= 1)
-BG_HD Probe wm_probe(uint32_t h, uint32_t lg) {
+// fingerprint from the top byte, first bucket from the low 24 bits scaled
+// to [0, nbp), second bucket wm_b2 (nbp >= 2)
+BG_HD Probe wm_probe(uint32_t h, uint32_t nbp) {
   Probe p;
-  const uint32_t m = (1u << lg) - 1;
   p.part = 0;
-  p.b1 = h & m;
+  p.b1 = wm_range(h << 8, nbp);
   const uint32_t t = h >> 24;
   p.tag = t ? t : 1u;
-  // b1 XOR an odd offset: never b1 (lg > 0), no compare-and-fix
-  p.b2 = p.b1 ^ wm_alt(p.tag, lg);
+  p.b2 = wm_b2(p.b1, p.tag, nbp);
   return p;
 }
 

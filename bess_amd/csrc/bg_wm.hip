@@ -5,6 +5,7 @@
 // same body per rule-set shape with the tuple data as constants.
 #include <hip/hip_runtime.h>
 
+#include "bg_launch.h"
 #include "bg_wm_body.h"
 
 namespace bg {
@@ -13,6 +14,23 @@ namespace {
 template <int KW, int NCH, int PAIR>
 __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   wm_tags_body<WmRuntimeSpec, KW, NCH, PAIR>(a);
+}
+
+template <int KW>
+__global__ __launch_bounds__(kWmBlock) void wm_stream_kernel(WmArgs a) {
+  wm_tags_stream_body<WmRuntimeSpec, KW>(a);
+}
+
+template <int KW>
+hipError_t launch_stream(WmArgs a, uint32_t slots, int num_cus, hipStream_t s) {
+  a.ring_slots = slots;
+  const uint64_t ntiles = (a.n + 63) / 64;
+  uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
+  if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((wm_stream_kernel<KW>), dim3((unsigned)blocks), dim3(kWmBlock),
+                     wm_stream_lds_bytes(a.t.nbp, KW, slots), s, a);
+  return hipGetLastError();
 }
 
 template <int KW, int NCH, int PAIR>
@@ -40,9 +58,13 @@ hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   // (both chunks inside the slot: no read past a staged row or the slab)
   const bool pair = n2 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
                     a.fp.win_lo + 32 <= a.stride && a.stride <= 65536;
+  // the streamed form when its ring fits beside the tag words (bg_wm_body.h)
+  const uint32_t slots = pair && !(path_flags() & kPathWmNoStream)
+                             ? wm_stream_slots(a.t.nbp, a.t.kw) : 0u;
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
-    return pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                     \
+    return slots ? launch_stream<KW>(a, slots, num_cus, s)                 \
+           : pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                   \
                 : n2 ? launch_tags<KW, 2, 0>(a, num_cus, s)                \
                      : launch_tags<KW, 4, 0>(a, num_cus, s);
   BG_WT(1) BG_WT(2) BG_WT(4) BG_WT(8)

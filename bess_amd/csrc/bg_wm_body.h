@@ -29,7 +29,7 @@
 //   3. every (packet, tuple) whose buckets hold the packet's fingerprint
 //      goes into a per-wave LDS queue as (first bucket, lane, tuple,
 //      fingerprint) -- the second bucket follows from the first and the
-//      fingerprint (wm_alt) -- at a scalar base + mbcnt of the tuple's
+//      fingerprint (wm_b2) -- at a scalar base + mbcnt of the tuple's
 //      match mask, so the key checks run on dense lanes instead of on
 //      whichever lanes matched;
 //   4. the queue (<= 256 entries; more go in further rounds) is checked
@@ -145,12 +145,12 @@ __device__ __forceinline__ uint32_t bucket_matches(const uint32_t *tags, uint32_
 }
 
 // Entry e = (packet, tuple, first bucket b1, fingerprint); its second bucket
-// is b1 ^ wm_alt(fingerprint). Candidate slots: the matches of b1 (z1),
-// then those of b2 (z2); the next candidate's slot index.
-__device__ __forceinline__ uint32_t next_slot(uint32_t e, uint32_t lg, uint32_t z1,
+// is wm_b2(b1, fingerprint). Candidate slots: the matches of b1 (z1), then
+// those of b2 (z2); the next candidate's slot index.
+__device__ __forceinline__ uint32_t next_slot(uint32_t e, uint32_t nbp, uint32_t z1,
                                               uint32_t z2) {
   const uint32_t b1 = e & 0x7FFFu;
-  const uint32_t b = z1 ? b1 : b1 ^ wm_alt(e >> 24, lg);
+  const uint32_t b = z1 ? b1 : wm_b2(b1, e >> 24, nbp);
   return b * kSlots + (__builtin_ctz(z1 ? z1 : z2) >> 3);
 }
 
@@ -166,7 +166,7 @@ template <int KW, int R>
 __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags,
                                            const uint64_t *mlds, uint64_t *best,
                                            const uint32_t *q, uint32_t m, int lane,
-                                           uint32_t lg, const uint64_t (&k)[KW]) {
+                                           uint32_t nbp, const uint64_t (&k)[KW]) {
   const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
   const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
   uint32_t e[R], z1[R], z2[R];
@@ -184,8 +184,8 @@ __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags
       if (i < m) {
         const uint32_t b1 = e[r] & 0x7FFFu;
         z1[r] = bucket_matches(tags, b1, e[r]);
-        z2[r] = bucket_matches(tags, b1 ^ wm_alt(e[r] >> 24, lg), e[r]);
-        const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
+        z2[r] = bucket_matches(tags, wm_b2(b1, e[r] >> 24, nbp), e[r]);
+        const uint32_t slot = next_slot(e[r], nbp, z1[r], z2[r]);
 #ifdef BG_AB  // phase timing: checks without their L2 loads
         if (a.ab_phase == 3) continue;
 #endif
@@ -217,7 +217,7 @@ __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags
 #pragma unroll
     for (int r = 0; r < R; r++) {
       while (z1[r] | z2[r]) {
-        const uint32_t slot = next_slot(e[r], lg, z1[r], z2[r]);
+        const uint32_t slot = next_slot(e[r], nbp, z1[r], z2[r]);
         if (z1[r])
           z1[r] &= z1[r] - 1;
         else
@@ -239,11 +239,11 @@ template <int KW>
 __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
                                          const uint64_t *mlds, uint64_t *best,
                                          const uint32_t *q, uint32_t m, int lane,
-                                         uint32_t lg, const uint64_t (&k)[KW]) {
+                                         uint32_t nbp, const uint64_t (&k)[KW]) {
   if (m <= 64)  // wave-uniform
-    wm_check_r<KW, 1>(a, tags, mlds, best, q, m, lane, lg, k);
+    wm_check_r<KW, 1>(a, tags, mlds, best, q, m, lane, nbp, k);
   else
-    wm_check_r<KW, kPerLane>(a, tags, mlds, best, q, m, lane, lg, k);
+    wm_check_r<KW, kPerLane>(a, tags, mlds, best, q, m, lane, nbp, k);
 }
 
 // bit 7 of each byte of x that is zero, OR-ed over two words (the SWAR
@@ -299,21 +299,127 @@ __device__ __forceinline__ void pair_window(const uint32_t (&r)[8], int lane,
   w[9] = 0;
 }
 
+// One tile's lookups (lane = packet idx, its header window w): steps 1-5 of
+// the file comment. `prefetch` runs right after the direct tuples' reads are
+// issued (wm_tags_body issues the next tile's window there: vector loads
+// retire in order, so the direct values, consumed in this tile, must not be
+// younger than a prefetch the next tile consumes).
+template <class Spec, int KW, int NCH, class Prefetch>
+__device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
+                                        const uint64_t *mlds, uint64_t *best, uint32_t *q,
+                                        uint32_t nbp, int lane, uint64_t idx, bool live,
+                                        const uint32_t (&w)[NCH * 4 + 2], Prefetch prefetch) {
+  uint64_t k[KW];
+  Spec::template key<KW, NCH>(w, a, k);
+  // direct tuples: one value read each, issued now, folded at the end
+  const uint32_t ndir = Spec::ndirect(a);
+  uint64_t dv[kMaxDirect];
+#pragma unroll
+  for (int d = 0; d < kMaxDirect; d++) {
+    dv[d] = ~0ull;
+    if ((uint32_t)d < ndir && live) {
+      const uint64_t off =
+          reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
+              tuple_words(a, offsetof(WmArgs, doff)))[d];
+      dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)
+          [direct_index_k<KW>(k, Spec::dspec(a, d))];
+    }
+  }
+  prefetch();
+#ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
+  if (a.ab_phase == 1) {
+    if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
+    return;
+  }
+#endif
+  const uint32_t hmask = Spec::hashed(a);
+
+  // A. every hashed tuple's probe: both tag words from LDS (all reads in
+  // flight before any is used); ent[tu] is the packet's queue entry when
+  // a bucket holds its fingerprint, else 0 (an entry is never 0: its
+  // fingerprint is not)
+  uint32_t ent[kMaxTuples];
+#pragma unroll
+  for (int tu = 0; tu < kMaxTuples; tu++) {
+    ent[tu] = 0;
+    if ((hmask >> tu) & 1u) {  // wave-uniform (a scalar test, or a constant)
+      const Probe p = wm_probe(Spec::template hash<KW>(k, tu, a), nbp);
+      const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
+      const uint32_t zz = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
+      ent[tu] = zz ? p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24)
+                   : 0u;
+    }
+  }
+  // B/C. one queue entry per (packet, tuple) with a fingerprint match,
+  // tuple-major: the wave's mask of matching lanes gives each lane its
+  // position (a scalar base + mbcnt) and the base advances by the mask's
+  // popcount. Usually the tile's entries fit one queue; more go in
+  // further rounds of kQueue.
+  const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
+  uint64_t mk[kMaxTuples];
+  uint32_t total = 0;
+#pragma unroll
+  for (int tu = 0; tu < kMaxTuples; tu++) {
+    mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
+    total += (uint32_t)__popcll(mk[tu]);
+  }
+  for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
+    uint32_t base = 0;
+#pragma unroll
+    for (int tu = 0; tu < kMaxTuples; tu++) {
+      const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
+      const bool mine = live && ent[tu] != 0;
+      if (total <= kQueue) {  // wave-uniform: one round, no window test
+        if (mine) q[pos] = ent[tu];
+      } else if (mine && pos - r0 < kQueue) {
+        q[pos - r0] = ent[tu];
+      }
+      base += (uint32_t)__popcll(mk[tu]);
+    }
+#ifdef BG_AB  // phase timing: + hashes, tag reads and the queue writes
+    if (a.ab_phase == 2) break;
+#endif
+    lds_fence();
+    const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
+    wm_check<KW>(a, tags, mlds, best, q, m, lane, nbp, k);
+    lds_fence();  // the queue is rewritten by the next round
+  }
+  lds_fence();
+  uint64_t bb = best[lane];
+  best[lane] = 0;
+#pragma unroll
+  for (int d = 0; d < kMaxDirect; d++) {
+    const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFu;
+    if ((uint32_t)(dv[d] >> 48) == tu) {  // same order as wm_fold
+      const uint64_t comb = ((uint64_t)((uint32_t)dv[d] ^ 0x80000000u) << 32) |
+                            (1u << 19) | (tu << 16) | ((uint32_t)(dv[d] >> 32) & 0xFFFFu);
+      bb = comb > bb ? comb : bb;
+    }
+  }
+  if (live) a.gates[idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
+}
+
+// stage the tag words and the tuple masks (every thread of the workgroup);
+// returns the masks' LDS address
+template <int KW>
+__device__ __forceinline__ uint64_t *wm_stage_tags(const WmArgs &a, uint8_t *lds,
+                                                   uint32_t tag_bytes) {
+  const uint4 *src = reinterpret_cast<const uint4 *>(a.t.base);
+  uint4 *dst = reinterpret_cast<uint4 *>(lds);
+  for (uint32_t i = threadIdx.x; i < tag_bytes / 16; i += kWmBlock) dst[i] = src[i];
+  uint64_t *mlds = reinterpret_cast<uint64_t *>(lds + tag_bytes);
+  const kconst_u64 tm = tuple_masks(a);
+  if (threadIdx.x < kMaxTuples * KW)
+    mlds[threadIdx.x] = tm[(threadIdx.x / KW) * kMaxKeyWords + threadIdx.x % KW];
+  return mlds;
+}
+
 template <class Spec, int KW, int NCH, int PAIR>
 __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
-  {  // stage the tag words
-    const uint4 *src = reinterpret_cast<const uint4 *>(a.t.base);
-    uint4 *dst = reinterpret_cast<uint4 *>(lds);
-    for (uint32_t i = threadIdx.x; i < tag_bytes / 16; i += kWmBlock) dst[i] = src[i];
-  }
-  uint64_t *mlds = reinterpret_cast<uint64_t *>(lds + tag_bytes);
-  {
-    const kconst_u64 tm = tuple_masks(a);
-    if (threadIdx.x < kMaxTuples * KW)
-      mlds[threadIdx.x] = tm[(threadIdx.x / KW) * kMaxKeyWords + threadIdx.x % KW];
-  }
+  const uint64_t *mlds = wm_stage_tags<KW>(a, lds, tag_bytes);
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + wid * kWaveLds;
@@ -322,7 +428,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   best[lane] = 0;
   __syncthreads();
 
-  const uint32_t lg = 31 - __builtin_clz(a.t.nbp);
+  const uint32_t nbp = a.t.nbp;
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
@@ -343,106 +449,146 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
 #pragma unroll
       for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
     }
-    uint64_t k[KW];
-    Spec::template key<KW, NCH>(w, a, k);
-    // direct tuples: one value read each, issued now, folded at the end
-    const uint32_t ndir = Spec::ndirect(a);
-    uint64_t dv[kMaxDirect];
-#pragma unroll
-    for (int d = 0; d < kMaxDirect; d++) {
-      dv[d] = ~0ull;
-      if ((uint32_t)d < ndir && live) {
-        const uint64_t off =
-            reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
-                tuple_words(a, offsetof(WmArgs, doff)))[d];
-        dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)
-            [direct_index_k<KW>(k, Spec::dspec(a, d))];
+    // the next tile's header window
+    wm_tile<Spec, KW, NCH>(a, tags, mlds, best, q, nbp, lane, idx, live, w, [&]() {
+      if constexpr (PAIR) {
+        if (t + nw < ntiles)
+          load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);
+      } else {
+        const uint64_t nidx = (t + nw) * 64 + lane;
+        if (t + nw < ntiles && nidx < a.n)
+          load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
       }
-    }
-    // the next tile's header window, issued AFTER the direct reads: vector
-    // loads retire in order (vmcnt), so waiting for a load also waits for
-    // every older one -- the direct values, consumed in this tile, must not
-    // be younger than the prefetch the next tile consumes
-    if constexpr (PAIR) {
-      if (t + nw < ntiles)
-        load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);
-    } else {
-      const uint64_t nidx = (t + nw) * 64 + lane;
-      if (t + nw < ntiles && nidx < a.n)
-        load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
-    }
-#ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
-    if (a.ab_phase == 1) {
-      if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
-      continue;
-    }
-#endif
-    const uint32_t hmask = Spec::hashed(a);
+    });
+  }
+}
 
-    // A. every hashed tuple's probe: both tag words from LDS (all reads in
-    // flight before any is used); ent[tu] is the packet's queue entry when
-    // a bucket holds its fingerprint, else 0 (an entry is never 0: its
-    // fingerprint is not)
-    uint32_t ent[kMaxTuples];
-#pragma unroll
-    for (int tu = 0; tu < kMaxTuples; tu++) {
-      ent[tu] = 0;
-      if ((hmask >> tu) & 1u) {  // wave-uniform (a scalar test, or a constant)
-        const Probe p = wm_probe(Spec::template hash<KW>(k, tu, a), lg);
-        const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);  // tag in every byte
-        const uint32_t zz = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
-        ent[tu] = zz ? p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24)
-                     : 0u;
+// ---------------------------------------------------------------------------
+// Streamed form (pair-shaped windows: two 16-byte chunks inside the slot's
+// first 64 bytes). The header stream is decoupled from the lookups: in the
+// form above every wave prefetches one tile, and its key / value loads from
+// L2 retire behind that prefetch (vector loads retire in order), so a wave
+// has one tile of windows in flight for part of its time. Here
+// kStreamProducers waves per workgroup only load windows -- straight into
+// an LDS ring of `a.ring_slots` tiles (global_load_lds), kStreamDepth tiles
+// in flight each, waited for with an explicit vmcnt -- and the other waves
+// (consumers) take tiles from the ring in order and do the lookups, their
+// own loads being only the L2 checks.
+//
+// Ring protocol: the workgroup's tiles j = 0, 1, ... (global tile blockIdx.x
+// + j * gridDim.x) go through ring slot j % R. ready[s] = j + 1 once tile j's
+// windows are in slot s; done[s] = j + 1 once its consumer has read them.
+// Producer p loads tiles p, p + P, ...; it loads tile j only when the slot's
+// previous tile j - R is done, and publishes a tile once kStreamDepth - 1
+// younger ones are issued (or at its end). Consumer c takes tiles c, c + C,
+// ... Every wait is for a smaller tile index, and R > P * kStreamDepth: the
+// smallest unfinished tile can always advance (its producer's pending waits
+// are for tiles below it, all done), so the workgroup drains and every wave
+// leaves after its last tile.
+// ---------------------------------------------------------------------------
+// ring flags: a volatile LDS word (an LDS-typed pointer: a generic volatile
+// access would be a flat instruction, which counts in vmcnt and would make
+// the producer wait for its loads); the data written before a publish has
+// landed first (lgkmcnt), and a wave's LDS operations execute in order
+typedef volatile __attribute__((address_space(3))) uint32_t lds_flag_t;
+__device__ __forceinline__ void lds_wait_eq(const uint32_t *p, uint32_t v) {
+  lds_flag_t *f = (lds_flag_t *)(p);
+  while (*f != v) __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
+  lds_fence();
+  *(lds_flag_t *)(p) = v;
+}
+
+// the pair-shaped windows of tile p0 (slots p0 .. p0 + 63; indices past
+// the slab clamped to n - 1) straight into LDS at `dst` (global_load_lds:
+// lane l's 16 bytes land at dst + 16 l, so slot m's window is at dst + 32 m):
+// no registers, and the producer alone decides when to wait for them
+__device__ __forceinline__ void dma_pair(const uint8_t *__restrict__ frames, uint64_t n,
+                                         uint64_t p0, int lane, uint32_t win_lo,
+                                         uint64_t stride, uint8_t *dst) {
+  uint64_t s0 = p0 + (uint32_t)(lane >> 1), s1 = s0 + 32;
+  s0 = s0 < n ? s0 : n - 1;
+  s1 = s1 < n ? s1 : n - 1;
+  const uint32_t c = (uint32_t)(lane & 1) * 16 + win_lo;
+  typedef const __attribute__((address_space(1))) void *gptr;
+  typedef __attribute__((address_space(3))) void *lptr;
+  __builtin_amdgcn_global_load_lds((gptr)(frames + s0 * stride + c), (lptr)dst, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((gptr)(frames + s1 * stride + c), (lptr)(dst + 1024), 16,
+                                   0, 0);
+}
+
+template <class Spec, int KW>
+__device__ __forceinline__ void wm_tags_stream_body(const WmArgs &a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  constexpr int P = kStreamProducers, C = kWaves - kStreamProducers, D = kStreamDepth;
+  const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
+  const uint64_t *mlds = wm_stage_tags<KW>(a, lds, tag_bytes);
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
+  // (the wave index in a scalar register: the role and tile branches below
+  // are uniform)
+  const int lane = threadIdx.x & 63,
+            wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint8_t *waves = lds + tag_bytes + kMaxTuples * KW * 8;
+  const uint32_t R = a.ring_slots;
+  uint8_t *ring = waves + C * kWaveLds;
+  uint32_t *ready = reinterpret_cast<uint32_t *>(ring + (uint64_t)R * kStreamTileBytes);
+  uint32_t *done = ready + R;
+  for (uint32_t i = threadIdx.x; i < 2 * R; i += kWmBlock) ready[i] = 0;
+  if (wid >= P) reinterpret_cast<uint64_t *>(waves + (wid - P) * kWaveLds)[lane] = 0;
+  __syncthreads();
+
+  const uint64_t ntiles = (a.n + 63) / 64, G = gridDim.x;
+  // the workgroup's tiles (< 2^32: n < 2^38 packets)
+  const uint64_t K = ntiles > blockIdx.x ? (ntiles - blockIdx.x + G - 1) / G : 0;
+  const uint32_t win_lo = a.fp.win_lo;
+  if (wid < P) {  // producer: windows of tiles wid, wid + P, ... into the ring
+    const uint32_t I = K > (uint64_t)wid ? (uint32_t)((K - wid + P - 1) / P) : 0u;
+    // tile i of this producer: j = wid + P i, slot j % R (kept incrementally)
+    uint32_t slot = (uint32_t)wid % R, pslot = slot;  // issue / publish cursors
+    uint32_t pj = (uint32_t)wid;
+    auto publish = [&]() {  // the oldest issued tile: its windows have landed
+      if (lane == 0) *(lds_flag_t *)&ready[pslot] = pj + 1;
+      pj += P;
+      pslot += P;
+      if (pslot >= R) pslot -= R;
+    };
+    for (uint32_t i = 0; i < I; i++) {
+      const uint32_t j = (uint32_t)wid + P * i;
+      if (j >= R) lds_wait_eq(&done[slot], j - R + 1);  // the slot's last tile read
+      dma_pair(a.frames, a.n, (blockIdx.x + (uint64_t)j * G) * 64, lane, win_lo, a.stride,
+               ring + (uint64_t)slot * kStreamTileBytes);
+      slot += P;
+      if (slot >= R) slot -= R;
+      if (i + 1 >= (uint32_t)D) {  // D tiles in flight: the oldest has landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (D - 1)) : "memory");
+        publish();
       }
     }
-    // B/C. one queue entry per (packet, tuple) with a fingerprint match,
-    // tuple-major: the wave's mask of matching lanes gives each lane its
-    // position (a scalar base + mbcnt) and the base advances by the mask's
-    // popcount. Usually the tile's entries fit one queue; more go in
-    // further rounds of kQueue.
-    const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
-    uint64_t mk[kMaxTuples];
-    uint32_t total = 0;
-#pragma unroll
-    for (int tu = 0; tu < kMaxTuples; tu++) {
-      mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
-      total += (uint32_t)__popcll(mk[tu]);
-    }
-    for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
-      uint32_t base = 0;
-#pragma unroll
-      for (int tu = 0; tu < kMaxTuples; tu++) {
-        const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
-        const bool mine = live && ent[tu] != 0;
-        if (total <= kQueue) {  // wave-uniform: one round, no window test
-          if (mine) q[pos] = ent[tu];
-        } else if (mine && pos - r0 < kQueue) {
-          q[pos - r0] = ent[tu];
-        }
-        base += (uint32_t)__popcll(mk[tu]);
-      }
-#ifdef BG_AB  // phase timing: + hashes, tag reads and the queue writes
-      if (a.ab_phase == 2) break;
-#endif
-      lds_fence();
-      const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
-      wm_check<KW>(a, tags, mlds, best, q, m, lane, lg, k);
-      lds_fence();  // the queue is rewritten by the next round
-    }
-    lds_fence();
-    uint64_t bb = best[lane];
-    best[lane] = 0;
-#pragma unroll
-    for (int d = 0; d < kMaxDirect; d++) {
-      const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFu;
-      if ((uint32_t)(dv[d] >> 48) == tu) {  // same order as wm_fold
-        const uint64_t comb = ((uint64_t)((uint32_t)dv[d] ^ 0x80000000u) << 32) |
-                              (1u << 19) | (tu << 16) | ((uint32_t)(dv[d] >> 32) & 0xFFFFu);
-        bb = comb > bb ? comb : bb;
-      }
-    }
-    if (live) a.gates[idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    while (pj < (uint32_t)wid + P * I) publish();
+    return;
+  }
+  // consumer
+  const int c = wid - P;
+  uint8_t *wl = waves + c * kWaveLds;
+  uint64_t *best = reinterpret_cast<uint64_t *>(wl);
+  uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
+  const uint32_t nbp = a.t.nbp;
+  uint32_t s = (uint32_t)c % R;
+  for (uint32_t j = (uint32_t)c; j < K; j += C) {
+    lds_wait_eq(&ready[s], j + 1);
+    const uint4 *src = reinterpret_cast<const uint4 *>(ring + (uint64_t)s * kStreamTileBytes) +
+                       2 * lane;
+    const uint4 x = src[0], y = src[1];
+    uint32_t w[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, 0u, 0u};
+    // the slot goes back once the reads have returned
+    if (lane == 0) lds_publish(&done[s], j + 1);
+    s += C;
+    while (s >= R) s -= R;
+    const uint64_t idx = (blockIdx.x + (uint64_t)j * G) * 64 + lane;
+    wm_tile<Spec, KW, 2>(a, tags, mlds, best, q, nbp, lane, idx, idx < a.n, w, [] {});
   }
 }
 

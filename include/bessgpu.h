@@ -293,6 +293,9 @@ int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
 #define BG_PATH_RING_HOST_DESC 1024 /* rings created now keep their descriptors in
                                        pinned host memory (not device memory
                                        through the BAR) */
+#define BG_PATH_WM_NO_STREAM 2048 /* WildcardMatch: the tag-word kernel in which
+                                     every wave loads its own windows (not
+                                     the streamed form's producer waves) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
 /* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */

@@ -160,10 +160,14 @@ def test_c5_8_partitions_attached(c5):
 
 
 # ------------------------------------------------------------------- C4
-@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_TAGS])
+@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_TAGS,
+                                   LB.BG_PATH_WM_NO_STREAM,
+                                   LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_NO_STREAM])
 def test_c4_imix_2k_slots(flags):
-    """flags 0: the run-time compiled kernel (bg_wm_jit.cc) once ready;
-    BG_PATH_WM_NO_JIT the ahead-of-time one; BG_PATH_WM_NO_TAGS the key filter"""
+    """flags 0: the run-time compiled kernel (bg_wm_jit.cc) once ready, in
+    its streamed form (producer waves, bg_wm_body.h); BG_PATH_WM_NO_JIT the
+    ahead-of-time one; BG_PATH_WM_NO_TAGS the key filter;
+    BG_PATH_WM_NO_STREAM the form in which every wave loads its windows"""
     n = 1 << 18
     rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n, stride=2048)
     assert set(np.unique(flen)) == {60, 590, 1514}
@@ -223,7 +227,9 @@ def test_c4_header_slab_full_size():
     del frames
     d_g = torch.zeros(n0 * rep, dtype=torch.int16, device="cuda")
     t.jit_wait()
-    for flags in (0, LB.BG_PATH_WM_NO_JIT):  # run-time compiled, ahead-of-time
+    # run-time compiled, ahead-of-time; streamed or not
+    for flags in (0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_STREAM,
+                  LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_NO_STREAM):
         d_g.zero_()
         with LB.kernel_paths(flags):
             t.classify(h, 64, n0 * rep, 8192, d_g)

@@ -84,8 +84,10 @@ def test_source_carries_the_image_constants():
     t = bench_table(20000)
     src = t.jit_source(-1)
     assert "struct WmJitSpec" in src
-    # the 5-tuple in 64 B slots: the pair-load and lane-per-packet variants
+    # the 5-tuple in 64 B slots: the pair-load and lane-per-packet variants,
+    # and the streamed form (its LDS ring fits beside the tag words)
     assert "bg_wm_jit_pair" in src and "bg_wm_jit_n2" in src
+    assert "bg_wm_jit_stream" in src
     assert "bg_wm_jit_n4" not in src
     # the /8 destination and the source-port tuples are direct tuples
     assert "ndirect(const WmArgs &) { return 2u; }" in src
@@ -131,7 +133,7 @@ def test_jit_vs_oracle_random_layouts(seed, stride, n):
     assert t.table_info()[1] == 3  # tag words in LDS
     d_frames = torch.from_numpy(frames.reshape(-1)).cuda()
     outs = []
-    for flags in (0, LB.BG_PATH_WM_NO_JIT):
+    for flags in (0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_NO_STREAM):
         d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
         with LB.kernel_paths(flags):
             t.classify(d_frames, stride, n, 777, d_g)
@@ -151,8 +153,8 @@ def test_jit_vs_oracle_random_layouts(seed, stride, n):
     want = np.zeros(n, np.uint16)
     L.or_wm_process(wm, frames.ctypes.data, stride, n, 777, want.ctypes.data)
     L.or_wm_free(wm)
-    assert (outs[0] == want).all(), fields
-    assert (outs[1] == want).all(), fields
+    for o in outs:
+        assert (o == want).all(), fields
     assert (want != 777).mean() > 0.2
 
 
