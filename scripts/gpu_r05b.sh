@@ -18,7 +18,7 @@ step() {  # name timeout cmd...
 step dbg 180 python -u scripts/dbg_wm_staged.py
 step tests 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_wm_jit.py "tests/test_gpu_configs.py::test_c4_imix_2k_slots" \
-  "tests/test_gpu_configs.py::test_c4_header_slab_full_size" tests/test_gpu_wm.py
+  "tests/test_gpu_configs.py::test_c4_header_slab_full_size"
 step wm 300 python -u bench.py --only wm --no-cpu --steps 20 --warmup 5
 step pool 600 python -u bench.py --only plugin_pool
 echo done >> "$OUT/steps.log"
