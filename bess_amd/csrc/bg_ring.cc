@@ -96,6 +96,21 @@ namespace {
 constexpr uint64_t kMaskAddr = (1ull << 48) - 1;
 constexpr size_t kTicketMaxPkts = (size_t)1 << 27;  // packets per ticket
 
+// A waiting host thread spins for a while, then sleeps between checks: the
+// GPU box's CPUs are a cgroup quota (16 per GPU) that the submitters share
+// with the HIP runtime's threads; 16 threads spinning in their waits used
+// it up, and a throttled quota stops every thread of the process until the
+// next period -- the submitters that still had tickets to write included.
+// `spin` counts the checks so far.
+void wait_pause(uint64_t spin) {
+  if (spin < 4096) {  // ~20-40 us of pause loops
+    _mm_pause();
+    return;
+  }
+  timespec ts{0, spin < 8192 ? 2000L : 20000L};
+  nanosleep(&ts, nullptr);
+}
+
 double now_s() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -460,7 +475,7 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
         if (int rc = grid_failed(r)) return rc;
         return fail(ETIMEDOUT, "ring lane full for 10 s");
       }
-      _mm_pause();
+      wait_pause(spin);
     }
   }
   const uint64_t t = l.next;
@@ -503,7 +518,7 @@ int bg_ring_wait(bg_ring *r, int lane, int64_t ticket) {
       if (int rc = grid_failed(r)) return rc;
       return fail(ETIMEDOUT, "ticket %lld: 10 s", (long long)ticket);
     }
-    _mm_pause();
+    wait_pause(spin);
   }
 }
 

@@ -390,7 +390,9 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
   best[lane] = 0;
 #pragma unroll
   for (int d = 0; d < kMaxDirect; d++) {
-    const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFu;
+    // (an unused direct slot names no tuple: its value is the all-ones
+    // "empty", whose tuple field 0xFFFF must not match it)
+    const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFFFFFu;
     if ((uint32_t)(dv[d] >> 48) == tu) {  // same order as wm_fold
       const uint64_t comb = ((uint64_t)((uint32_t)dv[d] ^ 0x80000000u) << 32) |
                             (1u << 19) | (tu << 16) | ((uint32_t)(dv[d] >> 32) & 0xFFFFu);

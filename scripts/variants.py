@@ -28,7 +28,7 @@ from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
-         "BG_WM_PHASE",
+         "BG_WM_PHASE", "BG_WM_NO_STREAM",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE"]
@@ -219,12 +219,22 @@ def main():
         variants = {"full": {}, "read_key": {"BG_WM_PHASE": 1},
                     "enqueue": {"BG_WM_PHASE": 2},
                     "checks_no_l2": {"BG_WM_PHASE": 3}}
+        # the streamed form (producer waves) and the one without
+        variants.update({k + "_nostream": dict(v, BG_WM_NO_STREAM=1)
+                         for k, v in list(variants.items())})
         r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants,
                           reps=20)
         for k in r:
             r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
         out["wmphase"] = r
-        del d, g
+        # the same on the frames in 2 KB slots (1 M of them)
+        f2 = torch.from_numpy(P.wm_workload(100000, 1 << 20, stride=2048)[4].reshape(-1)).to(dev)
+        n2 = 1 << 20
+        r = time_variants(lambda: t.classify(f2, 2048, n2, 8192, g), variants, reps=20)
+        for k in r:
+            r[k]["Mpps"] = round(n2 / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+        out["wmphase_2k"] = r
+        del d, g, f2
     if "wm" in which.split(","):
         n = 1 << 22
         rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n, stride=64,

@@ -203,9 +203,11 @@ def test_em_sharded_build_matches_single(dev):
 def classify_all_paths_wm(t, d_frames, stride, n, default_gate, dev, tags):
     """classify_all_paths with BG_PATH_WM_NO_TAGS kept on (tags == 0)"""
     keep = 0 if tags else LB.BG_PATH_WM_NO_TAGS
-    paths = TABLE_PATHS
+    # the tag-word kernel streamed (producer waves) and not
+    paths = TABLE_PATHS + ((LB.BG_PATH_WM_NO_STREAM,) if tags else ())
     if tags and wm_jit_ready(t):  # the run-time compiled kernel, then without it
-        paths = TABLE_PATHS + (LB.BG_PATH_WM_NO_JIT,)
+        paths = paths + (LB.BG_PATH_WM_NO_JIT,
+                         LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_NO_STREAM)
     outs = []
     for flags in paths:
         with LB.kernel_paths(flags | keep):
@@ -346,6 +348,33 @@ def test_wm_direct_tuples_vs_oracle(dev):
         t.delete(k, m)
     keep = np.array([(k.tobytes(), m.tobytes()) not in gone for k, m in zip(rk, rm)])
     check(keep)
+
+
+@pytest.mark.parametrize("ndirect", [0, 1])
+def test_wm_tags_fewer_direct_tuples(dev, ndirect):
+    """Tag-word images with no or one direct tuple (masks of three bytes and
+    more, or one one-byte mask): a direct slot left unused must not match
+    (round 5: its all-ones "empty" value named tuple 0xFFFF, which is what
+    an unused slot carried, so every packet without a hit got gate 0xFFFF
+    instead of the default gate)"""
+    masks = [P._m(sip=0xFFFFFFFF, dport=0xFFFF), P._m(sip=0xFFFF0000, dip=0xFFFF0000),
+             P._m(dip=0xFFFFFF00), P._m(proto=0xFF, sport=0xFFFF, dport=0xFFFF)]
+    if ndirect:
+        masks.append(P._m(dip=0xFF000000))
+    n = 65536
+    rk, rm, prio, gates, frames, _ = P.wm_workload(40000, n, seed=91, stride=64,
+                                                  sizes=((60, 1),), masks=masks)
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    got = classify_all_paths_wm(t, to_dev(frames, dev), 64, n, 77, dev, 1)
+    assert t.table_info()[1] == 3 and t.direct_tuples() == ndirect
+    wm = oracle_wm(P.FIVE_TUPLE, rk, rm, prio, gates)
+    want = np.zeros(n, np.uint16)
+    O.lib().or_wm_process(wm, frames.ctypes.data, 64, n, 77, want.ctypes.data)
+    O.lib().or_wm_free(wm)
+    assert (got == want).all()
+    assert 0.05 < (want == 77).mean() < 0.95
 
 
 @pytest.mark.parametrize("filler", [0, 5000])
