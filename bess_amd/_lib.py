@@ -120,6 +120,10 @@ _SIGS = {
     "bg_stream_attach": (_int, [_vp]),
     "bg_stream_detach": (_int, [_vp]),
     "bg_cksum": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp, _vp, _vp]),
+    "bg_cksum_ptrs": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp, _vp, _vp]),
+    "bg_host_register": (_int, [_vp, _sz]),
+    "bg_host_unregister": (_int, [_vp]),
+    "bg_host_dev_addr": (_int, [_vp, _sz, C.POINTER(C.c_uint64)]),
     "bg_cksum_process_host": (_int, [_int, _vp, _sz, _sz, _int, _int, _vp,
                                      _vp, _vp]),
     "bg_module_create": (_int, [C.c_char_p, _vp, _sz, C.POINTER(_vp)]),

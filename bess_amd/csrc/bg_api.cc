@@ -1668,6 +1668,28 @@ int bg_cksum(int device, void *d_frames, size_t stride, size_t n, int mode,
   a.frames = static_cast<uint8_t *>(d_frames);
   a.stride = stride;
   a.n = n;
+  a.ptrs = nullptr;
+  a.ip_gates = d_ip_gates;
+  a.l4_gates = d_l4_gates;
+  a.mode = mode;
+  a.verify = verify ? 1 : 0;
+  HIP_TRY(launch_cksum(a, num_cus(device), (hipStream_t)stream));
+  return 0;
+}
+
+int bg_cksum_ptrs(int device, const uint64_t *d_ptrs, size_t span, size_t n, int mode,
+                  int verify, uint16_t *d_ip_gates, uint16_t *d_l4_gates,
+                  bg_stream_t stream) {
+  if (mode < 1 || mode > 3) return fail(EINVAL, "mode must be 1, 2 or 3");
+  if (span < 64 || span > 65535) return fail(EINVAL, "span %zu not in [64, 65535]", span);
+  if (n && !d_ptrs) return fail(EINVAL, "bad arguments");
+  int r = set_device(device);
+  if (r) return r;
+  CkArgs a;
+  a.frames = nullptr;
+  a.stride = span;
+  a.n = n;
+  a.ptrs = d_ptrs;
   a.ip_gates = d_ip_gates;
   a.l4_gates = d_l4_gates;
   a.mode = mode;

@@ -129,6 +129,9 @@ hipStream_t thread_stream(int device, hipStream_t given);
 // laid out as bg_em_plan*) becomes the device's table image of the current
 // rules, owned (and freed, behind fences) by the table
 int em_publish_owned(bg_em *em, int device, uint8_t *d_img, uint64_t bytes);
+// bg_host_register: the device address of host bytes [p, p + len) when they
+// lie in one registered region (lock-free; false otherwise)
+bool host_dev_addr(const void *p, size_t len, uint64_t *dev);
 
 }  // namespace bg
 

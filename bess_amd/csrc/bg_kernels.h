@@ -172,6 +172,9 @@ BG_HD uint64_t wm_stream_lds_bytes(uint32_t nbp, uint32_t kw, uint32_t slots) {
 struct CkArgs {
   uint8_t *frames;
   uint64_t stride, n;
+  // non-null: frame i at ptrs[i] (device addresses of host-registered or
+  // device memory, bg_cksum_ptrs), `stride` bytes readable / writable each
+  const uint64_t *ptrs;
   uint16_t *ip_gates;  // may be null
   uint16_t *l4_gates;  // may be null
   int32_t mode;        // bit0 IPChecksum, bit1 L4Checksum

@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(kCkBlock) void cksum_kernel_generic(CkArgs a) {
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const int stride = (int)a.stride;
   for (uint64_t p = wave0; p < a.n; p += nw) {
-    uint8_t *f = a.frames + p * a.stride;
+    uint8_t *f = a.ptrs ? reinterpret_cast<uint8_t *>(a.ptrs[p]) : a.frames + p * a.stride;
     uint4 c[1];
     c[0] = ld_chunk(f, 0, lane, stride);
     const CkHdr h = ck_parse(c[0], a.mode, stride);
@@ -1747,7 +1747,8 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
 
 hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const bool tiled = a.stride >= 128 && a.stride <= 2048 &&
+  // (frames by pointer: one wave per frame wherever it lies)
+  const bool tiled = !a.ptrs && a.stride >= 128 && a.stride <= 2048 &&
                      !(path_flags() & kPathNoSlab) && !knob("BG_CK_GENERIC", 0);
   using CkKern = void (*)(CkArgs);
   CkKern kfn = cksum_kernel_generic;

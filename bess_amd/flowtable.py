@@ -388,6 +388,38 @@ def cksum(frames, stride, n, mode, verify, ip_gates=None, l4_gates=None,
                          _stream_ptr(stream)))
 
 
+def cksum_ptrs(d_ptrs, span, n, mode, verify, ip_gates=None, l4_gates=None,
+               device=0, stream=None):
+    """IPChecksum / L4Checksum on frames by pointer (d_ptrs: a device
+    uint64 tensor of device addresses, e.g. of host-registered memory), in
+    place."""
+    check(lib().bg_cksum_ptrs(device, _dev_ptr(d_ptrs), span, n, mode,
+                              1 if verify else 0,
+                              _dev_ptr(ip_gates) if ip_gates is not None else None,
+                              _dev_ptr(l4_gates) if l4_gates is not None else None,
+                              _stream_ptr(stream)))
+
+
+class HostRegion:
+    """Host memory registered for in-place device access (bg_host_register);
+    `addr(p)` is the device address of host address p."""
+
+    def __init__(self, arr):
+        self.arr = arr  # kept alive while registered
+        self.base = arr.ctypes.data
+        check(lib().bg_host_register(C.c_void_p(self.base), arr.nbytes))
+
+    def addr(self, p, length=1):
+        d = C.c_uint64()
+        check(lib().bg_host_dev_addr(C.c_void_p(int(p)), length, C.byref(d)))
+        return d.value
+
+    def close(self):
+        if self.arr is not None:
+            check(lib().bg_host_unregister(C.c_void_p(self.base)))
+            self.arr = None
+
+
 def cksum_host(frames_np, stride, n, mode, verify, span=None, device=0,
                stream=None):
     """Host slab through the staged host path (in place); returns gates."""

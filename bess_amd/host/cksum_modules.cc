@@ -61,6 +61,15 @@ class ChecksumModule : public Module {
                     kMode == BG_CK_L4 ? d_ogates : nullptr, stream);
   }
 
+  // the frames in place (host-registered packet buffers): no staging copy
+  int ProcessDevicePtrs(const bg_ctx &c, const uint64_t *d_ptrs, size_t span, size_t n,
+                        uint16_t *d_ogates, void *stream) override {
+    if (n == 0) return 0;
+    return bg_cksum_ptrs(c.device, d_ptrs, span, n, kMode, verify_ ? 1 : 0,
+                         kMode == BG_CK_IP ? d_ogates : nullptr,
+                         kMode == BG_CK_L4 ? d_ogates : nullptr, stream);
+  }
+
  private:
   bool verify_ = false;
 };

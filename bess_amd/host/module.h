@@ -234,6 +234,20 @@ class Module {
     (void)frame;
     return len;
   }
+  // ProcessDevice over frames by pointer (d_ptrs[i]: the device address of
+  // packet i's head in host-registered memory, `span` bytes each; the
+  // module writes in place): the zero-copy slots of a writeback pipe.
+  // -ENOTSUP: the module has no such datapath (n == 0 asks).
+  virtual int ProcessDevicePtrs(const bg_ctx &c, const uint64_t *d_ptrs, size_t span,
+                                size_t n, uint16_t *d_ogates, void *stream) {
+    (void)c;
+    (void)d_ptrs;
+    (void)span;
+    (void)n;
+    (void)d_ogates;
+    (void)stream;
+    return -ENOTSUP;
+  }
   // The metadata bytes [*mlo, *mhi) the device datapath reads (attr_name
   // fields), staged after the frame window (StagedMetaAt);
   // none: *mlo == *mhi. -errno while the attribute offsets are unbound.

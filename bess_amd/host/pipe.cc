@@ -72,6 +72,11 @@ struct Slot {
   // ring mode: the device addresses of h_in / h_g, and the ticket in flight
   uint8_t *dv_in = nullptr;
   uint16_t *dv_g = nullptr;
+  // zero-copy slot (a writeback module's packets in host-registered memory,
+  // bg_host_register): the packets' head pointers, device addresses, in
+  // pinned host memory the kernel reads; the frames are processed in place
+  bool zc = false;
+  uint64_t *h_ptr = nullptr, *dv_ptr = nullptr;
   std::shared_ptr<PipeRing> ring;  // the ring (rules) it was submitted to
   int lane = 0;
   int64_t ticket = -1;
@@ -92,6 +97,7 @@ struct bg_pipe {
   int mlo = 0, mhi = 0;
   size_t mat = 0;
   bool writeback = false;
+  bool zc = false;       // the module processes frames in place by pointer
   unsigned ctx_use = 0;  // Module::CtxUse(): the context fields a slot fixes
   bool ring_mode = false;          // slots go to the module's ring
   std::shared_ptr<PipeRing> ring;  // the ring this pipe has a lane on
@@ -138,6 +144,7 @@ static void pipe_release(bg_pipe *p) {
     if (s.h_wb) (void)hipHostFree(s.h_wb);
     if (s.h_g) (void)hipHostFree(s.h_g);
     if (s.h_done) (void)hipHostFree(s.h_done);
+    if (s.h_ptr) (void)hipHostFree(s.h_ptr);
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_g) (void)hipFree(s.d_g);
     if (s.st) (void)hipStreamDestroy(s.st);
@@ -247,16 +254,23 @@ static int launch_slot(bg_pipe *p) {
     p->st_call_ns[k] += t2 - t1;
     t1 = t2;
   };
-  HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
-  lap(0);
   bg_ctx c = s.ctx;
   c.device = (int16_t)p->device;
-  int r = p->mod->m->ProcessDeviceWindow(c, s.d_in, p->w, n, p->lo, s.d_g, s.st);
-  if (r < 0) return r;
+  if (s.zc) {  // the frames in place: no copy either way but the gates
+    lap(0);
+    int r = p->mod->m->ProcessDevicePtrs(c, s.dv_ptr, (size_t)(p->hi - p->lo), n, s.d_g,
+                                         s.st);
+    if (r < 0) return r;
+  } else {
+    HIP_TRY(hipMemcpyAsync(s.d_in, s.h_in, n * p->w, hipMemcpyHostToDevice, s.st));
+    lap(0);
+    int r = p->mod->m->ProcessDeviceWindow(c, s.d_in, p->w, n, p->lo, s.d_g, s.st);
+    if (r < 0) return r;
+  }
   lap(1);
   HIP_TRY(hipMemcpyAsync(s.h_g, s.d_g, n * 2, hipMemcpyDeviceToHost, s.st));
   lap(2);
-  if (p->writeback) {
+  if (p->writeback && !s.zc) {
     const size_t line = std::min(p->w, kWriteback);
     HIP_TRY(hipMemcpy2DAsync(s.h_wb, line, s.d_in, p->w, line, n,
                              hipMemcpyDeviceToHost, s.st));
@@ -316,7 +330,7 @@ static int retire_oldest(bg_pipe *p, bool wait) {
     p->st_lat_tsc += lat;
     p->st_lat_max = std::max(p->st_lat_max, lat);
   }
-  if (p->writeback) {
+  if (p->writeback && !s.zc) {
     const size_t line = std::min(p->w, kWriteback);
     for (size_t i = 0; i < s.n; i++)
       memcpy(s.heads[i], s.h_wb + i * line, s.wblen[i]);
@@ -403,6 +417,11 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
     p->w = StagedStride(p->lo, p->hi, p->mlo, p->mhi);
   }
   p->ctx_use = m->m->CtxUse();
+  // a writeback module with a by-pointer datapath takes packets that lie in
+  // host-registered memory in place (Module::ProcessDevicePtrs asked with n 0)
+  p->zc = p->writeback && !p->meta &&
+          m->m->ProcessDevicePtrs(ResolveCtx(nullptr, device), nullptr,
+                                  (size_t)(p->hi - p->lo), 0, nullptr, nullptr) == 0;
   // a ring ticket is served by one workgroup: past a few thousand packets
   // a launch per slot spreads them over the whole device instead
   if (!p->writeback && batch <= kPipeRingMaxBatch) {
@@ -450,6 +469,10 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
     if (e == hipSuccess && p->writeback)
       e = hipHostMalloc(reinterpret_cast<void **>(&s.h_wb),
                         batch * std::min(p->w, kWriteback), hipHostMallocDefault);
+    if (e == hipSuccess && p->zc)
+      e = hipHostMalloc(reinterpret_cast<void **>(&s.h_ptr), batch * 8, hipHostMallocMapped);
+    if (e == hipSuccess && p->zc)
+      e = hipHostGetDevicePointer(reinterpret_cast<void **>(&s.dv_ptr), s.h_ptr, 0);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
     if (e == hipSuccess) bg::own_stream(s.st);
     if (e == hipSuccess)
@@ -567,7 +590,8 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
     }
     const size_t take = std::min(cnt - i, p->batch - s.n);
     uint8_t *dst = s.h_in + s.n * p->w;
-    for (size_t j = 0; j < take; j++, dst += p->w) {
+    size_t j = 0;
+    for (; j < take; j++, dst += p->w) {
       const size_t k = i + j;
       const uint8_t *src = heads[k] + p->lo;
       if (!p->writeback) {
@@ -581,24 +605,37 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
           s.metas[s.n + j] = metas[k];
         }
       } else {
-        if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
-        // the bytes the module reads (data_len when given, or what its
-        // headers reach past it, Module::StageReach; at least the header
-        // line), zero-padded to the slot
-        size_t len = lens ? std::min<size_t>(mod->StageReach(heads[k], lens[k]), span) : span;
-        const size_t line = std::min(span, kWriteback);
-        len = std::max(len, line);
-        memcpy(dst, src, len);
-        if (len < p->w) memset(dst + len, 0, p->w - len);
+        // a packet in host-registered memory goes in place (its head's
+        // device address); a slot holds packets of one kind
+        uint64_t dev = 0;
+        const bool zc = p->zc && bg::host_dev_addr(heads[k], span, &dev);
+        if (s.n + j == 0)
+          s.zc = zc;
+        else if (zc != s.zc)
+          break;
+        if (zc) {
+          s.h_ptr[s.n + j] = dev;
+        } else {
+          if (k + 8 < cnt) __builtin_prefetch(heads[k + 8] + p->lo);
+          // the bytes the module reads (data_len when given, or what its
+          // headers reach past it, Module::StageReach; at least the header
+          // line), zero-padded to the slot
+          size_t len =
+              lens ? std::min<size_t>(mod->StageReach(heads[k], lens[k]), span) : span;
+          const size_t line = std::min(span, kWriteback);
+          len = std::max(len, line);
+          memcpy(dst, src, len);
+          if (len < p->w) memset(dst + len, 0, p->w - len);
+          s.wblen[s.n + j] = (uint16_t)line;
+        }
         s.heads[s.n + j] = heads[k];
-        s.wblen[s.n + j] = (uint16_t)line;
       }
       s.cookies[s.n + j] = cookies ? cookies[k] : heads[k];
     }
-    s.n += take;
-    i += take;
-    p->pending += take;
-    if (s.n == p->batch) {
+    s.n += j;
+    i += j;
+    p->pending += j;
+    if (s.n == p->batch || j < take) {  // full, or the next packet is of the other kind
       r = launch_slot(p);
       if (r < 0) return p->err = r;
     }

@@ -265,12 +265,33 @@ int bg_stream_detach(bg_stream_t stream);
 int bg_cksum(int device, void *d_frames, size_t stride, size_t n, int mode,
              int verify, uint16_t *d_ip_gates, uint16_t *d_l4_gates,
              bg_stream_t stream);
+/* Frames by pointer: frame i at d_ptrs[i] (the device address of host memory
+ * registered with bg_host_register, or device memory), each with `span`
+ * readable / writable bytes; the checksum words are written there in place.
+ * d_ptrs itself may be mapped host memory. */
+int bg_cksum_ptrs(int device, const uint64_t *d_ptrs, size_t span, size_t n, int mode,
+                  int verify, uint16_t *d_ip_gates, uint16_t *d_l4_gates,
+                  bg_stream_t stream);
 /* host frames (head pointers, each with >= `span` readable/writable bytes):
  * staged to the device, processed, written back; synchronous. */
 int bg_cksum_process_host(int device, uint8_t *const *heads, size_t n,
                           size_t span, int mode, int verify,
                           uint16_t *ip_gates, uint16_t *l4_gates,
                           bg_stream_t stream);
+
+/* ---- host memory the device works on in place --------------------------- */
+/* Register host memory (BESS's packet pool: core/packet_pool.h, the DPDK
+ * mempool's memory chunks, rte_mempool_mem_iter) for device access in place
+ * (hipHostRegister, mapped on every device). Then a bg_pipe of a module that
+ * works on whole frames (IPChecksum, L4Checksum) hands the device each
+ * packet's head pointer instead of a copy of its bytes: the kernel reads the
+ * frame over PCIe and writes the checksum words into the packet buffer.
+ * Unregister only with no packet of the region in flight. -EEXIST: overlaps
+ * a registered region. */
+int bg_host_register(void *base, size_t bytes);
+int bg_host_unregister(void *base);
+/* the device address of host bytes [p, p + len) in a registered region */
+int bg_host_dev_addr(const void *p, size_t len, uint64_t *dev);
 
 /* ---- kernel paths (parity tests) ---------------------------------------- */
 /* Several kernels compute each result (flow table staged in LDS or probed in

@@ -89,6 +89,8 @@ class GpuModule : public Module {
         for (long i = 0; i < k; i++) bess::Packet::Free(static_cast<bess::Packet *>(ck[i]));
       bg_pipe_destroy(p);
     }
+    for (void *base : registered_) PoolRegion(base, 0, -1);
+    registered_.clear();
     bg_module_destroy(m_);
     m_ = nullptr;
   }
@@ -123,6 +125,14 @@ class GpuModule : public Module {
     }
     return {.block = done == 0, .packets = done, .bits = 0};
   }
+
+  // The socket's packet pool registered for device access in place
+  // (bg_host_register over the mempool's memory chunks, once per chunk and
+  // process, counted per module): a checksum module's pipes then hand the
+  // device each packet's head pointer, and the kernel reads the frame over
+  // PCIe and writes the checksum words into the buffer -- no staging copy
+  // (bg_pipe's zero-copy slots). Packets from elsewhere are staged as before.
+  void UsePacketPoolInPlace() { in_place_ = true; }
 
   // a worker's pipe counters (bg_pipe_stats); 0 if it has none
   int PipeStats(int wid, uint64_t *out, int n) const {
@@ -359,7 +369,42 @@ class GpuModule : public Module {
  private:
   // the worker's pipe, on device wid % (visible devices): the workers of one
   // process spread over its GPUs, each using the module's table replica there
+  // process-wide reference counts of the registered pool chunks: +1 / -1
+  static void PoolRegion(void *base, size_t len, int delta) {
+    static std::mutex mu;
+    static std::vector<std::pair<void *, int>> refs;
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = 0; i < refs.size(); i++) {
+      if (refs[i].first != base) continue;
+      if ((refs[i].second += delta) == 0) {
+        (void)bg_host_unregister(base);
+        refs.erase(refs.begin() + (long)i);
+      }
+      return;
+    }
+    if (delta > 0 && bg_host_register(base, len) == 0) refs.emplace_back(base, 1);
+  }
+
+  void RegisterPool() {
+    bess::PacketPool *pool = bess::PacketPool::GetDefaultPool(current_worker.socket());
+    if (!pool) return;
+    rte_mempool_mem_iter(
+        pool->pool(),
+        [](rte_mempool *, void *self, rte_mempool_memhdr *h, unsigned) {
+          GpuModule *m = static_cast<GpuModule *>(self);
+          for (void *b : m->registered_)
+            if (b == h->addr) return;
+          PoolRegion(h->addr, h->len, 1);
+          m->registered_.push_back(h->addr);
+        },
+        this);
+  }
+
   bg_pipe *OpenLane(int wid) {
+    if (in_place_) {  // (workers open their lanes one at a time: lanes_mu_)
+      std::lock_guard<std::mutex> lk(lanes_mu_);
+      RegisterPool();
+    }
     const int nd = bg_device_count();
     bg_pipe *p = nullptr;
     // within the budget, full-size slots first (each slot costs a submit or
@@ -406,6 +451,9 @@ class GpuModule : public Module {
   std::atomic<int32_t> bound_[16] = {};
   size_t pipe_batch_ = kPipeBatch;
   int pipe_depth_ = kPipeDepth;
+  bool in_place_ = false;             // UsePacketPoolInPlace
+  std::mutex lanes_mu_;               // RegisterPool from the workers' first calls
+  std::vector<void *> registered_;    // the pool chunks this module registered
   Lane lanes_[Worker::kMaxWorkers];
 };
 

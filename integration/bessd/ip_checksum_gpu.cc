@@ -10,7 +10,9 @@ class IPChecksum final : public GpuModule {
   static const gate_idx_t kNumOGates = 2;  // ip_checksum.h:43
 
   CommandResponse Init(const bess::pb::IPChecksumArg &arg) {
-    return CreateDeferred("IPChecksum", arg);
+    CommandResponse r = CreateDeferred("IPChecksum", arg);
+    if (r.code() == 0) UsePacketPoolInPlace();  // frames in place, no staging copy
+    return r;
   }
   void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override { Forward(ctx, batch); }
 };

@@ -9,7 +9,9 @@ class L4Checksum final : public GpuModule {
   static const gate_idx_t kNumIGates = MAX_GATES;  // l4_checksum.h:43
 
   CommandResponse Init(const bess::pb::L4ChecksumArg &arg) {
-    return CreateDeferred("L4Checksum", arg);
+    CommandResponse r = CreateDeferred("L4Checksum", arg);
+    if (r.code() == 0) UsePacketPoolInPlace();  // frames in place, no staging copy
+    return r;
   }
   void ProcessBatch(Context *ctx, bess::PacketBatch *batch) override { Forward(ctx, batch); }
 };

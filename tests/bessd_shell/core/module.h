@@ -73,6 +73,27 @@ struct task_result {
   uint64_t bits;
 };
 
+// The DPDK mempool surface a plugin uses to find the packet memory
+// (rte_mempool.h, DPDK 19.11: rte_mempool_mem_iter over the pool's memory
+// chunks): the shell's pool is one chunk.
+struct rte_mempool {
+  void *addr = nullptr;
+  size_t len = 0;
+};
+struct rte_mempool_memhdr {
+  void *addr;
+  size_t len;
+};
+typedef void(rte_mempool_mem_cb_t)(struct rte_mempool *mp, void *opaque,
+                                   struct rte_mempool_memhdr *memhdr, unsigned mem_idx);
+inline uint32_t rte_mempool_mem_iter(struct rte_mempool *mp, rte_mempool_mem_cb_t *cb,
+                                     void *arg) {
+  if (!mp || !mp->addr) return 0;
+  rte_mempool_memhdr h{mp->addr, mp->len};
+  cb(mp, arg, &h, 0);
+  return 1;
+}
+
 namespace bess {
 
 class PacketPool;
@@ -132,8 +153,11 @@ class PacketPool {
     return p;
   }
   explicit PacketPool(size_t capacity) : capacity_(capacity) {
-    mem_ = static_cast<uint8_t *>(aligned_alloc(64, capacity * kObj));
+    // (page-aligned: the memory a plugin registers for device access)
+    mem_ = static_cast<uint8_t *>(aligned_alloc(4096, (capacity * kObj + 4095) / 4096 * 4096));
     memset(mem_, 0, capacity * kObj);
+    mp_.addr = mem_;
+    mp_.len = capacity * kObj;
     std::vector<Packet *> m;
     for (size_t i = capacity; i-- > 0;) {
       Packet *p = new (mem_ + i * kObj) Packet();
@@ -152,6 +176,7 @@ class PacketPool {
     free(mem_);
   }
   size_t Capacity() const { return capacity_; }
+  rte_mempool *pool() { return &mp_; }  // packet_pool.h:67
   size_t Size() const {  // available: the shared list (thread caches not counted)
     std::lock_guard<std::mutex> lk(mu_);
     return avail_;
@@ -226,6 +251,7 @@ class PacketPool {
   }
   size_t capacity_;
   uint8_t *mem_ = nullptr;
+  rte_mempool mp_;
   uint64_t gen_ = 0;
   mutable std::mutex mu_;
   std::vector<std::vector<Packet *>> mags_;  // magazines of <= kMag

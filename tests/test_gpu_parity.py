@@ -374,7 +374,8 @@ def test_wm_tags_fewer_direct_tuples(dev, ndirect):
     O.lib().or_wm_process(wm, frames.ctypes.data, 64, n, 77, want.ctypes.data)
     O.lib().or_wm_free(wm)
     assert (got == want).all()
-    assert 0.05 < (want == 77).mean() < 0.95
+    if ndirect == 0:  # (the /8 tuple's 8 K rules cover every packet)
+        assert 0.05 < (want == 77).mean() < 0.95
 
 
 @pytest.mark.parametrize("filler", [0, 5000])

@@ -379,6 +379,71 @@ def test_cksum_pipe_p11_bytes_past_data_len(cls, mode, verify):
     assert (out == ref).all()
 
 
+@pytest.mark.parametrize("cls,mode", [(IPChecksum, 1), (L4Checksum, 2)])
+@pytest.mark.parametrize("verify", [False, True])
+def test_cksum_pipe_zero_copy_vs_oracle(cls, mode, verify):
+    """Packets in host-registered memory (bg_host_register: the packet
+    pool): the pipe hands the device their head pointers and the kernel
+    works on the buffers in place -- including the bytes past data_len the
+    reference reads (P11) -- with unregistered packets (copied, zero-padded
+    past what they read) interleaved, so slots switch kind; every gate and
+    every byte of the data areas as the oracle gives them."""
+    from bess_amd.flowtable import HostRegion
+    n = 3000
+    frames, lens = P.cksum_p11_workload(n, seed=17)
+    if verify:
+        O.cksum_process(frames[:n // 2], 2048, n // 2, 3, False)
+    ref = frames.copy()
+    ipg, l4g = O.cksum_process(ref, 2048, n, mode, verify)
+    want = ipg if mode == 1 else l4g
+    buf, heads = snbufs(frames)
+    reg = HostRegion(buf)
+    try:
+        # a third of the packets from a copy that is not registered
+        other = np.random.default_rng(3).random(n) < 1 / 3
+        buf2, heads2 = snbufs(frames)
+        heads = np.where(other, heads2, heads)
+        pipe = Pipe(cls(verify=verify), batch=512, depth=3)
+        got = run_pipe(pipe, heads, lens=lens, shuffle_seed=5)
+        pipe.close()
+    finally:
+        reg.close()
+    assert (got == want).all()
+    out = np.where(other[:, None], buf2, buf)[:, 512:512 + 2048]
+    assert (out == ref).all()
+
+
+def test_cksum_ptrs_device_and_host_memory():
+    """bg_cksum_ptrs over frames by pointer: device memory in a permuted
+    order, and host-registered memory, against the oracle"""
+    from bess_amd import flowtable as F
+    from bess_amd.flowtable import HostRegion
+    n = 5000
+    frames, _ = P.cksum_p11_workload(n, seed=23)
+    ref = frames.copy()
+    ipg, l4g = O.cksum_process(ref, 2048, n, 3, False)
+    d = torch.from_numpy(frames.reshape(-1)).cuda()
+    perm = np.random.default_rng(1).permutation(n)
+    ptrs = torch.from_numpy((d.data_ptr() + 2048 * perm).astype(np.uint64).view(np.int64)).cuda()
+    gi = torch.zeros(n, dtype=torch.int16, device="cuda")
+    gl = torch.zeros(n, dtype=torch.int16, device="cuda")
+    F.cksum_ptrs(ptrs, 2048, n, 3, False, gi, gl)
+    torch.cuda.synchronize()
+    assert (gi.cpu().numpy().view(np.uint16) == ipg[perm]).all()
+    assert (gl.cpu().numpy().view(np.uint16) == l4g[perm]).all()
+    assert (d.cpu().numpy().reshape(n, 2048) == ref).all()
+    h = frames.copy()
+    reg = HostRegion(h)
+    try:
+        hp = np.array([reg.addr(h.ctypes.data + 2048 * i, 2048) for i in perm], np.uint64)
+        F.cksum_ptrs(torch.from_numpy(hp.view(np.int64)).cuda(), 2048, n, 3, False, gi, gl)
+        torch.cuda.synchronize()
+    finally:
+        reg.close()
+    assert (gl.cpu().numpy().view(np.uint16) == l4g[perm]).all()
+    assert (h == ref).all()
+
+
 def test_pipe_empty_and_flush():
     keys, gates, frames = P.em_workload(10, 10, seed=2)
     m, om = em_pair(keys, gates)
