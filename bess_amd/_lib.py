@@ -175,6 +175,7 @@ _SIGS = {
     "bg_ring_wait": (_int, [_vp, _int, C.c_int64]),
     "bg_ring_completed": (C.c_int64, [_vp, _int]),
     "bg_ring_run": (_int, [_vp, _int, _vp, _sz, _sz, _sz, _u16, _vp]),
+    "bg_ring_run_lanes": (C.c_double, [_vp, _int, _vp, _sz, _sz, _sz, _u16, _vp, _int]),
     "bg_ring_info": (_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(_int)]),
     "bg_ring_desc_in_device": (_int, [_vp]),
     "bg_ring_set_coherence": (_int, [_vp, _int, _int]),

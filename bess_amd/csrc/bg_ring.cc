@@ -39,6 +39,8 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/bessgpu.h"
 #include "bg_internal.h"
@@ -96,18 +98,18 @@ namespace {
 constexpr uint64_t kMaskAddr = (1ull << 48) - 1;
 constexpr size_t kTicketMaxPkts = (size_t)1 << 27;  // packets per ticket
 
-// A waiting host thread spins for a while, then sleeps between checks: the
-// GPU box's CPUs are a cgroup quota (16 per GPU) that the submitters share
-// with the HIP runtime's threads; 16 threads spinning in their waits used
-// it up, and a throttled quota stops every thread of the process until the
-// next period -- the submitters that still had tickets to write included.
-// `spin` counts the checks so far.
+// A thread waiting for a ticket's completion spins for a while (~0.1-0.2
+// ms of pause loops: a slot's usual latency), then sleeps between checks,
+// leaving the CPU to the workers (the GPU box's CPUs are a quota shared
+// with the HIP runtime's threads). `spin` counts the checks so far. (A
+// submitter waiting for lane space keeps spinning: that wait is the
+// pipe's backpressure, and its latency is the worker's.)
 void wait_pause(uint64_t spin) {
-  if (spin < 4096) {  // ~20-40 us of pause loops
+  if (spin < (1u << 15)) {
     _mm_pause();
     return;
   }
-  timespec ts{0, spin < 8192 ? 2000L : 20000L};
+  timespec ts{0, 10000L};
   nanosleep(&ts, nullptr);
 }
 
@@ -475,7 +477,7 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
         if (int rc = grid_failed(r)) return rc;
         return fail(ETIMEDOUT, "ring lane full for 10 s");
       }
-      wait_pause(spin);
+      _mm_pause();
     }
   }
   const uint64_t t = l.next;
@@ -542,6 +544,38 @@ int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride, size_t 
     if (last < 0) return (int)last;
   }
   return last < 0 ? 0 : bg_ring_wait(r, lane, last);
+}
+
+double bg_ring_run_lanes(bg_ring *r, int threads, const void *frames, size_t stride,
+                         size_t n, size_t burst, uint16_t default_gate, uint16_t *gates,
+                         int reps) {
+  if (threads < 1 || (uint32_t)threads > r->nlanes || reps < 1)
+    return fail(EINVAL, "threads %d / reps %d (lanes %u)", threads, reps, r->nlanes);
+  std::vector<std::thread> th;
+  std::atomic<int> ready{0}, err{0};
+  std::atomic<bool> go{false};
+  double t1[kRingMaxLanes] = {};
+  for (int i = 0; i < threads; i++) {
+    th.emplace_back([&, i] {
+      const size_t lo = n * i / threads, hi = n * (i + 1) / threads;
+      ready++;
+      while (!go.load(std::memory_order_acquire)) _mm_pause();
+      for (int k = 0; k < reps && !err.load(); k++) {
+        const int rc = bg_ring_run(r, i, static_cast<const uint8_t *>(frames) + lo * stride,
+                                   stride, hi - lo, burst, default_gate, gates + lo);
+        if (rc < 0) err.store(rc);
+      }
+      t1[i] = now_s();
+    });
+  }
+  while (ready.load() < threads) _mm_pause();
+  const double t0 = now_s();
+  go.store(true, std::memory_order_release);
+  for (auto &t : th) t.join();
+  if (err.load()) return (double)err.load();
+  double end = t0;
+  for (int i = 0; i < threads; i++) end = std::max(end, t1[i]);
+  return (end - t0) / reps;
 }
 
 #ifdef BG_AB

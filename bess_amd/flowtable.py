@@ -255,32 +255,16 @@ class Ring:
                                 C.c_void_p(gates.data_ptr() + 2 * offset)))
 
     def run_lanes(self, frames, stride, n, burst, default_gate, gates, threads, reps=1):
-        """`threads` submitters at once (threads <= lanes), thread i on lane
-        i over packets [i*n/threads, (i+1)*n/threads), `reps` times in a
-        row (so that starting the threads is not what gets timed); -> wall
-        seconds per rep"""
-        import threading
-        import time
-        errs = []
-
-        def work(i):
-            lo, hi = n * i // threads, n * (i + 1) // threads
-            try:
-                for _ in range(reps):
-                    self.run(frames, stride, hi - lo, burst, default_gate, gates, lane=i,
-                             offset=lo)
-            except Exception as e:  # reported below
-                errs.append(e)
-        ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-        t0 = time.perf_counter()
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join()
-        dt = time.perf_counter() - t0
-        if errs:
-            raise errs[0]
-        return dt / reps
+        """`threads` submitters at once (threads <= lanes; native threads,
+        bg_ring_run_lanes), thread i on lane i over packets
+        [i*n/threads, (i+1)*n/threads), `reps` passes each; -> wall seconds
+        per pass"""
+        dt = lib().bg_ring_run_lanes(self.h, threads, C.c_void_p(frames.data_ptr()),
+                                     stride, n, burst, default_gate,
+                                     C.c_void_p(gates.data_ptr()), reps)
+        if dt < 0:
+            raise BessGpuError(-int(dt), lib().bg_last_error().decode())
+        return dt
 
     def set_coherence(self, frames, done):
         """bg_ring_set_coherence: frames 0 for device memory written by

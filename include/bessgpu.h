@@ -694,6 +694,13 @@ int64_t bg_ring_completed(bg_ring *r, int lane);
  * to back, then waits for the last (the persistent series of the C2 sweep). */
 int bg_ring_run(bg_ring *r, int lane, const void *frames, size_t stride,
                 size_t n, size_t burst, uint16_t default_gate, uint16_t *gates);
+/* `threads` such workers at once (native threads, released together),
+ * worker i on lane i over packets [i n / threads, (i + 1) n / threads),
+ * `reps` passes each; returns the wall seconds per pass (from the release
+ * to the last worker's end), or -errno. */
+double bg_ring_run_lanes(bg_ring *r, int threads, const void *frames, size_t stride,
+                         size_t n, size_t burst, uint16_t default_gate, uint16_t *gates,
+                         int reps);
 /* kernel launches so far (1 + relaunches after idle exits), workgroups */
 int bg_ring_info(const bg_ring *r, uint64_t *launches, int *blocks);
 /* 1: the descriptors live in device memory the host writes through the
