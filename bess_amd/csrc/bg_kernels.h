@@ -159,6 +159,7 @@ BG_HD uint64_t wm_stream_fixed_lds(uint32_t nbp, uint32_t kw) {
 // ring slots that fit beside the tag words (0: too few for the producers'
 // depth, the streamed form does not apply)
 BG_HD uint32_t wm_stream_slots(uint32_t nbp, uint32_t kw) {
+  if (kw > 2) return 0;  // (its pipelined consumer's state would spill)
   const uint64_t fixed = wm_stream_fixed_lds(nbp, kw);
   if (fixed >= kLdsMax) return 0;
   uint64_t r = (kLdsMax - fixed) / (kStreamTileBytes + 8);

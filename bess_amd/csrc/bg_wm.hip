@@ -23,6 +23,9 @@ __global__ __launch_bounds__(kWmBlock) void wm_stream_kernel(WmArgs a) {
 
 template <int KW>
 hipError_t launch_stream(WmArgs a, uint32_t slots, int num_cus, hipStream_t s) {
+  if constexpr (KW > 2) {  // (wm_stream_slots is 0 for these)
+    return hipErrorInvalidValue;
+  } else {
   a.ring_slots = slots;
   const uint64_t ntiles = (a.n + 63) / 64;
   uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
@@ -31,6 +34,7 @@ hipError_t launch_stream(WmArgs a, uint32_t slots, int num_cus, hipStream_t s) {
   hipLaunchKernelGGL((wm_stream_kernel<KW>), dim3((unsigned)blocks), dim3(kWmBlock),
                      wm_stream_lds_bytes(a.t.nbp, KW, slots), s, a);
   return hipGetLastError();
+  }
 }
 
 template <int KW, int NCH, int PAIR>

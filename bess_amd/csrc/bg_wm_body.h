@@ -465,6 +465,94 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   }
 }
 
+// The probe of one tile (step 2): ent[tu] = the packet's queue entry for
+// hashed tuple tu when one of its buckets holds the packet's fingerprint,
+// else 0; all tag reads in flight before any is used.
+template <class Spec, int KW>
+__device__ __forceinline__ void wm_probe_tuples(const WmArgs &a, const uint32_t *tags,
+                                                uint32_t nbp, int lane,
+                                                const uint64_t (&k)[KW],
+                                                uint32_t (&ent)[kMaxTuples]) {
+  const uint32_t hmask = Spec::hashed(a);
+#pragma unroll
+  for (int tu = 0; tu < kMaxTuples; tu++) {
+    ent[tu] = 0;
+    if ((hmask >> tu) & 1u) {
+      const Probe p = wm_probe(Spec::template hash<KW>(k, tu, a), nbp);
+      const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);
+      const uint32_t zz = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
+      ent[tu] = zz ? p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24)
+                   : 0u;
+    }
+  }
+}
+
+// A tile whose checks' loads are in flight (the pipelined consumer): lane
+// = packet idx; its direct tuples' values; its queue entry (lanes < m: the
+// tile's m <= 64 entries, one per lane), the entry's candidate slots left,
+// the first candidate's value and key, the owner's key
+template <int KW>
+struct WmPend {
+  uint64_t idx;
+  uint32_t live, m;
+  uint64_t dv[kMaxDirect];
+  uint32_t e, z1, z2;
+  uint64_t v, sk[KW], kk[KW];
+};
+
+// the pending tile's end (steps 4-5): compare its loaded candidates, fold
+// the hits, try further candidates of fingerprint collisions, store gates
+template <class Spec, int KW>
+__device__ __forceinline__ void wm_finish(const WmArgs &a, const uint32_t *tags,
+                                          const uint64_t *mlds, uint64_t *best, int lane,
+                                          uint32_t nbp, WmPend<KW> &p) {
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
+  bool more = false;
+  if ((uint32_t)lane < p.m) {
+    if (wm_hit<KW>(mlds, p.e, p.v, p.sk, p.kk)) {
+      wm_fold(best, p.e, p.v);
+      p.z1 = p.z2 = 0;
+    } else if (p.z1) {
+      p.z1 &= p.z1 - 1;
+    } else {
+      p.z2 &= p.z2 - 1;
+    }
+    more = (p.z1 | p.z2) != 0;
+  }
+  if (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform, rare
+    while (p.z1 | p.z2) {
+      const uint32_t slot = next_slot(p.e, nbp, p.z1, p.z2);
+      if (p.z1)
+        p.z1 &= p.z1 - 1;
+      else
+        p.z2 &= p.z2 - 1;
+      const uint64_t vv = vals[slot];
+      uint64_t s2[KW];
+#pragma unroll
+      for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * KW + j];
+      if (wm_hit<KW>(mlds, p.e, vv, s2, p.kk)) {
+        wm_fold(best, p.e, vv);
+        p.z1 = p.z2 = 0;
+      }
+    }
+  }
+  lds_fence();
+  uint64_t bb = best[lane];
+  best[lane] = 0;
+  const uint32_t ndir = Spec::ndirect(a);
+#pragma unroll
+  for (int d = 0; d < kMaxDirect; d++) {
+    const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFFFFFu;
+    if ((uint32_t)(p.dv[d] >> 48) == tu) {
+      const uint64_t comb = ((uint64_t)((uint32_t)p.dv[d] ^ 0x80000000u) << 32) |
+                            (1u << 19) | (tu << 16) | ((uint32_t)(p.dv[d] >> 32) & 0xFFFFu);
+      bb = comb > bb ? comb : bb;
+    }
+  }
+  if (p.live) a.gates[p.idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
+}
+
 // ---------------------------------------------------------------------------
 // Streamed form (pair-shaped windows: two 16-byte chunks inside the slot's
 // first 64 bytes). The header stream is decoupled from the lookups: in the
@@ -572,26 +660,126 @@ __device__ __forceinline__ void wm_tags_stream_body(const WmArgs &a) {
     while (pj < (uint32_t)wid + P * I) publish();
     return;
   }
-  // consumer
+  // consumer, software-pipelined one tile deep: the L2 loads of tile j's
+  // checks are in flight while tile j + C is taken from the ring, keyed,
+  // hashed and probed; then tile j ends and tile j + C's loads are issued.
+  // A wave's only vector loads are its own checks' and direct tuples', so
+  // ending tile j waits for exactly those (vmcnt in order), never for the
+  // header stream.
   const int c = wid - P;
   uint8_t *wl = waves + c * kWaveLds;
   uint64_t *best = reinterpret_cast<uint64_t *>(wl);
   uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
   const uint32_t nbp = a.t.nbp;
+  const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
+  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
+  WmPend<KW> pd;
+  bool pending = false;
   uint32_t s = (uint32_t)c % R;
   for (uint32_t j = (uint32_t)c; j < K; j += C) {
+    // A1: the tile's windows, key, probes and queue
     lds_wait_eq(&ready[s], j + 1);
     const uint4 *src = reinterpret_cast<const uint4 *>(ring + (uint64_t)s * kStreamTileBytes) +
                        2 * lane;
     const uint4 x = src[0], y = src[1];
     uint32_t w[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, 0u, 0u};
-    // the slot goes back once the reads have returned
-    if (lane == 0) lds_publish(&done[s], j + 1);
+    if (lane == 0) lds_publish(&done[s], j + 1);  // (the reads have returned)
     s += C;
     while (s >= R) s -= R;
     const uint64_t idx = (blockIdx.x + (uint64_t)j * G) * 64 + lane;
-    wm_tile<Spec, KW, 2>(a, tags, mlds, best, q, nbp, lane, idx, idx < a.n, w, [] {});
+    const bool live = idx < a.n;
+    uint64_t k[KW];
+    Spec::template key<KW, 2>(w, a, k);
+    uint32_t total;
+    {
+      uint32_t ent[kMaxTuples];
+      wm_probe_tuples<Spec, KW>(a, tags, nbp, lane, k, ent);
+      const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
+      uint64_t mk[kMaxTuples];
+      total = 0;
+#pragma unroll
+      for (int tu = 0; tu < kMaxTuples; tu++) {
+        mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
+        total += (uint32_t)__popcll(mk[tu]);
+      }
+      if (total <= 64) {  // (uniform) the usual tile: one entry per lane at most
+        uint32_t base = 0;
+#pragma unroll
+        for (int tu = 0; tu < kMaxTuples; tu++) {
+          const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
+          if (live && ent[tu] != 0) q[pos] = ent[tu];
+          base += (uint32_t)__popcll(mk[tu]);
+        }
+      }
+    }
+    // B: the previous tile ends (its loads have had this tile's front)
+    if (pending) wm_finish<Spec, KW>(a, tags, mlds, best, lane, nbp, pd);
+    // A2: this tile's loads: direct tuples, then the checks' first candidates
+    pd.idx = idx;
+    pd.live = live ? 1u : 0u;
+    const uint32_t ndir = Spec::ndirect(a);
+#pragma unroll
+    for (int d = 0; d < kMaxDirect; d++) {
+      pd.dv[d] = ~0ull;
+      if ((uint32_t)d < ndir && live) {
+        const uint64_t off =
+            reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
+                tuple_words(a, offsetof(WmArgs, doff)))[d];
+        pd.dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)
+            [direct_index_k<KW>(k, Spec::dspec(a, d))];
+      }
+    }
+    pd.e = pd.z1 = pd.z2 = 0;
+    pd.v = 0;
+#pragma unroll
+    for (int q2 = 0; q2 < KW; q2++) pd.sk[q2] = pd.kk[q2] = 0;
+    if (total <= 64) {
+      pd.m = total;
+      if (total) {  // (uniform)
+        lds_fence();  // the queue written above
+        if ((uint32_t)lane < total) pd.e = q[lane];
+        owner_key<KW>(pd.e, k, pd.kk);
+        if ((uint32_t)lane < total) {
+          const uint32_t b1 = pd.e & 0x7FFFu;
+          pd.z1 = bucket_matches(tags, b1, pd.e);
+          pd.z2 = bucket_matches(tags, wm_b2(b1, pd.e >> 24, nbp), pd.e);
+          const uint32_t slot = next_slot(pd.e, nbp, pd.z1, pd.z2);
+          pd.v = vals[slot];
+#pragma unroll
+          for (int q2 = 0; q2 < KW; q2++) pd.sk[q2] = keys[(uint64_t)slot * KW + q2];
+        }
+      }
+    } else {
+      // a tile of more than 64 entries (rare): its checks here, in rounds
+      // of kQueue as wm_tile makes them (the previous tile has ended, so
+      // `best` is this tile's); its end then only folds and stores
+      pd.m = 0;
+      uint32_t ent[kMaxTuples];
+      wm_probe_tuples<Spec, KW>(a, tags, nbp, lane, k, ent);
+      const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
+      uint64_t mk[kMaxTuples];
+#pragma unroll
+      for (int tu = 0; tu < kMaxTuples; tu++)
+        mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
+      for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
+        uint32_t base = 0;
+#pragma unroll
+        for (int tu = 0; tu < kMaxTuples; tu++) {
+          const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
+          if (live && ent[tu] != 0 && pos - r0 < kQueue) q[pos - r0] = ent[tu];
+          base += (uint32_t)__popcll(mk[tu]);
+        }
+        lds_fence();
+        const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
+        wm_check<KW>(a, tags, mlds, best, q, m, lane, nbp, k);
+        lds_fence();
+      }
+    }
+    pending = true;
   }
+  if (pending) wm_finish<Spec, KW>(a, tags, mlds, best, lane, nbp, pd);
 }
 
 }  // namespace
