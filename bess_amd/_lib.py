@@ -26,7 +26,7 @@ BG_PATH_LPM_DIR24 = 128
 BG_PATH_PIPE_NO_RING = 256
 BG_PATH_WM_NO_JIT = 512
 BG_PATH_RING_HOST_DESC = 1024
-BG_PATH_WM_NO_STREAM = 2048
+BG_PATH_WM_STREAM = 2048
 KEY_BYTES = 64
 
 

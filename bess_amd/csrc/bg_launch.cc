@@ -37,7 +37,7 @@ uint32_t path_flags() {
   if (knob("BG_FORCE_LDS", 0)) f |= kPathForceLds;
   if (knob("BG_NOLDS", 0)) f |= kPathNoLds;
   if (knob("BG_NO_SLAB", 0)) f |= kPathNoSlab;
-  if (knob("BG_WM_NO_STREAM", 0)) f |= kPathWmNoStream;
+  if (knob("BG_WM_STREAM", 0)) f |= kPathWmStream;
 #endif
   return f;
 }

@@ -35,7 +35,7 @@ constexpr uint32_t kPathLpmDir24 = 128;  // IPLookup: DIR-24-8 (not DIR-16-8-8)
 constexpr uint32_t kPathPipeNoRing = 256;  // pipes launch per slot (no ring)
 constexpr uint32_t kPathWmNoJit = 512;   // WildcardMatch: never the run-time compiled kernel
 constexpr uint32_t kPathRingHostDesc = 1024;  // rings: descriptors in pinned host memory
-constexpr uint32_t kPathWmNoStream = 2048;  // WildcardMatch: never the streamed tag-word form
+constexpr uint32_t kPathWmStream = 2048;  // WildcardMatch: the streamed tag-word form
 constexpr uint32_t kPathAll = 4095;
 
 uint32_t path_flags();

@@ -62,8 +62,10 @@ hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   // (both chunks inside the slot: no read past a staged row or the slab)
   const bool pair = n2 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
                     a.fp.win_lo + 32 <= a.stride && a.stride <= 65536;
-  // the streamed form when its ring fits beside the tag words (bg_wm_body.h)
-  const uint32_t slots = pair && !(path_flags() & kPathWmNoStream)
+  // the streamed form when asked for and its ring fits beside the tag words
+  // (bg_wm_body.h; measured slower than this form on C4's slab and 2 KB
+  // slots)
+  const uint32_t slots = pair && (path_flags() & kPathWmStream)
                              ? wm_stream_slots(a.t.nbp, a.t.kw) : 0u;
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \

@@ -33,7 +33,11 @@ def rate(mpps):
 def main():
     line = open(sys.argv[1]).read().strip().splitlines()[-1]
     d = json.loads(line)
-    x = d["extra_configs"]
+    # (round 5 on: the §8f modules under "modules_8f", C1 at the top level)
+    x = dict(d.get("modules_8f", {}))
+    x.update(d["extra_configs"])
+    if "C1" in d:
+        x["C1"] = d["C1"]
     rows = []
     rows.append(("**C2** EM, 1 K rules (headline)", "%.4f ms" % d["roofline"]["kernel_ms"],
                  rate(d["value"]), "**%s**" % frac(d["roofline"]), tr(d["roofline"], 66),
@@ -62,6 +66,13 @@ def main():
             rows.append(("C4, the ahead-of-time kernel (same process)",
                          "%.4f / %.4f ms" % (a["ms_per_step"], a["slots_2k_ms_per_step"]),
                          "--", "--", "--", "--"))
+    em15 = x.get("EM_1500B")
+    if isinstance(em15, dict):
+        mc = em15.get("measured_ceiling") or {}
+        rows.append(("EM, 1 K rules, 1500 B packets (1496 B frames in 2 KB slots, 4 M)",
+                     "%.4f ms" % em15["ms_per_step"], rate(em15["Mpps"]),
+                     "%s (%.2f of s2k32)" % (frac(em15["roofline"]), mc.get("frac_of_ceiling", 0)),
+                     tr(em15["roofline"], 66), cpu(em15.get("cpu_baseline"))))
     c5 = x.get("C5")
     if c5:
         rows.append(("C5 EM, 1 M rules (1 GPU), table in L2/MALL", "%.4f ms" % c5["ms_per_step"],

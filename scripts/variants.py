@@ -28,7 +28,7 @@ from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 
 KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
-         "BG_WM_PHASE", "BG_WM_NO_STREAM",
+         "BG_WM_PHASE", "BG_WM_STREAM",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE"]
@@ -220,7 +220,7 @@ def main():
                     "enqueue": {"BG_WM_PHASE": 2},
                     "checks_no_l2": {"BG_WM_PHASE": 3}}
         # the streamed form (producer waves) and the one without
-        variants.update({k + "_nostream": dict(v, BG_WM_NO_STREAM=1)
+        variants.update({k + "_stream": dict(v, BG_WM_STREAM=1)
                          for k, v in list(variants.items())})
         r = time_variants(lambda: t.classify(d, 64, n, 8192, g), variants,
                           reps=20)

@@ -133,7 +133,7 @@ def test_jit_vs_oracle_random_layouts(seed, stride, n):
     assert t.table_info()[1] == 3  # tag words in LDS
     d_frames = torch.from_numpy(frames.reshape(-1)).cuda()
     outs = []
-    for flags in (0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_NO_STREAM):
+    for flags in (0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_STREAM):
         d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
         with LB.kernel_paths(flags):
             t.classify(d_frames, stride, n, 777, d_g)
