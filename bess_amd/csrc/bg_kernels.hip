@@ -1325,9 +1325,16 @@ __device__ __forceinline__ uint32_t tail_sum(const uint4 &c, int o, int hi) {
 }
 
 // RELOAD: phase 3 re-reads the header line (an L2 hit when it is still
-// resident) instead of holding it in 32 VGPRs through phase 2.
-template <bool RELOAD, int DEPTH>
+// resident) instead of holding it in 32 VGPRs through phase 2; 2 (STASH):
+// phase 1 parks the line in LDS (the wave's 64 lines, kCkStashStride
+// bytes apart) and phase 3 takes it from there -- no second read of the
+// line from L2 / HBM (A/B build: BG_CK_TILED=7).
+constexpr int kCkStashStride = 144;  // 128 B + 16: lanes' lines on other banks
+template <int RELOAD, int DEPTH>
 __device__ __forceinline__ void cksum_body(const CkArgs &a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ck_lds[];
+  uint4 *stash = reinterpret_cast<uint4 *>(
+      ck_lds + ((threadIdx.x >> 6) * 64 + (threadIdx.x & 63)) * kCkStashStride);
   const int lane = threadIdx.x & 63;
   const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
       ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -1350,6 +1357,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         h[4 * c + 1] = v.y;
         h[4 * c + 2] = v.z;
         h[4 * c + 3] = v.w;
+        if (RELOAD == 2) stash[c] = v;
       }
       L = ck_walk(mine, h, a.mode, stride);
     } else {
@@ -1408,7 +1416,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
     if (lane >= cnt) continue;
     // ---- phase 3: lane = frame
     if (RELOAD) {
-      const uint4 *q = reinterpret_cast<const uint4 *>(mine);
+      const uint4 *q = RELOAD == 2 ? stash : reinterpret_cast<const uint4 *>(mine);
 #pragma unroll
       for (int c = 0; c < kHdrDw / 4; c++) {
         const uint4 v = q[c];
@@ -1494,12 +1502,12 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
   }
 }
 
-template <bool RELOAD, int DEPTH>
+template <int RELOAD, int DEPTH>
 __global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
 void cksum_kernel(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
 
 #ifdef BG_AB
-template <bool RELOAD, int DEPTH>
+template <int RELOAD, int DEPTH>
 __global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
 __attribute__((amdgpu_waves_per_eu(5, 8)))
 void cksum_kernel_w5(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
@@ -1755,23 +1763,28 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (tiled) {
     // measured on MI355X (scripts/variants.py): re-reading the header line
     // in phase 3 beats holding it in registers; prefetch depth 2
-    kfn = cksum_kernel<true, 2>;
+    kfn = cksum_kernel<1, 2>;
 #ifdef BG_AB
     switch (knob("BG_CK_TILED", 0)) {
-      case 1: kfn = cksum_kernel<false, 1>; break;
-      case 2: kfn = cksum_kernel<true, 1>; break;
-      case 3: kfn = cksum_kernel<true, 3>; break;
-      case 4: kfn = cksum_kernel<false, 2>; break;
-      case 5: kfn = cksum_kernel_w5<true, 2>; break;
-      case 6: kfn = cksum_kernel_w5<true, 3>; break;
+      case 1: kfn = cksum_kernel<0, 1>; break;
+      case 2: kfn = cksum_kernel<1, 1>; break;
+      case 3: kfn = cksum_kernel<1, 3>; break;
+      case 4: kfn = cksum_kernel<0, 2>; break;
+      case 5: kfn = cksum_kernel_w5<1, 2>; break;
+      case 6: kfn = cksum_kernel_w5<1, 3>; break;
+      case 7: kfn = cksum_kernel<2, 2>; break;
       default: break;
     }
 #endif
   }
   const void *kern = reinterpret_cast<const void *>(kfn);
+  size_t lds = 0;
+#ifdef BG_AB  // the stash form's LDS: each wave's 64 header lines
+  if (kfn == reinterpret_cast<CkKern>(cksum_kernel<2, 2>)) lds = (size_t)kCkBlock * kCkStashStride;
+#endif
   int per_cu = knob("BG_CK_BLOCKS_PER_CU", 0);
   if (per_cu <= 0) {
-    const int occ = occupancy(kern, kCkBlock, 0, 7);
+    const int occ = occupancy(kern, kCkBlock, lds, 7);
     per_cu = occ * std::max(1, knob("BG_CK_GRID_MULT", 4));
   }
   const uint64_t waves_per_block = kCkBlock / 64;
@@ -1786,7 +1799,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
     waves = std::min<uint64_t>(a.n, max_waves);
   }
   const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kCkBlock), 0, s, a);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kCkBlock), lds, s, a);
   return hipGetLastError();
 }
 

@@ -141,6 +141,7 @@ def main():
                     "regs_d1": {"BG_CK_TILED": 1}, "reload_d1": {"BG_CK_TILED": 2},
                     "reload_d3": {"BG_CK_TILED": 3}, "regs_d2": {"BG_CK_TILED": 4},
                     "w5_d2": {"BG_CK_TILED": 5}, "w5_d3": {"BG_CK_TILED": 6},
+                    "stash_d2": {"BG_CK_TILED": 7},
                     "reload_d2_x8": {"BG_CK_GRID_MULT": 8},
                     "reload_d2_x2": {"BG_CK_GRID_MULT": 2}}
         outs = {}
