@@ -37,6 +37,8 @@
 //   slab130 : the same tile read, every line stored back in place (lane-
 //             contiguous 16 B stores) and the gates: UpdateTTL's / StaticNAT's
 //             traffic (130 B/packet basis)
+//   ck1502  : a wave per 2048 B slot reads its first 1496 bytes and stores
+//             two 2-byte words in place: C3's checksum traffic (1502 B basis)
 // `./hbm_probe GiB only SHAPE BLOCKS_PER_CU LAUNCHES` runs one shape (for
 // rocprofv3 --pmc passes: FETCH_SIZE per launch against a known shape).
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
@@ -217,6 +219,28 @@ __global__ __launch_bounds__(512) void slab130(u32x4 *src, size_t nslots, uint16
   }
 }
 
+// C3's checksum traffic alone: one wave per 2048 B slot reads the frame's
+// 1496 bytes (lanes contiguous, 16 B each: 94 chunks) and stores two 2-byte
+// words in place (the IPv4 and UDP checksum fields, offsets 24 and 40)
+__global__ __launch_bounds__(512) void ck1502(u32x4 *src, size_t nslots) {
+  const int lane = threadIdx.x & 63;
+  const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nslots;
+       t += nwaves) {
+    const u32x4 *g = src + t * 128;
+    u32x4 a = ldnt(g + lane);
+    if (lane < 94 - 64) {
+      const u32x4 b = ldnt(g + 64 + lane);
+      a.x ^= b.y;
+    }
+    uint32_t x = a.x ^ a.y ^ a.z ^ a.w;
+    x ^= __shfl_xor(x, 1);
+    uint16_t *f = reinterpret_cast<uint16_t *>(src + t * 128);
+    if (lane == 0) f[12] = (uint16_t)x;
+    if (lane == 1) f[20] = (uint16_t)(x >> 16);
+  }
+}
+
 #define CK(x)                                                            \
   do {                                                                   \
     hipError_t e = (x);                                                  \
@@ -246,15 +270,15 @@ int main(int argc, char **argv) {
   const bool sc = argc > 2 && argv[2][0] == 's';
   const bool only = argc > 5 && !strcmp(argv[2], "only");
   const bool cs = argc > 2 && argv[2][0] == 'c';
-  const char *names[13] = {"full16",  "em32",  "slot64", "half32", "wfull16", "w64s192", "w64s128",
-                           "s2k32",   "s2k64", "rnd36",  "rnd36s", "slab66",  "slab130"};
+  const char *names[14] = {"full16", "em32",  "slot64", "half32", "wfull16", "w64s192", "w64s128",
+                           "s2k32",  "s2k64", "rnd36",  "rnd36s", "slab66",  "slab130", "ck1502"};
   uint32_t *tab = nullptr;
   CK(hipMalloc(&tab, 36u << 20));
   CK(hipMemset(tab, 0x33, 36u << 20));
-  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 13 : 4;
+  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 14 : 4;
   int only_bpc = 0, only_launches = 0;
   if (only) {
-    for (int k = 0; k < 13; k++)
+    for (int k = 0; k < 14; k++)
       if (!strcmp(argv[3], names[k])) s0 = k, s1 = k + 1;
     only_bpc = atoi(argv[4]);
     only_launches = atoi(argv[5]);
@@ -268,7 +292,8 @@ int main(int argc, char **argv) {
       if (shape == 5) moved = (double)(bytes / 192) * 64;
       if (shape == 6) moved = (double)(bytes / 128) * 64;
       if (shape == 7 || shape == 8) pkts = (double)(bytes / 2048);
-      if (shape >= 7) moved = pkts * (shape == 12 ? 130 : 66);  // the algorithmic basis
+      if (shape == 13) pkts = (double)(bytes / 2048);
+      if (shape >= 7) moved = pkts * (shape == 13 ? 1502 : shape == 12 ? 130 : 66);  // the algorithmic basis
       auto launch = [&]() {
         if (shape == 0)
           hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
@@ -304,8 +329,10 @@ int main(int argc, char **argv) {
                              gates);
         else if (shape == 11)
           hipLaunchKernelGGL(slab66, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
-        else
+        else if (shape == 12)
           hipLaunchKernelGGL(slab130, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
+        else
+          hipLaunchKernelGGL(ck1502, dim3(blocks), dim3(512), 0, 0, src, bytes / 2048);
       };
       if (only) {  // a fixed number of launches, no timing (rocprofv3 passes)
         for (int w = 0; w < only_launches; w++) launch();
