@@ -149,12 +149,16 @@ BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
 // the consumer waves look up; ring slots: 64 x 32 B + two flag words
 constexpr int kStreamProducers = 1;
 constexpr int kStreamDepth = 16;  // tiles in flight per producer (vmcnt <= 63)
+constexpr int kStreamDepthDeep = 24;  // ... when the ring has the slots
+// a consumer wave's LDS: best[64] and a 64-entry queue (a tile of more
+// entries is checked in rounds of 64)
+constexpr uint32_t kStreamWaveLds = 64 * 8 + 64 * 4;
 constexpr uint32_t kStreamTileBytes = 64 * 32;
 constexpr uint32_t kStreamMaxSlots = 64;
 constexpr uint32_t kLdsMax = 160 * 1024;  // gfx950 LDS per workgroup
 BG_HD uint64_t wm_stream_fixed_lds(uint32_t nbp, uint32_t kw) {
   return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 +
-         (uint64_t)(kWmWaves - kStreamProducers) * kWmWaveLds;
+         (uint64_t)(kWmWaves - kStreamProducers) * kStreamWaveLds;
 }
 // ring slots that fit beside the tag words (0: too few for the producers'
 // depth, the streamed form does not apply)

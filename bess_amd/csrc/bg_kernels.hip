@@ -1328,7 +1328,10 @@ __device__ __forceinline__ uint32_t tail_sum(const uint4 &c, int o, int hi) {
 // resident) instead of holding it in 32 VGPRs through phase 2; 2 (STASH):
 // phase 1 parks the line in LDS (the wave's 64 lines, kCkStashStride
 // bytes apart) and phase 3 takes it from there -- no second read of the
-// line from L2 / HBM (A/B build: BG_CK_TILED=7).
+// line from L2 / HBM (A/B build: BG_CK_TILED=7); 3 (WORDS): phase 1 keeps
+// the two header words phase 3 needs (the old IPv4 checksum, bytes 24..25)
+// and phase 3 stores the checksum words alone -- no re-read and no line
+// store (BG_CK_TILED=8).
 constexpr int kCkStashStride = 144;  // 128 B + 16: lanes' lines on other banks
 template <int RELOAD, int DEPTH>
 __device__ __forceinline__ void cksum_body(const CkArgs &a) {
@@ -1348,6 +1351,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
     uint8_t *mine = a.frames + (p0 + (uint64_t)lane) * a.stride;
     uint32_t h[kHdrDw];
     CkLane L;
+    uint32_t ip_old = 0, w24 = 0, l4_old = 0;  // RELOAD == 3
     if (lane < cnt) {
       const uint4 *q = reinterpret_cast<const uint4 *>(mine);
 #pragma unroll
@@ -1360,6 +1364,11 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         if (RELOAD == 2) stash[c] = v;
       }
       L = ck_walk(mine, h, a.mode, stride);
+      if (RELOAD == 3) {
+        ip_old = L.ip_off == 14 ? hle16(h, 24) : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
+        w24 = hle16(h, 24);
+        l4_old = (L.flags & 16) ? ld_u16(mine + L.l4_ck) : 0u;  // (in the line: an L1 hit)
+      }
     } else {
 #pragma unroll
       for (int d = 0; d < kHdrDw; d++) h[d] = 0;
@@ -1415,7 +1424,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
     }
     if (lane >= cnt) continue;
     // ---- phase 3: lane = frame
-    if (RELOAD) {
+    if (RELOAD == 1 || RELOAD == 2) {
       const uint4 *q = RELOAD == 2 ? stash : reinterpret_cast<const uint4 *>(mine);
 #pragma unroll
       for (int c = 0; c < kHdrDw / 4; c++) {
@@ -1439,7 +1448,8 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
       } else if (a.verify) {
         ip_gate = fold16(L.s_ip) == 0xFFFFu ? 0u : 1u;
       } else {
-        const uint32_t old = L.ip_off == 14 ? hle16(h, 24)
+        const uint32_t old = RELOAD == 3 ? ip_old
+                             : L.ip_off == 14 ? hle16(h, 24)
                              : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
         ip_new = (~fold16(L.s_ip - old)) & 0xFFFFu;
         ip_wrote = true;
@@ -1457,13 +1467,13 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         l4_gate = kGateNone;
       } else {
         uint32_t s = L.s_l4 + tail;
-        uint32_t old = valid ? ld_u16(mine + L.l4_ck) : 0u;
+        uint32_t old = RELOAD == 3 ? l4_old : valid ? ld_u16(mine + L.l4_ck) : 0u;
         // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
         // the "L4 header" overlaps the IP checksum bytes 24..25.
         if (ip_wrote && L.ip_off == 14 && valid) {
           const int lo2 = (int)L.l4_lo > 24 ? (int)L.l4_lo : 24;
           const int hi2 = (int)L.l4_hi < 26 ? (int)L.l4_hi : 26;
-          s = s - dw_range_sum(hle16(h, 24), 24, lo2, hi2) +
+          s = s - dw_range_sum(RELOAD == 3 ? w24 : hle16(h, 24), 24, lo2, hi2) +
               dw_range_sum(ip_new, 24, lo2, hi2);
           if (L.l4_ck == 24) old = ip_new;
         }
@@ -1488,10 +1498,12 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
       // Store the whole 128 B header line first so the checksum words land
       // in a fully written L2 line (no read-modify-write of a partial line
       // in HBM), then the words themselves, in the reference's order.
-      uint4 *q = reinterpret_cast<uint4 *>(mine);
+      if (RELOAD != 3) {
+        uint4 *q = reinterpret_cast<uint4 *>(mine);
 #pragma unroll
-      for (int c = 0; c < kHdrDw / 4; c++)
-        q[c] = make_uint4(h[4 * c], h[4 * c + 1], h[4 * c + 2], h[4 * c + 3]);
+        for (int c = 0; c < kHdrDw / 4; c++)
+          q[c] = make_uint4(h[4 * c], h[4 * c + 1], h[4 * c + 2], h[4 * c + 3]);
+      }
       if (ip_wrote)
         *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
       if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
@@ -1761,9 +1773,13 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   using CkKern = void (*)(CkArgs);
   CkKern kfn = cksum_kernel_generic;
   if (tiled) {
-    // measured on MI355X (scripts/variants.py): re-reading the header line
-    // in phase 3 beats holding it in registers; prefetch depth 2
-    kfn = cksum_kernel<1, 2>;
+    // measured on MI355X (scripts/variants.py ck, profiles/r05/): phase 1
+    // keeping the two header words phase 3 needs and phase 3 storing the
+    // checksum words alone (no re-read of the line, no line store) beats
+    // re-reading the line (round 4's default, 0.2964 -> 0.2896 ms per 1 M
+    // frames, 31 B/pkt less fetched), holding it in registers (0.362) or
+    // parking it in LDS (0.368); prefetch depth 1
+    kfn = cksum_kernel<3, 1>;
 #ifdef BG_AB
     switch (knob("BG_CK_TILED", 0)) {
       case 1: kfn = cksum_kernel<0, 1>; break;
@@ -1773,6 +1789,9 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
       case 5: kfn = cksum_kernel_w5<1, 2>; break;
       case 6: kfn = cksum_kernel_w5<1, 3>; break;
       case 7: kfn = cksum_kernel<2, 2>; break;
+      case 8: kfn = cksum_kernel<3, 2>; break;
+      case 9: kfn = cksum_kernel<1, 2>; break;  // round 4's default
+      case 10: kfn = cksum_kernel_w5<3, 1>; break;
       default: break;
     }
 #endif

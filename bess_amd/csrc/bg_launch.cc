@@ -9,6 +9,7 @@
 
 #include "../../include/bessgpu.h"
 #include "bg_internal.h"
+#include "bg_kernels.h"
 
 namespace bg {
 
@@ -45,6 +46,16 @@ uint32_t path_flags() {
 // Entries are pushed once and never removed, so readers walk the list
 // without a lock; two threads racing on a new key both compute the same
 // answer and at worst push it twice.
+uint32_t stream_slots(uint32_t nbp, uint32_t kw) {
+  uint32_t r = wm_stream_slots(nbp, kw);
+#ifdef BG_AB
+  const int cap = knob("BG_WM_STREAM_SLOTS", 0);
+  if (cap > 0 && r > (uint32_t)cap)
+    r = cap > kStreamProducers * kStreamDepth + 4 ? (uint32_t)cap : 0u;
+#endif
+  return r;
+}
+
 int occupancy(const void *kernel, int block, size_t lds, int dflt) {
   for (OccEnt *e = g_occ.load(std::memory_order_acquire); e; e = e->next)
     if (e->kernel == kernel && e->lds == lds && e->block == block) return e->occ;

@@ -48,6 +48,11 @@ constexpr int knob(const char *, int dflt) { return dflt; }
 
 int occupancy(const void *kernel, int block, size_t lds, int dflt);
 
+// the WildcardMatch streamed form's ring slots (wm_stream_slots; the A/B
+// build caps them with BG_WM_STREAM_SLOTS, which also picks the shallower
+// producer depth)
+uint32_t stream_slots(uint32_t nbp, uint32_t kw);
+
 }  // namespace bg
 
 #endif  // BESS_AMD_BG_LAUNCH_H_

@@ -66,7 +66,7 @@ hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   // (bg_wm_body.h; measured slower than this form on C4's slab and 2 KB
   // slots)
   const uint32_t slots = pair && (path_flags() & kPathWmStream)
-                             ? wm_stream_slots(a.t.nbp, a.t.kw) : 0u;
+                             ? stream_slots(a.t.nbp, a.t.kw) : 0u;
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
     return slots ? launch_stream<KW>(a, slots, num_cus, s)                 \

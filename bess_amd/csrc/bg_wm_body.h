@@ -609,10 +609,11 @@ __device__ __forceinline__ void dma_pair(const uint8_t *__restrict__ frames, uin
                                    0, 0);
 }
 
-template <class Spec, int KW>
-__device__ __forceinline__ void wm_tags_stream_body(const WmArgs &a) {
+template <class Spec, int KW, int D>
+__device__ __forceinline__ void wm_stream_impl(const WmArgs &a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int P = kStreamProducers, C = kWaves - kStreamProducers, D = kStreamDepth;
+  constexpr int P = kStreamProducers, C = kWaves - kStreamProducers;
+  constexpr uint32_t kWaveLds = kStreamWaveLds, kQueue = 64;
   const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
   const uint64_t *mlds = wm_stage_tags<KW>(a, lds, tag_bytes);
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
@@ -780,6 +781,16 @@ __device__ __forceinline__ void wm_tags_stream_body(const WmArgs &a) {
     pending = true;
   }
   if (pending) wm_finish<Spec, KW>(a, tags, mlds, best, lane, nbp, pd);
+}
+
+// the producers' depth: kStreamDepthDeep tiles each when the ring has the
+// slots for it (wm_stream_slots), else kStreamDepth (a uniform branch)
+template <class Spec, int KW>
+__device__ __forceinline__ void wm_tags_stream_body(const WmArgs &a) {
+  if (a.ring_slots > (uint32_t)(kStreamProducers * kStreamDepthDeep + 4))
+    wm_stream_impl<Spec, KW, kStreamDepthDeep>(a);
+  else
+    wm_stream_impl<Spec, KW, kStreamDepth>(a);
 }
 
 }  // namespace

@@ -12,6 +12,12 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if len(sys.argv) > 1 and sys.argv[1].startswith("ab="):
+    # PMC passes of an A/B form: `ck_timing.py ab=8` launches
+    # cksum_kernel<3, 2> from the measurement build, three times
+    os.environ["BG_CK_TILED"] = sys.argv[1][3:]
+    from bess_amd import _lib  # noqa: E402
+    _lib.LIB_PATH = os.path.join(ROOT, "scripts", "bin", "libbessgpu_ab.so")
 from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
 
@@ -38,6 +44,12 @@ def main():
     del frames
     g = torch.empty(n, dtype=torch.int16, device=dev)
     fn = lambda: F.cksum(d, 2048, n, 3, False, None, g)  # noqa: E731
+    if len(sys.argv) > 1:
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        print(json.dumps({"launches": 3, "variant": sys.argv[1]}))
+        return
     out = {}
     out["bench_5_20"] = round(loop(fn, 5, 20), 4)
     out["bench_100_200"] = round(loop(fn, 100, 200), 4)

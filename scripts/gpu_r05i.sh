@@ -18,4 +18,8 @@ step timing 300 python -u scripts/ck_timing.py
 step c3 300 python -u bench.py --only cksum --no-cpu
 step probe 300 ./scripts/bin/hbm_probe 2 c
 step ck 600 python -u scripts/variants.py ck
+for v in 0 8; do
+  step pmc_f_$v 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_f_$v" -o pmc -- python3 "$GRAFT_REPO_ROOT/scripts/ck_timing.py" ab=$v
+  step pmc_w_$v 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_w_$v" -o pmc -- python3 "$GRAFT_REPO_ROOT/scripts/ck_timing.py" ab=$v
+done
 echo done >> "$OUT/steps.log"

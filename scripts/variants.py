@@ -137,13 +137,15 @@ def main():
         frames = P.cksum_workload(n, frame_len=1496)
         d = torch.from_numpy(frames.reshape(-1)).to(dev)
         l4 = torch.empty(n, dtype=torch.int16, device=dev)
-        variants = {"reload_d2": {}, "generic": {"BG_CK_GENERIC": 1},
+        variants = {"words_d1": {}, "reload_d2": {"BG_CK_TILED": 9},
+                    "generic": {"BG_CK_GENERIC": 1},
                     "regs_d1": {"BG_CK_TILED": 1}, "reload_d1": {"BG_CK_TILED": 2},
                     "reload_d3": {"BG_CK_TILED": 3}, "regs_d2": {"BG_CK_TILED": 4},
                     "w5_d2": {"BG_CK_TILED": 5}, "w5_d3": {"BG_CK_TILED": 6},
-                    "stash_d2": {"BG_CK_TILED": 7},
-                    "reload_d2_x8": {"BG_CK_GRID_MULT": 8},
-                    "reload_d2_x2": {"BG_CK_GRID_MULT": 2}}
+                    "stash_d2": {"BG_CK_TILED": 7}, "words_d2": {"BG_CK_TILED": 8},
+                    "words_d1_w5": {"BG_CK_TILED": 10},
+                    "words_d1_x8": {"BG_CK_GRID_MULT": 8},
+                    "words_d1_x2": {"BG_CK_GRID_MULT": 2}}
         outs = {}
         for name, env in variants.items():
             dd = torch.from_numpy(frames.reshape(-1)).to(dev)
@@ -236,6 +238,40 @@ def main():
             r[k]["Mpps"] = round(n2 / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
         out["wmphase_2k"] = r
         del d, g, f2
+    if "wmstream" in which:
+        # C4 (ahead-of-time kernel): every wave loading its own windows vs
+        # the streamed form at its deep producer depth (the ring C4's tag
+        # words leave) and at the shallow one (ring capped at 28 slots);
+        # header slab (8 M packets) and 2 KB slots (1 M); gates compared
+        rk, rm, prio, gates, frames, _ = P.wm_workload(100000, 1 << 20, stride=64,
+                                                      sizes=((60, 1),))
+        t = F.WmTable(P.FIVE_TUPLE)
+        for k, m, p, gg in zip(rk, rm, prio, gates):
+            t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
+        t.sync(0)
+        variants = {"per_wave": {}, "stream_deep": {"BG_WM_STREAM": 1},
+                    "stream_d16": {"BG_WM_STREAM": 1, "BG_WM_STREAM_SLOTS": 28}}
+        layouts = (("slab", torch.from_numpy(frames.reshape(-1)).to(dev).repeat(8), 64, 1 << 23),
+                   ("2k", torch.from_numpy(P.wm_workload(100000, 1 << 20, stride=2048)[4]
+                                           .reshape(-1)).to(dev), 2048, 1 << 20))
+        for name, d, stride, n in layouts:
+            g = torch.empty(n, dtype=torch.int16, device=dev)
+            ref = None
+            same = {}
+            for v, env in variants.items():
+                set_env(env)
+                g.fill_(0)
+                t.classify(d, stride, n, 8192, g)
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = g.clone()
+                same[v] = bool(torch.equal(g, ref))
+            r = time_variants(lambda: t.classify(d, stride, n, 8192, g), variants, reps=20)
+            for k in r:
+                r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+                r[k]["same_gates"] = same[k]
+            out["wmstream_" + name] = r
+            del d, g
     if "wm" in which.split(","):
         n = 1 << 22
         rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n, stride=64,
