@@ -15,8 +15,10 @@ step() {  # name timeout cmd...
   return 0
 }
 step tests 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_wm_jit.py tests/test_gpu_configs.py tests/test_gpu_pipe.py
+step forms 300 python -u scripts/ck_forms_parity.py
 step ck 600 python -u scripts/variants.py ck
 step wmstream 600 python -u scripts/variants.py wmstream
 step wm 600 python -u bench.py --only wm --no-cpu
 step c3 300 python -u bench.py --only cksum --no-cpu
+step probe 300 ./scripts/bin/hbm_probe 2 c
 echo done >> "$OUT/steps.log"

@@ -219,25 +219,19 @@ __global__ __launch_bounds__(512) void slab130(u32x4 *src, size_t nslots, uint16
   }
 }
 
-// C3's checksum traffic alone: one wave per 2048 B slot reads the frame's
-// 1496 bytes (lanes contiguous, 16 B each: 94 chunks) and stores two 2-byte
-// words in place (the IPv4 and UDP checksum fields, offsets 24 and 40)
+// C3's checksum traffic alone: the 94 16-byte chunks covering each 2048 B
+// slot's 1496-byte frame, read as one lane-contiguous stream (chunk u of the
+// grid = chunk u % 94 of slot u / 94), and two 2-byte words stored in place
+// per slot (the IPv4 and UDP checksum fields, offsets 24 and 40)
 __global__ __launch_bounds__(512) void ck1502(u32x4 *src, size_t nslots) {
-  const int lane = threadIdx.x & 63;
-  const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
-  for (size_t t = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nslots;
-       t += nwaves) {
-    const u32x4 *g = src + t * 128;
-    u32x4 a = ldnt(g + lane);
-    if (lane < 94 - 64) {
-      const u32x4 b = ldnt(g + 64 + lane);
-      a.x ^= b.y;
-    }
-    uint32_t x = a.x ^ a.y ^ a.z ^ a.w;
-    x ^= __shfl_xor(x, 1);
-    uint16_t *f = reinterpret_cast<uint16_t *>(src + t * 128);
-    if (lane == 0) f[12] = (uint16_t)x;
-    if (lane == 1) f[20] = (uint16_t)(x >> 16);
+  const uint32_t step = gridDim.x * blockDim.x, total = (uint32_t)(nslots * 94);
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += step) {
+    const uint32_t slot = u / 94u, c = u - slot * 94u;  // (32-bit: a multiply-high)
+    const u32x4 a = ldnt(src + (size_t)slot * 128 + c);
+    const uint32_t x = a.x ^ a.y ^ a.z ^ a.w;
+    uint16_t *f = reinterpret_cast<uint16_t *>(src + (size_t)slot * 128);
+    if (c == 1) f[12] = (uint16_t)x;  // bytes 24..25 (chunk 1)
+    if (c == 2) f[20] = (uint16_t)x;  // bytes 40..41 (chunk 2)
   }
 }
 

@@ -144,6 +144,8 @@ def main():
                     "w5_d2": {"BG_CK_TILED": 5}, "w5_d3": {"BG_CK_TILED": 6},
                     "stash_d2": {"BG_CK_TILED": 7}, "words_d2": {"BG_CK_TILED": 8},
                     "words_d1_w5": {"BG_CK_TILED": 10},
+                    "wide_d1": {"BG_CK_TILED": 11}, "wide_d2": {"BG_CK_TILED": 12},
+                    "wide_d3": {"BG_CK_TILED": 13},
                     "words_d1_x8": {"BG_CK_GRID_MULT": 8},
                     "words_d1_x2": {"BG_CK_GRID_MULT": 2}}
         outs = {}
