@@ -65,6 +65,9 @@ def parse():
                     help="skip the host end-to-end legs (16 launching threads "
                          "crash rocprofv3's kernel tracer)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed device work before each leg's warm-up "
+                         "(clock_settle); 0 = none")
     ap.add_argument("--cpu-table-only", action="store_true",
                     help="no GPU: the N-rank sharded table build of C5 over "
                          "gloo (CPU tests of the multi-GPU launch and control "
@@ -286,6 +289,7 @@ def run_em(args, rank, world, dev, torch, dist):
     torch.cuda.synchronize()
     parity = em_parity_sample(t, d_frames, d_gates, keys, gates,
                               min(n, 1 << 20), torch)
+    clock_settle(args, torch)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -417,6 +421,7 @@ def run_cksum(args, dev, torch):
     got = d[:4096 * 2048].cpu().numpy().reshape(4096, 2048)
     parity = bool((got == ref).all() and
                   (l4g[:4096].cpu().numpy().view(np.uint16) == l4w).all())
+    clock_settle(args, torch)
     for _ in range(args.warmup):  # recompute is idempotent
         F.cksum(d, 2048, n, 3, False, None, l4g)
     torch.cuda.synchronize()
@@ -926,9 +931,29 @@ def run_plugin_pool(args):
     return out
 
 
+def clock_settle(args, torch):
+    """Untimed, before a leg's warm-up: ~args.settle_ms of back-to-back
+    device work (a 64 MB in-place multiply; not the leg's kernel, so legs
+    that modify their packets in place keep their launch budget). A leg
+    starts after host work (its table build, the parity check) that left the
+    GPU idle, and the first ~25 launches over a fresh slab then run ~14 %
+    slow (profiles/r05/ck_timing_r05i.json): with the driver's --warmup 5 the
+    timed region would measure the clock ramp, not the kernel."""
+    if args.settle_ms <= 0:
+        return
+    x = torch.ones(16 << 20, dtype=torch.float32, device="cuda")
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < args.settle_ms:
+        for _ in range(16):
+            x.mul_(1.0)
+        torch.cuda.synchronize()
+    del x
+
+
 def _time_steps(step, args, torch):
     """warmup, then ms per launch over args.steps launches (HIP events on
     the launching stream)"""
+    clock_settle(args, torch)
     for _ in range(max(3, args.warmup // 4)):
         step()
     torch.cuda.synchronize()
@@ -1285,6 +1310,7 @@ def run_dnat(args, dev, torch):
     torch.cuda.synchronize()
     parity = bool((g[:k].cpu().numpy().view(np.uint16) == want).all() and
                   (copies[0][:k * 64].cpu().numpy().reshape(k, 64) == ref).all())
+    clock_settle(args, torch)
     timer = Timer(torch)
     timer.start()
     for i in range(reps):
@@ -1412,6 +1438,7 @@ def run_wm(args, dev, torch):
 
     def timed(slab, stride, gates, flags=0):
         with LB.kernel_paths(flags):
+            clock_settle(args, torch)
             for _ in range(args.warmup):
                 t.classify(slab, stride, n, 8192, gates)
             torch.cuda.synchronize()
@@ -1580,6 +1607,7 @@ def run_c5(args, dev, torch):
     torch.cuda.synchronize()
     ns = sample.shape[0]
     parity = c5_parity(keys, gates, sample, dg[:ns].cpu().numpy().view(np.uint16))
+    clock_settle(args, torch)
     for _ in range(args.warmup):
         t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
@@ -1685,6 +1713,7 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
     torch.cuda.synchronize()
     ns = sample.shape[0]
     parity = c5_parity(keys, gates, sample, dg[:ns].cpu().numpy().view(np.uint16))
+    clock_settle(args, torch)
     for _ in range(args.warmup):
         t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
@@ -1893,7 +1922,7 @@ def main():
         "metric": "Mpps + %HBM-roofline, device-resident parse+match, "
                   "64B/1500B, 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "Mpps", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup,
+        "steps": args.steps, "warmup": args.warmup, "settle_ms": args.settle_ms,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded 5-tuple traffic, 50% rule hits)",
