@@ -65,6 +65,8 @@ def parse():
                     help="skip the host end-to-end legs (16 launching threads "
                          "crash rocprofv3's kernel tracer)")
     ap.add_argument("--cpu-seconds", type=float, default=6.0)
+    ap.add_argument("--diag", action="store_true",
+                    help="host-leg diagnostics (pipe counters, cycles) to stderr")
     ap.add_argument("--settle-ms", type=float, default=100.0,
                     help="untimed device work before each leg's warm-up "
                          "(clock_settle); 0 = none")
@@ -802,9 +804,11 @@ def run_plugin_pipeline(args):
             exp = ["D" if int(w) >= 8192 else str(int(w)) for w in want]
             parity[str(t)] = outs[1].split()[1:] == exp
             cpu_parity[str(t)] = outs[3].split()[1:] == exp
-    # worker 0's pipe counters and cycles: diagnostics, to stderr (the line
-    # stays short enough for the driver's record to keep its configs)
-    log("e2e_plugin worker0_pipe_stats " + json.dumps(pipe_stats))
+    # worker 0's pipe counters and cycles: diagnostics, to stderr with
+    # --diag only (the driver's record keeps ~8 KB of stdout + stderr: the
+    # line's last sections must fit)
+    if args.diag:
+        log("e2e_plugin worker0_pipe_stats " + json.dumps(pipe_stats))
     return {"what": "Source -> ExactMatch plugin (deferred: per-worker bg_pipe, "
                     "task emits) -> Sink, 32-pkt batches, 1000 rules, %d 64B "
                     "pkts in 2624 B snbufs split over the workers as the "
@@ -916,7 +920,8 @@ def run_plugin_pool(args):
                 diag["cycles_w0_gpu"] = cyc[1][7:]
             if len(cyc) >= 4:
                 diag["cycles_w0_cpu"] = cyc[3][7:]
-            log("e2e_plugin_pool %s %s" % (name, json.dumps(diag)))
+            if args.diag:
+                log("e2e_plugin_pool %s %s" % (name, json.dumps(diag)))
             if len(st) >= 2:  # the submit cost per packet (the copy it saves)
                 f = st[1].split()
                 out[name]["submit_cyc_per_pkt"] = float(f[f.index("submit_cyc_per_pkt") + 1])
