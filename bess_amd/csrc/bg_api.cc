@@ -193,6 +193,11 @@ FieldPlan make_plan(const std::vector<bg_field> &fields, bool em_masks,
 void relayout(TableLayout &L, uint32_t nbp) {
   L.nbp = nbp;
   L.keys_off = align256((uint64_t)nbp * 4);
+  if (L.rec) {  // slot records (bg_table.h)
+    L.vals_off = L.keys_off + (uint64_t)L.kw * 8;
+    L.part_bytes = align256(L.keys_off + (uint64_t)nbp * kSlots * L.rec * 8);
+    return;
+  }
   L.vals_off = align256(L.keys_off + (uint64_t)nbp * kSlots * L.kw * 8);
   L.part_bytes =
       align256(L.vals_off + (L.vik ? 0 : (uint64_t)nbp * kSlots * L.val_bytes));
@@ -252,6 +257,7 @@ TableRef table_ref(const uint8_t *base, uint64_t bytes, const TableLayout &L,
   t.filt_words = filt_words;
   t.vik = L.vik;
   t.filt_off = filt_off;
+  t.rec = L.rec;
   t.lds = tb <= kLdsTableMax ? kLdsTable
           : tags_lds       ? kLdsTags
           : filt_words     ? kLdsFilter
@@ -279,8 +285,10 @@ int build_image(uint32_t kw, uint32_t val_bytes, uint32_t nparts,
   for (auto &m : members) maxc = std::max(maxc, m.size());
   TableLayout L = plan_layout(maxc, kw, val_bytes, nparts, kDefaultSeed, max_load, vik);
   L.probe = probe;
-  // WildcardMatch (probe 1): the bucket count the load asks for, not the
-  // next power of two (wm_probe takes any count)
+  // WildcardMatch (probe 1): key and value in one record per slot (a check
+  // is one L2 request, not two); the bucket count the load asks for, not
+  // the next power of two (wm_probe takes any count)
+  if (probe) L.rec = val_bytes == 8 && !vik ? wm_rec_words(kw) : 0u;
   if (probe)
     relayout(L, std::max<uint32_t>(2, (uint32_t)((double)maxc / (kSlots * max_load)) + 1));
   for (int attempt = 0; attempt < 8; attempt++) {
@@ -1241,7 +1249,14 @@ static bool wm_direct_spec(const bg_wm *wm, size_t t, uint32_t *spec) {
 // The direct tuples of a tag-word image: up to kMaxDirect tuples of one or
 // two mask bytes, one-byte masks first (their 2 KB tables stay in L2),
 // then the tuples with the most entries (each saves a hash, two tag reads
-// and its queue entries for every packet it matches).
+// and its queue entries for every packet it matches). A direct tuple costs
+// every packet one random L2 read; hashed, it costs an L2 read (one slot
+// record) only for the packets whose fingerprint it holds -- about its
+// density, entries / 65536, for a two-byte mask. The kernel's rate is
+// bounded by its L2 requests in flight per CU (DESIGN §3, C4 counters), so
+// a two-byte tuple goes direct only when at least half its 65536 keys are
+// rules.
+constexpr size_t kDirect2MinEntries = 32768;
 static void wm_pick_direct(bg_wm *wm) {
   struct Cand {
     bool two;  // two mask bytes
@@ -1252,7 +1267,11 @@ static void wm_pick_direct(bg_wm *wm) {
   for (size_t t = 0; t < wm->tuples.size(); t++) {
     uint32_t spec;
     if (!wm_direct_spec(wm, t, &spec) || wm->tuples[t].ht.empty()) continue;
-    cand.push_back({(spec >> 24) != 0, wm->tuples[t].ht.size(), (uint32_t)t});
+    const bool two = (spec >> 24) != 0;
+    if (two && wm->tuples[t].ht.size() <
+                   (size_t)knob("BG_WM_DIRECT2_MIN", (int)kDirect2MinEntries))
+      continue;
+    cand.push_back({two, wm->tuples[t].ht.size(), (uint32_t)t});
   }
   std::sort(cand.begin(), cand.end(), [](const Cand &a, const Cand &b) {
     if (a.two != b.two) return !a.two;

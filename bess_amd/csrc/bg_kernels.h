@@ -90,6 +90,10 @@ struct TableRef {
   uint32_t filt_words;            // 0: no filter
   uint32_t vik;                   // EM value in the key's top 2 bytes
   uint64_t filt_off;              // byte offset of the filter in the image
+  // words per slot record (bg_table.h; 0: separate key / value arrays).
+  // WildcardMatch kernels take wm_rec_words(kw) as a constant and their
+  // launchers refuse an image laid out otherwise.
+  uint32_t rec;
 };
 
 struct EmArgs {

@@ -17,6 +17,7 @@ TableLayout plan_layout(size_t max_part_entries, uint32_t kw,
   TableLayout L;
   L.vik = vik && val_bytes == 2 ? 1u : 0u;
   L.probe = 0;
+  L.rec = 0;
   L.kw = kw;
   L.val_bytes = val_bytes;
   L.nparts = nparts;
@@ -97,6 +98,12 @@ bool build_partition(const TableLayout &L, uint32_t part, size_t n,
     if (e < 0) continue;
     uint32_t b = sl / kSlots, s = sl % kSlots;
     tags[b] |= pr[e].tag << (8 * s);
+    if (L.rec) {  // key words, then the value, in the slot's record
+      memcpy(kslots + (uint64_t)sl * L.rec, keys + (uint64_t)e * L.kw, L.kw * 8);
+      memcpy(kslots + (uint64_t)sl * L.rec + L.kw, vals + (uint64_t)e * L.val_bytes,
+             L.val_bytes);
+      continue;
+    }
     memcpy(kslots + (uint64_t)sl * L.kw, keys + (uint64_t)e * L.kw, L.kw * 8);
     if (L.vik) {  // value in the key's last two bytes
       uint16_t v;

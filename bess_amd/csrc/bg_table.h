@@ -17,6 +17,9 @@
 //
 // Partition image (all offsets 256-byte aligned, `part_bytes` per part):
 //   [tags: nbp x u32][keys: nbp x 4 x kw x u64][vals: nbp x 4 x val_bytes]
+// or, for WildcardMatch (`rec` words per record), one record per slot:
+//   [tags: nbp x u32][records: nbp x 4 x (kw key words, the u64 value, pad)]
+// so that a check's key and value lie in one 64 B line (one L2 request).
 #ifndef BESS_AMD_BG_TABLE_H_
 #define BESS_AMD_BG_TABLE_H_
 
@@ -64,7 +67,19 @@ struct TableLayout {
   // 1: wm_probe of a 32-bit wm_hash value (WildcardMatch, one partition;
   // nbp any number >= 2)
   uint32_t probe;
+  // 0: separate key and value arrays; else the words per slot record (key
+  // words, then the 8-byte value at word kw; wm_rec_words), vals_off =
+  // keys_off + 8 kw
+  uint32_t rec;
 };
+
+// WildcardMatch slot records: the key words and the value, padded to a
+// power of two (kw 2: 32 B, so a record never straddles a 64 B line)
+BG_HD uint32_t wm_rec_words(uint32_t kw) {
+  uint32_t r = 1;
+  while (r < kw + 1) r <<= 1;
+  return r;
+}
 
 BG_HD uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 

@@ -189,9 +189,9 @@ __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags
 #ifdef BG_AB  // phase timing: checks without their L2 loads
         if (a.ab_phase == 3) continue;
 #endif
-        v[r] = vals[slot];
+        v[r] = vals[(uint64_t)slot * wm_rec_words(KW)];
 #pragma unroll
-        for (int j = 0; j < KW; j++) sk[r][j] = keys[(uint64_t)slot * KW + j];
+        for (int j = 0; j < KW; j++) sk[r][j] = keys[(uint64_t)slot * wm_rec_words(KW) + j];
       }
     }
   }
@@ -222,10 +222,10 @@ __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags
           z1[r] &= z1[r] - 1;
         else
           z2[r] &= z2[r] - 1;
-        const uint64_t vv = vals[slot];
+        const uint64_t vv = vals[(uint64_t)slot * wm_rec_words(KW)];
         uint64_t s2[KW];
 #pragma unroll
-        for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * KW + j];
+        for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * wm_rec_words(KW) + j];
         if (wm_hit<KW>(mlds, e[r], vv, s2, kk[r])) {
           wm_fold(best, e[r], vv);
           z1[r] = z2[r] = 0;
@@ -527,10 +527,10 @@ __device__ __forceinline__ void wm_finish(const WmArgs &a, const uint32_t *tags,
         p.z1 &= p.z1 - 1;
       else
         p.z2 &= p.z2 - 1;
-      const uint64_t vv = vals[slot];
+      const uint64_t vv = vals[(uint64_t)slot * wm_rec_words(KW)];
       uint64_t s2[KW];
 #pragma unroll
-      for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * KW + j];
+      for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * wm_rec_words(KW) + j];
       if (wm_hit<KW>(mlds, p.e, vv, s2, p.kk)) {
         wm_fold(best, p.e, vv);
         p.z1 = p.z2 = 0;
@@ -746,9 +746,9 @@ __device__ __forceinline__ void wm_stream_impl(const WmArgs &a) {
           pd.z1 = bucket_matches(tags, b1, pd.e);
           pd.z2 = bucket_matches(tags, wm_b2(b1, pd.e >> 24, nbp), pd.e);
           const uint32_t slot = next_slot(pd.e, nbp, pd.z1, pd.z2);
-          pd.v = vals[slot];
+          pd.v = vals[(uint64_t)slot * wm_rec_words(KW)];
 #pragma unroll
-          for (int q2 = 0; q2 < KW; q2++) pd.sk[q2] = keys[(uint64_t)slot * KW + q2];
+          for (int q2 = 0; q2 < KW; q2++) pd.sk[q2] = keys[(uint64_t)slot * wm_rec_words(KW) + q2];
         }
       }
     } else {

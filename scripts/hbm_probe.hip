@@ -37,8 +37,12 @@
 //   slab130 : the same tile read, every line stored back in place (lane-
 //             contiguous 16 B stores) and the gates: UpdateTTL's / StaticNAT's
 //             traffic (130 B/packet basis)
-//   ck1502  : a wave per 2048 B slot reads its first 1496 bytes and stores
-//             two 2-byte words in place: C3's checksum traffic (1502 B basis)
+//   ck1502  : the 94 16 B chunks of each 2048 B slot's 1496 B frame as one
+//             lane-contiguous stream, two 2-byte words stored in place per
+//             slot: C3's checksum traffic (1502 B basis)
+//   slab66c : slab66 with each wave taking runs of 8 consecutive tiles
+//   slab66g : slab66c with the run's 512 gates gathered in LDS and stored as
+//             one 1 KB block (16 B per lane)
 // `./hbm_probe GiB only SHAPE BLOCKS_PER_CU LAUNCHES` runs one shape (for
 // rocprofv3 --pmc passes: FETCH_SIZE per launch against a known shape).
 // Prints one JSON line per (shape, blocks/CU) with sustained TB/s of slab
@@ -201,6 +205,37 @@ __global__ __launch_bounds__(512) void slab66(const u32x4 *src, size_t nslots,
   }
 }
 
+// slab66 with each wave taking runs of 8 consecutive tiles (512 slots,
+// 32 KB); GW = 1: the 8 tiles' gates gathered in LDS and stored as one
+// 1 KB block (16 B per lane), GW = 0: stored per tile as slab66 does
+template <int GW>
+__global__ __launch_bounds__(512) void slab66g(const u32x4 *src, size_t nslots,
+                                               uint16_t *gates) {
+  __shared__ uint16_t gl[8][512];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  for (size_t r = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r * 512 < nslots;
+       r += nwaves) {
+#pragma unroll 1
+    for (int k = 0; k < 8; k++) {
+      const size_t t = r * 8 + k;
+      const u32x4 *g = src + t * 256;
+      const u32x4 a = ldnt(g + lane), b = ldnt(g + 64 + lane), c = ldnt(g + 128 + lane),
+                  d = ldnt(g + 192 + lane);
+      const uint16_t x = (uint16_t)(a.x ^ b.y ^ c.z ^ d.w);
+      if (GW)
+        gl[wid][k * 64 + lane] = x;
+      else
+        gates[t * 64 + lane] = x;
+    }
+    if (GW) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes
+      reinterpret_cast<u32x4 *>(gates + r * 512)[lane] =
+          reinterpret_cast<const u32x4 *>(gl[wid])[lane];
+    }
+  }
+}
+
 // slab66 with every line written back (in place)
 __global__ __launch_bounds__(512) void slab130(u32x4 *src, size_t nslots, uint16_t *gates) {
   const int lane = threadIdx.x & 63;
@@ -264,15 +299,16 @@ int main(int argc, char **argv) {
   const bool sc = argc > 2 && argv[2][0] == 's';
   const bool only = argc > 5 && !strcmp(argv[2], "only");
   const bool cs = argc > 2 && argv[2][0] == 'c';
-  const char *names[14] = {"full16", "em32",  "slot64", "half32", "wfull16", "w64s192", "w64s128",
-                           "s2k32",  "s2k64", "rnd36",  "rnd36s", "slab66",  "slab130", "ck1502"};
+  const char *names[16] = {"full16", "em32",  "slot64", "half32", "wfull16", "w64s192", "w64s128",
+                           "s2k32",  "s2k64", "rnd36",  "rnd36s", "slab66",  "slab130", "ck1502",
+                           "slab66c", "slab66g"};
   uint32_t *tab = nullptr;
   CK(hipMalloc(&tab, 36u << 20));
   CK(hipMemset(tab, 0x33, 36u << 20));
-  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 14 : 4;
+  int s0 = wr ? 4 : sc ? 7 : cs ? 11 : 0, s1 = wr ? 7 : sc ? 11 : cs ? 16 : 4;
   int only_bpc = 0, only_launches = 0;
   if (only) {
-    for (int k = 0; k < 14; k++)
+    for (int k = 0; k < 16; k++)
       if (!strcmp(argv[3], names[k])) s0 = k, s1 = k + 1;
     only_bpc = atoi(argv[4]);
     only_launches = atoi(argv[5]);
@@ -288,6 +324,7 @@ int main(int argc, char **argv) {
       if (shape == 7 || shape == 8) pkts = (double)(bytes / 2048);
       if (shape == 13) pkts = (double)(bytes / 2048);
       if (shape >= 7) moved = pkts * (shape == 13 ? 1502 : shape == 12 ? 130 : 66);  // the algorithmic basis
+      if (shape >= 14 && nslots % 512) continue;  // (whole 512-slot runs only)
       auto launch = [&]() {
         if (shape == 0)
           hipLaunchKernelGGL(full16, dim3(blocks), dim3(512), 0, 0, src,
@@ -325,8 +362,12 @@ int main(int argc, char **argv) {
           hipLaunchKernelGGL(slab66, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
         else if (shape == 12)
           hipLaunchKernelGGL(slab130, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
-        else
+        else if (shape == 13)
           hipLaunchKernelGGL(ck1502, dim3(blocks), dim3(512), 0, 0, src, bytes / 2048);
+        else if (shape == 14)
+          hipLaunchKernelGGL(slab66g<0>, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
+        else
+          hipLaunchKernelGGL(slab66g<1>, dim3(blocks), dim3(512), 0, 0, src, nslots, gates);
       };
       if (only) {  // a fixed number of launches, no timing (rocprofv3 passes)
         for (int w = 0; w < only_launches; w++) launch();

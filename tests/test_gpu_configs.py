@@ -234,7 +234,9 @@ def test_c4_header_slab_full_size():
         with LB.kernel_paths(flags):
             t.classify(h, 64, n0 * rep, 8192, d_g)
             torch.cuda.synchronize()
-        assert t.table_info()[1] == 3 and t.direct_tuples() == 2
+        # the /8 destination tuple is direct; the source port's 12.5 K rules
+        # (a fifth of the 65536 ports) stay hashed (bg_api.cc kDirect2MinEntries)
+        assert t.table_info()[1] == 3 and t.direct_tuples() == 1
         assert (d_g.cpu().numpy().view(np.uint16).reshape(rep, n0) == want).all(), flags
 
 

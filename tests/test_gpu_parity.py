@@ -350,6 +350,29 @@ def test_wm_direct_tuples_vs_oracle(dev):
     check(keep)
 
 
+def test_wm_dense_two_byte_direct_tuple(dev):
+    """A two-byte tuple goes direct (a 65536-entry table read once per
+    packet) only when at least half its keys are rules (bg_api.cc
+    kDirect2MinEntries); a sparser one is hashed. Both, against the oracle,
+    every table path."""
+    for nrules, nd in ((150000, 1), (30000, 0)):  # ~35 K of 50 K ports distinct; ~9.6 K
+        masks = [P._m(sport=0xFFFF), P._m(sip=0xFFFFFFFF, dport=0xFFFF),
+                 P._m(sip=0xFFFF0000, dip=0xFFFF0000)]
+        n = 65536
+        rk, rm, prio, gates, frames, _ = P.wm_workload(nrules, n, seed=93, stride=64,
+                                                      sizes=((60, 1),), masks=masks)
+        t = F.WmTable(P.FIVE_TUPLE)
+        for k, m, p, g in zip(rk, rm, prio, gates):
+            t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+        got = classify_all_paths_wm(t, to_dev(frames, dev), 64, n, 77, dev, 1)
+        assert t.table_info()[1] == 3 and t.direct_tuples() == nd, nrules
+        wm = oracle_wm(P.FIVE_TUPLE, rk, rm, prio, gates)
+        want = np.zeros(n, np.uint16)
+        O.lib().or_wm_process(wm, frames.ctypes.data, 64, n, 77, want.ctypes.data)
+        O.lib().or_wm_free(wm)
+        assert (got == want).all(), nrules
+
+
 @pytest.mark.parametrize("ndirect", [0, 1])
 def test_wm_tags_fewer_direct_tuples(dev, ndirect):
     """Tag-word images with no or one direct tuple (masks of three bytes and

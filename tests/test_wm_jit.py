@@ -89,8 +89,9 @@ def test_source_carries_the_image_constants():
     assert "bg_wm_jit_pair" in src and "bg_wm_jit_n2" in src
     assert "bg_wm_jit_stream" in src
     assert "bg_wm_jit_n4" not in src
-    # the /8 destination and the source-port tuples are direct tuples
-    assert "ndirect(const WmArgs &) { return 2u; }" in src
+    # the /8 destination tuple is direct; the source port's 2.5 K rules
+    # are too sparse a two-byte tuple to be (bg_api.cc kDirect2MinEntries)
+    assert "ndirect(const WmArgs &) { return 1u; }" in src
 
 
 def test_compiles_for_gfx950():
