@@ -243,6 +243,43 @@ def main():
             r[k]["Mpps"] = round(n2 / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
         out["wmphase_2k"] = r
         del d, g, f2
+    if "wmdirect" in which:
+        # C4 with the source-port tuple direct (the round-4 policy: every
+        # two-byte tuple, BG_WM_DIRECT2_MIN=0) vs hashed (>= 32768 rules);
+        # each table built under its setting; header slab and 2 KB slots
+        rk, rm, prio, gates, frames, _ = P.wm_workload(100000, 1 << 20, stride=64,
+                                                      sizes=((60, 1),))
+        f2 = torch.from_numpy(P.wm_workload(100000, 1 << 20, stride=2048)[4]
+                              .reshape(-1)).to(dev)
+        d = torch.from_numpy(frames.reshape(-1)).to(dev).repeat(8)
+        res = {}
+        ref = {}
+        for name, env in (("sport_hashed", {}), ("sport_direct", {"BG_WM_DIRECT2_MIN": 0})):
+            set_env(env)
+            os.environ.pop("BG_WM_DIRECT2_MIN", None)
+            os.environ.update({k: str(v) for k, v in env.items()})
+            t = F.WmTable(P.FIVE_TUPLE)
+            for k, m, p, gg in zip(rk, rm, prio, gates):
+                t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
+            t.sync(0)
+            t.jit_wait()  # (time the run-time compiled kernel of this shape)
+            os.environ.pop("BG_WM_DIRECT2_MIN", None)
+            r = {"direct_tuples": t.direct_tuples()}
+            for lay, dd, stride, n in (("slab", d, 64, 1 << 23), ("2k", f2, 2048, 1 << 20)):
+                g = torch.empty(n, dtype=torch.int16, device=dev)
+                t.classify(dd, stride, n, 8192, g)
+                torch.cuda.synchronize()
+                if lay in ref:
+                    r[lay + "_same_gates"] = bool(torch.equal(g, ref[lay]))
+                else:
+                    ref[lay] = g.clone()
+                tt = time_variants(lambda: t.classify(dd, stride, n, 8192, g), {"x": {}},
+                                   reps=20)["x"]
+                r[lay] = tt
+            res[name] = r
+            del t
+        out["wmdirect"] = res
+        del d, f2
     if "wmstream" in which:
         # C4 (ahead-of-time kernel): every wave loading its own windows vs
         # the streamed form at its deep producer depth (the ring C4's tag
