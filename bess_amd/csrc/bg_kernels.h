@@ -144,8 +144,11 @@ constexpr int kWmBlock = 1024;
 constexpr int kWmWaves = kWmBlock / 64;
 constexpr uint32_t kWmQueue = 256;
 constexpr uint32_t kWmWaveLds = 64 * 8 + kWmQueue * 4;
+// (after the tuple masks: the one-byte direct tuples' 256-entry tables,
+// kMaxDirect x 2 KB, read from LDS instead of one L2 request per packet)
+constexpr uint32_t kWmDirLds = 2048u * 2;
 BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
-  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 +
+  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
          (uint64_t)kWmWaves * kWmWaveLds;
 }
 // the streamed form (bg_wm_body.h wm_tags_stream_body): producer waves load
@@ -161,7 +164,7 @@ constexpr uint32_t kStreamTileBytes = 64 * 32;
 constexpr uint32_t kStreamMaxSlots = 64;
 constexpr uint32_t kLdsMax = 160 * 1024;  // gfx950 LDS per workgroup
 BG_HD uint64_t wm_stream_fixed_lds(uint32_t nbp, uint32_t kw) {
-  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 +
+  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
          (uint64_t)(kWmWaves - kStreamProducers) * kStreamWaveLds;
 }
 // ring slots that fit beside the tag words (0: too few for the producers'

@@ -299,6 +299,20 @@ __device__ __forceinline__ void pair_window(const uint32_t (&r)[8], int lane,
   w[9] = 0;
 }
 
+// direct tuple d's value for key k: a one-byte tuple's from its LDS copy
+// (after the tuple masks, wm_stage_tags), a two-byte tuple's from its
+// 65536-entry table in the image
+template <class Spec, int KW>
+__device__ __forceinline__ uint64_t wm_direct_value(const WmArgs &a, const uint64_t *mlds,
+                                                    const uint64_t (&k)[KW], int d) {
+  const uint32_t spec = Spec::dspec(a, d);
+  const uint32_t ix = direct_index_k<KW>(k, spec);
+  if ((spec >> 24) == 0) return mlds[kMaxTuples * KW + d * 256 + ix];
+  const uint64_t off = reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
+      tuple_words(a, offsetof(WmArgs, doff)))[d];
+  return reinterpret_cast<const uint64_t *>(a.t.base + off)[ix];
+}
+
 // One tile's lookups (lane = packet idx, its header window w): steps 1-5 of
 // the file comment. `prefetch` runs right after the direct tuples' reads are
 // issued (wm_tags_body issues the next tile's window there: vector loads
@@ -317,13 +331,7 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
 #pragma unroll
   for (int d = 0; d < kMaxDirect; d++) {
     dv[d] = ~0ull;
-    if ((uint32_t)d < ndir && live) {
-      const uint64_t off =
-          reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
-              tuple_words(a, offsetof(WmArgs, doff)))[d];
-      dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)
-          [direct_index_k<KW>(k, Spec::dspec(a, d))];
-    }
+    if ((uint32_t)d < ndir && live) dv[d] = wm_direct_value<Spec, KW>(a, mlds, k, d);
   }
   prefetch();
 #ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
@@ -414,8 +422,21 @@ __device__ __forceinline__ uint64_t *wm_stage_tags(const WmArgs &a, uint8_t *lds
   const kconst_u64 tm = tuple_masks(a);
   if (threadIdx.x < kMaxTuples * KW)
     mlds[threadIdx.x] = tm[(threadIdx.x / KW) * kMaxKeyWords + threadIdx.x % KW];
+  // the one-byte direct tuples' tables (256 values each) after the masks
+  // (wm_direct_value reads them there)
+  static_assert(kWmDirLds == kMaxDirect * 2048, "one 2 KB table per direct slot");
+  const uint32_t nd = tuple_words(a, offsetof(WmArgs, ndirect))[0];
+  const uint32_t d = threadIdx.x >> 7;  // 128 threads x 16 B per table
+  if (d < nd && d < (uint32_t)kMaxDirect &&
+      (tuple_words(a, offsetof(WmArgs, dspec))[d] >> 24) == 0) {
+    const uint64_t off = reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
+        tuple_words(a, offsetof(WmArgs, doff)))[d];
+    reinterpret_cast<uint4 *>(mlds + kMaxTuples * KW)[threadIdx.x] =
+        reinterpret_cast<const uint4 *>(a.t.base + off)[threadIdx.x & 127];
+  }
   return mlds;
 }
+
 
 template <class Spec, int KW, int NCH, int PAIR>
 __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
@@ -424,7 +445,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   const uint64_t *mlds = wm_stage_tags<KW>(a, lds, tag_bytes);
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + wid * kWaveLds;
+  uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + kWmDirLds + wid * kWaveLds;
   uint64_t *best = reinterpret_cast<uint64_t *>(wl);
   uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
   best[lane] = 0;
@@ -621,7 +642,7 @@ __device__ __forceinline__ void wm_stream_impl(const WmArgs &a) {
   // are uniform)
   const int lane = threadIdx.x & 63,
             wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint8_t *waves = lds + tag_bytes + kMaxTuples * KW * 8;
+  uint8_t *waves = lds + tag_bytes + kMaxTuples * KW * 8 + kWmDirLds;
   const uint32_t R = a.ring_slots;
   uint8_t *ring = waves + C * kWaveLds;
   uint32_t *ready = reinterpret_cast<uint32_t *>(ring + (uint64_t)R * kStreamTileBytes);
@@ -723,13 +744,7 @@ __device__ __forceinline__ void wm_stream_impl(const WmArgs &a) {
 #pragma unroll
     for (int d = 0; d < kMaxDirect; d++) {
       pd.dv[d] = ~0ull;
-      if ((uint32_t)d < ndir && live) {
-        const uint64_t off =
-            reinterpret_cast<const __attribute__((address_space(4))) uint64_t *>(
-                tuple_words(a, offsetof(WmArgs, doff)))[d];
-        pd.dv[d] = reinterpret_cast<const uint64_t *>(a.t.base + off)
-            [direct_index_k<KW>(k, Spec::dspec(a, d))];
-      }
+      if ((uint32_t)d < ndir && live) pd.dv[d] = wm_direct_value<Spec, KW>(a, mlds, k, d);
     }
     pd.e = pd.z1 = pd.z2 = 0;
     pd.v = 0;
