@@ -169,6 +169,38 @@ void em_classify_kernel(EmArgs a) {
   em_body<KW, NCH, PPL>(a, lds);
 }
 
+// ExactMatch on strided slots (1500 B frames in 2 KB slots: SURVEY §8d's
+// 1500 B point) whose key window is two chunks inside the slot's first
+// 64 B: a wave takes 64-slot tiles and loads their windows with pair loads
+// (bg_keys_dev.h: one 32 B request per slot instead of two 16 B ones, the
+// L2 requests in flight per CU being what bounds a scattered-window read,
+// DESIGN §3 C4), the next tile's issued before this tile's lookup.
+template <int KW>
+__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
+void em_pair_kernel(EmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (a.t.lds) copy_table_to_lds(lds, a.t);
+  const int lane = threadIdx.x & 63;
+  constexpr int kWaves = kEmBlock / 64;
+  const uint64_t nw = (uint64_t)gridDim.x * kWaves, ntiles = (a.n + 63) / 64;
+  uint64_t t = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint32_t stride = (uint32_t)a.stride;
+  uint32_t wn[8];
+  if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, stride, wn);
+  for (; t < ntiles; t += nw) {
+    uint32_t w[10];
+    pair_window<2>(wn, lane, w);
+    if (t + nw < ntiles) load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, stride, wn);
+    uint64_t k[KW];
+    extract_key<KW, 2>(w, a.fp, k);
+    const uint32_t g = a.t.lds == kLdsTable
+                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
+                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
+    const uint64_t idx = t * 64 + pair_slot(lane);
+    if (idx < a.n) a.gates[idx] = (uint16_t)g;
+  }
+}
+
 #ifdef BG_AB
 // next grid-stride packet's window prefetched (A/B experiments: BG_EM_PF=1)
 template <int KW, int NCH>
@@ -2079,6 +2111,16 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
                : launch_em_slab<KW, 4>(a, num_cus, s);
     BG_SLAB(1) BG_SLAB(2) BG_SLAB(4) BG_SLAB(8)
 #undef BG_SLAB
+  }
+  // strided slots with the window in the slot's first 64 B: pair loads
+  // (measured: scripts/variants.py em1500)
+  if (!a.fp.direct && fits_nch2(a.fp) && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
+      a.stride > 64 && a.stride <= 65536 && !(path_flags() & kPathNoSlab) &&
+      knob("BG_EM_PAIR", 1)) {
+#define BG_PAIR(KW) \
+  if (a.t.kw == KW) return launch_classify(em_pair_kernel<KW>, a, num_cus, s, 1);
+    BG_PAIR(1) BG_PAIR(2) BG_PAIR(4) BG_PAIR(8)
+#undef BG_PAIR
   }
 #ifdef BG_AB
   if (knob("BG_EM_PF", 0) && a.t.kw == 2 && fits_nch2(a.fp))

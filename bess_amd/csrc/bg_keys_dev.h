@@ -245,6 +245,54 @@ __device__ __forceinline__ void build_keys(const uint8_t *__restrict__ frames,
   }
 }
 
+// Pair loads (the WildcardMatch tag-word kernels' PAIR mode, the
+// ExactMatch pair kernel on strided slots): the two 16-byte window chunks of a slot
+// are loaded by a lane pair -- load 0 of lanes 2m, 2m+1 holds chunks q0,
+// q0+1 of slot m, load 1 those of slot 32+m -- so each load instruction
+// covers 32 B of each of 32 adjacent slots (half the cache lines per
+// instruction of one 16 B chunk per lane at a 64 B stride). One DPP swap
+// per dword completes the windows: lane 2m takes slot m, lane 2m+1 slot
+// 32+m.
+__device__ __forceinline__ uint64_t pair_slot(int lane) {
+  return (lane & 1) ? 32u + (lane >> 1) : (uint32_t)(lane >> 1);
+}
+
+__device__ __forceinline__ void load_pair(const uint8_t *__restrict__ frames,
+                                          uint64_t n, uint64_t p0, int lane,
+                                          uint32_t win_lo, uint32_t stride,
+                                          uint32_t (&r)[8]) {
+  const uint64_t s0 = p0 + (lane >> 1), s1 = s0 + 32;
+  // a uniform base plus a 32-bit lane offset recomputed here (hoisted out
+  // of the tile loop, the per-lane 64-bit addresses were spilled, and the
+  // reload's wait retired every load issued before it)
+  uint32_t ln = (uint32_t)lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t off = (ln >> 1) * stride + win_lo + (ln & 1) * 16;
+  const uint8_t *base = frames + p0 * stride;
+  uint4 x = make_uint4(0, 0, 0, 0), y = x;
+  if (s0 < n) x = ld_stream(reinterpret_cast<const uint4 *>(base + off));
+  if (s1 < n) y = ld_stream(reinterpret_cast<const uint4 *>(base + off + 32 * stride));
+  r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+  r[4] = y.x; r[5] = y.y; r[6] = y.z; r[7] = y.w;
+}
+
+template <int NCH>
+__device__ __forceinline__ void pair_window(const uint32_t (&r)[8], int lane,
+                                            uint32_t (&w)[NCH * 4 + 2]) {
+  static_assert(NCH == 2, "pair loads carry two chunks");
+  const bool odd = lane & 1;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    const uint32_t src = odd ? r[d] : r[4 + d];
+    // quad_perm [1,0,3,2]: swap with the neighbouring lane
+    const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)src, 0xB1, 0xF, 0xF, false);
+    w[d] = odd ? recv : r[d];
+    w[4 + d] = odd ? r[4 + d] : recv;
+  }
+  w[8] = 0;
+  w[9] = 0;
+}
+
 }  // namespace
 }  // namespace bg
 

@@ -2,7 +2,7 @@
 # Full GPU session: tests, smoke, bench, rocprofv3 kernel stats + PMC passes.
 # Stops at the first step that ends in anything but success / test failure.
 cd "$GRAFT_REPO_ROOT" || exit 1
-OUT="$GRAFT_REPO_ROOT/gpurun_out"
+OUT="$GRAFT_REPO_ROOT/gpurun_out/${OUTDIR:-.}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name timeout cmd...
@@ -16,7 +16,7 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [[ "$MODE" == *tests* ]] || [ "$MODE" = all ]; then
-  step tests 900 python -m pytest tests -m gpu -q -rf --timeout 600
+  step tests 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ "$MODE" == *bench* ]] || [ "$MODE" = all ]; then

@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_RUN", "BG_WM_STREAM_SLOTS"]
+         "BG_EM_RUN", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR"]
 
 
 def set_env(v):
@@ -66,7 +66,7 @@ def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "em,ck,wm"
     dev = torch.device("cuda:0")
     out = {}
-    if "em" in which:
+    if "em" in which.split(","):
         n = 16 << 20
         keys, gates, frames = P.em_workload(1000, n)
         d = torch.from_numpy(frames.reshape(-1)).to(dev)
@@ -101,6 +101,34 @@ def main():
             r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
             r[k]["GBps_66B"] = round(66 * n / (r[k]["median_ms"] * 1e-3) / 1e9, 1)
         out["em"] = r
+        del d, g
+    if "em1500" in which:
+        # bench.py's EM_1500B leg: 1 K-rule 5-tuple ExactMatch over 4 M
+        # 1496 B frames in 2 KB slots (first 64 B written): pair loads
+        # (em_pair_kernel) vs one lane per packet (em_classify_kernel)
+        n = 1 << 22
+        keys, gates, hdr = P.em_workload(1000, n, seed=0x5EED, stride=64,
+                                         frame_len=1496, pkt_seed=0x1500)
+        d = torch.zeros(n * 2048, dtype=torch.uint8, device=dev)
+        d.view(n, 2048)[:, :64] = torch.from_numpy(hdr).to(dev)
+        del hdr
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        t = F.EmTable(P.em_fields_5tuple())
+        t.add_many(keys, gates)
+        t.sync(0)
+        variants = {"pair": {}, "lane": {"BG_EM_PAIR": 0}}
+        ref = None
+        for name, env in variants.items():
+            set_env(env)
+            t.classify(d, 2048, n, 8192, g)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = g.clone()
+            assert torch.equal(g, ref), name
+        r = time_variants(lambda: t.classify(d, 2048, n, 8192, g), variants, reps=20)
+        for k in r:
+            r[k]["Mpps"] = round(n / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
+        out["em1500"] = r
         del d, g
     if "c5" in which:
         n = 16 << 20
