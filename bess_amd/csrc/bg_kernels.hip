@@ -106,6 +106,43 @@ __device__ __forceinline__ uint32_t em_lookup(const uint8_t *tab,
   return dflt;
 }
 
+// em_lookup for a table in L2 / MALL with the second bucket's tag word
+// read only when the first bucket does not hold the key (a miss reads
+// both, a hit placed in its first bucket one): fewer L2 requests per
+// packet, at one more dependent round trip for those that need b2.
+template <int KW>
+__device__ __forceinline__ uint32_t em_lookup_seq(const uint8_t *tab, const TableRef &t,
+                                                  const uint64_t (&k)[KW], uint32_t dflt) {
+  const uint64_t h = hash_words(k, KW, t.seed);
+  const Probe p = split_hash(h, t.nparts, t.nbp);
+  const uint8_t *pb = tab + (uint64_t)p.part * t.part_bytes;
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(pb);
+  const uint16_t *vals = reinterpret_cast<const uint16_t *>(pb + t.vals_off);
+  for (int pass = 0; pass < 2; pass++) {
+    const uint32_t b = pass ? p.b2 : p.b1;
+    uint32_t cand = tag_match(tags[b], p.tag);
+    while (cand) {
+      const int s = __builtin_ctz(cand);
+      cand &= cand - 1;
+      const uint32_t slot = b * kSlots + s;
+      uint64_t sk[KW];
+      load_key<KW>(pb + t.keys_off + (uint64_t)slot * KW * 8, sk);
+      uint32_t v;
+      if (t.vik) {
+        v = (uint32_t)(sk[KW - 1] >> 48);
+        sk[KW - 1] &= 0x0000FFFFFFFFFFFFULL;
+      } else {
+        v = vals[slot];
+      }
+      bool eq = true;
+#pragma unroll
+      for (int j = 0; j < KW; j++) eq &= sk[j] == k[j];
+      if (eq) return v;
+    }
+  }
+  return dflt;
+}
+
 // Table / filter fill: four 16-byte loads in flight per thread before
 // their LDS writes (a 40 KB table is ~5 loads per thread of a 512-thread
 // block; one round trip instead of five).
@@ -245,7 +282,7 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 }
 
 
-template <int KW, int NCH, int PF>
+template <int KW, int NCH, int PF, int SEQ = 0>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_slab_kernel(EmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -303,95 +340,12 @@ void em_slab_kernel(EmArgs a) {
     extract_key<KW, NCH>(w, a.fp, k);
     const uint32_t g = a.t.lds == kLdsTable
                            ? em_lookup<KW>(lds, a.t, k, a.default_gate)
-                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
+                           : SEQ ? em_lookup_seq<KW>(a.t.base, a.t, k, a.default_gate)
+                                 : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
     const uint64_t idx = t * 64 + lane;
     if (idx < a.n) a.gates[idx] = (uint16_t)g;
     lds_fence();  // this tile's stage reads retire before the next writes
     if (PF == 0 && t + nwaves < ntiles) load_tile(t + nwaves, v);
-  }
-}
-
-// Gate runs: each wave takes runs of kEmRun consecutive tiles (512 slots,
-// 32 KB of headers) and gathers the run's 512 gates in LDS, stored as one
-// 1 KB block (16 B per lane) instead of eight 128 B per-tile stores
-// (scripts/hbm_probe.hip slab66c / slab66g measure the shape alone).
-constexpr int kEmRun = 8;
-template <int KW, int NCH>
-__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
-void em_slab_run_kernel(EmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  copy_table_to_lds(lds, a.t);
-  const uint32_t stage_off =
-      a.t.lds == kLdsTable ? ((a.t.bytes_total + 15) & ~15u) : 0u;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  constexpr int kWaves = kEmBlock / 64;
-  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_off) + wid * 256;
-  uint16_t *gl = reinterpret_cast<uint16_t *>(lds + stage_off + kWaves * 4096) +
-                 wid * 64 * kEmRun;
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t ntiles = (a.n + 63) / 64;
-  const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
-  const uint32_t q0 = (uint32_t)a.fp.win_lo >> 4;
-  const bool g16 = (reinterpret_cast<uintptr_t>(a.gates) & 15) == 0;
-  uint4 v[4];
-  auto load_tile = [&](uint64_t tile, uint4 (&o)[4]) {
-    const uint64_t p0 = tile * 64;
-    const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
-    const uint4 *g = src + p0 * 4;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t u = c * 64 + lane;
-      o[c] = u < units ? ld_stream(g + u) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  // the wave's tile after t: the next of its run, else the first of its
-  // next run
-  auto next = [&](uint64_t t) -> uint64_t {
-    return (t % kEmRun != kEmRun - 1 && t + 1 < ntiles) ? t + 1
-                                                        : (t / kEmRun + nwaves) * kEmRun;
-  };
-  uint64_t t = ((uint64_t)blockIdx.x * kWaves + wid) * kEmRun;
-  if (t < ntiles) load_tile(t, v);
-  while (t < ntiles) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t u = c * 64 + lane;
-      stage[stage_unit(u >> 2, u & 3)] = v[c];
-    }
-    lds_fence();
-    const uint64_t tn = next(t);
-    if (tn < ntiles) load_tile(tn, v);
-    uint32_t w[NCH * 4 + 2];
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      uint4 x = make_uint4(0, 0, 0, 0);
-      if (c < a.fp.nch) x = stage[stage_unit(lane, q0 + c)];
-      w[4 * c] = x.x;
-      w[4 * c + 1] = x.y;
-      w[4 * c + 2] = x.z;
-      w[4 * c + 3] = x.w;
-    }
-    w[NCH * 4] = 0;
-    w[NCH * 4 + 1] = 0;
-    uint64_t k[KW];
-    extract_key<KW, NCH>(w, a.fp, k);
-    const uint32_t g = a.t.lds == kLdsTable
-                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
-                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
-    gl[(t % kEmRun) * 64 + lane] = (uint16_t)g;
-    lds_fence();  // this tile's stage reads and gate writes retire
-    if (t % kEmRun == kEmRun - 1 || t + 1 == ntiles) {  // the run ends (uniform)
-      const uint64_t p0 = (t / kEmRun) * kEmRun * 64;
-      const uint64_t cnt = a.n - p0 < (uint64_t)kEmRun * 64 ? a.n - p0 : (uint64_t)kEmRun * 64;
-      if (cnt == (uint64_t)kEmRun * 64 && g16) {
-        reinterpret_cast<uint4 *>(a.gates + p0)[lane] = reinterpret_cast<const uint4 *>(gl)[lane];
-      } else {
-        for (uint64_t i = lane; i < cnt; i += 64) a.gates[p0 + i] = gl[i];
-      }
-      lds_fence();  // the next run rewrites gl
-    }
-    t = tn;
   }
 }
 
@@ -2037,9 +1991,8 @@ hipError_t launch_em_slab(const EmArgs &a, int num_cus, hipStream_t s) {
   if (v2 == 1024)
     return launch_slab(em_slab2_kernel<KW, NCH, 1024>, a, num_cus, s, 1024,
                        (size_t)16 * 64 * NCH * 16);
-  if (knob("BG_EM_RUN", 0))
-    return launch_slab(em_slab_run_kernel<KW, NCH>, a, num_cus, s, kEmBlock,
-                       kStage + (size_t)(kEmBlock / 64) * 64 * kEmRun * 2);
+  if (knob("BG_EM_SEQ", 0))
+    return launch_slab(em_slab_kernel<KW, NCH, 1, 1>, a, num_cus, s, kEmBlock, kStage);
   // prefetch depth (tiles ahead)
   const int pf = std::min(2, std::max(0, knob("BG_SLAB_PF", 1)));
   if (pf == 0) return launch_slab(em_slab_kernel<KW, NCH, 0>, a, num_cus, s, kEmBlock, kStage);
