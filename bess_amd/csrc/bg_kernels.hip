@@ -282,7 +282,7 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 }
 
 
-template <int KW, int NCH, int PF, int SEQ = 0>
+template <int KW, int NCH, int PF, int SEQ = 0, int NTG = 0>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_slab_kernel(EmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -343,7 +343,12 @@ void em_slab_kernel(EmArgs a) {
                            : SEQ ? em_lookup_seq<KW>(a.t.base, a.t, k, a.default_gate)
                                  : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
     const uint64_t idx = t * 64 + lane;
-    if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    if (idx < a.n) {
+      if (NTG)  // (A/B: BG_EM_NTG) a streaming store
+        __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
+      else
+        a.gates[idx] = (uint16_t)g;
+    }
     lds_fence();  // this tile's stage reads retire before the next writes
     if (PF == 0 && t + nwaves < ntiles) load_tile(t + nwaves, v);
   }
@@ -1993,6 +1998,8 @@ hipError_t launch_em_slab(const EmArgs &a, int num_cus, hipStream_t s) {
                        (size_t)16 * 64 * NCH * 16);
   if (knob("BG_EM_SEQ", 0))
     return launch_slab(em_slab_kernel<KW, NCH, 1, 1>, a, num_cus, s, kEmBlock, kStage);
+  if (knob("BG_EM_NTG", 0))
+    return launch_slab(em_slab_kernel<KW, NCH, 1, 0, 1>, a, num_cus, s, kEmBlock, kStage);
   // prefetch depth (tiles ahead)
   const int pf = std::min(2, std::max(0, knob("BG_SLAB_PF", 1)));
   if (pf == 0) return launch_slab(em_slab_kernel<KW, NCH, 0>, a, num_cus, s, kEmBlock, kStage);
