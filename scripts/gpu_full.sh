@@ -33,7 +33,7 @@ if [[ "$MODE" == *pmc* ]] || [ "$MODE" = all ]; then
   i=0
   for C in ${PMC_SETS:-"FETCH_SIZE" "WRITE_SIZE"}; do
     i=$((i+1))
-    for W in ${PMC_WL:-em cksum wm wm2k c5 hashlb acl iplookup ttl nat dnat}; do
+    for W in ${PMC_WL:-em cksum wm wm2k em1500 c5 hashlb acl iplookup ttl nat dnat rewrite}; do
       case $W in
         em) ARGS="--no-extra --no-cpu --steps 3 --warmup 1" ;;
         wm) ARGS="--only wm --wm-layout slab --no-cpu --steps 3 --warmup 1" ;;

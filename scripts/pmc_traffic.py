@@ -27,16 +27,16 @@ KERNELS = {"em": "em_slab_kernel", "cksum": "cksum_kernel",
            "c5": "em_slab_kernel",
            "hashlb": "HlbOp<2>", "acl": "AclTreeOp", "iplookup": "Lpm16LdsOp",
            "ttl": "TtlOp<4>", "nat": "NatOp", "dnat": "dnat_fused_slab_kernel",
-           "rewrite": "rewrite_kernel"}
+           "rewrite": "rewrite_kernel", "em1500": "em_pair_kernel"}
 # algorithmic bytes per launch of each bench workload
 ALGO = {"em": 66 * (16 << 20), "cksum": 1502 * (1 << 20),
         "wm": 66 * (8 << 20), "wm2k": 66 * (8 << 20), "c5": 66 * (16 << 20),
         "hashlb": 66 * (16 << 20), "acl": 66 * (16 << 20),
         "iplookup": 66 * (16 << 20), "ttl": 130 * (16 << 20),
         "nat": 130 * (16 << 20), "dnat": 130 * (16 << 20),
-        "rewrite": 70 * (16 << 20)}
+        "rewrite": 70 * (16 << 20), "em1500": 66 * (4 << 20)}
 # FETCH_SIZE -> bytes factor by access shape (r03_calibration.json)
-FETCH = {"wm2k": 1}
+FETCH = {"wm2k": 1, "em1500": 1}
 
 
 def collect(root, wl):
