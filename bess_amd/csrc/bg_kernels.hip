@@ -234,7 +234,7 @@ void em_pair_kernel(EmArgs a) {
                            ? em_lookup<KW>(lds, a.t, k, a.default_gate)
                            : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
     const uint64_t idx = t * 64 + pair_slot(lane);
-    if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    if (idx < a.n) __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
   }
 }
 
@@ -282,7 +282,12 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 }
 
 
-template <int KW, int NCH, int PF, int SEQ = 0, int NTG = 0>
+// SEQ: a table in L2 / MALL is probed with em_lookup_seq (the second
+// bucket's tag word only when the first does not hold the key: C5 0.382 ->
+// 0.357 ms); NTG: the gates are stored nontemporally (streaming stores;
+// C2 0.1896 -> 0.1825 ms). Both measured in one process each
+// (scripts/variants.py em / c5, profiles/r05/em_variants_r05m.json).
+template <int KW, int NCH, int PF, int SEQ = 1, int NTG = 1>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_slab_kernel(EmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -344,7 +349,7 @@ void em_slab_kernel(EmArgs a) {
                                  : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
     const uint64_t idx = t * 64 + lane;
     if (idx < a.n) {
-      if (NTG)  // (A/B: BG_EM_NTG) a streaming store
+      if (NTG)  // a streaming store
         __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
       else
         a.gates[idx] = (uint16_t)g;
@@ -1996,10 +2001,11 @@ hipError_t launch_em_slab(const EmArgs &a, int num_cus, hipStream_t s) {
   if (v2 == 1024)
     return launch_slab(em_slab2_kernel<KW, NCH, 1024>, a, num_cus, s, 1024,
                        (size_t)16 * 64 * NCH * 16);
-  if (knob("BG_EM_SEQ", 0))
-    return launch_slab(em_slab_kernel<KW, NCH, 1, 1>, a, num_cus, s, kEmBlock, kStage);
-  if (knob("BG_EM_NTG", 0))
+  // round 4's form: both tag words read together, gates stored normally
+  if (knob("BG_EM_PAR2", 0))
     return launch_slab(em_slab_kernel<KW, NCH, 1, 0, 1>, a, num_cus, s, kEmBlock, kStage);
+  if (knob("BG_EM_TG", 0))
+    return launch_slab(em_slab_kernel<KW, NCH, 1, 1, 0>, a, num_cus, s, kEmBlock, kStage);
   // prefetch depth (tiles ahead)
   const int pf = std::min(2, std::max(0, knob("BG_SLAB_PF", 1)));
   if (pf == 0) return launch_slab(em_slab_kernel<KW, NCH, 0>, a, num_cus, s, kEmBlock, kStage);

@@ -125,7 +125,8 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
     const uint64_t idx = t * 64 + lane;
     if (idx < a.n) {
       uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * 64;
-      a.out[idx] = (uint16_t)Op::decide(a, lds, d, f);
+      // (a streaming store, as em_slab_kernel's gates: measured faster)
+      __builtin_nontemporal_store((uint16_t)Op::decide(a, lds, d, f), a.out + idx);
     }
     if constexpr (Op::kWrites) {
       // updated chunks back into this lane's slot of the stage, then the

@@ -360,7 +360,8 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
       bb = comb > bb ? comb : bb;
     }
   }
-  if (live) a.gates[idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
+  if (live)  // (a streaming store)
+    __builtin_nontemporal_store(bb ? (uint16_t)bb : (uint16_t)a.default_gate, a.gates + idx);
 }
 
 // stage the tag words and the tuple masks (every thread of the workgroup);
@@ -524,7 +525,8 @@ __device__ __forceinline__ void wm_finish(const WmArgs &a, const uint32_t *tags,
       bb = comb > bb ? comb : bb;
     }
   }
-  if (p.live) a.gates[p.idx] = bb ? (uint16_t)bb : (uint16_t)a.default_gate;
+  if (p.live)
+    __builtin_nontemporal_store(bb ? (uint16_t)bb : (uint16_t)a.default_gate, a.gates + p.idx);
 }
 
 // ---------------------------------------------------------------------------

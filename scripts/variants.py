@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_SEQ", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_NTG"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG"]
 
 
 def set_env(v):
@@ -78,7 +78,7 @@ def main():
         ref = None
         variants = {
             "default": {}, "slab_pf2": {"BG_SLAB_PF": 2},
-            "default_bpc2": {"BG_BLOCKS_PER_CU": 2}, "nt_gates": {"BG_EM_NTG": 1},
+            "default_bpc2": {"BG_BLOCKS_PER_CU": 2}, "temporal_gates": {"BG_EM_TG": 1},
             "slab_pf1_bpc1": {"BG_SLAB_PF": 1, "BG_BLOCKS_PER_CU": 1},
             "slab_pf2_bpc1": {"BG_SLAB_PF": 2, "BG_BLOCKS_PER_CU": 1},
             "slab_l2tab_pf2": {"BG_NOLDS": 1, "BG_SLAB_PF": 2},
@@ -139,7 +139,7 @@ def main():
         t.add_many(keys, gates)
         t.sync(0)
         variants = {
-            "default": {}, "seq_b2": {"BG_EM_SEQ": 1}, "slab_pf2": {"BG_SLAB_PF": 2},
+            "default": {}, "both_tags": {"BG_EM_PAR2": 1}, "slab_pf2": {"BG_SLAB_PF": 2},
             "slab_pf0": {"BG_SLAB_PF": 0},
             "slab_bpc2": {"BG_BLOCKS_PER_CU": 2},
             "slab_bpc4": {"BG_BLOCKS_PER_CU": 4},
