@@ -123,8 +123,38 @@ __device__ __forceinline__ SlotHit lookup_in(const TableRef &t, uint64_t key) {
   }
   return h;
 }
+// lookup_in with the second bucket's tag word read only when the first
+// bucket does not hold the endpoint (em_lookup_seq's probe order: fewer L2
+// requests per packet, one more dependent round trip for those in b2)
+__device__ __forceinline__ SlotHit lookup_in_seq(const TableRef &t, uint64_t key) {
+  const uint32_t *tags = reinterpret_cast<const uint32_t *>(t.base);
+  const u32x4 *kv = reinterpret_cast<const u32x4 *>(t.base + t.keys_off);
+  const Probe p = split_hash(hash_words(&key, 1, t.seed), 1, t.nbp);
+  SlotHit h;
+  h.slot = ~0u;
+  h.entry = 0;
+  h.ep = 0;
+  for (int pass = 0; pass < 2 && h.slot == ~0u; pass++) {
+    const uint32_t b = pass ? p.b2 : p.b1;
+    uint32_t c = tag_match(tags[b], p.tag);
+    while (c) {
+      const int s = __builtin_ctz(c);
+      c &= c - 1;
+      const uint32_t slot = b * kSlots + s;
+      const u32x4 k = kv[slot];
+      if ((k.x | (uint64_t)(k.y & 0x00FFFFFFu) << 32) == key) {
+        h.slot = slot;
+        h.entry = (k.w >> 16) | ((k.y >> 24) << 16);
+        h.ep = k.z | (uint64_t)(k.w & 0xFFFFu) << 32;
+        break;
+      }
+    }
+  }
+  return h;
+}
+template <int SEQ = 0>
 __device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
-  return lookup_in(a.t, key);
+  return SEQ ? lookup_in_seq(a.t, key) : lookup_in(a.t, key);
 }
 // endpoint -> entry index, or kDnatMiss
 __device__ __forceinline__ uint32_t lookup(const DnatArgs &a, uint64_t key) {
@@ -198,7 +228,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_apply_kernel(DnatArgs a) {
 // miss drops; a forward miss, or a forward hit on an expired mapping (a new
 // flow earlier in the batch may evict it: CreateNewEntry, nat.cc:224-231),
 // is appended to the list (wave-aggregated) for the host's in-order walk.
-template <class F>
+template <int SEQ = 0, class F>
 __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
                                           uint64_t i, bool live) {
   uint64_t key = ~0ull;
@@ -215,7 +245,7 @@ __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
       h.ep = key;
     } else
 #endif
-    if (key != ~0ull) h = lookup_hit(a, key);
+    if (key != ~0ull) h = lookup_hit<SEQ>(a, key);
     // a reverse miss: the forward entries are in the same map (nat.cc Find)
     if (h.slot == ~0u && key != ~0ull && a.dir == 1 && a.t2.base) h = lookup_in(a.t2, key);
     if (h.slot != ~0u && a.dir == 0) ts = a.ts[h.entry];
@@ -294,6 +324,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
 // decides and stamps its slot in LDS, and the tile goes back whole with
 // lane-contiguous 16-byte stores (no partial-line writes).
 constexpr int kNatSlabBlock = 512;
+template <int SEQ>
 __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -330,7 +361,7 @@ __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs
     const uint32_t units = units_of(t);
     if (t + nwaves < ntiles) load_tile(t + nwaves);
     const uint64_t idx = t * 64 + lane;
-    fused_one(a, me, idx, idx < a.n);
+    fused_one<SEQ>(a, me, idx, idx < a.n);
     lds_fence();
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -379,13 +410,12 @@ hipError_t launch_dnat_fused(const DnatArgs &a0, int num_cus, hipStream_t s) {
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
     const size_t lds = (size_t)(kNatSlabBlock / 64) * 4096;
-    int occ = occupancy(reinterpret_cast<const void *>(dnat_fused_slab_kernel),
-                        kNatSlabBlock, lds, 1);
+    auto kern = knob("BG_NAT_SEQ", 0) ? dnat_fused_slab_kernel<1> : dnat_fused_slab_kernel<0>;
+    int occ = occupancy(reinterpret_cast<const void *>(kern), kNatSlabBlock, lds, 1);
     occ = std::max(1, knob("BG_NAT_OCC", occ));
     const uint64_t need = (a.n + kNatSlabBlock - 1) / kNatSlabBlock;
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
-    hipLaunchKernelGGL(dnat_fused_slab_kernel, dim3((unsigned)blocks),
-                       dim3(kNatSlabBlock), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kNatSlabBlock), lds, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(dnat_fused_kernel, dim3((unsigned)grid_of(a.n, num_cus)),

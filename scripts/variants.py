@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_SEQ"]
 
 
 def set_env(v):
@@ -217,7 +217,7 @@ def main():
         src = torch.from_numpy(slab.reshape(-1)).to(dev)
         now = [t0]
         phases = (("full", {}), ("no_timestamp", {"BG_NAT_PHASE": 1}),
-                  ("no_lookup", {"BG_NAT_PHASE": 2}))
+                  ("no_lookup", {"BG_NAT_PHASE": 2}), ("seq_b2", {"BG_NAT_SEQ": 1}))
         res = {name: [] for name, _ in phases}
         for _ in range(3):
             for name, env in phases:
