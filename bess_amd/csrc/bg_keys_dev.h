@@ -124,6 +124,11 @@ __device__ __forceinline__ uint4 ld_stream(const uint4 *p) {
   u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// a streaming (nontemporal) 16-byte store
+__device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
+}
 
 // Key building (ExactMatchTable::MakeKeys exact_match_table.h:239-263 /
 // WildcardMatch::ProcessBatch wildcard_match.cc:169-197). The window

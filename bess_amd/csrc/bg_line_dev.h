@@ -77,7 +77,8 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
   }
 }
 
-template <class Op>
+// NTW: the written-back lines stored nontemporally (A/B: BG_LINE_NTW)
+template <class Op, int NTW = 0>
 __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args a,
                                                               uint32_t stage_words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -143,8 +144,12 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
       for (int c = 0; c < 4; c++) {
         const uint32_t u = c * 64 + lane;
         const uint32_t q = u & 3;
-        if (u < units && q >= (uint32_t)Op::c0 && q < (uint32_t)Op::c1)
-          dst[p0 * 4 + u] = stage[line_stage_unit(u >> 2, q)];
+        if (u < units && q >= (uint32_t)Op::c0 && q < (uint32_t)Op::c1) {
+          if (NTW)
+            st_stream(dst + p0 * 4 + u, stage[line_stage_unit(u >> 2, q)]);
+          else
+            dst[p0 * 4 + u] = stage[line_stage_unit(u >> 2, q)];
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -193,7 +198,8 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
   const uint64_t need = (a.n + kLineBlock - 1) / kLineBlock;
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
-    auto kern = line_slab_kernel<Op>;
+    auto kern = Op::kWrites && knob("BG_LINE_NTW", 0) ? line_slab_kernel<Op, 1>
+                                                      : line_slab_kernel<Op>;
     const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
     const int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));

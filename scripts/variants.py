@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_SEQ"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_SEQ", "BG_LINE_NTW"]
 
 
 def set_env(v):
@@ -270,6 +270,32 @@ def main():
             r[k]["Mpps"] = round(n2 / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
         out["wmphase_2k"] = r
         del d, g, f2
+    if "linew" in which:
+        # the writing header-line ops (UpdateTTL, StaticNAT: 16 M 64 B
+        # packets in place, as bench.py) with their written-back lines
+        # stored normally vs nontemporally (BG_LINE_NTW); TTL starts at 200
+        # and the 90 launches here stay above 1
+        from bess_amd.modules import StaticNAT, UpdateTTL
+        n = 16 << 20
+        _, _, frames = P.em_workload(1000, n, seed=0x5EED, pkt_seed=11)
+        frames[:, 22] = 200
+        rng = np.random.default_rng(13)
+        hit = rng.random(n) < 0.5
+        frames[hit, 26] = 10
+        frames[hit, 27] = rng.integers(0, 8, int(hit.sum()), dtype=np.uint8)
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        pairs = []  # bench.py nat_pairs(): 10.i/16 <-> 100.i/16, both ways
+        for back in (0, 1):
+            for i in range(8):
+                a, b = ("100.%d" % i, "10.%d" % i) if back else ("10.%d" % i, "100.%d" % i)
+                pairs.append({"int_range": {"start": a + ".0.0", "end": a + ".255.255"},
+                              "ext_range": {"start": b + ".0.0", "end": b + ".255.255"}})
+        for name, m in (("ttl", UpdateTTL()), ("static_nat", StaticNAT(pairs=pairs))):
+            d = torch.from_numpy(frames.reshape(-1)).to(dev)
+            r = time_variants(lambda: m.process_device(d, 64, n, g),
+                              {"lines": {}, "lines_nt": {"BG_LINE_NTW": 1}}, reps=8)
+            out["linew_" + name] = r
+            del d
     if "wmdirect" in which:
         # C4 with the source-port tuple direct (the round-4 policy: every
         # two-byte tuple, BG_WM_DIRECT2_MIN=0) vs hashed (>= 32768 rules);
