@@ -152,7 +152,7 @@ __device__ __forceinline__ SlotHit lookup_in_seq(const TableRef &t, uint64_t key
   }
   return h;
 }
-template <int SEQ = 0>
+template <int SEQ = 1>
 __device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
   return SEQ ? lookup_in_seq(a.t, key) : lookup_in(a.t, key);
 }
@@ -228,7 +228,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_apply_kernel(DnatArgs a) {
 // miss drops; a forward miss, or a forward hit on an expired mapping (a new
 // flow earlier in the batch may evict it: CreateNewEntry, nat.cc:224-231),
 // is appended to the list (wave-aggregated) for the host's in-order walk.
-template <int SEQ = 0, class F>
+template <int SEQ = 1, class F>
 __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
                                           uint64_t i, bool live) {
   uint64_t key = ~0ull;
@@ -324,7 +324,11 @@ __global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
 // decides and stamps its slot in LDS, and the tile goes back whole with
 // lane-contiguous 16-byte stores (no partial-line writes).
 constexpr int kNatSlabBlock = 512;
-template <int SEQ>
+// SEQ: the sequential second-bucket probe (lookup_in_seq: 0.6097 ->
+// 0.5443 ms per 16 M packets, scripts/variants.py natphase,
+// profiles/r05/natphase_r05n.json); NTW: the tile written back with
+// streaming stores (as the line ops')
+template <int SEQ, int NTW>
 __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -366,7 +370,13 @@ __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t u = c * 64 + lane;
-      if (u < units) src[t * 256 + u] = stage[(u >> 2) * 4 + (((u & 3) + (u >> 4)) & 3)];
+      if (u < units) {
+        const uint4 x = stage[(u >> 2) * 4 + (((u & 3) + (u >> 4)) & 3)];
+        if (NTW)
+          st_stream(src + t * 256 + u, x);
+        else
+          src[t * 256 + u] = x;
+      }
     }
     lds_fence();  // stage reads retire before the next tile's writes
   }
@@ -410,7 +420,11 @@ hipError_t launch_dnat_fused(const DnatArgs &a0, int num_cus, hipStream_t s) {
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
     const size_t lds = (size_t)(kNatSlabBlock / 64) * 4096;
-    auto kern = knob("BG_NAT_SEQ", 0) ? dnat_fused_slab_kernel<1> : dnat_fused_slab_kernel<0>;
+    // (A/B build: BG_NAT_PAR2 = both tag words together, BG_NAT_TW =
+    // normal line stores)
+    auto kern = knob("BG_NAT_PAR2", 0) ? dnat_fused_slab_kernel<0, 1>
+                : knob("BG_NAT_TW", 0) ? dnat_fused_slab_kernel<1, 0>
+                                       : dnat_fused_slab_kernel<1, 1>;
     int occ = occupancy(reinterpret_cast<const void *>(kern), kNatSlabBlock, lds, 1);
     occ = std::max(1, knob("BG_NAT_OCC", occ));
     const uint64_t need = (a.n + kNatSlabBlock - 1) / kNatSlabBlock;

@@ -77,8 +77,11 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
   }
 }
 
-// NTW: the written-back lines stored nontemporally (A/B: BG_LINE_NTW)
-template <class Op, int NTW = 0>
+// NTW: the written-back lines stored nontemporally (streaming stores:
+// UpdateTTL 0.4093 -> 0.3879 ms, StaticNAT 0.4131 -> 0.3908 per 16 M
+// packets, scripts/variants.py linew, profiles/r05/linew_r05n.json; A/B
+// build: BG_LINE_TW=1 for normal stores)
+template <class Op, int NTW = 1>
 __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args a,
                                                               uint32_t stage_words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -198,8 +201,8 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
   const uint64_t need = (a.n + kLineBlock - 1) / kLineBlock;
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
-    auto kern = Op::kWrites && knob("BG_LINE_NTW", 0) ? line_slab_kernel<Op, 1>
-                                                      : line_slab_kernel<Op>;
+    auto kern = Op::kWrites && knob("BG_LINE_TW", 0) ? line_slab_kernel<Op, 0>
+                                                     : line_slab_kernel<Op>;
     const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
     const int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
