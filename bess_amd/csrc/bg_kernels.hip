@@ -1414,7 +1414,7 @@ __device__ __forceinline__ uint32_t tail_sum(const uint4 &c, int o, int hi) {
 // line from L2 / HBM (A/B build: BG_CK_TILED=7); 3 (WORDS): phase 1 keeps
 // the two header words phase 3 needs (the old IPv4 checksum, bytes 24..25)
 // and phase 3 stores the checksum words alone -- no re-read and no line
-// store (BG_CK_TILED=8).
+// store (BG_CK_TILED=8); 4: the same with streaming stores (BG_CK_TILED=14).
 constexpr int kCkStashStride = 144;  // 128 B + 16: lanes' lines on other banks
 template <int RELOAD, int DEPTH>
 __device__ __forceinline__ void cksum_body(const CkArgs &a) {
@@ -1434,7 +1434,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
     uint8_t *mine = a.frames + (p0 + (uint64_t)lane) * a.stride;
     uint32_t h[kHdrDw];
     CkLane L;
-    uint32_t ip_old = 0, w24 = 0, l4_old = 0;  // RELOAD == 3
+    uint32_t ip_old = 0, w24 = 0, l4_old = 0;  // RELOAD >= 3
     if (lane < cnt) {
       const uint4 *q = reinterpret_cast<const uint4 *>(mine);
 #pragma unroll
@@ -1447,7 +1447,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         if (RELOAD == 2) stash[c] = v;
       }
       L = ck_walk(mine, h, a.mode, stride);
-      if (RELOAD == 3) {
+      if (RELOAD >= 3) {
         ip_old = L.ip_off == 14 ? hle16(h, 24) : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
         w24 = hle16(h, 24);
         l4_old = (L.flags & 16) ? ld_u16(mine + L.l4_ck) : 0u;  // (in the line: an L1 hit)
@@ -1531,7 +1531,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
       } else if (a.verify) {
         ip_gate = fold16(L.s_ip) == 0xFFFFu ? 0u : 1u;
       } else {
-        const uint32_t old = RELOAD == 3 ? ip_old
+        const uint32_t old = RELOAD >= 3 ? ip_old
                              : L.ip_off == 14 ? hle16(h, 24)
                              : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
         ip_new = (~fold16(L.s_ip - old)) & 0xFFFFu;
@@ -1550,13 +1550,13 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         l4_gate = kGateNone;
       } else {
         uint32_t s = L.s_l4 + tail;
-        uint32_t old = RELOAD == 3 ? l4_old : valid ? ld_u16(mine + L.l4_ck) : 0u;
+        uint32_t old = RELOAD >= 3 ? l4_old : valid ? ld_u16(mine + L.l4_ck) : 0u;
         // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
         // the "L4 header" overlaps the IP checksum bytes 24..25.
         if (ip_wrote && L.ip_off == 14 && valid) {
           const int lo2 = (int)L.l4_lo > 24 ? (int)L.l4_lo : 24;
           const int hi2 = (int)L.l4_hi < 26 ? (int)L.l4_hi : 26;
-          s = s - dw_range_sum(RELOAD == 3 ? w24 : hle16(h, 24), 24, lo2, hi2) +
+          s = s - dw_range_sum(RELOAD >= 3 ? w24 : hle16(h, 24), 24, lo2, hi2) +
               dw_range_sum(ip_new, 24, lo2, hi2);
           if (L.l4_ck == 24) old = ip_new;
         }
@@ -1581,286 +1581,29 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
       // Store the whole 128 B header line first so the checksum words land
       // in a fully written L2 line (no read-modify-write of a partial line
       // in HBM), then the words themselves, in the reference's order.
-      if (RELOAD != 3) {
+      if (RELOAD < 3) {
         uint4 *q = reinterpret_cast<uint4 *>(mine);
 #pragma unroll
         for (int c = 0; c < kHdrDw / 4; c++)
           q[c] = make_uint4(h[4 * c], h[4 * c + 1], h[4 * c + 2], h[4 * c + 3]);
       }
-      if (ip_wrote)
-        *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
-      if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
-        *reinterpret_cast<uint16_t *>(mine + L.l4_ck) = (uint16_t)l4_new;
+      if (RELOAD == 4) {  // (A/B: the words form with streaming stores)
+        if (ip_wrote)
+          __builtin_nontemporal_store((uint16_t)ip_new,
+                                      reinterpret_cast<uint16_t *>(mine + L.ip_off + 10));
+        if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
+          __builtin_nontemporal_store((uint16_t)l4_new, reinterpret_cast<uint16_t *>(mine + L.l4_ck));
+      } else {
+        if (ip_wrote)
+          *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
+        if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
+          *reinterpret_cast<uint16_t *>(mine + L.l4_ck) = (uint16_t)l4_new;
+      }
     }
     if (a.ip_gates) a.ip_gates[p0 + lane] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
     if (a.l4_gates) a.l4_gates[p0 + lane] = (uint16_t)l4_gate;
   }
 }
-
-// ---------------------------------------------------------------------------
-// Wide form: phase 1 (lane = frame) reads only bytes 0..47 -- every field the
-// walk reads at a fixed offset -- and the two variable-offset words (UDP
-// length, the old L4 checksum; L1 hits in the same line); it records the
-// byte ranges to sum. Phase 2 (frame by frame, all 64 lanes) loads the whole
-// summed range [0, end) lane-contiguously and reduces both sums there: the
-// L4 range over the wave, the IPv4 header over the first row of 16 lanes.
-// Phase 3 (lane = frame) folds and stores the checksum words alone. No
-// 128 B header line in registers (12 dwords instead of 32) and no
-// per-lane-strided line loads.
-// ---------------------------------------------------------------------------
-constexpr int kWideDw = 12;  // bytes 0..47
-
-struct CkWide {     // phase-1 state of this lane's frame
-  uint32_t flags;   // as CkLane
-  uint32_t ip_off;  // 14 / 18 / 22
-  uint32_t ip_lo, ip_hi;  // the IPv4 header to sum (ip_hi 0: none)
-  uint32_t l4_lo, l4_hi;  // the L4 range to sum (l4_hi 0: none)
-  uint32_t l4_ck, ps;
-  uint32_t ip_old, w24, l4_old;  // old IPv4 checksum, bytes 24..25, old L4 checksum
-};
-
-// ip_checksum.cc:50-74, l4_checksum.cc:53-82 (the walk of ck_walk, ranges
-// instead of sums)
-__device__ __forceinline__ CkWide ck_parse(const uint8_t *f, const uint32_t (&h)[kWideDw],
-                                           int mode, int stride) {
-  CkWide r;
-  r.flags = 0;
-  r.ip_off = 14;
-  r.ip_lo = r.ip_hi = r.l4_lo = r.l4_hi = 0;
-  r.l4_ck = r.ps = r.ip_old = r.l4_old = 0;
-  r.w24 = hle16(h, 24);
-  const uint32_t et12 = hbe16(h, 12);
-  if (mode & 1) {
-    uint32_t et = et12, off = 14;
-    bool fwd = false;
-    if (et == 0x88a8) {  // kQinQ must carry an 802.1Q tag
-      et = hbe16(h, 16);
-      off = 18;
-      if (et != 0x8100) fwd = true;
-    }
-    if (!fwd && et == 0x8100) {  // kVlan
-      et = off == 14 ? hbe16(h, 16) : hbe16(h, 20);
-      off += 4;
-    }
-    if (!fwd && et == 0x0800) {
-      r.flags |= 1;
-      r.ip_off = off;
-      const uint32_t vihl =
-          off == 14 ? hb(h, 14) : (off == 18 ? hb(h, 18) : hb(h, 22));
-      const uint32_t hl = (vihl & 15) * 4;
-      r.ip_old = off == 14 ? hle16(h, 24) : (off == 18 ? hle16(h, 28) : hle16(h, 32));
-      if (hl >= 20) {
-        r.ip_lo = off;
-        r.ip_hi = off + hl;
-      } else {
-        r.flags |= 2;  // IHL < 5: calc writes 0, verify fails
-      }
-    }
-  }
-  if ((mode & 2) && et12 == 0x0800) {
-    const uint32_t hl = (hb(h, 14) & 15) * 4;
-    const uint32_t proto = hb(h, 23);
-    const uint32_t l4_off = 14 + hl;
-    uint32_t kind = 3, len = 0, valid = 0;
-    if (proto == 17) {
-      kind = 1;
-      const uint32_t v = ld_u16(f + l4_off + 4);
-      len = ((v & 0xFF) << 8) | (v >> 8);
-      valid = len >= 8;
-      r.l4_ck = l4_off + 6;
-    } else if (proto == 6) {
-      kind = 2;
-      const uint32_t ip_len = hbe16(h, 16);
-      valid = ip_len >= hl + 20;
-      len = (ip_len - hl) & 0xFFFF;
-      r.l4_ck = l4_off + 16;
-    }
-    r.flags |= kind << 2;
-    if (kind != 3) {
-      if (valid) {
-        r.flags |= 16;
-        uint32_t hi = l4_off + len;
-        if (hi > (uint32_t)stride) hi = stride;  // reference reads past (UB)
-        r.l4_lo = l4_off;
-        r.l4_hi = hi;
-        r.l4_old = ld_u16(f + r.l4_ck);
-      }
-      r.ps = hle16(h, 26) + hle16(h, 28) + hle16(h, 30) + hle16(h, 32) +
-             ((len >> 8) | ((len & 0xFF) << 8)) + (kind == 1 ? 0x1100u : 0x0600u);
-    }
-  }
-  return r;
-}
-
-// u16-halves sum of the 16 bytes at frame offset o inside [lo, hi)
-__device__ __forceinline__ uint32_t chunk_range_sum(const uint4 &c, int o, int lo, int hi) {
-  if (o >= lo && o + 16 <= hi) {  // (most lanes) the whole chunk
-    return (c.x & 0xFFFFu) + (c.x >> 16) + (c.y & 0xFFFFu) + (c.y >> 16) +
-           (c.z & 0xFFFFu) + (c.z >> 16) + (c.w & 0xFFFFu) + (c.w >> 16);
-  }
-  return dw_range_sum(c.x, o, lo, hi) + dw_range_sum(c.y, o + 4, lo, hi) +
-         dw_range_sum(c.z, o + 8, lo, hi) + dw_range_sum(c.w, o + 12, lo, hi);
-}
-
-// sum over lanes 0..15, read from lane 15
-__device__ __forceinline__ uint32_t row0_sum(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false);   // quad [1,0,3,2]
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x4e, 0xf, 0xf, false);   // quad [2,3,0,1]
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  return __builtin_amdgcn_readlane(v, 15);
-}
-
-template <int DEPTH>
-__device__ __forceinline__ void cksum_wide_body(const CkArgs &a) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
-      ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  const int stride = (int)a.stride;
-  const uint64_t ntiles = (a.n + 63) / 64;
-  for (uint64_t tile = wave0; tile < ntiles; tile += nw) {
-    const uint64_t p0 = tile * 64;
-    const int cnt = (int)((a.n - p0) < 64 ? (a.n - p0) : 64);
-    // ---- phase 1: lane = frame
-    uint8_t *mine = a.frames + (p0 + (uint64_t)lane) * a.stride;
-    CkWide L;
-    uint32_t end = 0;  // the summed bytes end before `end`
-    if (lane < cnt) {
-      uint32_t h[kWideDw];
-      const uint4 *q = reinterpret_cast<const uint4 *>(mine);
-#pragma unroll
-      for (int c = 0; c < kWideDw / 4; c++) {
-        const uint4 v = q[c];
-        h[4 * c] = v.x;
-        h[4 * c + 1] = v.y;
-        h[4 * c + 2] = v.z;
-        h[4 * c + 3] = v.w;
-      }
-      L = ck_parse(mine, h, a.mode, stride);
-      end = L.l4_hi > L.ip_hi ? L.l4_hi : L.ip_hi;
-    } else {
-      L.flags = L.ip_lo = L.ip_hi = L.l4_lo = L.l4_hi = L.l4_ck = L.ps = 0;
-      L.ip_old = L.w24 = L.l4_old = 0;
-      L.ip_off = 14;
-    }
-    // ---- phase 2: bytes [0, end) of each frame across the wave, DEPTH
-    // frames prefetched ahead
-    uint32_t s_l4 = 0, s_ip = 0;
-    const uint8_t *f = a.frames + p0 * a.stride;
-    uint4 q0[DEPTH + 1], q1[DEPTH + 1];
-#pragma unroll
-    for (int d = 0; d <= DEPTH; d++) {
-      q0[d] = q1[d] = make_uint4(0, 0, 0, 0);
-      if (d < DEPTH && d < cnt) {
-        const int e = (int)__builtin_amdgcn_readlane(end, d);
-        if (e > 0) {
-          q0[d] = ld_chunk(f + (size_t)d * a.stride, 0, lane, e);
-          q1[d] = ld_chunk(f + (size_t)d * a.stride, 1, lane, e);
-        }
-      }
-    }
-    for (int j = 0; j < cnt; j++) {
-      if (j + DEPTH < cnt) {  // prefetch frame j+DEPTH
-        const int e = (int)__builtin_amdgcn_readlane(end, j + DEPTH);
-        if (e > 0) {
-          const uint8_t *fn = f + (size_t)DEPTH * a.stride;
-          q0[DEPTH] = ld_chunk(fn, 0, lane, e);
-          q1[DEPTH] = ld_chunk(fn, 1, lane, e);
-        }
-      }
-      const int o = lane * 16;
-      const int hi = (int)__builtin_amdgcn_readlane(L.l4_hi, j);
-      if (hi > 0) {  // wave-uniform
-        const int lo = (int)__builtin_amdgcn_readlane(L.l4_lo, j);
-        uint32_t s = o < hi ? chunk_range_sum(q0[0], o, lo, hi) : 0u;
-        if (o + 1024 < hi) s += chunk_range_sum(q1[0], o + 1024, lo, hi);
-        s = wave_sum(s);
-        s_l4 = lane == j ? s : s_l4;
-      }
-      const int ih = (int)__builtin_amdgcn_readlane(L.ip_hi, j);
-      if (ih > 0) {  // wave-uniform; the header lies in bytes < 82
-        const int il = (int)__builtin_amdgcn_readlane(L.ip_lo, j);
-        uint32_t s = o < ih ? chunk_range_sum(q0[0], o, il, ih) : 0u;
-        s = row0_sum(s);
-        s_ip = lane == j ? s : s_ip;
-      }
-#pragma unroll
-      for (int d = 0; d < DEPTH; d++) {
-        q0[d] = q0[d + 1];
-        q1[d] = q1[d + 1];
-      }
-      q0[DEPTH] = q1[DEPTH] = make_uint4(0, 0, 0, 0);
-      f += a.stride;
-    }
-    if (lane >= cnt) continue;
-    // ---- phase 3: lane = frame (as cksum_body's)
-    uint32_t ip_gate = 0;
-    bool ip_wrote = false;
-    uint32_t ip_new = 0;
-    if (L.flags & 1) {
-      if (L.flags & 2) {  // IHL < 5: calc writes 0, verify fails
-        if (a.verify) {
-          ip_gate = 1;
-        } else {
-          ip_wrote = true;
-        }
-      } else if (a.verify) {
-        ip_gate = fold16(s_ip) == 0xFFFFu ? 0u : 1u;
-      } else {
-        ip_new = (~fold16(s_ip - L.ip_old)) & 0xFFFFu;
-        ip_wrote = true;
-      }
-    }
-    uint32_t l4_gate = kGateNone, l4_new = 0;
-    bool l4_wrote = false;
-    const uint32_t kind = (L.flags >> 2) & 3;
-    const bool valid = L.flags & 16;
-    const bool l4_runs = (a.mode & 2) && (!(a.mode & 1) || ip_gate == 0);
-    if (l4_runs) {
-      if (kind == 0) {
-        l4_gate = 0;
-      } else if (kind == 3) {
-        l4_gate = kGateNone;
-      } else {
-        uint32_t s = s_l4;
-        uint32_t old = L.l4_old;
-        // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
-        // the "L4 header" overlaps the IP checksum bytes 24..25.
-        if (ip_wrote && L.ip_off == 14 && valid) {
-          const int lo2 = (int)L.l4_lo > 24 ? (int)L.l4_lo : 24;
-          const int hi2 = (int)L.l4_hi < 26 ? (int)L.l4_hi : 26;
-          s = s - dw_range_sum(L.w24, 24, lo2, hi2) + dw_range_sum(ip_new, 24, lo2, hi2);
-          if (L.l4_ck == 24) old = ip_new;
-        }
-        if (a.verify) {
-          if (!valid)
-            l4_gate = 1;
-          else if (kind == 1 && old == 0)
-            l4_gate = 0;  // UDP checksum 0 = not computed
-          else
-            l4_gate = fold16(s + L.ps) == 0xFFFFu ? 0u : 1u;
-        } else {
-          if (valid) {  // invalid UDP/TCP lengths write 0
-            l4_new = (~fold16(s - old + L.ps)) & 0xFFFFu;
-            if (kind == 1 && l4_new == 0) l4_new = 0xFFFFu;  // RFC 768
-          }
-          l4_wrote = true;
-          l4_gate = kind == 1 ? 0u : kGateNone;  // TCP: never emitted
-        }
-      }
-    }
-    if (ip_wrote) *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
-    if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
-      *reinterpret_cast<uint16_t *>(mine + L.l4_ck) = (uint16_t)l4_new;
-    if (a.ip_gates) a.ip_gates[p0 + lane] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
-    if (a.l4_gates) a.l4_gates[p0 + lane] = (uint16_t)l4_gate;
-  }
-}
-
-template <int DEPTH>
-__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
-void cksum_kernel_wide(CkArgs a) { cksum_wide_body<DEPTH>(a); }
 
 template <int RELOAD, int DEPTH>
 __global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
@@ -2158,9 +1901,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
       case 8: kfn = cksum_kernel<3, 2>; break;
       case 9: kfn = cksum_kernel<1, 2>; break;  // round 4's default
       case 10: kfn = cksum_kernel_w5<3, 1>; break;
-      case 11: kfn = cksum_kernel_wide<1>; break;
-      case 12: kfn = cksum_kernel_wide<2>; break;
-      case 13: kfn = cksum_kernel_wide<3>; break;
+      case 14: kfn = cksum_kernel<4, 1>; break;  // words, streaming stores
       default: break;
     }
 #endif

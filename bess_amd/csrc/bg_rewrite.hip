@@ -8,12 +8,18 @@
 #include <hip/hip_runtime.h>
 
 #include "bg_kernels.h"
+#include "bg_launch.h"
 
 namespace bg {
 namespace {
 
 constexpr int kRwBlock = 256;
 
+typedef unsigned int rw_u32x4 __attribute__((ext_vector_type(4)));
+
+// NT: streaming (nontemporal) stores for the templates and the metadata
+// (A/B build: BG_RW_NT)
+template <int NT>
 __global__ __launch_bounds__(kRwBlock) void rewrite_kernel(RewriteArgs a) {
   const uint32_t lpp = 1u << a.lpp_log2;
   const uint64_t lane_g = (uint64_t)blockIdx.x * kRwBlock + threadIdx.x;
@@ -29,10 +35,23 @@ __global__ __launch_bounds__(kRwBlock) void rewrite_kernel(RewriteArgs a) {
     const uint32_t chunks = ((size + 31) & ~31u) / 16;
     const uint4 *src = reinterpret_cast<const uint4 *>(a.tmpl + (uint64_t)t * kRwMaxSize);
     uint4 *dst = reinterpret_cast<uint4 *>(a.slots + i * a.stride + a.headroom);
-    for (uint32_t c = sub; c < chunks; c += lpp) dst[c] = src[c];
+    for (uint32_t c = sub; c < chunks; c += lpp) {
+      if (NT) {
+        const uint4 v = src[c];
+        const rw_u32x4 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<rw_u32x4 *>(dst + c));
+      } else {
+        dst[c] = src[c];
+      }
+    }
     if (sub == 0) {
-      a.head[i] = (uint16_t)a.headroom;
-      a.len[i] = size;
+      if (NT) {
+        __builtin_nontemporal_store((uint16_t)a.headroom, a.head + i);
+        __builtin_nontemporal_store(size, a.len + i);
+      } else {
+        a.head[i] = (uint16_t)a.headroom;
+        a.len[i] = size;
+      }
     }
   }
 }
@@ -45,7 +64,8 @@ hipError_t launch_rewrite(const RewriteArgs &a, int num_cus, hipStream_t s) {
   uint64_t blocks = (lanes + kRwBlock - 1) / kRwBlock;
   const uint64_t cap = (uint64_t)num_cus * 8;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(rewrite_kernel, dim3((unsigned)blocks), dim3(kRwBlock), 0, s, a);
+  auto kern = knob("BG_RW_NT", 0) ? rewrite_kernel<1> : rewrite_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kRwBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -22,8 +22,7 @@ from bess_amd import packets as P  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from test_gpu_parity import edge_frames  # noqa: E402
 
-FORMS = {"default": 0, "reload_d2": 9, "words_d2": 8, "stash_d2": 7,
-         "wide_d1": 11, "wide_d2": 12, "wide_d3": 13}
+FORMS = {"default": 0, "reload_d2": 9, "words_d2": 8, "stash_d2": 7, "words_nt": 14}
 
 
 def run(frames, mode, verify, dev):

@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT"]
 
 
 def set_env(v):
@@ -174,8 +174,7 @@ def main():
                     "w5_d2": {"BG_CK_TILED": 5}, "w5_d3": {"BG_CK_TILED": 6},
                     "stash_d2": {"BG_CK_TILED": 7}, "words_d2": {"BG_CK_TILED": 8},
                     "words_d1_w5": {"BG_CK_TILED": 10},
-                    "wide_d1": {"BG_CK_TILED": 11}, "wide_d2": {"BG_CK_TILED": 12},
-                    "wide_d3": {"BG_CK_TILED": 13},
+                    "words_nt": {"BG_CK_TILED": 14},
                     "words_d1_x8": {"BG_CK_GRID_MULT": 8},
                     "words_d1_x2": {"BG_CK_GRID_MULT": 2}}
         outs = {}
@@ -271,6 +270,19 @@ def main():
             r[k]["Mpps"] = round(n2 / (r[k]["median_ms"] * 1e-3) / 1e6, 1)
         out["wmphase_2k"] = r
         del d, g, f2
+    if "rewrite" in which:
+        # bench.py's Rewrite leg: 16 M packets in 192 B slots, 4 templates
+        # of 60 B; normal vs streaming stores (BG_RW_NT)
+        from bess_amd.modules import Rewrite
+        n = 16 << 20
+        m = Rewrite(templates=[bytes([i]) * 60 for i in range(1, 5)])
+        d = torch.zeros(n * 192, dtype=torch.uint8, device=dev)
+        dh = torch.empty(n, dtype=torch.int16, device=dev)
+        dl = torch.empty(n, dtype=torch.int32, device=dev)
+        r = time_variants(lambda: m.process_device(d, 192, n, dh, dl),
+                          {"stores": {}, "stores_nt": {"BG_RW_NT": 1}}, reps=10)
+        out["rewrite"] = r
+        del d
     if "linew" in which:
         # the writing header-line ops (UpdateTTL, StaticNAT: 16 M 64 B
         # packets in place, as bench.py) with their written-back lines
