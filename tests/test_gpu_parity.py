@@ -155,6 +155,38 @@ def test_em_field_layouts(fields, dev):
     assert (want != 8192).any()
 
 
+@pytest.mark.parametrize("stride", [80, 128, 192, 2048, 2624])
+@pytest.mark.parametrize("fields", [
+    [(23, 1, 0), (26, 4, 0), (30, 4, 0), (34, 2, 0), (36, 2, 0)],  # window at 16
+    [(0, 6, 0), (12, 2, 0)],                                         # at 0
+    [(40, 8, 0), (56, 4, 0)],                                        # at 32
+])
+def test_em_strided_slots_pair_kernel(fields, stride, dev):
+    """Frames in slots wider than 64 B with the key window inside the
+    slot's first 64 B: em_pair_kernel (two lanes per slot, one 32 B
+    request each, round 5) on the default path, the lane kernel under
+    BG_PATH_NO_SLAB -- every table path against the oracle, including a
+    last tile of fewer than 64 slots"""
+    rng = np.random.default_rng(stride)
+    fl = [(o, s, P.default_mask(s) if m == 0 else m) for o, s, m in fields]
+    n = 20000 + 37
+    frames = rng.integers(0, 4, (n, stride), dtype=np.uint8)
+    ks = sum(s for _, s, _ in fl)
+    keys = []
+    for i in rng.choice(n, 400, replace=False):
+        kb = b""
+        for off, size, mask in fl:
+            v = int.from_bytes(frames[i, off:off + size].tobytes(), "little")
+            kb += (v & mask).to_bytes(size, "little")
+        keys.append(kb)
+    keys = list(dict.fromkeys(keys))
+    karr = np.frombuffer(b"".join(keys), np.uint8).reshape(len(keys), ks)
+    gates = rng.integers(0, 8192, len(keys)).astype(np.uint16)
+    got, want, _ = em_compare(fl, karr, gates, frames, stride, 8192, dev)
+    assert (got == want).all()
+    assert (want != 8192).any()
+
+
 def test_em_add_delete_resync(dev):
     keys, gates, frames = P.em_workload(500, 8192, seed=3)
     t = F.EmTable(P.em_fields_5tuple())
