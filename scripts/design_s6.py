@@ -23,7 +23,6 @@ def main():
     passed = m.group(1) if m else "?"
     rel = os.path.relpath(line_path, ROOT)
     c2 = d["roofline"]
-    sw = d["batch_sweep_mpps"]
     head = f"""## 6. Measurements (MI355X, round 5)
 
 `python bench.py` prints one line with C2 as the headline. The line also
@@ -109,21 +108,15 @@ figure is compared with the CPU figure from the same call.
     {l4_p['16']} at 16 workers, PCIe-bound.
 
 """
-    sweep = ["C2 batch sweep (Mpps by packets per batch; resident packets):", "",
-             "| path | 32 | 64 | 128 | 256 | 512 | 1024 | 2048 | 4096 |",
-             "|---|---|---|---|---|---|---|---|---|"]
-    for k in ("stream", "graph", "persistent", "persistent_4sub", "persistent_16sub"):
-        sweep.append("| %s | %s |" % (k, " | ".join("%.0f" % sw[k][b] for b in
-                                                    ("32", "64", "128", "256", "512",
-                                                     "1024", "2048", "4096"))))
+    # (design_table.py's output ends with the batch sweep table)
     if "--write" not in sys.argv:
-        print(head + host + "\n".join(sweep))
+        print(head + SWEEP_NOTE + "\n\n" + host)
         return
     p = os.path.join(ROOT, "DESIGN.md")
     s = open(p).read()
     a = s.index("## 6. Measurements")
     b = s.index("**Counter calibration and measured ceilings")
-    s = s[:a] + head + "\n".join(sweep) + "\n\n" + SWEEP_NOTE + "\n" + s[b:]
+    s = s[:a] + head + SWEEP_NOTE + "\n\n" + s[b:]
     a = s.index("**Host end-to-end (PCIe-inclusive")
     b = s.index("## 7. Out of scope")
     s = s[:a] + host + s[b:]

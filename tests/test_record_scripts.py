@@ -1,7 +1,7 @@
 """The record tooling: DESIGN.md §6's table comes from a bench line
 (scripts/design_table.py) and profiles/rNN_kernels.md from a rocprofv3
 kernel trace (scripts/prof_summary.py) -- both checked here on the
-committed round-4 line and on kernel names as rocprofv3 prints them."""
+committed line §6 names and on kernel names as rocprofv3 prints them."""
 import csv
 import json
 import os
@@ -52,10 +52,19 @@ def test_prof_summary_splits_by_grid(tmp_path):
     assert lines[3].startswith("| em_slab_kernel<2, 2, 1> | 1 | 28 | 80 | 1 | 4.00 |")
 
 
+def design_line():
+    """the bench line DESIGN.md §6 says its table was generated from"""
+    import re
+    with open(os.path.join(ROOT, "DESIGN.md")) as f:
+        m = re.search(r"generated from one such line \(`([^`]+)`", f.read())
+    return os.path.join(ROOT, m.group(1)) if m else LINE
+
+
 def test_design_table_quotes_the_line():
-    with open(LINE) as f:
+    line = design_line()
+    with open(line) as f:
         d = json.loads(f.read().strip().splitlines()[-1])
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "design_table.py"), LINE],
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "design_table.py"), line],
                          capture_output=True, text=True, check=True).stdout
     head = next(l for l in out.splitlines() if l.startswith("| **C2**"))
     assert "%.4f ms" % d["roofline"]["kernel_ms"] in head
