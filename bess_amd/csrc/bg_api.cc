@@ -951,10 +951,8 @@ int bg_em_part_count(const bg_em *em, int part, int nparts, uint64_t *count) {
 int bg_em_plan_count(bg_em *em, int nparts, uint64_t max_part_entries,
                      uint64_t *part_bytes) {
   if (int r = check_nparts(nparts)) return r;
-  // (0.5: a partition build has no retry, and at <= 0.5 load the 16-bucket
-  // blocks of split_hash do not overflow -- Poisson(32) against 60 slots)
   em->planned = plan_layout(max_part_entries, em->kw, 2, (uint32_t)nparts,
-                            kDefaultSeed, 0.5, em_vik(em));
+                            kDefaultSeed, 0.75, em_vik(em));
   em->planned_valid = true;
   *part_bytes = em->planned.part_bytes;
   return 0;

@@ -188,25 +188,15 @@ BG_HD uint32_t log2_pow2(uint32_t x) {
 }
 
 // h1: first bucket (low bits) and fingerprint (top byte); h2: second
-// bucket and partition (top 3 bits). Buckets per partition are <= 2^24, so
-// no two fields share a bit. A table of >= 64 buckets keeps a key's two
-// buckets in one 64 B line of tag words (16 buckets; the second at an
-// offset in [1, 16) drawn from h2's low half): a probe's two tag words are
-// then one L2 request (a scattered lookup is bound by the requests a CU
-// keeps in flight). A 16-bucket block holds 64 slots, and at
-// the <= 0.75 load tables are built to, few blocks overflow; the builder
-// doubles the table when one does.
+// bucket (low bits) and partition (top 3 bits). Buckets per partition are
+// <= 2^24, so no two fields share a bit.
 BG_HD Probe split_hash(uint64_t h, uint32_t nparts, uint32_t nbp) {
   Probe p;
   const uint32_t m = nbp - 1, h1 = (uint32_t)h, h2 = (uint32_t)(h >> 32);
   p.part = (h2 >> 29) & (nparts - 1);
   p.b1 = h1 & m;
-  if (nbp >= 64) {
-    p.b2 = (p.b1 & ~15u) | ((p.b1 + 1u + (((h2 & 0xFFFFu) * 15u) >> 16)) & 15u);
-  } else {
-    p.b2 = h2 & m;
-    if (p.b2 == p.b1) p.b2 = (p.b1 ^ 1u) & m;
-  }
+  p.b2 = h2 & m;
+  if (p.b2 == p.b1) p.b2 = (p.b1 ^ 1u) & m;
   const uint32_t t = h1 >> 24;
   p.tag = t ? t : 1u;
   return p;
