@@ -423,7 +423,7 @@ def run_cksum(args, dev, torch):
     got = d[:4096 * 2048].cpu().numpy().reshape(4096, 2048)
     parity = bool((got == ref).all() and
                   (l4g[:4096].cpu().numpy().view(np.uint16) == l4w).all())
-    clock_settle(args, torch)
+    clock_settle(args, torch, lambda: F.cksum(d, 2048, n, 3, False, None, l4g))
     for _ in range(args.warmup):  # recompute is idempotent
         F.cksum(d, 2048, n, 3, False, None, l4g)
     torch.cuda.synchronize()
@@ -487,7 +487,8 @@ def run_em1500(args, dev, torch):
     want = np.zeros(ns, np.uint16)
     L.or_em_process(em, sample.ctypes.data, 64, ns, 8192, want.ctypes.data)
     parity = bool((dg[:ns].cpu().numpy().view(np.uint16) == want).all())
-    ms = _time_steps(lambda: t.classify(d, 2048, n, 8192, dg), args, torch)
+    ms = _time_steps(lambda: t.classify(d, 2048, n, 8192, dg), args, torch,
+                     settle_with_step=True)
     out = {"workload": "1500B pkts (1496B frames, 2048B slots), %d-rule 5-tuple "
                        "ExactMatch, %d resident pkts" % (args.rules, n),
            "pkts": n, "ms_per_step": round(ms, 4),
@@ -936,29 +937,36 @@ def run_plugin_pool(args):
     return out
 
 
-def clock_settle(args, torch):
+def clock_settle(args, torch, fn=None):
     """Untimed, before a leg's warm-up: ~args.settle_ms of back-to-back
-    device work (a 64 MB in-place multiply; not the leg's kernel, so legs
-    that modify their packets in place keep their launch budget). A leg
-    starts after host work (its table build, the parity check) that left the
-    GPU idle, and the first ~25 launches over a fresh slab then run ~14 %
-    slow (profiles/r05/ck_timing_r05i.json): with the driver's --warmup 5 the
-    timed region would measure the clock ramp, not the kernel."""
+    device work. A leg starts after host work (its table build, the parity
+    check) that left the GPU idle, and the first ~25 launches over a fresh
+    slab then run up to 14 % slow (profiles/r05/ck_timing_r05i.json): with
+    the driver's --warmup 5 the timed region would measure that ramp, not
+    the kernel. `fn`: the leg's own launch, for legs whose launches leave
+    their input as it was (classifiers, idempotent checksums); otherwise a
+    64 MB in-place multiply (legs that modify packets in place keep their
+    launch budget, and the headline keeps exactly its W warm-up steps of
+    its own kernel)."""
     if args.settle_ms <= 0:
         return
-    x = torch.ones(16 << 20, dtype=torch.float32, device="cuda")
+    x = None
+    if fn is None:
+        x = torch.ones(16 << 20, dtype=torch.float32, device="cuda")
+        fn = lambda: x.mul_(1.0)  # noqa: E731
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < args.settle_ms:
-        for _ in range(16):
-            x.mul_(1.0)
+        for _ in range(8):
+            fn()
         torch.cuda.synchronize()
     del x
 
 
-def _time_steps(step, args, torch):
+def _time_steps(step, args, torch, settle_with_step=False):
     """warmup, then ms per launch over args.steps launches (HIP events on
-    the launching stream)"""
-    clock_settle(args, torch)
+    the launching stream); settle_with_step: the step leaves its input as
+    it was, so clock_settle runs it"""
+    clock_settle(args, torch, step if settle_with_step else None)
     for _ in range(max(3, args.warmup // 4)):
         step()
     torch.cuda.synchronize()
@@ -1011,7 +1019,8 @@ def run_hashlb(args, dev, torch):
         k = min(n, 1 << 20)
         parity = bool((g[:k].cpu().numpy().view(np.uint16) ==
                        o.process(frames, 64, k)).all())
-        ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+        ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch,
+                         settle_with_step=True)
         out[name] = {"ms_per_step": round(ms, 4),
                      "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
                      "roofline": _roof(EM_BYTES_PER_PKT, n, ms,
@@ -1057,7 +1066,8 @@ def run_acl(args, dev, torch):
         k = min(n, 1 << 18)
         parity = bool((g[:k].cpu().numpy().view(np.uint16) ==
                        o.process(frames, 64, k)).all())
-        ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+        ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch,
+                         settle_with_step=True)
         e = {"ms_per_step": round(ms, 4), "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
              "roofline": _roof(EM_BYTES_PER_PKT, n, ms, "acl"),
              "parity": "bit-exact vs oracle on %d pkts" % k if parity else "MISMATCH"}
@@ -1099,7 +1109,8 @@ def run_iplookup(args, dev, torch):
     k = min(n, 1 << 20)
     parity = bool((g[:k].cpu().numpy().view(np.uint16) ==
                    o.process(frames, 64, k)).all())
-    ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch)
+    ms = _time_steps(lambda: m.process_device(d, 64, n, g), args, torch,
+                         settle_with_step=True)
     out = {"workload": "IPLookup: 64B pkts (64B slots), %d resident pkts, 10K "
                        "routes, DIR-16-8-8 (tbl16 in LDS)" % n, "pkts": n,
            "routes": len(o.rules),
@@ -1443,7 +1454,7 @@ def run_wm(args, dev, torch):
 
     def timed(slab, stride, gates, flags=0):
         with LB.kernel_paths(flags):
-            clock_settle(args, torch)
+            clock_settle(args, torch, lambda: t.classify(slab, stride, n, 8192, gates))
             for _ in range(args.warmup):
                 t.classify(slab, stride, n, 8192, gates)
             torch.cuda.synchronize()
@@ -1612,7 +1623,7 @@ def run_c5(args, dev, torch):
     torch.cuda.synchronize()
     ns = sample.shape[0]
     parity = c5_parity(keys, gates, sample, dg[:ns].cpu().numpy().view(np.uint16))
-    clock_settle(args, torch)
+    clock_settle(args, torch, lambda: t.classify(d, 64, n, 8192, dg))
     for _ in range(args.warmup):
         t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
@@ -1718,7 +1729,7 @@ def run_c5_multi(args, rank, world, dev, torch, dist):
     torch.cuda.synchronize()
     ns = sample.shape[0]
     parity = c5_parity(keys, gates, sample, dg[:ns].cpu().numpy().view(np.uint16))
-    clock_settle(args, torch)
+    clock_settle(args, torch, lambda: t.classify(d, 64, n, 8192, dg))
     for _ in range(args.warmup):
         t.classify(d, 64, n, 8192, dg)
     torch.cuda.synchronize()
