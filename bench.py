@@ -965,9 +965,10 @@ def clock_settle(args, torch, fn=None):
 
 def leg_steps(args):
     """timed launches of a configuration leg other than the headline: at
-    least 100 (the driver's --steps 20 times C4's 2 KB-slot leg 10-17 %
-    slower than 200 steps do, profiles/r05/bench_line_driver_args.json); the
-    headline times exactly --steps"""
+    least 100 (the driver's --steps 20 timed C4's 2 KB-slot leg 10-17 %
+    slower than 200 steps did: profiles/r05/bench_line_driver_args_before_
+    floor.json against bench_line_driver_args.json); the headline times
+    exactly --steps"""
     return max(args.steps, 100)
 
 
