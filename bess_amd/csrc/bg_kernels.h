@@ -151,6 +151,13 @@ BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
   return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
          (uint64_t)kWmWaves * kWmWaveLds;
 }
+// the line form (dense 64 B slots): per wave best[64], a 64-entry queue and
+// the tile's key windows (64 x 32 B) staged from whole-line loads
+constexpr uint32_t kWmWaveLdsLine = 64 * 8 + 64 * 4 + 64 * 32;
+BG_HD uint64_t wm_line_lds_bytes(uint32_t nbp, uint32_t kw) {
+  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
+         (uint64_t)kWmWaves * kWmWaveLdsLine;
+}
 // the streamed form (bg_wm_body.h wm_tags_stream_body): producer waves load
 // the pair-shaped windows (32 B per packet) into an LDS ring of tiles that
 // the consumer waves look up; ring slots: 64 x 32 B + two flag words

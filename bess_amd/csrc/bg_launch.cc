@@ -56,6 +56,12 @@ uint32_t stream_slots(uint32_t nbp, uint32_t kw) {
   return r;
 }
 
+bool wm_line_ok(const WmArgs &a) {
+  return a.stride == 64 && (reinterpret_cast<uintptr_t>(a.frames) & 15) == 0 &&
+         a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
+         wm_line_lds_bytes(a.t.nbp, a.t.kw) <= kLdsMax && knob("BG_WM_LINE", 1) != 0;
+}
+
 int occupancy(const void *kernel, int block, size_t lds, int dflt) {
   for (OccEnt *e = g_occ.load(std::memory_order_acquire); e; e = e->next)
     if (e->kernel == kernel && e->lds == lds && e->block == block) return e->occ;

@@ -53,6 +53,12 @@ int occupancy(const void *kernel, int block, size_t lds, int dflt);
 // producer depth)
 uint32_t stream_slots(uint32_t nbp, uint32_t kw);
 
+// the WildcardMatch tag-word kernels' line form applies (dense 64 B slots,
+// 16 B-aligned slab, the window two chunks inside the slot, its LDS fits;
+// the A/B build: BG_WM_LINE=0 turns it off)
+struct WmArgs;
+bool wm_line_ok(const WmArgs &a);
+
 }  // namespace bg
 
 #endif  // BESS_AMD_BG_LAUNCH_H_

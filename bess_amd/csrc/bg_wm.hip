@@ -39,7 +39,7 @@ hipError_t launch_stream(WmArgs a, uint32_t slots, int num_cus, hipStream_t s) {
 
 template <int KW, int NCH, int PAIR>
 hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
-  const size_t lds = wm_tags_lds_bytes(a.t.nbp, KW);
+  const size_t lds = PAIR == 2 ? wm_line_lds_bytes(a.t.nbp, KW) : wm_tags_lds_bytes(a.t.nbp, KW);
   const uint64_t ntiles = (a.n + 63) / 64;
   uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
@@ -67,9 +67,12 @@ hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   // slots)
   const uint32_t slots = pair && (path_flags() & kPathWmStream)
                              ? stream_slots(a.t.nbp, a.t.kw) : 0u;
+  // dense 64 B slots: the line form when its stages fit beside the tags
+  const bool line = pair && wm_line_ok(a);
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
     return slots ? launch_stream<KW>(a, slots, num_cus, s)                 \
+           : line ? launch_tags<KW, 2, 2>(a, num_cus, s)                   \
            : pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                   \
                 : n2 ? launch_tags<KW, 2, 0>(a, num_cus, s)                \
                      : launch_tags<KW, 4, 0>(a, num_cus, s);

@@ -235,12 +235,12 @@ __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags
   }
 }
 
-template <int KW>
+template <int KW, uint32_t QUEUE = kQueue>
 __device__ __forceinline__ void wm_check(const WmArgs &a, const uint32_t *tags,
                                          const uint64_t *mlds, uint64_t *best,
                                          const uint32_t *q, uint32_t m, int lane,
                                          uint32_t nbp, const uint64_t (&k)[KW]) {
-  if (m <= 64)  // wave-uniform
+  if (QUEUE <= 64 || m <= 64)  // wave-uniform (a 64-entry queue: always)
     wm_check_r<KW, 1>(a, tags, mlds, best, q, m, lane, nbp, k);
   else
     wm_check_r<KW, kPerLane>(a, tags, mlds, best, q, m, lane, nbp, k);
@@ -271,7 +271,7 @@ __device__ __forceinline__ uint64_t wm_direct_value(const WmArgs &a, const uint6
 // issued (wm_tags_body issues the next tile's window there: vector loads
 // retire in order, so the direct values, consumed in this tile, must not be
 // younger than a prefetch the next tile consumes).
-template <class Spec, int KW, int NCH, class Prefetch>
+template <class Spec, int KW, int NCH, uint32_t QUEUE = kQueue, class Prefetch>
 __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
                                         const uint64_t *mlds, uint64_t *best, uint32_t *q,
                                         uint32_t nbp, int lane, uint64_t idx, bool live,
@@ -324,16 +324,16 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
     mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
     total += (uint32_t)__popcll(mk[tu]);
   }
-  for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
+  for (uint32_t r0 = 0; r0 < total; r0 += QUEUE) {
     uint32_t base = 0;
 #pragma unroll
     for (int tu = 0; tu < kMaxTuples; tu++) {
       const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
           (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
       const bool mine = live && ent[tu] != 0;
-      if (total <= kQueue) {  // wave-uniform: one round, no window test
+      if (total <= QUEUE) {  // wave-uniform: one round, no window test
         if (mine) q[pos] = ent[tu];
-      } else if (mine && pos - r0 < kQueue) {
+      } else if (mine && pos - r0 < QUEUE) {
         q[pos - r0] = ent[tu];
       }
       base += (uint32_t)__popcll(mk[tu]);
@@ -342,8 +342,8 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
     if (a.ab_phase == 2) break;
 #endif
     lds_fence();
-    const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
-    wm_check<KW>(a, tags, mlds, best, q, m, lane, nbp, k);
+    const uint32_t m = total - r0 < QUEUE ? total - r0 : QUEUE;
+    wm_check<KW, QUEUE>(a, tags, mlds, best, q, m, lane, nbp, k);
     lds_fence();  // the queue is rewritten by the next round
   }
   lds_fence();
@@ -392,6 +392,14 @@ __device__ __forceinline__ uint64_t *wm_stage_tags(const WmArgs &a, uint8_t *lds
 }
 
 
+// PAIR 2 (the line form; dense 64 B slots, the window inside the slot): a
+// wave reads its tile's 64 slots (4 KB) with lane-contiguous 16-byte loads
+// -- one L2 request per 128 B line, two slots, where the pair loads make
+// one per slot (a scattered lookup is bound by the requests a CU keeps in
+// flight) -- keeps the two window chunks of each slot in a 2 KB
+// per-wave LDS stage, and each lane reads its slot's window there. The
+// next tile's loads are in flight meanwhile (16 VGPRs: the queue rounds
+// are of 64 entries, whose checks take one entry per lane).
 template <class Spec, int KW, int NCH, int PAIR>
 __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -399,7 +407,8 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   const uint64_t *mlds = wm_stage_tags<KW>(a, lds, tag_bytes);
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + kWmDirLds + wid * kWaveLds;
+  uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + kWmDirLds +
+                wid * (PAIR == 2 ? kWmWaveLdsLine : kWaveLds);
   uint64_t *best = reinterpret_cast<uint64_t *>(wl);
   uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
   best[lane] = 0;
@@ -409,6 +418,40 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
+  if constexpr (PAIR == 2) {
+    static_assert(NCH == 2, "the line form stages two window chunks per slot");
+    uint4 *stage = reinterpret_cast<uint4 *>(wl + 64 * 8 + 64 * 4);  // 64 x 2 chunks
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
+    const uint32_t q0 = a.fp.win_lo >> 4;
+    uint4 v[4];
+    auto load_tile = [&](uint64_t tile) {
+      const uint64_t p0 = tile * 64;
+      const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t u = c * 64 + lane;
+        v[c] = u < units ? ld_stream(src + p0 * 4 + u) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    if (t < ntiles) load_tile(t);
+    for (; t < ntiles; t += nw) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t u = c * 64 + lane, d = (u & 3) - q0;
+        if (d < 2u) stage[(u >> 2) * 2 + d] = v[c];
+      }
+      lds_fence();
+      const uint4 x = stage[lane * 2], y = stage[lane * 2 + 1];
+      uint32_t w[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, 0u, 0u};
+      const uint64_t idx = t * 64 + lane;
+      wm_tile<Spec, KW, 2, 64>(
+          a, tags, mlds, best, q, nbp, lane, idx, idx < a.n, w, [&]() {
+            if (t + nw < ntiles) load_tile(t + nw);
+          });
+      lds_fence();  // this tile's stage reads retire before the next writes
+    }
+    return;
+  }
   uint32_t wn[PAIR ? 8 : NCH * 4 + 2];
   if constexpr (PAIR) {
     if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);

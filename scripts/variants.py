@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT", "BG_WM_LINE"]
 
 
 def set_env(v):
@@ -357,7 +357,8 @@ def main():
         for k, m, p, gg in zip(rk, rm, prio, gates):
             t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
         t.sync(0)
-        variants = {"per_wave": {}, "stream_deep": {"BG_WM_STREAM": 1},
+        variants = {"per_wave": {}, "per_wave_pair": {"BG_WM_LINE": 0},
+                    "stream_deep": {"BG_WM_STREAM": 1},
                     "stream_d16": {"BG_WM_STREAM": 1, "BG_WM_STREAM_SLOTS": 28}}
         layouts = (("slab", torch.from_numpy(frames.reshape(-1)).to(dev).repeat(8), 64, 1 << 23),
                    ("2k", torch.from_numpy(P.wm_workload(100000, 1 << 20, stride=2048)[4]
