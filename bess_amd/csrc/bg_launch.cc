@@ -59,7 +59,7 @@ uint32_t stream_slots(uint32_t nbp, uint32_t kw) {
 bool wm_line_ok(const WmArgs &a) {
   return a.stride == 64 && (reinterpret_cast<uintptr_t>(a.frames) & 15) == 0 &&
          a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
-         wm_line_lds_bytes(a.t.nbp, a.t.kw) <= kLdsMax && knob("BG_WM_LINE", 1) != 0;
+         wm_line_lds_bytes(a.t.nbp, a.t.kw) <= kLdsMax && knob("BG_WM_LINE", 0) != 0;
 }
 
 int occupancy(const void *kernel, int block, size_t lds, int dflt) {

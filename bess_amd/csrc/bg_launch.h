@@ -54,8 +54,9 @@ int occupancy(const void *kernel, int block, size_t lds, int dflt);
 uint32_t stream_slots(uint32_t nbp, uint32_t kw);
 
 // the WildcardMatch tag-word kernels' line form applies (dense 64 B slots,
-// 16 B-aligned slab, the window two chunks inside the slot, its LDS fits;
-// the A/B build: BG_WM_LINE=0 turns it off)
+// 16 B-aligned slab, the window two chunks inside the slot, its LDS fits)
+// -- measured slower than the pair loads (C4 slab 0.1661 against 0.1532
+// ms), so only the A/B build selects it (BG_WM_LINE=1)
 struct WmArgs;
 bool wm_line_ok(const WmArgs &a);
 

@@ -357,7 +357,7 @@ def main():
         for k, m, p, gg in zip(rk, rm, prio, gates):
             t.add(k.tobytes(), m.tobytes(), int(p), int(gg))
         t.sync(0)
-        variants = {"per_wave": {}, "per_wave_pair": {"BG_WM_LINE": 0},
+        variants = {"per_wave": {}, "per_wave_line": {"BG_WM_LINE": 1},
                     "stream_deep": {"BG_WM_STREAM": 1},
                     "stream_d16": {"BG_WM_STREAM": 1, "BG_WM_STREAM_SLOTS": 28}}
         layouts = (("slab", torch.from_numpy(frames.reshape(-1)).to(dev).repeat(8), 64, 1 << 23),
