@@ -1719,7 +1719,13 @@ hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
     const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
     const size_t lds = tab + stage;
     int pc = knob("BG_BLOCKS_PER_CU", 0);
-    if (pc <= 0) pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
+    if (pc <= 0) {
+      pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
+      // a table in L2 / MALL: 2 workgroups per CU (16 waves) probe faster
+      // than the occupancy limit (C5: 0.3444 against 0.3557 ms,
+      // scripts/variants.py c5, profiles/r05/c5_variants_r05q.json)
+      if (a.t.lds == kLdsNone) pc = std::min(pc, 2);
+    }
     const uint64_t cap = (uint64_t)num_cus * pc;
     const uint64_t blocks = need > cap ? cap : need;
     if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&

@@ -140,6 +140,7 @@ def main():
         t.sync(0)
         variants = {
             "default": {}, "both_tags": {"BG_EM_PAR2": 1}, "slab_pf2": {"BG_SLAB_PF": 2},
+            "slab_bpc3": {"BG_BLOCKS_PER_CU": 3},
             "slab_pf0": {"BG_SLAB_PF": 0},
             "slab_bpc2": {"BG_BLOCKS_PER_CU": 2},
             "slab_bpc4": {"BG_BLOCKS_PER_CU": 4},
