@@ -190,7 +190,8 @@ __device__ __forceinline__ uint32_t ip_dst_le(uint32_t (&d)[16]) {
 }
 
 inline int line_occupancy(const void *kern, size_t lds) {
-  return occupancy(kern, kLineBlock, lds, 1);
+  const int k = knob("BG_LINE_OCC", 0);  // (A/B build: workgroups per CU)
+  return k > 0 ? k : occupancy(kern, kLineBlock, lds, 1);
 }
 
 // Residency-sized grid; the slab shape for dense 64-byte slots.

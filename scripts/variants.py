@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT", "BG_WM_LINE"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT", "BG_WM_LINE", "BG_NAT_OCC", "BG_LINE_OCC"]
 
 
 def set_env(v):
@@ -218,7 +218,8 @@ def main():
         now = [t0]
         phases = (("full", {}), ("no_timestamp", {"BG_NAT_PHASE": 1}),
                   ("no_lookup", {"BG_NAT_PHASE": 2}), ("both_tags", {"BG_NAT_PAR2": 1}),
-                  ("temporal_lines", {"BG_NAT_TW": 1}))
+                  ("temporal_lines", {"BG_NAT_TW": 1}), ("occ2", {"BG_NAT_OCC": 2}),
+                  ("occ3", {"BG_NAT_OCC": 3}))
         res = {name: [] for name, _ in phases}
         for _ in range(3):
             for name, env in phases:
@@ -288,7 +289,7 @@ def main():
         # the writing header-line ops (UpdateTTL, StaticNAT: 16 M 64 B
         # packets in place, as bench.py) with their written-back lines
         # stored nontemporally (the default) vs normally (BG_LINE_TW); TTL starts at 200
-        # and the 90 launches here stay above 1
+        # and the 180 launches here stay above 1
         from bess_amd.modules import StaticNAT, UpdateTTL
         n = 16 << 20
         _, _, frames = P.em_workload(1000, n, seed=0x5EED, pkt_seed=11)
@@ -307,7 +308,9 @@ def main():
         for name, m in (("ttl", UpdateTTL()), ("static_nat", StaticNAT(pairs=pairs))):
             d = torch.from_numpy(frames.reshape(-1)).to(dev)
             r = time_variants(lambda: m.process_device(d, 64, n, g),
-                              {"lines_nt": {}, "lines": {"BG_LINE_TW": 1}}, reps=8)
+                              {"lines_nt": {}, "lines": {"BG_LINE_TW": 1},
+                               "occ2": {"BG_LINE_OCC": 2}, "occ3": {"BG_LINE_OCC": 3}},
+                              reps=8)
             out["linew_" + name] = r
             del d
     if "wmdirect" in which:
