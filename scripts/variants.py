@@ -285,6 +285,21 @@ def main():
                           {"stores": {}, "stores_nt": {"BG_RW_NT": 1}}, reps=10)
         out["rewrite"] = r
         del d
+    if "lineocc" in which:
+        # the read-only line ops (HashLB l4 and 5-tuple fields on 16 M 64 B
+        # packets) at the occupancy limit vs 2 / 3 workgroups per CU
+        from bess_amd.modules import HashLB
+        n = 16 << 20
+        _, _, frames = P.em_workload(1000, n, seed=0x5EED, pkt_seed=5)
+        d = torch.from_numpy(frames.reshape(-1)).to(dev)
+        g = torch.empty(n, dtype=torch.int16, device=dev)
+        five = [{"offset": o, "num_bytes": sz} for o, sz in P.FIVE_TUPLE]
+        for name, kw in (("hashlb_l4", dict(mode="l4")), ("hashlb_fields", dict(fields=five))):
+            m = HashLB(gates=list(range(8)), **kw)
+            out["lineocc_" + name] = time_variants(
+                lambda: m.process_device(d, 64, n, g),
+                {"default": {}, "occ2": {"BG_LINE_OCC": 2}, "occ3": {"BG_LINE_OCC": 3}}, reps=20)
+        del d
     if "linew" in which:
         # the writing header-line ops (UpdateTTL, StaticNAT: 16 M 64 B
         # packets in place, as bench.py) with their written-back lines
