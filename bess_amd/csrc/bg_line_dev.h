@@ -206,10 +206,11 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
                                                      : line_slab_kernel<Op>;
     const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
     int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);
-    // a writing op: 2 workgroups per CU rather than the occupancy limit
-    // (StaticNAT 0.3761 -> 0.3627 ms, UpdateTTL 0.3738 -> 0.3721;
-    // profiles/r05/linew_r05u.json)
-    if (Op::kWrites && !knob("BG_LINE_OCC", 0)) occ = std::min(occ, 2);
+    // 2 workgroups per CU (16 waves) rather than the occupancy limit:
+    // HashLB l4 0.1906 -> 0.1809 ms, fields 0.1917 -> 0.1814, StaticNAT
+    // 0.3761 -> 0.3627, UpdateTTL 0.3738 -> 0.3721 (profiles/r05/
+    // lineocc_r05v.json, linew_r05u.json) -- as em_slab_kernel runs
+    if (!knob("BG_LINE_OCC", 0)) occ = std::min(occ, 2);
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLineBlock), lds, s, a,
                        (uint32_t)(tab / 4));
