@@ -7,6 +7,8 @@
 // writes 64 contiguous chunks of one or several packets per store.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "bg_kernels.h"
 #include "bg_launch.h"
 
@@ -62,7 +64,7 @@ hipError_t launch_rewrite(const RewriteArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0 || a.ntempl == 0) return hipSuccess;
   const uint64_t lanes = a.n << a.lpp_log2;
   uint64_t blocks = (lanes + kRwBlock - 1) / kRwBlock;
-  const uint64_t cap = (uint64_t)num_cus * 8;
+  const uint64_t cap = (uint64_t)num_cus * std::max(1, knob("BG_RW_BPC", 8));
   if (blocks > cap) blocks = cap;
   auto kern = knob("BG_RW_NT", 0) ? rewrite_kernel<1> : rewrite_kernel<0>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kRwBlock), 0, s, a);

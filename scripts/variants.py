@@ -32,7 +32,7 @@ KNOBS = ["BG_PPL", "BG_NOLDS", "BG_BLOCKS_PER_CU", "BG_GRID_MULT", "BG_FAT",
          "BG_CK_GENERIC", "BG_CK_BLOCKS_PER_CU", "BG_CK_GRID_MULT",
          "BG_CK_TILED", "BG_WM_V", "BG_WM_PF", "BG_EM_PF",
          "BG_NO_SLAB", "BG_SLAB_PF", "BG_WM_BLOCK", "BG_SLAB2", "BG_NAT_PHASE",
-         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT", "BG_WM_LINE", "BG_NAT_OCC", "BG_LINE_OCC"]
+         "BG_EM_PAR2", "BG_WM_STREAM_SLOTS", "BG_EM_PAIR", "BG_EM_TG", "BG_NAT_PAR2", "BG_NAT_TW", "BG_LINE_TW", "BG_RW_NT", "BG_WM_LINE", "BG_NAT_OCC", "BG_LINE_OCC", "BG_RW_BPC"]
 
 
 def set_env(v):
@@ -282,7 +282,9 @@ def main():
         dh = torch.empty(n, dtype=torch.int16, device=dev)
         dl = torch.empty(n, dtype=torch.int32, device=dev)
         r = time_variants(lambda: m.process_device(d, 192, n, dh, dl),
-                          {"stores": {}, "stores_nt": {"BG_RW_NT": 1}}, reps=10)
+                          {"stores": {}, "stores_nt": {"BG_RW_NT": 1},
+                           "bpc2": {"BG_RW_BPC": 2}, "bpc4": {"BG_RW_BPC": 4},
+                           "bpc16": {"BG_RW_BPC": 16}}, reps=10)
         out["rewrite"] = r
         del d
     if "lineocc" in which:
