@@ -2,7 +2,7 @@
 # Round 5 closing call: every GPU test, smoke, the bench as the driver runs
 # it and with the defaults, the kernel trace
 cd "$GRAFT_REPO_ROOT" || exit 1
-OUT="$GRAFT_REPO_ROOT/gpurun_out/r05s"
+OUT="$GRAFT_REPO_ROOT/gpurun_out/${OUTDIR:-r05s}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name timeout cmd...
