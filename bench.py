@@ -1491,8 +1491,6 @@ def run_wm(args, dev, torch):
 
     nan = float("nan")
     parity, ms2k, g2k, aot2k, aot_h = True, nan, None, nan, nan
-    # the streamed form (producer waves, opt-in: BG_PATH_WM_STREAM)
-    ns2k, ns_h = nan, nan
     if args.wm_layout != "slab":  # the frames in 2 KB slots
         d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
         d = d0.repeat(rep)
@@ -1503,8 +1501,7 @@ def run_wm(args, dev, torch):
         parity, g2k = check(dg)
         ms2k = timed(d, 2048, dg)
         same2k, aot2k = aot_check(d, 2048, dg, g2k)
-        same2s, ns2k = aot_check(d, 2048, dg, g2k, LB.BG_PATH_WM_STREAM)
-        parity = parity and same2k and same2s
+        parity = parity and same2k
         del d, dg
     gbs2k = EM_BYTES_PER_PKT * n / (ms2k * 1e-3) / 1e9
     # The same packets' header lines in a dense 64 B slab: the layout the
@@ -1523,8 +1520,7 @@ def run_wm(args, dev, torch):
             parity_h = parity_h and bool((gh == g2k).all())
         ms = timed(hs, 64, dgh)
         same_h, aot_h = aot_check(hs, 64, dgh, gh)
-        same_s, ns_h = aot_check(hs, 64, dgh, gh, LB.BG_PATH_WM_STREAM)
-        parity_h = parity_h and same_h and same_s
+        parity_h = parity_h and same_h
         del hs, dgh
     mpps = n / (ms * 1e-3) / 1e6
     gbs = EM_BYTES_PER_PKT * n / (ms * 1e-3) / 1e9
@@ -1544,9 +1540,6 @@ def run_wm(args, dev, torch):
            "ahead_of_time": {"ms_per_step": round(aot_h, 4),
                              "slots_2k_ms_per_step": round(aot2k, 4),
                              "same_gates": bool(parity and parity_h)},
-           "stream": {"what": "the streamed form: a producer wave loads the windows into an LDS ring, consumer waves look up (BG_PATH_WM_STREAM; measured, not the default)",
-                         "ms_per_step": round(ns_h, 4),
-                         "slots_2k_ms_per_step": round(ns2k, 4)},
            "roofline": {"bound": "hbm", "achieved": round(gbs, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4),

@@ -26,7 +26,6 @@ BG_PATH_LPM_DIR24 = 128
 BG_PATH_PIPE_NO_RING = 256
 BG_PATH_WM_NO_JIT = 512
 BG_PATH_RING_HOST_DESC = 1024
-BG_PATH_WM_STREAM = 2048
 KEY_BYTES = 64
 
 
@@ -144,7 +143,6 @@ _SIGS = {
     "bg_module_attr": (_int, [_vp, _int, C.c_char_p, _sz, C.POINTER(C.c_uint32)]),
     "bg_set_path_flags": (_int, [C.c_uint32]),
     "bg_get_path_flags": (C.c_uint32, []),
-    "bg_is_ab_build": (_int, []),
     "bg_debug_key": (_int, [C.POINTER(bg_field), _int, _int, _vp, _vp]),
     "bg_em_classify_window": (_int, [_vp, _vp, _sz, _sz, _int, _u16, _vp, _vp]),
     "bg_em_window": (None, [_vp, C.POINTER(_int), C.POINTER(_int)]),

@@ -556,10 +556,9 @@ static void em_entries(const bg_em *em, std::vector<uint64_t> *keys,
   }
 }
 
-// the gate fits in the key's unused top bytes (A/B knob BG_EM_VIK=0 of
-// libbessgpu_ab.so)
+// the gate fits in the key's unused top bytes (value in the key)
 static bool em_vik(const bg_em *em) {
-  return knob("BG_EM_VIK", 1) && em->raw_size + 2 <= em->kw * 8;
+  return em->raw_size + 2 <= em->kw * 8;
 }
 
 // the device's image if it is of the current rule-set version
@@ -1268,8 +1267,7 @@ static void wm_pick_direct(bg_wm *wm) {
     uint32_t spec;
     if (!wm_direct_spec(wm, t, &spec) || wm->tuples[t].ht.empty()) continue;
     const bool two = (spec >> 24) != 0;
-    if (two && wm->tuples[t].ht.size() <
-                   (size_t)knob("BG_WM_DIRECT2_MIN", (int)kDirect2MinEntries))
+    if (two && wm->tuples[t].ht.size() < kDirect2MinEntries)
       continue;
     cand.push_back({two, wm->tuples[t].ht.size(), (uint32_t)t});
   }
@@ -1337,11 +1335,9 @@ static int wm_build_host(bg_wm *wm, bool no_tags) {
   // its one- and two-byte tuples become direct tuples (WmArgs::ndirect).
   bool tags_lds = false;
   uint64_t aux_off = 0;
-  if (img.size() > kLdsTableMax && !no_tags && knob("BG_WM_TAGS", 1)) {
-    if (knob("BG_WM_DIRECT", 1)) {
-      wm_pick_direct(wm);
-      wm_entries(wm, &keys, &vals, &hashes);
-    }
+  if (img.size() > kLdsTableMax && !no_tags) {
+    wm_pick_direct(wm);
+    wm_entries(wm, &keys, &vals, &hashes);
     // the highest load that builds: the fewest tag words, the most LDS left
     // beside them (each packet checks the same 2 buckets per tuple; a fuller
     // bucket only adds fingerprint collisions, ~3 % per tuple at 0.95)
@@ -1385,9 +1381,8 @@ static int wm_build_host(bg_wm *wm, bool no_tags) {
   // key, 64 KB by default so two workgroups fit a CU -- measured faster
   // than 128 KB at one workgroup per CU) that the kernel stages in LDS.
   uint32_t fw = 0;
-  const int kb = knob("BG_WM_FILTER_KB", 64);  // A/B knob (variants.py)
-  if (img.size() > kLdsTableMax && !tags_lds && kb > 0 && nkeys > 0) {
-    const uint32_t cap = std::min<uint32_t>(kFilterMaxWords, (uint32_t)kb * 256);
+  if (img.size() > kLdsTableMax && !tags_lds && nkeys > 0) {
+    const uint32_t cap = std::min<uint32_t>(kFilterMaxWords, 64 * 256);
     fw = 1024;
     while (fw < cap && (uint64_t)fw * 32 < (uint64_t)nkeys * 16) fw *= 2;
     if ((uint64_t)fw * 32 < (uint64_t)nkeys * 4) fw = 0;  // < 4 bits/key
@@ -1517,10 +1512,9 @@ static int wm_launch(const std::vector<bg_field> &df, WmImage *img, const void *
   a.gates = d_gates;
   a.default_gate = default_gate;
   a.fp = make_plan(df, false, shift);
-  a.ab_phase = (uint32_t)knob("BG_WM_PHASE", 0);
   img->used_on(s);
   hipError_t e;
-  if (!a.ab_phase && wm_jit_launch(img->jit.get(), a, img->device, num_cus(img->device), s, &e)) {
+  if (wm_jit_launch(img->jit.get(), a, img->device, num_cus(img->device), s, &e)) {
     HIP_TRY(e);
     img->launched_on(s);
     return 0;

@@ -152,9 +152,11 @@ __device__ __forceinline__ SlotHit lookup_in_seq(const TableRef &t, uint64_t key
   }
   return h;
 }
-template <int SEQ = 1>
+// the second bucket read only when the first does not hold the key
+// (0.6097 -> 0.5443 ms per 16 M packets, scripts/variants.py natphase,
+// profiles/r05/natphase_r05n.json)
 __device__ __forceinline__ SlotHit lookup_hit(const DnatArgs &a, uint64_t key) {
-  return SEQ ? lookup_in_seq(a.t, key) : lookup_in(a.t, key);
+  return lookup_in_seq(a.t, key);
 }
 // endpoint -> entry index, or kDnatMiss
 __device__ __forceinline__ uint32_t lookup(const DnatArgs &a, uint64_t key) {
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_apply_kernel(DnatArgs a) {
 // miss drops; a forward miss, or a forward hit on an expired mapping (a new
 // flow earlier in the batch may evict it: CreateNewEntry, nat.cc:224-231),
 // is appended to the list (wave-aggregated) for the host's in-order walk.
-template <int SEQ = 1, class F>
+template <class F>
 __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
                                           uint64_t i, bool live) {
   uint64_t key = ~0ull;
@@ -237,21 +239,10 @@ __device__ __forceinline__ void fused_one(const DnatArgs &a, const F &f,
   uint64_t ts = 0;
   if (live) {
     key = endpoint(f, a.dir);
-#ifdef BG_AB
-    // timing: 2 = no table lookup at all (the endpoint maps to itself)
-    if (a.ab_phase == 2 && key != ~0ull) {
-      h.slot = 0;
-      h.entry = 0;
-      h.ep = key;
-    } else
-#endif
-    if (key != ~0ull) h = lookup_hit<SEQ>(a, key);
+    if (key != ~0ull) h = lookup_hit(a, key);
     // a reverse miss: the forward entries are in the same map (nat.cc Find)
     if (h.slot == ~0u && key != ~0ull && a.dir == 1 && a.t2.base) h = lookup_in(a.t2, key);
     if (h.slot != ~0u && a.dir == 0) ts = a.ts[h.entry];
-#ifdef BG_AB
-    if (a.ab_phase >= 1) ts = a.now;  // timing: the timestamp round trip
-#endif
   }
   // only a forward entry's timestamp decides expiry (nat.cc:222-226)
   bool expired = h.slot != ~0u && a.dir == 0 && a.now - ts > a.timeout;
@@ -324,11 +315,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
 // decides and stamps its slot in LDS, and the tile goes back whole with
 // lane-contiguous 16-byte stores (no partial-line writes).
 constexpr int kNatSlabBlock = 512;
-// SEQ: the sequential second-bucket probe (lookup_in_seq: 0.6097 ->
-// 0.5443 ms per 16 M packets, scripts/variants.py natphase,
-// profiles/r05/natphase_r05n.json); NTW: the tile written back with
-// streaming stores (as the line ops')
-template <int SEQ, int NTW>
+// The tile is written back with streaming stores (as the line ops').
 __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -365,17 +352,13 @@ __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs
     const uint32_t units = units_of(t);
     if (t + nwaves < ntiles) load_tile(t + nwaves);
     const uint64_t idx = t * 64 + lane;
-    fused_one<SEQ>(a, me, idx, idx < a.n);
+    fused_one(a, me, idx, idx < a.n);
     lds_fence();
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t u = c * 64 + lane;
       if (u < units) {
-        const uint4 x = stage[(u >> 2) * 4 + (((u & 3) + (u >> 4)) & 3)];
-        if (NTW)
-          st_stream(src + t * 256 + u, x);
-        else
-          src[t * 256 + u] = x;
+        st_stream(src + t * 256 + u, stage[(u >> 2) * 4 + (((u & 3) + (u >> 4)) & 3)]);
       }
     }
     lds_fence();  // stage reads retire before the next tile's writes
@@ -420,15 +403,11 @@ hipError_t launch_dnat_fused(const DnatArgs &a0, int num_cus, hipStream_t s) {
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
     const size_t lds = (size_t)(kNatSlabBlock / 64) * 4096;
-    // (A/B build: BG_NAT_PAR2 = both tag words together, BG_NAT_TW =
-    // normal line stores)
-    auto kern = knob("BG_NAT_PAR2", 0) ? dnat_fused_slab_kernel<0, 1>
-                : knob("BG_NAT_TW", 0) ? dnat_fused_slab_kernel<1, 0>
-                                       : dnat_fused_slab_kernel<1, 1>;
+    auto kern = dnat_fused_slab_kernel;
     int occ = occupancy(reinterpret_cast<const void *>(kern), kNatSlabBlock, lds, 1);
     // 2 workgroups per CU (16 waves) rather than the occupancy limit (3):
     // 0.5395 -> 0.5017 ms per 16 M packets (profiles/r05/natphase_r05u.json)
-    occ = std::max(1, knob("BG_NAT_OCC", std::min(occ, 2)));
+    occ = std::max(1, std::min(occ, 2));
     const uint64_t need = (a.n + kNatSlabBlock - 1) / kNatSlabBlock;
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kNatSlabBlock), lds, s, a);

@@ -550,7 +550,6 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   a.ts = h->d_ts;
   a.nent = h->ent_ep.size();
   a.out = d_out;
-  a.ab_phase = (uint32_t)knob("BG_NAT_PHASE", 0);
   HIP_TRY(hipMemsetAsync(h->d_nmiss, 0, 4, s));
   const int ncu = num_cus(dev);
   // final hits stamped on the device; forward misses and forward hits on

@@ -133,8 +133,6 @@ struct WmArgs {
   uint32_t dtu[kMaxDirect];    // tuple index
   uint32_t dspec[kMaxDirect];  // key byte a | byte b << 8 | mask a << 16 | mask b << 24
   uint64_t doff[kMaxDirect];   // the table's byte offset in the image
-  uint32_t ab_phase;  // A/B build only: stop after a phase (timing)
-  uint32_t ring_slots;  // the streamed form's LDS ring (wm_stream_slots)
 };
 
 // WildcardMatch tag-word kernels (bg_wm_body.h): one 1024-thread workgroup
@@ -150,42 +148,6 @@ constexpr uint32_t kWmDirLds = 2048u * 2;
 BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
   return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
          (uint64_t)kWmWaves * kWmWaveLds;
-}
-// the line form (dense 64 B slots): per wave best[64], a 64-entry queue and
-// the tile's key windows (64 x 32 B) staged from whole-line loads
-constexpr uint32_t kWmWaveLdsLine = 64 * 8 + 64 * 4 + 64 * 32;
-BG_HD uint64_t wm_line_lds_bytes(uint32_t nbp, uint32_t kw) {
-  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
-         (uint64_t)kWmWaves * kWmWaveLdsLine;
-}
-// the streamed form (bg_wm_body.h wm_tags_stream_body): producer waves load
-// the pair-shaped windows (32 B per packet) into an LDS ring of tiles that
-// the consumer waves look up; ring slots: 64 x 32 B + two flag words
-constexpr int kStreamProducers = 1;
-constexpr int kStreamDepth = 16;  // tiles in flight per producer (vmcnt <= 63)
-constexpr int kStreamDepthDeep = 24;  // ... when the ring has the slots
-// a consumer wave's LDS: best[64] and a 64-entry queue (a tile of more
-// entries is checked in rounds of 64)
-constexpr uint32_t kStreamWaveLds = 64 * 8 + 64 * 4;
-constexpr uint32_t kStreamTileBytes = 64 * 32;
-constexpr uint32_t kStreamMaxSlots = 64;
-constexpr uint32_t kLdsMax = 160 * 1024;  // gfx950 LDS per workgroup
-BG_HD uint64_t wm_stream_fixed_lds(uint32_t nbp, uint32_t kw) {
-  return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
-         (uint64_t)(kWmWaves - kStreamProducers) * kStreamWaveLds;
-}
-// ring slots that fit beside the tag words (0: too few for the producers'
-// depth, the streamed form does not apply)
-BG_HD uint32_t wm_stream_slots(uint32_t nbp, uint32_t kw) {
-  if (kw > 2) return 0;  // (its pipelined consumer's state would spill)
-  const uint64_t fixed = wm_stream_fixed_lds(nbp, kw);
-  if (fixed >= kLdsMax) return 0;
-  uint64_t r = (kLdsMax - fixed) / (kStreamTileBytes + 8);
-  if (r > kStreamMaxSlots) r = kStreamMaxSlots;
-  return r > (uint64_t)(kStreamProducers * kStreamDepth + 4) ? (uint32_t)r : 0u;
-}
-BG_HD uint64_t wm_stream_lds_bytes(uint32_t nbp, uint32_t kw, uint32_t slots) {
-  return wm_stream_fixed_lds(nbp, kw) + (uint64_t)slots * (kStreamTileBytes + 8);
 }
 
 struct CkArgs {
@@ -345,8 +307,7 @@ struct DnatArgs {
   uint16_t *out;
   // apply over a packet list: res[k] = packet, mres[k] = entry, keys[k] =
   // its endpoint, k < nlist (the fused kernel's forward misses)
-  uint32_t list;
-  uint32_t ab_phase;  // A/B build only (timing): 1 = no timestamp read/refresh
+  uint32_t list, pad;
   uint64_t nlist;
   const uint32_t *mres;
   // per listed packet: the translated endpoint as the walk found it when it
@@ -402,11 +363,6 @@ struct RingArgs {
   uint64_t idle_ticks;
   FieldPlan fp;
   TableRef t;
-  // A/B build only (BG_RING_TRACE): per (lane, ticket < trace_n) five
-  // s_memrealtime stamps -- claimed, seen published, descriptor read, gates
-  // stored, done written; null in the product
-  uint64_t *trace;
-  uint64_t trace_n;
 };
 // four waves: a ticket's packets are spread over 256 lanes (4 per lane per
 // round), so a 1024-packet batch takes one round of loads and lookups

@@ -238,32 +238,6 @@ void em_pair_kernel(EmArgs a) {
   }
 }
 
-#ifdef BG_AB
-// next grid-stride packet's window prefetched (A/B experiments: BG_EM_PF=1)
-template <int KW, int NCH>
-__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
-void em_classify_pf_kernel(EmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  copy_table_to_lds(lds, a.t);
-  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t wn[NCH * 4 + 2];
-  if (idx < a.n) load_window<NCH>(a.frames + idx * a.stride, a.fp, wn);
-  for (; idx < a.n; idx += step) {
-    uint32_t w[NCH * 4 + 2];
-#pragma unroll
-    for (int q = 0; q < NCH * 4 + 2; q++) w[q] = wn[q];
-    if (idx + step < a.n)
-      load_window<NCH>(a.frames + (idx + step) * a.stride, a.fp, wn);
-    uint64_t k[KW];
-    extract_key<KW, NCH>(w, a.fp, k);
-    const uint32_t g = a.t.lds == kLdsTable
-                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
-                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
-    a.gates[idx] = (uint16_t)g;
-  }
-}
-#endif  // BG_AB
 
 // ---------------------------------------------------------------------------
 // ExactMatch over a dense 64-byte-slot slab (stride 64, key window inside
@@ -275,19 +249,20 @@ void em_classify_pf_kernel(EmArgs a) {
 // 64 B stride reach ~5.0 TB/s. The stage is swizzled (slot s keeps chunk q
 // at unit 4s + ((q + s/4) & 3)) so both the writes and the per-slot reads
 // of 16 lanes hit 16 distinct 16-byte bank groups.
-// PF: the next tile's four loads are issued before this tile is looked up.
+// The next tile's four loads are issued before this tile is looked up (one
+// tile ahead: measured against none and two, scripts/variants.py).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
   return slot * 4 + ((q + (slot >> 2)) & 3);
 }
 
 
-// SEQ: a table in L2 / MALL is probed with em_lookup_seq (the second
-// bucket's tag word only when the first does not hold the key: C5 0.382 ->
-// 0.357 ms); NTG: the gates are stored nontemporally (streaming stores;
-// C2 0.1896 -> 0.1825 ms). Both measured in one process each
-// (scripts/variants.py em / c5, profiles/r05/em_variants_r05m.json).
-template <int KW, int NCH, int PF, int SEQ = 1, int NTG = 1>
+// A table in L2 / MALL is probed with em_lookup_seq (the second bucket's
+// tag word only when the first does not hold the key: C5 0.382 -> 0.357 ms);
+// the gates are stored nontemporally (streaming stores; C2 0.1896 -> 0.1825
+// ms). Both measured in one process each (scripts/variants.py em / c5,
+// profiles/r05/em_variants_r05m.json).
+template <int KW, int NCH>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_slab_kernel(EmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -303,7 +278,7 @@ void em_slab_kernel(EmArgs a) {
   const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
   const uint32_t q0 = (uint32_t)a.fp.win_lo >> 4;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
-  uint4 v[4], v2[4];
+  uint4 v[4];
   auto load_tile = [&](uint64_t tile, uint4 (&o)[4]) {
     const uint64_t p0 = tile * 64;
     const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
@@ -315,7 +290,6 @@ void em_slab_kernel(EmArgs a) {
     }
   };
   if (t < ntiles) load_tile(t, v);
-  if (PF == 2 && t + nwaves < ntiles) load_tile(t + nwaves, v2);
   for (; t < ntiles; t += nwaves) {
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -323,12 +297,7 @@ void em_slab_kernel(EmArgs a) {
       stage[stage_unit(u >> 2, u & 3)] = v[c];
     }
     lds_fence();
-    if (PF == 1 && t + nwaves < ntiles) load_tile(t + nwaves, v);
-    if (PF == 2) {
-#pragma unroll
-      for (int c = 0; c < 4; c++) v[c] = v2[c];
-      if (t + 2 * nwaves < ntiles) load_tile(t + 2 * nwaves, v2);
-    }
+    if (t + nwaves < ntiles) load_tile(t + nwaves, v);
     uint32_t w[NCH * 4 + 2];
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -345,96 +314,14 @@ void em_slab_kernel(EmArgs a) {
     extract_key<KW, NCH>(w, a.fp, k);
     const uint32_t g = a.t.lds == kLdsTable
                            ? em_lookup<KW>(lds, a.t, k, a.default_gate)
-                           : SEQ ? em_lookup_seq<KW>(a.t.base, a.t, k, a.default_gate)
-                                 : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
+                           : em_lookup_seq<KW>(a.t.base, a.t, k, a.default_gate);
     const uint64_t idx = t * 64 + lane;
-    if (idx < a.n) {
-      if (NTG)  // a streaming store
-        __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
-      else
-        a.gates[idx] = (uint16_t)g;
-    }
-    lds_fence();  // this tile's stage reads retire before the next writes
-    if (PF == 0 && t + nwaves < ntiles) load_tile(t + nwaves, v);
-  }
-}
-
-#ifdef BG_AB
-// Compact-stage slab kernel: only the NCH chunks of each slot's key window
-// are loaded and staged (64 x NCH x 16 B per wave instead of 4 KB), so a
-// workgroup of BLOCK threads fits beside the LDS table at twice the
-// occupancy. Lane l of load c takes unit u = 64c + l of the tile: slot
-// u / NCH, window chunk u % NCH -- pieces of 16 * NCH contiguous bytes per
-// slot. Stage unit of (slot s, chunk j): s*NCH + ((j + s/8) % NCH), which
-// keeps the per-slot reads of 16 lanes on distinct bank groups.
-template <int KW, int NCH, int BLOCK>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80)))
-void em_slab2_kernel(EmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  copy_table_to_lds(lds, a.t);
-  const uint32_t stage_off =
-      a.t.lds == kLdsTable ? ((a.t.bytes_total + 15) & ~15u) : 0u;
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  constexpr int kWaves = BLOCK / 64;
-  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_off) + wid * (64 * NCH);
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t ntiles = (a.n + 63) / 64;
-  const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
-  const uint32_t q0 = (uint32_t)a.fp.win_lo >> 4;
-  const uint32_t nch = (uint32_t)a.fp.nch;
-  uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
-  uint4 v[NCH];
-  auto load_tile = [&](uint64_t tile) {
-    const uint64_t p0 = tile * 64;
-    const uint32_t nslots = (uint32_t)(a.n - p0 < 64 ? a.n - p0 : 64);
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      const uint32_t u = c * 64 + lane;
-      const uint32_t sl = u / NCH, j = u % NCH;
-      v[c] = (sl < nslots && j < nch) ? ld_stream(src + (p0 + sl) * 4 + q0 + j)
-                                      : make_uint4(0, 0, 0, 0);
-    }
-  };
-  if (t < ntiles) load_tile(t);
-  for (; t < ntiles; t += nwaves) {
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      const uint32_t u = c * 64 + lane;
-      const uint32_t sl = u / NCH, j = u % NCH;
-      stage[sl * NCH + ((j + (sl >> 3)) % NCH)] = v[c];
-    }
-    lds_fence();
-    if (t + nwaves < ntiles) load_tile(t + nwaves);
-    uint32_t w[NCH * 4 + 2];
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-      const uint4 x = stage[lane * NCH + ((c + (lane >> 3)) % NCH)];
-      w[4 * c] = x.x;
-      w[4 * c + 1] = x.y;
-      w[4 * c + 2] = x.z;
-      w[4 * c + 3] = x.w;
-    }
-    w[NCH * 4] = 0;
-    w[NCH * 4 + 1] = 0;
-    uint64_t k[KW];
-    extract_key<KW, NCH>(w, a.fp, k);
-    const uint32_t g = a.t.lds == kLdsTable
-                           ? em_lookup<KW>(lds, a.t, k, a.default_gate)
-                           : em_lookup<KW>(a.t.base, a.t, k, a.default_gate);
-    const uint64_t idx = t * 64 + lane;
-    if (idx < a.n) a.gates[idx] = (uint16_t)g;
+    if (idx < a.n)  // a streaming store
+      __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
     lds_fence();  // this tile's stage reads retire before the next writes
   }
 }
 
-// unconstrained SGPRs (A/B experiments only: BG_FAT=1)
-template <int KW, int NCH, int PPL>
-__global__ __launch_bounds__(kEmBlock) void em_classify_fat_kernel(EmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  em_body<KW, NCH, PPL>(a, lds);
-}
-#endif  // BG_AB
 
 // ---------------------------------------------------------------------------
 // Persistent ExactMatch over a ring of batch descriptors (RingArgs,
@@ -566,11 +453,6 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldon
     const uint64_t t = *sh_t + wl;
     const bool release = *sh_rel != 0;
     ring_barrier();  // B2: the gates are stored (sh_* free for the next run)
-#ifdef BG_AB
-    uint64_t *tr = a.trace && wl < k && t < a.trace_n
-                       ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5 : nullptr;
-    if (tr) tr[3] = __builtin_amdgcn_s_memrealtime();
-#endif
     // every wave's gate stores (system-scope write-through stores,
     // completed by each wave's vmcnt(0) before B2) reach the host before
     // the done words; with kRingRelease the L2 is written back first
@@ -579,12 +461,6 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldon
     if (wl < k)
       __hip_atomic_store(ldone + t % a.nslots, (uint32_t)(t + 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-#ifdef BG_AB
-    if (tr) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      tr[4] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
   }
 }
 
@@ -628,9 +504,6 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
   // wave 0's claim state (uniform): the claimed range [next, end)
   uint64_t next = 0, end = 0;
   uint32_t claim = 1;  // tickets per claim
-#ifdef BG_AB
-  uint64_t tclaim = 0;
-#endif
   for (;;) {
     if (threadIdx.x < 64) {  // wave 0
       if (next == end) {
@@ -638,9 +511,6 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         if (wl == 0) t = atomicAdd(dl, (unsigned long long)claim);
         next = __shfl(t, 0);
         end = next + claim;
-#ifdef BG_AB
-        tclaim = __builtin_amdgcn_s_memrealtime();
-#endif
       }
       uint64_t p = 0;
       if (wl == 0) {
@@ -660,14 +530,6 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
       const uint32_t k = p > next ? (uint32_t)((p < end ? p : end) - next) : 0u;
       const uint64_t t = next + wl;
       uint64_t w[4] = {0, 0, 0, 0};
-#ifdef BG_AB
-      uint64_t *tr = a.trace && wl < k && t < a.trace_n
-                         ? a.trace + ((uint64_t)lane * a.trace_n + t) * 5 : nullptr;
-      if (tr) {
-        tr[0] = tclaim;
-        tr[1] = __builtin_amdgcn_s_memrealtime();
-      }
-#endif
       if (wl < k) {
         const uint64_t tag = (t + 1) & 0xFFFF;
         const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
@@ -683,9 +545,6 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       else if (k)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#ifdef BG_AB
-      if (tr) tr[2] = __builtin_amdgcn_s_memrealtime();
-#endif
       // the run's packet prefix sums (inclusive scan over the wave)
       uint32_t c = wl < k ? (uint32_t)w[2] : 0u;
 #pragma unroll
@@ -891,31 +750,24 @@ __device__ __forceinline__ uint32_t wm_lookup_seq(const uint8_t *tab,
   return gate;
 }
 
-// lookup variant: V 1 = wm_lookup_seq, 2 = batched rounds over groups of G
-template <int KW, bool FILT, int V, int G>
-__device__ __forceinline__ uint32_t wm_lookup_v(const uint8_t *tab,
-                                                const WmArgs &a,
-                                                const uint64_t (&k)[KW],
-                                                const uint32_t *filt) {
-  return wm_lookup_seq<KW, FILT>(tab, a, k, filt);
-}
-
-template <int KW, bool FILT, int V, int G>
+// the table in LDS, the key filter in LDS, or the table in L2 / MALL
+template <int KW>
 __device__ __forceinline__ uint32_t wm_lookup_any(const WmArgs &a,
                                                   const uint64_t (&k)[KW],
                                                   const uint8_t *lds) {
-  if (a.t.lds == kLdsTable)
-    return wm_lookup_v<KW, false, V, G>(lds, a, k, nullptr);
+  if (a.t.lds == kLdsTable) return wm_lookup_seq<KW, false>(lds, a, k, nullptr);
   if (a.t.lds == kLdsFilter)
-    return wm_lookup_v<KW, true, V, G>(a.t.base, a, k,
-                                       reinterpret_cast<const uint32_t *>(lds));
-  return wm_lookup_v<KW, false, V, G>(a.t.base, a, k, nullptr);
+    return wm_lookup_seq<KW, true>(a.t.base, a, k, reinterpret_cast<const uint32_t *>(lds));
+  return wm_lookup_seq<KW, false>(a.t.base, a, k, nullptr);
 }
 
-template <int KW, int NCH, int PPL, int V, int G, bool PF>
+// measured on MI355X (scripts/variants.py, C4): the sequential resolve
+// beats a batched-rounds lookup, which hashes every tuple twice; with one
+// packet per lane the next packet's header is prefetched
+template <int KW, int NCH, int PPL>
 __device__ __forceinline__ void wm_body(const WmArgs &a, uint8_t *lds) {
   copy_table_to_lds(lds, a.t);
-  if constexpr (PF && NCH > 0 && PPL == 1) {
+  if constexpr (NCH > 0 && PPL == 1) {
     // one packet per lane, the next grid-stride packet's header window
     // loaded while this one is looked up
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
@@ -930,7 +782,7 @@ __device__ __forceinline__ void wm_body(const WmArgs &a, uint8_t *lds) {
         load_window<NCH>(a.frames + (idx + step) * a.stride, a.fp, wn);
       uint64_t k[KW];
       extract_key<KW, NCH>(w, a.fp, k);
-      a.gates[idx] = (uint16_t)wm_lookup_any<KW, true, V, G>(a, k, lds);
+      a.gates[idx] = (uint16_t)wm_lookup_any<KW>(a, k, lds);
     }
     return;
   }
@@ -942,7 +794,7 @@ __device__ __forceinline__ void wm_body(const WmArgs &a, uint8_t *lds) {
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
       const uint64_t idx = base + (uint64_t)j * blockDim.x;
-      const uint32_t g = wm_lookup_any<KW, true, V, G>(a, k[j], lds);
+      const uint32_t g = wm_lookup_any<KW>(a, k[j], lds);
       if (idx < a.n) a.gates[idx] = (uint16_t)g;
     }
   }
@@ -952,10 +804,7 @@ template <int KW, int NCH, int PPL>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void wm_classify_kernel(WmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  // measured on MI355X (scripts/variants.py, C4): the sequential resolve
-  // beats the batched-rounds lookup, which hashes every tuple twice; the
-  // next packet's header is prefetched (PPL = 1)
-  wm_body<KW, NCH, PPL, 1, 8, true>(a, lds);
+  wm_body<KW, NCH, PPL>(a, lds);
 }
 
 // The persistent ring over a WildcardMatch table (bg::wm_ring_create): the
@@ -965,10 +814,7 @@ void wm_classify_kernel(WmArgs a) {
 // lookup's dependent L2 reads are the latency; four packets' lookups inlined
 // in a row spilled). WmArgs is the FIRST argument: the
 // lookup reads the tuple data at the kernarg segment's start (tuple_masks).
-#ifndef BG_WM_RING_PPL
-#define BG_WM_RING_PPL 1
-#endif
-constexpr int kWmRingPpl = BG_WM_RING_PPL;
+constexpr int kWmRingPpl = 1;
 template <int KW, int NCH>
 __global__ __launch_bounds__(kRingThreads) __attribute__((amdgpu_num_sgpr(80)))
 void wm_ring_kernel(WmArgs w, RingArgs a) {
@@ -979,29 +825,11 @@ void wm_ring_kernel(WmArgs w, RingArgs a) {
   }
   copy_table_to_lds(lds, w.t);  // (ends with a barrier)
   ring_serve<KW, NCH, kWmRingPpl>(a, [&](const uint64_t(&key)[KW], uint32_t dflt) -> uint32_t {
-    const uint32_t g = wm_lookup_any<KW, true, 1, 8>(w, key, lds);
+    const uint32_t g = wm_lookup_any<KW>(w, key, lds);
     return g == kRingNoGate ? dflt : g;
   });
 }
 
-#ifdef BG_AB
-// 1024-thread workgroups: one LDS key-filter copy serves 16 waves
-// (A/B: BG_WM_BLOCK=1024)
-template <int PPL>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_num_sgpr(80)))
-void wm_classify_k1024_kernel(WmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wm_body<2, 2, PPL, 1, 8, PPL == 1>(a, lds);
-}
-
-// A/B variants for the 5-tuple shape (BG_WM_V / BG_WM_G)
-template <int PPL, int V, int G, bool PF>
-__global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
-void wm_classify_exp_kernel(WmArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wm_body<2, 2, PPL, V, G, PF>(a, lds);
-}
-#endif  // BG_AB
 
 // ---------------------------------------------------------------------------
 // IPChecksum + L4Checksum, one wave per frame.
@@ -1407,20 +1235,13 @@ __device__ __forceinline__ uint32_t tail_sum(const uint4 &c, int o, int hi) {
   return s;
 }
 
-// RELOAD: phase 3 re-reads the header line (an L2 hit when it is still
-// resident) instead of holding it in 32 VGPRs through phase 2; 2 (STASH):
-// phase 1 parks the line in LDS (the wave's 64 lines, kCkStashStride
-// bytes apart) and phase 3 takes it from there -- no second read of the
-// line from L2 / HBM (A/B build: BG_CK_TILED=7); 3 (WORDS): phase 1 keeps
-// the two header words phase 3 needs (the old IPv4 checksum, bytes 24..25)
-// and phase 3 stores the checksum words alone -- no re-read and no line
-// store (BG_CK_TILED=8); 4: the same with streaming stores (BG_CK_TILED=14).
-constexpr int kCkStashStride = 144;  // 128 B + 16: lanes' lines on other banks
-template <int RELOAD, int DEPTH>
+// Phase 1 keeps the two header words phase 3 needs (the old IPv4 checksum,
+// bytes 24..25) and phase 3 stores the checksum words alone: no re-read of
+// the header line and no line store. Measured against re-reading the line
+// in phase 3, holding it in VGPRs through phase 2 and parking it in LDS
+// (round 5, scripts/variants.py ck, profiles/r05/ck_variants_*.json).
+template <int DEPTH>
 __device__ __forceinline__ void cksum_body(const CkArgs &a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t ck_lds[];
-  uint4 *stash = reinterpret_cast<uint4 *>(
-      ck_lds + ((threadIdx.x >> 6) * 64 + (threadIdx.x & 63)) * kCkStashStride);
   const int lane = threadIdx.x & 63;
   const uint64_t wave0 = __builtin_amdgcn_readfirstlane(
       ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -1434,7 +1255,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
     uint8_t *mine = a.frames + (p0 + (uint64_t)lane) * a.stride;
     uint32_t h[kHdrDw];
     CkLane L;
-    uint32_t ip_old = 0, w24 = 0, l4_old = 0;  // RELOAD >= 3
+    uint32_t ip_old = 0, w24 = 0, l4_old = 0;
     if (lane < cnt) {
       const uint4 *q = reinterpret_cast<const uint4 *>(mine);
 #pragma unroll
@@ -1444,14 +1265,11 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         h[4 * c + 1] = v.y;
         h[4 * c + 2] = v.z;
         h[4 * c + 3] = v.w;
-        if (RELOAD == 2) stash[c] = v;
       }
       L = ck_walk(mine, h, a.mode, stride);
-      if (RELOAD >= 3) {
-        ip_old = L.ip_off == 14 ? hle16(h, 24) : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
-        w24 = hle16(h, 24);
-        l4_old = (L.flags & 16) ? ld_u16(mine + L.l4_ck) : 0u;  // (in the line: an L1 hit)
-      }
+      ip_old = L.ip_off == 14 ? hle16(h, 24) : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
+      w24 = hle16(h, 24);
+      l4_old = (L.flags & 16) ? ld_u16(mine + L.l4_ck) : 0u;  // (in the line: an L1 hit)
     } else {
 #pragma unroll
       for (int d = 0; d < kHdrDw; d++) h[d] = 0;
@@ -1507,17 +1325,6 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
     }
     if (lane >= cnt) continue;
     // ---- phase 3: lane = frame
-    if (RELOAD == 1 || RELOAD == 2) {
-      const uint4 *q = RELOAD == 2 ? stash : reinterpret_cast<const uint4 *>(mine);
-#pragma unroll
-      for (int c = 0; c < kHdrDw / 4; c++) {
-        const uint4 v = q[c];
-        h[4 * c] = v.x;
-        h[4 * c + 1] = v.y;
-        h[4 * c + 2] = v.z;
-        h[4 * c + 3] = v.w;
-      }
-    }
     uint32_t ip_gate = 0;
     bool ip_wrote = false;
     uint32_t ip_new = 0;
@@ -1531,10 +1338,7 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
       } else if (a.verify) {
         ip_gate = fold16(L.s_ip) == 0xFFFFu ? 0u : 1u;
       } else {
-        const uint32_t old = RELOAD >= 3 ? ip_old
-                             : L.ip_off == 14 ? hle16(h, 24)
-                             : (L.ip_off == 18 ? hle16(h, 28) : hle16(h, 32));
-        ip_new = (~fold16(L.s_ip - old)) & 0xFFFFu;
+        ip_new = (~fold16(L.s_ip - ip_old)) & 0xFFFFu;
         ip_wrote = true;
       }
     }
@@ -1550,13 +1354,13 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         l4_gate = kGateNone;
       } else {
         uint32_t s = L.s_l4 + tail;
-        uint32_t old = RELOAD >= 3 ? l4_old : valid ? ld_u16(mine + L.l4_ck) : 0u;
+        uint32_t old = l4_old;
         // Pipeline order: L4Checksum sees IPChecksum's write. With IHL < 5
         // the "L4 header" overlaps the IP checksum bytes 24..25.
         if (ip_wrote && L.ip_off == 14 && valid) {
           const int lo2 = (int)L.l4_lo > 24 ? (int)L.l4_lo : 24;
           const int hi2 = (int)L.l4_hi < 26 ? (int)L.l4_hi : 26;
-          s = s - dw_range_sum(RELOAD >= 3 ? w24 : hle16(h, 24), 24, lo2, hi2) +
+          s = s - dw_range_sum(w24, 24, lo2, hi2) +
               dw_range_sum(ip_new, 24, lo2, hi2);
           if (L.l4_ck == 24) old = ip_new;
         }
@@ -1577,44 +1381,19 @@ __device__ __forceinline__ void cksum_body(const CkArgs &a) {
         }
       }
     }
-    if (ip_wrote || l4_wrote) {
-      // Store the whole 128 B header line first so the checksum words land
-      // in a fully written L2 line (no read-modify-write of a partial line
-      // in HBM), then the words themselves, in the reference's order.
-      if (RELOAD < 3) {
-        uint4 *q = reinterpret_cast<uint4 *>(mine);
-#pragma unroll
-        for (int c = 0; c < kHdrDw / 4; c++)
-          q[c] = make_uint4(h[4 * c], h[4 * c + 1], h[4 * c + 2], h[4 * c + 3]);
-      }
-      if (RELOAD == 4) {  // (A/B: the words form with streaming stores)
-        if (ip_wrote)
-          __builtin_nontemporal_store((uint16_t)ip_new,
-                                      reinterpret_cast<uint16_t *>(mine + L.ip_off + 10));
-        if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
-          __builtin_nontemporal_store((uint16_t)l4_new, reinterpret_cast<uint16_t *>(mine + L.l4_ck));
-      } else {
-        if (ip_wrote)
-          *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
-        if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
-          *reinterpret_cast<uint16_t *>(mine + L.l4_ck) = (uint16_t)l4_new;
-      }
-    }
+    // the checksum words, in the reference's order (IPChecksum first)
+    if (ip_wrote) *reinterpret_cast<uint16_t *>(mine + L.ip_off + 10) = (uint16_t)ip_new;
+    if (l4_wrote && L.l4_ck + 2 <= (uint32_t)stride)
+      *reinterpret_cast<uint16_t *>(mine + L.l4_ck) = (uint16_t)l4_new;
     if (a.ip_gates) a.ip_gates[p0 + lane] = (a.mode & 1) ? (uint16_t)ip_gate : kGateNone;
     if (a.l4_gates) a.l4_gates[p0 + lane] = (uint16_t)l4_gate;
   }
 }
 
-template <int RELOAD, int DEPTH>
+template <int DEPTH>
 __global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
-void cksum_kernel(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
+void cksum_kernel(CkArgs a) { cksum_body<DEPTH>(a); }
 
-#ifdef BG_AB
-template <int RELOAD, int DEPTH>
-__global__ __launch_bounds__(kCkBlock) __attribute__((amdgpu_num_sgpr(80)))
-__attribute__((amdgpu_waves_per_eu(5, 8)))
-void cksum_kernel_w5(CkArgs a) { cksum_body<RELOAD, DEPTH>(a); }
-#endif
 
 // any stride: frame chunks loaded after the header walk, one frame at a time
 __global__ __launch_bounds__(kCkBlock) void cksum_kernel_generic(CkArgs a) {
@@ -1651,18 +1430,12 @@ hipError_t launch_classify(K kernel, Args a, int num_cus, hipStream_t s,
   // Measured on MI355X (scripts/variants.py): with the table in LDS two
   // 512-thread blocks per CU (16 waves) stream fastest -- fewer LDS table
   // fills; with the table in L2/MALL, twice the resident grid.
-  const int per_cu = knob("BG_BLOCKS_PER_CU", 0);
   for (int pass = 0; pass < 2; pass++) {
     const size_t lds = a.t.lds == kLdsTable    ? a.t.bytes_total
                        : a.t.lds == kLdsFilter ? (size_t)a.t.filt_words * 4
                                                : 0;
-    int pc = per_cu;
-    if (pc <= 0) {
-      const int occ =
-          occupancy(reinterpret_cast<const void *>(kernel), block, lds, 2);
-      pc = a.t.lds ? std::min(occ, 2) : occ * 2;
-      pc *= std::max(1, knob("BG_GRID_MULT", 1));
-    }
+    const int occ = occupancy(reinterpret_cast<const void *>(kernel), block, lds, 2);
+    const int pc = a.t.lds ? std::min(occ, 2) : occ * 2;
     const uint64_t cap = (uint64_t)num_cus * pc;
     const uint64_t blocks = need > cap ? cap : need;
     if (a.t.lds && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
@@ -1681,19 +1454,13 @@ hipError_t dispatch(const Args &a, int num_cus, hipStream_t s, int dflt_ppl) {
   int maxops = 0;
   for (int q = 0; q < a.fp.nkd; q++) maxops = std::max(maxops, kd_nops_of(a.fp, q));
   const int nch = a.fp.direct ? 0 : (a.fp.nch <= 2 && maxops <= 2 ? 2 : 4);
-  const int ppl = knob("BG_PPL", dflt_ppl);
+  const int ppl = dflt_ppl;
 #define BG_CASE(KW, NCH, PPL)                                                   \
   if (a.t.kw == KW && nch == NCH && ppl == PPL)                                 \
     return launch_classify(Sel<KW, NCH, PPL>::kernel(), a, num_cus, s, PPL);
-#ifdef BG_AB
-#define BG_PPLS(KW, NCH) BG_CASE(KW, NCH, 1) BG_CASE(KW, NCH, 2)
-#else
-#define BG_PPLS(KW, NCH) BG_CASE(KW, NCH, 1)
-#endif
-#define BG_NCHS(KW) BG_PPLS(KW, 0) BG_PPLS(KW, 2) BG_PPLS(KW, 4)
+#define BG_NCHS(KW) BG_CASE(KW, 0, 1) BG_CASE(KW, 2, 1) BG_CASE(KW, 4, 1)
   BG_NCHS(1) BG_NCHS(2) BG_NCHS(4) BG_NCHS(8)
 #undef BG_NCHS
-#undef BG_PPLS
 #undef BG_CASE
   return hipErrorInvalidValue;
 }
@@ -1718,14 +1485,11 @@ hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
   for (int pass = 0; pass < 2; pass++) {
     const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
     const size_t lds = tab + stage;
-    int pc = knob("BG_BLOCKS_PER_CU", 0);
-    if (pc <= 0) {
-      pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
-      // a table in L2 / MALL: 2 workgroups per CU (16 waves) probe faster
-      // than the occupancy limit (C5: 0.3444 against 0.3557 ms,
-      // scripts/variants.py c5, profiles/r05/c5_variants_r05q.json)
-      if (a.t.lds == kLdsNone) pc = std::min(pc, 2);
-    }
+    int pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
+    // a table in L2 / MALL: 2 workgroups per CU (16 waves) probe faster
+    // than the occupancy limit (C5: 0.3444 against 0.3557 ms,
+    // scripts/variants.py c5, profiles/r05/c5_variants_r05q.json)
+    if (a.t.lds == kLdsNone) pc = std::min(pc, 2);
     const uint64_t cap = (uint64_t)num_cus * pc;
     const uint64_t blocks = need > cap ? cap : need;
     if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&
@@ -1742,26 +1506,7 @@ hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
 template <int KW, int NCH>
 hipError_t launch_em_slab(const EmArgs &a, int num_cus, hipStream_t s) {
   constexpr size_t kStage = (size_t)(kEmBlock / 64) * 4096;
-#ifdef BG_AB
-  const int v2 = knob("BG_SLAB2", 0);
-  if (v2 == 512)
-    return launch_slab(em_slab2_kernel<KW, NCH, 512>, a, num_cus, s, 512,
-                       (size_t)8 * 64 * NCH * 16);
-  if (v2 == 1024)
-    return launch_slab(em_slab2_kernel<KW, NCH, 1024>, a, num_cus, s, 1024,
-                       (size_t)16 * 64 * NCH * 16);
-  // round 4's form: both tag words read together, gates stored normally
-  if (knob("BG_EM_PAR2", 0))
-    return launch_slab(em_slab_kernel<KW, NCH, 1, 0, 1>, a, num_cus, s, kEmBlock, kStage);
-  if (knob("BG_EM_TG", 0))
-    return launch_slab(em_slab_kernel<KW, NCH, 1, 1, 0>, a, num_cus, s, kEmBlock, kStage);
-  // prefetch depth (tiles ahead)
-  const int pf = std::min(2, std::max(0, knob("BG_SLAB_PF", 1)));
-  if (pf == 0) return launch_slab(em_slab_kernel<KW, NCH, 0>, a, num_cus, s, kEmBlock, kStage);
-  if (pf == 2) return launch_slab(em_slab_kernel<KW, NCH, 2>, a, num_cus, s, kEmBlock, kStage);
-#endif
-  // one tile ahead: measured on MI355X (scripts/variants.py) against 0 and 2
-  return launch_slab(em_slab_kernel<KW, NCH, 1>, a, num_cus, s, kEmBlock, kStage);
+  return launch_slab(em_slab_kernel<KW, NCH>, a, num_cus, s, kEmBlock, kStage);
 }
 
 }  // namespace
@@ -1830,22 +1575,12 @@ hipError_t launch_em(const EmArgs &a, int num_cus, hipStream_t s) {
   // strided slots with the window in the slot's first 64 B: pair loads
   // (measured: scripts/variants.py em1500)
   if (!a.fp.direct && fits_nch2(a.fp) && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
-      a.stride > 64 && a.stride <= 65536 && !(path_flags() & kPathNoSlab) &&
-      knob("BG_EM_PAIR", 1)) {
+      a.stride > 64 && a.stride <= 65536 && !(path_flags() & kPathNoSlab)) {
 #define BG_PAIR(KW) \
   if (a.t.kw == KW) return launch_classify(em_pair_kernel<KW>, a, num_cus, s, 1);
     BG_PAIR(1) BG_PAIR(2) BG_PAIR(4) BG_PAIR(8)
 #undef BG_PAIR
   }
-#ifdef BG_AB
-  if (knob("BG_EM_PF", 0) && a.t.kw == 2 && fits_nch2(a.fp))
-    return launch_classify(em_classify_pf_kernel<2, 2>, a, num_cus, s, 1);
-  if (knob("BG_FAT", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {
-    if (knob("BG_PPL", kDefaultPpl) == 2)
-      return launch_classify(em_classify_fat_kernel<2, 2, 2>, a, num_cus, s, 2);
-    return launch_classify(em_classify_fat_kernel<2, 2, 1>, a, num_cus, s, 1);
-  }
-#endif
   return dispatch<EmSel>(a, num_cus, s, kDefaultPpl);
 }
 
@@ -1860,23 +1595,6 @@ hipError_t launch_wm(const WmArgs &a, int num_cus, hipStream_t s) {
     b.t.lds = kLdsNone;
     return dispatch<WmSel>(b, num_cus, s, 1);
   }
-#ifdef BG_AB
-  if (knob("BG_WM_BLOCK", 512) == 1024 && a.t.kw == 2 && fits_nch2(a.fp)) {
-    if (knob("BG_PPL", 1) == 2)
-      return launch_classify(wm_classify_k1024_kernel<2>, a, num_cus, s, 2, 1024);
-    return launch_classify(wm_classify_k1024_kernel<1>, a, num_cus, s, 1, 1024);
-  }
-  if (knob("BG_WM_V", 0) && a.t.kw == 2 && fits_nch2(a.fp)) {
-    const int ppl = knob("BG_PPL", 2);
-    const bool pf = knob("BG_WM_PF", 0) != 0;
-#define BG_WMX(P, PF) \
-  if (ppl == P && pf == PF) \
-    return launch_classify(wm_classify_exp_kernel<P, 1, 8, PF>, a, num_cus, s, P);
-    BG_WMX(1, false) BG_WMX(2, false) BG_WMX(1, true)
-#undef BG_WMX
-    return hipErrorInvalidValue;
-  }
-#endif
   return dispatch<WmSel>(a, num_cus, s, 1);
 }
 
@@ -1884,7 +1602,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   // (frames by pointer: one wave per frame wherever it lies)
   const bool tiled = !a.ptrs && a.stride >= 128 && a.stride <= 2048 &&
-                     !(path_flags() & kPathNoSlab) && !knob("BG_CK_GENERIC", 0);
+                     !(path_flags() & kPathNoSlab);
   using CkKern = void (*)(CkArgs);
   CkKern kfn = cksum_kernel_generic;
   if (tiled) {
@@ -1894,34 +1612,11 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
     // re-reading the line (round 4's default, 0.2964 -> 0.2896 ms per 1 M
     // frames, 31 B/pkt less fetched), holding it in registers (0.362) or
     // parking it in LDS (0.368); prefetch depth 1
-    kfn = cksum_kernel<3, 1>;
-#ifdef BG_AB
-    switch (knob("BG_CK_TILED", 0)) {
-      case 1: kfn = cksum_kernel<0, 1>; break;
-      case 2: kfn = cksum_kernel<1, 1>; break;
-      case 3: kfn = cksum_kernel<1, 3>; break;
-      case 4: kfn = cksum_kernel<0, 2>; break;
-      case 5: kfn = cksum_kernel_w5<1, 2>; break;
-      case 6: kfn = cksum_kernel_w5<1, 3>; break;
-      case 7: kfn = cksum_kernel<2, 2>; break;
-      case 8: kfn = cksum_kernel<3, 2>; break;
-      case 9: kfn = cksum_kernel<1, 2>; break;  // round 4's default
-      case 10: kfn = cksum_kernel_w5<3, 1>; break;
-      case 14: kfn = cksum_kernel<4, 1>; break;  // words, streaming stores
-      default: break;
-    }
-#endif
+    kfn = cksum_kernel<1>;
   }
   const void *kern = reinterpret_cast<const void *>(kfn);
-  size_t lds = 0;
-#ifdef BG_AB  // the stash form's LDS: each wave's 64 header lines
-  if (kfn == reinterpret_cast<CkKern>(cksum_kernel<2, 2>)) lds = (size_t)kCkBlock * kCkStashStride;
-#endif
-  int per_cu = knob("BG_CK_BLOCKS_PER_CU", 0);
-  if (per_cu <= 0) {
-    const int occ = occupancy(kern, kCkBlock, lds, 7);
-    per_cu = occ * std::max(1, knob("BG_CK_GRID_MULT", 4));
-  }
+  // four residency-sized rounds of workgroups (scripts/variants.py ck)
+  const int per_cu = occupancy(kern, kCkBlock, 0, 7) * 4;
   const uint64_t waves_per_block = kCkBlock / 64;
   const uint64_t max_waves = (uint64_t)num_cus * per_cu * waves_per_block;
   uint64_t waves;
@@ -1934,7 +1629,7 @@ hipError_t launch_cksum(const CkArgs &a, int num_cus, hipStream_t s) {
     waves = std::min<uint64_t>(a.n, max_waves);
   }
   const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
-  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kCkBlock), lds, s, a);
+  hipLaunchKernelGGL(kfn, dim3((unsigned)blocks), dim3(kCkBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -178,8 +178,7 @@ hipError_t launch_hlb(const HlbArgs &a, int num_cus, hipStream_t s) {
   // the slab kernel's lane-contiguous loads (wider strides keep the
   // lane-per-packet kernel, which loads only the window's chunks)
   const bool line = nch > 0 && a.fp.win_lo + 16 * nch <= 64 && a.stride == 64 &&
-                    ((uintptr_t)a.frames & 15) == 0 && !(path_flags() & kPathNoSlab) &&
-                    !knob("BG_HLB_FIELDS_LANE", 0);
+                    ((uintptr_t)a.frames & 15) == 0 && !(path_flags() & kPathNoSlab);
 #define BG_HLB(KW, NCH)                                                       \
   if (kw == KW && nch == NCH)                                                 \
     return line && NCH > 0 ? launch_line<HlbFieldsOp<KW, (NCH > 0 ? NCH : 2)>>(a, num_cus, s) \

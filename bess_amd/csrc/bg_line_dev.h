@@ -77,11 +77,10 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
   }
 }
 
-// NTW: the written-back lines stored nontemporally (streaming stores:
+// The written-back lines are stored nontemporally (streaming stores:
 // UpdateTTL 0.4093 -> 0.3879 ms, StaticNAT 0.4131 -> 0.3908 per 16 M
-// packets, scripts/variants.py linew, profiles/r05/linew_r05n.json; A/B
-// build: BG_LINE_TW=1 for normal stores)
-template <class Op, int NTW = 1>
+// packets, scripts/variants.py linew, profiles/r05/linew_r05n.json).
+template <class Op>
 __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args a,
                                                               uint32_t stage_words) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -147,12 +146,8 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
       for (int c = 0; c < 4; c++) {
         const uint32_t u = c * 64 + lane;
         const uint32_t q = u & 3;
-        if (u < units && q >= (uint32_t)Op::c0 && q < (uint32_t)Op::c1) {
-          if (NTW)
-            st_stream(dst + p0 * 4 + u, stage[line_stage_unit(u >> 2, q)]);
-          else
-            dst[p0 * 4 + u] = stage[line_stage_unit(u >> 2, q)];
-        }
+        if (u < units && q >= (uint32_t)Op::c0 && q < (uint32_t)Op::c1)
+          st_stream(dst + p0 * 4 + u, stage[line_stage_unit(u >> 2, q)]);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -190,8 +185,7 @@ __device__ __forceinline__ uint32_t ip_dst_le(uint32_t (&d)[16]) {
 }
 
 inline int line_occupancy(const void *kern, size_t lds) {
-  const int k = knob("BG_LINE_OCC", 0);  // (A/B build: workgroups per CU)
-  return k > 0 ? k : occupancy(kern, kLineBlock, lds, 1);
+  return occupancy(kern, kLineBlock, lds, 1);
 }
 
 // Residency-sized grid; the slab shape for dense 64-byte slots.
@@ -202,15 +196,14 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
   const uint64_t need = (a.n + kLineBlock - 1) / kLineBlock;
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
-    auto kern = Op::kWrites && knob("BG_LINE_TW", 0) ? line_slab_kernel<Op, 0>
-                                                     : line_slab_kernel<Op>;
+    auto kern = line_slab_kernel<Op>;
     const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
     int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);
     // 2 workgroups per CU (16 waves) rather than the occupancy limit:
     // HashLB l4 0.1906 -> 0.1809 ms, fields 0.1917 -> 0.1814, StaticNAT
     // 0.3761 -> 0.3627, UpdateTTL 0.3738 -> 0.3721 (profiles/r05/
     // lineocc_r05v.json, linew_r05u.json) -- as em_slab_kernel runs
-    if (!knob("BG_LINE_OCC", 0)) occ = std::min(occ, 2);
+    occ = std::min(occ, 2);
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLineBlock), lds, s, a,
                        (uint32_t)(tab / 4));

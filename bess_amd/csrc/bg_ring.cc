@@ -190,7 +190,6 @@ void ring_release(bg_ring *r) {
   if (r->h_reset) (void)hipHostFree(r->h_reset);
   if (r->d_dev) (void)hipFree(r->d_dev);
   if (r->d_table) (void)hipFree(r->d_table);
-  if (r->a.trace) (void)hipFree(r->a.trace);
   if (r->ev) (void)hipEventDestroy(r->ev);
   if (r->st) (void)hipStreamDestroy(r->st);
 }
@@ -356,18 +355,6 @@ static int ring_alloc(int device, int lanes, int slots, int blocks, uint32_t idl
   a.nslots = (uint32_t)slots;
   a.nlanes = (uint32_t)lanes;
   a.idle_ticks = (uint64_t)idle_us * 100;  // s_memrealtime: 100 MHz
-  a.trace = nullptr;
-  a.trace_n = 0;
-#ifdef BG_AB  // per-ticket stamps (scripts/ring_probe.py trace)
-  if (const int tn = knob("BG_RING_TRACE", 0)) {
-    const size_t bytes = nl * (size_t)tn * 5 * 8;
-    if (hipMalloc(reinterpret_cast<void **>(&a.trace), bytes) == hipSuccess &&
-        hipMemset(a.trace, 0, bytes) == hipSuccess)
-      a.trace_n = (uint64_t)tn;
-    else
-      a.trace = nullptr;
-  }
-#endif
   if (!a.desc || !a.done || !a.stop || !a.pub || !a.ended) {
     ring_release(r);
     delete r;
@@ -492,9 +479,8 @@ int64_t bg_ring_submit(bg_ring *r, int lane, const void *frames, size_t stride,
   // A descriptor in device memory goes through the CPU's write-combining
   // buffers and may reach the device after the count below: the tags make
   // a worker read it again until it has. Its stores fill one 64-byte
-  // buffer, which leaves at once. (An sfence per ticket here,
-  // BG_RING_SFENCE=1 in the A/B build, costs a PCIe flush, ~300 ns.)
-  if (r->d_desc && knob("BG_RING_SFENCE", 0)) _mm_sfence();
+  // buffer, which leaves at once. (An sfence per ticket here costs a PCIe
+  // flush, ~300 ns: measured in round 4.)
   __atomic_store_n(l.h_pub, t + 1, __ATOMIC_RELEASE);
   l.next = t + 1;
   if (int rc = ensure_running(r)) return rc;
@@ -578,18 +564,6 @@ double bg_ring_run_lanes(bg_ring *r, int threads, const void *frames, size_t str
   return (end - t0) / reps;
 }
 
-#ifdef BG_AB
-// the A/B build's per-ticket stamps (lanes x trace_n x 5 u64); returns
-// trace_n, 0 without a trace
-int bg_ring_trace(bg_ring *r, uint64_t *out, size_t cap_words) {
-  if (!r->a.trace) return 0;
-  const size_t w = (size_t)r->nlanes * r->a.trace_n * 5;
-  if (cap_words < w) return fail(ENOBUFS, "trace needs %zu words", w);
-  HIP_TRY(hipStreamSynchronize(r->st));
-  HIP_TRY(hipMemcpy(out, r->a.trace, w * 8, hipMemcpyDeviceToHost));
-  return (int)r->a.trace_n;
-}
-#endif
 
 int bg_ring_desc_in_device(const bg_ring *r) { return r && r->d_desc ? 1 : 0; }
 
@@ -597,10 +571,6 @@ int bg_ring_set_coherence(bg_ring *r, int frames, int done) {
   if (!r || frames < 0 || frames > 1 || done < 0 || done > 1)
     return fail(EINVAL, "bad arguments");
   uint64_t c = (frames ? kRingSysAcquire : 0) | (done ? kRingRelease : 0);
-#ifdef BG_AB  // A/B: BG_RING_COHERENCE=1+bit0 sys acquire, +bit1 release
-  if (const int k = knob("BG_RING_COHERENCE", 0))
-    c = ((k - 1) & 1 ? kRingSysAcquire : 0) | ((k - 1) & 2 ? kRingRelease : 0);
-#endif
   r->coherence = c;
   return 0;
 }

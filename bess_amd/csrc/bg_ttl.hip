@@ -7,7 +7,7 @@
 // 64 B slots): writing the whole 64-byte line (C1 = 4) takes 0.41 ms where
 // writing bytes [0, 32) (C1 = 2) takes 0.62 ms -- a partial line costs the
 // memory a read-modify-write. C1 = 2 remains for 32-byte staged windows
-// (host pipe) and the BG_TTL_LINE=0 A/B knob (libbessgpu_ab.so only).
+// (host pipe).
 #include <hip/hip_runtime.h>
 #include "bg_kernels.h"
 #include "bg_launch.h"
@@ -42,7 +42,7 @@ struct TtlOp {
 }  // namespace
 
 hipError_t launch_ttl(const TtlArgs &a, int num_cus, hipStream_t s) {
-  if (a.stride >= 64 && knob("BG_TTL_LINE", 1)) return launch_line<TtlOp<4>>(a, num_cus, s);
+  if (a.stride >= 64) return launch_line<TtlOp<4>>(a, num_cus, s);
   return launch_line<TtlOp<2>>(a, num_cus, s);
 }
 

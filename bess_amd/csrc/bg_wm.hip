@@ -16,30 +16,9 @@ __global__ __launch_bounds__(kWmBlock) void wm_tags_kernel(WmArgs a) {
   wm_tags_body<WmRuntimeSpec, KW, NCH, PAIR>(a);
 }
 
-template <int KW>
-__global__ __launch_bounds__(kWmBlock) void wm_stream_kernel(WmArgs a) {
-  wm_tags_stream_body<WmRuntimeSpec, KW>(a);
-}
-
-template <int KW>
-hipError_t launch_stream(WmArgs a, uint32_t slots, int num_cus, hipStream_t s) {
-  if constexpr (KW > 2) {  // (wm_stream_slots is 0 for these)
-    return hipErrorInvalidValue;
-  } else {
-  a.ring_slots = slots;
-  const uint64_t ntiles = (a.n + 63) / 64;
-  uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
-  if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
-  if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((wm_stream_kernel<KW>), dim3((unsigned)blocks), dim3(kWmBlock),
-                     wm_stream_lds_bytes(a.t.nbp, KW, slots), s, a);
-  return hipGetLastError();
-  }
-}
-
 template <int KW, int NCH, int PAIR>
 hipError_t launch_tags(const WmArgs &a, int num_cus, hipStream_t s) {
-  const size_t lds = PAIR == 2 ? wm_line_lds_bytes(a.t.nbp, KW) : wm_tags_lds_bytes(a.t.nbp, KW);
+  const size_t lds = wm_tags_lds_bytes(a.t.nbp, KW);
   const uint64_t ntiles = (a.n + 63) / 64;
   uint64_t blocks = (ntiles + kWaves - 1) / kWaves;
   if (blocks > (uint64_t)num_cus) blocks = (uint64_t)num_cus;
@@ -62,20 +41,14 @@ hipError_t launch_wm_tags(const WmArgs &a, int num_cus, hipStream_t s) {
   // (both chunks inside the slot: no read past a staged row or the slab)
   const bool pair = n2 && a.fp.win_lo % 16 == 0 && a.fp.win_lo + 32 <= 64 &&
                     a.fp.win_lo + 32 <= a.stride && a.stride <= 65536;
-  // the streamed form when asked for and its ring fits beside the tag words
-  // (bg_wm_body.h; measured slower than this form on C4's slab and 2 KB
-  // slots)
-  const uint32_t slots = pair && (path_flags() & kPathWmStream)
-                             ? stream_slots(a.t.nbp, a.t.kw) : 0u;
-  // dense 64 B slots: the line form when its stages fit beside the tags
-  const bool line = pair && wm_line_ok(a);
+  // (measured and not kept, round 5: a streamed form -- producer waves
+  // loading the windows into an LDS ring -- and a line form staging whole
+  // 64 B slots through LDS; both slower on C4)
 #define BG_WT(KW)                                                          \
   if (a.t.kw == KW)                                                        \
-    return slots ? launch_stream<KW>(a, slots, num_cus, s)                 \
-           : line ? launch_tags<KW, 2, 2>(a, num_cus, s)                   \
-           : pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                   \
-                : n2 ? launch_tags<KW, 2, 0>(a, num_cus, s)                \
-                     : launch_tags<KW, 4, 0>(a, num_cus, s);
+    return pair ? launch_tags<KW, 2, 1>(a, num_cus, s)                     \
+           : n2 ? launch_tags<KW, 2, 0>(a, num_cus, s)                     \
+                : launch_tags<KW, 4, 0>(a, num_cus, s);
   BG_WT(1) BG_WT(2) BG_WT(4) BG_WT(8)
 #undef BG_WT
   return hipErrorInvalidValue;

@@ -186,9 +186,6 @@ __device__ __forceinline__ void wm_check_r(const WmArgs &a, const uint32_t *tags
         z1[r] = bucket_matches(tags, b1, e[r]);
         z2[r] = bucket_matches(tags, wm_b2(b1, e[r] >> 24, nbp), e[r]);
         const uint32_t slot = next_slot(e[r], nbp, z1[r], z2[r]);
-#ifdef BG_AB  // phase timing: checks without their L2 loads
-        if (a.ab_phase == 3) continue;
-#endif
         v[r] = vals[(uint64_t)slot * wm_rec_words(KW)];
 #pragma unroll
         for (int j = 0; j < KW; j++) sk[r][j] = keys[(uint64_t)slot * wm_rec_words(KW) + j];
@@ -287,12 +284,6 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
     if ((uint32_t)d < ndir && live) dv[d] = wm_direct_value<Spec, KW>(a, mlds, k, d);
   }
   prefetch();
-#ifdef BG_AB  // phase timing (scripts/variants.py wmphase): header read only
-  if (a.ab_phase == 1) {
-    if (live) a.gates[idx] = (uint16_t)(k[0] ^ (k[KW - 1] >> 32));
-    return;
-  }
-#endif
   const uint32_t hmask = Spec::hashed(a);
 
   // A. every hashed tuple's probe: both tag words from LDS (all reads in
@@ -338,9 +329,6 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
       }
       base += (uint32_t)__popcll(mk[tu]);
     }
-#ifdef BG_AB  // phase timing: + hashes, tag reads and the queue writes
-    if (a.ab_phase == 2) break;
-#endif
     lds_fence();
     const uint32_t m = total - r0 < QUEUE ? total - r0 : QUEUE;
     wm_check<KW, QUEUE>(a, tags, mlds, best, q, m, lane, nbp, k);
@@ -392,14 +380,8 @@ __device__ __forceinline__ uint64_t *wm_stage_tags(const WmArgs &a, uint8_t *lds
 }
 
 
-// PAIR 2 (the line form; dense 64 B slots, the window inside the slot): a
-// wave reads its tile's 64 slots (4 KB) with lane-contiguous 16-byte loads
-// -- one L2 request per 128 B line, two slots, where the pair loads make
-// one per slot (a scattered lookup is bound by the requests a CU keeps in
-// flight) -- keeps the two window chunks of each slot in a 2 KB
-// per-wave LDS stage, and each lane reads its slot's window there. The
-// next tile's loads are in flight meanwhile (16 VGPRs: the queue rounds
-// are of 64 entries, whose checks take one entry per lane).
+// PAIR 1: the pair loads (lanes 2m / 2m+1 load slot m's two window chunks,
+// one 32 B request per slot); 0: one slot per lane, NCH chunks.
 template <class Spec, int KW, int NCH, int PAIR>
 __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -408,7 +390,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t *wl = lds + tag_bytes + kMaxTuples * KW * 8 + kWmDirLds +
-                wid * (PAIR == 2 ? kWmWaveLdsLine : kWaveLds);
+                wid * kWaveLds;
   uint64_t *best = reinterpret_cast<uint64_t *>(wl);
   uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
   best[lane] = 0;
@@ -418,40 +400,6 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
   uint64_t t = (uint64_t)blockIdx.x * kWaves + wid;
-  if constexpr (PAIR == 2) {
-    static_assert(NCH == 2, "the line form stages two window chunks per slot");
-    uint4 *stage = reinterpret_cast<uint4 *>(wl + 64 * 8 + 64 * 4);  // 64 x 2 chunks
-    const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
-    const uint32_t q0 = a.fp.win_lo >> 4;
-    uint4 v[4];
-    auto load_tile = [&](uint64_t tile) {
-      const uint64_t p0 = tile * 64;
-      const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint32_t u = c * 64 + lane;
-        v[c] = u < units ? ld_stream(src + p0 * 4 + u) : make_uint4(0, 0, 0, 0);
-      }
-    };
-    if (t < ntiles) load_tile(t);
-    for (; t < ntiles; t += nw) {
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint32_t u = c * 64 + lane, d = (u & 3) - q0;
-        if (d < 2u) stage[(u >> 2) * 2 + d] = v[c];
-      }
-      lds_fence();
-      const uint4 x = stage[lane * 2], y = stage[lane * 2 + 1];
-      uint32_t w[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, 0u, 0u};
-      const uint64_t idx = t * 64 + lane;
-      wm_tile<Spec, KW, 2, 64>(
-          a, tags, mlds, best, q, nbp, lane, idx, idx < a.n, w, [&]() {
-            if (t + nw < ntiles) load_tile(t + nw);
-          });
-      lds_fence();  // this tile's stage reads retire before the next writes
-    }
-    return;
-  }
   uint32_t wn[PAIR ? 8 : NCH * 4 + 2];
   if constexpr (PAIR) {
     if (t < ntiles) load_pair(a.frames, a.n, t * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);
@@ -481,329 +429,6 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
       }
     });
   }
-}
-
-// The probe of one tile (step 2): ent[tu] = the packet's queue entry for
-// hashed tuple tu when one of its buckets holds the packet's fingerprint,
-// else 0; all tag reads in flight before any is used.
-template <class Spec, int KW>
-__device__ __forceinline__ void wm_probe_tuples(const WmArgs &a, const uint32_t *tags,
-                                                uint32_t nbp, int lane,
-                                                const uint64_t (&k)[KW],
-                                                uint32_t (&ent)[kMaxTuples]) {
-  const uint32_t hmask = Spec::hashed(a);
-#pragma unroll
-  for (int tu = 0; tu < kMaxTuples; tu++) {
-    ent[tu] = 0;
-    if ((hmask >> tu) & 1u) {
-      const Probe p = wm_probe(Spec::template hash<KW>(k, tu, a), nbp);
-      const uint32_t tb = __builtin_amdgcn_perm(0u, p.tag, 0u);
-      const uint32_t zz = zero_bytes2(tags[p.b1] ^ tb, tags[p.b2] ^ tb);
-      ent[tu] = zz ? p.b1 | ((uint32_t)lane << 15) | ((uint32_t)tu << 21) | (p.tag << 24)
-                   : 0u;
-    }
-  }
-}
-
-// A tile whose checks' loads are in flight (the pipelined consumer): lane
-// = packet idx; its direct tuples' values; its queue entry (lanes < m: the
-// tile's m <= 64 entries, one per lane), the entry's candidate slots left,
-// the first candidate's value and key, the owner's key
-template <int KW>
-struct WmPend {
-  uint64_t idx;
-  uint32_t live, m;
-  uint64_t dv[kMaxDirect];
-  uint32_t e, z1, z2;
-  uint64_t v, sk[KW], kk[KW];
-};
-
-// the pending tile's end (steps 4-5): compare its loaded candidates, fold
-// the hits, try further candidates of fingerprint collisions, store gates
-template <class Spec, int KW>
-__device__ __forceinline__ void wm_finish(const WmArgs &a, const uint32_t *tags,
-                                          const uint64_t *mlds, uint64_t *best, int lane,
-                                          uint32_t nbp, WmPend<KW> &p) {
-  const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
-  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
-  bool more = false;
-  if ((uint32_t)lane < p.m) {
-    if (wm_hit<KW>(mlds, p.e, p.v, p.sk, p.kk)) {
-      wm_fold(best, p.e, p.v);
-      p.z1 = p.z2 = 0;
-    } else if (p.z1) {
-      p.z1 &= p.z1 - 1;
-    } else {
-      p.z2 &= p.z2 - 1;
-    }
-    more = (p.z1 | p.z2) != 0;
-  }
-  if (__builtin_amdgcn_ballot_w64(more)) {  // wave-uniform, rare
-    while (p.z1 | p.z2) {
-      const uint32_t slot = next_slot(p.e, nbp, p.z1, p.z2);
-      if (p.z1)
-        p.z1 &= p.z1 - 1;
-      else
-        p.z2 &= p.z2 - 1;
-      const uint64_t vv = vals[(uint64_t)slot * wm_rec_words(KW)];
-      uint64_t s2[KW];
-#pragma unroll
-      for (int j = 0; j < KW; j++) s2[j] = keys[(uint64_t)slot * wm_rec_words(KW) + j];
-      if (wm_hit<KW>(mlds, p.e, vv, s2, p.kk)) {
-        wm_fold(best, p.e, vv);
-        p.z1 = p.z2 = 0;
-      }
-    }
-  }
-  lds_fence();
-  uint64_t bb = best[lane];
-  best[lane] = 0;
-  const uint32_t ndir = Spec::ndirect(a);
-#pragma unroll
-  for (int d = 0; d < kMaxDirect; d++) {
-    const uint32_t tu = (uint32_t)d < ndir ? Spec::dtu(a, d) : 0xFFFFFFFFu;
-    if ((uint32_t)(p.dv[d] >> 48) == tu) {
-      const uint64_t comb = ((uint64_t)((uint32_t)p.dv[d] ^ 0x80000000u) << 32) |
-                            (1u << 19) | (tu << 16) | ((uint32_t)(p.dv[d] >> 32) & 0xFFFFu);
-      bb = comb > bb ? comb : bb;
-    }
-  }
-  if (p.live)
-    __builtin_nontemporal_store(bb ? (uint16_t)bb : (uint16_t)a.default_gate, a.gates + p.idx);
-}
-
-// ---------------------------------------------------------------------------
-// Streamed form (pair-shaped windows: two 16-byte chunks inside the slot's
-// first 64 bytes). The header stream is decoupled from the lookups: in the
-// form above every wave prefetches one tile, and its key / value loads from
-// L2 retire behind that prefetch (vector loads retire in order), so a wave
-// has one tile of windows in flight for part of its time. Here
-// kStreamProducers waves per workgroup only load windows -- straight into
-// an LDS ring of `a.ring_slots` tiles (global_load_lds), kStreamDepth tiles
-// in flight each, waited for with an explicit vmcnt -- and the other waves
-// (consumers) take tiles from the ring in order and do the lookups, their
-// own loads being only the L2 checks.
-//
-// Ring protocol: the workgroup's tiles j = 0, 1, ... (global tile blockIdx.x
-// + j * gridDim.x) go through ring slot j % R. ready[s] = j + 1 once tile j's
-// windows are in slot s; done[s] = j + 1 once its consumer has read them.
-// Producer p loads tiles p, p + P, ...; it loads tile j only when the slot's
-// previous tile j - R is done, and publishes a tile once kStreamDepth - 1
-// younger ones are issued (or at its end). Consumer c takes tiles c, c + C,
-// ... Every wait is for a smaller tile index, and R > P * kStreamDepth: the
-// smallest unfinished tile can always advance (its producer's pending waits
-// are for tiles below it, all done), so the workgroup drains and every wave
-// leaves after its last tile.
-// ---------------------------------------------------------------------------
-// ring flags: a volatile LDS word (an LDS-typed pointer: a generic volatile
-// access would be a flat instruction, which counts in vmcnt and would make
-// the producer wait for its loads); the data written before a publish has
-// landed first (lgkmcnt), and a wave's LDS operations execute in order
-typedef volatile __attribute__((address_space(3))) uint32_t lds_flag_t;
-__device__ __forceinline__ void lds_wait_eq(const uint32_t *p, uint32_t v) {
-  lds_flag_t *f = (lds_flag_t *)(p);
-  while (*f != v) __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
-  lds_fence();
-  *(lds_flag_t *)(p) = v;
-}
-
-// the pair-shaped windows of tile p0 (slots p0 .. p0 + 63; indices past
-// the slab clamped to n - 1) straight into LDS at `dst` (global_load_lds:
-// lane l's 16 bytes land at dst + 16 l, so slot m's window is at dst + 32 m):
-// no registers, and the producer alone decides when to wait for them
-__device__ __forceinline__ void dma_pair(const uint8_t *__restrict__ frames, uint64_t n,
-                                         uint64_t p0, int lane, uint32_t win_lo,
-                                         uint64_t stride, uint8_t *dst) {
-  uint64_t s0 = p0 + (uint32_t)(lane >> 1), s1 = s0 + 32;
-  s0 = s0 < n ? s0 : n - 1;
-  s1 = s1 < n ? s1 : n - 1;
-  const uint32_t c = (uint32_t)(lane & 1) * 16 + win_lo;
-  typedef const __attribute__((address_space(1))) void *gptr;
-  typedef __attribute__((address_space(3))) void *lptr;
-  __builtin_amdgcn_global_load_lds((gptr)(frames + s0 * stride + c), (lptr)dst, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds((gptr)(frames + s1 * stride + c), (lptr)(dst + 1024), 16,
-                                   0, 0);
-}
-
-template <class Spec, int KW, int D>
-__device__ __forceinline__ void wm_stream_impl(const WmArgs &a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  constexpr int P = kStreamProducers, C = kWaves - kStreamProducers;
-  constexpr uint32_t kWaveLds = kStreamWaveLds, kQueue = 64;
-  const uint32_t tag_bytes = (a.t.nbp * 4 + 15) & ~15u;
-  const uint64_t *mlds = wm_stage_tags<KW>(a, lds, tag_bytes);
-  const uint32_t *tags = reinterpret_cast<const uint32_t *>(lds);
-  // (the wave index in a scalar register: the role and tile branches below
-  // are uniform)
-  const int lane = threadIdx.x & 63,
-            wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint8_t *waves = lds + tag_bytes + kMaxTuples * KW * 8 + kWmDirLds;
-  const uint32_t R = a.ring_slots;
-  uint8_t *ring = waves + C * kWaveLds;
-  uint32_t *ready = reinterpret_cast<uint32_t *>(ring + (uint64_t)R * kStreamTileBytes);
-  uint32_t *done = ready + R;
-  for (uint32_t i = threadIdx.x; i < 2 * R; i += kWmBlock) ready[i] = 0;
-  if (wid >= P) reinterpret_cast<uint64_t *>(waves + (wid - P) * kWaveLds)[lane] = 0;
-  __syncthreads();
-
-  const uint64_t ntiles = (a.n + 63) / 64, G = gridDim.x;
-  // the workgroup's tiles (< 2^32: n < 2^38 packets)
-  const uint64_t K = ntiles > blockIdx.x ? (ntiles - blockIdx.x + G - 1) / G : 0;
-  const uint32_t win_lo = a.fp.win_lo;
-  if (wid < P) {  // producer: windows of tiles wid, wid + P, ... into the ring
-    const uint32_t I = K > (uint64_t)wid ? (uint32_t)((K - wid + P - 1) / P) : 0u;
-    // tile i of this producer: j = wid + P i, slot j % R (kept incrementally)
-    uint32_t slot = (uint32_t)wid % R, pslot = slot;  // issue / publish cursors
-    uint32_t pj = (uint32_t)wid;
-    auto publish = [&]() {  // the oldest issued tile: its windows have landed
-      if (lane == 0) *(lds_flag_t *)&ready[pslot] = pj + 1;
-      pj += P;
-      pslot += P;
-      if (pslot >= R) pslot -= R;
-    };
-    for (uint32_t i = 0; i < I; i++) {
-      const uint32_t j = (uint32_t)wid + P * i;
-      if (j >= R) lds_wait_eq(&done[slot], j - R + 1);  // the slot's last tile read
-      dma_pair(a.frames, a.n, (blockIdx.x + (uint64_t)j * G) * 64, lane, win_lo, a.stride,
-               ring + (uint64_t)slot * kStreamTileBytes);
-      slot += P;
-      if (slot >= R) slot -= R;
-      if (i + 1 >= (uint32_t)D) {  // D tiles in flight: the oldest has landed
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (D - 1)) : "memory");
-        publish();
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    while (pj < (uint32_t)wid + P * I) publish();
-    return;
-  }
-  // consumer, software-pipelined one tile deep: the L2 loads of tile j's
-  // checks are in flight while tile j + C is taken from the ring, keyed,
-  // hashed and probed; then tile j ends and tile j + C's loads are issued.
-  // A wave's only vector loads are its own checks' and direct tuples', so
-  // ending tile j waits for exactly those (vmcnt in order), never for the
-  // header stream.
-  const int c = wid - P;
-  uint8_t *wl = waves + c * kWaveLds;
-  uint64_t *best = reinterpret_cast<uint64_t *>(wl);
-  uint32_t *q = reinterpret_cast<uint32_t *>(wl + 64 * 8);
-  const uint32_t nbp = a.t.nbp;
-  const uint64_t *vals = reinterpret_cast<const uint64_t *>(a.t.base + a.t.vals_off);
-  const uint64_t *keys = reinterpret_cast<const uint64_t *>(a.t.base + a.t.keys_off);
-  WmPend<KW> pd;
-  bool pending = false;
-  uint32_t s = (uint32_t)c % R;
-  for (uint32_t j = (uint32_t)c; j < K; j += C) {
-    // A1: the tile's windows, key, probes and queue
-    lds_wait_eq(&ready[s], j + 1);
-    const uint4 *src = reinterpret_cast<const uint4 *>(ring + (uint64_t)s * kStreamTileBytes) +
-                       2 * lane;
-    const uint4 x = src[0], y = src[1];
-    uint32_t w[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, 0u, 0u};
-    if (lane == 0) lds_publish(&done[s], j + 1);  // (the reads have returned)
-    s += C;
-    while (s >= R) s -= R;
-    const uint64_t idx = (blockIdx.x + (uint64_t)j * G) * 64 + lane;
-    const bool live = idx < a.n;
-    uint64_t k[KW];
-    Spec::template key<KW, 2>(w, a, k);
-    uint32_t total;
-    {
-      uint32_t ent[kMaxTuples];
-      wm_probe_tuples<Spec, KW>(a, tags, nbp, lane, k, ent);
-      const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
-      uint64_t mk[kMaxTuples];
-      total = 0;
-#pragma unroll
-      for (int tu = 0; tu < kMaxTuples; tu++) {
-        mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
-        total += (uint32_t)__popcll(mk[tu]);
-      }
-      if (total <= 64) {  // (uniform) the usual tile: one entry per lane at most
-        uint32_t base = 0;
-#pragma unroll
-        for (int tu = 0; tu < kMaxTuples; tu++) {
-          const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
-          if (live && ent[tu] != 0) q[pos] = ent[tu];
-          base += (uint32_t)__popcll(mk[tu]);
-        }
-      }
-    }
-    // B: the previous tile ends (its loads have had this tile's front)
-    if (pending) wm_finish<Spec, KW>(a, tags, mlds, best, lane, nbp, pd);
-    // A2: this tile's loads: direct tuples, then the checks' first candidates
-    pd.idx = idx;
-    pd.live = live ? 1u : 0u;
-    const uint32_t ndir = Spec::ndirect(a);
-#pragma unroll
-    for (int d = 0; d < kMaxDirect; d++) {
-      pd.dv[d] = ~0ull;
-      if ((uint32_t)d < ndir && live) pd.dv[d] = wm_direct_value<Spec, KW>(a, mlds, k, d);
-    }
-    pd.e = pd.z1 = pd.z2 = 0;
-    pd.v = 0;
-#pragma unroll
-    for (int q2 = 0; q2 < KW; q2++) pd.sk[q2] = pd.kk[q2] = 0;
-    if (total <= 64) {
-      pd.m = total;
-      if (total) {  // (uniform)
-        lds_fence();  // the queue written above
-        if ((uint32_t)lane < total) pd.e = q[lane];
-        owner_key<KW>(pd.e, k, pd.kk);
-        if ((uint32_t)lane < total) {
-          const uint32_t b1 = pd.e & 0x7FFFu;
-          pd.z1 = bucket_matches(tags, b1, pd.e);
-          pd.z2 = bucket_matches(tags, wm_b2(b1, pd.e >> 24, nbp), pd.e);
-          const uint32_t slot = next_slot(pd.e, nbp, pd.z1, pd.z2);
-          pd.v = vals[(uint64_t)slot * wm_rec_words(KW)];
-#pragma unroll
-          for (int q2 = 0; q2 < KW; q2++) pd.sk[q2] = keys[(uint64_t)slot * wm_rec_words(KW) + q2];
-        }
-      }
-    } else {
-      // a tile of more than 64 entries (rare): its checks here, in rounds
-      // of kQueue as wm_tile makes them (the previous tile has ended, so
-      // `best` is this tile's); its end then only folds and stores
-      pd.m = 0;
-      uint32_t ent[kMaxTuples];
-      wm_probe_tuples<Spec, KW>(a, tags, nbp, lane, k, ent);
-      const uint64_t livemask = __builtin_amdgcn_ballot_w64(live);
-      uint64_t mk[kMaxTuples];
-#pragma unroll
-      for (int tu = 0; tu < kMaxTuples; tu++)
-        mk[tu] = __builtin_amdgcn_ballot_w64(ent[tu] != 0) & livemask;
-      for (uint32_t r0 = 0; r0 < total; r0 += kQueue) {
-        uint32_t base = 0;
-#pragma unroll
-        for (int tu = 0; tu < kMaxTuples; tu++) {
-          const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(mk[tu] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[tu], base));
-          if (live && ent[tu] != 0 && pos - r0 < kQueue) q[pos - r0] = ent[tu];
-          base += (uint32_t)__popcll(mk[tu]);
-        }
-        lds_fence();
-        const uint32_t m = total - r0 < kQueue ? total - r0 : kQueue;
-        wm_check<KW>(a, tags, mlds, best, q, m, lane, nbp, k);
-        lds_fence();
-      }
-    }
-    pending = true;
-  }
-  if (pending) wm_finish<Spec, KW>(a, tags, mlds, best, lane, nbp, pd);
-}
-
-// the producers' depth: kStreamDepthDeep tiles each when the ring has the
-// slots for it (wm_stream_slots), else kStreamDepth (a uniform branch)
-template <class Spec, int KW>
-__device__ __forceinline__ void wm_tags_stream_body(const WmArgs &a) {
-  if (a.ring_slots > (uint32_t)(kStreamProducers * kStreamDepthDeep + 4))
-    wm_stream_impl<Spec, KW, kStreamDepthDeep>(a);
-  else
-    wm_stream_impl<Spec, KW, kStreamDepth>(a);
 }
 
 }  // namespace

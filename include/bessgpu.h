@@ -314,13 +314,8 @@ int bg_host_dev_addr(const void *p, size_t len, uint64_t *dev);
 #define BG_PATH_RING_HOST_DESC 1024 /* rings created now keep their descriptors in
                                        pinned host memory (not device memory
                                        through the BAR) */
-#define BG_PATH_WM_STREAM 2048 /* WildcardMatch: the streamed tag-word kernel
-                                  (a producer wave loads the windows into an
-                                  LDS ring, consumer waves look up) */
 int bg_set_path_flags(uint32_t flags);
 uint32_t bg_get_path_flags(void);
-/* 1 only in libbessgpu_ab.so, the A/B measurement build of scripts/ */
-int bg_is_ab_build(void);
 
 /* ---- diagnostics ------------------------------------------------------- */
 /* The key the classify kernels build for `frame` from `fields` (em_masks 1:

@@ -160,14 +160,11 @@ def test_c5_8_partitions_attached(c5):
 
 
 # ------------------------------------------------------------------- C4
-@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_TAGS,
-                                   LB.BG_PATH_WM_STREAM,
-                                   LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_STREAM])
+@pytest.mark.parametrize("flags", [0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_TAGS])
 def test_c4_imix_2k_slots(flags):
     """flags 0: the run-time compiled kernel (bg_wm_jit.cc) once ready;
     BG_PATH_WM_NO_JIT the ahead-of-time one; BG_PATH_WM_NO_TAGS the key
-    filter; BG_PATH_WM_STREAM the streamed form (producer waves,
-    bg_wm_body.h)"""
+    filter"""
     n = 1 << 18
     rk, rm, prio, gates, frames, flen = P.wm_workload(100000, n, stride=2048)
     assert set(np.unique(flen)) == {60, 590, 1514}
@@ -227,9 +224,8 @@ def test_c4_header_slab_full_size():
     del frames
     d_g = torch.zeros(n0 * rep, dtype=torch.int16, device="cuda")
     t.jit_wait()
-    # run-time compiled, ahead-of-time; streamed or not
-    for flags in (0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_STREAM,
-                  LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_STREAM):
+    # run-time compiled, ahead-of-time
+    for flags in (0, LB.BG_PATH_WM_NO_JIT):
         d_g.zero_()
         with LB.kernel_paths(flags):
             t.classify(h, 64, n0 * rep, 8192, d_g)

@@ -235,11 +235,9 @@ def test_em_sharded_build_matches_single(dev):
 def classify_all_paths_wm(t, d_frames, stride, n, default_gate, dev, tags):
     """classify_all_paths with BG_PATH_WM_NO_TAGS kept on (tags == 0)"""
     keep = 0 if tags else LB.BG_PATH_WM_NO_TAGS
-    # the tag-word kernel streamed (producer waves) and not
-    paths = TABLE_PATHS + ((LB.BG_PATH_WM_STREAM,) if tags else ())
+    paths = TABLE_PATHS
     if tags and wm_jit_ready(t):  # the run-time compiled kernel, then without it
-        paths = paths + (LB.BG_PATH_WM_NO_JIT,
-                         LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_STREAM)
+        paths = paths + (LB.BG_PATH_WM_NO_JIT,)
     outs = []
     for flags in paths:
         with LB.kernel_paths(flags | keep):

@@ -84,11 +84,9 @@ def test_source_carries_the_image_constants():
     t = bench_table(20000)
     src = t.jit_source(-1)
     assert "struct WmJitSpec" in src
-    # the 5-tuple in 64 B slots: the pair-load and lane-per-packet variants,
-    # and the streamed form (its LDS ring fits beside the tag words)
+    # the 5-tuple in 64 B slots: the pair-load and lane-per-packet variants
     assert "bg_wm_jit_pair" in src and "bg_wm_jit_n2" in src
-    assert "bg_wm_jit_stream" in src
-    assert "bg_wm_jit_n4" not in src
+    assert "bg_wm_jit_n4" not in src and "stream" not in src
     # the /8 destination tuple is direct; the source port's 2.5 K rules
     # are too sparse a two-byte tuple to be (bg_api.cc kDirect2MinEntries)
     assert "ndirect(const WmArgs &) { return 1u; }" in src
@@ -134,7 +132,7 @@ def test_jit_vs_oracle_random_layouts(seed, stride, n):
     assert t.table_info()[1] == 3  # tag words in LDS
     d_frames = torch.from_numpy(frames.reshape(-1)).cuda()
     outs = []
-    for flags in (0, LB.BG_PATH_WM_NO_JIT, LB.BG_PATH_WM_NO_JIT | LB.BG_PATH_WM_STREAM):
+    for flags in (0, LB.BG_PATH_WM_NO_JIT):
         d_g = torch.zeros(n, dtype=torch.int16, device="cuda")
         with LB.kernel_paths(flags):
             t.classify(d_frames, stride, n, 777, d_g)
