@@ -99,10 +99,13 @@ int bg_host_unregister(void *base) {
     bg::Region &r = bg::g_regions[i];
     if (r.bytes.load(std::memory_order_relaxed) &&
         r.base.load(std::memory_order_relaxed) == reinterpret_cast<uintptr_t>(base)) {
-      r.bytes.store(0, std::memory_order_release);
+      // lookups stop finding the region before it is unpinned; if the
+      // runtime refuses, the region stays pinned and is tracked again
+      const uint64_t bytes = r.bytes.exchange(0, std::memory_order_acq_rel);
       hipError_t e = hipHostUnregister(base);
       if (e != hipSuccess) {
         (void)hipGetLastError();
+        r.bytes.store(bytes, std::memory_order_release);
         return fail(EIO, "hipHostUnregister: %s", hipGetErrorString(e));
       }
       return 0;

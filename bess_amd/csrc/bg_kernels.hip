@@ -1092,9 +1092,9 @@ __device__ __forceinline__ uint4 ld_chunk(const uint8_t *f, int k, int lane,
 //      [128, l4_end) (next frame prefetched), unmasked u16-halves sums with
 //      one tail mask, DPP wave reduction; the sum goes back to the frame's
 //      lane. Frames whose L4 range ends below 128 skip this phase.
-//   3. lane = frame: fold, patch the checksum words into the registers of
-//      the header line and store the whole 128 B line (no partial-line
-//      read-modify-write in HBM), write the gates.
+//   3. lane = frame: fold, store the checksum words (the old words were
+//      kept from phase 1: no second read of the header line), write the
+//      gates.
 // The scalar unit only handles the per-frame loop.
 // ---------------------------------------------------------------------------
 constexpr int kHdrDw = 32;  // 128-byte header line

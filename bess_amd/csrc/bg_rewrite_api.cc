@@ -10,59 +10,120 @@
 
 #include <algorithm>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "bg_internal.h"
 
 using namespace bg;
 
+// One device copy of the templates. A kernel launched against it may still
+// be queued on its stream when the templates change, so the copy is never
+// overwritten: a change uploads a new generation, and the old one is freed
+// once the events recorded behind its launches (one per stream it was
+// launched on) have completed -- this handle's own launches only, never the
+// device's other work (round 5 synchronized the whole device here, which on
+// the datapath waited for other pipes' persistent ring kernels).
+struct RwGen {
+  int device = -1;
+  uint8_t *d_tmpl = nullptr;    // kRwMaxTemplates x kRwMaxSize
+  uint16_t *d_size = nullptr;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> launched;  // stream -> last launch
+  bool done() const {  // every launch against it has finished
+    for (auto &e : launched)
+      if (hipEventQuery(e.second) == hipErrorNotReady) return false;
+    return true;
+  }
+  void release() {
+    for (auto &e : launched) {
+      (void)hipEventSynchronize(e.second);
+      (void)hipEventDestroy(e.second);
+    }
+    launched.clear();
+    if (d_tmpl) (void)hipFree(d_tmpl);
+    if (d_size) (void)hipFree(d_size);
+    d_tmpl = nullptr;
+    d_size = nullptr;
+  }
+};
+
 struct bg_rewrite {
   std::vector<uint8_t> tmpl;    // n x kRwMaxSize, zero past each size
   std::vector<uint16_t> size;
   uint64_t next = 0;            // next_turn_
   bool dirty = true;
-  bool uploaded = false;        // d_tmpl holds templates a kernel may read
-  int device = -1;
-  uint8_t *d_tmpl = nullptr;    // kRwMaxTemplates x kRwMaxSize
-  uint16_t *d_size = nullptr;
+  RwGen cur;                    // the templates launches read now
+  std::vector<RwGen> retired;   // older copies, launches maybe still queued
   std::mutex mu;
   ~bg_rewrite() {
-    if (d_tmpl) (void)hipFree(d_tmpl);
-    if (d_size) (void)hipFree(d_size);
+    cur.release();
+    for (auto &g : retired) g.release();
   }
 };
 
 namespace {
 
+// the current templates on `device`, uploaded on `s` (which later launches
+// on `s` follow; other streams: the upload is synchronized)
 int sync_templates(bg_rewrite *h, int device, hipStream_t s) {
-  if (h->device != device) {
-    if (h->d_tmpl) (void)hipFree(h->d_tmpl);
-    if (h->d_size) (void)hipFree(h->d_size);
-    h->d_tmpl = nullptr;
-    h->d_size = nullptr;
-    h->device = device;
-    h->dirty = true;
-    h->uploaded = false;
+  if (!h->dirty && h->cur.device == device && h->cur.d_tmpl) return 0;
+  if (h->size.empty()) {
+    h->dirty = false;
+    return 0;
   }
-  if (!h->d_tmpl) {
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_tmpl),
-                      (size_t)kRwMaxTemplates * kRwMaxSize));
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->d_size), kRwMaxTemplates * 2));
+  // free the retired copies whose launches have all finished
+  for (size_t i = 0; i < h->retired.size();) {
+    if (h->retired[i].done()) {
+      h->retired[i].release();
+      h->retired.erase(h->retired.begin() + i);
+    } else {
+      i++;
+    }
   }
-  if (h->dirty && !h->size.empty()) {
-    // a rewrite launched earlier, on any stream, may still read the old
-    // templates: they are overwritten only once the device is idle (template
-    // changes are THREAD_UNSAFE commands, made with the workers paused, so
-    // this waits for queued batches only)
-    if (h->uploaded) HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyAsync(h->d_tmpl, h->tmpl.data(), h->tmpl.size(),
-                           hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(h->d_size, h->size.data(), h->size.size() * 2,
-                           hipMemcpyHostToDevice, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    h->uploaded = true;
+  if (h->cur.d_tmpl) {
+    if (h->cur.launched.empty()) {
+      h->cur.release();  // never launched against: reuse nothing, free now
+    } else {
+      h->retired.push_back(std::move(h->cur));
+      h->cur = RwGen();
+    }
   }
+  RwGen g;
+  g.device = device;
+  if (hipMalloc(reinterpret_cast<void **>(&g.d_tmpl), (size_t)kRwMaxTemplates * kRwMaxSize) !=
+          hipSuccess ||
+      hipMalloc(reinterpret_cast<void **>(&g.d_size), kRwMaxTemplates * 2) != hipSuccess) {
+    g.release();
+    return fail(ENOMEM, "no device memory for the templates");
+  }
+  if (hipMemcpyAsync(g.d_tmpl, h->tmpl.data(), h->tmpl.size(), hipMemcpyHostToDevice, s) !=
+          hipSuccess ||
+      hipMemcpyAsync(g.d_size, h->size.data(), h->size.size() * 2, hipMemcpyHostToDevice, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    g.release();
+    return fail(EIO, "template upload failed");
+  }
+  h->cur = std::move(g);
   h->dirty = false;
+  return 0;
+}
+
+// an event behind this launch on `s` (re-recorded per launch: the stream's
+// last launch against the current templates)
+int note_launch(bg_rewrite *h, hipStream_t s) {
+  for (auto &e : h->cur.launched)
+    if (e.first == s) {
+      HIP_TRY(hipEventRecord(e.second, s));
+      return 0;
+    }
+  hipEvent_t ev;
+  HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  if (hipEventRecord(ev, s) != hipSuccess) {
+    (void)hipEventDestroy(ev);
+    return fail(EIO, "hipEventRecord failed");
+  }
+  h->cur.launched.emplace_back(s, ev);
   return 0;
 }
 
@@ -183,8 +244,8 @@ int bg_rewrite_process(bg_rewrite *h, int device, void *d_slots, size_t stride,
   a.slots = static_cast<uint8_t *>(d_slots);
   a.stride = stride;
   a.n = n;
-  a.tmpl = h->d_tmpl;
-  a.tsize = h->d_size;
+  a.tmpl = h->cur.d_tmpl;
+  a.tsize = h->cur.d_size;
   a.ntempl = nt;
   a.start = nt == 1 ? 0u : (uint32_t)h->next;  // DoRewriteSingle keeps turn 0
   a.headroom = headroom;
@@ -195,6 +256,7 @@ int bg_rewrite_process(bg_rewrite *h, int device, void *d_slots, size_t stride,
   a.head = d_head;
   a.len = d_len;
   HIP_TRY(launch_rewrite(a, num_cus(device), s));
+  if ((r = note_launch(h, s))) return r;
   if (nt > 1) h->next = (h->next + n) % nt;  // consecutive batches' turns
   return 0;
 }

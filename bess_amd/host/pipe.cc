@@ -418,8 +418,10 @@ int bg_pipe_create(bg_module *m, int device, size_t batch, int depth,
   }
   p->ctx_use = m->m->CtxUse();
   // a writeback module with a by-pointer datapath takes packets that lie in
-  // host-registered memory in place (Module::ProcessDevicePtrs asked with n 0)
-  p->zc = p->writeback && !p->meta &&
+  // host-registered memory in place (Module::ProcessDevicePtrs asked with n
+  // 0); its kernel reads each frame from the pointer on, so only a window
+  // that starts at the head (lo 0: the checksum modules) goes in place
+  p->zc = p->writeback && !p->meta && p->lo == 0 &&
           m->m->ProcessDevicePtrs(ResolveCtx(nullptr, device), nullptr,
                                   (size_t)(p->hi - p->lo), 0, nullptr, nullptr) == 0;
   // a ring ticket is served by one workgroup: past a few thousand packets
@@ -606,9 +608,12 @@ static int submit(bg_pipe *p, const bg_ctx *ctx, uint8_t *const *heads,
         }
       } else {
         // a packet in host-registered memory goes in place (its head's
-        // device address); a slot holds packets of one kind
+        // device address) when its head is 16-byte aligned, as the kernel's
+        // 16-byte frame loads are (a head moved by prepend / adj goes
+        // staged); a slot holds packets of one kind
         uint64_t dev = 0;
-        const bool zc = p->zc && bg::host_dev_addr(heads[k], span, &dev);
+        const bool zc = p->zc && ((uintptr_t)heads[k] & 15) == 0 &&
+                        bg::host_dev_addr(heads[k], span, &dev);
         if (s.n + j == 0)
           s.zc = zc;
         else if (zc != s.zc)

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-6 GPU call: `gpurun -- bash scripts/gpu_r06.sh OUTDIR [steps]`
+# steps (comma list): wide (the full-width WildcardMatch tests), tests (the
+# whole -m gpu suite), smoke, bench (default bench line), prof (kernel
+# trace of the bench per leg). Stops at the first step that ends in
+# anything but success / test failure.
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT="$GRAFT_REPO_ROOT/gpurun_out/$1"
+STEPS=${2:-wide,tests,smoke}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >> "$OUT/steps.log"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "== $name rc=$rc" >> "$OUT/steps.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name rc=$rc" >> "$OUT/steps.log"; exit $rc; fi
+  return 0
+}
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+if has wide; then
+  step wide 600 python -u -m pytest tests/test_gpu_wm_wide.py -m gpu -v -rf --timeout 300 --timeout-method thread
+fi
+if has tests; then
+  step tests 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
+fi
+if has smoke; then
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if has bench; then
+  step bench 900 python bench.py
+fi
+echo done >> "$OUT/steps.log"

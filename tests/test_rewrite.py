@@ -131,3 +131,54 @@ def test_gpu_host_packets_and_clear():
         else:
             for i in range(n):
                 assert (buf[i, 128:128 + ln[i]] == ref[i, 128:128 + ln[i]]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_template_change_waits_only_for_its_own_launches():
+    """A template change while a batch launched on another stream is still
+    queued (behind ~0.5 s of other work there): the next call uploads a new
+    copy of the templates and returns without waiting for that stream or the
+    device (round 5 synchronized the whole device here, so a Rewrite worker
+    stalled behind every other pipe's persistent kernel -- ADVICE r05); the
+    queued batch still reads the templates it was launched with."""
+    import time
+    import torch
+    ts, ts2 = templates(3, 81, 0, 300), templates(2, 82, 0, 300)
+    m, o = Rewrite(templates=ts), OM.OracleRewrite(ts)
+    n, stride = 2000, 512
+    s1, s2 = slab(n, stride, 1), slab(n, stride, 2)
+    d1 = torch.from_numpy(s1.reshape(-1).copy()).cuda()
+    d2 = torch.from_numpy(s2.reshape(-1).copy()).cuda()
+    h1 = torch.zeros(n, dtype=torch.int16, device="cuda")
+    l1 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    h2 = torch.zeros(n, dtype=torch.int16, device="cuda")
+    l2 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    busy, other = torch.cuda.Stream(), torch.cuda.Stream()
+    # the first call uploads the templates (synchronously, on its stream)
+    w = slab(5, stride, 3)
+    dw = torch.from_numpy(w.reshape(-1).copy()).cuda()
+    hw = torch.zeros(5, dtype=torch.int16, device="cuda")
+    lw = torch.zeros(5, dtype=torch.int32, device="cuda")
+    m.process_device(dw, stride, 5, hw, lw, stream=other)
+    o.process(w, stride, 5, np.zeros(5, np.uint16), np.zeros(5, np.uint32))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(busy):
+        torch.cuda._sleep(int(1e9))  # ~0.5 s of device work on `busy`
+    m.process_device(d1, stride, n, h1, l1, stream=busy)  # queued behind it
+    m.add(templates=ts2)
+    t0 = time.perf_counter()
+    m.process_device(d2, stride, n, h2, l2, stream=other)
+    other.synchronize()
+    dt = time.perf_counter() - t0
+    still_busy = not busy.query()
+    torch.cuda.synchronize()
+    assert still_busy and dt < 0.25, dt
+    for d, h, ln, s in ((d1, h1, l1, s1), (d2, h2, l2, s2)):
+        oh = np.zeros(n, np.uint16)
+        ol = np.zeros(n, np.uint32)
+        o.process(s, stride, n, oh, ol)
+        assert (h.cpu().numpy().view(np.uint16) == oh).all()
+        assert (ln.cpu().numpy().view(np.uint32) == ol).all()
+        assert (d.cpu().numpy().reshape(n, stride) == s).all()
+        if s is s1:
+            o.add(ts2)
