@@ -45,6 +45,20 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
 EM_BYTES_PER_PKT = 66  # 64 B header line read + 2 B gate written
 CK_BYTES_PER_PKT = 1502  # 1496 B frame read + IP csum + L4 csum + gate (2 B each)
+PCIE_GBS = 63.0  # host link, PCIe Gen5 x16 per direction (MI355X_MICROARCH.md, spec)
+
+
+def pcie(mpps, h2d, d2h):
+    """A host-memory leg against its link: bytes per packet each way (the
+    staged window or the in-place frame reads host -> device, gates and
+    written-back lines device -> host), their GB/s at `mpps`, and the busier
+    direction's fraction of the spec rate (the host legs' bound)"""
+    if not isinstance(mpps, (int, float)):
+        return None
+    gh, gd = mpps * 1e6 * h2d / 1e9, mpps * 1e6 * d2h / 1e9
+    return {"h2d_bytes_per_pkt": h2d, "d2h_bytes_per_pkt": d2h,
+            "h2d_GBps": round(gh, 2), "d2h_GBps": round(gd, 2),
+            "pcie_frac": round(max(gh, gd) / PCIE_GBS, 4)}
 
 
 def log(*a):
@@ -488,7 +502,7 @@ def run_em1500(args, dev, torch):
     want = np.zeros(ns, np.uint16)
     L.or_em_process(em, sample.ctypes.data, 64, ns, 8192, want.ctypes.data)
     parity = bool((dg[:ns].cpu().numpy().view(np.uint16) == want).all())
-    ms = _time_steps(lambda: t.classify(d, 2048, n, 8192, dg), args, torch,
+    ms = _time_steps(lambda: t.classify(d, 2048, n, 8192, dg), args, torch, reps=leg_steps(args),
                      settle_with_step=True)
     out = {"workload": "1500B pkts (1496B frames, 2048B slots), %d-rule 5-tuple "
                        "ExactMatch, %d resident pkts" % (args.rules, n),
@@ -675,6 +689,8 @@ def run_e2e_pipe(args, torch):
                     lambda: Pipe(m, batch=batch, depth=depth), heads, None, th,
                     reps=2 if th == 1 else 4)
         em["Mpps_by_threads_" + key] = rates
+        # the staged 16 B field window in, the 2 B gate out
+        em["pcie_16_threads_" + key] = pcie(rates.get("16"), 16, 2)
     out["ExactMatch_64B"] = em
     del snb
     # WildcardMatch, C4 rules (100 K over 8 masks), IMIX frames: the heavier
@@ -705,6 +721,7 @@ def run_e2e_pipe(args, torch):
         rates[str(th)] = _pipe_rate(lambda: Pipe(mw, batch=65536, depth=4), heads,
                                     None, th, reps=4)
     wmr["Mpps_by_threads_batch65536"] = rates
+    wmr["pcie_16_threads"] = pcie(rates.get("16"), 16, 2)
     out["WildcardMatch_IMIX_100K"] = wmr
     del snb
     # L4Checksum (recompute), 1500 B packets: frames H2D, header lines back
@@ -728,7 +745,7 @@ def run_e2e_pipe(args, torch):
             lambda: Pipe(mk, batch=8192, depth=4, span=1504), heads, lens, th,
             reps=4)
     ck["Mpps_by_threads_batch8192"] = rates
-    ck["bytes_per_pkt_pcie"] = {"h2d": 1504, "d2h": 130}
+    ck["pcie_16_threads"] = pcie(rates.get("16"), 1504, 130)
     out["L4Checksum_1500B"] = ck
     return out
 
@@ -819,6 +836,7 @@ def run_plugin_pipeline(args):
             "pipe": {"mode": "ring (bg_em_ring, one lane per worker)",
                      "batch": 1024, "depth": 8},
             "parity": parity,
+            "pcie_16_workers": pcie(res.get("16"), 16, 2),
             "cpu_same_harness": {
                 "what": "the same Source -> Sink workers with the restated "
                         "reference ExactMatch::ProcessBatch (oracle: head_data() "
@@ -912,21 +930,30 @@ def run_plugin_pool(args):
                          "never_emitted_per_pass": exp.count("-"),
                          "source_waits": int(pools[-1][3])}
             # worker 0's pipe counters and TSC cycles per packet of the timed
-            # GPU pass (where the host side's time goes)
+            # passes (where the host side's time goes), the plugin's and the
+            # restated reference's side by side
             st = [x for x in lines if x.startswith("stats")]
             cyc = [x for x in lines if x.startswith("cycles")]
-            diag = {}
-            if len(st) >= 2:
-                diag["pipe_w0"] = st[1][6:]
-            if len(cyc) >= 2:
-                diag["cycles_w0_gpu"] = cyc[1][7:]
-            if len(cyc) >= 4:
-                diag["cycles_w0_cpu"] = cyc[3][7:]
-            if args.diag:
-                log("e2e_plugin_pool %s %s" % (name, json.dumps(diag)))
+            if args.diag and len(st) >= 2:
+                log("e2e_plugin_pool %s pipe_w0 %s" % (name, st[1][6:]))
             if len(st) >= 2:  # the submit cost per packet (the copy it saves)
                 f = st[1].split()
                 out[name]["submit_cyc_per_pkt"] = float(f[f.index("submit_cyc_per_pkt") + 1])
+                out[name]["poll_cyc_per_pkt"] = float(f[f.index("poll_cyc_per_pkt") + 1])
+
+            def phases(line):
+                f = line.split()
+                return {k: float(f[f.index(k) + 1]) for k in
+                        ("source", "proc", "sink", "task") if k in f}
+            if len(cyc) >= 4:
+                out[name]["w0_cycles_per_pkt"] = {
+                    "plugin": phases(cyc[1]), "reference": phases(cyc[3]),
+                    "tsc_ghz": float(cyc[1].split()[-1])}
+            # the frames read in place from the registered pool (L4Checksum:
+            # 1504 B of 16 B loads per 1496 B frame, the checksum word and
+            # gate back) or the staged 16 B field window (WildcardMatch)
+            out[name]["pcie"] = pcie(out[name]["Mpps"], *((16, 2) if name == "WildcardMatch"
+                                                          else (1504, 4)))
             if name == "WildcardMatch":
                 out[name]["rules"] = nr
             if len(stats) >= 4 and len(outs) >= 4:
@@ -972,16 +999,15 @@ def leg_steps(args):
     return max(args.steps, 100)
 
 
-def _time_steps(step, args, torch, settle_with_step=False):
-    """warmup, then ms per launch over args.steps launches (HIP events on
-    the launching stream); settle_with_step: the step leaves its input as
-    it was, so clock_settle runs it"""
+def _time_steps(step, args, torch, settle_with_step=False, reps=10):
+    """warmup, then ms per launch over `reps` launches (HIP events on the
+    launching stream); settle_with_step: the step leaves its input as it
+    was, so clock_settle runs it"""
     clock_settle(args, torch, step if settle_with_step else None)
     for _ in range(max(3, args.warmup // 4)):
         step()
     torch.cuda.synchronize()
     timer = Timer(torch)
-    reps = 10
     timer.start()
     for _ in range(reps):
         step()

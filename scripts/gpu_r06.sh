@@ -3,7 +3,8 @@
 # steps (comma list): wide (the full-width WildcardMatch tests), tests (the
 # whole -m gpu suite), smoke, bench (default bench line), prof (kernel
 # trace of the bench per leg). Stops at the first step that ends in
-# anything but success / test failure.
+# anything but success / test failure. sel: the tests named in $SEL;
+# prof: scripts/prof_legs.py over $LEGS (default: every leg).
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT="$GRAFT_REPO_ROOT/gpurun_out/$1"
 STEPS=${2:-wide,tests,smoke}
@@ -22,11 +23,18 @@ has() { [[ ",$STEPS," == *",$1,"* ]]; }
 if has wide; then
   step wide 600 python -u -m pytest tests/test_gpu_wm_wide.py -m gpu -v -rf --timeout 300 --timeout-method thread
 fi
+if has sel; then  # SEL: test files / node ids
+  step sel 600 python -u -m pytest $SEL -m gpu -v -rf --timeout 300 --timeout-method thread
+fi
 if has tests; then
   step tests 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
 fi
 if has smoke; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if has prof; then  # a kernel trace per bench leg (scripts/prof_legs.py)
+  step prof 1000 python scripts/prof_legs.py run "$OUT/legs" $LEGS
+  python scripts/prof_legs.py summary "$OUT/legs" > "$OUT/kernels_by_leg.md" 2>&1 || true
 fi
 if has bench; then
   step bench 900 python bench.py

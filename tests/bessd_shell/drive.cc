@@ -415,7 +415,7 @@ static int run() {
       std::atomic<int> started{0}, finished{0};
       std::atomic<bool> go{false};
       std::vector<uint64_t> sunk(nw, 0);
-      uint64_t tsc[3] = {0, 0, 0};
+      uint64_t tsc[4] = {0, 0, 0, 0};
       double t0 = 0, t1 = 0;
       const uint64_t tsc0 = __rdtsc();
       auto worker = [&](int w) {
@@ -442,11 +442,12 @@ static int run() {
         while (!go.load()) {
         }
         uint64_t nb = 0;
-        uint64_t c_proc = 0, c_sink = 0, c_task = 0;  // TSC cycles per phase
+        uint64_t c_src = 0, c_proc = 0, c_sink = 0, c_task = 0;  // TSC cycles per phase
         for (int r = 0; r < reps; r++)
           for (size_t b0 = lo; b0 < hi; b0 += bess::PacketBatch::kMaxBurst) {
             bess::PacketBatch batch;  // the Source's batch
             const size_t cnt = std::min(hi - b0, (size_t)bess::PacketBatch::kMaxBurst);
+            const uint64_t cs = __rdtsc();
             if (ppool) {
               // packets from the pool, each filled with its frame (Source
               // copies its template the same way); an empty pool: wait
@@ -473,6 +474,7 @@ static int run() {
                 batch.add(reinterpret_cast<bess::Packet *>(pool + i * kObj));
             }
             const uint64_t c0 = __rdtsc();
+            c_src += c0 - cs;
             if (cpu) {  // ExactMatch::ProcessBatch restated (exact_match.cc:224-244)
                         // or WildcardMatch's (cpu_wm), L4Checksum's (cpu_l4)
               uint8_t *heads[bess::PacketBatch::kMaxBurst];
@@ -517,6 +519,7 @@ static int run() {
           tsc[0] = c_proc;
           tsc[1] = c_sink;
           tsc[2] = c_task;
+          tsc[3] = c_src;
         }
       };
       std::vector<std::thread> th;
@@ -529,11 +532,12 @@ static int run() {
       const double dt = t1 - t0;
       const double pk = (double)n * reps;
       printf("pipeline %.3f %.6f %.0f\n", pk / dt / 1e6, dt, pk);
-      // worker 0's cycles per packet of its own: ProcessBatch, Sink, task
+      // worker 0's cycles per packet of its own: ProcessBatch, Sink, task,
+      // and the Source's allocation and frame copy (pool runs)
       const double ghz = (double)(__rdtsc() - tsc0) / (now_s() - t0 + 1e-12) / 1e9;
       const double p0 = pk / nw;
-      printf("cycles w0 proc %.1f sink %.1f task %.1f per_pkt tsc_ghz %.2f\n",
-             tsc[0] / p0, tsc[1] / p0, tsc[2] / p0, ghz);
+      printf("cycles w0 proc %.1f sink %.1f task %.1f source %.1f per_pkt tsc_ghz %.2f\n",
+             tsc[0] / p0, tsc[1] / p0, tsc[2] / p0, tsc[3] / p0, ghz);
       printf("out");
       for (size_t i = 0; i < n; i++) {
         if (verify)
