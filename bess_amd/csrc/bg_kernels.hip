@@ -441,10 +441,9 @@ __device__ __forceinline__ void ring_barrier() {
 // never wait for those stores, so no claim or frame load of the next run
 // waits behind the writes' trip to the host. Its barriers pair one to one
 // with em_ring_kernel's.
-__device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldone,
-                                            const uint64_t *sh_t, const uint32_t *sh_k,
-                                            const uint32_t *sh_rel, uint32_t lane) {
-  (void)lane;
+__device__ __forceinline__ void ring_done_wave(const RingArgs &a, const uint64_t *sh_t,
+                                            const uint32_t *sh_k, const uint32_t *sh_rel,
+                                            const uint32_t *sh_lane) {
   const uint32_t wl = threadIdx.x & 63;
   for (;;) {
     ring_barrier();  // B1: the run is in sh_*
@@ -452,6 +451,7 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldon
     if (!k) return;
     const uint64_t t = *sh_t + wl;
     const bool release = *sh_rel != 0;
+    uint32_t *ldone = a.done + (size_t)*sh_lane * a.nslots;  // the run's lane
     ring_barrier();  // B2: the gates are stored (sh_* free for the next run)
     // every wave's gate stores (system-scope write-through stores,
     // completed by each wave's vmcnt(0) before B2) reach the host before
@@ -464,9 +464,13 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldon
   }
 }
 
-// Workgroup b >= 1 serves submission lane (b - 1) % nlanes. Its first wave
-// claims a range of the lane's next tickets (one atomic; claims run ahead of
-// publication, so the lane's workgroups queue up on its coming tickets),
+// Workgroup b >= 1 has home lane (b - 1) % nlanes. Its first wave claims a
+// range of a lane's next tickets (one atomic; claims run ahead of
+// publication, so a lane's workgroups queue up on its coming tickets): the
+// home lane's, unless the home lane has no published ticket left unclaimed
+// while another lane has -- then that lane's (lanes are shared: a lane whose
+// submitter runs ahead, or the last lane of a pass, is served by every idle
+// workgroup instead of its 1/nlanes of the grid),
 // waits until the range's next ticket is published and takes every ticket
 // of the range published by then as one run (<= kRingRunMax tickets: a
 // 32-packet batch alone would leave 7/8 of the workgroup's lanes idle),
@@ -488,16 +492,15 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
   __shared__ uint64_t sh_w[kRingRunMax][4];
   __shared__ uint32_t sh_pre[kRingRunMax + 1];  // the run's packet prefix sums
   __shared__ uint64_t sh_t;
-  __shared__ uint32_t sh_k, sh_rel;
-  const uint32_t lane = (blockIdx.x - 1) % a.nlanes;
-  unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
+  __shared__ uint32_t sh_k, sh_rel, sh_lane;
+  const uint32_t home = (blockIdx.x - 1) % a.nlanes;
   const unsigned long long *dstop = a.dev + (size_t)a.nlanes * kRingLaneWords;
-  const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * kRingDescWords;
-  uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   if (threadIdx.x >= kRingBlock) {  // wave-uniform
-    ring_done_wave(a, ldone, &sh_t, &sh_k, &sh_rel, lane);
+    ring_done_wave(a, &sh_t, &sh_k, &sh_rel, &sh_lane);
     return;
   }
+  uint32_t lane = home;  // the lane of the current claim (wave 0, uniform)
+  unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
   const uint64_t mask48 = (1ull << 48) - 1;
   constexpr int kPpl = PPL;  // packets per lane per round, loads in flight
   const uint32_t wl = threadIdx.x & 63;
@@ -507,6 +510,22 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
   for (;;) {
     if (threadIdx.x < 64) {  // wave 0
       if (next == end) {
+        // the lane to claim on: wave lane j looks at lane (home + j) %
+        // nlanes; the first with a published ticket nobody claimed yet (the
+        // home lane first), else the home lane (a claim ahead)
+        uint32_t pick = home;
+        if (a.nlanes > 1) {
+          const uint32_t cand = (home + wl) % a.nlanes;
+          bool open = false;
+          if (wl < a.nlanes) {
+            const unsigned long long *dc = a.dev + (size_t)cand * kRingLaneWords;
+            open = ld_agent(dc) < ld_agent(dc + 1);
+          }
+          const uint64_t m = __ballot(open);
+          if (m) pick = (home + (uint32_t)__builtin_ctzll(m)) % a.nlanes;
+        }
+        lane = pick;
+        dl = a.dev + (size_t)lane * kRingLaneWords;
         uint64_t t = 0;
         if (wl == 0) t = atomicAdd(dl, (unsigned long long)claim);
         next = __shfl(t, 0);
@@ -532,7 +551,8 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
       uint64_t w[4] = {0, 0, 0, 0};
       if (wl < k) {
         const uint64_t tag = (t + 1) & 0xFFFF;
-        const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
+        const uint64_t *d =
+            a.desc + ((size_t)lane * a.nslots + t % a.nslots) * kRingDescWords;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
       // acquire: the batches' frames were written (by the host or a copy)
@@ -564,6 +584,7 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         sh_t = next;
         sh_k = k;
         sh_rel = rel ? 1u : 0u;
+        sh_lane = lane;
       }
       next += k;
       // the next claim: about kRingRunPackets packets of this lane's batches

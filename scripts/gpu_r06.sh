@@ -36,6 +36,12 @@ if has prof; then  # a kernel trace per bench leg (scripts/prof_legs.py)
   step prof 1000 python scripts/prof_legs.py run "$OUT/legs" $LEGS
   python scripts/prof_legs.py summary "$OUT/legs" > "$OUT/kernels_by_leg.md" 2>&1 || true
 fi
+if has sweep; then  # the C2 batch sweep alone (ring rows)
+  step sweep 600 python bench.py --only sweep --no-cpu
+fi
+if has placement; then  # C4's 2 KB-slot time over separately placed slabs
+  step placement 600 python scripts/slab_placement.py "$OUT/placement.json"
+fi
 if has bench; then
   step bench 900 python bench.py
 fi

@@ -120,7 +120,7 @@ def summary(out):
         rows = []
         with open(traces[0]) as f:
             for r in csv.DictReader(f):
-                if pat not in r["Kernel_Name"]:
+                if pat not in short_name(r["Kernel_Name"]):
                     continue
                 blocks = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
                 d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3

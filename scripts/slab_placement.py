@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Does C4's 2 KB-slot time depend on where its 16 GB slab lies? (DESIGN §8
+open item 7)
+
+    python scripts/slab_placement.py OUT.json
+
+One process: the C4 rule set (100 K WildcardMatch rules over 8 masks) and
+8 M IMIX frames in 2 KB slots, timed (the run-time compiled kernel, 100
+launches after a settle, HIP events) over
+  * slab A: the bench's allocation (torch.repeat of the 1 M frames, 16 GB);
+  * slab B: a second 16 GB allocation holding the same bytes;
+  * slab A again (the first measurement's repeatability);
+  * slab C: one 16 GB + 4 KB allocation, the frames copied to byte offsets
+    0, 256, 512, 1024 and 2048 inside it (the windows' address bits below
+    and at the slot size move; the physical pages do not).
+Each entry records the slab's device address modulo 2 MB and 1 GB."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bess_amd import flowtable as F  # noqa: E402
+from bess_amd import packets as P  # noqa: E402
+
+
+def main():
+    out_path = sys.argv[1]
+    n0, rep = 1 << 20, 8
+    n = n0 * rep
+    rk, rm, prio, gates, frames, _ = P.wm_workload(100000, n0, stride=2048)
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    t.jit_wait()
+    dg = torch.empty(n, dtype=torch.int16, device="cuda")
+    ref = None
+
+    def timed(slab, k=100):
+        t.classify(slab, 2048, n, 8192, dg)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.1:  # settle (as bench.py clock_settle)
+            for _ in range(8):
+                t.classify(slab, 2048, n, 8192, dg)
+            torch.cuda.synchronize()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(k):
+            t.classify(slab, 2048, n, 8192, dg)
+        b.record()
+        b.synchronize()
+        return a.elapsed_time(b) / k
+
+    def entry(name, slab):
+        nonlocal ref
+        ms = timed(slab)
+        g = dg.cpu().numpy()
+        if ref is None:
+            ref = g.copy()
+        p = slab.data_ptr()
+        e = {"slab": name, "ms": round(ms, 4), "addr_mod_2MB": p % (2 << 20),
+             "addr_mod_1GB": p % (1 << 30), "same_gates": bool((g == ref).all())}
+        print(json.dumps(e), flush=True)
+        return e
+
+    res = []
+    d0 = torch.from_numpy(frames.reshape(-1)).cuda()
+    A = d0.repeat(rep)
+    del d0
+    res.append(entry("A (bench allocation)", A))
+    B = torch.empty_like(A)
+    B.copy_(A)
+    res.append(entry("B (second 16 GB allocation)", B))
+    res.append(entry("A again", A))
+    del B
+    torch.cuda.empty_cache()
+    size = A.numel()
+    C = torch.empty(size + 4096, dtype=torch.uint8, device="cuda")
+    for off in (0, 256, 512, 1024, 2048):
+        v = C[off:off + size]
+        v.copy_(A)
+        res.append(entry("C + %d" % off, v))
+    with open(out_path, "w") as f:
+        json.dump({"what": __doc__.strip().splitlines()[0], "pkts": n, "results": res}, f,
+                  indent=1)
+
+
+if __name__ == "__main__":
+    main()
