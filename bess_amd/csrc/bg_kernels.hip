@@ -533,16 +533,31 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
       }
       uint64_t p = 0;
       if (wl == 0) {
+        // Every waiting workgroup polls here, all on the few lines of the
+        // lanes' counters: polls back off (s_sleep 2 -> 32, ~0.1 -> 0.9 us)
+        // so that waiting does not crowd those lines -- the claim atomics
+        // and the dispatcher's mirror stores go to the same ones -- and the
+        // stop word is read relaxed (an acquire per poll invalidated the
+        // caches every iteration); the acquire follows only once it is set.
+        uint32_t nap = 0;
         for (;;) {
           p = ld_agent(dl + 1);
           if (p > next) break;
           // stopping (the dispatcher's mirrors precede its stop word):
           // published meanwhile?
-          if (__hip_atomic_load(dstop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+          if (__hip_atomic_load(dstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             p = ld_agent(dl + 1);
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
+          if (nap < 4) {
+            __builtin_amdgcn_s_sleep(2);
+          } else if (nap < 8) {
+            __builtin_amdgcn_s_sleep(8);
+          } else {
+            __builtin_amdgcn_s_sleep(32);
+          }
+          nap++;
         }
       }
       p = __shfl(p, 0);

@@ -42,6 +42,17 @@ fi
 if has placement; then  # C4's 2 KB-slot time over separately placed slabs
   step placement 600 python scripts/slab_placement.py "$OUT/placement.json"
 fi
+if has ringab; then  # the sweep's ring rows: product vs $RINGLIBS, interleaved
+  for rep in 1 2; do
+    for L in product $RINGLIBS; do
+      if [ "$L" = product ]; then LA=""; else LA="--lib scripts/bin/libbessgpu_$L.so"; fi
+      step "sweep_${L}_$rep" 600 python bench.py --only sweep --no-cpu $LA
+    done
+  done
+fi
+if has scatter; then  # scripts/scatter_probe.hip, every variant
+  step scatter 600 scripts/bin/scatter_probe 16
+fi
 if has bench; then
   step bench 900 python bench.py
 fi

@@ -8,16 +8,20 @@ One process: the C4 rule set (100 K WildcardMatch rules over 8 masks) and
 8 M IMIX frames in 2 KB slots, timed (the run-time compiled kernel, 100
 launches after a settle, HIP events) over
   * slab A: the bench's allocation (torch.repeat of the 1 M frames, 16 GB);
-  * slab B: a second 16 GB allocation holding the same bytes;
+  * D / E: hipExtMallocWithFlags with hipDeviceMallocContiguous / 0;
+  * slab B: a second torch allocation holding the same bytes;
   * slab A again (the first measurement's repeatability);
+  * A2: a torch allocation made after A was freed;
   * slab C: one 16 GB + 4 KB allocation, the frames copied to byte offsets
-    0, 256, 512, 1024 and 2048 inside it (the windows' address bits below
-    and at the slot size move; the physical pages do not).
+    0 and 1024 inside it (the windows' address bits below and at the slot
+    size move; the physical pages do not).
 Each entry records the slab's device address modulo 2 MB and 1 GB."""
 import json
 import os
 import sys
 import time
+
+import ctypes as C
 
 import numpy as np
 import torch
@@ -27,6 +31,15 @@ sys.path.insert(0, ROOT)
 
 from bess_amd import flowtable as F  # noqa: E402
 from bess_amd import packets as P  # noqa: E402
+
+
+class Raw:
+    """a device address where the bess_amd wrappers take a tensor"""
+    def __init__(self, p):
+        self.p = p
+
+    def data_ptr(self):
+        return self.p
 
 
 def main():
@@ -74,18 +87,38 @@ def main():
     d0 = torch.from_numpy(frames.reshape(-1)).cuda()
     A = d0.repeat(rep)
     del d0
+    size = A.numel()
     res.append(entry("A (bench allocation)", A))
+    # hipExtMallocWithFlags: physically contiguous (best effort), and plain
+    hip = C.CDLL("libamdhip64.so")
+    raw = []
+    for name, flags in (("D (hipDeviceMallocContiguous)", 4), ("E (hipExtMallocWithFlags 0)", 0)):
+        p = C.c_void_p()
+        rc = hip.hipExtMallocWithFlags(C.byref(p), C.c_size_t(size), C.c_uint(flags))
+        if rc:
+            res.append({"slab": name, "error": rc})
+            continue
+        raw.append(p)
+        assert hip.hipMemcpy(p, C.c_void_p(A.data_ptr()), C.c_size_t(size), 3) == 0
+        res.append(entry(name, Raw(p.value)))
     B = torch.empty_like(A)
     B.copy_(A)
-    res.append(entry("B (second 16 GB allocation)", B))
+    res.append(entry("B (second torch allocation)", B))
     res.append(entry("A again", A))
-    del B
+    # A's memory handed back and taken again
+    del A
     torch.cuda.empty_cache()
-    size = A.numel()
-    C = torch.empty(size + 4096, dtype=torch.uint8, device="cuda")
-    for off in (0, 256, 512, 1024, 2048):
-        v = C[off:off + size]
-        v.copy_(A)
+    A2 = torch.empty_like(B)
+    A2.copy_(B)
+    res.append(entry("A2 (after A was freed)", A2))
+    del A2
+    for p in raw:
+        hip.hipFree(p)
+    torch.cuda.empty_cache()
+    Cs = torch.empty(size + 4096, dtype=torch.uint8, device="cuda")
+    for off in (0, 1024):
+        v = Cs[off:off + size]
+        v.copy_(B)
         res.append(entry("C + %d" % off, v))
     with open(out_path, "w") as f:
         json.dump({"what": __doc__.strip().splitlines()[0], "pkts": n, "results": res}, f,
