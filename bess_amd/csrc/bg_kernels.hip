@@ -441,9 +441,9 @@ __device__ __forceinline__ void ring_barrier() {
 // never wait for those stores, so no claim or frame load of the next run
 // waits behind the writes' trip to the host. Its barriers pair one to one
 // with em_ring_kernel's.
-__device__ __forceinline__ void ring_done_wave(const RingArgs &a, const uint64_t *sh_t,
-                                            const uint32_t *sh_k, const uint32_t *sh_rel,
-                                            const uint32_t *sh_lane) {
+__device__ __forceinline__ void ring_done_wave(const RingArgs &a, uint32_t *ldone,
+                                            const uint64_t *sh_t, const uint32_t *sh_k,
+                                            const uint32_t *sh_rel) {
   const uint32_t wl = threadIdx.x & 63;
   for (;;) {
     ring_barrier();  // B1: the run is in sh_*
@@ -451,7 +451,6 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, const uint64_t
     if (!k) return;
     const uint64_t t = *sh_t + wl;
     const bool release = *sh_rel != 0;
-    uint32_t *ldone = a.done + (size_t)*sh_lane * a.nslots;  // the run's lane
     ring_barrier();  // B2: the gates are stored (sh_* free for the next run)
     // every wave's gate stores (system-scope write-through stores,
     // completed by each wave's vmcnt(0) before B2) reach the host before
@@ -464,13 +463,9 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, const uint64_t
   }
 }
 
-// Workgroup b >= 1 has home lane (b - 1) % nlanes. Its first wave claims a
-// range of a lane's next tickets (one atomic; claims run ahead of
-// publication, so a lane's workgroups queue up on its coming tickets): the
-// home lane's, unless the home lane has no published ticket left unclaimed
-// while another lane has -- then that lane's (lanes are shared: a lane whose
-// submitter runs ahead, or the last lane of a pass, is served by every idle
-// workgroup instead of its 1/nlanes of the grid),
+// Workgroup b >= 1 serves submission lane (b - 1) % nlanes. Its first wave
+// claims a range of the lane's next tickets (one atomic; claims run ahead of
+// publication, so the lane's workgroups queue up on its coming tickets),
 // waits until the range's next ticket is published and takes every ticket
 // of the range published by then as one run (<= kRingRunMax tickets: a
 // 32-packet batch alone would leave 7/8 of the workgroup's lanes idle),
@@ -481,7 +476,11 @@ __device__ __forceinline__ void ring_done_wave(const RingArgs &a, const uint64_t
 // stores) and marks the tickets done in host memory after them
 // (kRingRelease: behind a system-scope release). The range length adapts to
 // the batch size the lane sees: about kRingRunPackets packets per claim.
-// Create a ring with as many lanes as workers submit on.
+// Create a ring with as many lanes as workers submit on. (Round 6 measured
+// workgroups claiming on another lane when their own had no unclaimed
+// published ticket: the sweep's 4-submitter rows fell from ~40 to ~20 Gpps
+// -- the scans and the extra claimers crowd the lanes' counter lines --
+// profiles/r06/ring_ab_r06g.json.)
 //
 // The serving loop is shared by the table kinds: `look(key, default_gate)`
 // is the classifier (em_ring_kernel: ExactMatch, wm_ring_kernel:
@@ -492,15 +491,16 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
   __shared__ uint64_t sh_w[kRingRunMax][4];
   __shared__ uint32_t sh_pre[kRingRunMax + 1];  // the run's packet prefix sums
   __shared__ uint64_t sh_t;
-  __shared__ uint32_t sh_k, sh_rel, sh_lane;
-  const uint32_t home = (blockIdx.x - 1) % a.nlanes;
+  __shared__ uint32_t sh_k, sh_rel;
+  const uint32_t lane = (blockIdx.x - 1) % a.nlanes;
+  unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
   const unsigned long long *dstop = a.dev + (size_t)a.nlanes * kRingLaneWords;
+  const uint64_t *ldesc = a.desc + (size_t)lane * a.nslots * kRingDescWords;
+  uint32_t *ldone = a.done + (size_t)lane * a.nslots;
   if (threadIdx.x >= kRingBlock) {  // wave-uniform
-    ring_done_wave(a, &sh_t, &sh_k, &sh_rel, &sh_lane);
+    ring_done_wave(a, ldone, &sh_t, &sh_k, &sh_rel);
     return;
   }
-  uint32_t lane = home;  // the lane of the current claim (wave 0, uniform)
-  unsigned long long *dl = a.dev + (size_t)lane * kRingLaneWords;
   const uint64_t mask48 = (1ull << 48) - 1;
   constexpr int kPpl = PPL;  // packets per lane per round, loads in flight
   const uint32_t wl = threadIdx.x & 63;
@@ -510,22 +510,6 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
   for (;;) {
     if (threadIdx.x < 64) {  // wave 0
       if (next == end) {
-        // the lane to claim on: wave lane j looks at lane (home + j) %
-        // nlanes; the first with a published ticket nobody claimed yet (the
-        // home lane first), else the home lane (a claim ahead)
-        uint32_t pick = home;
-        if (a.nlanes > 1) {
-          const uint32_t cand = (home + wl) % a.nlanes;
-          bool open = false;
-          if (wl < a.nlanes) {
-            const unsigned long long *dc = a.dev + (size_t)cand * kRingLaneWords;
-            open = ld_agent(dc) < ld_agent(dc + 1);
-          }
-          const uint64_t m = __ballot(open);
-          if (m) pick = (home + (uint32_t)__builtin_ctzll(m)) % a.nlanes;
-        }
-        lane = pick;
-        dl = a.dev + (size_t)lane * kRingLaneWords;
         uint64_t t = 0;
         if (wl == 0) t = atomicAdd(dl, (unsigned long long)claim);
         next = __shfl(t, 0);
@@ -533,13 +517,11 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
       }
       uint64_t p = 0;
       if (wl == 0) {
-        // Every waiting workgroup polls here, all on the few lines of the
-        // lanes' counters: polls back off (s_sleep 2 -> 32, ~0.1 -> 0.9 us)
-        // so that waiting does not crowd those lines -- the claim atomics
-        // and the dispatcher's mirror stores go to the same ones -- and the
-        // stop word is read relaxed (an acquire per poll invalidated the
-        // caches every iteration); the acquire follows only once it is set.
-        uint32_t nap = 0;
+        // The stop word is read relaxed: an acquire load per poll put a
+        // cache invalidate (buffer_inv) in every iteration of every waiting
+        // workgroup (the ring sweep +10-15 % without it, profiles/r06/
+        // ring_ab_r06g.json); the acquire follows only once it is set.
+        // (Backing the polls off, s_sleep 2 -> 32, measured no better.)
         for (;;) {
           p = ld_agent(dl + 1);
           if (p > next) break;
@@ -550,14 +532,7 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
             p = ld_agent(dl + 1);
             break;
           }
-          if (nap < 4) {
-            __builtin_amdgcn_s_sleep(2);
-          } else if (nap < 8) {
-            __builtin_amdgcn_s_sleep(8);
-          } else {
-            __builtin_amdgcn_s_sleep(32);
-          }
-          nap++;
+          __builtin_amdgcn_s_sleep(2);
         }
       }
       p = __shfl(p, 0);
@@ -566,8 +541,7 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
       uint64_t w[4] = {0, 0, 0, 0};
       if (wl < k) {
         const uint64_t tag = (t + 1) & 0xFFFF;
-        const uint64_t *d =
-            a.desc + ((size_t)lane * a.nslots + t % a.nslots) * kRingDescWords;
+        const uint64_t *d = ldesc + (t % a.nslots) * kRingDescWords;
         while (!ring_read(d, tag, w)) __builtin_amdgcn_s_sleep(1);
       }
       // acquire: the batches' frames were written (by the host or a copy)
@@ -599,7 +573,6 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         sh_t = next;
         sh_k = k;
         sh_rel = rel ? 1u : 0u;
-        sh_lane = lane;
       }
       next += k;
       // the next claim: about kRingRunPackets packets of this lane's batches

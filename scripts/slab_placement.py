@@ -8,7 +8,8 @@ One process: the C4 rule set (100 K WildcardMatch rules over 8 masks) and
 8 M IMIX frames in 2 KB slots, timed (the run-time compiled kernel, 100
 launches after a settle, HIP events) over
   * slab A: the bench's allocation (torch.repeat of the 1 M frames, 16 GB);
-  * D / E: hipExtMallocWithFlags with hipDeviceMallocContiguous / 0;
+  * D1-3 / E1-3: hipExtMallocWithFlags with hipDeviceMallocContiguous / 0,
+    interleaved;
   * slab B: a second torch allocation holding the same bytes;
   * slab A again (the first measurement's repeatability);
   * A2: a torch allocation made after A was freed;
@@ -92,7 +93,9 @@ def main():
     # hipExtMallocWithFlags: physically contiguous (best effort), and plain
     hip = C.CDLL("libamdhip64.so")
     raw = []
-    for name, flags in (("D (hipDeviceMallocContiguous)", 4), ("E (hipExtMallocWithFlags 0)", 0)):
+    for name, flags in (("D1 (hipDeviceMallocContiguous)", 4), ("E1 (hipExtMallocWithFlags 0)", 0),
+                        ("D2 (hipDeviceMallocContiguous)", 4), ("E2 (hipExtMallocWithFlags 0)", 0),
+                        ("D3 (hipDeviceMallocContiguous)", 4), ("E3 (hipExtMallocWithFlags 0)", 0)):
         p = C.c_void_p()
         rc = hip.hipExtMallocWithFlags(C.byref(p), C.c_size_t(size), C.c_uint(flags))
         if rc:
