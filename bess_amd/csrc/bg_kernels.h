@@ -377,9 +377,17 @@ constexpr int kRingThreads = kRingBlock + 64;
 constexpr int kRingLaneWords = 16;
 // A worker workgroup takes up to kRingRunMax published tickets of its lane
 // as one run, and claims about kRingRunPackets packets' worth of tickets at
-// a time (one round of its 256 lanes x 4 packets)
+// a time while its lane has a backlog: four rounds of its 256 lanes x 4
+// packets (kRingRunPacketsIdle, one round, while the lane's tickets arrive
+// slower than they are served). Claims of one round (round 5) left a run's
+// fixed costs -- the claim, the publication wait, the descriptor reads, the
+// acquire, the done words -- on 1024 packets, and 512 / 1024-packet tickets
+// ran at 25-36 Gpps from 16 submitters against 48 at 256; claims of four
+// rounds: 58-62 Gpps at every size from 256 up, 16 submitters above 4
+// (profiles/r06/ring_ab_r06h.json: claims of 1, 2 and 4 rounds measured)
 constexpr uint32_t kRingRunMax = 16;
-constexpr uint32_t kRingRunPackets = kRingBlock * 4;
+constexpr uint32_t kRingRunPackets = kRingBlock * 16;
+constexpr uint32_t kRingRunPacketsIdle = kRingBlock * 4;
 // a descriptor slot: 4 tagged words + 4 of padding, one 64-byte line, so a
 // host writing it through write-combining buffers fills a whole buffer,
 // which leaves for the device at once (a half-written line can wait in the

@@ -507,6 +507,7 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
   // wave 0's claim state (uniform): the claimed range [next, end)
   uint64_t next = 0, end = 0;
   uint32_t claim = 1;  // tickets per claim
+  bool fresh = false, backlog = false;  // the claim is new / was published whole
   for (;;) {
     if (threadIdx.x < 64) {  // wave 0
       if (next == end) {
@@ -514,6 +515,7 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         if (wl == 0) t = atomicAdd(dl, (unsigned long long)claim);
         next = __shfl(t, 0);
         end = next + claim;
+        fresh = true;
       }
       uint64_t p = 0;
       if (wl == 0) {
@@ -536,6 +538,8 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         }
       }
       p = __shfl(p, 0);
+      if (fresh) backlog = p >= end;  // the whole claim was waiting for us
+      fresh = false;
       const uint32_t k = p > next ? (uint32_t)((p < end ? p : end) - next) : 0u;
       const uint64_t t = next + wl;
       uint64_t w[4] = {0, 0, 0, 0};
@@ -575,10 +579,15 @@ __device__ __forceinline__ void ring_serve(const RingArgs &a, Look look) {
         sh_rel = rel ? 1u : 0u;
       }
       next += k;
-      // the next claim: about kRingRunPackets packets of this lane's batches
+      // the next claim: about kRingRunPackets packets of this lane's
+      // batches while the lane has a backlog (its tickets were all
+      // published before this workgroup got to them), one round's worth
+      // while it trickles (tickets a busy workgroup has claimed wait for
+      // it, however many others are idle)
       if (k && next == end) {
         const uint32_t per = max(total / k, 1u);
-        claim = min(max(kRingRunPackets / per, 1u), (uint32_t)kRingRunMax);
+        const uint32_t want = backlog ? kRingRunPackets : kRingRunPacketsIdle;
+        claim = min(max(want / per, 1u), (uint32_t)kRingRunMax);
       }
     }
     // B1 (ring_barrier): the frames' freshness for every wave is the

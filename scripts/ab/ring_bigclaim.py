@@ -1,0 +1,4 @@
+# the ring's claims always about kRingRunPackets packets (no backlog test)
+p='bess_amd/csrc/bg_kernels.hip'; s=open(p).read()
+a="const uint32_t want = backlog ? kRingRunPackets : kRingRunPacketsIdle;"
+assert s.count(a)==1; open(p,'w').write(s.replace(a, "const uint32_t want = kRingRunPackets;"))

@@ -47,6 +47,9 @@ if has ringab; then  # the sweep's ring rows: product vs $RINGLIBS, interleaved
     for L in product $RINGLIBS; do
       if [ "$L" = product ]; then LA=""; else LA="--lib scripts/bin/libbessgpu_$L.so"; fi
       step "sweep_${L}_$rep" 600 python bench.py --only sweep --no-cpu $LA
+      if [ -n "$PIPEAB" ]; then
+        step "pipe_${L}_$rep" 600 python bench.py --only pipe --no-cpu $LA
+      fi
     done
   done
 fi

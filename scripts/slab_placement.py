@@ -2,7 +2,10 @@
 """Does C4's 2 KB-slot time depend on where its 16 GB slab lies? (DESIGN §8
 open item 7)
 
-    python scripts/slab_placement.py OUT.json
+    python scripts/slab_placement.py OUT.json [pmc]
+
+(pmc: 21 launches per slab and no settle, for rocprofv3 --pmc passes whose
+per-dispatch rows are then grouped by slab in this order.)
 
 One process: the C4 rule set (100 K WildcardMatch rules over 8 masks) and
 8 M IMIX frames in 2 KB slots, timed (the run-time compiled kernel, 100
@@ -55,11 +58,15 @@ def main():
     dg = torch.empty(n, dtype=torch.int16, device="cuda")
     ref = None
 
+    pmc = len(sys.argv) > 2 and sys.argv[2] == "pmc"
+
     def timed(slab, k=100):
         t.classify(slab, 2048, n, 8192, dg)
         torch.cuda.synchronize()
+        if pmc:  # counter passes: 1 + 20 launches per slab, nothing else
+            k = 20
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < 0.1:  # settle (as bench.py clock_settle)
+        while not pmc and time.perf_counter() - t0 < 0.1:  # settle (as bench.py clock_settle)
             for _ in range(8):
                 t.classify(slab, 2048, n, 8192, dg)
             torch.cuda.synchronize()
