@@ -40,7 +40,7 @@ if has sweep; then  # the C2 batch sweep alone (ring rows)
   step sweep 600 python bench.py --only sweep --no-cpu
 fi
 if has placement; then  # C4's 2 KB-slot time over separately placed slabs
-  step placement 600 python scripts/slab_placement.py "$OUT/placement.json"
+  step placement 600 python scripts/slab_placement.py "$OUT/placement.json" $PLACEMENT
 fi
 if has ringab; then  # the sweep's ring rows: product vs $RINGLIBS, interleaved
   for rep in 1 2; do

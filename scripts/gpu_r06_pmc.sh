@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6 counter passes: `gpurun -- bash scripts/gpu_r06_pmc.sh OUTDIR [what]`
 #   what: scatter (scripts/scatter_probe.hip variants) and/or placement
-#   (scripts/slab_placement.py pmc), comma list; one rocprofv3 run per pass.
+#   (scripts/slab_placement.py pmc), tcc (per-channel L2 requests of the
+#   same run), comma list; one rocprofv3 run per pass.
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 OUT="$R/gpurun_out/$1"
@@ -33,5 +34,9 @@ if [[ ",$WHAT," == *",scatter,"* ]]; then
 fi
 if [[ ",$WHAT," == *",placement,"* ]]; then
   pass placement python3 $R/scripts/slab_placement.py "$OUT/placement_pmc.json" pmc
+fi
+if [[ ",$WHAT," == *",tcc,"* ]]; then  # per-instance L2 channel requests, A vs the rest
+  P1="TCC_EA0_RDREQ"; P2="TCC_REQ"
+  pass placement_tcc python3 $R/scripts/slab_placement.py "$OUT/placement_tcc.json" pmc
 fi
 echo done >> "$OUT/steps.log"

@@ -5,7 +5,9 @@ open item 7)
     python scripts/slab_placement.py OUT.json [pmc]
 
 (pmc: 21 launches per slab and no settle, for rocprofv3 --pmc passes whose
-per-dispatch rows are then grouped by slab in this order.)
+per-dispatch rows are then grouped by slab in this order; many: the bench's
+allocation, then six hipDeviceMallocContiguous and six plain 16 GB
+allocations, interleaved and all kept.)
 
 One process: the C4 rule set (100 K WildcardMatch rules over 8 masks) and
 8 M IMIX frames in 2 KB slots, timed (the run-time compiled kernel, 100
@@ -92,6 +94,27 @@ def main():
         return e
 
     res = []
+    if len(sys.argv) > 2 and sys.argv[2] == "many":
+        # six physically contiguous and six plain allocations, interleaved,
+        # all kept alive (independent placements), after the bench's own
+        d0 = torch.from_numpy(frames.reshape(-1)).cuda()
+        A = d0.repeat(rep)
+        del d0
+        size = A.numel()
+        res.append(entry("A (bench allocation)", A))
+        hip = C.CDLL("libamdhip64.so")
+        for i in range(6):
+            for name, flags in (("contiguous", 4), ("plain", 0)):
+                p = C.c_void_p()
+                rc = hip.hipExtMallocWithFlags(C.byref(p), C.c_size_t(size), C.c_uint(flags))
+                if rc:
+                    res.append({"slab": "%s %d" % (name, i), "error": rc})
+                    continue
+                assert hip.hipMemcpy(p, C.c_void_p(A.data_ptr()), C.c_size_t(size), 3) == 0
+                res.append(entry("%s %d" % (name, i), Raw(p.value)))
+        with open(out_path, "w") as f:
+            json.dump({"what": "many", "pkts": n, "results": res}, f, indent=1)
+        return
     d0 = torch.from_numpy(frames.reshape(-1)).cuda()
     A = d0.repeat(rep)
     del d0
