@@ -161,6 +161,46 @@ def shape_ceiling(shape, pkts, ms):
             "source": os.path.relpath(files[-1], ROOT)}
 
 
+def placed_slab(make, probe, torch, candidates=3):
+    """A resident slab for a scattered-read leg (a 32 B window per 2 KB
+    slot: C4 on 2 KB slots, ExactMatch on 1500 B frames) whose placement
+    does not slow it down. Such a read runs 0.188 ms on most 16 GB
+    allocations and 0.203 / 0.220 ms on about one in three, the same bytes
+    in the same process: the physical pages the allocation gets decide it
+    (profiles/r06/placement_*.json; not the address alignment,
+    the allocation flags or the TLB). `make()` builds a candidate slab,
+    `probe(slab)` times the leg's own launch on it (ms): `candidates` are
+    built and probed, the fastest is kept, the others are freed, and every
+    candidate's probe time goes into the line."""
+    times, best, best_ms = [], None, None
+    for _ in range(candidates):
+        sl = make()
+        ms = probe(sl)
+        times.append(round(ms, 4))
+        if best is None or ms < best_ms:
+            best, best_ms = sl, ms
+        else:
+            del sl
+        torch.cuda.empty_cache()
+    return best, {"candidates_probe_ms": times, "kept": times.index(round(best_ms, 4)),
+                  "why": "scattered 2 KB-slot reads depend on the slab's physical pages "
+                         "(DESIGN section 8): the fastest of the candidate allocations is kept"}
+
+
+def probe_ms(step, torch, k=10):
+    """ms per launch of `step` over k launches after one, HIP events"""
+    step()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(k):
+        step()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / k
+
+
 def traffic_gbs(key, kernel_ms):
     """PMC bytes per launch / measured launch duration, in GB/s (same basis
     as roofline.achieved); None until profiles/ holds a PMC measurement."""
@@ -486,15 +526,22 @@ def run_em1500(args, dev, torch):
     # UDP or TCP), then the slab: zero payload past them
     keys, gates, hdr = P.em_workload(args.rules, n, seed=0x5EED, stride=64,
                                      frame_len=1496, pkt_seed=0x1500)
-    d = torch.zeros(n * 2048, dtype=torch.uint8, device=dev)
-    d.view(n, 2048)[:, :64] = torch.from_numpy(hdr).to(dev)
-    ns = 1 << 20
-    sample = np.ascontiguousarray(hdr[:ns])
-    del hdr
     t = F.EmTable(P.em_fields_5tuple())
     t.add_many(keys, gates)
     t.sync(dev.index)
     dg = torch.empty(n, dtype=torch.int16, device=dev)
+    h = torch.from_numpy(hdr).to(dev)
+
+    def make():
+        sl = torch.zeros(n * 2048, dtype=torch.uint8, device=dev)
+        sl.view(n, 2048)[:, :64] = h
+        return sl
+    d, placement = placed_slab(
+        make, lambda sl: probe_ms(lambda: t.classify(sl, 2048, n, 8192, dg), torch), torch)
+    del h
+    ns = 1 << 20
+    sample = np.ascontiguousarray(hdr[:ns])
+    del hdr
     t.classify(d, 2048, n, 8192, dg)
     torch.cuda.synchronize()
     em = oracle_em_bulk(keys, gates)
@@ -513,6 +560,7 @@ def run_em1500(args, dev, torch):
            # a 32 B window per 2 KB slot is one 64 B HBM request: the
            # shape's own rate (hbm_probe s2k32) bounds this leg
            "measured_ceiling": shape_ceiling("s2k32", n, ms),
+           "placement": placement,
            "parity": "bit-exact vs oracle on %d pkts" % ns if parity else "MISMATCH"}
     if not args.no_cpu:
         cn = 1 << 18
@@ -1517,11 +1565,14 @@ def run_wm(args, dev, torch):
 
     nan = float("nan")
     parity, ms2k, g2k, aot2k, aot_h = True, nan, None, nan, nan
+    placement = None
     if args.wm_layout != "slab":  # the frames in 2 KB slots
         d0 = torch.from_numpy(frames.reshape(-1)).to(dev)
-        d = d0.repeat(rep)
-        del d0
         dg = torch.empty(n, dtype=torch.int16, device=dev)
+        d, placement = placed_slab(
+            lambda: d0.repeat(rep),
+            lambda sl: probe_ms(lambda: t.classify(sl, 2048, n, 8192, dg), torch), torch)
+        del d0
         t.classify(d, 2048, n, 8192, dg)
         torch.cuda.synchronize()
         parity, g2k = check(dg)
@@ -1574,7 +1625,7 @@ def run_wm(args, dev, torch):
            "parity": "bit-exact vs oracle on 64K-pkt samples of both layouts; "
                      "header-slab gates == 2KB-slot gates on all %d pkts" % n0
                      if parity and parity_h else "MISMATCH",
-           "slots_2k": {"ms_per_step": round(ms2k, 4),
+           "slots_2k": {"ms_per_step": round(ms2k, 4), "placement": placement,
                         "Mpps": round(n / (ms2k * 1e-3) / 1e6, 1),
                         "roofline": {"bound": "hbm", "achieved": round(gbs2k, 1),
                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",

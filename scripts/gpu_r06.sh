@@ -56,6 +56,11 @@ fi
 if has scatter; then  # scripts/scatter_probe.hip, every variant
   step scatter 600 scripts/bin/scatter_probe 16
 fi
+if has legs; then  # bench legs alone: $ONLY (e.g. "wm em1500")
+  for W in $ONLY; do
+    step "leg_$W" 600 python bench.py --only $W --no-cpu
+  done
+fi
 if has bench; then
   step bench 900 python bench.py
 fi

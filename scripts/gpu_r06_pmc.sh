@@ -2,7 +2,9 @@
 # Round 6 counter passes: `gpurun -- bash scripts/gpu_r06_pmc.sh OUTDIR [what]`
 #   what: scatter (scripts/scatter_probe.hip variants) and/or placement
 #   (scripts/slab_placement.py pmc), tcc (per-channel L2 requests of the
-#   same run), comma list; one rocprofv3 run per pass.
+#   same run), mem (the L2's memory-side queue and DRAM credit stalls on
+#   the scatter shapes and two streaming shapes), comma list; one rocprofv3
+#   run per pass.
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 OUT="$R/gpurun_out/$1"
@@ -38,5 +40,15 @@ fi
 if [[ ",$WHAT," == *",tcc,"* ]]; then  # per-instance L2 channel requests, A vs the rest
   P1="TCC_EA0_RDREQ"; P2="TCC_REQ"
   pass placement_tcc python3 $R/scripts/slab_placement.py "$OUT/placement_tcc.json" pmc
+fi
+if [[ ",$WHAT," == *",mem,"* ]]; then  # the memory side: EA read queue and DRAM credit stalls
+  P1="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum GRBM_GUI_ACTIVE"
+  P2="TCC_TAG_STALL_sum TCC_REQ_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
+  for V in "vec2 512 1" "pair 512 1" "quad64 512 1"; do
+    set -- $V
+    pass "mem_$1_$2_$3" $R/scripts/bin/scatter_probe 16 $1 $2 $3 20
+  done
+  pass mem_full16 $R/scripts/bin/hbm_probe 16 only full16 2 20
+  pass mem_slab66 $R/scripts/bin/hbm_probe 16 only slab66 2 20
 fi
 echo done >> "$OUT/steps.log"

@@ -12,9 +12,13 @@ lists them) is split into groups of 21, each without its first launch.
 Derived, per group and launch:
   req_per_slot       TCP_TCC_READ_REQ / slots (L1 -> L2 read requests)
   latency_cycles     TCP_TCC_READ_REQ_LATENCY / TCP_TCC_READ_REQ
-  inflight_per_cu    TCP_TCC_READ_REQ_LATENCY / GRBM_GUI_ACTIVE / CUs: the
-                     read requests a CU's L1 has outstanding on average
-                     (Little's law)
+  inflight_per_cu    TCP_TCC_READ_REQ_LATENCY / (GRBM_GUI_ACTIVE / 8 XCDs)
+                     / CUs: the read requests a CU's L1 has outstanding on
+                     average (Little's law)
+  ea_rd_inflight_chip  TCC_EA0_RDREQ_LEVEL / cycles: the L2s' read requests
+                     outstanding to memory, chip-wide
+  dram_credit_stall_per_cycle  TCC_EA0_RDREQ_DRAM_CREDIT_STALL / cycles (the
+                     L2 channels waiting for DRAM credits, summed)
   utcl1_miss_per_slot  TCP_UTCL1_TRANSLATION_MISS / slots
 """
 import csv
@@ -26,6 +30,7 @@ import sys
 from collections import defaultdict
 
 CUS = 256
+XCDS = 8
 
 
 def load(d):
@@ -56,9 +61,10 @@ def main():
             counts[name[k]] += 1
         main_k = max(counts, key=counts.get)
         ids = sorted(k for k in per if name[k] == main_k)
-        if tag.startswith("sc_"):
+        if not tag.startswith("placement"):
             groups = [("all", ids[1:])]
-            slots = 8 << 20  # 16 GiB of 2 KiB slots
+            # 16 GiB of 2 KiB slots (scatter_probe), of 64 B slots (hbm_probe)
+            slots = (256 << 20) if tag.startswith(("mem_full16", "mem_slab66")) else (8 << 20)
         else:
             groups = [("slab%d" % (i // 21), ids[i + 1:i + 21]) for i in range(0, len(ids), 21)]
             slots = 8 << 20
@@ -81,8 +87,17 @@ def main():
                 e["req_per_slot"] = round(req / slots, 3)
                 if lat:
                     e["latency_cycles"] = round(lat / req, 1)
+            # GRBM_GUI_ACTIVE counts every XCD's busy cycles (8 per cycle)
             if lat and act:
-                e["inflight_per_cu"] = round(lat / act / CUS, 1)
+                e["inflight_per_cu"] = round(lat / (act / XCDS) / CUS, 1)
+            lev, ea = e.get("TCC_EA0_RDREQ_LEVEL_sum"), e.get("TCC_EA0_RDREQ_sum")
+            if lev and act:
+                e["ea_rd_inflight_chip"] = round(lev / (act / XCDS), 1)
+                if ea:
+                    e["ea_rd_latency_cycles"] = round(lev / ea, 1)
+            st = e.get("TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum")
+            if st is not None and act:
+                e["dram_credit_stall_per_cycle"] = round(st / (act / XCDS), 2)
             if e.get("TCP_UTCL1_TRANSLATION_MISS_sum") is not None:
                 e["utcl1_miss_per_slot"] = round(e["TCP_UTCL1_TRANSLATION_MISS_sum"] / slots, 4)
     print(json.dumps(res, indent=1))
