@@ -53,6 +53,9 @@ if has ringab; then  # the sweep's ring rows: product vs $RINGLIBS, interleaved
     done
   done
 fi
+if has gate; then  # scripts/gate_probe.hip: C2's shape, gate stores placed differently
+  step gate 300 scripts/bin/gate_probe 1
+fi
 if has scatter; then  # scripts/scatter_probe.hip, every variant
   step scatter 600 scripts/bin/scatter_probe 16
 fi
