@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""DESIGN.md §6 (round 5) from one bench line: the measurement table
+"""DESIGN.md §6 (round 6) from one bench line: the measurement table
 (scripts/design_table.py), the sweep, and the host end-to-end figures, all
 read from the line, so the record quotes a measured line and nothing else.
 
@@ -23,25 +23,28 @@ def main():
     passed = m.group(1) if m else "?"
     rel = os.path.relpath(line_path, ROOT)
     c2 = d["roofline"]
-    head = f"""## 6. Measurements (MI355X, round 5)
+    head = f"""## 6. Measurements (MI355X, round 6)
 
 `python bench.py` prints one line with C2 as the headline. The line also
 carries the batch sweep, C1, C3, EM on 1500 B frames, C4, C5, the §8f
 modules, the host end-to-end legs, the roofline and the CPU baselines. The
 table below is generated from one such line (`{rel}`, `python
 scripts/design_s6.py <line> <tests log>`): the round's last full call on
-the final tree (`scripts/gpu_full.sh tests,bench,prof`), in which {passed}
-GPU tests passed and smoke was bit-exact. Its kernel trace is summarised
-per grid in `profiles/r05_kernels.md`, and its raw stats are in
-`profiles/r05/bench_kernel_stats_final.csv`. "traffic / algorithmic" is
-the PMC HBM bytes per launch over the algorithmic bytes. The bytes come
-from `profiles/r05_traffic.json`: FETCH_SIZE / WRITE_SIZE passes on this
-round's kernels, with the per-shape factor calibrated below. C4's 1.25x
-counts the random 64 B slot records at the x2 of a 128 B request, so it is
-an upper bound. C2's kernel took {c2['kernel_ms']} ms, which is
-{c2['frac']:.3f} of the HBM roofline and
-{d['measured_ceiling']['frac_of_ceiling']:.2f} of its own access shape
-measured alone (`slab66`).
+the final tree (`scripts/gpu_r06.sh`), in which {passed} GPU tests passed
+and smoke was bit-exact. Every leg's kernel has a row of its own in
+`profiles/r06_kernels.md` (`scripts/prof_legs.py`: one traced process per
+leg, the leg's timed launches split from its warm-up; every row within 1 %
+of the leg's HIP-event time but NAT's, whose line time includes its host
+walk), with the raw stats under `profiles/r06/legs_*/`. "traffic /
+algorithmic" is the PMC HBM bytes per launch over the algorithmic bytes
+(the latest `profiles/r*_traffic.json`: FETCH_SIZE / WRITE_SIZE passes,
+with the per-shape factor calibrated below). C4's 1.25x counts the random
+64 B slot records at the x2 of a 128 B request, so it is an upper bound.
+C2's kernel took {c2['kernel_ms']} ms, which is {c2['frac']:.3f} of the
+HBM roofline and {d['measured_ceiling']['frac_of_ceiling']:.2f} of its own
+access shape measured alone (`slab66`). The 2 KB-slot legs (C4's 2 KB
+slots, EM on 1500 B frames) run on the fastest of three slab placements
+(§8, the line's `placement`).
 
 {table.rstrip()}
 
@@ -56,6 +59,14 @@ measured alone (`slab66`).
     l4_p = pipe["L4Checksum_1500B"]["Mpps_by_threads_batch8192"]
     pw, pc = pl["Mpps_by_workers"], pl["cpu_same_harness"]["Mpps_by_workers"]
     wm, l4 = pool["WildcardMatch"], pool["L4Checksum"]
+    wc, lc = wm.get("w0_cycles_per_pkt", {}), l4.get("w0_cycles_per_pkt", {})
+
+    def cyc(c, who):
+        x = c.get(who, {})
+        return " / ".join("%s %.0f" % (k, x[k]) for k in ("source", "proc", "sink", "task")
+                          if k in x)
+    l4pc = l4.get("pcie") or {}
+    l4pp = pipe["L4Checksum_1500B"].get("pcie_16_threads") or {}
     host = f"""**Host end-to-end (PCIe-inclusive; never the bench `value`).** Frames sit
 in 2624 B snbuf-like host buffers (frame at +512), 262,144 of them (688 MB,
 so a pass is cold in the caches of one worker). The figures below are
@@ -92,10 +103,24 @@ figure is compared with the CPU figure from the same call.
     {l4['cpu_same_harness']['Mpps']} for the restated reference in the same
     harness.
 
-  The pool leg is bound by the host. With deferred emission each worker
-  keeps its budget of packets in flight, and the Sources' frame copies into
-  buffers that left the cache cost more than the lookups the GPU takes
-  over. For L4Checksum every frame also crosses PCIe.
+  Where worker 0's cycles go, per packet (TSC at {wc.get('tsc_ghz', '?')} GHz;
+  Source = pool allocation and frame copy, proc = ProcessBatch, sink, task
+  = the module's emit task):
+  * WildcardMatch: plugin {cyc(wc, 'plugin')}; reference
+    {cyc(wc, 'reference')}. The plugin's ProcessBatch (submit to the pipe,
+    emit what finished) costs a quarter of the reference's lookups; its
+    Source costs about twice the reference's, because with deferred
+    emission the worker's budget of packets stays in flight and the pool
+    buffers the Source refills have left the cache.
+  * L4Checksum: plugin {cyc(lc, 'plugin')}; reference {cyc(lc, 'reference')}.
+    The plugin's ProcessBatch time is the wait for ring slots: the frames
+    are read in place over PCIe at {l4pc.get('h2d_GBps', '?')} GB/s,
+    {l4pc.get('pcie_frac', '?')} of the link's 63 GB/s (PCIe Gen5 x16,
+    MI355X_MICROARCH.md). The restated reference on the same 16 workers
+    summed {l4['cpu_same_harness']['Mpps']} Mpps x 1,496 B: more than
+    PCIe can carry at any rate, so at 1500 B a device-side L4Checksum
+    cannot beat 16 host cores; it pays only where the frames are already
+    in device memory (C3: {d['extra_configs']['C3']['Mpps'] if isinstance(d['extra_configs'].get('C3'), dict) else '?'} Mpps resident).
 * Aggregation queue (`bg_pipe_run`, native worker loops), Mpps with
   1 / 4 / 16 workers:
   * ExactMatch, ring mode (1024-packet slots): {em_ring['1']} /
@@ -105,7 +130,12 @@ figure is compared with the CPU figure from the same call.
     snbufs, 64 K-packet slots (launches): {wm_p['1']} / {wm_p['4']} /
     {wm_p['16']}, bit-exact.
   * L4Checksum at 1500 B (1504 B H2D + 130 B D2H per packet):
-    {l4_p['16']} at 16 workers, PCIe-bound.
+    {l4_p['16']} at 16 workers, {l4pp.get('h2d_GBps', '?')} GB/s host to
+    device, {l4pp.get('pcie_frac', '?')} of PCIe.
+  * The staged 16 B windows of ExactMatch / WildcardMatch use a small part
+    of the link (`pcie_*` fields of the line: ExactMatch ring, 16 workers,
+    {pipe['ExactMatch_64B'].get('pcie_16_threads_ring_batch1024_depth8', {}).get('pcie_frac', '?')}):
+    those legs are bound by the host threads.
 
 """
     # (design_table.py's output ends with the batch sweep table)
@@ -127,11 +157,11 @@ SWEEP_NOTE = """The stream row is launch-bound; the sweep's stream is attached
 (`bg_stream_attach`, §1): unattached, each launch also records the image's
 retirement event there (~4 µs per launch, `profiles/r04_launch_probe.jsonl`).
 The persistent rows are the ring with ticket runs (§3), one submission lane
-per submitter. Since round 5 the submitters are native threads released
-together (`bg_ring_run_lanes`), each making 4 passes over its part of the
-16 M slab. Until round 4 they were Python threads, whose start skew kept
-16 of them at the rate of 4 (ticket stamps: 1.1 ms from claim to seen at
-16, against 33 µs at 4)."""
+per submitter; the submitters are native threads released together
+(`bg_ring_run_lanes`), each making 4 passes over its part of the 16 M
+slab. Since round 6 a workgroup claims four rounds' worth of tickets while
+its lane has a backlog (§3): the dip round 5 left at 512 / 1024-packet
+tickets is gone, and 16 submitters run above 4 at every size."""
 
 
 if __name__ == "__main__":
