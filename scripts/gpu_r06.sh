@@ -53,6 +53,14 @@ if has ringab; then  # the sweep's ring rows: product vs $RINGLIBS, interleaved
     done
   done
 fi
+if has c2ab; then  # the headline kernel: product vs $C2LIBS, interleaved
+  for rep in 1 2; do
+    for L in product $C2LIBS; do
+      if [ "$L" = product ]; then LA=""; else LA="--lib scripts/bin/libbessgpu_$L.so"; fi
+      step "c2_${L}_$rep" 300 python bench.py --no-extra --no-cpu --steps 200 --warmup 20 $LA
+    done
+  done
+fi
 if has gate; then  # scripts/gate_probe.hip: C2's shape, gate stores placed differently
   step gate 300 scripts/bin/gate_probe 1
 fi
