@@ -58,6 +58,19 @@ if has c2ab; then  # the headline kernel: product vs $C2LIBS, interleaved
     for L in product $C2LIBS; do
       if [ "$L" = product ]; then LA=""; else LA="--lib scripts/bin/libbessgpu_$L.so"; fi
       step "c2_${L}_$rep" 300 python bench.py --no-extra --no-cpu --steps 200 --warmup 20 $LA
+      if [ -n "$C5AB" ]; then
+        step "c5_${L}_$rep" 300 python bench.py --only c5 --no-cpu $LA
+      fi
+    done
+  done
+fi
+if has legab; then  # bench legs $ABLEGS: product vs $LEGLIBS, interleaved
+  for rep in 1 2; do
+    for L in product $LEGLIBS; do
+      if [ "$L" = product ]; then LA=""; else LA="--lib scripts/bin/libbessgpu_$L.so"; fi
+      for W in $ABLEGS; do
+        step "leg_${W}_${L}_$rep" 300 python bench.py --only $W --no-cpu $LA
+      done
     done
   done
 fi
