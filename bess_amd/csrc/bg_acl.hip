@@ -23,6 +23,7 @@ namespace {
 struct AclOp {
   using Args = AclArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const AclArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const AclArgs &) {}
@@ -81,6 +82,7 @@ __device__ __forceinline__ uint32_t masked_ne(uint32_t v, uint32_t a, uint32_t m
 struct AclLdsOp {
   using Args = AclArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const AclArgs &a) { return (size_t)a.nrules * 32; }
   __device__ static void stage(uint32_t *lds, const AclArgs &a) {
@@ -133,6 +135,7 @@ constexpr size_t kAclLdsRules = 48 << 10;
 struct AclBvOp {
   using Args = AclArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const AclArgs &a) { return (size_t)(a.k0 + a.k1) * 4; }
   __device__ static void stage(uint32_t *lds, const AclArgs &a) {
@@ -198,6 +201,7 @@ struct AclBvOp {
 struct AclTreeOp {
   using Args = AclArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const AclArgs &a) { return (size_t)a.tree_words * 4; }
   __device__ static void stage(uint32_t *lds, const AclArgs &a) {

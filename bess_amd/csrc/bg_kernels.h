@@ -16,6 +16,9 @@ constexpr int kMaxTuples = 8;
 constexpr int kMaxDirect = 2;  // direct tuples per WildcardMatch image (WmArgs)
 constexpr int kMaxWindowChunks = 4;      // 16-byte chunks staged per packet
 constexpr uint32_t kLdsTableMax = 40960;  // tables up to this size go to LDS
+// tiles whose 2-byte results a slab kernel's wave holds in registers before
+// it stores them (em_slab_kernel, line_slab_kernel; bg_kernels.hip)
+constexpr int kGateHold = 32;
 constexpr uint16_t kGateNone = 0xFFFF;
 
 // How a packet's key is built from its frame bytes. Field f contributes

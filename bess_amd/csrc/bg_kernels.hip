@@ -262,6 +262,15 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 // the gates are stored nontemporally (streaming stores; C2 0.1896 -> 0.1825
 // ms). Both measured in one process each (scripts/variants.py em / c5,
 // profiles/r05/em_variants_r05m.json).
+// Round 6: a wave holds the gates of kGateHold consecutive grid-stride
+// tiles in registers and stores them together after those tiles' reads:
+// the 2-byte gate stores interleaved with the header stream cost the
+// stream (scripts/gate_probe.hip: C2's shape 0.1706 ms with per-tile
+// stores, 0.1659 with 16 tiles held, 0.1549 reading alone). With the table
+// in LDS at one workgroup per CU (launch_slab), C2 0.1837 -> 0.1674 ms,
+// 0.753 -> 0.827 of the roofline; C5 0.3448 -> 0.3424 (profiles/r06/
+// c2_ab_r06m.json, c2_ab_r06n.json, c2_ab_r06o.json: held 8 / 16 / 24 / 32
+// / 64 / 128 tiles measured; 64 and more spill).
 template <int KW, int NCH>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_slab_kernel(EmArgs a) {
@@ -290,7 +299,13 @@ void em_slab_kernel(EmArgs a) {
     }
   };
   if (t < ntiles) load_tile(t, v);
-  for (; t < ntiles; t += nwaves) {
+  for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * kGateHold) {
+  uint16_t held[kGateHold];
+#pragma unroll
+  for (int h = 0; h < kGateHold; h++) {
+    const uint64_t t = t0 + (uint64_t)h * nwaves;
+    held[h] = 0;
+    if (t >= ntiles) break;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t u = c * 64 + lane;
@@ -315,10 +330,14 @@ void em_slab_kernel(EmArgs a) {
     const uint32_t g = a.t.lds == kLdsTable
                            ? em_lookup<KW>(lds, a.t, k, a.default_gate)
                            : em_lookup_seq<KW>(a.t.base, a.t, k, a.default_gate);
-    const uint64_t idx = t * 64 + lane;
-    if (idx < a.n)  // a streaming store
-      __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
+    held[h] = (uint16_t)g;
     lds_fence();  // this tile's stage reads retire before the next writes
+  }
+#pragma unroll
+  for (int h = 0; h < kGateHold; h++) {  // the held gates, streaming stores
+    const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + lane;
+    if (idx < a.n) __builtin_nontemporal_store(held[h], a.gates + idx);
+  }
   }
 }
 
@@ -1506,8 +1525,10 @@ hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
     int pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
     // a table in L2 / MALL: 2 workgroups per CU (16 waves) probe faster
     // than the occupancy limit (C5: 0.3444 against 0.3557 ms,
-    // scripts/variants.py c5, profiles/r05/c5_variants_r05q.json)
-    if (a.t.lds == kLdsNone) pc = std::min(pc, 2);
+    // scripts/variants.py c5, profiles/r05/c5_variants_r05q.json); the
+    // table in LDS: one (8 waves, the table copied once per CU), with the
+    // gates held (round 6: 0.1674 against 0.1757 ms at two, c2_ab_r06m/n)
+    pc = std::min(pc, a.t.lds == kLdsNone ? 2 : 1);
     const uint64_t cap = (uint64_t)num_cus * pc;
     const uint64_t blocks = need > cap ? cap : need;
     if (a.t.lds == kLdsTable && pass == 0 && a.n < blocks * kLdsMinPktsPerBlock &&

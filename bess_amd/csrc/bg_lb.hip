@@ -51,6 +51,7 @@ template <int MODE>
 struct HlbOp {
   using Args = HlbArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 1;
   // 16-byte chunks of the first 64 bytes each mode reads
   static constexpr int c0 = MODE == kHlbL3 ? 1 : 0;
   static constexpr int c1 = MODE == kHlbL2 ? 1 : MODE == kHlbL3 ? 3 : 4;
@@ -88,6 +89,7 @@ template <int KW, int NCH>
 struct HlbFieldsOp {
   using Args = HlbArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 1;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const HlbArgs &x) { return HlbOp<kHlbL4>::lds_bytes(x); }
   __device__ static void stage(uint32_t *lds, const HlbArgs &x) { hlb_stage_lds(lds, x); }

@@ -6,6 +6,7 @@
 //   using Args = ...;   // with frames, stride, n, out (uint16_t per packet)
 //   static constexpr int c0, c1;   // 16-byte chunks [c0, c1) of the line used
 //   static constexpr bool kWrites;  // d[] chunks [c0, c1) are written back
+//   static constexpr int kSlabPerCu;  // line_slab_kernel workgroups per CU
 //   static size_t lds_bytes(const Args &);            (host) tables in LDS
 //   __device__ static void stage(uint32_t *lds, const Args &);   fill them
 //   __device__ static uint32_t decide(const Args &, const uint32_t *lds,
@@ -80,6 +81,11 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
 // The written-back lines are stored nontemporally (streaming stores:
 // UpdateTTL 0.4093 -> 0.3879 ms, StaticNAT 0.4131 -> 0.3908 per 16 M
 // packets, scripts/variants.py linew, profiles/r05/linew_r05n.json).
+// A reading op's wave holds kGateHold tiles' results in registers and
+// stores them together (as em_slab_kernel; round 6: HashLB l4 0.1811 ->
+// 0.1635 ms at one workgroup per CU, ACL 0.2157 -> 0.1910 at two,
+// profiles/r06/legs_ab_r06o.json); a writing op stores each tile's (its
+// line stores are per tile anyway: holding measured no better).
 template <class Op>
 __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args a,
                                                               uint32_t stage_words) {
@@ -106,8 +112,15 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
                  : make_uint4(0, 0, 0, 0);
     }
   };
+  constexpr int H = Op::kWrites ? 1 : kGateHold;
   if (t < ntiles) load_tile(t);
-  for (; t < ntiles; t += nwaves) {
+  for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * H) {
+  uint16_t held[H];
+#pragma unroll
+  for (int h = 0; h < H; h++) {
+    const uint64_t t = t0 + (uint64_t)h * nwaves;
+    held[h] = 0;
+    if (t >= ntiles) break;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t u = c * 64 + lane;
@@ -128,8 +141,7 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
     const uint64_t idx = t * 64 + lane;
     if (idx < a.n) {
       uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * 64;
-      // (a streaming store, as em_slab_kernel's gates: measured faster)
-      __builtin_nontemporal_store((uint16_t)Op::decide(a, lds, d, f), a.out + idx);
+      held[h] = (uint16_t)Op::decide(a, lds, d, f);
     }
     if constexpr (Op::kWrites) {
       // updated chunks back into this lane's slot of the stage, then the
@@ -151,6 +163,12 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+#pragma unroll
+  for (int h = 0; h < H; h++) {  // streaming stores, as em_slab_kernel's gates
+    const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + lane;
+    if (idx < a.n) __builtin_nontemporal_store(held[h], a.out + idx);
+  }
   }
 }
 
@@ -202,8 +220,9 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
     // 2 workgroups per CU (16 waves) rather than the occupancy limit:
     // HashLB l4 0.1906 -> 0.1809 ms, fields 0.1917 -> 0.1814, StaticNAT
     // 0.3761 -> 0.3627, UpdateTTL 0.3738 -> 0.3721 (profiles/r05/
-    // lineocc_r05v.json, linew_r05u.json) -- as em_slab_kernel runs
-    occ = std::min(occ, 2);
+    // lineocc_r05v.json, linew_r05u.json); HashLB with held gates at one
+    // (round 6, above): the op's kSlabPerCu
+    occ = std::min(occ, Op::kSlabPerCu);
     const uint64_t blocks = std::max<uint64_t>(1, std::min(need, (uint64_t)num_cus * occ));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLineBlock), lds, s, a,
                        (uint32_t)(tab / 4));

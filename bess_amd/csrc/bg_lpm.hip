@@ -22,6 +22,7 @@ namespace {
 struct LpmOp {
   using Args = LpmArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 1, c1 = 3;  // bytes [16, 48): dst IP at 30..33
   static size_t lds_bytes(const LpmArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const LpmArgs &) {}
@@ -41,6 +42,7 @@ struct LpmOp {
 struct Lpm16Op {
   using Args = LpmArgs;
   static constexpr bool kWrites = false;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 1, c1 = 3;
   static size_t lds_bytes(const LpmArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const LpmArgs &) {}
@@ -57,7 +59,7 @@ struct Lpm16Op {
 // the same with tbl16 staged in LDS (128 KB: one workgroup per CU, so
 // 1024 threads with a packet per lane and no slab stage): one L2 request
 // per packet in a /16 block with longer routes, none otherwise
-struct Lpm16LdsOp {
+struct Lpm16LdsOp {  // (line_kernel only: launch_line_wide)
   using Args = LpmArgs;
   static constexpr bool kWrites = false;
   static constexpr int c0 = 1, c1 = 3;

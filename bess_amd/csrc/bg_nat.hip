@@ -46,6 +46,7 @@ __device__ __forceinline__ bool l4_lo_at(int j, uint32_t ihl, bool udp) {
 struct NatOp {
   using Args = NatArgs;
   static constexpr bool kWrites = true;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 0, c1 = 4;
   static size_t lds_bytes(const NatArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const NatArgs &) {}

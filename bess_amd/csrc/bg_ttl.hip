@@ -20,6 +20,7 @@ template <int C1>
 struct TtlOp {
   using Args = TtlArgs;
   static constexpr bool kWrites = true;
+  static constexpr int kSlabPerCu = 2;
   static constexpr int c0 = 0, c1 = C1;
   static size_t lds_bytes(const TtlArgs &) { return 0; }
   __device__ static void stage(uint32_t *, const TtlArgs &) {}
