@@ -85,7 +85,10 @@ if has legs; then  # bench legs alone: $ONLY (e.g. "wm em1500")
     step "leg_$W" 600 python bench.py --only $W --no-cpu
   done
 fi
+if has dip; then  # the ring sweep's rows, every repetition (scripts/ring_dip_probe.py)
+  step dip 600 python scripts/ring_dip_probe.py "$OUT/dip.json" 8
+fi
 if has bench; then
-  step bench 900 python bench.py
+  step bench 900 python3 bench.py --gpus 1 --steps 20 --warmup 5
 fi
 echo done >> "$OUT/steps.log"
