@@ -16,6 +16,10 @@
 //             registers, stored after them (streaming)
 //   hold64    the same over 64 tiles: with 4096 waves and 16 M slots every
 //             wave's gates leave after its last read
+//   hold32 / hold128   the same over 32 / 128 tiles
+//   lds64 / lds128     the gates of 64 / 128 tiles held in LDS (a loop that is
+//             not unrolled: the classifier's tile body is too large to
+//             unroll 64 times), then stored from LDS 16 B per lane
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -75,6 +79,35 @@ __global__ __launch_bounds__(512) void hold(const u32x4 *src, size_t ntiles, uin
   }
 }
 
+template <int R>
+__global__ __launch_bounds__(512) void ldshold(const u32x4 *src, size_t ntiles,
+                                               uint16_t *gates) {
+  __shared__ __attribute__((aligned(16))) uint16_t held[8][R * 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const size_t nw = ((size_t)gridDim.x * blockDim.x) >> 6;
+  uint16_t *h = held[wid];
+  for (size_t b = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; b < ntiles;
+       b += nw * R) {
+#pragma unroll 1
+    for (int k = 0; k < R; k++) {
+      const size_t t = b + (size_t)k * nw;
+      if (t >= ntiles) break;
+      h[k * 64 + lane] = tile_x(src, t, lane);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS writes done
+    // 16 B per lane: 8 lanes per tile, 8 tiles per store instruction
+#pragma unroll
+    for (int i = 0; i < R / 8; i++) {
+      const int k = i * 8 + (lane >> 3);
+      const size_t t = b + (size_t)k * nw;
+      if (t < ntiles)
+        __builtin_nontemporal_store(reinterpret_cast<const u32x4 *>(h + k * 64)[lane & 7],
+                                    reinterpret_cast<u32x4 *>(gates + t * 64) + (lane & 7));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 #define CK(x)                                                                  \
   do {                                                                         \
     hipError_t e_ = (x);                                                       \
@@ -104,7 +137,9 @@ int main(int argc, char **argv) {
     const char *name;
     Kern k;
   } vars[] = {{"read64", per_tile<0>}, {"slab66", per_tile<1>}, {"slab66nt", per_tile<2>},
-              {"hold16", hold<16>},     {"hold64", hold<64>}};
+              {"hold16", hold<16>},     {"hold32", hold<32>},
+              {"hold64", hold<64>},     {"hold128", hold<128>},
+              {"lds64", ldshold<64>},   {"lds128", ldshold<128>}};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
