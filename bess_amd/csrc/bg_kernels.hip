@@ -262,15 +262,28 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 // the gates are stored nontemporally (streaming stores; C2 0.1896 -> 0.1825
 // ms). Both measured in one process each (scripts/variants.py em / c5,
 // profiles/r05/em_variants_r05m.json).
-// Round 6: a wave holds the gates of kGateHold consecutive grid-stride
-// tiles in registers and stores them together after those tiles' reads:
-// the 2-byte gate stores interleaved with the header stream cost the
-// stream (scripts/gate_probe.hip: C2's shape 0.1706 ms with per-tile
-// stores, 0.1659 with 16 tiles held, 0.1549 reading alone). With the table
-// in LDS at one workgroup per CU (launch_slab), C2 0.1837 -> 0.1674 ms,
-// 0.753 -> 0.827 of the roofline; C5 0.3448 -> 0.3424 (profiles/r06/
-// c2_ab_r06m.json, c2_ab_r06n.json, c2_ab_r06o.json: held 8 / 16 / 24 / 32
-// / 64 / 128 tiles measured; 64 and more spill).
+// Round 6: the 2-byte gate stores interleaved with the header stream cost
+// the stream (scripts/gate_probe.hip, C2's shape with no lookup: 0.1690 ms
+// with each tile's gates stored after it, 0.1649 with 16 tiles' held in
+// registers, 0.1593 / 0.1568 with 64 / 128 tiles' held in LDS, 0.1501
+// reading alone; profiles/r06/gate_probe_r06q.jsonl). A wave holds its
+// tiles' gates and stores them together after those tiles' reads:
+//  * table in LDS (C2; one workgroup per CU): in LDS, em_hold_tiles() tiles
+//    (up to 128: what the CU's LDS leaves after the table and the stages),
+//    stored 16 B per lane. C2 0.1837 (per-tile stores) -> 0.1674 (32 tiles
+//    in registers) -> 0.1615 ms (64 in LDS): 0.857 of the roofline
+//    (profiles/r06/c2_ab_r06n.json, c2_ab_r06q.json);
+//  * table in L2 / MALL (C5; two workgroups per CU): kGateHold tiles in
+//    registers (0.3448 -> 0.3424 ms; LDS holding at one workgroup per CU
+//    0.376). The register form unrolls the tile body kGateHold times: past
+//    32 it spills (64: 0.333 ms, c2_ab_r06o.json).
+__host__ __device__ constexpr uint32_t em_hold_tiles(uint32_t tab_bytes) {
+  const uint32_t stage = (kEmBlock / 64) * 4096u, per_tile = (kEmBlock / 64) * 128u;
+  const uint32_t room = tab_bytes + stage < kLdsPerCu ? kLdsPerCu - tab_bytes - stage : 0u;
+  const uint32_t h = (room / per_tile) & ~7u;
+  return h < (uint32_t)kGateHoldLds ? h : (uint32_t)kGateHoldLds;
+}
+
 template <int KW, int NCH>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
 void em_slab_kernel(EmArgs a) {
@@ -280,8 +293,8 @@ void em_slab_kernel(EmArgs a) {
       a.t.lds == kLdsTable ? ((a.t.bytes_total + 15) & ~15u) : 0u;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_off) + wid * 256;
   constexpr int kWaves = kEmBlock / 64;
+  uint4 *stage = reinterpret_cast<uint4 *>(lds + stage_off) + wid * 256;
   const uint64_t nwaves = (uint64_t)gridDim.x * kWaves;
   const uint64_t ntiles = (a.n + 63) / 64;
   const uint4 *src = reinterpret_cast<const uint4 *>(a.frames);
@@ -298,21 +311,16 @@ void em_slab_kernel(EmArgs a) {
       o[c] = u < units ? ld_stream(g + u) : make_uint4(0, 0, 0, 0);
     }
   };
-  if (t < ntiles) load_tile(t, v);
-  for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * kGateHold) {
-  uint16_t held[kGateHold];
-#pragma unroll
-  for (int h = 0; h < kGateHold; h++) {
-    const uint64_t t = t0 + (uint64_t)h * nwaves;
-    held[h] = 0;
-    if (t >= ntiles) break;
+  // tile tt (its loads in v): staged, the next tile's loads issued, this
+  // lane's slot looked up; returns its gate
+  auto tile_gate = [&](uint64_t tt) -> uint32_t {
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t u = c * 64 + lane;
       stage[stage_unit(u >> 2, u & 3)] = v[c];
     }
     lds_fence();
-    if (t + nwaves < ntiles) load_tile(t + nwaves, v);
+    if (tt + nwaves < ntiles) load_tile(tt + nwaves, v);
     uint32_t w[NCH * 4 + 2];
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
@@ -330,14 +338,56 @@ void em_slab_kernel(EmArgs a) {
     const uint32_t g = a.t.lds == kLdsTable
                            ? em_lookup<KW>(lds, a.t, k, a.default_gate)
                            : em_lookup_seq<KW>(a.t.base, a.t, k, a.default_gate);
-    held[h] = (uint16_t)g;
     lds_fence();  // this tile's stage reads retire before the next writes
+    return g;
+  };
+  if (t < ntiles) load_tile(t, v);
+  const uint32_t hl = a.t.lds == kLdsTable ? em_hold_tiles(stage_off) : 0u;
+  if (hl) {  // (a multiple of 8; the launch sized the LDS for it)
+    uint16_t *hold = reinterpret_cast<uint16_t *>(lds + stage_off + kWaves * 4096) +
+                     (size_t)wid * hl * 64;
+    const bool al16 = ((uintptr_t)a.gates & 15) == 0;
+    for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * hl) {
+#pragma unroll 1
+      for (uint32_t h = 0; h < hl; h++) {
+        const uint64_t tt = t0 + (uint64_t)h * nwaves;
+        if (tt >= ntiles) break;
+        hold[h * 64 + lane] = (uint16_t)tile_gate(tt);
+      }
+      lds_fence();
+      // the held gates, 16 B (8 gates) per lane: 8 lanes per tile
+#pragma unroll 1
+      for (uint32_t i = 0; i < hl; i += 8) {
+        const uint32_t h = i + (lane >> 3);
+        const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + (lane & 7) * 8;
+        if (idx >= a.n) continue;
+        const uint4 x = reinterpret_cast<const uint4 *>(hold + h * 64)[lane & 7];
+        if (al16 && idx + 8 <= a.n) {
+          st_stream(reinterpret_cast<uint4 *>(a.gates + idx), x);
+        } else {
+          const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+          for (int j = 0; j < 8 && idx + j < a.n; j++)
+            a.gates[idx + j] = (uint16_t)(xs[j >> 1] >> (16 * (j & 1)));
+        }
+      }
+      lds_fence();  // the region's reads retire before the next round writes
+    }
+    return;
   }
+  for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * kGateHold) {
+    uint16_t held[kGateHold];
 #pragma unroll
-  for (int h = 0; h < kGateHold; h++) {  // the held gates, streaming stores
-    const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + lane;
-    if (idx < a.n) __builtin_nontemporal_store(held[h], a.gates + idx);
-  }
+    for (int h = 0; h < kGateHold; h++) {
+      const uint64_t tt = t0 + (uint64_t)h * nwaves;
+      held[h] = 0;
+      if (tt >= ntiles) break;
+      held[h] = (uint16_t)tile_gate(tt);
+    }
+#pragma unroll
+    for (int h = 0; h < kGateHold; h++) {  // the held gates, streaming stores
+      const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + lane;
+      if (idx < a.n) __builtin_nontemporal_store(held[h], a.gates + idx);
+    }
   }
 }
 
@@ -1521,7 +1571,11 @@ hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
   const uint64_t need = (a.n + block - 1) / block;
   for (int pass = 0; pass < 2; pass++) {
     const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
-    const size_t lds = tab + stage;
+    // (em_slab_kernel's gates held in LDS beside an LDS table)
+    const size_t hold = a.t.lds == kLdsTable
+                            ? (size_t)em_hold_tiles((uint32_t)tab) * (block / 64) * 128
+                            : 0;
+    const size_t lds = tab + stage + hold;
     int pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);
     // a table in L2 / MALL: 2 workgroups per CU (16 waves) probe faster
     // than the occupancy limit (C5: 0.3444 against 0.3557 ms,

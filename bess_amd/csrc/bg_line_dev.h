@@ -48,14 +48,27 @@ __device__ __forceinline__ uint32_t line_stage_unit(uint32_t slot, uint32_t q) {
   return slot * 4 + ((q + (slot >> 2)) & 3);
 }
 
+// A reading op's lane holds kLineHold grid-stride results in registers and
+// stores them together, nontemporally, after their lookups (as the slab
+// kernels' held gates; round 6: IPLookup with tbl16 in LDS 0.2148 -> 0.1770
+// ms, 8 held 0.1810, profiles/r06/lpm_ab_r06q.json).
+constexpr int kLineHold = 16;
+
 template <class Op, int kBlock = kLineBlock>
 __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   Op::stage(lds, a);
   __syncthreads();
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < a.n;
-       idx += step) {
+  constexpr int H = Op::kWrites ? 1 : kLineHold;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.n;
+       i0 += step * H) {
+  uint16_t held[H];
+#pragma unroll
+  for (int h = 0; h < H; h++) {
+    const uint64_t idx = i0 + (uint64_t)h * step;
+    held[h] = 0;
+    if (idx >= a.n) break;
     uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * a.stride;
     const uint4 *p = reinterpret_cast<const uint4 *>(f);
     uint32_t d[16];
@@ -68,13 +81,19 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
       d[4 * c + 2] = v.z;
       d[4 * c + 3] = v.w;
     }
-    a.out[idx] = (uint16_t)Op::decide(a, lds, d, f);
+    held[h] = (uint16_t)Op::decide(a, lds, d, f);
     if constexpr (Op::kWrites) {
       uint4 *q = reinterpret_cast<uint4 *>(f);
 #pragma unroll
       for (int c = Op::c0; c < Op::c1; c++)
         q[c] = make_uint4(d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]);
     }
+  }
+#pragma unroll
+  for (int h = 0; h < H; h++) {
+    const uint64_t idx = i0 + (uint64_t)h * step;
+    if (idx < a.n) __builtin_nontemporal_store(held[h], a.out + idx);
+  }
   }
 }
 

@@ -122,6 +122,34 @@ def test_em_5tuple_vs_oracle(n_rules, n_pkts, dev):
     assert in_lds == (n_rules <= 1000)
 
 
+@pytest.mark.parametrize("n_pkts", [1, 7, 64, 64 * 8 + 7, 100003, (1 << 20) + 37])
+@pytest.mark.parametrize("gate_off", [0, 1, 3])
+def test_em_slab_held_gates(n_pkts, gate_off, dev):
+    """em_slab_kernel with its table in LDS holds the gates of up to 128
+    tiles per wave in LDS and stores them 16 B per lane (bg_kernels.hip):
+    ragged packet counts (partial tiles, a partial last 8-gate group) and
+    gate arrays not 16 B aligned (2-byte stores) land exactly where the
+    oracle's do, and nothing past n is written."""
+    keys, gates, frames = P.em_workload(1000, n_pkts, seed=0x5EED)
+    t = F.EmTable(P.em_fields_5tuple())
+    t.add_many(keys, gates)
+    em = oracle_em(P.em_fields_5tuple(), keys, gates)
+    want = np.zeros(n_pkts, np.uint16)
+    O.lib().or_em_process(em, frames.ctypes.data, 64, n_pkts, 8192, want.ctypes.data)
+    O.lib().or_em_free(em)
+    d_frames = to_dev(frames, dev)
+    for flags in (0, LB.BG_PATH_FORCE_LDS):
+        buf = torch.full((n_pkts + gate_off + 16,), 0x5A5A, dtype=torch.int16, device=dev)
+        with LB.kernel_paths(flags):
+            t.classify(d_frames, 64, n_pkts, 8192, buf[gate_off:gate_off + n_pkts])
+            torch.cuda.synchronize()
+        out = buf.cpu().numpy().view(np.uint16)
+        assert (out[gate_off:gate_off + n_pkts] == want).all(), flags
+        assert (out[:gate_off] == 0x5A5A).all() and (out[gate_off + n_pkts:] == 0x5A5A).all()
+    nbytes, in_lds = t.table_info()
+    assert in_lds
+
+
 @pytest.mark.parametrize("fields", [
     [(0, 4, 0), (6, 2, 0)],                       # 1 key word
     [(23, 1, 0), (26, 4, 0), (30, 4, 0)],         # 2 words (9 B)
