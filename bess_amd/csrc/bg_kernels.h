@@ -19,10 +19,11 @@ constexpr uint32_t kLdsTableMax = 40960;  // tables up to this size go to LDS
 // tiles whose 2-byte results a slab kernel's wave holds in registers before
 // it stores them (em_slab_kernel, line_slab_kernel; bg_kernels.hip)
 constexpr int kGateHold = 32;
-// em_slab_kernel with its table in LDS holds the gates in LDS instead: up
-// to kGateHoldLds tiles per wave, as many as the CU's LDS (kLdsPerCu, one
-// workgroup per CU) leaves after the table and the per-wave stages
-constexpr int kGateHoldLds = 128;
+// A slab kernel at one workgroup per CU (em_slab_kernel with its table in
+// LDS, line_slab_kernel for a reading op whose kSlabPerCu is 1) holds the
+// results in LDS instead: up to kGateHoldLds tiles per wave, as many as the
+// CU's LDS (kLdsPerCu) leaves after the tables and the per-wave stages
+constexpr int kGateHoldLds = 64;
 constexpr uint32_t kLdsPerCu = 163840;
 constexpr uint16_t kGateNone = 0xFFFF;
 

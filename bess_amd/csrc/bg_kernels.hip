@@ -268,7 +268,7 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 // registers, 0.1593 / 0.1568 with 64 / 128 tiles' held in LDS, 0.1501
 // reading alone; profiles/r06/gate_probe_r06q.jsonl). A wave holds its
 // tiles' gates and stores them together after those tiles' reads:
-//  * table in LDS (C2; one workgroup per CU): in LDS, em_hold_tiles() tiles
+//  * table in LDS (C2; one workgroup per CU): in LDS, lds_hold_tiles() tiles
 //    (up to 128: what the CU's LDS leaves after the table and the stages),
 //    stored 16 B per lane. C2 0.1837 (per-tile stores) -> 0.1674 (32 tiles
 //    in registers) -> 0.1615 ms (64 in LDS): 0.857 of the roofline
@@ -277,12 +277,6 @@ __device__ __forceinline__ uint32_t stage_unit(uint32_t slot, uint32_t q) {
 //    registers (0.3448 -> 0.3424 ms; LDS holding at one workgroup per CU
 //    0.376). The register form unrolls the tile body kGateHold times: past
 //    32 it spills (64: 0.333 ms, c2_ab_r06o.json).
-__host__ __device__ constexpr uint32_t em_hold_tiles(uint32_t tab_bytes) {
-  const uint32_t stage = (kEmBlock / 64) * 4096u, per_tile = (kEmBlock / 64) * 128u;
-  const uint32_t room = tab_bytes + stage < kLdsPerCu ? kLdsPerCu - tab_bytes - stage : 0u;
-  const uint32_t h = (room / per_tile) & ~7u;
-  return h < (uint32_t)kGateHoldLds ? h : (uint32_t)kGateHoldLds;
-}
 
 template <int KW, int NCH>
 __global__ __launch_bounds__(kEmBlock) __attribute__((amdgpu_num_sgpr(80)))
@@ -342,11 +336,10 @@ void em_slab_kernel(EmArgs a) {
     return g;
   };
   if (t < ntiles) load_tile(t, v);
-  const uint32_t hl = a.t.lds == kLdsTable ? em_hold_tiles(stage_off) : 0u;
+  const uint32_t hl = a.t.lds == kLdsTable ? lds_hold_tiles(stage_off) : 0u;
   if (hl) {  // (a multiple of 8; the launch sized the LDS for it)
     uint16_t *hold = reinterpret_cast<uint16_t *>(lds + stage_off + kWaves * 4096) +
                      (size_t)wid * hl * 64;
-    const bool al16 = ((uintptr_t)a.gates & 15) == 0;
     for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * hl) {
 #pragma unroll 1
       for (uint32_t h = 0; h < hl; h++) {
@@ -355,21 +348,7 @@ void em_slab_kernel(EmArgs a) {
         hold[h * 64 + lane] = (uint16_t)tile_gate(tt);
       }
       lds_fence();
-      // the held gates, 16 B (8 gates) per lane: 8 lanes per tile
-#pragma unroll 1
-      for (uint32_t i = 0; i < hl; i += 8) {
-        const uint32_t h = i + (lane >> 3);
-        const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + (lane & 7) * 8;
-        if (idx >= a.n) continue;
-        const uint4 x = reinterpret_cast<const uint4 *>(hold + h * 64)[lane & 7];
-        if (al16 && idx + 8 <= a.n) {
-          st_stream(reinterpret_cast<uint4 *>(a.gates + idx), x);
-        } else {
-          const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-          for (int j = 0; j < 8 && idx + j < a.n; j++)
-            a.gates[idx + j] = (uint16_t)(xs[j >> 1] >> (16 * (j & 1)));
-        }
-      }
+      store_held(hold, hl, t0, nwaves, lane, a.gates, a.n);
       lds_fence();  // the region's reads retire before the next round writes
     }
     return;
@@ -1573,7 +1552,7 @@ hipError_t launch_slab(K kern, EmArgs a, int num_cus, hipStream_t s, int block,
     const size_t tab = a.t.lds == kLdsTable ? (a.t.bytes_total + 15) & ~(size_t)15 : 0;
     // (em_slab_kernel's gates held in LDS beside an LDS table)
     const size_t hold = a.t.lds == kLdsTable
-                            ? (size_t)em_hold_tiles((uint32_t)tab) * (block / 64) * 128
+                            ? (size_t)lds_hold_tiles((uint32_t)tab) * (block / 64) * 128
                             : 0;
     const size_t lds = tab + stage + hold;
     int pc = occupancy(reinterpret_cast<const void *>(kern), block, lds, 1);

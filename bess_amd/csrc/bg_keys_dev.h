@@ -130,6 +130,42 @@ __device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
 }
 
+#ifndef __HIPCC_RTC__  // (the slab kernels only; not in run-time compiled code)
+// Tiles of 2-byte results a slab kernel's wave holds in LDS at one 512-
+// thread workgroup per CU (8 waves, 4 KB stage each), beside tab_bytes of
+// tables: a multiple of 8, at most kGateHoldLds; 0 when nothing fits.
+__host__ __device__ constexpr uint32_t lds_hold_tiles(uint32_t tab_bytes) {
+  constexpr uint32_t stage = 8 * 4096u, per_tile = 8 * 128u;
+  const uint32_t room = tab_bytes + stage < kLdsPerCu ? kLdsPerCu - tab_bytes - stage : 0u;
+  const uint32_t h = (room / per_tile) & ~7u;
+  return h < (uint32_t)kGateHoldLds ? h : (uint32_t)kGateHoldLds;
+}
+
+// The wave's held results (hold[h * 64 + lane] = tile t0 + h * nwaves's
+// result for slot lane, h < hl) to out[]: 16 B (8 results) per lane, 8
+// lanes per tile, streaming; 2-byte stores for a partial last group or an
+// out[] not 16 B aligned. Nothing at or past n is written.
+__device__ __forceinline__ void store_held(const uint16_t *hold, uint32_t hl, uint64_t t0,
+                                           uint64_t nwaves, int lane, uint16_t *out,
+                                           uint64_t n) {
+  const bool al16 = ((uintptr_t)out & 15) == 0;
+#pragma unroll 1
+  for (uint32_t i = 0; i < hl; i += 8) {
+    const uint32_t h = i + (lane >> 3);
+    const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + (lane & 7) * 8;
+    if (idx >= n) continue;
+    const uint4 x = reinterpret_cast<const uint4 *>(hold + h * 64)[lane & 7];
+    if (al16 && idx + 8 <= n) {
+      st_stream(reinterpret_cast<uint4 *>(out + idx), x);
+    } else {
+      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+      for (int j = 0; j < 8 && idx + j < n; j++)
+        out[idx + j] = (uint16_t)(xs[j >> 1] >> (16 * (j & 1)));
+    }
+  }
+}
+#endif
+
 // Key building (ExactMatchTable::MakeKeys exact_match_table.h:239-263 /
 // WildcardMatch::ProcessBatch wildcard_match.cc:169-197). The window
 // [win_lo, win_lo + 16*nch) of a frame is staged in registers with 16-byte

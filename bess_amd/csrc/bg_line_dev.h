@@ -100,14 +100,23 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
 // The written-back lines are stored nontemporally (streaming stores:
 // UpdateTTL 0.4093 -> 0.3879 ms, StaticNAT 0.4131 -> 0.3908 per 16 M
 // packets, scripts/variants.py linew, profiles/r05/linew_r05n.json).
-// A reading op's wave holds kGateHold tiles' results in registers and
-// stores them together (as em_slab_kernel; round 6: HashLB l4 0.1811 ->
-// 0.1635 ms at one workgroup per CU, ACL 0.2157 -> 0.1910 at two,
-// profiles/r06/legs_ab_r06o.json); a writing op stores each tile's (its
-// line stores are per tile anyway: holding measured no better).
+// A reading op's wave holds its tiles' results and stores them together
+// after those tiles' reads (as em_slab_kernel): at one workgroup per CU
+// (kSlabPerCu 1) in LDS, line_hold_tiles() tiles (HashLB l4 0.1653 ->
+// 0.1605 ms, profiles/r06/legs_ab_r06r.json), otherwise kGateHold tiles in
+// registers (HashLB l4 0.1811 -> 0.1635 ms at one workgroup per CU, ACL
+// 0.2157 -> 0.1910 at two, legs_ab_r06o.json; ACL holding in LDS at two
+// measured slower, 0.2019 against 0.1978). A writing op stores each tile's
+// (its line stores are per tile anyway: holding measured no better).
+template <class Op>
+__host__ __device__ constexpr uint32_t line_hold_tiles(uint32_t tab_bytes) {
+  return Op::kWrites || Op::kSlabPerCu != 1 ? 0u : lds_hold_tiles(tab_bytes);
+}
+
 template <class Op>
 __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args a,
                                                               uint32_t stage_words) {
+  static_assert(kLineBlock == 512, "lds_hold_tiles sizes 8 waves' stages");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   Op::stage(lds, a);
   __syncthreads();
@@ -131,22 +140,17 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
                  : make_uint4(0, 0, 0, 0);
     }
   };
-  constexpr int H = Op::kWrites ? 1 : kGateHold;
-  if (t < ntiles) load_tile(t);
-  for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * H) {
-  uint16_t held[H];
-#pragma unroll
-  for (int h = 0; h < H; h++) {
-    const uint64_t t = t0 + (uint64_t)h * nwaves;
-    held[h] = 0;
-    if (t >= ntiles) break;
+  // tile tt (its loads in v): staged, the next tile's loads issued, this
+  // lane's slot decided (a writing op's tile written back); returns the
+  // lane's result (0 past n)
+  auto tile_result = [&](uint64_t tt) -> uint32_t {
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       const uint32_t u = c * 64 + lane;
       stage[line_stage_unit(u >> 2, u & 3)] = v[c];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + nwaves < ntiles) load_tile(t + nwaves);
+    if (tt + nwaves < ntiles) load_tile(tt + nwaves);
     uint32_t d[16];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -157,10 +161,11 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
       d[4 * c + 2] = x.z;
       d[4 * c + 3] = x.w;
     }
-    const uint64_t idx = t * 64 + lane;
+    const uint64_t idx = tt * 64 + lane;
+    uint32_t r = 0;
     if (idx < a.n) {
       uint8_t *f = const_cast<uint8_t *>(a.frames) + idx * 64;
-      held[h] = (uint16_t)Op::decide(a, lds, d, f);
+      r = Op::decide(a, lds, d, f);
     }
     if constexpr (Op::kWrites) {
       // updated chunks back into this lane's slot of the stage, then the
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
         stage[line_stage_unit(lane, c)] =
             make_uint4(d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const uint64_t p0 = t * 64;
+      const uint64_t p0 = tt * 64;
       const uint64_t units = (a.n - p0 < 64 ? a.n - p0 : 64) * 4;
       uint4 *dst = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(a.frames));
 #pragma unroll
@@ -182,12 +187,43 @@ __global__ __launch_bounds__(kLineBlock) void line_slab_kernel(typename Op::Args
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return r;
+  };
+  if (t < ntiles) load_tile(t);
+  const uint32_t hl = line_hold_tiles<Op>(stage_words * 4);
+  if (hl) {  // (a multiple of 8; the launch sized the LDS for it)
+    uint16_t *hold = reinterpret_cast<uint16_t *>(lds + stage_words + kWaves * 1024) +
+                     (size_t)wid * hl * 64;
+    for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * hl) {
+#pragma unroll 1
+      for (uint32_t h = 0; h < hl; h++) {
+        const uint64_t tt = t0 + (uint64_t)h * nwaves;
+        if (tt >= ntiles) break;
+        hold[h * 64 + lane] = (uint16_t)tile_result(tt);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      store_held(hold, hl, t0, nwaves, lane, a.out, a.n);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
   }
+  // (an op at one workgroup per CU holds in LDS above unless its tables
+  // leave no room: then per-tile stores, and no unrolled register hold)
+  constexpr int H = Op::kWrites || Op::kSlabPerCu == 1 ? 1 : kGateHold;
+  for (uint64_t t0 = t; t0 < ntiles; t0 += nwaves * H) {
+    uint16_t held[H];
 #pragma unroll
-  for (int h = 0; h < H; h++) {  // streaming stores, as em_slab_kernel's gates
-    const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + lane;
-    if (idx < a.n) __builtin_nontemporal_store(held[h], a.out + idx);
-  }
+    for (int h = 0; h < H; h++) {
+      const uint64_t tt = t0 + (uint64_t)h * nwaves;
+      held[h] = 0;
+      if (tt >= ntiles) break;
+      held[h] = (uint16_t)tile_result(tt);
+    }
+#pragma unroll
+    for (int h = 0; h < H; h++) {  // streaming stores, as em_slab_kernel's gates
+      const uint64_t idx = (t0 + (uint64_t)h * nwaves) * 64 + lane;
+      if (idx < a.n) __builtin_nontemporal_store(held[h], a.out + idx);
+    }
   }
 }
 
@@ -234,7 +270,8 @@ hipError_t launch_line(const typename Op::Args &a, int num_cus, hipStream_t s) {
   if (a.stride == 64 && ((uintptr_t)a.frames & 15) == 0 &&
       !(path_flags() & kPathNoSlab)) {
     auto kern = line_slab_kernel<Op>;
-    const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096;
+    const size_t lds = tab + (size_t)(kLineBlock / 64) * 4096 +
+                       (size_t)line_hold_tiles<Op>((uint32_t)tab) * (kLineBlock / 64) * 128;
     int occ = line_occupancy(reinterpret_cast<const void *>(kern), lds);
     // 2 workgroups per CU (16 waves) rather than the occupancy limit:
     // HashLB l4 0.1906 -> 0.1809 ms, fields 0.1917 -> 0.1814, StaticNAT

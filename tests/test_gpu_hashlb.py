@@ -67,6 +67,27 @@ def test_l4_on_the_c2_slab():
     assert counts.min() > 0.9 * counts.mean()  # flows spread evenly
 
 
+@pytest.mark.parametrize("n", [1, 9, 64 * 8 + 7, 1 << 20, (1 << 21) + 37])
+@pytest.mark.parametrize("out_off", [0, 1])
+@pytest.mark.parametrize("fields", [None, [{"offset": o, "num_bytes": s}
+                                           for o, s in P.FIVE_TUPLE]])
+def test_held_results_on_dense_slots(n, out_off, fields):
+    """line_slab_kernel at one workgroup per CU (HashLB) holds up to 64
+    tiles' gates per wave in LDS and stores them 16 B per lane
+    (bg_line_dev.h): ragged counts, an output array not 16 B aligned
+    (2-byte stores), nothing written outside [0, n)"""
+    f = frames(n, 64, seed=n + out_off)
+    g = list(range(13))
+    m = HashLB(gates=g, fields=fields) if fields else HashLB(gates=g)
+    o = OM.OracleHashLB(gates=g, fields=fields) if fields else OM.OracleHashLB(gates=g)
+    d = torch.from_numpy(f.reshape(-1)).cuda()
+    buf = torch.full((n + out_off + 16,), 0x5A5A, dtype=torch.int16, device="cuda")
+    m.process_device(d, 64, n, buf[out_off:out_off + n])
+    out = buf.cpu().numpy().view(np.uint16)
+    assert (out[out_off:out_off + n] == o.process(f, 64, n)).all()
+    assert (out[:out_off] == 0x5A5A).all() and (out[out_off + n:] == 0x5A5A).all()
+
+
 FIELDSETS = [
     [{"offset": o, "num_bytes": s} for o, s in P.FIVE_TUPLE],   # 13 -> 16 B
     [{"offset": 26, "num_bytes": 8}],                            # 8 B
