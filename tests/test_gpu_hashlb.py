@@ -77,6 +77,9 @@ def test_held_results_on_dense_slots(n, out_off, fields):
     (bg_line_dev.h): ragged counts, an output array not 16 B aligned
     (2-byte stores), nothing written outside [0, n)"""
     f = frames(n, 64, seed=n + out_off)
+    # IHL 0..11: the l4 ports inside the 64 B slot (12..15 reach into the
+    # next slot, which the reference reads as whatever follows the packet)
+    f[:, 14] = (f[:, 14] & 0xF0) | (np.arange(n) % 12).astype(np.uint8)
     g = list(range(13))
     m = HashLB(gates=g, fields=fields) if fields else HashLB(gates=g)
     o = OM.OracleHashLB(gates=g, fields=fields) if fields else OM.OracleHashLB(gates=g)
