@@ -345,7 +345,13 @@ def run_em(args, rank, world, dev, torch, dist):
     torch.cuda.synchronize()
     parity = em_parity_sample(t, d_frames, d_gates, keys, gates,
                               min(n, 1 << 20), torch)
-    clock_settle(args, torch)
+    # settle with the headline's own (idempotent) launch: after ~5 launches
+    # the next ~45 run 10-15 % slow whatever the slab's history, then the
+    # kernel holds its steady state (a power-management transient, launch by
+    # launch: profiles/r06/first_launch_r06v.json); the driver's --warmup 5
+    # would otherwise time that transient (0.170-0.176 against 0.164 ms for
+    # 200 steps on one box, profiles/r06/headline_steps_r06u.json)
+    clock_settle(args, torch, step)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -1020,10 +1026,9 @@ def clock_settle(args, torch, fn=None):
     slab then run up to 14 % slow (profiles/r05/ck_timing_r05i.json): with
     the driver's --warmup 5 the timed region would measure that ramp, not
     the kernel. `fn`: the leg's own launch, for legs whose launches leave
-    their input as it was (classifiers, idempotent checksums); otherwise a
-    64 MB in-place multiply (legs that modify packets in place keep their
-    launch budget, and the headline keeps exactly its W warm-up steps of
-    its own kernel)."""
+    their input as it was (classifiers -- the headline among them, since
+    round 6 -- and idempotent checksums); otherwise a 64 MB in-place
+    multiply (legs that modify packets in place keep their launch budget)."""
     if args.settle_ms <= 0:
         return
     x = None
@@ -2021,6 +2026,8 @@ def main():
                   "64B/1500B, 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "Mpps", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "settle_ms": args.settle_ms,
+        "settle": "untimed, before the warm-up: ~settle_ms of the headline's own "
+                  "launch (it leaves the slab as it was)",
         "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded 5-tuple traffic, 50% rule hits)",
