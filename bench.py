@@ -2050,7 +2050,9 @@ def main():
         "parity": "bit-exact vs oracle on 1M-pkt sample" if r["parity"]
                   else "MISMATCH",
         # the same memory traffic without the lookup (hbm_probe slab66)
-        "measured_ceiling": shape_ceiling("slab66", r["n"], kern_ms),
+        # the fastest measured shape that writes the gates (round 6: gates
+        # held in LDS to the end; the reads alone are c2_read64)
+        "measured_ceiling": shape_ceiling("c2_lds128", r["n"], kern_ms),
         "cpu_baseline": None,
     }
     comm = None  # C5's communicator (N > 1), closed before the process group

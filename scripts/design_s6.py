@@ -42,7 +42,9 @@ with the per-shape factor calibrated below). C4's 1.25x counts the random
 64 B slot records at the x2 of a 128 B request, so it is an upper bound.
 C2's kernel took {c2['kernel_ms']} ms, which is {c2['frac']:.3f} of the
 HBM roofline and {d['measured_ceiling']['frac_of_ceiling']:.2f} of its own
-access shape measured alone (`slab66`). The 2 KB-slot legs (C4's 2 KB
+access shape measured alone with the gate stores and no lookup
+(`{d['measured_ceiling']['shape']}`, `scripts/gate_probe.hip`, {d['measured_ceiling']['probe_ms_for_these_pkts']} ms;
+the same reads without the gate stores take 0.1501 ms). The 2 KB-slot legs (C4's 2 KB
 slots, EM on 1500 B frames) run on the fastest of three slab placements
 (§8, the line's `placement`).
 
