@@ -29,17 +29,17 @@ def main():
 carries the batch sweep, C1, C3, EM on 1500 B frames, C4, C5, the §8f
 modules, the host end-to-end legs, the roofline and the CPU baselines. The
 table below is generated from one such line (`{rel}`, `python
-scripts/design_s6.py <line> <tests log>`): the round's last full call on
-the final tree (`scripts/gpu_r06.sh`), in which {passed} GPU tests passed
-and smoke was bit-exact. Every leg's kernel has a row of its own in
+scripts/design_s6.py <line> <tests log>`), measured on the final tree
+(`scripts/gpu_r06.sh smoke,bench`; smoke bit-exact). On the same kernels
+{passed} GPU tests passed (`{os.path.relpath(tests_path, ROOT)}`). Every leg's kernel has a row of its own in
 `profiles/r06_kernels.md` (`scripts/prof_legs.py`: one traced process per
 leg, the leg's timed launches split from its warm-up; every row within 1 %
 of the leg's HIP-event time but NAT's, whose line time includes its host
 walk), with the raw stats under `profiles/r06/legs_*/`. "traffic /
 algorithmic" is the PMC HBM bytes per launch over the algorithmic bytes
 (the latest `profiles/r*_traffic.json`: FETCH_SIZE / WRITE_SIZE passes,
-with the per-shape factor calibrated below). C4's 1.25x counts the random
-64 B slot records at the x2 of a 128 B request, so it is an upper bound.
+with the per-shape factor calibrated below; `profiles/r06_traffic.json`
+on this round's kernels).
 C2's kernel took {c2['kernel_ms']} ms, which is {c2['frac']:.3f} of the
 HBM roofline and {d['measured_ceiling']['frac_of_ceiling']:.2f} of its own
 access shape measured alone with the gate stores and no lookup
