@@ -22,6 +22,16 @@ def main():
     m = re.search(r"(\d+) passed", open(tests_path).read())
     passed = m.group(1) if m else "?"
     rel = os.path.relpath(line_path, ROOT)
+    pcie = {}
+    probe = os.path.join(ROOT, "profiles", "r06", "pcie_probe_r06pc.jsonl")
+    if os.path.exists(probe):
+        for ln in open(probe):
+            if ln.startswith("{"):
+                e = json.loads(ln)
+                pcie[e["shape"]] = e["GBps"]
+
+    def zc(gbps, shape):
+        return "%.2f" % (gbps / pcie[shape]) if gbps and shape in pcie else "?"
     c2 = d["roofline"]
     head = f"""## 6. Measurements (MI355X, round 6)
 
@@ -118,7 +128,12 @@ figure is compared with the CPU figure from the same call.
     The plugin's ProcessBatch time is the wait for ring slots: the frames
     are read in place over PCIe at {l4pc.get('h2d_GBps', '?')} GB/s,
     {l4pc.get('pcie_frac', '?')} of the link's 63 GB/s (PCIe Gen5 x16,
-    MI355X_MICROARCH.md). The restated reference on the same 16 workers
+    MI355X_MICROARCH.md) and {zc(l4pc.get('h2d_GBps'), 'zc_read1500r')} of what a
+    kernel reading the same layout in place reaches alone
+    (`scripts/pcie_probe.hip`: 1504 B at +512 of every 2624 B buffer,
+    {pcie.get('zc_read1500r', '?')} GB/s; 2 KB slots {pcie.get('zc_read1500', '?')}; the DMA engines'
+    pinned copies {pcie.get('h2d_copy', '?')} H2D / {pcie.get('d2h_copy', '?')} D2H,
+    `profiles/r06/pcie_probe_r06pc.jsonl`). The restated reference on the same 16 workers
     summed {l4['cpu_same_harness']['Mpps']} Mpps x 1,496 B: more than
     PCIe can carry at any rate, so at 1500 B a device-side L4Checksum
     cannot beat 16 host cores; it pays only where the frames are already
@@ -133,7 +148,8 @@ figure is compared with the CPU figure from the same call.
     {wm_p['16']}, bit-exact.
   * L4Checksum at 1500 B (1504 B H2D + 130 B D2H per packet):
     {l4_p['16']} at 16 workers, {l4pp.get('h2d_GBps', '?')} GB/s host to
-    device, {l4pp.get('pcie_frac', '?')} of PCIe.
+    device, {l4pp.get('pcie_frac', '?')} of PCIe and {zc(l4pp.get('h2d_GBps'), 'h2d_copy')} of the
+    measured pinned-copy rate.
   * The staged 16 B windows of ExactMatch / WildcardMatch use a small part
     of the link (`pcie_*` fields of the line: ExactMatch ring, 16 workers,
     {pipe['ExactMatch_64B'].get('pcie_16_threads_ring_batch1024_depth8', {}).get('pcie_frac', '?')}):
