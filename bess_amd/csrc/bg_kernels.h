@@ -154,9 +154,22 @@ constexpr uint32_t kWmWaveLds = 64 * 8 + kWmQueue * 4;
 // (after the tuple masks: the one-byte direct tuples' 256-entry tables,
 // kMaxDirect x 2 KB, read from LDS instead of one L2 request per packet)
 constexpr uint32_t kWmDirLds = 2048u * 2;
-BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
+// ... and, when the CU's LDS has room for them after all that, each wave's
+// gates of up to kWmGateHold tiles (stored together after those tiles,
+// as the slab kernels hold theirs; bg_wm_body.h)
+constexpr uint32_t kWmGateHold = 8;
+BG_HD uint64_t wm_tags_lds_base(uint32_t nbp, uint32_t kw) {
   return ((uint64_t)nbp * 4 + 15) / 16 * 16 + (uint64_t)kMaxTuples * kw * 8 + kWmDirLds +
          (uint64_t)kWmWaves * kWmWaveLds;
+}
+BG_HD uint32_t wm_hold_tiles(uint32_t nbp, uint32_t kw) {
+  const uint64_t base = wm_tags_lds_base(nbp, kw);
+  const uint64_t room = base < kLdsPerCu ? kLdsPerCu - base : 0;
+  const uint32_t h = (uint32_t)(room / ((uint64_t)kWmWaves * 128)) & ~7u;
+  return h < kWmGateHold ? h : kWmGateHold;
+}
+BG_HD uint64_t wm_tags_lds_bytes(uint32_t nbp, uint32_t kw) {
+  return wm_tags_lds_base(nbp, kw) + (uint64_t)kWmWaves * 128 * wm_hold_tiles(nbp, kw);
 }
 
 struct CkArgs {

@@ -130,7 +130,6 @@ __device__ __forceinline__ void st_stream(uint4 *p, const uint4 &v) {
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(p));
 }
 
-#ifndef __HIPCC_RTC__  // (the slab kernels only; not in run-time compiled code)
 // Tiles of 2-byte results a slab kernel's wave holds in LDS at one 512-
 // thread workgroup per CU (8 waves, 4 KB stage each), beside tab_bytes of
 // tables: a multiple of 8, at most kGateHoldLds; 0 when nothing fits.
@@ -141,14 +140,14 @@ __host__ __device__ constexpr uint32_t lds_hold_tiles(uint32_t tab_bytes) {
   return h < (uint32_t)kGateHoldLds ? h : (uint32_t)kGateHoldLds;
 }
 
-// The wave's held results (hold[h * 64 + lane] = tile t0 + h * nwaves's
-// result for slot lane, h < hl) to out[]: 16 B (8 results) per lane, 8
+// The wave's held results (hold[h * 64 + s] = tile t0 + h * nwaves's
+// result for slot s, h < hl) to out[]: 16 B (8 results) per lane, 8
 // lanes per tile, streaming; 2-byte stores for a partial last group or an
 // out[] not 16 B aligned. Nothing at or past n is written.
 __device__ __forceinline__ void store_held(const uint16_t *hold, uint32_t hl, uint64_t t0,
                                            uint64_t nwaves, int lane, uint16_t *out,
                                            uint64_t n) {
-  const bool al16 = ((uintptr_t)out & 15) == 0;
+  const bool al16 = (reinterpret_cast<unsigned long long>(out) & 15) == 0;
 #pragma unroll 1
   for (uint32_t i = 0; i < hl; i += 8) {
     const uint32_t h = i + (lane >> 3);
@@ -164,7 +163,6 @@ __device__ __forceinline__ void store_held(const uint16_t *hold, uint32_t hl, ui
     }
   }
 }
-#endif
 
 // Key building (ExactMatchTable::MakeKeys exact_match_table.h:239-263 /
 // WildcardMatch::ProcessBatch wildcard_match.cc:169-197). The window

@@ -269,7 +269,7 @@ __device__ __forceinline__ uint64_t wm_direct_value(const WmArgs &a, const uint6
 // retire in order, so the direct values, consumed in this tile, must not be
 // younger than a prefetch the next tile consumes).
 template <class Spec, int KW, int NCH, uint32_t QUEUE = kQueue, class Prefetch>
-__device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
+__device__ __forceinline__ uint32_t wm_tile(const WmArgs &a, const uint32_t *tags,
                                         const uint64_t *mlds, uint64_t *best, uint32_t *q,
                                         uint32_t nbp, int lane, uint64_t idx, bool live,
                                         const uint32_t (&w)[NCH * 4 + 2], Prefetch prefetch) {
@@ -348,8 +348,7 @@ __device__ __forceinline__ void wm_tile(const WmArgs &a, const uint32_t *tags,
       bb = comb > bb ? comb : bb;
     }
   }
-  if (live)  // (a streaming store)
-    __builtin_nontemporal_store(bb ? (uint16_t)bb : (uint16_t)a.default_gate, a.gates + idx);
+  return bb ? (uint32_t)(uint16_t)bb : a.default_gate;
 }
 
 // stage the tag words and the tuple masks (every thread of the workgroup);
@@ -380,6 +379,9 @@ __device__ __forceinline__ uint64_t *wm_stage_tags(const WmArgs &a, uint8_t *lds
 }
 
 
+// Round 6: the gates of kWmGateHold tiles are held in LDS and stored
+// together (C4 on the header slab 0.1502 -> 0.1435 ms, mean of 4 runs each,
+// profiles/r06/wm_hold_ab_r06wm2.json; 16 tiles no better than 8).
 // PAIR 1: the pair loads (lanes 2m / 2m+1 load slot m's two window chunks,
 // one 32 B request per slot); 0: one slot per lane, NCH chunks.
 template <class Spec, int KW, int NCH, int PAIR>
@@ -407,7 +409,17 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
     if (t < ntiles && t * 64 + lane < a.n)
       load_window<NCH>(a.frames + (t * 64 + lane) * a.stride, a.fp, wn);
   }
-  for (; t < ntiles; t += nw) {
+  // the gates: held in LDS for hl tiles and stored 16 B per lane after
+  // them (wm_hold_tiles: when the CU's LDS has room), else each tile's
+  // stored after it (streaming)
+  const uint32_t hl = wm_hold_tiles(nbp, KW);
+  uint16_t *hold = reinterpret_cast<uint16_t *>(lds + wm_tags_lds_base(nbp, KW)) +
+                   (size_t)wid * hl * 64;
+  const uint32_t per_round = hl ? hl : 1u;
+  for (uint64_t t0 = t; t0 < ntiles; t0 += nw * per_round) {
+  for (uint32_t hh = 0; hh < per_round; hh++) {
+    t = t0 + (uint64_t)hh * nw;
+    if (t >= ntiles) break;
     const uint64_t idx = t * 64 + (PAIR ? pair_slot(lane) : (uint64_t)lane);
     const bool live = idx < a.n;
     uint32_t w[NCH * 4 + 2];
@@ -418,7 +430,7 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
       for (int i = 0; i < NCH * 4 + 2; i++) w[i] = wn[i];
     }
     // the next tile's header window
-    wm_tile<Spec, KW, NCH>(a, tags, mlds, best, q, nbp, lane, idx, live, w, [&]() {
+    const uint32_t g = wm_tile<Spec, KW, NCH>(a, tags, mlds, best, q, nbp, lane, idx, live, w, [&]() {
       if constexpr (PAIR) {
         if (t + nw < ntiles)
           load_pair(a.frames, a.n, (t + nw) * 64, lane, a.fp.win_lo, (uint32_t)a.stride, wn);
@@ -428,6 +440,16 @@ __device__ __forceinline__ void wm_tags_body(const WmArgs &a) {
           load_window<NCH>(a.frames + nidx * a.stride, a.fp, wn);
       }
     });
+    if (hl)
+      hold[hh * 64 + (uint32_t)(idx - t * 64)] = (uint16_t)g;
+    else if (live)  // (a streaming store)
+      __builtin_nontemporal_store((uint16_t)g, a.gates + idx);
+  }
+  if (hl) {
+    lds_fence();
+    store_held(hold, hl, t0, nw, lane, a.gates, a.n);
+    lds_fence();  // the region's reads retire before the next round writes
+  }
   }
 }
 

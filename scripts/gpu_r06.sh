@@ -64,8 +64,8 @@ if has c2ab; then  # the headline kernel: product vs $C2LIBS, interleaved
     done
   done
 fi
-if has legab; then  # bench legs $ABLEGS: product vs $LEGLIBS, interleaved
-  for rep in 1 2; do
+if has legab; then  # bench legs $ABLEGS: product vs $LEGLIBS, interleaved ($REPS times)
+  for rep in $(seq 1 ${REPS:-2}); do
     for L in product $LEGLIBS; do
       if [ "$L" = product ]; then LA=""; else LA="--lib scripts/bin/libbessgpu_$L.so"; fi
       for W in $ABLEGS; do

@@ -353,6 +353,36 @@ def test_wm_vs_oracle(n_rules, n_pkts, tags, dev):
     assert (want != 77).mean() > 0.3
 
 
+@pytest.mark.parametrize("n_rules", [100000, 200000])
+@pytest.mark.parametrize("n_pkts", [1, 7, 64 * 16 + 9, (1 << 20) + 37])
+@pytest.mark.parametrize("gate_off", [0, 1])
+def test_wm_tags_held_gates(n_rules, n_pkts, gate_off, dev):
+    """the tag-word kernels hold each wave's gates of up to 8 tiles in LDS
+    when the CU's LDS has room after the tag words (wm_hold_tiles) and store
+    them 16 B per lane: ragged counts, gate arrays not 16 B aligned, both
+    WildcardMatch forms (run-time compiled and ahead of time), and nothing
+    written outside [0, n)"""
+    rk, rm, prio, gates, frames, _ = P.wm_workload(n_rules, n_pkts, seed=n_rules + 7,
+                                                  stride=64, sizes=((60, 1),))
+    t = F.WmTable(P.FIVE_TUPLE)
+    for k, m, p, g in zip(rk, rm, prio, gates):
+        t.add(k.tobytes(), m.tobytes(), int(p), int(g))
+    wm = oracle_wm(P.FIVE_TUPLE, rk, rm, prio, gates)
+    want = np.zeros(n_pkts, np.uint16)
+    O.lib().or_wm_process(wm, frames.ctypes.data, 64, n_pkts, 77, want.ctypes.data)
+    O.lib().or_wm_free(wm)
+    d_frames = to_dev(frames, dev)
+    wm_jit_ready(t)
+    for flags in (0, LB.BG_PATH_WM_NO_JIT):
+        buf = torch.full((n_pkts + gate_off + 16,), 0x5A5A, dtype=torch.int16, device=dev)
+        with LB.kernel_paths(flags):
+            t.classify(d_frames, 64, n_pkts, 77, buf[gate_off:gate_off + n_pkts])
+            torch.cuda.synchronize()
+        out = buf.cpu().numpy().view(np.uint16)
+        assert (out[gate_off:gate_off + n_pkts] == want).all(), flags
+        assert (out[:gate_off] == 0x5A5A).all() and (out[gate_off + n_pkts:] == 0x5A5A).all()
+
+
 def test_wm_direct_tuples_vs_oracle(dev):
     """Tuples whose masks cover one or two key bytes -- whole and partial
     bytes -- are direct tuples of the tag-word image (bg_wm.hip, WmArgs::
