@@ -125,7 +125,7 @@ def test_em_5tuple_vs_oracle(n_rules, n_pkts, dev):
 @pytest.mark.parametrize("n_pkts", [1, 7, 64, 64 * 8 + 7, 100003, (1 << 20) + 37])
 @pytest.mark.parametrize("gate_off", [0, 1, 3])
 def test_em_slab_held_gates(n_pkts, gate_off, dev):
-    """em_slab_kernel with its table in LDS holds the gates of up to 128
+    """em_slab_kernel with its table in LDS holds the gates of up to 64
     tiles per wave in LDS and stores them 16 B per lane (bg_kernels.hip):
     ragged packet counts (partial tiles, a partial last 8-gate group) and
     gate arrays not 16 B aligned (2-byte stores) land exactly where the
