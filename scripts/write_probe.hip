@@ -1,0 +1,102 @@
+// write_probe.hip -- Rewrite's store shape alone (the 64 B template written
+// into every 192 B slot at +128, plus 2 B data_off and 4 B length per
+// packet), against plain streaming writes, over 16 M slots: the ceiling
+// bench.py's Rewrite leg is placed against. Not part of
+// libbessgpu.
+//
+//   hipcc --offload-arch=gfx950 -O3 -o scripts/bin/write_probe scripts/write_probe.hip
+//   ./write_probe [Mslots]       (16 by default)
+//
+// Shapes (4 lanes per packet, 16 B per lane, grid-strided as rewrite_kernel):
+//   tmpl      the 64 B at +128 of each 192 B slot (one full line in three)
+//   tmpl_hl   + the 2 B data_off and 4 B length arrays (Rewrite's stores)
+//   dense64   64 B per packet, contiguous (a plain streaming write)
+//   dense192  the whole 192 B slot (contiguous; 3x the bytes)
+// Each: best of 5 x 10 launches per blocks-per-CU setting, GB/s of the
+// bytes the shape writes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                  \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+// MODE 0 tmpl, 1 tmpl_hl, 2 dense64, 3 dense192
+template <int MODE>
+__global__ __launch_bounds__(256) void wr(uint4 *slots, uint16_t *head, uint32_t *len,
+                                          size_t n) {
+  constexpr int kChunks = MODE == 3 ? 12 : 4;  // 16 B chunks per packet
+  constexpr int kStride = MODE == 2 ? 4 : 12;  // 16 B units per slot
+  constexpr int kOff = MODE <= 1 ? 8 : 0;      // +128 B
+  const size_t lane_g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t lanes = (size_t)gridDim.x * blockDim.x;
+  const uint4 v = make_uint4((uint32_t)lane_g, 1, 2, 3);
+  for (size_t u = lane_g; u < n * kChunks; u += lanes) {
+    const size_t i = u / kChunks, c = u % kChunks;
+    slots[i * kStride + kOff + c] = v;
+    if (MODE == 1 && c == 0) {
+      head[i] = 128;
+      len[i] = 60;
+    }
+  }
+}
+
+int main(int argc, char **argv) {
+  const size_t n = (size_t)(argc > 1 ? atoi(argv[1]) : 16) << 20;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  uint4 *slots = nullptr;
+  uint16_t *head = nullptr;
+  uint32_t *len = nullptr;
+  CK(hipMalloc(&slots, n * 192));
+  CK(hipMalloc(&head, n * 2));
+  CK(hipMalloc(&len, n * 4));
+  CK(hipMemset(slots, 0, n * 192));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  struct S {
+    const char *name;
+    void (*k)(uint4 *, uint16_t *, uint32_t *, size_t);
+    double bytes_per_pkt;
+  } shapes[] = {{"tmpl", wr<0>, 64}, {"tmpl_hl", wr<1>, 70}, {"dense64", wr<2>, 64},
+                {"dense192", wr<3>, 192}};
+  for (auto &sh : shapes) {
+    for (int bpc : {2, 4, 8}) {
+      const int blocks = cus * bpc;
+      auto launch = [&] {
+        hipLaunchKernelGGL(sh.k, dim3(blocks), dim3(256), 0, 0, slots, head, len, n);
+      };
+      for (int w = 0; w < 10; w++) launch();
+      CK(hipDeviceSynchronize());
+      std::vector<float> ms;
+      for (int r = 0; r < 5; r++) {
+        CK(hipEventRecord(e0, 0));
+        for (int k = 0; k < 10; k++) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t / 10);
+      }
+      const float best = *std::min_element(ms.begin(), ms.end());
+      printf("{\"shape\": \"%s\", \"blocks_per_cu\": %d, \"ms\": %.4f, \"GBps\": %.1f, "
+             "\"Gpkts_per_s\": %.2f, \"pkts\": %zu}\n",
+             sh.name, bpc, best, n * sh.bytes_per_pkt / (best * 1e-3) / 1e9,
+             n / (best * 1e-3) / 1e9, n);
+      fflush(stdout);
+    }
+  }
+  CK(hipGetLastError());
+  return 0;
+}
