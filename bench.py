@@ -1027,13 +1027,18 @@ def clock_settle(args, torch, fn=None):
     the driver's --warmup 5 the timed region would measure that ramp, not
     the kernel. `fn`: the leg's own launch, for legs whose launches leave
     their input as it was (classifiers -- the headline among them, since
-    round 6 -- and idempotent checksums); otherwise a 64 MB in-place
-    multiply (legs that modify packets in place keep their launch budget)."""
+    round 6 -- and idempotent checksums); otherwise an in-place multiply
+    over 1 GB (legs that modify packets in place keep their launch budget).
+    The work must stream HBM: after ~100 ms of it, launches 5-25 of C2's
+    kernel ran 0.1667-0.1684 ms against 0.1652-0.1654 after its own
+    launches, 0.1723-0.1738 after the same multiply over 64 MB (which stays
+    in the Infinity Cache; the round-5 settle) and 0.185-0.193 after none
+    (profiles/r06/first_launch_settle_r06ad.json)."""
     if args.settle_ms <= 0:
         return
     x = None
     if fn is None:
-        x = torch.ones(16 << 20, dtype=torch.float32, device="cuda")
+        x = torch.ones(256 << 20, dtype=torch.float32, device="cuda")
         fn = lambda: x.mul_(1.0)  # noqa: E731
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < args.settle_ms:

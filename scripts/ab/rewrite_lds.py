@@ -3,6 +3,7 @@
 # instead of two dependent L2 reads. RW_BPC (8) caps workgroups per CU.
 import os
 BPC = int(os.environ.get("RW_BPC", "8"))
+U = int(os.environ.get("RW_UNROLL", "1"))  # packets per thread per pass, loads first
 p = 'bess_amd/csrc/bg_rewrite.hip'
 s = open(p).read()
 a = s[s.index("__global__ __launch_bounds__(kRwBlock) void rewrite_kernel(RewriteArgs a) {"):
@@ -23,7 +24,34 @@ b = """__global__ __launch_bounds__(kRwBlock) void rewrite_kernel(RewriteArgs a)
   uint64_t i = lane_g >> a.lpp_log2;
   uint32_t t = (uint32_t)((a.start + i) % a.ntempl);
   const uint32_t tstep = (uint32_t)(step % a.ntempl);
-  for (; i < a.n; i += step, t = t + tstep >= a.ntempl ? t + tstep - a.ntempl : t + tstep) {
+  auto adv = [&](uint32_t x) { return x + tstep >= a.ntempl ? x + tstep - a.ntempl : x + tstep; };
+  if (a.units <= lpp) {  // one chunk per lane per packet: U packets per pass, loads first
+    constexpr int U = @U@;
+    for (; i < a.n; i += step * U) {
+      uint32_t sz[U];
+      uint4 x[U];
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        sz[k] = lsz[t];
+        x[k] = lt[(size_t)t * a.units + (sub < a.units ? sub : 0)];
+        t = adv(t);
+      }
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        const uint64_t ii = i + (uint64_t)k * step;
+        if (ii >= a.n) break;
+        const uint32_t chunks = ((sz[k] + 31) & ~31u) / 16;
+        uint4 *dst = reinterpret_cast<uint4 *>(a.slots + ii * a.stride + a.headroom);
+        if (sub < chunks) dst[sub] = x[k];
+        if (sub == 0) {
+          a.head[ii] = (uint16_t)a.headroom;
+          a.len[ii] = sz[k];
+        }
+      }
+    }
+    return;
+  }
+  for (; i < a.n; i += step, t = adv(t)) {
     const uint32_t size = lsz[t];
     const uint32_t chunks = ((size + 31) & ~31u) / 16;
     const uint4 *src = lt + (size_t)t * a.units;
@@ -36,7 +64,7 @@ b = """__global__ __launch_bounds__(kRwBlock) void rewrite_kernel(RewriteArgs a)
   }
 }
 
-"""
+""".replace("@U@", str(U))
 s = s.replace(a, b)
 a = """  const uint64_t cap = (uint64_t)num_cus * 8;
   if (blocks > cap) blocks = cap;

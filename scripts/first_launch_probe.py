@@ -8,7 +8,8 @@ own HIP events, 300 launches, for a slab that is
   devcopy  uploaded, then rewritten by a device copy (slab -> new slab),
   fresh    a new allocation filled by a device kernel (never crossed PCIe).
 Each case has its own allocation; the order is interleaved twice.
-Usage: python scripts/first_launch_probe.py OUT.json"""
+Usage: python scripts/first_launch_probe.py OUT.json [settle]
+(settle: one slab, each kind of untimed settle work before the launches)"""
 import json
 import os
 import sys
@@ -60,6 +61,31 @@ def main():
         print(json.dumps(r), flush=True)
         res["cases"].append(r)
 
+    if len(sys.argv) > 2 and sys.argv[2] == "settle":
+        # the slab kept; 300 ms of host idle, then ~100 ms of untimed device
+        # work of each kind before the 300 launches: none, bench.py's
+        # multiply over 64 MB (it stays in the 256 MB Infinity Cache), the
+        # same over 1 GB (through HBM), the headline's own launch
+        d = host.to(dev)
+        x64 = torch.ones(16 << 20, dtype=torch.float32, device=dev)
+        x1g = torch.ones(256 << 20, dtype=torch.float32, device=dev)
+        works = {"none": None, "mul64m": lambda: x64.mul_(1.0),
+                 "mul1g": lambda: x1g.mul_(1.0),
+                 "own": lambda: t.classify(d, 64, n, 8192, d_gates)}
+        for rep in (1, 2):
+            for name, fn in works.items():
+                torch.cuda.synchronize()
+                time.sleep(0.3)
+                if fn is not None:
+                    t0 = time.perf_counter()
+                    while time.perf_counter() - t0 < 0.1:
+                        for _ in range(8):
+                            fn()
+                        torch.cuda.synchronize()
+                run(d, "settle_" + name, rep)
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1)
+        return
     for rep in (1, 2):
         for name in ("h2d", "h2d_idle", "devread", "devcopy", "fresh"):
             if name == "fresh":
