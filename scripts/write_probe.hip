@@ -12,6 +12,8 @@
 //   tmpl_hl   + the 2 B data_off and 4 B length arrays (Rewrite's stores)
 //   dense64   64 B per packet, contiguous (a plain streaming write)
 //   dense192  the whole 192 B slot (contiguous; 3x the bytes)
+//   kernel    rewrite_kernel's body itself: 4 templates of 60 B read from a
+//             4 x 1536 B buffer, sizes from an array, the round-robin turn
 // Each: best of 5 x 10 launches per blocks-per-CU setting, GB/s of the
 // bytes the shape writes.
 #include <hip/hip_runtime.h>
@@ -51,6 +53,32 @@ __global__ __launch_bounds__(256) void wr(uint4 *slots, uint16_t *head, uint32_t
   }
 }
 
+// rewrite_kernel's loop (bess_amd/csrc/bg_rewrite.hip) on the probe's slab
+__global__ __launch_bounds__(256) void wr_kernel(uint4 *slots, uint16_t *head, uint32_t *len,
+                                                 size_t n, const uint8_t *tmpl,
+                                                 const uint16_t *tsize) {
+  constexpr uint32_t ntempl = 4, lpp_log2 = 2, headroom = 128, stride = 192;
+  const uint32_t lpp = 1u << lpp_log2;
+  const uint64_t lane_g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t step = ((uint64_t)gridDim.x * 256) >> lpp_log2;
+  const uint32_t sub = (uint32_t)lane_g & (lpp - 1);
+  uint64_t i = lane_g >> lpp_log2;
+  uint32_t t = (uint32_t)(i % ntempl);
+  const uint32_t tstep = (uint32_t)(step % ntempl);
+  uint8_t *base = reinterpret_cast<uint8_t *>(slots);
+  for (; i < n; i += step, t = t + tstep >= ntempl ? t + tstep - ntempl : t + tstep) {
+    const uint32_t size = tsize[t];
+    const uint32_t chunks = ((size + 31) & ~31u) / 16;
+    const uint4 *src = reinterpret_cast<const uint4 *>(tmpl + (uint64_t)t * 1536);
+    uint4 *dst = reinterpret_cast<uint4 *>(base + i * stride + headroom);
+    for (uint32_t c = sub; c < chunks; c += lpp) dst[c] = src[c];
+    if (sub == 0) {
+      head[i] = (uint16_t)headroom;
+      len[i] = size;
+    }
+  }
+}
+
 int main(int argc, char **argv) {
   const size_t n = (size_t)(argc > 1 ? atoi(argv[1]) : 16) << 20;
   int cus = 0;
@@ -62,6 +90,18 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&head, n * 2));
   CK(hipMalloc(&len, n * 4));
   CK(hipMemset(slots, 0, n * 192));
+  uint8_t *tmpl = nullptr;
+  uint16_t *tsize = nullptr;
+  CK(hipMalloc(&tmpl, 4 * 1536));
+  CK(hipMalloc(&tsize, 4 * 2));
+  {
+    std::vector<uint8_t> h(4 * 1536, 0);
+    for (int t = 0; t < 4; t++)
+      for (int b = 0; b < 60; b++) h[t * 1536 + b] = (uint8_t)(t * 61 + b);
+    const uint16_t sz[4] = {60, 60, 60, 60};
+    CK(hipMemcpy(tmpl, h.data(), h.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(tsize, sz, sizeof sz, hipMemcpyHostToDevice));
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -70,12 +110,17 @@ int main(int argc, char **argv) {
     void (*k)(uint4 *, uint16_t *, uint32_t *, size_t);
     double bytes_per_pkt;
   } shapes[] = {{"tmpl", wr<0>, 64}, {"tmpl_hl", wr<1>, 70}, {"dense64", wr<2>, 64},
-                {"dense192", wr<3>, 192}};
+                {"dense192", wr<3>, 192},
+                {"kernel", nullptr, 70}};
   for (auto &sh : shapes) {
     for (int bpc : {2, 4, 8}) {
       const int blocks = cus * bpc;
       auto launch = [&] {
-        hipLaunchKernelGGL(sh.k, dim3(blocks), dim3(256), 0, 0, slots, head, len, n);
+        if (sh.k)
+          hipLaunchKernelGGL(sh.k, dim3(blocks), dim3(256), 0, 0, slots, head, len, n);
+        else
+          hipLaunchKernelGGL(wr_kernel, dim3(blocks), dim3(256), 0, 0, slots, head, len, n,
+                             (const uint8_t *)tmpl, (const uint16_t *)tsize);
       };
       for (int w = 0; w < 10; w++) launch();
       CK(hipDeviceSynchronize());
