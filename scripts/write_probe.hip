@@ -12,6 +12,8 @@
 //   tmpl_hl   + the 2 B data_off and 4 B length arrays (Rewrite's stores)
 //   dense64   64 B per packet, contiguous (a plain streaming write)
 //   dense192  the whole 192 B slot (contiguous; 3x the bytes)
+//   tile      tmpl_hl with a wave per 64 consecutive packets: 4 rounds of 16
+//             packets' 64 B, then data_off / length of all 64 as whole lines
 //   kernel    rewrite_kernel's body itself: 4 templates of 60 B read from a
 //             4 x 1536 B buffer, sizes from an array, the round-robin turn
 // Each: best of 5 x 10 launches per blocks-per-CU setting, GB/s of the
@@ -49,6 +51,26 @@ __global__ __launch_bounds__(256) void wr(uint4 *slots, uint16_t *head, uint32_t
     if (MODE == 1 && c == 0) {
       head[i] = 128;
       len[i] = 60;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void wr_tile(uint4 *slots, uint16_t *head, uint32_t *len,
+                                               size_t n) {
+  const int lane = threadIdx.x & 63;
+  const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  const uint4 v = make_uint4((uint32_t)lane, 1, 2, 3);
+  for (size_t tile = wave; tile * 64 < n; tile += waves) {
+    const size_t p0 = tile * 64;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const size_t i = p0 + r * 16 + (lane >> 2);
+      if (i < n) slots[i * 12 + 8 + (lane & 3)] = v;
+    }
+    if (p0 + lane < n) {
+      head[p0 + lane] = 128;
+      len[p0 + lane] = 60;
     }
   }
 }
@@ -111,7 +133,7 @@ int main(int argc, char **argv) {
     double bytes_per_pkt;
   } shapes[] = {{"tmpl", wr<0>, 64}, {"tmpl_hl", wr<1>, 70}, {"dense64", wr<2>, 64},
                 {"dense192", wr<3>, 192},
-                {"kernel", nullptr, 70}};
+                {"tile", wr_tile, 70}, {"kernel", nullptr, 70}};
   for (auto &sh : shapes) {
     for (int bpc : {2, 4, 8}) {
       const int blocks = cus * bpc;
