@@ -303,6 +303,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_image_kernel(
 
 // any stride: lane = packet, header bytes straight from HBM
 __global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.nmiss_next) *a.nmiss_next = 0;
   const uint64_t step = (uint64_t)gridDim.x * kNatBlock;
   const uint64_t n_pad = (a.n + 63) & ~63ull;  // whole waves reach the ballot
   for (uint64_t i = (uint64_t)blockIdx.x * kNatBlock + threadIdx.x; i < n_pad;
@@ -317,6 +318,7 @@ __global__ __launch_bounds__(kNatBlock) void dnat_fused_kernel(DnatArgs a) {
 constexpr int kNatSlabBlock = 512;
 // The tile is written back with streaming stores (as the line ops').
 __global__ __launch_bounds__(kNatSlabBlock) void dnat_fused_slab_kernel(DnatArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.nmiss_next) *a.nmiss_next = 0;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   constexpr int kWaves = kNatSlabBlock / 64;

@@ -228,11 +228,19 @@ struct bg_dnat {
   size_t d_n = 0;
   uint64_t *d_up = nullptr;  // update lists (ensure_up)
   size_t d_upcap = 0;
+  // Forward-miss counters: two device words used in turn, each launch
+  // zeroing the other (no memset node between calls), and the count read
+  // back into pinned host memory. `miss_stale`: a call ended between its
+  // launch and its read-back, so the turn's word may not be zero.
+  uint32_t *h_nmiss = nullptr;
+  uint32_t miss_turn = 0;
+  bool miss_stale = false;
   std::mutex mu;
   ~bg_dnat() {
     for (void *p : {(void *)d_ent, (void *)d_ts, (void *)d_keys, (void *)d_res,
                     (void *)d_nmiss, (void *)d_mres, (void *)d_up, (void *)d_meps})
       if (p) (void)hipFree(p);
+    if (h_nmiss) (void)hipHostFree(h_nmiss);
   }
 
   // HashTable::Insert; rev: a reverse entry (external endpoint -> internal)
@@ -378,7 +386,11 @@ struct bg_dnat {
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_res), d_n * 4));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_mres), d_n * 4));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_meps), d_n * 8));
-    if (!d_nmiss) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_nmiss), 4));
+    if (!d_nmiss) {
+      HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d_nmiss), 8));
+      HIP_TRY(hipMemset(d_nmiss, 0, 8));
+    }
+    if (!h_nmiss) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_nmiss), 4));
     return 0;
   }
 
@@ -545,20 +557,24 @@ int bg_dnat_process(bg_dnat *h, void *d_frames, size_t stride, size_t n,
   for (uint32_t j = 0; j < a.next; j++) a.ext[j] = h->ext[j];
   a.keys = h->d_keys;
   a.res = h->d_res;
-  a.nmiss = h->d_nmiss;
+  a.nmiss = h->d_nmiss + h->miss_turn;
+  a.nmiss_next = h->d_nmiss + (h->miss_turn ^ 1);
   a.ent = h->d_ent;
   a.ts = h->d_ts;
   a.nent = h->ent_ep.size();
   a.out = d_out;
-  HIP_TRY(hipMemsetAsync(h->d_nmiss, 0, 4, s));
+  if (h->miss_stale) HIP_TRY(hipMemsetAsync(a.nmiss, 0, 4, s));
+  h->miss_stale = true;
   const int ncu = num_cus(dev);
   // final hits stamped on the device; forward misses and forward hits on
   // expired mappings listed (reverse traffic never creates a mapping)
   HIP_TRY(launch_dnat_fused(a, ncu, s));
-  uint32_t nlist = 0;
   if (dir == 0)
-    HIP_TRY(hipMemcpyAsync(&nlist, h->d_nmiss, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h->h_nmiss, a.nmiss, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  const uint32_t nlist = dir == 0 ? *h->h_nmiss : 0;
+  h->miss_turn ^= 1;  // the launch zeroed the other word
+  h->miss_stale = false;
   if (nlist == 0) return 0;
   // the listed packets in packet order on the host (DoProcessBatch 321-363)
   std::vector<uint32_t> idx(nlist), ent(nlist);

@@ -323,6 +323,7 @@ struct DnatArgs {
   uint64_t *keys;    // per packet: the endpoint key
   uint32_t *res;     // per packet: entry / kDnatMiss / kDnatInvalid
   uint32_t *nmiss;   // forward misses of the batch
+  uint32_t *nmiss_next;  // the next call's counter: zeroed by this launch
   const uint64_t *ent;  // per entry: translated endpoint
   uint64_t *ts;      // per entry: last_refresh
   uint64_t nent;     // entries the two arrays hold
