@@ -42,7 +42,7 @@ LEGS = {
     "ttl": ("--only ttl --no-cpu", "TtlOp", ("ms_per_step",), 10),
     "nat": ("--only nat --no-cpu", "NatOp", ("ms_per_step",), 10),
     "dnat": ("--only dnat --no-cpu --no-churn", "dnat_fused_slab_kernel", ("ms_per_step",), 10),
-    "rewrite": ("--only rewrite --no-cpu", "rewrite_kernel", ("ms_per_step",), 10),
+    "rewrite": ("--only rewrite --no-cpu", "rewrite_kernel", ("ms_per_step",), 100),
 }
 
 
