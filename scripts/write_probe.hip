@@ -14,6 +14,8 @@
 //   dense192  the whole 192 B slot (contiguous; 3x the bytes)
 //   tile      tmpl_hl with a wave per 64 consecutive packets: 4 rounds of 16
 //             packets' 64 B, then data_off / length of all 64 as whole lines
+//   split     tmpl's grid-strided template stores first, then data_off /
+//             length grid-strided a lane per packet (whole lines), in one launch
 //   kernel    rewrite_kernel's body itself: 4 templates of 60 B read from a
 //             4 x 1536 B buffer, sizes from an array, the round-robin turn
 // Each: best of 5 x 10 launches per blocks-per-CU setting, GB/s of the
@@ -75,6 +77,18 @@ __global__ __launch_bounds__(256) void wr_tile(uint4 *slots, uint16_t *head, uin
   }
 }
 
+__global__ __launch_bounds__(256) void wr_split(uint4 *slots, uint16_t *head, uint32_t *len,
+                                                size_t n) {
+  const size_t lane_g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t lanes = (size_t)gridDim.x * blockDim.x;
+  const uint4 v = make_uint4((uint32_t)lane_g, 1, 2, 3);
+  for (size_t u = lane_g; u < n * 4; u += lanes) slots[(u >> 2) * 12 + 8 + (u & 3)] = v;
+  for (size_t i = lane_g; i < n; i += lanes) {
+    head[i] = 128;
+    len[i] = 60;
+  }
+}
+
 // rewrite_kernel's loop (bess_amd/csrc/bg_rewrite.hip) on the probe's slab
 __global__ __launch_bounds__(256) void wr_kernel(uint4 *slots, uint16_t *head, uint32_t *len,
                                                  size_t n, const uint8_t *tmpl,
@@ -133,7 +147,7 @@ int main(int argc, char **argv) {
     double bytes_per_pkt;
   } shapes[] = {{"tmpl", wr<0>, 64}, {"tmpl_hl", wr<1>, 70}, {"dense64", wr<2>, 64},
                 {"dense192", wr<3>, 192},
-                {"tile", wr_tile, 70}, {"kernel", nullptr, 70}};
+                {"tile", wr_tile, 70}, {"split", wr_split, 70}, {"kernel", nullptr, 70}};
   for (auto &sh : shapes) {
     for (int bpc : {2, 4, 8}) {
       const int blocks = cus * bpc;
