@@ -44,8 +44,8 @@ scripts/design_s6.py <line> <tests log>`), measured on the final tree
 {passed} GPU tests passed (`{os.path.relpath(tests_path, ROOT)}`). Every leg's kernel has a row of its own in
 `profiles/r06_kernels.md` (`scripts/prof_legs.py`: one traced process per
 leg, the leg's timed launches split from its warm-up; every row within 1 %
-of the leg's HIP-event time but NAT's, whose line time includes its host
-walk), with the raw stats under `profiles/r06/legs_*/`. "traffic /
+of the leg's HIP-event time but NAT's, whose line time includes the
+synchronous miss-count read-back of every call), with the raw stats under `profiles/r06/legs_*/`. "traffic /
 algorithmic" is the PMC HBM bytes per launch over the algorithmic bytes
 (the latest `profiles/r*_traffic.json`: FETCH_SIZE / WRITE_SIZE passes,
 with the per-shape factor calibrated below; `profiles/r06_traffic.json`
