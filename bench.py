@@ -1308,7 +1308,7 @@ def run_rewrite(args, dev, torch):
     out = {"workload": "Rewrite: 4 templates of 60B round robin into %d resident "
                        "192B packet slots" % n, "pkts": n, "ms_per_step": round(ms, 4),
            "Mpps": round(n / (ms * 1e-3) / 1e6, 1),
-           "roofline": _roof(70, n, ms),
+           "roofline": _roof(70, n, ms, "rewrite"),
            "parity": "bit-exact (slots, data_off, lengths) vs oracle on %d pkts" % k
                      if parity else "MISMATCH"}
     if not args.no_cpu:
