@@ -128,18 +128,27 @@ def test_oracle_translation_keeps_checksums_valid():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stride", [STRIDE, 64])
-def test_gpu_batches_vs_oracle(stride):
+@pytest.mark.parametrize("stride,ihl_mode", [(STRIDE, "mixed"), (64, "mixed"), (64, "ihl5")])
+def test_gpu_batches_vs_oracle(stride, ihl_mode):
     """stride 64 runs the slab kernel (dnat_fused_slab_kernel); batches
     where no mapping can expire take the fused path (new flows listed and
     walked on the host, mixed with hits), the batch 301 s later the
-    classify-then-decide path"""
-    import functools
+    classify-then-decide path. ihl_mode "mixed": 20 % of frames carry IP
+    options (IHL 6-7), so nearly every 64-packet tile has one; "ihl5": IHL 5
+    everywhere but one packet in every seventh tile (a tile-uniform fast
+    path for option-free headers was measured, scripts/ab/nat_reg_slot.py,
+    and would be told apart by exactly this mix)"""
     import torch
     from bess_amd.modules import NAT
     rng = np.random.default_rng(11)
     m, o = NAT(ext_addrs=EXT, seed=0xABC), OM.OracleNAT(ext_addrs=EXT, seed=0xABC)
-    frames_ = functools.partial(frames, stride=stride)
+
+    def frames_(*fa, **kw):
+        ihl = None
+        if ihl_mode == "ihl5":
+            ihl = np.full(len(fa[0]), 5)
+            ihl[np.arange(len(ihl)) % 448 == 3] = 6
+        return frames(*fa, ihl=ihl, stride=stride, **kw)
 
     def run(f, igate, now):
         ref = f.copy()
