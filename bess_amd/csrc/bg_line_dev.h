@@ -106,7 +106,9 @@ __global__ __launch_bounds__(kBlock) void line_kernel(typename Op::Args a) {
 // 0.1605 ms, profiles/r06/legs_ab_r06r.json), otherwise kGateHold tiles in
 // registers (HashLB l4 0.1811 -> 0.1635 ms at one workgroup per CU, ACL
 // 0.2157 -> 0.1910 at two, legs_ab_r06o.json; ACL holding in LDS at two
-// measured slower, 0.2019 against 0.1978). A writing op stores each tile's
+// measured slower, 0.2019 against 0.1978; ACL at three or four workgroups
+// per CU 0.209-0.212 against 0.192-0.196, acl_occ_ab_r06ao.json). A
+// writing op stores each tile's
 // (its line stores are per tile anyway: holding measured no better).
 template <class Op>
 __host__ __device__ constexpr uint32_t line_hold_tiles(uint32_t tab_bytes) {
