@@ -33,7 +33,8 @@ ALGO = {"em": 66 * (16 << 20), "cksum": 1502 * (1 << 20),
         "wm": 66 * (8 << 20), "wm2k": 66 * (8 << 20), "c5": 66 * (16 << 20),
         "hashlb": 66 * (16 << 20), "acl": 66 * (16 << 20),
         "iplookup": 66 * (16 << 20), "ttl": 130 * (16 << 20),
-        "nat": 130 * (16 << 20), "dnat": 130 * (16 << 20),
+        # StaticNAT writes back only the translated half (round 6): 66 + 64 / 2
+        "nat": 98 * (16 << 20), "dnat": 130 * (16 << 20),
         "rewrite": 70 * (16 << 20), "em1500": 66 * (4 << 20)}
 # FETCH_SIZE -> bytes factor by access shape (r03_calibration.json)
 FETCH = {"wm2k": 1, "em1500": 1}
